@@ -1,0 +1,279 @@
+"""Mistral / Llama decoder (the summarization LLM).
+
+Replaces the LLM the reference reaches over HTTP (Ollama ``/api/generate``,
+adapters/copilot_summarization/copilot_summarization/local_llm_summarizer.py:107; llama.cpp
+``/completion``, llamacpp_summarizer.py:108; model ``mistral-7b-instruct-v0.2``,
+docker-compose.infra.yml:296-298).  Inference only.
+
+MI355X layout choices:
+  * fused weights: one QKV projection [(Hq+2Hkv)*D, H], one gate|up projection [2F, H], so a
+    layer is 4 GEMMs (hipBLASLt) + 4 hand-written HIP kernels (fused residual+RMSNorm x2,
+    RoPE+paged-KV write, attention, SwiGLU);
+  * tensor parallel (Megatron column/row split) with one all-reduce after o_proj and one after
+    down_proj, vocab-parallel lm_head + all-gather of logits -- see :mod:`..parallel.tp`;
+  * weights random-initialised directly on the device (no network: BASELINE "random-init
+    weights"), or loaded from HF-style safetensors when a checkpoint directory is given.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import math
+from pathlib import Path
+
+import torch
+import torch.nn.functional as F
+
+from ..ops import kernels as K
+from ..ops.reference import rope_cos_sin
+
+
+@dataclasses.dataclass(frozen=True)
+class DecoderConfig:
+    name: str
+    vocab_size: int
+    hidden: int
+    layers: int
+    heads: int
+    kv_heads: int
+    head_dim: int
+    ffn: int
+    rope_theta: float = 10000.0
+    rms_eps: float = 1e-5
+    max_positions: int = 32768
+    tie_embeddings: bool = False
+    bos_id: int = 1
+    eos_id: int = 2
+
+    @property
+    def q_size(self) -> int:
+        return self.heads * self.head_dim
+
+    @property
+    def kv_size(self) -> int:
+        return self.kv_heads * self.head_dim
+
+    def num_params(self) -> int:
+        h, f, v = self.hidden, self.ffn, self.vocab_size
+        per_layer = h * (self.q_size + 2 * self.kv_size) + self.q_size * h + 3 * h * f + 2 * h
+        return self.layers * per_layer + v * h * (1 if self.tie_embeddings else 2) + h
+
+    def flops_per_token(self, ctx: int = 0) -> float:
+        """Dense GEMM flops per token (+ attention over ``ctx`` keys)."""
+        h, f = self.hidden, self.ffn
+        gemm = 2 * (h * (self.q_size + 2 * self.kv_size) + self.q_size * h + 3 * h * f)
+        attn = 4 * self.heads * self.head_dim * ctx
+        return self.layers * (gemm + attn) + 2 * h * self.vocab_size
+
+
+PRESETS: dict[str, DecoderConfig] = {
+    # mistral-7b-instruct-v0.2 (what docker-compose.infra.yml:296 serves): no sliding window, theta 1e6
+    "mistral-7b": DecoderConfig("mistral-7b", 32000, 4096, 32, 32, 8, 128, 14336, rope_theta=1e6,
+                                max_positions=32768),
+    "llama-3-8b": DecoderConfig("llama-3-8b", 128256, 4096, 32, 32, 8, 128, 14336, rope_theta=5e5,
+                                max_positions=8192, bos_id=128000, eos_id=128009),
+    "llama-3-70b": DecoderConfig("llama-3-70b", 128256, 8192, 80, 64, 8, 128, 28672, rope_theta=5e5,
+                                 max_positions=8192, bos_id=128000, eos_id=128009),
+    # small configs for tests / smoke runs
+    "tiny": DecoderConfig("tiny", 512, 256, 2, 4, 2, 128, 512, rope_theta=1e4, max_positions=4096),
+    "small": DecoderConfig("small", 32000, 1024, 4, 8, 2, 128, 2816, rope_theta=1e6, max_positions=8192),
+}
+
+
+def get_config(name_or_cfg) -> DecoderConfig:
+    if isinstance(name_or_cfg, DecoderConfig):
+        return name_or_cfg
+    if name_or_cfg not in PRESETS:
+        raise KeyError(f"unknown decoder preset {name_or_cfg!r}; known: {sorted(PRESETS)}")
+    return PRESETS[name_or_cfg]
+
+
+class DecoderWeights:
+    """Per-rank (TP-sharded) weights, all bf16 on one device."""
+
+    def __init__(self, cfg: DecoderConfig, device, tp_rank: int = 0, tp_size: int = 1, dtype=torch.bfloat16):
+        if cfg.heads % tp_size or cfg.kv_heads % tp_size or cfg.ffn % tp_size or cfg.vocab_size % tp_size:
+            raise ValueError(f"{cfg.name}: heads/kv_heads/ffn/vocab must divide tp_size={tp_size}")
+        self.cfg, self.device, self.dtype = cfg, torch.device(device), dtype
+        self.tp_rank, self.tp_size = tp_rank, tp_size
+        self.heads = cfg.heads // tp_size
+        self.kv_heads = cfg.kv_heads // tp_size
+        self.ffn = cfg.ffn // tp_size
+        self.vocab_shard = cfg.vocab_size // tp_size
+        self.layers: list[dict[str, torch.Tensor]] = []
+        self.embed: torch.Tensor | None = None
+        self.final_norm: torch.Tensor | None = None
+        self.lm_head: torch.Tensor | None = None
+        self.cos_sin = rope_cos_sin(cfg.max_positions, cfg.head_dim, cfg.rope_theta, device=self.device)
+
+    # ---------------------------------------------------------------- init
+    @classmethod
+    def random(cls, cfg, device, seed: int = 0, tp_rank: int = 0, tp_size: int = 1, std: float = 0.02):
+        w = cls(cfg, device, tp_rank, tp_size)
+        gen = torch.Generator(device=w.device)
+        gen.manual_seed(seed * 1000003 + tp_rank)
+        D = cfg.head_dim
+
+        def rnd(*shape, scale=std):
+            t = torch.empty(*shape, dtype=w.dtype, device=w.device)
+            t.normal_(0.0, scale, generator=gen)
+            return t
+
+        h = cfg.hidden
+        out_std = std / math.sqrt(2 * cfg.layers)
+        for _ in range(cfg.layers):
+            w.layers.append({
+                "attn_norm": torch.ones(h, dtype=w.dtype, device=w.device),
+                "qkv": rnd((w.heads + 2 * w.kv_heads) * D, h),
+                "o": rnd(h, w.heads * D, scale=out_std),
+                "mlp_norm": torch.ones(h, dtype=w.dtype, device=w.device),
+                "gate_up": rnd(2 * w.ffn, h),
+                "down": rnd(h, w.ffn, scale=out_std),
+            })
+        w.embed = rnd(cfg.vocab_size, h, scale=1.0)  # embeddings replicated (gather is cheap)
+        w.final_norm = torch.ones(h, dtype=w.dtype, device=w.device)
+        w.lm_head = rnd(w.vocab_shard, h)
+        return w
+
+    @classmethod
+    def from_safetensors(cls, cfg, ckpt_dir, device, tp_rank: int = 0, tp_size: int = 1):
+        """Load HF Llama/Mistral safetensors (``model.layers.N.self_attn.q_proj.weight`` names)."""
+        from safetensors import safe_open
+
+        w = cls(cfg, device, tp_rank, tp_size)
+        files = sorted(Path(ckpt_dir).glob("*.safetensors"))
+        if not files:
+            raise FileNotFoundError(f"no *.safetensors in {ckpt_dir}")
+        tensors = {}
+        for f in files:
+            with safe_open(str(f), framework="pt", device="cpu") as fh:
+                for k in fh.keys():
+                    tensors[k] = fh.get_tensor(k)
+        D = cfg.head_dim
+
+        def shard_rows(t, n):
+            return t.view(tp_size, n, *t.shape[1:])[tp_rank] if tp_size > 1 else t
+
+        def shard_cols(t, n):
+            return t.view(t.shape[0], tp_size, n)[:, tp_rank].contiguous() if tp_size > 1 else t
+
+        def dev(t):
+            return t.to(device=w.device, dtype=w.dtype).contiguous()
+
+        for i in range(cfg.layers):
+            p = f"model.layers.{i}."
+            q = shard_rows(tensors[p + "self_attn.q_proj.weight"], w.heads * D)
+            k = shard_rows(tensors[p + "self_attn.k_proj.weight"], w.kv_heads * D)
+            v = shard_rows(tensors[p + "self_attn.v_proj.weight"], w.kv_heads * D)
+            g = shard_rows(tensors[p + "mlp.gate_proj.weight"], w.ffn)
+            u = shard_rows(tensors[p + "mlp.up_proj.weight"], w.ffn)
+            w.layers.append({
+                "attn_norm": dev(tensors[p + "input_layernorm.weight"]),
+                "qkv": dev(torch.cat([q, k, v], 0)),
+                "o": dev(shard_cols(tensors[p + "self_attn.o_proj.weight"], w.heads * D)),
+                "mlp_norm": dev(tensors[p + "post_attention_layernorm.weight"]),
+                "gate_up": dev(torch.cat([g, u], 0)),
+                "down": dev(shard_cols(tensors[p + "mlp.down_proj.weight"], w.ffn)),
+            })
+        w.embed = dev(tensors["model.embed_tokens.weight"])
+        w.final_norm = dev(tensors["model.norm.weight"])
+        head = tensors.get("lm_head.weight", tensors["model.embed_tokens.weight"])
+        w.lm_head = dev(shard_rows(head, w.vocab_shard))
+        return w
+
+    def nbytes(self) -> int:
+        n = sum(t.numel() * t.element_size() for layer in self.layers for t in layer.values())
+        return n + sum(t.numel() * t.element_size() for t in (self.embed, self.final_norm, self.lm_head))
+
+
+def load_config_json(path) -> DecoderConfig:
+    """DecoderConfig from an HF ``config.json``."""
+    c = json.loads(Path(path).read_text())
+    return DecoderConfig(
+        name=c.get("_name_or_path", "hf"), vocab_size=c["vocab_size"], hidden=c["hidden_size"],
+        layers=c["num_hidden_layers"], heads=c["num_attention_heads"],
+        kv_heads=c.get("num_key_value_heads", c["num_attention_heads"]),
+        head_dim=c.get("head_dim", c["hidden_size"] // c["num_attention_heads"]), ffn=c["intermediate_size"],
+        rope_theta=c.get("rope_theta", 10000.0), rms_eps=c.get("rms_norm_eps", 1e-5),
+        max_positions=c.get("max_position_embeddings", 4096), tie_embeddings=c.get("tie_word_embeddings", False),
+        bos_id=c.get("bos_token_id", 1) or 1, eos_id=c.get("eos_token_id", 2) if isinstance(c.get("eos_token_id", 2), int) else c["eos_token_id"][0])
+
+
+class DecoderModel:
+    """Stateless forward functions over :class:`DecoderWeights` + a paged KV cache."""
+
+    def __init__(self, weights: DecoderWeights, tp_group=None):
+        self.w = weights
+        self.cfg = weights.cfg
+        self.tp_group = tp_group
+        self.scale = 1.0 / math.sqrt(self.cfg.head_dim)
+
+    def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+        if self.w.tp_size > 1:
+            torch.distributed.all_reduce(x, group=self.tp_group)
+        return x
+
+    def _layer_pre(self, i, x, residual):
+        """Returns normed input of layer i and the residual stream."""
+        lw = self.w.layers[i]
+        if residual is None:
+            residual = x.clone()
+            h = K.rmsnorm(x, lw["attn_norm"], self.cfg.rms_eps)
+        else:
+            h = K.rmsnorm(x, lw["attn_norm"], self.cfg.rms_eps, residual=residual)
+        return h, residual
+
+    def _mlp(self, i, attn_out, residual):
+        lw = self.w.layers[i]
+        h = K.rmsnorm(attn_out, lw["mlp_norm"], self.cfg.rms_eps, residual=residual)
+        gu = F.linear(h, lw["gate_up"])
+        a = K.silu_mul(gu)
+        return self._all_reduce(F.linear(a, lw["down"]))
+
+    def forward_prefill(self, ids, positions, slots, cu_q, ctx_lens, block_tables, kv, tiles=None,
+                        last_idx=None) -> torch.Tensor:
+        """Packed varlen prefill. Returns hidden states of rows ``last_idx`` (or all rows)."""
+        cfg, w = self.cfg, self.w
+        x = K.embedding(w.embed, ids)
+        residual = None
+        for i in range(cfg.layers):
+            lw = w.layers[i]
+            h, residual = self._layer_pre(i, x, residual)
+            qkv = F.linear(h, lw["qkv"])
+            q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
+                                cfg.head_dim)
+            attn = K.prefill_attention(q, kv.k[i], kv.v[i], block_tables, cu_q, ctx_lens, self.scale, tiles=tiles)
+            o = self._all_reduce(F.linear(attn.view(attn.shape[0], -1), lw["o"]))
+            x = self._mlp(i, o, residual)
+        if last_idx is not None:
+            x = x.index_select(0, last_idx)
+            residual = residual.index_select(0, last_idx)
+        return K.rmsnorm(x, w.final_norm, cfg.rms_eps, residual=residual)
+
+    def forward_decode(self, ids, positions, slots, ctx_lens, block_tables, kv, attn_workspace=None,
+                       part_blocks=16) -> torch.Tensor:
+        """One token per sequence. Returns final-normed hidden [B, H]."""
+        cfg, w = self.cfg, self.w
+        x = K.embedding(w.embed, ids)
+        residual = None
+        B = ids.shape[0]
+        for i in range(cfg.layers):
+            lw = w.layers[i]
+            h, residual = self._layer_pre(i, x, residual)
+            qkv = F.linear(h, lw["qkv"])
+            q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
+                                cfg.head_dim)
+            attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
+                                            part_blocks=part_blocks, workspace=attn_workspace)
+            o = self._all_reduce(F.linear(attn.view(B, -1), lw["o"]))
+            x = self._mlp(i, o, residual)
+        return K.rmsnorm(x, w.final_norm, cfg.rms_eps, residual=residual)
+
+    def logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        """[B, V] logits (all-gathered over the vocab-parallel shards)."""
+        local = F.linear(hidden, self.w.lm_head)
+        if self.w.tp_size == 1:
+            return local
+        parts = [torch.empty_like(local) for _ in range(self.w.tp_size)]
+        torch.distributed.all_gather(parts, local, group=self.tp_group)
+        return torch.cat(parts, -1)

@@ -1,0 +1,179 @@
+"""BERT-family sentence encoder (all-MiniLM-L6-v2, bge-small/base) for the embedding service.
+
+Replaces ``SentenceTransformer(model).encode(text)`` (adapters/copilot_embedding/copilot_embedding/
+sentence_transformer_provider.py:50,93) and the HF ``AutoModel`` mean-pool provider
+(huggingface_provider.py:44,98-101).  The reference embeds ONE chunk per call
+(embedding/app/service.py:384-393); this encoder runs packed varlen batches (no padding) of
+hundreds of chunks per forward:
+
+    embed gather + pos + type + LayerNorm       (1 HIP kernel)
+    per layer: QKV GEMM(+bias)  -> varlen bidirectional MFMA attention (HIP)
+               O GEMM -> bias + residual + LayerNorm (HIP)
+               FFN-up GEMM -> bias + GELU (HIP) -> FFN-down GEMM -> bias + residual + LN (HIP)
+    masked mean / CLS pooling + L2 normalise    (1 HIP kernel)
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from pathlib import Path
+
+import torch
+import torch.nn.functional as F
+
+from ..ops import kernels as K
+
+
+@dataclasses.dataclass(frozen=True)
+class EncoderConfig:
+    name: str
+    vocab_size: int = 30522
+    hidden: int = 384
+    layers: int = 6
+    heads: int = 12
+    ffn: int = 1536
+    max_positions: int = 512
+    max_seq_length: int = 256     # sentence-transformers truncation length
+    ln_eps: float = 1e-12
+    pooling: str = "mean"         # "mean" (MiniLM) or "cls" (BGE)
+    normalize: bool = True
+
+    @property
+    def head_dim(self) -> int:
+        return self.hidden // self.heads
+
+
+ENCODER_PRESETS = {
+    "minilm-l6": EncoderConfig("all-MiniLM-L6-v2"),
+    "all-MiniLM-L6-v2": EncoderConfig("all-MiniLM-L6-v2"),
+    "bge-small": EncoderConfig("bge-small-en-v1.5", layers=12, max_seq_length=512, pooling="cls"),
+    "bge-base": EncoderConfig("bge-base-en-v1.5", hidden=768, layers=12, heads=12, ffn=3072, max_seq_length=512,
+                              pooling="cls"),
+    "tiny": EncoderConfig("tiny", vocab_size=1000, hidden=64, layers=2, heads=2, ffn=128, max_positions=512,
+                          max_seq_length=128),
+}
+
+
+def get_encoder_config(name) -> EncoderConfig:
+    if isinstance(name, EncoderConfig):
+        return name
+    key = name.split("/")[-1]
+    if key not in ENCODER_PRESETS:
+        raise KeyError(f"unknown encoder {name!r}; known: {sorted(ENCODER_PRESETS)}")
+    return ENCODER_PRESETS[key]
+
+
+class EncoderModel:
+    def __init__(self, cfg: EncoderConfig, device, dtype=torch.bfloat16):
+        self.cfg, self.device, self.dtype = cfg, torch.device(device), dtype
+        self.p: dict[str, torch.Tensor] = {}
+        self.layers: list[dict[str, torch.Tensor]] = []
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+
+    @classmethod
+    def random(cls, cfg, device, seed: int = 0, std: float = 0.02):
+        m = cls(get_encoder_config(cfg), device)
+        c = m.cfg
+        gen = torch.Generator(device=m.device)
+        gen.manual_seed(seed)
+
+        def rnd(*shape):
+            t = torch.empty(*shape, dtype=m.dtype, device=m.device)
+            return t.normal_(0.0, std, generator=gen)
+
+        def ones(n):
+            return torch.ones(n, dtype=m.dtype, device=m.device)
+
+        def zeros(n):
+            return torch.zeros(n, dtype=m.dtype, device=m.device)
+
+        h, f = c.hidden, c.ffn
+        m.p = {"word": rnd(c.vocab_size, h), "pos": rnd(c.max_positions, h), "type": rnd(2, h),
+               "emb_g": ones(h), "emb_b": zeros(h)}
+        for _ in range(c.layers):
+            m.layers.append({"qkv": rnd(3 * h, h), "qkv_b": zeros(3 * h), "o": rnd(h, h), "o_b": zeros(h),
+                             "ln1_g": ones(h), "ln1_b": zeros(h), "up": rnd(f, h), "up_b": zeros(f),
+                             "down": rnd(h, f), "down_b": zeros(h), "ln2_g": ones(h), "ln2_b": zeros(h)})
+        return m
+
+    @classmethod
+    def from_safetensors(cls, cfg, ckpt_dir, device):
+        """Load an HF BertModel checkpoint (``model.safetensors``)."""
+        from safetensors import safe_open
+
+        m = cls(get_encoder_config(cfg), device)
+        files = sorted(Path(ckpt_dir).glob("*.safetensors"))
+        t = {}
+        for fpath in files:
+            with safe_open(str(fpath), framework="pt", device="cpu") as fh:
+                for k in fh.keys():
+                    t[k.removeprefix("bert.")] = fh.get_tensor(k)
+
+        def d(x):
+            return x.to(device=m.device, dtype=m.dtype).contiguous()
+
+        m.p = {"word": d(t["embeddings.word_embeddings.weight"]), "pos": d(t["embeddings.position_embeddings.weight"]),
+               "type": d(t["embeddings.token_type_embeddings.weight"]), "emb_g": d(t["embeddings.LayerNorm.weight"]),
+               "emb_b": d(t["embeddings.LayerNorm.bias"])}
+        for i in range(m.cfg.layers):
+            p = f"encoder.layer.{i}."
+            a = p + "attention."
+            m.layers.append({
+                "qkv": d(torch.cat([t[a + "self.query.weight"], t[a + "self.key.weight"], t[a + "self.value.weight"]])),
+                "qkv_b": d(torch.cat([t[a + "self.query.bias"], t[a + "self.key.bias"], t[a + "self.value.bias"]])),
+                "o": d(t[a + "output.dense.weight"]), "o_b": d(t[a + "output.dense.bias"]),
+                "ln1_g": d(t[a + "output.LayerNorm.weight"]), "ln1_b": d(t[a + "output.LayerNorm.bias"]),
+                "up": d(t[p + "intermediate.dense.weight"]), "up_b": d(t[p + "intermediate.dense.bias"]),
+                "down": d(t[p + "output.dense.weight"]), "down_b": d(t[p + "output.dense.bias"]),
+                "ln2_g": d(t[p + "output.LayerNorm.weight"]), "ln2_b": d(t[p + "output.LayerNorm.bias"]),
+            })
+        return m
+
+    # ------------------------------------------------------------------ forward
+    def forward_packed(self, ids: torch.Tensor, positions: torch.Tensor, cu_seqlens: torch.Tensor, max_seqlen: int,
+                       tiles=None) -> torch.Tensor:
+        """Token states [T, H] for packed varlen input."""
+        c = self.cfg
+        x = K.embed_layernorm(ids, positions, self.p["word"], self.p["pos"], self.p["type"], self.p["emb_g"],
+                              self.p["emb_b"], c.ln_eps)
+        for lw in self.layers:
+            qkv = F.linear(x, lw["qkv"], lw["qkv_b"])
+            a = K.encoder_attention(qkv, cu_seqlens, c.heads, c.head_dim, self.scale, max_seqlen, tiles=tiles)
+            o = F.linear(a.view(a.shape[0], -1), lw["o"])
+            x = K.layernorm(o, lw["ln1_g"], lw["ln1_b"], c.ln_eps, bias=lw["o_b"], residual=x)
+            h = K.bias_gelu(F.linear(x, lw["up"]), lw["up_b"])
+            o2 = F.linear(h, lw["down"])
+            x = K.layernorm(o2, lw["ln2_g"], lw["ln2_b"], c.ln_eps, bias=lw["down_b"], residual=x)
+        return x
+
+    @torch.inference_mode()
+    def encode_ids(self, batch: list[list[int]], pooling: str | None = None, normalize: bool | None = None,
+                   max_tokens_per_forward: int = 65536) -> torch.Tensor:
+        """Sentence embeddings [n, H] fp32 for pre-tokenised sequences (truncated to max_seq_length)."""
+        c = self.cfg
+        pooling = pooling or c.pooling
+        normalize = c.normalize if normalize is None else normalize
+        seqs = [s[:c.max_seq_length] for s in batch]
+        outs = []
+        i = 0
+        while i < len(seqs):
+            j, tok = i, 0
+            while j < len(seqs) and (tok + len(seqs[j]) <= max_tokens_per_forward or j == i):
+                tok += len(seqs[j])
+                j += 1
+            part = seqs[i:j]
+            ids = [t for s in part for t in s]
+            pos = [p for s in part for p in range(len(s))]
+            cu = [0]
+            for s in part:
+                cu.append(cu[-1] + len(s))
+            dev = self.device
+            cu_t = torch.tensor(cu, dtype=torch.int32, device=dev)
+            seq_t, q0_t = K.prefill_tiles(cu)
+            tiles = (torch.tensor(seq_t, dtype=torch.int32, device=dev), torch.tensor(q0_t, dtype=torch.int32, device=dev))
+            h = self.forward_packed(torch.tensor(ids, dtype=torch.int32, device=dev),
+                                    torch.tensor(pos, dtype=torch.int32, device=dev), cu_t,
+                                    max(len(s) for s in part), tiles=tiles)
+            outs.append(K.pool(h, cu_t, pooling, normalize))
+            i = j
+        return torch.cat(outs, 0)

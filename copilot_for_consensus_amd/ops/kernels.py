@@ -1,0 +1,317 @@
+"""Python entry points of the native HIP kernels.
+
+Every function takes torch tensors.  CUDA (= HIP on ROCm) tensors go to ``libcfc_kernels.so`` on
+PyTorch's current stream (so the calls are hipGraph-capturable); CPU tensors run the fp32
+reference in :mod:`.reference` (CI / BASELINE config 1 have no GPU).  There is no silent
+fallback for GPU tensors: a missing native library raises.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import reference as ref
+from ._native import check, kernels
+
+KV_BLOCK = ref.KV_BLOCK
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _req(t: torch.Tensor, dtype, name: str):
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+
+
+# ----------------------------------------------------------------------------- norms
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor | None = None,
+            out: torch.Tensor | None = None) -> torch.Tensor:
+    """out = RMSNorm(x [+ residual]) * w; with ``residual`` it is updated in place to x + residual."""
+    if not x.is_cuda:
+        o, r = ref.rmsnorm(x, w, eps, residual)
+        if residual is not None:
+            residual.copy_(r)
+        if out is not None:
+            out.copy_(o)
+            return out
+        return o
+    _req(x, torch.bfloat16, "x")
+    dim = x.shape[-1]
+    rows = x.numel() // dim
+    out = torch.empty_like(x) if out is None else out
+    check(kernels().cfc_rmsnorm(out.data_ptr(), _p(residual), x.data_ptr(), w.data_ptr(), rows, dim, float(eps),
+                                1 if residual is not None else 0, _stream(x)), "cfc_rmsnorm")
+    return out
+
+
+def layernorm(x, gamma, beta, eps, bias=None, residual=None, out=None):
+    """LN(x [+ bias + residual]) (post-LN BERT sub-layer epilogue)."""
+    if not x.is_cuda:
+        return ref.layernorm(x, gamma, beta, eps, bias, residual)
+    _req(x, torch.bfloat16, "x")
+    dim = x.shape[-1]
+    rows = x.numel() // dim
+    out = torch.empty_like(x) if out is None else out
+    mode = 1 if (bias is not None or residual is not None) else 0
+    if mode == 1 and (bias is None or residual is None):
+        raise ValueError("layernorm: bias and residual must be given together")
+    check(kernels().cfc_layernorm(out.data_ptr(), x.data_ptr(), _p(bias), _p(residual), gamma.data_ptr(),
+                                  beta.data_ptr(), None, None, None, None, rows, dim, float(eps), mode, _stream(x)),
+          "cfc_layernorm")
+    return out
+
+
+def embed_layernorm(ids, positions, word_emb, pos_emb, type_emb, gamma, beta, eps):
+    if not word_emb.is_cuda:
+        return ref.embed_layernorm(ids, positions, word_emb, pos_emb, type_emb, gamma, beta, eps)
+    _req(ids, torch.int32, "ids")
+    _req(positions, torch.int32, "positions")
+    T, dim = ids.numel(), word_emb.shape[1]
+    out = torch.empty(T, dim, dtype=word_emb.dtype, device=word_emb.device)
+    check(kernels().cfc_layernorm(out.data_ptr(), word_emb.data_ptr(), None, None, gamma.data_ptr(), beta.data_ptr(),
+                                  ids.data_ptr(), positions.data_ptr(), pos_emb.data_ptr(), type_emb.data_ptr(), T,
+                                  dim, float(eps), 2, _stream(word_emb)), "cfc_layernorm(embed)")
+    return out
+
+
+# ----------------------------------------------------------------------------- decoder ops
+
+def rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D, q_out=None):
+    if not qkv.is_cuda:
+        q = ref.rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D)
+        if q_out is not None:
+            q_out.view_as(q).copy_(q)
+            return q_out
+        return q
+    _req(qkv, torch.bfloat16, "qkv")
+    _req(positions, torch.int32, "positions")
+    _req(slots, torch.int32, "slots")
+    T = qkv.shape[0]
+    if qkv.shape[1] != (Hq + 2 * Hkv) * D:
+        raise ValueError("rope_kv_write: qkv width mismatch")
+    q_out = torch.empty(T, Hq, D, dtype=qkv.dtype, device=qkv.device) if q_out is None else q_out
+    check(kernels().cfc_rope_kv_write(qkv.data_ptr(), positions.data_ptr(), slots.data_ptr(), cos_sin.data_ptr(),
+                                      q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), T, Hq, Hkv, D,
+                                      _stream(qkv)), "cfc_rope_kv_write")
+    return q_out
+
+
+def decode_partitions(max_ctx: int, part_blocks: int) -> int:
+    return max(1, math.ceil(math.ceil(max_ctx / KV_BLOCK) / part_blocks))
+
+
+def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out=None, part_blocks=16,
+                           num_partitions=None, workspace=None):
+    """q [B, Hq, D]; caches [nblk, Hkv, 32, D] / [nblk, Hkv, D, 32]; returns [B, Hq, D]."""
+    if not q.is_cuda:
+        return ref.paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale)
+    B, Hq, D = q.shape
+    Hkv = k_cache.shape[1]
+    _req(block_tables, torch.int32, "block_tables")
+    _req(ctx_lens, torch.int32, "ctx_lens")
+    max_blocks = block_tables.shape[1]
+    Pn = num_partitions or math.ceil(max_blocks / part_blocks)
+    out = torch.empty_like(q) if out is None else out
+    if Pn > 1:
+        if workspace is None:
+            workspace = torch.empty(B * Hq * Pn * (D + 2), dtype=torch.float32, device=q.device)
+        part_o = workspace
+        part_ml = workspace[B * Hq * Pn * D:]
+    else:
+        part_o = part_ml = None
+    check(kernels().cfc_paged_decode_attention(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                                               block_tables.data_ptr(), ctx_lens.data_ptr(), B, Hq, Hkv, D,
+                                               max_blocks, part_blocks, Pn, float(scale), _p(part_o), _p(part_ml),
+                                               out.data_ptr(), _stream(q)), "cfc_paged_decode_attention")
+    return out
+
+
+def prefill_tiles(cu_q: list[int], tile: int = 64):
+    seqs, q0 = [], []
+    for s in range(len(cu_q) - 1):
+        n = cu_q[s + 1] - cu_q[s]
+        for r in range(0, n, tile):
+            seqs.append(s)
+            q0.append(r)
+    return seqs, q0
+
+
+def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, tiles=None, out=None):
+    """q [T, Hq, D] (packed varlen); cu_q [S+1] int32; ctx_lens [S] int32 (cached + new)."""
+    if not q.is_cuda:
+        return ref.prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale)
+    T, Hq, D = q.shape
+    Hkv = k_cache.shape[1]
+    if tiles is None:
+        seqs, q0 = prefill_tiles(cu_q.tolist())
+        tiles = (torch.tensor(seqs, dtype=torch.int32, device=q.device),
+                 torch.tensor(q0, dtype=torch.int32, device=q.device))
+    tile_seq, tile_q0 = tiles
+    out = torch.empty_like(q) if out is None else out
+    check(kernels().cfc_prefill_attention(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                                          block_tables.data_ptr(), cu_q.data_ptr(), ctx_lens.data_ptr(),
+                                          tile_seq.data_ptr(), tile_q0.data_ptr(), tile_seq.numel(), Hq, Hkv, D,
+                                          block_tables.shape[1], float(scale), out.data_ptr(), _stream(q)),
+          "cfc_prefill_attention")
+    return out
+
+
+def encoder_attention(qkv, cu_seqlens, H, D, scale, max_seqlen, tiles=None, out=None):
+    if not qkv.is_cuda:
+        return ref.encoder_attention(qkv, cu_seqlens, H, D, scale)
+    T = qkv.shape[0]
+    if tiles is None:
+        seqs, q0 = prefill_tiles(cu_seqlens.tolist())
+        tiles = (torch.tensor(seqs, dtype=torch.int32, device=qkv.device),
+                 torch.tensor(q0, dtype=torch.int32, device=qkv.device))
+    out = torch.empty(T, H, D, dtype=qkv.dtype, device=qkv.device) if out is None else out
+    check(kernels().cfc_encoder_attention(qkv.data_ptr(), cu_seqlens.data_ptr(), tiles[0].data_ptr(),
+                                          tiles[1].data_ptr(), tiles[0].numel(), H, D, int(max_seqlen),
+                                          float(scale), out.data_ptr(), _stream(qkv)), "cfc_encoder_attention")
+    return out
+
+
+def silu_mul(gu, out=None):
+    if not gu.is_cuda:
+        return ref.silu_mul(gu)
+    _req(gu, torch.bfloat16, "gu")
+    T, F2 = gu.shape
+    out = torch.empty(T, F2 // 2, dtype=gu.dtype, device=gu.device) if out is None else out
+    check(kernels().cfc_silu_mul(out.data_ptr(), gu.data_ptr(), T, F2 // 2, _stream(gu)), "cfc_silu_mul")
+    return out
+
+
+def bias_gelu(x, bias, out=None):
+    if not x.is_cuda:
+        return ref.bias_gelu(x, bias)
+    _req(x, torch.bfloat16, "x")
+    T, F = x.shape
+    out = torch.empty_like(x) if out is None else out
+    check(kernels().cfc_bias_gelu(out.data_ptr(), x.data_ptr(), _p(bias), T, F, _stream(x)), "cfc_bias_gelu")
+    return out
+
+
+def embedding(table, ids, out=None):
+    if not table.is_cuda:
+        return table[ids.long()]
+    _req(ids, torch.int32, "ids")
+    T, dim = ids.numel(), table.shape[1]
+    out = torch.empty(T, dim, dtype=table.dtype, device=table.device) if out is None else out
+    check(kernels().cfc_embedding(out.data_ptr(), table.data_ptr(), ids.data_ptr(), T, dim, _stream(table)),
+          "cfc_embedding")
+    return out
+
+
+def sample(logits, out_ids, temperature=0.0, seed=0, step=None):
+    """Greedy (temperature <= 0) or Gumbel-max sampling of one token per row into out_ids (int32)."""
+    if not logits.is_cuda:
+        if temperature <= 0:
+            out_ids.copy_(ref.sample_greedy(logits))
+        else:
+            g = torch.Generator().manual_seed(int(seed) + int(step[0]) if step is not None else int(seed))
+            p = torch.softmax(logits.float() / temperature, -1)
+            out_ids.copy_(torch.multinomial(p, 1, generator=g)[:, 0].to(torch.int32))
+        return out_ids
+    _req(logits, torch.bfloat16, "logits")
+    B, V = logits.shape
+    check(kernels().cfc_sample(logits.data_ptr(), B, V, float(temperature), int(seed) & 0xFFFFFFFF, _p(step),
+                               out_ids.data_ptr(), _stream(logits)), "cfc_sample")
+    return out_ids
+
+
+def decode_advance(next_ids, tokens, step, input_ids, positions, ctx_lens, slots, block_tables, done, stop_ids):
+    """Device-side bookkeeping after each decode step (graph-capturable, no host sync)."""
+    B = next_ids.numel()
+    max_new = tokens.shape[1]
+    if not next_ids.is_cuda:
+        st = int(step[0])
+        if st < max_new:
+            tokens[:, st] = next_ids
+        input_ids.copy_(next_ids)
+        positions += 1
+        ctx_lens.copy_(positions + 1)
+        pos = positions.long()
+        slots.copy_(block_tables[torch.arange(B), pos // KV_BLOCK] * KV_BLOCK + pos % KV_BLOCK)
+        if stop_ids.numel():
+            done |= torch.isin(next_ids, stop_ids).to(done.dtype)
+        step += 1
+        return
+    check(kernels().cfc_decode_advance(next_ids.data_ptr(), tokens.data_ptr(), max_new, step.data_ptr(),
+                                       input_ids.data_ptr(), positions.data_ptr(), ctx_lens.data_ptr(),
+                                       slots.data_ptr(), block_tables.data_ptr(), block_tables.shape[1],
+                                       done.data_ptr(), _p(stop_ids) if stop_ids.numel() else None,
+                                       stop_ids.numel(), B, _stream(next_ids)), "cfc_decode_advance")
+
+
+# ----------------------------------------------------------------------------- vector search
+
+def knn_scores(X, Q, xnorm2=None, qnorm2=None, out=None):
+    """scores [nq, N] fp32 for nq <= 16 queries (dot, or -squared-L2 when norms are given)."""
+    if not X.is_cuda:
+        return ref.knn_scores(X, Q, xnorm2, qnorm2)
+    N, dim = X.shape
+    nq = Q.shape[0]
+    out = torch.empty(nq, N, dtype=torch.float32, device=X.device) if out is None else out
+    check(kernels().cfc_knn_scores(X.data_ptr(), Q.data_ptr(), N, nq, dim, _p(xnorm2), _p(qnorm2), out.data_ptr(),
+                                   _stream(X)), "cfc_knn_scores")
+    return out
+
+
+def topk(scores: torch.Tensor, k: int, ids: torch.Tensor | None = None):
+    """Exact top-k per row of ``scores`` [nq, n]; returns (values, ids) sorted descending."""
+    nq, n = scores.shape
+    k_eff = min(k, n)
+    if not scores.is_cuda:
+        v, i = torch.topk(scores.float(), k_eff, dim=1)
+        if ids is not None:
+            i = torch.gather(ids, 1, i)
+        return v, i
+    lib = kernels()
+    chunk = lib.cfc_topk_chunk_size()
+    cur_v, cur_i, cur_n = scores.contiguous(), ids, n
+    while True:
+        nch = math.ceil(cur_n / chunk)
+        ov = torch.empty(nq, nch * k_eff, dtype=torch.float32, device=scores.device)
+        oi = torch.empty(nq, nch * k_eff, dtype=torch.int64, device=scores.device)
+        check(lib.cfc_topk_pass(cur_v.data_ptr(), _p(cur_i), nq, cur_n, cur_v.shape[1], k_eff, ov.data_ptr(),
+                                oi.data_ptr(), _stream(scores)), "cfc_topk_pass")
+        cur_v, cur_i, cur_n = ov, oi, nch * k_eff
+        if nch == 1:
+            break
+    order = torch.argsort(cur_v, dim=1, descending=True, stable=True)
+    return torch.gather(cur_v, 1, order), torch.gather(cur_i, 1, order)
+
+
+def l2_normalize(x, out=None, norms2=None):
+    if not x.is_cuda:
+        o, n2 = ref.l2_normalize(x)
+        if norms2 is not None:
+            norms2.copy_(n2)
+        return o
+    rows, dim = x.shape
+    out = torch.empty_like(x) if out is None else out
+    check(kernels().cfc_l2_normalize(out.data_ptr(), x.data_ptr(), _p(norms2), rows, dim, _stream(x)),
+          "cfc_l2_normalize")
+    return out
+
+
+def pool(hidden, cu_seqlens, mode="mean", normalize=True):
+    """[nseq, dim] fp32 sentence embeddings from packed token states."""
+    if not hidden.is_cuda:
+        return ref.pool(hidden, cu_seqlens, mode, normalize)
+    nseq = cu_seqlens.numel() - 1
+    dim = hidden.shape[-1]
+    out = torch.empty(nseq, dim, dtype=torch.float32, device=hidden.device)
+    check(kernels().cfc_pool(out.data_ptr(), None, hidden.data_ptr(), cu_seqlens.data_ptr(), nseq, dim,
+                             1 if mode == "cls" else 0, 1 if normalize else 0, _stream(hidden)), "cfc_pool")
+    return out

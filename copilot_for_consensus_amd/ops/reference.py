@@ -1,0 +1,194 @@
+"""Plain-PyTorch fp32 reference implementations of every native op.
+
+They define the exact semantics (including the paged KV-cache layouts) that the HIP kernels in
+``csrc/kernels`` must reproduce; the numerics tests compare the two, and CPU-only runs (CI,
+BASELINE config 1) execute these.  Inputs/outputs use the same dtypes as the kernels (bf16
+activations), the math runs in fp32.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+KV_BLOCK = 32
+
+
+def v_slot_perm(device=None) -> torch.Tensor:
+    """slot index (0..31) of every key inside a KV block in the transposed V cache."""
+    k = torch.arange(KV_BLOCK, device=device)
+    hi, g, j = k >> 4, (k >> 2) & 3, (k & 3) + 4 * (k >> 4)
+    del hi
+    return 8 * g + j
+
+
+def rmsnorm(x, w, eps, residual=None):
+    """Returns (out, new_residual).  With residual: residual <- x + residual; out = norm(residual)."""
+    if residual is not None:
+        r = (x.float() + residual.float()).to(x.dtype)
+        base = r
+    else:
+        r = None
+        base = x
+    xf = base.float()
+    out = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    return out.to(x.dtype), r
+
+
+def layernorm(x, gamma, beta, eps, bias=None, residual=None):
+    xf = x.float()
+    if bias is not None:
+        xf = xf + bias.float()
+    if residual is not None:
+        xf = xf + residual.float()
+    out = torch.nn.functional.layer_norm(xf, (xf.shape[-1],), gamma.float(), beta.float(), eps)
+    return out.to(x.dtype)
+
+
+def embed_layernorm(ids, positions, word_emb, pos_emb, type_emb, gamma, beta, eps):
+    x = word_emb[ids.long()].float() + pos_emb[positions.long()].float() + type_emb[0].float()
+    return torch.nn.functional.layer_norm(x, (x.shape[-1],), gamma.float(), beta.float(), eps).to(word_emb.dtype)
+
+
+def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None) -> torch.Tensor:
+    """[max_pos, D/2, 2] fp32 table of (cos, sin) for rotate-half RoPE."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    t = torch.arange(max_pos, dtype=torch.float64)
+    ang = torch.outer(t, inv)
+    return torch.stack([ang.cos(), ang.sin()], -1).float().to(device)
+
+
+def rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D):
+    """Apply RoPE to q/k of the fused projection, write k/v into the paged cache. Returns q."""
+    T = qkv.shape[0]
+    x = qkv.float().view(T, Hq + 2 * Hkv, D)
+    cs = cos_sin[positions.long()]  # [T, D/2, 2]
+    cos, sin = cs[..., 0][:, None, :], cs[..., 1][:, None, :]
+    half = D // 2
+
+    def rot(t):
+        a, b = t[..., :half], t[..., half:]
+        return torch.cat([a * cos - b * sin, b * cos + a * sin], -1)
+
+    q = rot(x[:, :Hq]).to(qkv.dtype)
+    k = rot(x[:, Hq:Hq + Hkv]).to(qkv.dtype)
+    v = x[:, Hq + Hkv:].to(qkv.dtype)
+    perm = v_slot_perm(qkv.device)
+    for t in range(T):
+        s = int(slots[t])
+        if s < 0:
+            continue
+        blk, off = divmod(s, KV_BLOCK)
+        k_cache[blk, :, off, :] = k[t]
+        v_cache[blk, :, :, int(perm[off])] = v[t]
+    return q
+
+
+def gather_kv(k_cache, v_cache, block_table, n):
+    """Contiguous K, V [n, Hkv, D] of one sequence from the paged caches."""
+    perm = v_slot_perm(k_cache.device)
+    nb = (n + KV_BLOCK - 1) // KV_BLOCK
+    blocks = block_table[:nb].long()
+    k = k_cache[blocks].permute(0, 2, 1, 3).reshape(nb * KV_BLOCK, k_cache.shape[1], k_cache.shape[3])
+    v = v_cache[blocks][..., perm].permute(0, 3, 1, 2).reshape(nb * KV_BLOCK, v_cache.shape[1], v_cache.shape[2])
+    return k[:n], v[:n]
+
+
+def _attend(q, k, v, scale, causal_offset=None):
+    """q [m, Hq, D], k/v [n, Hkv, D] -> [m, Hq, D] fp32 (GQA)."""
+    Hq, Hkv = q.shape[1], k.shape[1]
+    G = Hq // Hkv
+    kk = k.float().repeat_interleave(G, 1)
+    vv = v.float().repeat_interleave(G, 1)
+    s = torch.einsum("mhd,nhd->hmn", q.float(), kk) * scale
+    if causal_offset is not None:
+        m, n = q.shape[0], k.shape[0]
+        pos = torch.arange(m, device=q.device)[:, None] + causal_offset
+        mask = torch.arange(n, device=q.device)[None, :] > pos
+        s = s.masked_fill(mask[None], float("-inf"))
+    p = torch.softmax(s, -1)
+    return torch.einsum("hmn,nhd->mhd", p, vv)
+
+
+def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale):
+    out = torch.empty_like(q)
+    for b in range(q.shape[0]):
+        n = int(ctx_lens[b])
+        k, v = gather_kv(k_cache, v_cache, block_tables[b], n)
+        out[b] = _attend(q[b:b + 1], k, v, scale)[0].to(q.dtype)
+    return out
+
+
+def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale):
+    out = torch.empty_like(q)
+    for s in range(len(cu_q) - 1):
+        a, b = int(cu_q[s]), int(cu_q[s + 1])
+        if b == a:
+            continue
+        n = int(ctx_lens[s])
+        k, v = gather_kv(k_cache, v_cache, block_tables[s], n)
+        out[a:b] = _attend(q[a:b], k, v, scale, causal_offset=n - (b - a)).to(q.dtype)
+    return out
+
+
+def encoder_attention(qkv, cu_seqlens, H, D, scale):
+    T = qkv.shape[0]
+    x = qkv.view(T, 3, H, D)
+    out = torch.empty(T, H, D, dtype=qkv.dtype, device=qkv.device)
+    for s in range(len(cu_seqlens) - 1):
+        a, b = int(cu_seqlens[s]), int(cu_seqlens[s + 1])
+        if b == a:
+            continue
+        out[a:b] = _attend(x[a:b, 0], x[a:b, 1], x[a:b, 2], scale).to(qkv.dtype)
+    return out
+
+
+def silu_mul(gu):
+    F = gu.shape[-1] // 2
+    g, u = gu[..., :F].float(), gu[..., F:].float()
+    return (torch.nn.functional.silu(g) * u).to(gu.dtype)
+
+
+def bias_gelu(x, bias):
+    xf = x.float() + (bias.float() if bias is not None else 0.0)
+    return torch.nn.functional.gelu(xf).to(x.dtype)
+
+
+def sample_greedy(logits):
+    return torch.argmax(logits.float(), -1).to(torch.int32)
+
+
+def knn_scores(X, Q, xnorm2=None, qnorm2=None):
+    dots = Q.float() @ X.float().T
+    if xnorm2 is None:
+        return dots
+    return -(xnorm2.float()[None, :] + qnorm2.float()[:, None] - 2 * dots)
+
+
+def l2_normalize(x):
+    xf = x.float()
+    n2 = xf.pow(2).sum(-1)
+    inv = torch.where(n2 > 0, torch.rsqrt(n2), torch.zeros_like(n2))
+    return (xf * inv[:, None]).to(x.dtype), n2
+
+
+def pool(hidden, cu_seqlens, mode="mean", normalize=True):
+    outs = []
+    for s in range(len(cu_seqlens) - 1):
+        a, b = int(cu_seqlens[s]), int(cu_seqlens[s + 1])
+        h = hidden[a:b].float()
+        if b == a:
+            v = torch.zeros(hidden.shape[-1], device=hidden.device)
+        elif mode == "cls":
+            v = h[0]
+        else:
+            v = h.mean(0)
+        if normalize:
+            n = v.norm()
+            v = v / n if n > 0 else v
+        outs.append(v)
+    return torch.stack(outs) if outs else torch.empty(0, hidden.shape[-1])
+
+
+def softmax_scale(head_dim: int) -> float:
+    return 1.0 / math.sqrt(head_dim)

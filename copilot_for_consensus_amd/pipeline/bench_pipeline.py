@@ -1,0 +1,84 @@
+"""The benchmark's unit of work: one batch of threads summarized end to end on one GPU."""
+from __future__ import annotations
+
+import dataclasses
+import random
+import time
+
+import torch
+
+
+@dataclasses.dataclass
+class StepResult:
+    threads: int
+    latencies_s: list[float]
+    generated_tokens: int
+    prompt_tokens: int
+    stage_s: dict[str, float]
+
+    def summary(self) -> str:
+        st = " ".join(f"{k}={v:.2f}s" for k, v in self.stage_s.items())
+        return (f"threads={self.threads} prompt_tok={self.prompt_tokens} gen_tok={self.generated_tokens} "
+                f"p50={sorted(self.latencies_s)[len(self.latencies_s) // 2]:.2f}s {st}")
+
+
+class BenchPipeline:
+    def __init__(self, model="mistral-7b", encoder="minilm-l6", device="cuda", threads_per_step=128,
+                 max_new_tokens=512, tp=1, prefill_tokens=16384, llm_only=False, use_graph=True, seed=0):
+        from ..models.decoder import DecoderModel, DecoderWeights, get_config
+        from ..runtime.engine import LLMEngine
+        from ..runtime.kv_cache import PagedKVCache, blocks_needed
+
+        if tp != 1:
+            raise NotImplementedError("bench TP>1 is launched through parallel.tp (DP bench uses tp=1)")
+        self.device = torch.device(device)
+        self.cfg = get_config(model)
+        self.threads_per_step = threads_per_step
+        self.max_new = max_new_tokens
+        self.llm_only = llm_only
+        self.rng = random.Random(seed)
+        self.seed = seed
+        w = DecoderWeights.random(self.cfg, self.device, seed=1234)
+        self.model = DecoderModel(w)
+        # KV budget: every thread of a step at the longest prompt we generate (3k) + max_new, x1.1
+        max_prompt = 3200
+        nblk = int(1.1 * threads_per_step * blocks_needed(max_prompt + max_new_tokens)) + 64
+        self.kv = PagedKVCache(self.cfg.layers, nblk, w.kv_heads, self.cfg.head_dim, self.device)
+        self.engine = LLMEngine(self.model, self.kv, max_prefill_tokens=prefill_tokens, use_graph=use_graph)
+        self.rag = None
+        if not llm_only:
+            from .rag import RagPipeline
+            self.rag = RagPipeline(encoder=encoder, device=self.device, decoder_vocab=self.cfg.vocab_size,
+                                   bos_id=self.cfg.bos_id, seed=seed)
+
+    def _synthetic_prompts(self, n):
+        # ~2.5-3k prompt tokens: BASELINE.md "prefill of about 2.5k-3k tokens"
+        out = []
+        for _ in range(n):
+            L = self.rng.randint(2560, 3072)
+            out.append([self.cfg.bos_id] + [self.rng.randrange(3, self.cfg.vocab_size) for _ in range(L - 1)])
+        return out
+
+    def run_step(self, step: int) -> StepResult:
+        t0 = time.perf_counter()
+        stages = {}
+        if self.rag is None:
+            prompts = self._synthetic_prompts(self.threads_per_step)
+            ctx = None
+        else:
+            ctx = self.rag.prepare(self.threads_per_step, step)
+            prompts = ctx.prompts
+            stages.update(ctx.stage_s)
+        t1 = time.perf_counter()
+        res = self.engine.generate(prompts, self.max_new, temperature=0.0, ignore_eos=True)
+        t2 = time.perf_counter()
+        stages["prefill"] = res.prefill_s
+        stages["decode"] = res.decode_s
+        if ctx is not None:
+            self.rag.finish(ctx, res)
+            stages["report"] = time.perf_counter() - t2
+        t3 = time.perf_counter()
+        lat = [t3 - t0] * len(prompts)
+        stages["total"] = t3 - t0
+        del t1
+        return StepResult(len(prompts), lat, sum(len(t) for t in res.tokens), sum(res.prompt_lens), stages)

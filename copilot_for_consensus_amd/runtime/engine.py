@@ -1,0 +1,248 @@
+"""Batched LLM generation engine (prefill + hipGraph-captured decode) over the paged KV cache.
+
+The reference summarizes one thread at a time per replica with a blocking HTTP call to
+Ollama/llama.cpp (summarization/app/service.py:289; local_llm_summarizer.py:107).  Here a
+batch of threads is generated together:
+
+  1. packed varlen prefill in chunks of ``max_prefill_tokens`` (large GEMMs for hipBLASLt, our
+     flash prefill kernel over the paged cache; long prompts are split = chunked prefill);
+  2. one decode step = embedding -> 32 x (RMSNorm, QKV GEMM, RoPE+KV write, paged decode
+     attention, O GEMM, RMSNorm, gate|up GEMM, SwiGLU, down GEMM) -> lm_head -> sampler ->
+     on-device state advance.  The whole step is captured once in a hipGraph and replayed
+     ``max_new_tokens-1`` times with NO host work or sync in between (EOS/stop flags live on the
+     device and are polled every ``stop_check_interval`` steps).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+import time
+
+import torch
+
+from ..ops import kernels as K
+from ..ops.reference import KV_BLOCK
+from .kv_cache import PagedKVCache, blocks_needed
+
+
+@dataclasses.dataclass
+class GenerationResult:
+    tokens: list[list[int]]          # generated ids per prompt (stop token excluded)
+    prompt_lens: list[int]
+    prefill_s: float = 0.0
+    decode_s: float = 0.0
+    ttft_s: float = 0.0
+    decode_steps: int = 0
+
+    @property
+    def total_s(self) -> float:
+        return self.prefill_s + self.decode_s
+
+
+class _DecodeState:
+    """Static device buffers a captured decode graph reads and writes."""
+
+    def __init__(self, B, max_blocks, max_new, device, n_part_ws):
+        i32 = dict(dtype=torch.int32, device=device)
+        self.ids = torch.zeros(B, **i32)
+        self.positions = torch.zeros(B, **i32)
+        self.ctx_lens = torch.ones(B, **i32)
+        self.slots = torch.zeros(B, **i32)
+        self.block_tables = torch.zeros(B, max_blocks, **i32)
+        self.step = torch.zeros(1, **i32)
+        self.tokens = torch.zeros(B, max_new, **i32)
+        self.done = torch.zeros(B, **i32)
+        self.next_ids = torch.zeros(B, **i32)
+        self.stop_ids = torch.zeros(0, **i32)
+        self.workspace = torch.empty(max(1, n_part_ws), dtype=torch.float32, device=device)
+        self.graph = None
+
+    def tensors(self):
+        return [self.ids, self.positions, self.ctx_lens, self.slots, self.block_tables, self.step, self.tokens,
+                self.done, self.next_ids]
+
+
+class LLMEngine:
+    def __init__(self, model, kv: PagedKVCache, max_prefill_tokens: int = 16384, use_graph: bool = True,
+                 stop_check_interval: int = 64):
+        self.model = model
+        self.cfg = model.cfg
+        self.kv = kv
+        self.device = kv.device
+        self.max_prefill_tokens = max_prefill_tokens
+        self.use_graph = use_graph and kv.device.type == "cuda"
+        self.stop_check_interval = stop_check_interval
+        self._states: dict[tuple, _DecodeState] = {}
+
+    # ------------------------------------------------------------------ helpers
+    def _part_blocks(self, B, max_blocks):
+        target = 4096
+        P = max(1, math.ceil(target / max(1, B * self.model.w.kv_heads)))
+        return max(4, math.ceil(max_blocks / P))
+
+    def _i32(self, x):
+        return torch.tensor(x, dtype=torch.int32, device=self.device)
+
+    def _prefill(self, prompts, tables, temperature, seed):
+        """Chunked packed prefill; returns first sampled token per prompt."""
+        n = len(prompts)
+        first = [0] * n
+        pos = [0] * n  # tokens of each prompt already in the cache
+        order = list(range(n))
+        while order:
+            chunk, budget = [], self.max_prefill_tokens
+            for s in list(order):
+                if budget <= 0:
+                    break
+                take = min(len(prompts[s]) - pos[s], budget)
+                chunk.append((s, pos[s], pos[s] + take))
+                budget -= take
+                if pos[s] + take == len(prompts[s]):
+                    order.remove(s)
+                else:
+                    break  # a split sequence ends the chunk
+            ids, positions, slots, cu, ctx, rows, last_rows, finishing = [], [], [], [0], [], [], [], []
+            for (s, a, b) in chunk:
+                toks = prompts[s][a:b]
+                ids.extend(toks)
+                positions.extend(range(a, b))
+                bt = tables[s]
+                slots.extend(bt[p // KV_BLOCK] * KV_BLOCK + p % KV_BLOCK for p in range(a, b))
+                cu.append(cu[-1] + (b - a))
+                ctx.append(b)
+                rows.append(s)
+                if b == len(prompts[s]):
+                    last_rows.append(cu[-1] - 1)
+                    finishing.append(s)
+                pos[s] = b
+            maxb = max(len(tables[s]) for s in rows)
+            bt = torch.zeros(len(rows), maxb, dtype=torch.int32)
+            for r, s in enumerate(rows):
+                bt[r, :len(tables[s])] = torch.tensor(tables[s], dtype=torch.int32)
+            tseq, tq0 = K.prefill_tiles(cu)
+            hidden = self.model.forward_prefill(
+                self._i32(ids), self._i32(positions), self._i32(slots), self._i32(cu), self._i32(ctx),
+                bt.to(self.device), self.kv, tiles=(self._i32(tseq), self._i32(tq0)),
+                last_idx=torch.tensor(last_rows, dtype=torch.long, device=self.device) if last_rows else None)
+            if finishing:
+                logits = self.model.logits(hidden)
+                out = torch.empty(len(finishing), dtype=torch.int32, device=self.device)
+                K.sample(logits, out, temperature, seed, torch.zeros(1, dtype=torch.int32, device=self.device))
+                for s, t in zip(finishing, out.tolist()):
+                    first[s] = t
+        return first
+
+    def _decode_step(self, st: _DecodeState, part_blocks, temperature, seed):
+        hidden = self.model.forward_decode(st.ids, st.positions, st.slots, st.ctx_lens, st.block_tables, self.kv,
+                                           attn_workspace=st.workspace, part_blocks=part_blocks)
+        logits = self.model.logits(hidden)
+        K.sample(logits, st.next_ids, temperature, seed, st.step)
+        K.decode_advance(st.next_ids, st.tokens, st.step, st.ids, st.positions, st.ctx_lens, st.slots,
+                         st.block_tables, st.done, st.stop_ids)
+
+    def _state(self, B, max_blocks, max_new, part_blocks, stop_ids):
+        key = (B, max_blocks, max_new, tuple(stop_ids))
+        st = self._states.get(key)
+        if st is None:
+            P = math.ceil(max_blocks / part_blocks)
+            ws = B * self.model.w.heads * P * (self.cfg.head_dim + 2) if P > 1 else 1
+            st = _DecodeState(B, max_blocks, max_new, self.device, ws)
+            # persistent: a captured graph holds this pointer
+            st.stop_ids = torch.tensor(list(stop_ids), dtype=torch.int32, device=self.device)
+            self._states[key] = st
+        return st
+
+    def _capture(self, st, part_blocks, temperature, seed):
+        saved = [t.clone() for t in st.tensors()]
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._decode_step(st, part_blocks, temperature, seed)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        for t, v in zip(st.tensors(), saved):
+            t.copy_(v)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._decode_step(st, part_blocks, temperature, seed)
+        for t, v in zip(st.tensors(), saved):
+            t.copy_(v)
+        st.graph = (g, part_blocks, temperature, seed)
+
+    # ------------------------------------------------------------------ API
+    @torch.inference_mode()
+    def generate(self, prompts: list[list[int]], max_new_tokens: int, temperature: float = 0.0, seed: int = 0,
+                 stop_ids: tuple[int, ...] = (), ignore_eos: bool = False) -> GenerationResult:
+        B = len(prompts)
+        if B == 0:
+            return GenerationResult([], [])
+        if any(len(p) == 0 for p in prompts):
+            raise ValueError("empty prompt")
+        if not ignore_eos and self.cfg.eos_id not in stop_ids:
+            stop_ids = tuple(stop_ids) + (self.cfg.eos_id,)
+        if ignore_eos:
+            stop_ids = ()
+        lens = [len(p) for p in prompts]
+        if max(lens) + max_new_tokens > self.cfg.max_positions:
+            raise ValueError("prompt + max_new_tokens exceeds max_positions")
+        # round the block-table width up so graphs are reused across batches of similar length
+        need = [blocks_needed(n + max_new_tokens) for n in lens]
+        max_blocks = 8 * math.ceil(max(need) / 8)
+        tables = [self.kv.pool.alloc(n) for n in need]
+        try:
+            sync = self.device.type == "cuda"
+            if sync:
+                torch.cuda.synchronize(self.device)
+            t0 = time.perf_counter()
+            first = self._prefill(prompts, tables, temperature, seed)
+            if sync:
+                torch.cuda.synchronize(self.device)
+            t1 = time.perf_counter()
+
+            part_blocks = self._part_blocks(B, max_blocks)
+            st = self._state(B, max_blocks, max_new_tokens, part_blocks, stop_ids)
+            st.block_tables.zero_()
+            bt = torch.zeros(B, max_blocks, dtype=torch.int32)
+            for b, t in enumerate(tables):
+                bt[b, :len(t)] = torch.tensor(t, dtype=torch.int32)
+            st.block_tables.copy_(bt)
+            f = torch.tensor(first, dtype=torch.int32)
+            lens_t = torch.tensor(lens, dtype=torch.int32)
+            st.ids.copy_(f)
+            st.positions.copy_(lens_t)
+            st.ctx_lens.copy_(lens_t + 1)
+            pos = lens_t.long()
+            st.slots.copy_(bt[torch.arange(B), pos // KV_BLOCK] * KV_BLOCK + pos % KV_BLOCK)
+            st.tokens.zero_()
+            st.tokens[:, 0].copy_(f)
+            st.step.fill_(1)
+            st.done.copy_(torch.isin(f, st.stop_ids.cpu()).to(torch.int32) if stop_ids else torch.zeros(B, dtype=torch.int32))
+
+            steps = 0
+            if self.use_graph and (st.graph is None or st.graph[1:] != (part_blocks, temperature, seed)):
+                self._capture(st, part_blocks, temperature, seed)
+            for i in range(1, max_new_tokens):
+                if self.use_graph:
+                    st.graph[0].replay()
+                else:
+                    self._decode_step(st, part_blocks, temperature, seed)
+                steps += 1
+                if stop_ids and (i % self.stop_check_interval == 0) and bool(st.done.all()):
+                    break
+            tokens = st.tokens.cpu()
+            if sync:
+                torch.cuda.synchronize(self.device)
+            t2 = time.perf_counter()
+        finally:
+            for t in tables:
+                self.kv.pool.free(t)
+        out = []
+        stop = set(stop_ids)
+        for b in range(B):
+            row = tokens[b, :steps + 1].tolist()
+            for j, t in enumerate(row):
+                if t in stop:
+                    row = row[:j]
+                    break
+            out.append(row)
+        return GenerationResult(out, lens, prefill_s=t1 - t0, decode_s=t2 - t1, ttft_s=t1 - t0, decode_steps=steps)

@@ -1,0 +1,563 @@
+// Attention kernels for gfx950 (CDNA4), bf16 in / fp32 accumulate on MFMA 16x16x32.
+//
+//   * paged decode attention (GQA, split-K over context partitions + LSE combine)
+//   * varlen causal prefill attention over the paged KV cache (flash-style online softmax)
+//   * varlen bidirectional encoder attention (BERT / MiniLM / BGE, head_dim 32 or 64)
+//
+// They replace the attention inside the engines the reference drives over HTTP
+// (Ollama /api/generate: local_llm_summarizer.py:107; llama.cpp /completion:
+// llamacpp_summarizer.py:108) and inside SentenceTransformer.encode
+// (sentence_transformer_provider.py:93).  The reference itself has no kernels.
+//
+// Layout decisions (MI355X-first, not a CUDA translation):
+//   * "Swapped" products: S^T = K . Q^T and O^T = V^T . P^T.  With the 16x16x32 C/D map
+//     (col = lane&15, row = 4*(lane>>4)+i) every lane then owns ONE query column, so the
+//     online-softmax max/sum are lane-local plus two xor-shuffles, and the S^T accumulator is
+//     already the P^T B-operand of the next MFMA (guide §3 "accumulator as the next operand").
+//   * KV cache block = 32 tokens = one MFMA k-step.  K is stored [blk][kvh][32][D] (row = key),
+//     V is stored TRANSPOSED [blk][kvh][D][32] with the keys of each block permuted so that slot
+//     8g+j holds key perm(g,j) = (j<4 ? 4g+j : 16+4g+j-4).  That is exactly the key order a lane
+//     holds in its S^T registers, so the V^T A-operand is one contiguous 16-byte load per lane
+//     (no LDS transpose, no ds_read_tr needed) in both decode (straight from HBM) and prefill.
+//   * LDS tiles are XOR-swizzled for conflict-free ds_read_b128 (guide §5.5 T2); the swizzles
+//     were derived against the gfx950 ds_read_b128 lane groups {0-3,12-15,20-27}, ...
+#include "common.h"
+
+namespace {
+
+constexpr int KV_BS = 32;          // tokens per KV-cache block
+constexpr float LOG2E = 1.4426950408889634f;
+
+__device__ __forceinline__ bf16x8_t as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+__device__ __forceinline__ f32x4_t mfma16(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// P^T fragment for keys [32ks, 32ks+32): {p[2ks][0..3], p[2ks+1][0..3]} as bf16.
+__device__ __forceinline__ bf16x8_t pack_p(const f32x4_t& a, const f32x4_t& b) {
+  uint4 u;
+  u.x = pack2bf(a[0], a[1]); u.y = pack2bf(a[2], a[3]);
+  u.z = pack2bf(b[0], b[1]); u.w = pack2bf(b[2], b[3]);
+  return as_bf16x8(u);
+}
+
+// ------------------------------------------------------------------------------------------
+// Paged decode attention.
+// grid = (P partitions, Hkv, B); block = 256 (4 waves).  Each wave walks the partition's KV
+// blocks with stride 4, K/V fragments straight from HBM into VGPRs (guide: "GEMV / M<=16 decode:
+// load straight to VGPRs"), next block prefetched while the current one is in the MFMAs.
+// The G = Hq/Hkv query heads of the kv-head share every K/V byte (GQA packing: the G heads are
+// the MFMA's B columns).
+// ------------------------------------------------------------------------------------------
+template <int G>
+__global__ void __launch_bounds__(256) paged_decode_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    const int32_t* __restrict__ block_tables, const int32_t* __restrict__ ctx_lens, float scale_log2, int Hkv,
+    int max_blocks, int part_blocks, int P, float* __restrict__ part_o, float* __restrict__ part_ml,
+    uint16_t* __restrict__ out) {
+  constexpr int D = 128;
+  const int p = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int Hq = Hkv * G;
+  const int ctx = ctx_lens[b];
+  const int nblk = (ctx + KV_BS - 1) / KV_BS;
+  const int blk0 = p * part_blocks;
+  const int blk1 = min(nblk, blk0 + part_blocks);
+
+  __shared__ float sm_o[4][D][17];
+  __shared__ float sm_m[4][16], sm_l[4][16];
+
+  // Q^T B-operand: lane holds Q[head h*G+col][32c + 8g .. +7]; columns >= G are zero.
+  bf16x8_t qf[4];
+  {
+    const bool valid = col < G;
+    const uint16_t* qr = q + ((size_t)b * Hq + h * G + (valid ? col : 0)) * D;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      uint4 v = valid ? *reinterpret_cast<const uint4*>(qr + 32 * c + 8 * g) : make_uint4(0, 0, 0, 0);
+      qf[c] = as_bf16x8(v);
+    }
+  }
+
+  f32x4_t o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+  const int32_t* bt = block_tables + (size_t)b * max_blocks;
+  const size_t head_stride = (size_t)KV_BS * D;  // elements per (block, kv-head)
+
+  uint4 kr[8], vr[8];
+  auto load_blk = [&](int bi, uint4* kk, uint4* vv) {
+    const size_t base = ((size_t)bt[bi] * Hkv + h) * head_stride;
+    const uint16_t* kb = kc + base;
+    const uint16_t* vb = vc + base;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        kk[st * 4 + c] = *reinterpret_cast<const uint4*>(kb + (16 * st + col) * D + 32 * c + 8 * g);
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+      vv[dt] = *reinterpret_cast<const uint4*>(vb + (16 * dt + col) * KV_BS + 8 * g);
+  };
+
+  int bi = blk0 + w;
+  if (bi < blk1) load_blk(bi, kr, vr);
+  for (; bi < blk1; bi += 4) {
+    uint4 kn[8], vn[8];
+    const bool more = bi + 4 < blk1;
+    if (more) load_blk(bi + 4, kn, vn);
+
+    f32x4_t s[2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      s[st] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s[st] = mfma16(as_bf16x8(kr[st * 4 + c]), qf[c], s[st]);
+    }
+    const int key0 = bi * KV_BS;
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = key0 + 16 * st + 4 * g + i;
+        float v = s[st][i] * scale_log2;
+        v = key < ctx ? v : -INFINITY;
+        s[st][i] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mn = fmaxf(m, tmax);
+    const float alpha = exp2f(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { const float e = exp2f(s[st][i] - mn); s[st][i] = e; rs += e; }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mn;
+    const bf16x8_t pf = pack_p(s[0], s[1]);
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      o[dt] *= alpha;
+      o[dt] = mfma16(as_bf16x8(vr[dt]), pf, o[dt]);
+    }
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { kr[i] = kn[i]; vr[i] = vn[i]; }
+    }
+  }
+
+  // Combine the 4 waves through LDS.  Lane (col, g) holds O^T[d = 16dt + 4g + i][col].
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sm_o[w][16 * dt + 4 * g + i][col] = o[dt][i];
+  if (g == 0) { sm_m[w][col] = m; sm_l[w][col] = l; }
+  __syncthreads();
+
+  for (int idx = threadIdx.x; idx < G * D; idx += 256) {
+    const int qh = idx / D, d = idx % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, sm_m[ww][qh]);
+    float L = 0.f, O = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) {
+        const float f = exp2f(sm_m[ww][qh] - M);
+        L += sm_l[ww][qh] * f;
+        O += sm_o[ww][d][qh] * f;
+      }
+    }
+    const int head = h * G + qh;
+    if (P == 1) {
+      out[((size_t)b * Hq + head) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+    } else {
+      const size_t pi = ((size_t)b * Hq + head) * P + p;
+      part_o[pi * D + d] = O;
+      if (d == 0) { part_ml[pi * 2] = M; part_ml[pi * 2 + 1] = L; }
+    }
+  }
+}
+
+// grid = (Hq, B), block = 128: merge the P partition results of one (seq, head).
+__global__ void __launch_bounds__(128) decode_combine_kernel(const float* __restrict__ part_o,
+                                                             const float* __restrict__ part_ml, int P, int Hq,
+                                                             uint16_t* __restrict__ out) {
+  constexpr int D = 128;
+  const int head = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
+  const size_t base = ((size_t)b * Hq + head) * P;
+  float M = -INFINITY;
+  for (int p = 0; p < P; ++p) M = fmaxf(M, part_ml[(base + p) * 2]);
+  float L = 0.f, O = 0.f;
+  if (M != -INFINITY) {
+    for (int p = 0; p < P; ++p) {
+      const float mp = part_ml[(base + p) * 2];
+      if (mp == -INFINITY) continue;
+      const float f = exp2f(mp - M);
+      L += part_ml[(base + p) * 2 + 1] * f;
+      O += part_o[(base + p) * D + d] * f;
+    }
+  }
+  out[((size_t)b * Hq + head) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+}
+
+// ------------------------------------------------------------------------------------------
+// Varlen causal prefill over the paged cache (D = 128).
+// grid = (n_tiles, Hq); block = 256 = 4 waves x 16 query rows = 64-row query tile.
+// Tile t covers query rows [tile_q0[t], +64) of sequence tile_seq[t]; those rows sit at
+// positions ctx - q_len + row (chunked prefill / prefix reuse: keys come from the cache).
+// K tile (64 keys x 128) and V^T tile (2 blocks x 128 x 32) are double-buffered in LDS,
+// register-staged: next tile's global loads issue before this tile's MFMAs, LDS writes after
+// (guide §5.5 T14), one barrier per tile.
+// ------------------------------------------------------------------------------------------
+constexpr int PF_KT = 64;  // keys per tile
+
+__device__ __forceinline__ int k_lds_off(int row, int ch) { return row * 256 + ((ch ^ (row & 15)) << 4); }
+__device__ __forceinline__ int v_lds_off(int blk, int d, int ch) {
+  return blk * 128 * 64 + d * 64 + ((ch ^ (((d >> 3) & 1) << 1)) << 4);
+}
+
+__global__ void __launch_bounds__(256) prefill_paged_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    const int32_t* __restrict__ block_tables, const int32_t* __restrict__ cu_q, const int32_t* __restrict__ ctx_lens,
+    const int32_t* __restrict__ tile_seq, const int32_t* __restrict__ tile_q0, float scale_log2, int Hq, int Hkv,
+    int max_blocks, uint16_t* __restrict__ out) {
+  constexpr int D = 128;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = blockIdx.x, hq = blockIdx.y;
+  const int G = Hq / Hkv, hk = hq / G;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
+  const int col = lane & 15, g = lane >> 4;
+  const int s = tile_seq[t], qs = tile_q0[t];
+  const int q_begin = cu_q[s], q_len = cu_q[s + 1] - q_begin;
+  const int ctx = ctx_lens[s];
+  const int pos_base = ctx - q_len;
+  const int row_last = min(qs + 63, q_len - 1);
+  const int kend = pos_base + row_last + 1;  // keys [0, kend) are needed by this tile
+  const int ntiles = (kend + PF_KT - 1) / PF_KT;
+  const int32_t* bt = block_tables + (size_t)s * max_blocks;
+
+  // Q^T fragments for this wave's 16 rows.
+  const int my_row = qs + 16 * w + col;
+  const int my_pos = pos_base + my_row;
+  bf16x8_t qf[4];
+  {
+    const int r = min(my_row, q_len - 1);
+    const uint16_t* qr = q + ((size_t)(q_begin + r) * Hq + hq) * D;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) qf[c] = as_bf16x8(*reinterpret_cast<const uint4*>(qr + 32 * c + 8 * g));
+  }
+
+  // LDS: [K buf0 16K][K buf1 16K][V buf0 16K][V buf1 16K]
+
+  uint4 kst[4], vst[4];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = tid + 256 * i;
+      {  // K: row = id>>4 (key within tile), ch = id&15
+        const int row = id >> 4, ch = id & 15, key = kt * PF_KT + row;
+        if (key < kend) {
+          const int blk = bt[key / KV_BS];
+          kst[i] = *reinterpret_cast<const uint4*>(kc + (((size_t)blk * Hkv + hk) * KV_BS + (key % KV_BS)) * D + ch * 8);
+        } else {
+          kst[i] = make_uint4(0, 0, 0, 0);
+        }
+      }
+      {  // V^T: blk_i = id>>9, d = (id>>2)&127, ch = id&3
+        const int bi = id >> 9, d = (id >> 2) & 127, ch = id & 3;
+        const int key0 = kt * PF_KT + bi * KV_BS;
+        if (key0 < kend) {
+          const int blk = bt[key0 / KV_BS];
+          vst[i] = *reinterpret_cast<const uint4*>(vc + (((size_t)blk * Hkv + hk) * D + d) * KV_BS + ch * 8);
+        } else {
+          vst[i] = make_uint4(0, 0, 0, 0);
+        }
+      }
+    }
+  };
+  auto lwrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = tid + 256 * i;
+      *reinterpret_cast<uint4*>(smem + buf * 16384 + k_lds_off(id >> 4, id & 15)) = kst[i];
+      *reinterpret_cast<uint4*>(smem + 32768 + buf * 16384 + v_lds_off(id >> 9, (id >> 2) & 127, id & 3)) = vst[i];
+    }
+  };
+
+  f32x4_t o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+  gload(0);
+  lwrite(0);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < ntiles;
+    if (more) gload(kt + 1);
+
+    const char* kb = smem + cur * 16384;
+    const char* vb = smem + 32768 + cur * 16384;
+    f32x4_t sc[4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      sc[st] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const int row = 16 * st + col;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint4 kv = *reinterpret_cast<const uint4*>(kb + k_lds_off(row, 4 * c + g));
+        sc[st] = mfma16(as_bf16x8(kv), qf[c], sc[st]);
+      }
+    }
+    const int key0 = kt * PF_KT;
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = key0 + 16 * st + 4 * g + i;
+        float v = sc[st][i] * scale_log2;
+        v = key <= my_pos ? v : -INFINITY;
+        sc[st][i] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mn = fmaxf(m, tmax);
+    // Rows past q_len (tile tail) can see only masked keys; keep them finite.
+    const float mref = mn == -INFINITY ? 0.f : mn;
+    const float alpha = exp2f(m - mref);
+    float rs = 0.f;
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { const float e = exp2f(sc[st][i] - mref); sc[st][i] = e; rs += e; }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mn;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8_t pf = pack_p(sc[2 * ks], sc[2 * ks + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        const uint4 vv = *reinterpret_cast<const uint4*>(vb + v_lds_off(ks, 16 * dt + col, g));
+        o[dt] = mfma16(as_bf16x8(vv), pf, o[dt]);
+      }
+    }
+    if (more) lwrite(cur ^ 1);
+    __syncthreads();
+  }
+
+  if (my_row < q_len) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    uint16_t* orow = out + ((size_t)(q_begin + my_row) * Hq + hq) * D;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      uint2 pk;
+      pk.x = pack2bf(o[dt][0] * inv, o[dt][1] * inv);
+      pk.y = pack2bf(o[dt][2] * inv, o[dt][3] * inv);
+      *reinterpret_cast<uint2*>(orow + 16 * dt + 4 * g) = pk;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Varlen bidirectional encoder attention (BERT family), D in {32, 64}, S <= 512.
+// Input qkv is the fused projection output [T, 3*H*D] (q | k | v, head-major inside each).
+// grid = (n_tiles, H); block = 256 = 4 waves x 16 query rows.  The WHOLE key/value range of
+// the sequence is staged once in LDS (K row-major, V transposed with the per-32-key slot
+// permutation), then each wave runs the swapped-product online softmax over it.
+// ------------------------------------------------------------------------------------------
+template <int D>
+__global__ void __launch_bounds__(256) encoder_attn_kernel(const uint16_t* __restrict__ qkv,
+                                                           const int32_t* __restrict__ cu_seqlens,
+                                                           const int32_t* __restrict__ tile_seq,
+                                                           const int32_t* __restrict__ tile_q0, float scale_log2,
+                                                           int H, uint16_t* __restrict__ out) {
+  constexpr int NC = D / 8;         // 16-byte chunks per K row
+  constexpr int KSTEPS = D / 32;    // MFMA k-steps over head_dim
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int t = blockIdx.x, h = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
+  const int col = lane & 15, g = lane >> 4;
+  const int s = tile_seq[t], qs = tile_q0[t];
+  const int beg = cu_seqlens[s], S = cu_seqlens[s + 1] - beg;
+  const int Spad = (S + 127) & ~127;       // V^T rows hold Spad slots (multiple of 128 => >=16 chunks)
+  const int row_stride = 3 * H * D;
+  char* klds = smem;                              // [Spad][D]  bf16, swizzled per 16-row group
+  char* vlds = smem + (size_t)Spad * D * 2;       // [D][Spad]  bf16, slot-permuted, swizzled
+
+  // K rows: chunk ch of row r at r*D*2 + ((ch ^ sw(r)) * 16).
+  auto koff = [&](int r, int ch) -> int {
+    if constexpr (D == 32) return r * 64 + ((ch ^ (((r >> 3) & 1) << 1)) << 4);
+    else return r * 128 + ((ch ^ (r & 7)) << 4);
+  };
+  // V^T element (d, slot): row d has Spad*2 bytes; 16-byte chunk c = slot>>3 swizzled by d&15.
+  auto voff_chunk = [&](int d, int c) -> int { return d * Spad * 2 + ((c ^ (d & 15)) << 4); };
+
+  for (int id = tid; id < Spad * NC; id += 256) {
+    const int r = id / NC, ch = id % NC;
+    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+    if (r < S) {
+      const uint16_t* base = qkv + (size_t)(beg + r) * row_stride;
+      kv = *reinterpret_cast<const uint4*>(base + H * D + h * D + ch * 8);
+      vv = *reinterpret_cast<const uint4*>(base + 2 * H * D + h * D + ch * 8);
+    }
+    *reinterpret_cast<uint4*>(klds + koff(r, ch)) = kv;
+    // scatter V row r (d = ch*8 .. +7) into V^T at the permuted slot of key r
+    const int kin = r & 31, hi = kin >> 4, gg = (kin >> 2) & 3, jj = (kin & 3) + 4 * hi;
+    const int slot = (r & ~31) + 8 * gg + jj;
+    const uint16_t* ve = reinterpret_cast<const uint16_t*>(&vv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int d = ch * 8 + e;
+      *reinterpret_cast<uint16_t*>(vlds + voff_chunk(d, slot >> 3) + (slot & 7) * 2) = ve[e];
+    }
+  }
+
+  const int my_row = qs + 16 * w + col;
+  bf16x8_t qf[KSTEPS];
+  {
+    const int r = min(my_row, S - 1);
+    const uint16_t* qr = qkv + (size_t)(beg + r) * row_stride + h * D;
+#pragma unroll
+    for (int c = 0; c < KSTEPS; ++c) qf[c] = as_bf16x8(*reinterpret_cast<const uint4*>(qr + 32 * c + 8 * g));
+  }
+  __syncthreads();
+
+  constexpr int DT = D / 16;
+  f32x4_t o[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) o[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+  for (int k0 = 0; k0 < S; k0 += 32) {
+    f32x4_t sc[2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      sc[st] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const int r = k0 + 16 * st + col;
+#pragma unroll
+      for (int c = 0; c < KSTEPS; ++c) {
+        const uint4 kv = *reinterpret_cast<const uint4*>(klds + koff(r, 4 * c + g));
+        sc[st] = mfma16(as_bf16x8(kv), qf[c], sc[st]);
+      }
+    }
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = k0 + 16 * st + 4 * g + i;
+        float v = sc[st][i] * scale_log2;
+        v = key < S ? v : -INFINITY;
+        sc[st][i] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mn = fmaxf(m, tmax);
+    const float alpha = exp2f(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { const float e = exp2f(sc[st][i] - mn); sc[st][i] = e; rs += e; }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mn;
+    const bf16x8_t pf = pack_p(sc[0], sc[1]);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      o[dt] *= alpha;
+      const uint4 vv = *reinterpret_cast<const uint4*>(vlds + voff_chunk(16 * dt + col, (k0 >> 3) + g));
+      o[dt] = mfma16(as_bf16x8(vv), pf, o[dt]);
+    }
+  }
+
+  if (my_row < S) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    uint16_t* orow = out + ((size_t)(beg + my_row) * H + h) * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      uint2 pk;
+      pk.x = pack2bf(o[dt][0] * inv, o[dt][1] * inv);
+      pk.y = pack2bf(o[dt][2] * inv, o[dt][3] * inv);
+      *reinterpret_cast<uint2*>(orow + 16 * dt + 4 * g) = pk;
+    }
+  }
+}
+
+}  // namespace
+
+// q: [B, Hq, 128] bf16; caches per layer as documented above; out: [B, Hq, 128] bf16.
+// part_o / part_ml: fp32 workspaces of B*Hq*P*128 and B*Hq*P*2 floats (unused when P == 1).
+CFC_API int cfc_paged_decode_attention(const void* q, const void* k_cache, const void* v_cache,
+                                       const int32_t* block_tables, const int32_t* ctx_lens, int B, int Hq, int Hkv,
+                                       int head_dim, int max_blocks, int part_blocks, int P, float scale,
+                                       float* part_o, float* part_ml, void* out, hipStream_t stream) {
+  if (head_dim != 128 || Hq % Hkv != 0 || B <= 0 || P <= 0) return -1;
+  const int G = Hq / Hkv;
+  dim3 grid(P, Hkv, B);
+  const float sl2 = scale * LOG2E;
+#define DEC_ARGS (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, ctx_lens, sl2, \
+    Hkv, max_blocks, part_blocks, P, part_o, part_ml, (uint16_t*)out
+  switch (G) {
+    case 1: paged_decode_kernel<1><<<grid, 256, 0, stream>>>(DEC_ARGS); break;
+    case 2: paged_decode_kernel<2><<<grid, 256, 0, stream>>>(DEC_ARGS); break;
+    case 4: paged_decode_kernel<4><<<grid, 256, 0, stream>>>(DEC_ARGS); break;
+    case 8: paged_decode_kernel<8><<<grid, 256, 0, stream>>>(DEC_ARGS); break;
+    case 16: paged_decode_kernel<16><<<grid, 256, 0, stream>>>(DEC_ARGS); break;
+    default: return -3;
+  }
+#undef DEC_ARGS
+  if (P > 1) decode_combine_kernel<<<dim3(Hq, B), 128, 0, stream>>>(part_o, part_ml, P, Hq, (uint16_t*)out);
+  return CFC_CHECK_LAUNCH();
+}
+
+CFC_API int cfc_prefill_attention(const void* q, const void* k_cache, const void* v_cache, const int32_t* block_tables,
+                                  const int32_t* cu_q, const int32_t* ctx_lens, const int32_t* tile_seq,
+                                  const int32_t* tile_q0, int n_tiles, int Hq, int Hkv, int head_dim, int max_blocks,
+                                  float scale, void* out, hipStream_t stream) {
+  if (head_dim != 128 || Hq % Hkv != 0) return -1;
+  if (n_tiles <= 0) return 0;
+  const size_t lds = 65536;
+  prefill_paged_kernel<<<dim3(n_tiles, Hq), 256, lds, stream>>>(
+      (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, cu_q, ctx_lens, tile_seq,
+      tile_q0, scale * LOG2E, Hq, Hkv, max_blocks, (uint16_t*)out);
+  return CFC_CHECK_LAUNCH();
+}
+
+CFC_API int cfc_encoder_attention(const void* qkv, const int32_t* cu_seqlens, const int32_t* tile_seq,
+                                  const int32_t* tile_q0, int n_tiles, int H, int head_dim, int max_seqlen, float scale,
+                                  void* out, hipStream_t stream) {
+  if (n_tiles <= 0) return 0;
+  if (max_seqlen > 512) return -2;
+  const int spad = (max_seqlen + 127) & ~127;
+  const size_t lds = (size_t)spad * head_dim * 2 * 2;
+  if (head_dim == 32) {
+    encoder_attn_kernel<32><<<dim3(n_tiles, H), 256, lds, stream>>>((const uint16_t*)qkv, cu_seqlens, tile_seq, tile_q0,
+                                                                    scale * LOG2E, H, (uint16_t*)out);
+  } else if (head_dim == 64) {
+    encoder_attn_kernel<64><<<dim3(n_tiles, H), 256, lds, stream>>>((const uint16_t*)qkv, cu_seqlens, tile_seq, tile_q0,
+                                                                    scale * LOG2E, H, (uint16_t*)out);
+  } else {
+    return -1;
+  }
+  return CFC_CHECK_LAUNCH();
+}

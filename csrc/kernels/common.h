@@ -1,0 +1,80 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of copilot_for_consensus_amd.
+//
+// Conventions used by every kernel in this directory:
+//   * bf16 tensors are passed as `const uint16_t*` / `uint16_t*` (raw bits) and converted with
+//     the helpers below; vector loads go through 16-byte `uint4` (8 bf16) whenever the row
+//     length allows it (guide §6 Guideline 13: scalar bf16 loads cost 2-2.5x).
+//   * Wavefront = 64 lanes; block sizes are multiples of 64.
+//   * Every launcher is `extern "C"` and takes an explicit hipStream_t so PyTorch's current
+//     stream (and therefore hipGraph capture) is honoured.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CFC_API extern "C" __attribute__((visibility("default")))
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// Round-to-nearest-even f32 -> bf16 (NaN preserved by forcing a quiet NaN payload).
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+__device__ __forceinline__ uint32_t pack2bf(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ void unpack8(const uint4 v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 r;
+  r.x = pack2bf(f[0], f[1]); r.y = pack2bf(f[2], f[3]);
+  r.z = pack2bf(f[4], f[5]); r.w = pack2bf(f[6], f[7]);
+  return r;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024 (multiple of 64). `red` must hold >= 16 floats.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+// XCD-aware bijective remap of a 1-D block id (guide §5 "XCD swizzle must be bijective"):
+// consecutive logical tiles land on the same XCD so neighbouring tiles share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+#define CFC_CHECK_LAUNCH() (int)hipGetLastError()

@@ -1,0 +1,264 @@
+// Memory-bound fused elementwise kernels for the decoder/encoder hot path:
+//   * RoPE (rotate-half, host-precomputed cos/sin table) fused with the paged KV-cache write
+//   * SwiGLU activation (silu(gate) * up) on the fused gate|up projection output
+//   * bias + GELU (erf) for the BERT FFN
+//   * token-embedding gather
+//   * greedy argmax / Gumbel-max temperature sampling + on-device decode-state advance, so a
+//     whole decode step (and the EOS/stop check) replays from a hipGraph with no
+//     host synchronisation.
+// All loads/stores are 16-byte vectors (guide §6 Guideline 13).
+#include "common.h"
+
+namespace {
+
+constexpr int KV_BS = 32;
+
+__device__ __forceinline__ int v_slot(int key_in_block) {
+  const int hi = key_in_block >> 4, g = (key_in_block >> 2) & 3, j = (key_in_block & 3) + 4 * hi;
+  return 8 * g + j;
+}
+
+// grid = T tokens, block = 256.
+// qkv: [T, (Hq + 2*Hkv) * D] (q heads | k heads | v heads), positions [T], slots [T] (-1 = skip
+// cache write), cos_sin [max_pos][D/2][2] fp32 (cos, sin interleaved).
+__global__ void __launch_bounds__(256) rope_kv_kernel(const uint16_t* __restrict__ qkv, const int32_t* __restrict__ positions,
+                                                      const int32_t* __restrict__ slots, const float* __restrict__ cos_sin,
+                                                      uint16_t* __restrict__ q_out, uint16_t* __restrict__ k_cache,
+                                                      uint16_t* __restrict__ v_cache, int Hq, int Hkv, int D) {
+  const int tok = blockIdx.x;
+  const int half = D / 2, nv = half / 8;  // 8-element vectors per half-head
+  const int stride = (Hq + 2 * Hkv) * D;
+  const uint16_t* row = qkv + (size_t)tok * stride;
+  const int pos = positions[tok];
+  const int slot = slots[tok];
+  const float* cs = cos_sin + (size_t)pos * half * 2;
+  const int n_rot = (Hq + Hkv) * nv;
+  const int n_v = Hkv * (D / 8);
+  for (int it = threadIdx.x; it < n_rot + n_v; it += blockDim.x) {
+    if (it < n_rot) {
+      const int head = it / nv, c = it % nv;  // head < Hq: query, else key (head - Hq)
+      const uint16_t* src = row + head * D;
+      float a[8], b[8], ra[8], rb[8];
+      unpack8(*reinterpret_cast<const uint4*>(src + c * 8), a);
+      unpack8(*reinterpret_cast<const uint4*>(src + half + c * 8), b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float cv = cs[(c * 8 + j) * 2], sv = cs[(c * 8 + j) * 2 + 1];
+        ra[j] = a[j] * cv - b[j] * sv;
+        rb[j] = b[j] * cv + a[j] * sv;
+      }
+      const uint4 pa = pack8(ra), pb = pack8(rb);
+      if (head < Hq) {
+        uint16_t* dst = q_out + ((size_t)tok * Hq + head) * D;
+        *reinterpret_cast<uint4*>(dst + c * 8) = pa;
+        *reinterpret_cast<uint4*>(dst + half + c * 8) = pb;
+      } else if (slot >= 0) {
+        const int kh = head - Hq;
+        const int blk = slot / KV_BS, off = slot % KV_BS;
+        uint16_t* dst = k_cache + (((size_t)blk * Hkv + kh) * KV_BS + off) * D;
+        *reinterpret_cast<uint4*>(dst + c * 8) = pa;
+        *reinterpret_cast<uint4*>(dst + half + c * 8) = pb;
+      }
+    } else if (slot >= 0) {
+      const int v = it - n_rot;
+      const int kh = v / (D / 8), c = v % (D / 8);
+      const uint4 val = *reinterpret_cast<const uint4*>(row + (Hq + Hkv + kh) * D + c * 8);
+      const int blk = slot / KV_BS, off = slot % KV_BS;
+      const int sl = v_slot(off);
+      uint16_t* dst = v_cache + (((size_t)blk * Hkv + kh) * D + c * 8) * KV_BS + sl;
+      const uint16_t* e = reinterpret_cast<const uint16_t*>(&val);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dst[j * KV_BS] = e[j];
+    }
+  }
+}
+
+// out[t, f] = silu(gu[t, f]) * gu[t, F + f]
+__global__ void silu_mul_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ gu, int T, int F) {
+  const int nvec = F / 8;
+  const size_t total = (size_t)T * nvec;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t t = i / nvec, c = i % nvec;
+    float a[8], b[8], r[8];
+    unpack8(*reinterpret_cast<const uint4*>(gu + t * 2 * F + c * 8), a);
+    unpack8(*reinterpret_cast<const uint4*>(gu + t * 2 * F + F + c * 8), b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = a[j] / (1.f + __expf(-a[j])) * b[j];
+    *reinterpret_cast<uint4*>(out + t * F + c * 8) = pack8(r);
+  }
+}
+
+// out[t, f] = gelu_erf(x[t, f] + bias[f])   (in place allowed)
+__global__ void bias_gelu_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ x,
+                                 const uint16_t* __restrict__ bias, int T, int F) {
+  const int nvec = F / 8;
+  const size_t total = (size_t)T * nvec;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t c = i % nvec;
+    float a[8], b[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[i], a);
+    if (bias) unpack8(reinterpret_cast<const uint4*>(bias)[c], b);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = a[j] + b[j];
+      a[j] = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+    }
+    reinterpret_cast<uint4*>(out)[i] = pack8(a);
+  }
+}
+
+// out[t, :] = table[ids[t], :]
+__global__ void embedding_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ table,
+                                 const int32_t* __restrict__ ids, int T, int dim) {
+  const int nvec = dim / 8;
+  const int t = blockIdx.x;
+  const uint4* src = reinterpret_cast<const uint4*>(table + (size_t)ids[t] * dim);
+  uint4* dst = reinterpret_cast<uint4*>(out + (size_t)t * dim);
+  for (int c = threadIdx.x; c < nvec; c += blockDim.x) dst[c] = src[c];
+}
+
+__device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+
+// One workgroup per row. temperature <= 0 => greedy argmax (lowest index wins ties);
+// otherwise Gumbel-max sampling: argmax(logit/T + Gumbel(seed, step, row, idx)), which draws
+// exactly from softmax(logit/T).  `step` is read from device memory so graph replays advance it.
+__global__ void __launch_bounds__(256) sample_kernel(const uint16_t* __restrict__ logits, int V, float temperature,
+                                                     uint32_t seed, const int32_t* __restrict__ step_ptr,
+                                                     int32_t* __restrict__ out_ids) {
+  const int row = blockIdx.x;
+  const uint16_t* lr = logits + (size_t)row * V;
+  const uint32_t step = step_ptr ? (uint32_t)*step_ptr : 0u;
+  float best = -INFINITY;
+  int best_i = 0x7fffffff;
+  const int nvec = V / 8;
+  const bool sample = temperature > 0.f;
+  const float inv_t = sample ? 1.f / temperature : 1.f;
+  for (int c = threadIdx.x; c < nvec; c += blockDim.x) {
+    float v[8];
+    unpack8(reinterpret_cast<const uint4*>(lr)[c], v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float x = v[j];
+      const int idx = c * 8 + j;
+      if (sample) {
+        const uint32_t h = hash_u32(seed ^ hash_u32(step * 0x9E3779B9u ^ hash_u32(row * 0x85EBCA6Bu ^ (uint32_t)idx)));
+        const float u = ((h >> 8) + 0.5f) * (1.f / 16777216.f);
+        x = x * inv_t - __logf(-__logf(u));
+      }
+      if (x > best || (x == best && idx < best_i)) { best = x; best_i = idx; }
+    }
+  }
+  for (int idx = nvec * 8 + threadIdx.x; idx < V; idx += blockDim.x) {  // tail (V % 8)
+    float x = bf2f(lr[idx]);
+    if (x > best || (x == best && idx < best_i)) { best = x; best_i = idx; }
+  }
+  __shared__ float sb[4];
+  __shared__ int si[4];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(best_i, o, 64);
+    if (ob > best || (ob == best && oi < best_i)) { best = ob; best_i = oi; }
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { sb[wid] = best; si[wid] = best_i; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i)
+      if (sb[i] > best || (sb[i] == best && si[i] < best_i)) { best = sb[i]; best_i = si[i]; }
+    out_ids[row] = best_i;
+  }
+}
+
+// Advance the per-sequence decode state after sampling (one thread per sequence):
+//   tokens[b][step] = next[b]; input_ids[b] = next[b]; positions[b]++; ctx_lens[b]++;
+//   slots[b] = block_tables[b][pos/32]*32 + pos%32; done[b] |= next[b] in stop_ids.
+// Thread 0 of block 0 also bumps the device step counter.
+__global__ void decode_advance_kernel(const int32_t* __restrict__ next, int32_t* __restrict__ tokens, int max_new,
+                                      int32_t* __restrict__ step_ptr, int32_t* __restrict__ input_ids,
+                                      int32_t* __restrict__ positions, int32_t* __restrict__ ctx_lens,
+                                      int32_t* __restrict__ slots, const int32_t* __restrict__ block_tables,
+                                      int max_blocks, int32_t* __restrict__ done, const int32_t* __restrict__ stop_ids,
+                                      int n_stop, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int step = *step_ptr;
+  __syncthreads();
+  if (b < B) {
+    const int tok = next[b];
+    if (step < max_new) tokens[(size_t)b * max_new + step] = tok;
+    input_ids[b] = tok;
+    const int pos = positions[b] + 1;
+    positions[b] = pos;
+    ctx_lens[b] = pos + 1;
+    slots[b] = block_tables[(size_t)b * max_blocks + pos / KV_BS] * KV_BS + pos % KV_BS;
+    int d = done[b];
+    for (int i = 0; i < n_stop; ++i) d |= (tok == stop_ids[i]);
+    done[b] = d;
+  }
+  if (b == 0) *step_ptr = step + 1;
+}
+
+inline int ew_grid(size_t total) {
+  size_t g = (total + 255) / 256;
+  return (int)(g > 4096 ? 4096 : (g == 0 ? 1 : g));
+}
+
+}  // namespace
+
+CFC_API int cfc_rope_kv_write(const void* qkv, const int32_t* positions, const int32_t* slots, const float* cos_sin,
+                              void* q_out, void* k_cache, void* v_cache, int T, int Hq, int Hkv, int head_dim,
+                              hipStream_t stream) {
+  if (head_dim % 16 != 0 || T < 0) return -1;
+  if (T == 0) return 0;
+  rope_kv_kernel<<<T, 256, 0, stream>>>((const uint16_t*)qkv, positions, slots, cos_sin, (uint16_t*)q_out,
+                                         (uint16_t*)k_cache, (uint16_t*)v_cache, Hq, Hkv, head_dim);
+  return CFC_CHECK_LAUNCH();
+}
+
+CFC_API int cfc_silu_mul(void* out, const void* gu, int T, int F, hipStream_t stream) {
+  if (F % 8 != 0) return -1;
+  if (T == 0) return 0;
+  silu_mul_kernel<<<ew_grid((size_t)T * F / 8), 256, 0, stream>>>((uint16_t*)out, (const uint16_t*)gu, T, F);
+  return CFC_CHECK_LAUNCH();
+}
+
+CFC_API int cfc_bias_gelu(void* out, const void* x, const void* bias, int T, int F, hipStream_t stream) {
+  if (F % 8 != 0) return -1;
+  if (T == 0) return 0;
+  bias_gelu_kernel<<<ew_grid((size_t)T * F / 8), 256, 0, stream>>>((uint16_t*)out, (const uint16_t*)x,
+                                                                   (const uint16_t*)bias, T, F);
+  return CFC_CHECK_LAUNCH();
+}
+
+CFC_API int cfc_embedding(void* out, const void* table, const int32_t* ids, int T, int dim, hipStream_t stream) {
+  if (dim % 8 != 0) return -1;
+  if (T == 0) return 0;
+  embedding_kernel<<<T, 256, 0, stream>>>((uint16_t*)out, (const uint16_t*)table, ids, T, dim);
+  return CFC_CHECK_LAUNCH();
+}
+
+CFC_API int cfc_sample(const void* logits, int B, int V, float temperature, uint32_t seed, const int32_t* step_ptr,
+                       int32_t* out_ids, hipStream_t stream) {
+  if (B == 0) return 0;
+  sample_kernel<<<B, 256, 0, stream>>>((const uint16_t*)logits, V, temperature, seed, step_ptr, out_ids);
+  return CFC_CHECK_LAUNCH();
+}
+
+CFC_API int cfc_decode_advance(const int32_t* next, int32_t* tokens, int max_new, int32_t* step_ptr, int32_t* input_ids,
+                               int32_t* positions, int32_t* ctx_lens, int32_t* slots, const int32_t* block_tables,
+                               int max_blocks, int32_t* done, const int32_t* stop_ids, int n_stop, int B,
+                               hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (B > 1024) return -1;  // single workgroup: the step counter bump must not race other blocks
+  decode_advance_kernel<<<1, ((B + 63) / 64) * 64, 0, stream>>>(next, tokens, max_new, step_ptr, input_ids, positions,
+                                                               ctx_lens, slots, block_tables, max_blocks, done,
+                                                               stop_ids, n_stop, B);
+  return CFC_CHECK_LAUNCH();
+}

@@ -1,0 +1,79 @@
+"""CPU path of the decoder/encoder (reference ops): engine plumbing, chunked prefill, stops."""
+import torch
+
+from copilot_for_consensus_amd.models.decoder import DecoderModel, DecoderWeights, get_config
+from copilot_for_consensus_amd.models.encoder import EncoderModel
+from copilot_for_consensus_amd.ops import reference as R
+from copilot_for_consensus_amd.runtime.engine import LLMEngine
+from copilot_for_consensus_amd.runtime.kv_cache import BlockPool, PagedKVCache
+
+
+def _engine(seed=0, prefill=4096):
+    cfg = get_config("tiny")
+    m = DecoderModel(DecoderWeights.random(cfg, "cpu", seed=seed))
+    kv = PagedKVCache(cfg.layers, 32, cfg.kv_heads, cfg.head_dim, "cpu")
+    return LLMEngine(m, kv, max_prefill_tokens=prefill)
+
+
+def test_generate_shapes_and_block_reuse():
+    eng = _engine()
+    free0 = eng.kv.pool.num_free()
+    res = eng.generate([[1, 2, 3, 4], [1] * 50], max_new_tokens=5, ignore_eos=True)
+    assert [len(t) for t in res.tokens] == [5, 5]
+    assert eng.kv.pool.num_free() == free0
+
+
+def test_chunked_prefill_equals_full_prefill():
+    prompts = [[1] + list(range(3, 120)), [1, 7, 7, 7]]
+    a = _engine(prefill=4096).generate(prompts, 4, ignore_eos=True).tokens
+    b = _engine(prefill=50).generate(prompts, 4, ignore_eos=True).tokens
+    assert a == b
+
+
+def test_incremental_decode_matches_full_recompute():
+    # token t+1 from decode == greedy from a fresh prefill of prompt + generated[:t]
+    eng = _engine(seed=2)
+    p = [1, 11, 12, 13, 14, 15]
+    gen = eng.generate([p], 4, ignore_eos=True).tokens[0]
+    for t in range(1, 4):
+        again = eng.generate([p + gen[:t]], 1, ignore_eos=True).tokens[0]
+        assert again[0] == gen[t]
+
+
+def test_stop_tokens_truncate():
+    eng = _engine(seed=1)
+    full = eng.generate([[1, 2, 3]], 6, ignore_eos=True).tokens[0]
+    stop = full[2]
+    cut = eng.generate([[1, 2, 3]], 6, stop_ids=(stop,)).tokens[0]
+    assert cut == full[:full.index(stop)]
+
+
+def test_blockpool():
+    bp = BlockPool(10)
+    a = bp.alloc(4)
+    b = bp.alloc(6)
+    assert sorted(a + b) == list(range(10)) and bp.num_free() == 0
+    try:
+        bp.alloc(1)
+        raise AssertionError("expected MemoryError")
+    except MemoryError:
+        pass
+    bp.free(a)
+    assert bp.num_free() == 4
+
+
+def test_encoder_cpu_pooling_normalized():
+    enc = EncoderModel.random("tiny", "cpu", seed=0)
+    e = enc.encode_ids([[1, 2, 3], [4, 5, 6, 7, 8]])
+    assert e.shape == (2, 64)
+    assert torch.allclose(e.norm(dim=1), torch.ones(2), atol=1e-3)
+
+
+def test_v_slot_perm_is_permutation():
+    p = R.v_slot_perm()
+    assert sorted(p.tolist()) == list(range(32))
+    # slot 8g+j holds key perm(g, j) = j<4 ? 4g+j : 16+4g+j-4
+    inv = {int(s): k for k, s in enumerate(p.tolist())}
+    for g in range(4):
+        for j in range(8):
+            assert inv[8 * g + j] == (4 * g + j if j < 4 else 16 + 4 * g + j - 4)

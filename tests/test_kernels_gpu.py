@@ -1,0 +1,202 @@
+"""Numerics of every HIP kernel vs the plain-PyTorch fp32 reference (ops/reference.py)."""
+import math
+
+import pytest
+import torch
+
+from copilot_for_consensus_amd.ops import kernels as K
+from copilot_for_consensus_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, atol, rtol=2e-2):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    assert torch.allclose(a, b, atol=atol, rtol=rtol), f"max abs err {err}"
+
+
+@pytest.fixture(autouse=True)
+def _native_loaded():
+    from copilot_for_consensus_amd.ops import _native
+    _native.kernels()  # must load: no silent fallback on a GPU box
+    torch.manual_seed(0)
+
+
+@pytest.mark.parametrize("dim", [384, 4096, 8192])
+def test_rmsnorm(dim):
+    x = torch.randn(37, dim, device=DEV).bfloat16()
+    r = torch.randn(37, dim, device=DEV).bfloat16()
+    w = (1 + 0.1 * torch.randn(dim, device=DEV)).bfloat16()
+    ref_o, ref_r = R.rmsnorm(x.cpu(), w.cpu(), 1e-5, r.cpu())
+    rr = r.clone()
+    o = K.rmsnorm(x, w, 1e-5, residual=rr)
+    _close(rr, ref_r, 1e-2)
+    _close(o, ref_o, 3e-2)
+    _close(K.rmsnorm(x, w, 1e-5), R.rmsnorm(x.cpu(), w.cpu(), 1e-5)[0], 3e-2)
+
+
+@pytest.mark.parametrize("dim", [384, 768])
+def test_layernorm_variants(dim):
+    x = torch.randn(50, dim, device=DEV).bfloat16()
+    res = torch.randn(50, dim, device=DEV).bfloat16()
+    b = torch.randn(dim, device=DEV).bfloat16()
+    g = (1 + 0.1 * torch.randn(dim, device=DEV)).bfloat16()
+    be = (0.1 * torch.randn(dim, device=DEV)).bfloat16()
+    _close(K.layernorm(x, g, be, 1e-12), R.layernorm(x.cpu(), g.cpu(), be.cpu(), 1e-12), 3e-2)
+    _close(K.layernorm(x, g, be, 1e-12, bias=b, residual=res),
+           R.layernorm(x.cpu(), g.cpu(), be.cpu(), 1e-12, b.cpu(), res.cpu()), 3e-2)
+    V = 1000
+    we, pe, te = (torch.randn(n, dim, device=DEV).bfloat16() for n in (V, 512, 2))
+    ids = torch.randint(0, V, (50,), device=DEV, dtype=torch.int32)
+    pos = torch.randint(0, 512, (50,), device=DEV, dtype=torch.int32)
+    _close(K.embed_layernorm(ids, pos, we, pe, te, g, be, 1e-12),
+           R.embed_layernorm(ids.cpu(), pos.cpu(), we.cpu(), pe.cpu(), te.cpu(), g.cpu(), be.cpu(), 1e-12), 3e-2)
+
+
+def _kv_setup(Hkv, D, nblk):
+    kc = torch.zeros(nblk, Hkv, R.KV_BLOCK, D, device=DEV).bfloat16()
+    vc = torch.zeros(nblk, Hkv, D, R.KV_BLOCK, device=DEV).bfloat16()
+    return kc, vc
+
+
+def test_rope_kv_write():
+    Hq, Hkv, D, T = 8, 2, 128, 45
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV).bfloat16()
+    pos = torch.randint(0, 3000, (T,), device=DEV, dtype=torch.int32)
+    slots = torch.randperm(20 * 32, device=DEV)[:T].to(torch.int32)
+    cs = R.rope_cos_sin(4096, D, 1e6, device=DEV)
+    kc, vc = _kv_setup(Hkv, D, 20)
+    kc2, vc2 = kc.cpu().clone(), vc.cpu().clone()
+    q = K.rope_kv_write(qkv, pos, slots, cs, kc, vc, Hq, Hkv, D)
+    qr = R.rope_kv_write(qkv.cpu(), pos.cpu(), slots.cpu(), cs.cpu(), kc2, vc2, Hq, Hkv, D)
+    _close(q, qr, 2e-2)
+    _close(kc, kc2, 2e-2)
+    _close(vc, vc2, 1e-6, 0)
+
+
+def _fill_cache(ctx_lens, Hkv, D, extra_blocks=3):
+    """Random K/V for every sequence, written through the reference writer; returns tables."""
+    tables, nblk = [], 0
+    for n in ctx_lens:
+        nb = math.ceil(n / 32)
+        tables.append(list(range(nblk, nblk + nb)))
+        nblk += nb
+    nblk += extra_blocks
+    perm = torch.randperm(nblk).tolist()  # scatter blocks around the pool
+    tables = [[perm[b] for b in t] for t in tables]
+    kc = (torch.randn(nblk, Hkv, 32, D)).bfloat16()
+    vc = (torch.randn(nblk, Hkv, D, 32)).bfloat16()
+    maxb = max(len(t) for t in tables) + 2
+    bt = torch.full((len(tables), maxb), 0, dtype=torch.int32)
+    for i, t in enumerate(tables):
+        bt[i, :len(t)] = torch.tensor(t, dtype=torch.int32)
+    return kc, vc, bt
+
+
+@pytest.mark.parametrize("G", [1, 4, 8])
+@pytest.mark.parametrize("part_blocks", [4, 1000])
+def test_paged_decode(G, part_blocks):
+    Hkv, D = 2, 128
+    Hq = Hkv * G
+    ctx = [1, 31, 32, 33, 100, 517, 2049, 64]
+    kc, vc, bt = _fill_cache(ctx, Hkv, D)
+    q = torch.randn(len(ctx), Hq, D).bfloat16()
+    cl = torch.tensor(ctx, dtype=torch.int32)
+    ref = R.paged_decode_attention(q, kc, vc, bt, cl, 1 / math.sqrt(D))
+    out = K.paged_decode_attention(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), cl.to(DEV), 1 / math.sqrt(D),
+                                   part_blocks=part_blocks)
+    _close(out, ref, 2e-2)
+
+
+@pytest.mark.parametrize("G", [1, 4])
+def test_prefill_attention(G):
+    Hkv, D = 2, 128
+    Hq = Hkv * G
+    # (q_len, ctx_len): fresh prompts and chunked continuation (ctx > q_len)
+    seqs = [(1, 1), (17, 17), (64, 64), (200, 200), (70, 300), (129, 1000)]
+    kc, vc, bt = _fill_cache([c for _, c in seqs], Hkv, D)
+    cu = [0]
+    for qn, _ in seqs:
+        cu.append(cu[-1] + qn)
+    q = torch.randn(cu[-1], Hq, D).bfloat16()
+    cu_t = torch.tensor(cu, dtype=torch.int32)
+    cl = torch.tensor([c for _, c in seqs], dtype=torch.int32)
+    ref = R.prefill_attention(q, kc, vc, bt, cu_t, cl, 1 / math.sqrt(D))
+    out = K.prefill_attention(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), cu_t.to(DEV), cl.to(DEV),
+                              1 / math.sqrt(D))
+    _close(out, ref, 2e-2)
+
+
+@pytest.mark.parametrize("D", [32, 64])
+def test_encoder_attention(D):
+    H = 4
+    lens = [1, 5, 31, 64, 130, 256]
+    cu = [0]
+    for n in lens:
+        cu.append(cu[-1] + n)
+    qkv = torch.randn(cu[-1], 3 * H * D).bfloat16()
+    cu_t = torch.tensor(cu, dtype=torch.int32)
+    ref = R.encoder_attention(qkv, cu_t, H, D, 1 / math.sqrt(D))
+    out = K.encoder_attention(qkv.to(DEV), cu_t.to(DEV), H, D, 1 / math.sqrt(D), max(lens))
+    _close(out, ref, 2e-2)
+
+
+def test_silu_mul_and_gelu():
+    gu = torch.randn(33, 2 * 1536, device=DEV).bfloat16()
+    _close(K.silu_mul(gu), R.silu_mul(gu.cpu()), 2e-2)
+    x = torch.randn(33, 1536, device=DEV).bfloat16()
+    b = torch.randn(1536, device=DEV).bfloat16()
+    _close(K.bias_gelu(x, b), R.bias_gelu(x.cpu(), b.cpu()), 2e-2)
+
+
+def test_embedding_and_greedy_sample():
+    table = torch.randn(1000, 256, device=DEV).bfloat16()
+    ids = torch.randint(0, 1000, (17,), device=DEV, dtype=torch.int32)
+    _close(K.embedding(table, ids), table.cpu()[ids.cpu().long()], 0, 0)
+    logits = torch.randn(9, 32000, device=DEV).bfloat16()
+    out = torch.empty(9, dtype=torch.int32, device=DEV)
+    K.sample(logits, out)
+    assert out.cpu().tolist() == R.sample_greedy(logits.cpu()).tolist()
+
+
+def test_gumbel_sampling_distribution():
+    # 4-way categorical at T=1: empirical frequencies match softmax
+    probs = torch.tensor([0.1, 0.2, 0.3, 0.4])
+    logits = probs.log().repeat(4096, 1).bfloat16().to(DEV)
+    out = torch.empty(4096, dtype=torch.int32, device=DEV)
+    step = torch.tensor([3], dtype=torch.int32, device=DEV)
+    K.sample(logits, out, temperature=1.0, seed=11, step=step)
+    freq = torch.bincount(out.cpu().long(), minlength=4).float() / 4096
+    assert (freq - probs).abs().max() < 0.03, freq
+
+
+def test_knn_scores_and_topk():
+    N, dim = 50_000, 384
+    X = torch.randn(N, dim, device=DEV).bfloat16()
+    Xn = K.l2_normalize(X)
+    _close(Xn[:100], R.l2_normalize(X[:100].cpu())[0], 1e-2)
+    Q = K.l2_normalize(torch.randn(5, dim, device=DEV).bfloat16())
+    s = K.knn_scores(Xn, Q)
+    _close(s[:, :2000], R.knn_scores(Xn[:2000].cpu(), Q.cpu()), 1e-2)
+    v, i = K.topk(s, 150)
+    rv, ri = torch.topk(s, 150, dim=1)
+    _close(v, rv, 1e-6, 0)
+    # ids may differ only among exact ties
+    assert (s.gather(1, i.to(DEV)) == v.to(DEV)).all()
+    # squared-L2 mode
+    n2 = torch.empty(N, device=DEV)
+    K.l2_normalize(X, norms2=n2)
+    qn2 = Q.float().pow(2).sum(1)
+    s2 = K.knn_scores(X, Q, n2, qn2)
+    _close(s2[:, :1000], R.knn_scores(X[:1000].cpu(), Q.cpu(), n2[:1000].cpu(), qn2.cpu()), 0.5, 1e-2)
+
+
+def test_pool():
+    lens = [3, 1, 40]
+    cu = torch.tensor([0, 3, 4, 44], dtype=torch.int32)
+    h = torch.randn(44, 384).bfloat16()
+    for mode in ("mean", "cls"):
+        _close(K.pool(h.to(DEV), cu.to(DEV), mode, True), R.pool(h, cu, mode, True), 1e-3)
+    del lens
