@@ -65,10 +65,10 @@ def get_encoder_config(name) -> EncoderConfig:
 
 class EncoderModel:
     def __init__(self, cfg: EncoderConfig, device, dtype=torch.bfloat16):
-        self.cfg, self.device, self.dtype = cfg, torch.device(device), dtype
+        self.cfg, self.device, self.dtype = get_encoder_config(cfg), torch.device(device), dtype
         self.p: dict[str, torch.Tensor] = {}
         self.layers: list[dict[str, torch.Tensor]] = []
-        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self.scale = 1.0 / math.sqrt(self.cfg.head_dim)
 
     @classmethod
     def random(cls, cfg, device, seed: int = 0, std: float = 0.02):

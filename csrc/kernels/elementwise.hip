@@ -137,26 +137,27 @@ __global__ void __launch_bounds__(256) sample_kernel(const uint16_t* __restrict_
   const uint32_t step = step_ptr ? (uint32_t)*step_ptr : 0u;
   float best = -INFINITY;
   int best_i = 0x7fffffff;
-  const int nvec = V / 8;
+  const int nvec = (V % 8 == 0) ? V / 8 : 0;  // 16-byte row alignment needed for vector loads
   const bool sample = temperature > 0.f;
   const float inv_t = sample ? 1.f / temperature : 1.f;
+  auto score = [&](float x, int idx) -> float {
+    if (!sample) return x;
+    const uint32_t h = hash_u32(seed ^ hash_u32(step * 0x9E3779B9u ^ hash_u32(row * 0x85EBCA6Bu ^ (uint32_t)idx)));
+    const float u = ((h >> 8) + 0.5f) * (1.f / 16777216.f);
+    return x * inv_t - __logf(-__logf(u));
+  };
   for (int c = threadIdx.x; c < nvec; c += blockDim.x) {
     float v[8];
     unpack8(reinterpret_cast<const uint4*>(lr)[c], v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float x = v[j];
       const int idx = c * 8 + j;
-      if (sample) {
-        const uint32_t h = hash_u32(seed ^ hash_u32(step * 0x9E3779B9u ^ hash_u32(row * 0x85EBCA6Bu ^ (uint32_t)idx)));
-        const float u = ((h >> 8) + 0.5f) * (1.f / 16777216.f);
-        x = x * inv_t - __logf(-__logf(u));
-      }
+      const float x = score(v[j], idx);
       if (x > best || (x == best && idx < best_i)) { best = x; best_i = idx; }
     }
   }
   for (int idx = nvec * 8 + threadIdx.x; idx < V; idx += blockDim.x) {  // tail (V % 8)
-    float x = bf2f(lr[idx]);
+    const float x = score(bf2f(lr[idx]), idx);
     if (x > best || (x == best && idx < best_i)) { best = x; best_i = idx; }
   }
   __shared__ float sb[4];
