@@ -169,7 +169,7 @@ class EncoderModel:
                 cu.append(cu[-1] + len(s))
             dev = self.device
             cu_t = torch.tensor(cu, dtype=torch.int32, device=dev)
-            seq_t, q0_t = K.prefill_tiles(cu)
+            seq_t, q0_t = K.prefill_tiles(cu, K.ENCODER_TILE_ROWS)
             tiles = (torch.tensor(seq_t, dtype=torch.int32, device=dev), torch.tensor(q0_t, dtype=torch.int32, device=dev))
             h = self.forward_packed(torch.tensor(ids, dtype=torch.int32, device=dev),
                                     torch.tensor(pos, dtype=torch.int32, device=dev), cu_t,

@@ -136,14 +136,23 @@ def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, o
     return out
 
 
-def prefill_tiles(cu_q: list[int], tile: int = 64):
-    seqs, q0 = [], []
+PREFILL_TILE_ROWS = 128   # query rows per workgroup of the decoder prefill kernel
+ENCODER_TILE_ROWS = 64    # query rows per workgroup of the encoder attention kernel
+
+
+def prefill_tiles(cu_q: list[int], tile: int = PREFILL_TILE_ROWS, ctx_lens: list[int] | None = None):
+    """(tile_seq, tile_q0) lists.  With ``ctx_lens`` the tiles are ordered heaviest-first (most
+    keys to visit under the causal mask) so the long diagonal tiles start first and the grid
+    drains evenly."""
+    tiles = []
     for s in range(len(cu_q) - 1):
         n = cu_q[s + 1] - cu_q[s]
+        base = (ctx_lens[s] - n) if ctx_lens is not None else 0
         for r in range(0, n, tile):
-            seqs.append(s)
-            q0.append(r)
-    return seqs, q0
+            tiles.append((base + min(r + tile, n), s, r))
+    if ctx_lens is not None:
+        tiles.sort(key=lambda x: -x[0])
+    return [t[1] for t in tiles], [t[2] for t in tiles]
 
 
 def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, tiles=None, out=None):
@@ -153,7 +162,7 @@ def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, 
     T, Hq, D = q.shape
     Hkv = k_cache.shape[1]
     if tiles is None:
-        seqs, q0 = prefill_tiles(cu_q.tolist())
+        seqs, q0 = prefill_tiles(cu_q.tolist(), PREFILL_TILE_ROWS, ctx_lens.tolist())
         tiles = (torch.tensor(seqs, dtype=torch.int32, device=q.device),
                  torch.tensor(q0, dtype=torch.int32, device=q.device))
     tile_seq, tile_q0 = tiles
@@ -171,7 +180,7 @@ def encoder_attention(qkv, cu_seqlens, H, D, scale, max_seqlen, tiles=None, out=
         return ref.encoder_attention(qkv, cu_seqlens, H, D, scale)
     T = qkv.shape[0]
     if tiles is None:
-        seqs, q0 = prefill_tiles(cu_seqlens.tolist())
+        seqs, q0 = prefill_tiles(cu_seqlens.tolist(), ENCODER_TILE_ROWS)
         tiles = (torch.tensor(seqs, dtype=torch.int32, device=qkv.device),
                  torch.tensor(q0, dtype=torch.int32, device=qkv.device))
     out = torch.empty(T, H, D, dtype=qkv.dtype, device=qkv.device) if out is None else out

@@ -73,6 +73,9 @@ class LLMEngine:
         self.use_graph = use_graph and kv.device.type == "cuda"
         self.stop_check_interval = stop_check_interval
         self._states: dict[tuple, _DecodeState] = {}
+        if self.device.type == "cuda":
+            from .gemm_tuning import enable_tuned_gemms
+            self.tuned_gemms = enable_tuned_gemms()
 
     # ------------------------------------------------------------------ helpers
     def _part_blocks(self, B, max_blocks):
@@ -119,7 +122,7 @@ class LLMEngine:
             bt = torch.zeros(len(rows), maxb, dtype=torch.int32)
             for r, s in enumerate(rows):
                 bt[r, :len(tables[s])] = torch.tensor(tables[s], dtype=torch.int32)
-            tseq, tq0 = K.prefill_tiles(cu)
+            tseq, tq0 = K.prefill_tiles(cu, K.PREFILL_TILE_ROWS, ctx)
             hidden = self.model.forward_prefill(
                 self._i32(ids), self._i32(positions), self._i32(slots), self._i32(cu), self._i32(ctx),
                 bt.to(self.device), self.kv, tiles=(self._i32(tseq), self._i32(tq0)),

@@ -1,0 +1,444 @@
+"""Document storage: interface, in-memory store with indexes + Mongo operators, validating
+decorator, MongoDB driver (optional, needs pymongo) and factory.
+
+Interface = adapters/copilot_storage/copilot_storage/document_store.py:40-138 of the reference
+(insert_document / get_document / query_documents(filter, limit, sort_by, sort_order) /
+update_document / delete_document / aggregate_documents) plus batched ``insert_many`` /
+``update_many`` so the pipeline's per-document hot loops become one call.
+"""
+from __future__ import annotations
+
+import copy
+import threading
+import uuid
+from abc import ABC, abstractmethod
+from collections import defaultdict
+from typing import Any
+
+from .query import apply_update, get_path, matches, simple_equality_keys
+
+SYSTEM_FIELDS = ("_rid", "_self", "_etag", "_attachments", "_ts")
+
+
+class DocumentStoreError(Exception):
+    pass
+
+
+class DocumentStoreNotConnectedError(DocumentStoreError):
+    pass
+
+
+class DocumentStoreConnectionError(DocumentStoreError):
+    pass
+
+
+class DocumentNotFoundError(DocumentStoreError):
+    pass
+
+
+class DocumentAlreadyExistsError(DocumentStoreError):
+    pass
+
+
+def sanitize_document(doc: dict) -> dict:
+    for f in SYSTEM_FIELDS:
+        doc.pop(f, None)
+    return doc
+
+
+class DocumentStore(ABC):
+    def connect(self) -> None:
+        pass
+
+    def disconnect(self) -> None:
+        pass
+
+    @abstractmethod
+    def insert_document(self, collection: str, doc: dict[str, Any]) -> str: ...
+
+    @abstractmethod
+    def get_document(self, collection: str, doc_id: str) -> dict[str, Any] | None: ...
+
+    @abstractmethod
+    def query_documents(self, collection: str, filter_dict: dict[str, Any], limit: int = 100,
+                        sort_by: str | None = None, sort_order: str = "desc", skip: int = 0) -> list[dict]: ...
+
+    @abstractmethod
+    def update_document(self, collection: str, doc_id: str, patch: dict[str, Any]) -> None: ...
+
+    @abstractmethod
+    def delete_document(self, collection: str, doc_id: str) -> None: ...
+
+    # ---- batched helpers (default: loop) ----
+    def insert_many(self, collection: str, docs: list[dict], ignore_duplicates: bool = True) -> list[str]:
+        ids = []
+        for d in docs:
+            try:
+                ids.append(self.insert_document(collection, d))
+            except DocumentAlreadyExistsError:
+                if not ignore_duplicates:
+                    raise
+        return ids
+
+    def update_many(self, collection: str, filter_dict: dict, patch: dict) -> int:
+        n = 0
+        for d in self.query_documents(collection, filter_dict, limit=1 << 62):
+            self.update_document(collection, d["_id"], patch)
+            n += 1
+        return n
+
+    def delete_many(self, collection: str, filter_dict: dict) -> int:
+        n = 0
+        for d in self.query_documents(collection, filter_dict, limit=1 << 62):
+            self.delete_document(collection, d["_id"])
+            n += 1
+        return n
+
+    def count_documents(self, collection: str, filter_dict: dict | None = None) -> int:
+        return len(self.query_documents(collection, filter_dict or {}, limit=1 << 62))
+
+    def aggregate_documents(self, collection: str, pipeline: list[dict]) -> list[dict]:
+        raise NotImplementedError
+
+
+# Fields indexed in every collection (hash index: value -> set(ids)); mirrors the reference's
+# collections.config.json indexes that the pipeline actually filters on.
+DEFAULT_INDEXES = {
+    "messages": ("archive_id", "thread_id", "message_id"),
+    "chunks": ("thread_id", "message_doc_id", "embedding_generated", "archive_id"),
+    "threads": ("archive_id", "summary_id"),
+    "archives": ("source", "status", "file_hash"),
+    "summaries": ("thread_id",),
+    "sources": ("name",),
+}
+
+
+def _hashable(v):
+    if isinstance(v, list):
+        return None
+    try:
+        hash(v)
+        return v
+    except TypeError:
+        return None
+
+
+class InMemoryDocumentStore(DocumentStore):
+    """Thread-safe in-memory store with hash indexes and Mongo query operators."""
+
+    def __init__(self, indexes: dict[str, tuple[str, ...]] | None = None, **_):
+        self._lock = threading.RLock()
+        self.collections: dict[str, dict[str, dict]] = defaultdict(dict)
+        self._index_fields = dict(DEFAULT_INDEXES if indexes is None else indexes)
+        self._idx: dict[tuple[str, str], dict[Any, set]] = defaultdict(lambda: defaultdict(set))
+        self.connected = False
+
+    @classmethod
+    def from_config(cls, _cfg=None):
+        return cls()
+
+    def connect(self) -> None:
+        self.connected = True
+
+    def disconnect(self) -> None:
+        self.connected = False
+
+    # ---------------------------------------------------------------- index maintenance
+    def _index_add(self, coll, doc):
+        for f in self._index_fields.get(coll, ()):
+            v = _hashable(doc.get(f))
+            if f in doc and (v is not None or doc.get(f) is None):
+                self._idx[(coll, f)][v].add(doc["_id"])
+
+    def _index_remove(self, coll, doc):
+        for f in self._index_fields.get(coll, ()):
+            v = _hashable(doc.get(f))
+            if f in doc:
+                self._idx[(coll, f)][v].discard(doc["_id"])
+
+    def _candidates(self, coll, flt):
+        best = None
+        for f, (kind, val) in simple_equality_keys(flt).items():
+            if f == "_id":
+                ids = set(val) if kind == "in" else {val}
+            elif f in self._index_fields.get(coll, ()):
+                idx = self._idx[(coll, f)]
+                if kind == "in":
+                    ids = set()
+                    for v in val:
+                        hv = _hashable(v)
+                        ids |= idx.get(hv, set())
+                else:
+                    ids = set(idx.get(_hashable(val), set()))
+            else:
+                continue
+            if best is None or len(ids) < len(best):
+                best = ids
+        return best
+
+    # ---------------------------------------------------------------- API
+    def insert_document(self, collection: str, doc: dict[str, Any]) -> str:
+        with self._lock:
+            doc_id = doc.get("_id") or str(uuid.uuid4())
+            coll = self.collections[collection]
+            if doc_id in coll:
+                raise DocumentAlreadyExistsError(f"Document with id {doc_id} already exists in {collection}")
+            d = copy.deepcopy(doc)
+            d["_id"] = doc_id
+            coll[doc_id] = d
+            self._index_add(collection, d)
+            return doc_id
+
+    def get_document(self, collection: str, doc_id: str) -> dict[str, Any] | None:
+        with self._lock:
+            d = self.collections[collection].get(doc_id)
+            return sanitize_document(copy.deepcopy(d)) if d is not None else None
+
+    def _select(self, collection, filter_dict):
+        coll = self.collections[collection]
+        cand = self._candidates(collection, filter_dict)
+        it = (coll[i] for i in cand if i in coll) if cand is not None else coll.values()
+        return [d for d in it if matches(d, filter_dict)]
+
+    def query_documents(self, collection: str, filter_dict: dict[str, Any] | None = None, limit: int = 100,
+                        sort_by: str | None = None, sort_order: str = "desc", skip: int = 0) -> list[dict]:
+        if sort_order not in ("asc", "desc"):
+            raise DocumentStoreError(f"Invalid sort_order {sort_order!r}")
+        with self._lock:
+            res = self._select(collection, filter_dict or {})
+            if sort_by:
+                # None sorts first in asc / last in desc (Cosmos/Mongo behaviour)
+                def key(d):
+                    v = get_path(d, sort_by)
+                    return (0, "") if v is None or v is get_path({}, "x") else (1, v if isinstance(v, (int, float)) else str(v))
+                try:
+                    res.sort(key=key, reverse=sort_order == "desc")
+                except TypeError:
+                    res.sort(key=lambda d: str(get_path(d, sort_by)), reverse=sort_order == "desc")
+            res = res[skip:skip + limit] if limit is not None else res[skip:]
+            return [sanitize_document(copy.deepcopy(d)) for d in res]
+
+    def count_documents(self, collection: str, filter_dict: dict | None = None) -> int:
+        with self._lock:
+            return len(self._select(collection, filter_dict or {}))
+
+    def update_document(self, collection: str, doc_id: str, patch: dict[str, Any]) -> None:
+        with self._lock:
+            d = self.collections[collection].get(doc_id)
+            if d is None:
+                raise DocumentNotFoundError(f"Document {doc_id} not found in collection {collection}")
+            self._index_remove(collection, d)
+            apply_update(d, copy.deepcopy(patch))
+            d["_id"] = doc_id
+            self._index_add(collection, d)
+
+    def update_many(self, collection: str, filter_dict: dict, patch: dict) -> int:
+        with self._lock:
+            docs = self._select(collection, filter_dict)
+            for d in docs:
+                self._index_remove(collection, d)
+                apply_update(d, copy.deepcopy(patch))
+                self._index_add(collection, d)
+            return len(docs)
+
+    def delete_document(self, collection: str, doc_id: str) -> None:
+        with self._lock:
+            d = self.collections[collection].pop(doc_id, None)
+            if d is None:
+                raise DocumentNotFoundError(f"Document {doc_id} not found in collection {collection}")
+            self._index_remove(collection, d)
+
+    def delete_many(self, collection: str, filter_dict: dict) -> int:
+        with self._lock:
+            docs = self._select(collection, filter_dict)
+            for d in docs:
+                self.collections[collection].pop(d["_id"], None)
+                self._index_remove(collection, d)
+            return len(docs)
+
+    def clear_collection(self, collection: str) -> None:
+        with self._lock:
+            self.collections[collection].clear()
+            for k in [k for k in self._idx if k[0] == collection]:
+                del self._idx[k]
+
+    def clear_all(self) -> None:
+        with self._lock:
+            self.collections.clear()
+            self._idx.clear()
+
+    def aggregate_documents(self, collection: str, pipeline: list[dict]) -> list[dict]:
+        """$match / $lookup / $project / $sort / $limit / $skip / $count / $group(count|sum)."""
+        with self._lock:
+            docs = [copy.deepcopy(d) for d in self.collections[collection].values()]
+            for stage in pipeline:
+                (op, spec), = stage.items()
+                if op == "$match":
+                    docs = [d for d in docs if matches(d, spec)]
+                elif op == "$lookup":
+                    other = self.collections[spec["from"]].values()
+                    for d in docs:
+                        lv = get_path(d, spec["localField"])
+                        d[spec["as"]] = [copy.deepcopy(o) for o in other
+                                         if (get_path(o, spec["foreignField"]) == lv) or
+                                         (isinstance(lv, list) and get_path(o, spec["foreignField"]) in lv)]
+                elif op == "$project":
+                    inc = {k for k, v in spec.items() if v}
+                    docs = [{k: d[k] for k in d if k in inc or (k == "_id" and spec.get("_id", 1))} for d in docs]
+                elif op == "$sort":
+                    for k, direction in reversed(list(spec.items())):
+                        docs.sort(key=lambda d: (get_path(d, k) is None, str(get_path(d, k))), reverse=direction < 0)
+                elif op == "$limit":
+                    docs = docs[:spec]
+                elif op == "$skip":
+                    docs = docs[spec:]
+                elif op == "$count":
+                    docs = [{spec: len(docs)}]
+                elif op == "$group":
+                    key = spec["_id"]
+                    groups: dict = {}
+                    for d in docs:
+                        gk = get_path(d, key[1:]) if isinstance(key, str) and key.startswith("$") else key
+                        g = groups.setdefault(_hashable(gk), {"_id": gk})
+                        for name, acc in spec.items():
+                            if name == "_id":
+                                continue
+                            (aop, aarg), = acc.items()
+                            if aop == "$sum":
+                                inc = aarg if isinstance(aarg, (int, float)) else (get_path(d, aarg[1:]) or 0)
+                                g[name] = g.get(name, 0) + inc
+                            elif aop == "$max":
+                                v = get_path(d, aarg[1:])
+                                g[name] = v if name not in g else max(g[name], v)
+                            elif aop == "$min":
+                                v = get_path(d, aarg[1:])
+                                g[name] = v if name not in g else min(g[name], v)
+                    docs = list(groups.values())
+                else:
+                    raise DocumentStoreError(f"unsupported aggregation stage {op}")
+            return [sanitize_document(d) for d in docs]
+
+
+class ValidatingDocumentStore(DocumentStore):
+    """Validates inserted documents against the collection schema (reference
+    validating_document_store.py:35); strict mode raises, lenient mode records errors."""
+
+    def __init__(self, store: DocumentStore, schema_provider=None, strict: bool = True):
+        from ..contracts.registry import default_provider
+        self._inner = store
+        self._schemas = schema_provider or default_provider()
+        self.strict = strict
+        self.validation_errors: list[tuple[str, list[str]]] = []
+
+    def _check(self, collection, doc):
+        errs = self._schemas.validate_document(collection, doc)
+        if errs:
+            self.validation_errors.append((collection, errs))
+            if self.strict:
+                raise DocumentStoreError(f"{collection} document failed validation: {'; '.join(errs[:5])}")
+
+    def insert_document(self, collection, doc):
+        self._check(collection, doc)
+        return self._inner.insert_document(collection, doc)
+
+    def insert_many(self, collection, docs, ignore_duplicates=True):
+        for d in docs:
+            self._check(collection, d)
+        return self._inner.insert_many(collection, docs, ignore_duplicates)
+
+    def get_document(self, collection, doc_id):
+        return self._inner.get_document(collection, doc_id)
+
+    def query_documents(self, collection, filter_dict=None, limit=100, sort_by=None, sort_order="desc", skip=0):
+        return self._inner.query_documents(collection, filter_dict or {}, limit, sort_by, sort_order, skip)
+
+    def update_document(self, collection, doc_id, patch):
+        return self._inner.update_document(collection, doc_id, patch)
+
+    def update_many(self, collection, filter_dict, patch):
+        return self._inner.update_many(collection, filter_dict, patch)
+
+    def delete_document(self, collection, doc_id):
+        return self._inner.delete_document(collection, doc_id)
+
+    def delete_many(self, collection, filter_dict):
+        return self._inner.delete_many(collection, filter_dict)
+
+    def count_documents(self, collection, filter_dict=None):
+        return self._inner.count_documents(collection, filter_dict)
+
+    def aggregate_documents(self, collection, pipeline):
+        return self._inner.aggregate_documents(collection, pipeline)
+
+    def connect(self):
+        self._inner.connect()
+
+    def disconnect(self):
+        self._inner.disconnect()
+
+    def __getattr__(self, name):
+        return getattr(self._inner, name)
+
+
+class MongoDocumentStore(DocumentStore):
+    """MongoDB driver (reference mongo_document_store.py:33); needs ``pymongo``."""
+
+    def __init__(self, host="documentdb", port=27017, database="copilot", username=None, password=None, **_):
+        try:
+            import pymongo  # type: ignore
+        except ImportError as e:  # pragma: no cover
+            raise ImportError("DOCUMENT_STORE_TYPE=mongodb needs 'pymongo'; use 'inmemory'") from e
+        self._pymongo = pymongo
+        self._args = dict(host=host, port=int(port), username=username, password=password)
+        self._dbname = database
+        self.db = None
+
+    def connect(self):
+        self.client = self._pymongo.MongoClient(**{k: v for k, v in self._args.items() if v is not None})
+        self.db = self.client[self._dbname]
+
+    def _c(self, collection):
+        if self.db is None:
+            raise DocumentStoreNotConnectedError("call connect() first")
+        return self.db[collection]
+
+    def insert_document(self, collection, doc):
+        try:
+            return str(self._c(collection).insert_one(dict(doc)).inserted_id)
+        except self._pymongo.errors.DuplicateKeyError as e:
+            raise DocumentAlreadyExistsError(str(e)) from e
+
+    def get_document(self, collection, doc_id):
+        return self._c(collection).find_one({"_id": doc_id})
+
+    def query_documents(self, collection, filter_dict=None, limit=100, sort_by=None, sort_order="desc", skip=0):
+        cur = self._c(collection).find(filter_dict or {})
+        if sort_by:
+            cur = cur.sort(sort_by, -1 if sort_order == "desc" else 1)
+        return list(cur.skip(skip).limit(limit))
+
+    def update_document(self, collection, doc_id, patch):
+        upd = patch if any(k.startswith("$") for k in patch) else {"$set": patch}
+        if self._c(collection).update_one({"_id": doc_id}, upd).matched_count == 0:
+            raise DocumentNotFoundError(doc_id)
+
+    def delete_document(self, collection, doc_id):
+        if self._c(collection).delete_one({"_id": doc_id}).deleted_count == 0:
+            raise DocumentNotFoundError(doc_id)
+
+    def aggregate_documents(self, collection, pipeline):
+        return list(self._c(collection).aggregate(pipeline))
+
+
+def create_document_store(cfg=None, enable_validation: bool = False, strict: bool = True) -> DocumentStore:
+    name = getattr(cfg, "driver_name", cfg) or "inmemory"
+    kw = dict(getattr(cfg, "driver_config", {}) or {})
+    if name == "inmemory":
+        store: DocumentStore = InMemoryDocumentStore()
+    elif name == "mongodb":
+        store = MongoDocumentStore(**kw)
+    elif name == "azure_cosmosdb":
+        raise ImportError("azure_cosmosdb driver needs azure-cosmos (not in this image)")
+    else:
+        raise ValueError(f"unknown document_store driver {name!r}")
+    return ValidatingDocumentStore(store, strict=strict) if enable_validation else store

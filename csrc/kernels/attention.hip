@@ -22,6 +22,7 @@
 //   * LDS tiles are XOR-swizzled for conflict-free ds_read_b128 (guide §5.5 T2); the swizzles
 //     were derived against the gfx950 ds_read_b128 lane groups {0-3,12-15,20-27}, ...
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -212,27 +213,39 @@ __global__ void __launch_bounds__(128) decode_combine_kernel(const float* __rest
 
 // ------------------------------------------------------------------------------------------
 // Varlen causal prefill over the paged cache (D = 128).
-// grid = (n_tiles, Hq); block = 256 = 4 waves x 16 query rows = 64-row query tile.
-// Tile t covers query rows [tile_q0[t], +64) of sequence tile_seq[t]; those rows sit at
+// grid = (n_tiles, Hq); block = 512 = 8 waves x 16 query rows = 128-row query tile.
+// Tile t covers query rows [tile_q0[t], +128) of sequence tile_seq[t]; those rows sit at
 // positions ctx - q_len + row (chunked prefill / prefix reuse: keys come from the cache).
-// K tile (64 keys x 128) and V^T tile (2 blocks x 128 x 32) are double-buffered in LDS,
-// register-staged: next tile's global loads issue before this tile's MFMAs, LDS writes after
-// (guide §5.5 T14), one barrier per tile.
+//   * K tile (64 keys x 128) and V^T tile (2 blocks x 128 x 32) double-buffered in LDS and shared
+//     by all 8 waves; register-staged (next tile's loads issue before this tile's MFMAs, LDS
+//     writes after -- guide §5.5 T14); one barrier per tile.
+//   * <= 128 VGPRs so two workgroups (16 waves, 4 per SIMD) share a CU: one wave's softmax VALU
+//     overlaps another's MFMAs (a 1-wave-per-SIMD build of this loop was VALU-serialised).
+//   * VALU trimmed: Q is pre-scaled by softmax_scale*log2(e) once (scores come out of the MFMA
+//     in the exp2 domain), the causal mask is applied only on tiles that cross the diagonal, and
+//     the O rescale is deferred until the running max grows by > RESCALE_THR (guide T13; P is
+//     then bounded by 2^THR, exact after the final 1/l).
+//   * The host orders tiles heaviest-first (most keys) so the causal triangle drains evenly.
 // ------------------------------------------------------------------------------------------
-constexpr int PF_KT = 64;  // keys per tile
+constexpr int PF_KT = 64;     // keys per tile
+constexpr int PF_WAVES = 8;
+constexpr int PF_ROWS = 16 * PF_WAVES;
+constexpr float RESCALE_THR = 8.0f;
 
 __device__ __forceinline__ int k_lds_off(int row, int ch) { return row * 256 + ((ch ^ (row & 15)) << 4); }
 __device__ __forceinline__ int v_lds_off(int blk, int d, int ch) {
   return blk * 128 * 64 + d * 64 + ((ch ^ (((d >> 3) & 1) << 1)) << 4);
 }
 
-__global__ void __launch_bounds__(256) prefill_paged_kernel(
+template <int MINW>
+__global__ void __launch_bounds__(512, MINW) prefill_paged_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, const int32_t* __restrict__ cu_q, const int32_t* __restrict__ ctx_lens,
     const int32_t* __restrict__ tile_seq, const int32_t* __restrict__ tile_q0, float scale_log2, int Hq, int Hkv,
     int max_blocks, uint16_t* __restrict__ out) {
   constexpr int D = 128;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // LDS: [K buf0 16K][K buf1 16K][V buf0 16K][V buf1 16K]
   const int t = blockIdx.x, hq = blockIdx.y;
   const int G = Hq / Hkv, hk = hq / G;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
@@ -241,29 +254,33 @@ __global__ void __launch_bounds__(256) prefill_paged_kernel(
   const int q_begin = cu_q[s], q_len = cu_q[s + 1] - q_begin;
   const int ctx = ctx_lens[s];
   const int pos_base = ctx - q_len;
-  const int row_last = min(qs + 63, q_len - 1);
+  const int row_last = min(qs + PF_ROWS - 1, q_len - 1);
   const int kend = pos_base + row_last + 1;  // keys [0, kend) are needed by this tile
   const int ntiles = (kend + PF_KT - 1) / PF_KT;
   const int32_t* bt = block_tables + (size_t)s * max_blocks;
 
-  // Q^T fragments for this wave's 16 rows.
   const int my_row = qs + 16 * w + col;
   const int my_pos = pos_base + my_row;
+  const int wave_min_pos = pos_base + qs + 16 * w;
   bf16x8_t qf[4];
   {
-    const int r = min(my_row, q_len - 1);
-    const uint16_t* qr = q + ((size_t)(q_begin + r) * Hq + hq) * D;
+    const int rr = min(my_row, q_len - 1);
+    const uint16_t* qr = q + ((size_t)(q_begin + rr) * Hq + hq) * D;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) qf[c] = as_bf16x8(*reinterpret_cast<const uint4*>(qr + 32 * c + 8 * g));
+    for (int c = 0; c < 4; ++c) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(qr + 32 * c + 8 * g), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= scale_log2;
+      qf[c] = as_bf16x8(pack8(f));
+    }
   }
 
-  // LDS: [K buf0 16K][K buf1 16K][V buf0 16K][V buf1 16K]
-
-  uint4 kst[4], vst[4];
+  uint4 kst[2], vst[2];
   auto gload = [&](int kt) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int id = tid + 256 * i;
+    for (int i = 0; i < 2; ++i) {
+      const int id = tid + 512 * i;
       {  // K: row = id>>4 (key within tile), ch = id&15
         const int row = id >> 4, ch = id & 15, key = kt * PF_KT + row;
         if (key < kend) {
@@ -287,8 +304,8 @@ __global__ void __launch_bounds__(256) prefill_paged_kernel(
   };
   auto lwrite = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int id = tid + 256 * i;
+    for (int i = 0; i < 2; ++i) {
+      const int id = tid + 512 * i;
       *reinterpret_cast<uint4*>(smem + buf * 16384 + k_lds_off(id >> 4, id & 15)) = kst[i];
       *reinterpret_cast<uint4*>(smem + 32768 + buf * 16384 + v_lds_off(id >> 9, (id >> 2) & 127, id & 3)) = vst[i];
     }
@@ -309,53 +326,56 @@ __global__ void __launch_bounds__(256) prefill_paged_kernel(
 
     const char* kb = smem + cur * 16384;
     const char* vb = smem + 32768 + cur * 16384;
-    f32x4_t sc[4];
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      sc[st] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      const int row = 16 * st + col;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const uint4 kv = *reinterpret_cast<const uint4*>(kb + k_lds_off(row, 4 * c + g));
-        sc[st] = mfma16(as_bf16x8(kv), qf[c], sc[st]);
-      }
-    }
     const int key0 = kt * PF_KT;
-    float tmax = -INFINITY;
+    // tiles wholly above this wave's rows (possible only in the last tiles): skip the math
+    if (key0 <= wave_min_pos + 15) {
+      f32x4_t sc[4];
 #pragma unroll
-    for (int st = 0; st < 4; ++st)
+      for (int st = 0; st < 4; ++st) {
+        sc[st] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        const int row = 16 * st + col;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = key0 + 16 * st + 4 * g + i;
-        float v = sc[st][i] * scale_log2;
-        v = key <= my_pos ? v : -INFINITY;
-        sc[st][i] = v;
-        tmax = fmaxf(tmax, v);
+        for (int c = 0; c < 4; ++c)
+          sc[st] = mfma16(as_bf16x8(*reinterpret_cast<const uint4*>(kb + k_lds_off(row, 4 * c + g))), qf[c], sc[st]);
       }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mn = fmaxf(m, tmax);
-    // Rows past q_len (tile tail) can see only masked keys; keep them finite.
-    const float mref = mn == -INFINITY ? 0.f : mn;
-    const float alpha = exp2f(m - mref);
-    float rs = 0.f;
+      if (key0 + PF_KT - 1 > wave_min_pos) {  // diagonal tile: causal mask
 #pragma unroll
-    for (int st = 0; st < 4; ++st)
+        for (int st = 0; st < 4; ++st)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { const float e = exp2f(sc[st][i] - mref); sc[st][i] = e; rs += e; }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = mn;
+          for (int i = 0; i < 4; ++i)
+            if (key0 + 16 * st + 4 * g + i > my_pos) sc[st][i] = -INFINITY;
+      }
+      float tmax = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
+                         fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
+      tmax = fmaxf(tmax, fmaxf(fmaxf(fmaxf(sc[2][0], sc[2][1]), fmaxf(sc[2][2], sc[2][3])),
+                               fmaxf(fmaxf(sc[3][0], sc[3][1]), fmaxf(sc[3][2], sc[3][3]))));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      // deferred rescale: keep the old max unless some row of the wave grew by > THR
+      if (!__all(tmax - m <= RESCALE_THR)) {
+        const float mn = fmaxf(m, tmax);
+        const float mref = mn == -INFINITY ? 0.f : mn;
+        const float alpha = exp2f(m - mref);
+        l *= alpha;
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
+        for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
+        m = mn;
+      }
+      const float mref = m == -INFINITY ? 0.f : m;
+      float rs = 0.f;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8_t pf = pack_p(sc[2 * ks], sc[2 * ks + 1]);
+      for (int st = 0; st < 4; ++st)
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        const uint4 vv = *reinterpret_cast<const uint4*>(vb + v_lds_off(ks, 16 * dt + col, g));
-        o[dt] = mfma16(as_bf16x8(vv), pf, o[dt]);
+        for (int i = 0; i < 4; ++i) { const float e = exp2f(sc[st][i] - mref); sc[st][i] = e; rs += e; }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      l += rs;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8_t pf = pack_p(sc[2 * ks], sc[2 * ks + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt)
+          o[dt] = mfma16(as_bf16x8(*reinterpret_cast<const uint4*>(vb + v_lds_off(ks, 16 * dt + col, g))), pf, o[dt]);
       }
     }
     if (more) lwrite(cur ^ 1);
@@ -530,6 +550,8 @@ CFC_API int cfc_paged_decode_attention(const void* q, const void* k_cache, const
   return CFC_CHECK_LAUNCH();
 }
 
+CFC_API int cfc_prefill_tile_rows() { return PF_ROWS; }
+
 CFC_API int cfc_prefill_attention(const void* q, const void* k_cache, const void* v_cache, const int32_t* block_tables,
                                   const int32_t* cu_q, const int32_t* ctx_lens, const int32_t* tile_seq,
                                   const int32_t* tile_q0, int n_tiles, int Hq, int Hkv, int head_dim, int max_blocks,
@@ -537,9 +559,13 @@ CFC_API int cfc_prefill_attention(const void* q, const void* k_cache, const void
   if (head_dim != 128 || Hq % Hkv != 0) return -1;
   if (n_tiles <= 0) return 0;
   const size_t lds = 65536;
-  prefill_paged_kernel<<<dim3(n_tiles, Hq), 256, lds, stream>>>(
-      (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, cu_q, ctx_lens, tile_seq,
-      tile_q0, scale * LOG2E, Hq, Hkv, max_blocks, (uint16_t*)out);
+  // variant 0: <=128 VGPRs (2 workgroups / CU); variant 1: <=256 VGPRs (1 workgroup / CU)
+  static const int variant = [] { const char* e = getenv("CFC_PREFILL_VARIANT"); return e ? atoi(e) : 0; }();
+#define PF_ARGS (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, cu_q, ctx_lens, \
+    tile_seq, tile_q0, scale * LOG2E, Hq, Hkv, max_blocks, (uint16_t*)out
+  if (variant == 1) prefill_paged_kernel<2><<<dim3(n_tiles, Hq), 512, lds, stream>>>(PF_ARGS);
+  else prefill_paged_kernel<4><<<dim3(n_tiles, Hq), 512, lds, stream>>>(PF_ARGS);
+#undef PF_ARGS
   return CFC_CHECK_LAUNCH();
 }
 

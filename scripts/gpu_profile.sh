@@ -1,0 +1,12 @@
+#!/bin/bash
+# rocprofv3 kernel-trace + stats of a short LLM bench (decode-heavy and prefill phases).
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || exit 1
+rm -rf gpurun_out/prof
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
+  python bench.py "$@" > gpurun_out/prof_bench.log 2>&1; rc=$?
+tail -3 gpurun_out/prof_bench.log
+[ $rc -eq 0 ] || exit $rc
+python scripts/prof_summary.py gpurun_out/prof gpurun_out/prof_summary.txt | head -40

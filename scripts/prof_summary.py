@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --stats / --kernel-trace CSV output into a short text table."""
+import csv
+import glob
+import sys
+from collections import defaultdict
+
+
+def main(root, out=None, top=30):
+    stats = glob.glob(f"{root}/**/*kernel_stats.csv", recursive=True)
+    lines = []
+    if stats:
+        rows = list(csv.DictReader(open(stats[0])))
+        tot = sum(float(r["TotalDurationNs"]) for r in rows)
+        lines.append(f"# {stats[0]}\n# total kernel time {tot/1e6:.1f} ms over {sum(int(r['Calls']) for r in rows)} dispatches")
+        lines.append(f"{'pct':>6} {'total_ms':>10} {'calls':>7} {'avg_us':>9}  kernel")
+        for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:top]:
+            lines.append(f"{100*float(r['TotalDurationNs'])/tot:6.2f} {float(r['TotalDurationNs'])/1e6:10.2f} "
+                         f"{int(r['Calls']):7d} {float(r['AverageNs'])/1e3:9.1f}  {r['Name'][:150]}")
+    else:
+        traces = glob.glob(f"{root}/**/*kernel_trace.csv", recursive=True)
+        agg = defaultdict(lambda: [0, 0.0])
+        for t in traces:
+            for r in csv.DictReader(open(t)):
+                d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                a = agg[r["Kernel_Name"]]
+                a[0] += 1
+                a[1] += d
+        tot = sum(v[1] for v in agg.values()) or 1
+        lines.append(f"{'pct':>6} {'total_ms':>10} {'calls':>7} {'avg_us':>9}  kernel")
+        for k, (n, d) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
+            lines.append(f"{100*d/tot:6.2f} {d/1e6:10.2f} {n:7d} {d/n/1e3:9.1f}  {k[:150]}")
+    text = "\n".join(lines)
+    print(text)
+    if out:
+        open(out, "w").write(text + "\n")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
