@@ -65,6 +65,8 @@ def main(argv=None):
                          max_new_tokens=args.max_new, tp=args.tp, prefill_tokens=args.prefill_tokens,
                          llm_only=args.llm_only, use_graph=not args.no_graph, seed=args.seed + 7919 * rank)
 
+    pipe.prepare_sources(list(range(args.warmup + args.steps)))
+
     def barrier():
         if world > 1:
             dist.barrier()

@@ -6,11 +6,11 @@ copilot_message_bus/factory.py:94,147): the validating decorator wraps the drive
 from __future__ import annotations
 
 from .base import EventPublisher, EventSubscriber, topic_matches
-from .inproc import (InProcBroker, InProcPublisher, InProcSubscriber, NoopPublisher, NoopSubscriber,
+from .inproc import (CountingPublisher, InProcBroker, InProcPublisher, InProcSubscriber, NoopPublisher, NoopSubscriber,
                      default_broker, reset_default_broker)
 from .validating import EventValidationError, ValidatingEventPublisher, ValidatingEventSubscriber
 
-__all__ = ["EventPublisher", "EventSubscriber", "topic_matches", "InProcBroker", "InProcPublisher",
+__all__ = ["CountingPublisher", "EventPublisher", "EventSubscriber", "topic_matches", "InProcBroker", "InProcPublisher",
            "InProcSubscriber", "NoopPublisher", "NoopSubscriber", "default_broker", "reset_default_broker",
            "EventValidationError", "ValidatingEventPublisher", "ValidatingEventSubscriber", "create_publisher",
            "create_subscriber"]

@@ -194,6 +194,17 @@ class NoopPublisher(EventPublisher):
         self.published_events.clear()
 
 
+class CountingPublisher(EventPublisher):
+    """Counts events per type without retaining payloads (long-running batch pipelines)."""
+
+    def __init__(self, **_):
+        self.counts: dict[str, int] = collections.Counter()
+        self.bytes = 0
+
+    def publish(self, exchange: str, routing_key: str, event: dict[str, Any]) -> None:
+        self.counts[event.get("event_type", "?")] += 1
+
+
 class NoopSubscriber(EventSubscriber):
     """Callbacks driven by ``inject_event`` (reference noop_subscriber.py:18,101-123)."""
 

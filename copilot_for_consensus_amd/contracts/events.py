@@ -179,7 +179,11 @@ def event_schema(event_type: str) -> dict:
         "title": f"{event_type} Event",
         "allOf": [
             {"$ref": "./event-envelope.schema.json"},
-            {"type": "object", "properties": {"event_type": {"const": event_type}, "data": data},
+            # envelope fields repeated so additionalProperties:false is correct under strict Draft
+            # 2020-12 semantics (the reference instead strips it at validation time,
+            # schema_validator.py _strip_allof_additional_properties)
+            {"type": "object", "properties": {"event_type": {"const": event_type}, "event_id": UUID, "timestamp": DT,
+                                              "version": s(), "data": data},
              "required": ["event_type", "event_id", "timestamp", "version", "data"], "additionalProperties": False},
         ],
     }

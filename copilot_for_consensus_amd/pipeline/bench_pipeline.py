@@ -41,15 +41,22 @@ class BenchPipeline:
         w = DecoderWeights.random(self.cfg, self.device, seed=1234)
         self.model = DecoderModel(w)
         # KV budget: every thread of a step at the longest prompt we generate (3k) + max_new, x1.1
-        max_prompt = 3200
+        max_prompt = 4096
         nblk = int(1.1 * threads_per_step * blocks_needed(max_prompt + max_new_tokens)) + 64
         self.kv = PagedKVCache(self.cfg.layers, nblk, w.kv_heads, self.cfg.head_dim, self.device)
         self.engine = LLMEngine(self.model, self.kv, max_prefill_tokens=prefill_tokens, use_graph=use_graph)
         self.rag = None
         if not llm_only:
+            from ..bus import CountingPublisher
             from .rag import RagPipeline
+            self.events = CountingPublisher()
             self.rag = RagPipeline(encoder=encoder, device=self.device, decoder_vocab=self.cfg.vocab_size,
-                                   bos_id=self.cfg.bos_id, seed=seed)
+                                   bos_id=self.cfg.bos_id, seed=seed, publisher=self.events, llm_model=model)
+
+    def prepare_sources(self, steps: list[int]) -> None:
+        """Generate the synthetic archives of the given steps up front (outside the timed region)."""
+        if self.rag is not None:
+            self.rag.prepare_sources(self.threads_per_step, steps)
 
     def _synthetic_prompts(self, n):
         # ~2.5-3k prompt tokens: BASELINE.md "prefill of about 2.5k-3k tokens"

@@ -1,0 +1,223 @@
+"""Python front-ends of the C++ tokenizers (csrc/runtime/tokenizer.cpp).
+
+* :class:`BPETokenizer` -- SentencePiece-style BPE for the Mistral/Llama decoder.  Loads an HF
+  ``tokenizer.json`` (BPE model) when a checkpoint is available; otherwise trains a 32000-entry
+  vocabulary with the native trainer on the synthetic corpus (random-init weights need a
+  tokenizer of the right vocabulary size, not a specific one).
+* :class:`WordPieceTokenizer` -- BERT uncased WordPiece for the encoder.  Loads ``vocab.txt`` or
+  derives a 30522-entry vocabulary from the trained BPE pieces (word-initial pieces, ``##``
+  continuations), with BERT's special-token ids ([PAD]=0 [UNK]=100 [CLS]=101 [SEP]=102).
+Trained vocabularies are cached as JSON under ``_lib/tokenizers`` (deterministic, git-ignored).
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import threading
+from pathlib import Path
+
+import numpy as np
+
+from ..ops._native import runtime
+
+CACHE_DIR = Path(__file__).resolve().parent.parent / "_lib" / "tokenizers"
+_lock = threading.Lock()
+
+
+def _c(s: str) -> tuple[bytes, int]:
+    b = s.encode("utf-8")
+    return b, len(b)
+
+
+class BPETokenizer:
+    def __init__(self, vocab: list[str], merges: list[tuple[int, int]], bos_id: int = 1, eos_id: int = 2):
+        self.vocab = vocab
+        self.bos_id, self.eos_id = bos_id, eos_id
+        self._lib = runtime()
+        self._h = self._lib.cfc_bpe_create()
+        for i, t in enumerate(vocab):
+            b, n = _c(t)
+            self._lib.cfc_bpe_add_token(self._h, b, n, i)
+        tok2id = {t: i for i, t in enumerate(vocab)}
+        for rank, (a, b) in enumerate(merges):
+            merged = tok2id.get(vocab[a] + vocab[b])
+            if merged is not None:
+                self._lib.cfc_bpe_add_merge(self._h, a, b, rank, merged)
+        self._lib.cfc_bpe_finalize(self._h)
+        self._buf = np.empty(1 << 16, dtype=np.int32)
+        self._enc_lock = threading.Lock()
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._lib.cfc_bpe_destroy(h)
+            self._h = None
+
+    @property
+    def vocab_size(self) -> int:
+        return len(self.vocab)
+
+    def encode(self, text: str, add_bos: bool = True) -> list[int]:
+        b, n = _c(text)
+        with self._enc_lock:
+            cap = len(self._buf)
+            k = self._lib.cfc_bpe_encode(self._h, b, n, self._buf.ctypes.data, cap)
+            if k > cap:
+                self._buf = np.empty(k * 2, dtype=np.int32)
+                k = self._lib.cfc_bpe_encode(self._h, b, n, self._buf.ctypes.data, len(self._buf))
+            ids = self._buf[:k].tolist()
+        return ([self.bos_id] + ids) if add_bos else ids
+
+    def decode(self, ids: list[int]) -> str:
+        arr = np.asarray([i for i in ids if i not in (self.bos_id, self.eos_id)], dtype=np.int32)
+        cap = max(64, 16 * len(arr))
+        out = ctypes.create_string_buffer(cap)
+        n = self._lib.cfc_bpe_decode(self._h, arr.ctypes.data, len(arr), out, cap)
+        return out.raw[:min(n, cap)].decode("utf-8", errors="replace")
+
+    # ---------------------------------------------------------------- constructors
+    @classmethod
+    def from_hf_json(cls, path) -> "BPETokenizer":
+        d = json.loads(Path(path).read_text())
+        model = d["model"]
+        if model.get("type") != "BPE":
+            raise ValueError("tokenizer.json is not a BPE model")
+        v = model["vocab"]
+        vocab = [None] * (max(v.values()) + 1)
+        for t, i in v.items():
+            vocab[i] = t
+        for at in d.get("added_tokens", []):
+            if at["id"] < len(vocab):
+                vocab[at["id"]] = at["content"]
+        vocab = [t if t is not None else f"<unused{i}>" for i, t in enumerate(vocab)]
+        merges = []
+        for m in model["merges"]:
+            a, b = m.split(" ", 1) if isinstance(m, str) else m
+            if a in v and b in v:
+                merges.append((v[a], v[b]))
+        specials = {at["content"]: at["id"] for at in d.get("added_tokens", [])}
+        return cls(vocab, merges, specials.get("<s>", 1), specials.get("</s>", 2))
+
+    @classmethod
+    def train(cls, corpus: str, vocab_size: int = 32000) -> "BPETokenizer":
+        vocab, pairs = train_bpe(corpus, vocab_size)
+        return cls(vocab, pairs)
+
+
+def train_bpe(corpus: str, vocab_size: int) -> tuple[list[str], list[tuple[int, int]]]:
+    """Native BPE training -> (vocab, merges).  Layout: <unk> <s> </s>, 256 byte tokens, the
+    corpus' base characters, then one token per merge in rank order."""
+    lib = runtime()
+    b, n = _c(corpus)
+    base_buf = ctypes.create_string_buffer(4 << 20)
+    merges = np.empty(2 * vocab_size, dtype=np.int32)
+    nm = lib.cfc_bpe_train(b, n, vocab_size, base_buf, merges.ctypes.data, vocab_size)
+    base = [x.decode("utf-8", errors="replace") for x in base_buf.raw.split(b"\0\0", 1)[0].split(b"\0") if x]
+    vocab = ["<unk>", "<s>", "</s>"] + [f"<0x{i:02X}>" for i in range(256)] + base
+    pairs = [(int(merges[2 * i]), int(merges[2 * i + 1])) for i in range(nm)]
+    for a, bb in pairs:
+        vocab.append(vocab[a] + vocab[bb])
+    while len(vocab) < vocab_size:
+        vocab.append(f"<unused{len(vocab)}>")
+    vocab = vocab[:vocab_size]
+    return vocab, [p for p in pairs if max(p) < vocab_size]
+
+
+_SYNTH_TOKENIZERS: dict = {}
+
+
+def synthetic_bpe(vocab_size: int = 32000, corpus_words: int = 800_000) -> BPETokenizer:
+    """Deterministic BPE trained on the synthetic mailing-list distribution (cached on disk)."""
+    key = ("bpe", vocab_size)
+    with _lock:
+        if key in _SYNTH_TOKENIZERS:
+            return _SYNTH_TOKENIZERS[key]
+        path = CACHE_DIR / f"synthetic_bpe_{vocab_size}.json"
+        if path.exists():
+            d = json.loads(path.read_text())
+            tok = BPETokenizer(d["vocab"], [tuple(m) for m in d["merges"]])
+        else:
+            from ..utils.synthetic import SyntheticArchive
+            vocab, pairs = train_bpe(SyntheticArchive(seed=777).corpus(corpus_words), vocab_size)
+            CACHE_DIR.mkdir(parents=True, exist_ok=True)
+            tmp = path.with_suffix(".tmp")
+            tmp.write_text(json.dumps({"vocab": vocab, "merges": pairs}))
+            tmp.replace(path)
+            tok = BPETokenizer(vocab, pairs)
+        _SYNTH_TOKENIZERS[key] = tok
+        return tok
+
+
+class WordPieceTokenizer:
+    PAD, UNK, CLS, SEP, MASK = 0, 100, 101, 102, 103
+
+    def __init__(self, vocab: list[str], lowercase: bool = True, max_length: int = 512):
+        self.vocab = vocab
+        self.max_length = max_length
+        self._lib = runtime()
+        tok2id = {t: i for i, t in enumerate(vocab)}
+        self.unk_id = tok2id.get("[UNK]", self.UNK)
+        self.cls_id = tok2id.get("[CLS]", self.CLS)
+        self.sep_id = tok2id.get("[SEP]", self.SEP)
+        self._h = self._lib.cfc_wp_create(self.unk_id, self.cls_id, self.sep_id, 1 if lowercase else 0)
+        for i, t in enumerate(vocab):
+            b, n = _c(t)
+            self._lib.cfc_wp_add_token(self._h, b, n, i)
+        self._buf = np.empty(1 << 16, dtype=np.int32)
+        self._enc_lock = threading.Lock()
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._lib.cfc_wp_destroy(h)
+            self._h = None
+
+    def encode(self, text: str, max_length: int | None = None) -> list[int]:
+        """[CLS] pieces [SEP], truncated to max_length (sentence-transformers behaviour)."""
+        L = max_length or self.max_length
+        b, n = _c(text)
+        with self._enc_lock:
+            k = self._lib.cfc_wp_encode(self._h, b, n, self._buf.ctypes.data, len(self._buf))
+            if k > len(self._buf):
+                self._buf = np.empty(2 * k, dtype=np.int32)
+                k = self._lib.cfc_wp_encode(self._h, b, n, self._buf.ctypes.data, len(self._buf))
+            ids = self._buf[:min(k, L - 2)].tolist()
+        return [self.cls_id] + ids + [self.sep_id]
+
+    def encode_batch(self, texts: list[str], max_length: int | None = None) -> list[list[int]]:
+        return [self.encode(t, max_length) for t in texts]
+
+    @classmethod
+    def from_vocab_txt(cls, path, **kw) -> "WordPieceTokenizer":
+        return cls(Path(path).read_text(encoding="utf-8").splitlines(), **kw)
+
+
+def synthetic_wordpiece(vocab_size: int = 30522, max_length: int = 256) -> WordPieceTokenizer:
+    key = ("wp", vocab_size, max_length)
+    with _lock:
+        if key in _SYNTH_TOKENIZERS:
+            return _SYNTH_TOKENIZERS[key]
+    bpe = synthetic_bpe()
+    vocab = ["[PAD]"] + [f"[unused{i}]" for i in range(99)] + ["[UNK]", "[CLS]", "[SEP]", "[MASK]"]
+    seen = set(vocab)
+    for c in "abcdefghijklmnopqrstuvwxyz0123456789.,!?;:'\"()-_/<>@[]{}#$%&*+=|~^`\\":
+        for t in (c, "##" + c):
+            if t not in seen:
+                seen.add(t)
+                vocab.append(t)
+    for t in bpe.vocab[259:]:
+        if t.startswith("<unused"):
+            continue
+        piece = t[1:] if t.startswith("▁") else "##" + t
+        piece = piece.lower()
+        if piece and piece != "##" and piece not in seen:
+            seen.add(piece)
+            vocab.append(piece)
+        if len(vocab) >= vocab_size:
+            break
+    while len(vocab) < vocab_size:
+        vocab.append(f"[unused{len(vocab)}]")
+    tok = WordPieceTokenizer(vocab[:vocab_size], max_length=max_length)
+    with _lock:
+        _SYNTH_TOKENIZERS[key] = tok
+    return tok

@@ -1,0 +1,207 @@
+"""Summarizers (API of adapters/copilot_summarization: Summarizer.summarize(Thread) -> Summary,
+summarizer.py:20; models Thread / Summary / Citation, models.py).
+
+* :class:`HipLLMSummarizer` (driver ``hip``) -- the MI355X decoder engine (runtime/engine.py):
+  ``summarize_batch`` generates many threads at once (continuous prefill + hipGraph decode), and
+  token counts are real tokenizer counts (the local reference backends report word counts,
+  local_llm_summarizer.py:101,129).
+* :class:`MockSummarizer` -- deterministic canned summary with optional latency.
+* :class:`LocalLLMSummarizer` (Ollama ``/api/generate``), :class:`LlamaCppSummarizer`
+  (``/completion``), :class:`OpenAISummarizer` -- HTTP drivers kept for deployment parity.
+"""
+from __future__ import annotations
+
+import dataclasses
+import time
+from abc import ABC, abstractmethod
+
+import torch
+
+
+@dataclasses.dataclass
+class Citation:
+    message_id: str
+    chunk_id: str
+    offset: int = 0
+
+
+@dataclasses.dataclass
+class Thread:
+    thread_id: str
+    messages: list[str]
+    top_k: int = 10
+    context_window_tokens: int = 4096
+    prompt: str = "Summarize the following discussion thread:"
+
+
+@dataclasses.dataclass
+class Summary:
+    thread_id: str
+    summary_markdown: str
+    citations: list[Citation] = dataclasses.field(default_factory=list)
+    llm_backend: str = "unknown"
+    llm_model: str = "unknown"
+    tokens_prompt: int = 0
+    tokens_completion: int = 0
+    latency_ms: int = 0
+
+
+class Summarizer(ABC):
+    backend = "unknown"
+    model = "unknown"
+
+    @abstractmethod
+    def summarize(self, thread: Thread) -> Summary: ...
+
+    def summarize_batch(self, threads: list[Thread]) -> list[Summary]:
+        return [self.summarize(t) for t in threads]
+
+
+class MockSummarizer(Summarizer):
+    backend, model = "mock", "mock"
+
+    def __init__(self, mock_latency_ms: int = 100, **_):
+        self.latency_ms = int(mock_latency_ms or 0)
+
+    def summarize(self, thread: Thread) -> Summary:
+        if self.latency_ms:
+            time.sleep(self.latency_ms / 1000)
+        body = "\n".join(f"- {m[:80]}" for m in thread.messages[:5])
+        md = f"# Summary of thread {thread.thread_id}\n\n{len(thread.messages)} excerpts reviewed.\n\n{body}\n"
+        return Summary(thread.thread_id, md, [], self.backend, self.model, len(thread.prompt.split()),
+                       len(md.split()), self.latency_ms)
+
+
+class HipLLMSummarizer(Summarizer):
+    backend = "hip"
+
+    def __init__(self, model: str = "mistral-7b", checkpoint_dir: str | None = None, tensor_parallel: int = 1,
+                 max_new_tokens: int = 512, temperature: float = 0.0, max_batch: int = 128,
+                 kv_cache_tokens: int = 524288, device: str = "cuda", seed: int = 1234, tp_group=None,
+                 tp_rank: int = 0, ignore_eos: bool = False, **_):
+        from ..models.decoder import DecoderModel, DecoderWeights, get_config, load_config_json
+        from ..runtime.engine import LLMEngine
+        from ..runtime.kv_cache import PagedKVCache
+        from ..runtime.tokenizer import BPETokenizer, synthetic_bpe
+        dev = torch.device(device if (not str(device).startswith("cuda") or torch.cuda.is_available()) else "cpu")
+        if checkpoint_dir:
+            from pathlib import Path
+            cfg = load_config_json(Path(checkpoint_dir) / "config.json")
+            w = DecoderWeights.from_safetensors(cfg, checkpoint_dir, dev, tp_rank, tensor_parallel)
+            self.tokenizer = BPETokenizer.from_hf_json(Path(checkpoint_dir) / "tokenizer.json")
+        else:
+            cfg = get_config(model)
+            w = DecoderWeights.random(cfg, dev, seed=seed, tp_rank=tp_rank, tp_size=tensor_parallel)
+            self.tokenizer = synthetic_bpe(cfg.vocab_size)
+        self.cfg = cfg
+        self.model = cfg.name
+        self.decoder = DecoderModel(w, tp_group=tp_group)
+        self.kv = PagedKVCache.for_budget(cfg.layers, w.kv_heads, cfg.head_dim, dev, kv_cache_tokens)
+        self.engine = LLMEngine(self.decoder, self.kv)
+        self.max_new_tokens, self.temperature = int(max_new_tokens), float(temperature)
+        self.max_batch = int(max_batch)
+        self.ignore_eos = ignore_eos
+        self.context_limit = cfg.max_positions - self.max_new_tokens
+
+    def _tokens(self, prompt: str) -> list[int]:
+        ids = self.tokenizer.encode(prompt)
+        if len(ids) > self.context_limit:  # keep the head (instructions) and the tail (latest excerpts)
+            half = self.context_limit // 2
+            ids = ids[:half] + ids[-(self.context_limit - half):]
+        return ids
+
+    def summarize_batch(self, threads: list[Thread], token_ids: list[list[int]] | None = None) -> list[Summary]:
+        out: list[Summary] = []
+        for s in range(0, len(threads), self.max_batch):
+            part = threads[s:s + self.max_batch]
+            ids = token_ids[s:s + self.max_batch] if token_ids is not None else [self._tokens(t.prompt) for t in part]
+            t0 = time.perf_counter()
+            res = self.engine.generate(ids, self.max_new_tokens, temperature=self.temperature,
+                                       ignore_eos=self.ignore_eos)
+            ms = int(1000 * (time.perf_counter() - t0))
+            for t, p, g in zip(part, ids, res.tokens):
+                text = self.tokenizer.decode(g).strip() or "(empty summary)"
+                out.append(Summary(t.thread_id, text, [], self.backend, self.model, len(p), len(g), ms))
+        return out
+
+    def summarize(self, thread: Thread) -> Summary:
+        return self.summarize_batch([thread])[0]
+
+
+class _HTTPSummarizer(Summarizer):
+    def _post(self, url, payload, timeout):
+        import requests
+        r = requests.post(url, json=payload, timeout=timeout)
+        r.raise_for_status()
+        return r.json()
+
+
+class LocalLLMSummarizer(_HTTPSummarizer):
+    """Ollama ``/api/generate`` (reference local_llm_summarizer.py:67,107)."""
+    backend = "local"
+
+    def __init__(self, local_llm_model="mistral", local_llm_endpoint="http://ollama:11434",
+                 local_llm_timeout_seconds=300, **_):
+        self.model, self.endpoint, self.timeout = local_llm_model, local_llm_endpoint, local_llm_timeout_seconds
+
+    def summarize(self, thread):
+        t0 = time.perf_counter()
+        d = self._post(f"{self.endpoint}/api/generate", {"model": self.model, "prompt": thread.prompt,
+                                                          "stream": False}, self.timeout)
+        text = d.get("response", "")
+        return Summary(thread.thread_id, text, [], self.backend, self.model, len(thread.prompt.split()),
+                       len(text.split()), int(1000 * (time.perf_counter() - t0)))
+
+
+class LlamaCppSummarizer(_HTTPSummarizer):
+    """llama.cpp server ``/completion`` (reference llamacpp_summarizer.py:68,108-113)."""
+    backend = "llamacpp"
+
+    def __init__(self, llamacpp_model="mistral", llamacpp_endpoint="http://llama-cpp:8081",
+                 llamacpp_timeout_seconds=300, **_):
+        self.model, self.endpoint, self.timeout = llamacpp_model, llamacpp_endpoint, llamacpp_timeout_seconds
+
+    def summarize(self, thread):
+        t0 = time.perf_counter()
+        d = self._post(f"{self.endpoint}/completion", {"prompt": thread.prompt, "n_predict": 512, "temperature": 0.7,
+                                                        "stop": ["</s>", "\n\n\n"]}, self.timeout)
+        text = d.get("content", "")
+        return Summary(thread.thread_id, text, [], self.backend, self.model, len(thread.prompt.split()),
+                       len(text.split()), int(1000 * (time.perf_counter() - t0)))
+
+
+class OpenAISummarizer(Summarizer):  # pragma: no cover - optional dependency
+    backend = "openai"
+
+    def __init__(self, openai_api_key=None, openai_model=None, openai_base_url=None, **_):
+        try:
+            import openai
+        except ImportError as e:
+            raise ImportError("openai is not installed") from e
+        self.client = openai.OpenAI(api_key=openai_api_key, base_url=openai_base_url)
+        self.model = openai_model or "gpt-4o-mini"
+
+    def summarize(self, thread):
+        t0 = time.perf_counter()
+        r = self.client.chat.completions.create(model=self.model, messages=[{"role": "user", "content": thread.prompt}],
+                                                max_tokens=thread.context_window_tokens)
+        text = r.choices[0].message.content or ""
+        return Summary(thread.thread_id, text, [], self.backend, self.model, r.usage.prompt_tokens,
+                       r.usage.completion_tokens, int(1000 * (time.perf_counter() - t0)))
+
+
+def create_llm_backend(cfg=None, **overrides) -> Summarizer:
+    name = getattr(cfg, "driver_name", cfg) or "hip"
+    kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
+    kw.update(overrides)
+    if name == "hip":
+        return HipLLMSummarizer(**kw)
+    if name == "mock":
+        return MockSummarizer(**kw)
+    if name == "local":
+        return LocalLLMSummarizer(**kw)
+    if name == "llamacpp":
+        return LlamaCppSummarizer(**kw)
+    if name in ("openai", "azure_openai_gpt"):
+        return OpenAISummarizer(**kw)
+    raise ValueError(f"unknown llm backend {name!r}")

@@ -1,0 +1,439 @@
+"""Vector stores: interface, HBM-resident HIP flat / IVF indexes, in-memory reference, factory.
+
+Interface = adapters/copilot_vectorstore/copilot_vectorstore/interface.py:12-114 of the reference
+(add_embedding / add_embeddings [upsert] / query(vector, top_k) -> [SearchResult] / delete / clear /
+count / get).  Replaces Qdrant / FAISS / Azure AI Search on the hot path:
+
+* :class:`HipFlatIndex` -- the whole index lives in one bf16 [capacity, dim] HBM tensor (a
+  288 GB MI355X holds 100M x 384 bf16 = 77 GB with room to spare); cosine = dot product of
+  L2-normalised rows (normalised on insert by a HIP kernel), or squared-L2 with stored norms
+  (FAISS IndexFlatL2 parity, score 1/(1+d), faiss_store.py:224).  Queries: <=16 at a time run the
+  fused MFMA scan kernel, larger batches a hipBLASLt GEMM; exact top-k by the radix-select kernel.
+  Vectors produced on the GPU (the encoder) are inserted without a host round trip.
+  Upserts overwrite in place; deletes tombstone + periodic compaction.
+* :class:`HipIVFIndex` -- IVF-flat: k-means coarse quantiser trained on the GPU, rows stored
+  list-contiguous, ``nprobe`` lists scanned per query.
+* :class:`InMemoryVectorStore` -- numpy reference (fixes the reference's duplicate-id error,
+  inmemory.py:46, which violates the upsert contract).
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import math
+import threading
+from abc import ABC, abstractmethod
+from pathlib import Path
+from typing import Any, Sequence
+
+import numpy as np
+import torch
+
+
+@dataclasses.dataclass
+class SearchResult:
+    id: str
+    score: float
+    vector: list[float]
+    metadata: dict[str, Any]
+
+
+class VectorStore(ABC):
+    def add_embedding(self, id: str, vector, metadata: dict[str, Any] | None = None) -> None:
+        self.add_embeddings([id], [vector], [metadata or {}])
+
+    @abstractmethod
+    def add_embeddings(self, ids: Sequence[str], vectors, metadatas: Sequence[dict] | None = None) -> None: ...
+
+    @abstractmethod
+    def query(self, query_vector, top_k: int = 10) -> list[SearchResult]: ...
+
+    @abstractmethod
+    def delete(self, id: str) -> None: ...
+
+    @abstractmethod
+    def clear(self) -> None: ...
+
+    @abstractmethod
+    def count(self) -> int: ...
+
+    @abstractmethod
+    def get(self, id: str) -> SearchResult: ...
+
+    def query_batch(self, query_vectors, top_k: int = 10) -> list[list[SearchResult]]:
+        return [self.query(q, top_k) for q in query_vectors]
+
+
+def _as_matrix(vectors, dim: int | None, device=None, dtype=torch.float32) -> torch.Tensor:
+    if isinstance(vectors, torch.Tensor):
+        t = vectors
+    else:
+        t = torch.as_tensor(np.asarray(vectors, dtype=np.float32))
+    if t.dim() == 1:
+        t = t[None]
+    if dim is not None and t.shape[1] != dim:
+        raise ValueError(f"vector dimension {t.shape[1]} != index dimension {dim}")
+    return t.to(device=device, dtype=dtype) if device is not None else t.to(dtype)
+
+
+class InMemoryVectorStore(VectorStore):
+    """numpy cosine store (reference semantics, but upsert-correct)."""
+
+    def __init__(self, dimension: int | None = None, **_):
+        self.dim = dimension
+        self._ids: list[str] = []
+        self._row: dict[str, int] = {}
+        self._vecs: list[np.ndarray] = []
+        self._meta: list[dict] = []
+        self._lock = threading.Lock()
+
+    def add_embeddings(self, ids, vectors, metadatas=None):
+        mats = _as_matrix(vectors, self.dim).cpu().numpy()
+        if len(ids) != len(mats):
+            raise ValueError("ids and vectors length mismatch")
+        metadatas = metadatas or [{} for _ in ids]
+        with self._lock:
+            if self.dim is None:
+                self.dim = mats.shape[1]
+            for i, v, m in zip(ids, mats, metadatas):
+                if i in self._row:
+                    r = self._row[i]
+                    self._vecs[r], self._meta[r] = v.copy(), dict(m)
+                else:
+                    self._row[i] = len(self._ids)
+                    self._ids.append(i)
+                    self._vecs.append(v.copy())
+                    self._meta.append(dict(m))
+
+    def query(self, query_vector, top_k=10):
+        if not self._ids:
+            return []
+        q = _as_matrix(query_vector, self.dim).cpu().numpy()[0]
+        X = np.stack(self._vecs)
+        sims = X @ q / np.maximum(np.linalg.norm(X, axis=1) * max(np.linalg.norm(q), 1e-12), 1e-12)
+        order = np.argsort(-sims, kind="stable")[:top_k]
+        return [SearchResult(self._ids[r], float(sims[r]), self._vecs[r].tolist(), dict(self._meta[r])) for r in order]
+
+    def delete(self, id):
+        with self._lock:
+            r = self._row.pop(id)
+            last = len(self._ids) - 1
+            if r != last:
+                self._ids[r], self._vecs[r], self._meta[r] = self._ids[last], self._vecs[last], self._meta[last]
+                self._row[self._ids[r]] = r
+            self._ids.pop()
+            self._vecs.pop()
+            self._meta.pop()
+
+    def clear(self):
+        with self._lock:
+            self._ids, self._row, self._vecs, self._meta = [], {}, [], []
+
+    def count(self):
+        return len(self._ids)
+
+    def get(self, id):
+        r = self._row[id]
+        return SearchResult(id, 1.0, self._vecs[r].tolist(), dict(self._meta[r]))
+
+
+class HipFlatIndex(VectorStore):
+    """Exact flat index resident in HBM (see module docstring)."""
+
+    def __init__(self, dimension: int = 384, distance: str = "cosine", capacity: int = 1 << 16, device="cuda",
+                 faiss_scores: bool = False, **_):
+        if distance not in ("cosine", "dot", "l2", "euclid"):
+            raise ValueError(f"unknown distance {distance!r}")
+        self.dim = int(dimension)
+        self.metric = "l2" if distance in ("l2", "euclid") else distance
+        self.faiss_scores = faiss_scores
+        self.device = torch.device(device if (device != "cuda" or torch.cuda.is_available()) else "cpu")
+        self._cap = 0
+        self._n = 0                       # rows in use (incl. tombstones)
+        self._X = torch.empty(0, self.dim, dtype=torch.bfloat16, device=self.device)
+        self._norm2 = torch.empty(0, dtype=torch.float32, device=self.device)
+        self._alive = torch.empty(0, dtype=torch.bool, device=self.device)
+        self._ids: list[str | None] = []
+        self._row: dict[str, int] = {}
+        self._meta: list[dict | None] = []
+        self._dead = 0
+        self._lock = threading.RLock()
+        self._reserve(capacity)
+
+    # ------------------------------------------------------------------ storage
+    def _reserve(self, n: int) -> None:
+        if n <= self._cap:
+            return
+        cap = max(n, 2 * self._cap, 1024)
+        X = torch.zeros(cap, self.dim, dtype=torch.bfloat16, device=self.device)
+        n2 = torch.zeros(cap, dtype=torch.float32, device=self.device)
+        al = torch.zeros(cap, dtype=torch.bool, device=self.device)
+        if self._n:
+            X[:self._n] = self._X[:self._n]
+            n2[:self._n] = self._norm2[:self._n]
+            al[:self._n] = self._alive[:self._n]
+        self._X, self._norm2, self._alive, self._cap = X, n2, al, cap
+
+    def _prepare(self, vecs: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        from ..ops import kernels as K
+        v = vecs.to(device=self.device, dtype=torch.bfloat16).contiguous()
+        n2 = torch.empty(v.shape[0], dtype=torch.float32, device=self.device)
+        if self.metric == "cosine":
+            v = K.l2_normalize(v, norms2=n2)
+            n2.fill_(1.0)
+        else:
+            n2 = v.float().pow(2).sum(1)
+        return v, n2
+
+    def add_embeddings(self, ids, vectors, metadatas=None):
+        vecs = _as_matrix(vectors, self.dim)
+        if len(ids) != vecs.shape[0]:
+            raise ValueError("ids and vectors length mismatch")
+        metadatas = list(metadatas) if metadatas is not None else [{} for _ in ids]
+        v, n2 = self._prepare(vecs)
+        with self._lock:
+            rows = []
+            for i in ids:
+                r = self._row.get(i)
+                if r is None:
+                    r = self._n
+                    self._n += 1
+                    self._row[i] = r
+                    self._ids.append(i)
+                    self._meta.append(None)
+                rows.append(r)
+            self._reserve(self._n)
+            idx = torch.tensor(rows, dtype=torch.long, device=self.device)
+            self._X.index_copy_(0, idx, v)
+            self._norm2.index_copy_(0, idx, n2)
+            self._alive[idx] = True
+            for r, m in zip(rows, metadatas):
+                self._meta[r] = dict(m or {})
+
+    def delete(self, id):
+        with self._lock:
+            r = self._row.pop(id)  # KeyError if absent (reference contract)
+            self._alive[r] = False
+            self._ids[r] = None
+            self._meta[r] = None
+            self._dead += 1
+            if self._dead > 1024 and self._dead > self._n // 4:
+                self.compact()
+
+    def compact(self) -> None:
+        with self._lock:
+            keep = [r for r in range(self._n) if self._ids[r] is not None]
+            idx = torch.tensor(keep, dtype=torch.long, device=self.device)
+            n = len(keep)
+            self._X[:n] = self._X.index_select(0, idx) if n else self._X[:0]
+            self._norm2[:n] = self._norm2.index_select(0, idx) if n else self._norm2[:0]
+            self._alive[:n] = True
+            self._alive[n:] = False
+            self._ids = [self._ids[r] for r in keep]
+            self._meta = [self._meta[r] for r in keep]
+            self._row = {i: r for r, i in enumerate(self._ids)}
+            self._n, self._dead = n, 0
+
+    def clear(self):
+        with self._lock:
+            self._n, self._dead = 0, 0
+            self._ids, self._row, self._meta = [], {}, []
+            self._alive.zero_()
+
+    def count(self):
+        return self._n - self._dead
+
+    def get(self, id):
+        r = self._row[id]
+        return SearchResult(id, 1.0, self._X[r].float().cpu().tolist(), dict(self._meta[r]))
+
+    # ------------------------------------------------------------------ search
+    def search(self, Q: torch.Tensor, k: int, rows: tuple[int, int] | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+        """Device-side exact search: (scores [nq, k], row indices [nq, k]) for queries Q."""
+        from ..ops import kernels as K
+        lo, hi = rows if rows is not None else (0, self._n)
+        Q = _as_matrix(Q, self.dim, device=self.device, dtype=torch.bfloat16)
+        nq = Q.shape[0]
+        if hi <= lo:
+            return (torch.empty(nq, 0, device=self.device), torch.empty(nq, 0, dtype=torch.long, device=self.device))
+        X = self._X[lo:hi]
+        if self.metric == "cosine":
+            Qn = K.l2_normalize(Q.contiguous())
+            qn2 = None
+        else:
+            Qn = Q.contiguous()
+            qn2 = Qn.float().pow(2).sum(1)
+        xn2 = self._norm2[lo:hi] if self.metric == "l2" else None
+        if Q.is_cuda and nq <= 16:
+            scores = K.knn_scores(X, Qn, xn2, qn2)
+        else:
+            scores = Qn.float() @ X.float().T if not Q.is_cuda else (Qn @ X.T).float()
+            if self.metric == "l2":
+                scores = -(xn2[None, :] + qn2[:, None] - 2 * scores)
+        if self._dead:
+            scores = scores.masked_fill(~self._alive[lo:hi][None, :], float("-inf"))
+        v, i = K.topk(scores.contiguous(), k)
+        return v, i + lo
+
+    def _to_results(self, v: torch.Tensor, i: torch.Tensor, with_vectors: bool = True) -> list[list[SearchResult]]:
+        v, i = v.cpu(), i.cpu()
+        out = []
+        for qv, qi in zip(v.tolist(), i.tolist()):
+            res = []
+            for s, r in zip(qv, qi):
+                if r < 0 or s == float("-inf") or self._ids[r] is None:
+                    continue
+                if self.metric == "l2":
+                    s = 1.0 / (1.0 + max(0.0, -s)) if self.faiss_scores else -s
+                vec = self._X[r].float().cpu().tolist() if with_vectors else []
+                res.append(SearchResult(self._ids[r], float(s), vec, dict(self._meta[r])))
+            out.append(res)
+        return out
+
+    def query(self, query_vector, top_k=10):
+        return self.query_batch(_as_matrix(query_vector, self.dim), top_k)[0]
+
+    def query_batch(self, query_vectors, top_k=10, with_vectors: bool = False):
+        with self._lock:
+            if self.count() == 0:
+                return [[] for _ in range(len(query_vectors))]
+            Q = _as_matrix(query_vectors, self.dim)
+            outs = []
+            for s in range(0, Q.shape[0], 16):
+                v, i = self.search(Q[s:s + 16], min(top_k, self.count()))
+                outs.extend(self._to_results(v, i, with_vectors))
+            return outs
+
+    # ------------------------------------------------------------------ persistence
+    def save(self, path) -> None:
+        """Index shard = safetensors blob (vectors, norms) + JSON sidecar (ids, metadata)."""
+        from safetensors.torch import save_file
+        p = Path(path)
+        p.mkdir(parents=True, exist_ok=True)
+        with self._lock:
+            self.compact()
+            save_file({"vectors": self._X[:self._n].contiguous().cpu(), "norm2": self._norm2[:self._n].cpu()},
+                      str(p / "vectors.safetensors"))
+            (p / "index.json").write_text(json.dumps({"dim": self.dim, "metric": self.metric, "ids": self._ids,
+                                                      "metadata": self._meta}))
+
+    @classmethod
+    def load(cls, path, device="cuda") -> "HipFlatIndex":
+        from safetensors.torch import load_file
+        p = Path(path)
+        meta = json.loads((p / "index.json").read_text())
+        t = load_file(str(p / "vectors.safetensors"))
+        idx = cls(meta["dim"], "l2" if meta["metric"] == "l2" else meta["metric"], capacity=len(meta["ids"]) + 1024,
+                  device=device)
+        n = len(meta["ids"])
+        idx._X[:n] = t["vectors"].to(idx.device)
+        idx._norm2[:n] = t["norm2"].to(idx.device)
+        idx._alive[:n] = True
+        idx._ids = list(meta["ids"])
+        idx._meta = list(meta["metadata"])
+        idx._row = {i: r for r, i in enumerate(idx._ids)}
+        idx._n = n
+        return idx
+
+
+class HipIVFIndex(HipFlatIndex):
+    """IVF-flat: rows grouped by nearest centroid; ``nprobe`` lists scanned per query."""
+
+    def __init__(self, dimension=384, distance="cosine", nlist: int = 0, nprobe: int = 8, **kw):
+        super().__init__(dimension, distance, **kw)
+        self.nlist, self.nprobe = int(nlist), int(nprobe)
+        self.centroids: torch.Tensor | None = None
+        self._list_off: list[int] = []
+        self._trained_n = 0
+
+    def train(self, sample: torch.Tensor | None = None, iters: int = 10, seed: int = 0) -> None:
+        """k-means on the GPU (GEMM assignment + index_add centroid update), then regroup rows."""
+        with self._lock:
+            self.compact()
+            n = self._n
+            if n == 0:
+                return
+            nlist = self.nlist or max(1, int(math.sqrt(n)))
+            X = (sample if sample is not None else self._X[:n]).to(self.device).float()
+            g = torch.Generator(device="cpu").manual_seed(seed)
+            C = X[torch.randperm(X.shape[0], generator=g)[:nlist].to(self.device)].clone()
+            for _ in range(iters):
+                a = torch.argmax(X @ C.T, 1) if self.metric != "l2" else torch.argmin(torch.cdist(X, C), 1)
+                sums = torch.zeros_like(C).index_add_(0, a, X)
+                cnt = torch.bincount(a, minlength=C.shape[0]).clamp_min(1).float()[:, None]
+                C = sums / cnt
+                if self.metric == "cosine":
+                    C = torch.nn.functional.normalize(C, dim=1)
+            self.centroids = C.to(torch.bfloat16)
+            self.nlist = C.shape[0]
+            self._regroup()
+
+    def _assign(self, X: torch.Tensor) -> torch.Tensor:
+        C = self.centroids.float()
+        return torch.argmax(X.float() @ C.T, 1) if self.metric != "l2" else torch.argmin(torch.cdist(X.float(), C), 1)
+
+    def _regroup(self):
+        n = self._n
+        a = self._assign(self._X[:n])
+        order = torch.argsort(a, stable=True)
+        self._X[:n] = self._X[:n].index_select(0, order)
+        self._norm2[:n] = self._norm2[:n].index_select(0, order)
+        o = order.cpu().tolist()
+        self._ids = [self._ids[r] for r in o]
+        self._meta = [self._meta[r] for r in o]
+        self._row = {i: r for r, i in enumerate(self._ids)}
+        counts = torch.bincount(a, minlength=self.nlist).cpu().tolist()
+        self._list_off = [0]
+        for c in counts:
+            self._list_off.append(self._list_off[-1] + c)
+        self._trained_n = n
+
+    def add_embeddings(self, ids, vectors, metadatas=None):
+        super().add_embeddings(ids, vectors, metadatas)
+        # rows appended after training form an unsorted tail scanned exhaustively until re-train
+        if self.centroids is not None and self._n > 2 * max(self._trained_n, 1):
+            self._regroup()
+
+    def search(self, Q, k, rows=None):
+        if self.centroids is None or rows is not None:
+            return super().search(Q, k, rows)
+        Q = _as_matrix(Q, self.dim, device=self.device, dtype=torch.bfloat16)
+        probe = torch.topk((Q.float() @ self.centroids.float().T), min(self.nprobe, self.nlist), dim=1).indices.cpu()
+        vs, is_ = [], []
+        for qi in range(Q.shape[0]):
+            cand_v, cand_i = [], []
+            spans = [(self._list_off[c], self._list_off[c + 1]) for c in probe[qi].tolist()]
+            spans.append((self._trained_n, self._n))  # un-grouped tail
+            for lo, hi in spans:
+                if hi > lo:
+                    v, i = super().search(Q[qi:qi + 1], min(k, hi - lo), rows=(lo, hi))
+                    cand_v.append(v)
+                    cand_i.append(i)
+            v = torch.cat(cand_v, 1)
+            i = torch.cat(cand_i, 1)
+            top = torch.topk(v, min(k, v.shape[1]), dim=1)
+            vs.append(top.values)
+            is_.append(torch.gather(i, 1, top.indices))
+        kk = min(x.shape[1] for x in vs)
+        return torch.cat([x[:, :kk] for x in vs]), torch.cat([x[:, :kk] for x in is_])
+
+
+def create_vector_store(cfg=None, **overrides) -> VectorStore:
+    name = getattr(cfg, "driver_name", cfg) or "hip"
+    kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
+    kw.update(overrides)
+    if name == "hip":
+        if kw.get("index_type", "flat") == "ivf":
+            return HipIVFIndex(**kw)
+        return HipFlatIndex(**kw)
+    if name == "faiss":
+        # FAISS parity (IndexFlatL2 semantics, score = 1/(1+d)) on the HIP index
+        kw.setdefault("distance", "l2")
+        return HipFlatIndex(faiss_scores=True, **kw) if kw.get("index_type", "flat") == "flat" else \
+            HipIVFIndex(faiss_scores=True, **kw)
+    if name == "inmemory":
+        return InMemoryVectorStore(**kw)
+    if name in ("qdrant", "azure_ai_search"):
+        raise ImportError(f"vector_store driver {name!r} needs an external service client not in this image; "
+                          "use VECTOR_STORE_TYPE=hip (HBM-resident index)")
+    raise ValueError(f"unknown vector_store driver {name!r}")

@@ -1,0 +1,45 @@
+"""BASELINE config 1 on CPU: parse -> chunk -> embed -> index -> select -> prompt -> generate -> report."""
+
+from copilot_for_consensus_amd.contracts import ids as cids
+from copilot_for_consensus_amd.contracts.registry import default_provider
+from copilot_for_consensus_amd.bus import NoopPublisher
+from copilot_for_consensus_amd.models.decoder import DecoderModel, DecoderWeights, get_config
+from copilot_for_consensus_amd.pipeline.rag import RagPipeline
+from copilot_for_consensus_amd.runtime.engine import LLMEngine
+from copilot_for_consensus_amd.runtime.kv_cache import PagedKVCache
+
+
+def test_rag_pipeline_end_to_end_cpu():
+    pub = NoopPublisher()
+    rag = RagPipeline(encoder="tiny", device="cpu", decoder_vocab=512, seed=3, index_prefill=200, publisher=pub)
+    rag.prepare_sources(3, [0])
+    batch = rag.prepare(3, 0)
+    assert len(batch.threads) == 3 and len(batch.prompts) == 3
+    for sel in batch.selections:
+        assert 1 <= len(sel.selected_chunks) <= 5
+        assert sel.total_tokens <= 2048
+    # prompts contain the excerpts and all placeholders were substituted
+    assert all("{" not in p.split("Most relevant excerpts:")[0][-200:] for p in batch.prompt_texts)
+    assert all("Message 1:" in p for p in batch.prompt_texts)
+    cfg = get_config("tiny")
+    eng = LLMEngine(DecoderModel(DecoderWeights.random(cfg, "cpu", seed=0)),
+                    PagedKVCache(cfg.layers, 2048 // 32 * 3 + 256, cfg.kv_heads, cfg.head_dim, "cpu"))
+    prompts = [p[:200] for p in batch.prompts]  # tiny model: clip prompts to keep CPU time low
+    res = eng.generate(prompts, 4, ignore_eos=True)
+    reports = rag.finish(batch, res)
+    assert len(reports) == 3
+    sp = default_provider()
+    types = [e["event_type"] for e in pub.get_events()]
+    for t in ("ArchiveIngested", "JSONParsed", "ChunksPrepared", "EmbeddingsGenerated", "SummarizationRequested",
+              "SummaryComplete", "ReportPublished"):
+        assert t in types, t
+    for e in pub.get_events():
+        assert sp.validate_event(e) == [], e["event_type"]
+    # ids follow the reference derivations
+    sc = pub.get_events("SummaryComplete")[0]["data"]
+    assert sc["summary_id"] == cids.summary_id(sc["thread_id"], [c["chunk_id"] for c in sc["citations"]])
+    rep = rag.docs.get_document("summaries", cids.report_id(sc["summary_id"]))
+    assert rep is not None and rep["thread_id"] == sc["thread_id"]
+    th = rag.docs.get_document("threads", sc["thread_id"])
+    assert th["summary_id"] == rep["_id"]
+    assert rag.docs.count_documents("chunks", {"embedding_generated": False}) == 0
