@@ -1,0 +1,308 @@
+"""Logging, metrics, error reporting and tracing spans.
+
+* Logger (adapters/copilot_logging): ``StdoutLogger`` emits one JSON object per line
+  (timestamp, level, logger, message, **kv) -- stdout_logger.py:64-93; ``SilentLogger``.
+* MetricsCollector (adapters/copilot_metrics base.py:20-64): increment / observe / gauge /
+  safe_push.  ``PrometheusMetricsCollector`` keeps counters, gauges and histograms in-process and
+  renders the Prometheus text exposition format (services can serve ``/metrics`` -- the reference
+  only pushes); ``PushGatewayMetricsCollector`` PUTs that text to a Pushgateway; ``NoOp``.
+  Metric names are the reference's (``<svc>_event_retry_*``, ``embedding_generation_duration_seconds``,
+  ``summarization_latency_seconds`` ...).  GPU metrics (tokens/s, TTFT, HBM) are gauges here.
+* ErrorReporter (adapters/copilot_error_reporting): console / silent / sentry(optional).
+* ``span`` -- a timing context manager recorded into a histogram and, on a GPU, bracketed with a
+  roctx range when the ROCm tracer is importable (rocprofv3 --marker-trace shows pipeline stages).
+"""
+from __future__ import annotations
+
+import collections
+import contextlib
+import json
+import logging
+import sys
+import threading
+import time
+import traceback
+import urllib.request
+from abc import ABC, abstractmethod
+from datetime import datetime, timezone
+from typing import Any
+
+# ------------------------------------------------------------------------------------- logging
+
+_LEVELS = {"DEBUG": 10, "INFO": 20, "WARNING": 30, "ERROR": 40, "CRITICAL": 50}
+
+
+class Logger(ABC):
+    @abstractmethod
+    def log(self, level: str, message: str, **kw) -> None: ...
+
+    def debug(self, m, **kw): self.log("DEBUG", m, **kw)
+    def info(self, m, **kw): self.log("INFO", m, **kw)
+    def warning(self, m, **kw): self.log("WARNING", m, **kw)
+    def error(self, m, **kw): self.log("ERROR", m, **kw)
+
+    def exception(self, m, **kw):
+        kw["traceback"] = traceback.format_exc()
+        self.log("ERROR", m, **kw)
+
+
+class StdoutLogger(Logger):
+    def __init__(self, level: str = "INFO", name: str | None = None, stream=None, **_):
+        self.level = _LEVELS.get(str(level).upper(), 20)
+        self.name = name or "copilot"
+        self.stream = stream or sys.stdout
+        self._lock = threading.Lock()
+
+    def log(self, level, message, **kw):
+        if _LEVELS.get(level, 20) < self.level:
+            return
+        rec = {"timestamp": datetime.now(timezone.utc).isoformat().replace("+00:00", "Z"), "level": level,
+               "logger": self.name, "message": message}
+        for k, v in kw.items():
+            rec[k] = v if isinstance(v, (str, int, float, bool, type(None), list, dict)) else repr(v)
+        line = json.dumps(rec, default=str)
+        with self._lock:
+            self.stream.write(line + "\n")
+            self.stream.flush()
+
+
+class SilentLogger(Logger):
+    def __init__(self, **_):
+        self.records: list[tuple[str, str, dict]] = []
+
+    def log(self, level, message, **kw):
+        if len(self.records) < 10000:
+            self.records.append((level, message, kw))
+
+
+_default_logger: Logger | None = None
+
+
+def create_logger(cfg=None, **overrides) -> Logger:
+    name = getattr(cfg, "driver_name", cfg) or "stdout"
+    kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
+    kw.update(overrides)
+    return {"stdout": StdoutLogger, "silent": SilentLogger}[name](**kw)
+
+
+def set_default_logger(lg: Logger) -> None:
+    global _default_logger
+    _default_logger = lg
+
+
+def get_logger(name: str | None = None) -> Logger:
+    return _default_logger or StdoutLogger(name=name)
+
+
+def uvicorn_log_config(level: str = "INFO") -> dict:
+    """uvicorn dictConfig emitting JSON lines (reference copilot_logging/uvicorn_config.py)."""
+    fmt = '{"timestamp":"%(asctime)s","level":"%(levelname)s","logger":"%(name)s","message":"%(message)s"}'
+    return {"version": 1, "disable_existing_loggers": False,
+            "formatters": {"json": {"format": fmt}},
+            "handlers": {"default": {"class": "logging.StreamHandler", "formatter": "json", "stream": "ext://sys.stdout"}},
+            "loggers": {"uvicorn": {"handlers": ["default"], "level": level},
+                        "uvicorn.access": {"handlers": ["default"], "level": level, "propagate": False}}}
+
+
+# ------------------------------------------------------------------------------------- metrics
+
+def _key(name, tags):
+    return (name, tuple(sorted((tags or {}).items())))
+
+
+DEFAULT_BUCKETS = (0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1, 2.5, 5, 10, 30, 60, 120, 300)
+
+
+class MetricsCollector(ABC):
+    @abstractmethod
+    def increment(self, name: str, value: float = 1.0, tags: dict | None = None) -> None: ...
+
+    @abstractmethod
+    def observe(self, name: str, value: float, tags: dict | None = None) -> None: ...
+
+    @abstractmethod
+    def gauge(self, name: str, value: float, tags: dict | None = None) -> None: ...
+
+    def push(self) -> None:
+        pass
+
+    def safe_push(self) -> None:
+        try:
+            self.push()
+        except Exception:  # metrics must never break the pipeline
+            pass
+
+
+class NoOpMetricsCollector(MetricsCollector):
+    def __init__(self, **_):
+        pass
+
+    def increment(self, name, value=1.0, tags=None): pass
+    def observe(self, name, value, tags=None): pass
+    def gauge(self, name, value, tags=None): pass
+
+
+class PrometheusMetricsCollector(MetricsCollector):
+    def __init__(self, namespace: str = "copilot", raise_on_error: bool = False, buckets=DEFAULT_BUCKETS, **_):
+        self.namespace = namespace
+        self.buckets = tuple(buckets)
+        self._lock = threading.Lock()
+        self.counters: dict = collections.defaultdict(float)
+        self.gauges: dict = {}
+        self.hist: dict = {}
+
+    def _n(self, name):
+        return f"{self.namespace}_{name}" if self.namespace and not name.startswith(self.namespace + "_") else name
+
+    def increment(self, name, value=1.0, tags=None):
+        with self._lock:
+            self.counters[_key(self._n(name), tags)] += value
+
+    def gauge(self, name, value, tags=None):
+        with self._lock:
+            self.gauges[_key(self._n(name), tags)] = float(value)
+
+    def observe(self, name, value, tags=None):
+        with self._lock:
+            k = _key(self._n(name), tags)
+            h = self.hist.get(k)
+            if h is None:
+                h = self.hist[k] = [[0] * len(self.buckets), 0.0, 0]
+            for i, b in enumerate(self.buckets):
+                if value <= b:
+                    h[0][i] += 1
+            h[1] += value
+            h[2] += 1
+
+    def get_counter(self, name, tags=None) -> float:
+        return self.counters.get(_key(self._n(name), tags), 0.0)
+
+    @staticmethod
+    def _labels(tags, extra=None):
+        items = list(tags) + (extra or [])
+        return "{" + ",".join(f'{k}="{v}"' for k, v in items) + "}" if items else ""
+
+    def render(self) -> str:
+        """Prometheus text exposition format 0.0.4."""
+        out = []
+        with self._lock:
+            for (n, t), v in sorted(self.counters.items()):
+                out.append(f"{n}{self._labels(t)} {v}")
+            for (n, t), v in sorted(self.gauges.items()):
+                out.append(f"{n}{self._labels(t)} {v}")
+            for (n, t), (counts, s, c) in sorted(self.hist.items()):
+                for b, cnt in zip(self.buckets, counts):
+                    out.append(f"{n}_bucket{self._labels(t, [('le', b)])} {cnt}")
+                out.append(f"{n}_bucket{self._labels(t, [('le', '+Inf')])} {c}")
+                out.append(f"{n}_sum{self._labels(t)} {s}")
+                out.append(f"{n}_count{self._labels(t)} {c}")
+        return "\n".join(out) + "\n"
+
+
+class PushGatewayMetricsCollector(PrometheusMetricsCollector):
+    def __init__(self, gateway: str | None = None, job: str = "copilot", namespace: str = "copilot",
+                 raise_on_error: bool = False, grouping_key: dict | None = None, **_):
+        super().__init__(namespace)
+        self.gateway, self.job = gateway, job
+        self.grouping_key = grouping_key or {}
+        self.raise_on_error = raise_on_error
+
+    def push(self):
+        if not self.gateway:
+            return
+        url = self.gateway.rstrip("/")
+        if not url.startswith("http"):
+            url = "http://" + url
+        url += f"/metrics/job/{self.job}" + "".join(f"/{k}/{v}" for k, v in self.grouping_key.items())
+        req = urllib.request.Request(url, data=self.render().encode(), method="PUT",
+                                     headers={"Content-Type": "text/plain; version=0.0.4"})
+        try:
+            urllib.request.urlopen(req, timeout=5).read()
+        except Exception:
+            if self.raise_on_error:
+                raise
+
+
+def create_metrics_collector(cfg=None, **overrides) -> MetricsCollector:
+    name = getattr(cfg, "driver_name", cfg) or "noop"
+    kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
+    kw.update(overrides)
+    if name == "noop":
+        return NoOpMetricsCollector()
+    if name == "prometheus":
+        return PrometheusMetricsCollector(**kw)
+    if name == "pushgateway":
+        return PushGatewayMetricsCollector(**kw)
+    if name == "azure_monitor":
+        raise ImportError("azure_monitor metrics need the OpenTelemetry Azure exporter (not in this image)")
+    raise ValueError(f"unknown metrics driver {name!r}")
+
+
+# ------------------------------------------------------------------------------ error reporting
+
+class ErrorReporter(ABC):
+    @abstractmethod
+    def report(self, error: BaseException, context: dict | None = None) -> None: ...
+
+    def capture_message(self, message: str, level: str = "error", context: dict | None = None) -> None:
+        self.report(RuntimeError(message), context)
+
+
+class ConsoleErrorReporter(ErrorReporter):
+    def __init__(self, logger_name: str | None = None, logger: Logger | None = None, **_):
+        self.logger = logger or StdoutLogger(name=logger_name or "errors", stream=sys.stderr)
+        self.reported: list[tuple[BaseException, dict]] = []
+
+    def report(self, error, context=None):
+        self.reported.append((error, dict(context or {})))
+        self.logger.error(f"{type(error).__name__}: {error}", context=context or {})
+
+
+class SilentErrorReporter(ErrorReporter):
+    def __init__(self, **_):
+        self.reported: list[tuple[BaseException, dict]] = []
+
+    def report(self, error, context=None):
+        self.reported.append((error, dict(context or {})))
+
+
+def create_error_reporter(cfg=None, **overrides) -> ErrorReporter:
+    name = getattr(cfg, "driver_name", cfg) or "console"
+    kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
+    kw.update(overrides)
+    if name == "console":
+        return ConsoleErrorReporter(**kw)
+    if name == "silent":
+        return SilentErrorReporter()
+    if name == "sentry":
+        raise ImportError("sentry error reporting needs sentry-sdk (not in this image)")
+    raise ValueError(f"unknown error reporter {name!r}")
+
+
+# ------------------------------------------------------------------------------------- tracing
+
+try:  # pragma: no cover - only on ROCm builds that ship roctx python bindings
+    from roctx import rangePop as _rpop, rangePush as _rpush  # type: ignore
+except Exception:  # noqa: BLE001
+    _rpush = _rpop = None
+
+
+@contextlib.contextmanager
+def span(name: str, metrics: MetricsCollector | None = None, tags: dict | None = None, sync_device=None):
+    """Time a pipeline stage; observes ``<name>_duration_seconds`` and marks a roctx range."""
+    if _rpush:
+        _rpush(name)
+    t = time.perf_counter()
+    try:
+        yield
+    finally:
+        if sync_device is not None:
+            import torch
+            torch.cuda.synchronize(sync_device)
+        if metrics is not None:
+            metrics.observe(f"{name}_duration_seconds", time.perf_counter() - t, tags)
+        if _rpop:
+            _rpop()
+
+
+del logging

@@ -1,0 +1,281 @@
+"""JWT signing/verification without third-party crypto (PyJWT / cryptography are not in the image).
+
+Reference: adapters/copilot_jwt_signer (LocalJWTSigner RSA/EC/HMAC, local_signer.py:214-271) and
+copilot_auth/jwt_manager.py (mint :154, validate :265, JWKS :322).
+
+* HS256 -- stdlib ``hmac``.
+* RS256 -- RSASSA-PKCS1-v1_5 with SHA-256 implemented on Python integers: key generation
+  (Miller-Rabin primes, e = 65537), CRT signing, public verification, JWK / JWKS export
+  (``kty=RSA, n, e, kid``) so services can verify tokens from the auth service's JWKS exactly as
+  with the reference.  (Timing side channels are out of scope for this signer; use the
+  key-vault signer in hostile environments.)
+"""
+from __future__ import annotations
+
+import base64
+import hashlib
+import hmac
+import json
+import secrets as _secrets
+import time
+import uuid
+from abc import ABC, abstractmethod
+from typing import Any
+
+
+class JWTError(ValueError):
+    pass
+
+
+def b64u(b: bytes) -> str:
+    return base64.urlsafe_b64encode(b).rstrip(b"=").decode()
+
+
+def b64u_dec(s: str) -> bytes:
+    return base64.urlsafe_b64decode(s + "=" * (-len(s) % 4))
+
+
+def _int_to_b(n: int, length: int | None = None) -> bytes:
+    length = length or max(1, (n.bit_length() + 7) // 8)
+    return n.to_bytes(length, "big")
+
+
+# ------------------------------------------------------------------------------------ RSA math
+
+_SMALL_PRIMES = [p for p in range(3, 2000, 2) if all(p % q for q in range(3, int(p ** 0.5) + 1, 2))]
+
+
+def _is_probable_prime(n: int, rounds: int = 40) -> bool:
+    if n < 2:
+        return False
+    for p in _SMALL_PRIMES:
+        if n % p == 0:
+            return n == p
+    d, r = n - 1, 0
+    while d % 2 == 0:
+        d //= 2
+        r += 1
+    for _ in range(rounds):
+        a = _secrets.randbelow(n - 3) + 2
+        x = pow(a, d, n)
+        if x in (1, n - 1):
+            continue
+        for _ in range(r - 1):
+            x = pow(x, 2, n)
+            if x == n - 1:
+                break
+        else:
+            return False
+    return True
+
+
+def _gen_prime(bits: int) -> int:
+    while True:
+        c = _secrets.randbits(bits) | (1 << (bits - 1)) | (1 << (bits - 2)) | 1
+        if _is_probable_prime(c):
+            return c
+
+
+class RSAKey:
+    def __init__(self, n: int, e: int, d: int | None = None, p: int | None = None, q: int | None = None):
+        self.n, self.e, self.d, self.p, self.q = n, e, d, p, q
+        self.size = (n.bit_length() + 7) // 8
+        if p and q and d:
+            self.dp, self.dq, self.qinv = d % (p - 1), d % (q - 1), pow(q, -1, p)
+
+    @classmethod
+    def generate(cls, bits: int = 2048, e: int = 65537) -> "RSAKey":
+        while True:
+            p, q = _gen_prime(bits // 2), _gen_prime(bits // 2)
+            if p == q:
+                continue
+            phi = (p - 1) * (q - 1)
+            try:
+                d = pow(e, -1, phi)
+            except ValueError:
+                continue
+            return cls(p * q, e, d, p, q)
+
+    _SHA256_PREFIX = bytes.fromhex("3031300d060960864801650304020105000420")
+
+    def _emsa(self, msg: bytes) -> int:
+        t = self._SHA256_PREFIX + hashlib.sha256(msg).digest()
+        em = b"\x00\x01" + b"\xff" * (self.size - len(t) - 3) + b"\x00" + t
+        return int.from_bytes(em, "big")
+
+    def sign(self, msg: bytes) -> bytes:
+        if self.d is None:
+            raise JWTError("private key required")
+        m = self._emsa(msg)
+        if self.p:
+            s1, s2 = pow(m, self.dp, self.p), pow(m, self.dq, self.q)
+            s = s2 + self.q * ((self.qinv * (s1 - s2)) % self.p)
+        else:
+            s = pow(m, self.d, self.n)
+        return _int_to_b(s, self.size)
+
+    def verify(self, msg: bytes, sig: bytes) -> bool:
+        if len(sig) != self.size:
+            return False
+        return pow(int.from_bytes(sig, "big"), self.e, self.n) == self._emsa(msg)
+
+    def public_jwk(self, kid: str) -> dict:
+        return {"kty": "RSA", "use": "sig", "alg": "RS256", "kid": kid, "n": b64u(_int_to_b(self.n)),
+                "e": b64u(_int_to_b(self.e))}
+
+    @classmethod
+    def from_jwk(cls, jwk: dict) -> "RSAKey":
+        return cls(int.from_bytes(b64u_dec(jwk["n"]), "big"), int.from_bytes(b64u_dec(jwk["e"]), "big"))
+
+    def private_json(self) -> str:
+        return json.dumps({k: hex(getattr(self, k)) for k in ("n", "e", "d", "p", "q")})
+
+    @classmethod
+    def from_private_json(cls, s: str) -> "RSAKey":
+        d = {k: int(v, 16) for k, v in json.loads(s).items()}
+        return cls(d["n"], d["e"], d["d"], d.get("p"), d.get("q"))
+
+
+# ------------------------------------------------------------------------------------ signers
+
+class JWTSigner(ABC):
+    algorithm: str
+    key_id: str
+
+    @abstractmethod
+    def sign(self, message: bytes) -> bytes: ...
+
+    @abstractmethod
+    def verify(self, message: bytes, signature: bytes) -> bool: ...
+
+    def get_public_key_jwk(self) -> dict | None:
+        return None
+
+    def health_check(self) -> bool:
+        return True
+
+
+class HMACSigner(JWTSigner):
+    algorithm = "HS256"
+
+    def __init__(self, secret_key: str | bytes | None = None, key_id: str = "default", **_):
+        if not secret_key:
+            secret_key = _secrets.token_hex(32)
+        self.key = secret_key.encode() if isinstance(secret_key, str) else secret_key
+        self.key_id = key_id
+
+    def sign(self, message):
+        return hmac.new(self.key, message, hashlib.sha256).digest()
+
+    def verify(self, message, signature):
+        return hmac.compare_digest(self.sign(message), signature)
+
+
+class RSASigner(JWTSigner):
+    algorithm = "RS256"
+
+    def __init__(self, private_key: str | RSAKey | None = None, key_id: str = "default", bits: int = 2048, **_):
+        if isinstance(private_key, RSAKey):
+            self.key = private_key
+        elif private_key:
+            self.key = RSAKey.from_private_json(private_key)
+        else:
+            self.key = RSAKey.generate(bits)
+        self.key_id = key_id
+
+    def sign(self, message):
+        return self.key.sign(message)
+
+    def verify(self, message, signature):
+        return self.key.verify(message, signature)
+
+    def get_public_key_jwk(self):
+        return self.key.public_jwk(self.key_id)
+
+
+def create_jwt_signer(cfg=None, **overrides) -> JWTSigner:
+    kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
+    kw.update(overrides)
+    alg = str(kw.pop("algorithm", "HS256")).upper()
+    if alg == "HS256":
+        return HMACSigner(**kw)
+    if alg == "RS256":
+        return RSASigner(**kw)
+    raise JWTError(f"unsupported JWT algorithm {alg}")
+
+
+# ------------------------------------------------------------------------------------ tokens
+
+def encode(claims: dict, signer: JWTSigner) -> str:
+    header = {"alg": signer.algorithm, "typ": "JWT", "kid": signer.key_id}
+    signing_input = f"{b64u(json.dumps(header, separators=(',', ':')).encode())}." \
+                    f"{b64u(json.dumps(claims, separators=(',', ':')).encode())}"
+    return f"{signing_input}.{b64u(signer.sign(signing_input.encode()))}"
+
+
+def decode_unverified(token: str) -> tuple[dict, dict]:
+    try:
+        h, p, _ = token.split(".")
+        return json.loads(b64u_dec(h)), json.loads(b64u_dec(p))
+    except Exception as e:
+        raise JWTError("malformed token") from e
+
+
+def decode(token: str, verify_key, audience: str | list[str] | None = None, issuer: str | None = None,
+           leeway: int = 90, now: float | None = None) -> dict:
+    """Verify signature (a signer, an RSAKey, or a JWKS dict) and registered claims."""
+    header, claims = decode_unverified(token)
+    h, p, s = token.split(".")
+    msg = f"{h}.{p}".encode()
+    sig = b64u_dec(s)
+    alg = header.get("alg")
+    if isinstance(verify_key, dict) and "keys" in verify_key:
+        jwk = next((k for k in verify_key["keys"] if k.get("kid") == header.get("kid")), None)
+        if jwk is None:
+            raise JWTError("unknown kid")
+        verify_key = RSAKey.from_jwk(jwk)
+    if isinstance(verify_key, RSAKey):
+        ok = alg == "RS256" and verify_key.verify(msg, sig)
+    elif isinstance(verify_key, JWTSigner):
+        ok = alg == verify_key.algorithm and verify_key.verify(msg, sig)
+    else:
+        raise JWTError("no verification key")
+    if not ok:
+        raise JWTError("invalid signature")
+    now = time.time() if now is None else now
+    if "exp" in claims and now > claims["exp"] + leeway:
+        raise JWTError("token expired")
+    if "nbf" in claims and now < claims["nbf"] - leeway:
+        raise JWTError("token not yet valid")
+    if audience is not None:
+        aud = claims.get("aud")
+        auds = aud if isinstance(aud, list) else [aud]
+        want = audience if isinstance(audience, list) else [audience]
+        if not set(auds) & set(want):
+            raise JWTError("audience mismatch")
+    if issuer is not None and claims.get("iss") != issuer:
+        raise JWTError("issuer mismatch")
+    return claims
+
+
+class JWTManager:
+    """Mints service tokens and publishes the JWKS (copilot_auth/jwt_manager.py:35)."""
+
+    def __init__(self, signer: JWTSigner, issuer: str = "copilot-auth", audience: str = "copilot-for-consensus",
+                 default_expiry: int = 1800):
+        self.signer, self.issuer, self.audience, self.default_expiry = signer, issuer, audience, default_expiry
+
+    def mint_token(self, subject: str, claims: dict | None = None, expires_in: int | None = None,
+                   audience: str | None = None) -> str:
+        now = int(time.time())
+        c: dict[str, Any] = {"iss": self.issuer, "sub": subject, "aud": audience or self.audience, "iat": now,
+                             "nbf": now, "exp": now + int(expires_in or self.default_expiry), "jti": str(uuid.uuid4())}
+        c.update(claims or {})
+        return encode(c, self.signer)
+
+    def validate_token(self, token: str, audience: str | None = None, max_skew: int = 90) -> dict:
+        return decode(token, self.signer, audience=audience or self.audience, issuer=self.issuer, leeway=max_skew)
+
+    def get_jwks(self) -> dict:
+        jwk = self.signer.get_public_key_jwk()
+        return {"keys": [jwk] if jwk else []}
