@@ -30,7 +30,7 @@ BASELINE_THREADS_PER_S = 1.0 / 3.0
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="mistral-7b")
     ap.add_argument("--encoder", default="minilm-l6")
@@ -41,6 +41,7 @@ def parse_args(argv=None):
     ap.add_argument("--llm-only", action="store_true", help="skip the CPU/encoder/kNN stages (diagnostic)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-overlap", action="store_true", help="run pipeline stages strictly sequentially")
     return ap.parse_args(argv)
 
 
@@ -72,21 +73,19 @@ def main(argv=None):
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    for i in range(args.warmup):
-        t = time.perf_counter()
-        r = pipe.run_step(i)
+    t = time.perf_counter()
+    for i, r in enumerate(pipe.run_steps(list(range(args.warmup)), overlap=not args.no_overlap)):
         if rank == 0:
-            print(f"[bench] warmup {i}: {time.perf_counter() - t:.2f}s {r.summary()}", file=sys.stderr, flush=True)
+            print(f"[bench] warmup {i}: {r.summary()}", file=sys.stderr, flush=True)
 
     barrier()
     t0 = time.perf_counter()
-    results = []
-    for i in range(args.steps):
-        results.append(pipe.run_step(args.warmup + i))
-        if rank == 0:
-            print(f"[bench] step {i}: {results[-1].summary()}", file=sys.stderr, flush=True)
+    results = pipe.run_steps(list(range(args.warmup, args.warmup + args.steps)), overlap=not args.no_overlap)
     barrier()
     elapsed = time.perf_counter() - t0
+    if rank == 0:
+        for i, r in enumerate(results):
+            print(f"[bench] step {i}: {r.summary()}", file=sys.stderr, flush=True)
 
     threads_local = sum(r.threads for r in results)
     lat_local = [x for r in results for x in r.latencies_s]

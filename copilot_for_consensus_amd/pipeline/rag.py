@@ -47,7 +47,8 @@ class PreparedBatch:
 class RagPipeline:
     def __init__(self, encoder: str = "minilm-l6", device="cuda", decoder_vocab: int = 32000, bos_id: int = 1,
                  seed: int = 0, top_k: int = 5, context_window_tokens: int = 2048, index_prefill: int = 1_000_000,
-                 publisher=None, validate_events: bool = True, llm_model: str = "mistral-7b"):
+                 publisher=None, validate_events: bool = True, llm_model: str = "mistral-7b",
+                 max_prompt_tokens: int | None = None):
         from ..embedding import HipEncoderProvider
         from ..runtime.tokenizer import synthetic_bpe
         from ..vectorstore import HipFlatIndex
@@ -76,6 +77,7 @@ class RagPipeline:
         self.generator = SyntheticArchive(seed=seed)
         self.sources: dict[int, bytes] = {}
         self.llm_model = llm_model
+        self.max_prompt_tokens = max_prompt_tokens
 
     # ------------------------------------------------------------------ data source
     def prepare_sources(self, n_threads: int, steps: list[int]) -> None:
@@ -201,9 +203,17 @@ class RagPipeline:
         st["select"] = time.perf_counter() - t
 
         t = time.perf_counter()
-        prompts = [self.bpe.encode(p) for p in texts]
+        prompts = [self._clip(self.bpe.encode(p)) for p in texts]
         st["tokenize"] = time.perf_counter() - t
         return PreparedBatch(prepared_threads, prompts, texts, sels, ctxs, st, aid)
+
+    def _clip(self, ids: list[int]) -> list[int]:
+        """Keep the instructions (head) and the latest excerpts (tail) if a prompt exceeds the context."""
+        L = self.max_prompt_tokens
+        if L is None or len(ids) <= L:
+            return ids
+        half = L // 2
+        return ids[:half] + ids[-(L - half):]
 
     def finish(self, batch: PreparedBatch, gen) -> list[dict]:
         """Detokenise, build citations + ids, persist summaries, update threads, emit events."""
