@@ -48,6 +48,8 @@ class BenchPipeline:
         self.engine = LLMEngine(self.model, self.kv, max_prefill_tokens=prefill_tokens, use_graph=use_graph)
         self.rag = None
         self.side_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self._last_gen_s: float | None = None
+        self._last_prep_s = 0.0
         if not llm_only:
             from ..bus import CountingPublisher
             from .rag import RagPipeline
@@ -70,7 +72,13 @@ class BenchPipeline:
             out.append([self.cfg.bos_id] + [self.rng.randrange(3, self.cfg.vocab_size) for _ in range(L - 1)])
         return out
 
-    def _prepare(self, step: int):
+    def _prepare(self, step: int, not_before: float | None = None):
+        if not_before is not None:
+            # just-in-time: start this batch's CPU/encoder work so it completes as the running
+            # LLM batch drains -- overlapped, but the threads do not queue behind a whole batch
+            delay = not_before - time.perf_counter()
+            if delay > 0:
+                time.sleep(delay)
         t0 = time.perf_counter()
         if self.rag is None:
             return t0, None, self._synthetic_prompts(self.threads_per_step), {}
@@ -96,8 +104,16 @@ class BenchPipeline:
         try:
             for n, step in enumerate(steps):
                 t0, ctx, prompts, stages = pending
-                fut = pool.submit(self._prepare, steps[n + 1]) if (pool and n + 1 < len(steps)) else None
+                fut = None
+                if pool and n + 1 < len(steps):
+                    start_at = None
+                    if self._last_gen_s is not None:
+                        start_at = time.perf_counter() + max(0.0, self._last_gen_s - 2.0 * self._last_prep_s - 0.25)
+                    fut = pool.submit(self._prepare, steps[n + 1], start_at)
+                tg = time.perf_counter()
                 res = self.engine.generate(prompts, self.max_new, temperature=0.0, ignore_eos=True)
+                self._last_gen_s = time.perf_counter() - tg
+                self._last_prep_s = sum(v for k, v in stages.items())
                 stages["prefill"] = res.prefill_s
                 stages["decode"] = res.decode_s
                 t2 = time.perf_counter()

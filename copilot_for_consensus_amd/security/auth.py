@@ -1,0 +1,259 @@
+"""Authentication: OIDC identity providers (PKCE + nonce), role store, service JWT middleware.
+
+Reference: adapters/copilot_auth (OIDCProvider oidc_provider.py:23 with PKCE :360; GitHub / Google /
+Microsoft / Mock providers; JWTMiddleware middleware.py:52 with JWKS fetch :122-270 and role check
+:424), auth/app/service.py:171 (initiate_login :398, handle_callback :471, validate_token :583,
+get_jwks :625) and auth/app/role_store.py:28.
+"""
+from __future__ import annotations
+
+import base64
+import hashlib
+import json
+import secrets
+import threading
+import time
+import urllib.parse
+import urllib.request
+from abc import ABC, abstractmethod
+from typing import Any
+
+from .jwt import JWTError, JWTManager, decode
+
+
+def pkce_pair() -> tuple[str, str]:
+    verifier = base64.urlsafe_b64encode(secrets.token_bytes(32)).rstrip(b"=").decode()
+    challenge = base64.urlsafe_b64encode(hashlib.sha256(verifier.encode()).digest()).rstrip(b"=").decode()
+    return verifier, challenge
+
+
+class IdentityProvider(ABC):
+    name = "base"
+
+    @abstractmethod
+    def authorization_url(self, state: str, nonce: str, code_challenge: str) -> str: ...
+
+    @abstractmethod
+    def exchange_code(self, code: str, code_verifier: str, nonce: str) -> dict:
+        """-> user info {sub, email, name, provider}."""
+
+
+class OIDCProvider(IdentityProvider):
+    def __init__(self, name: str, client_id: str, client_secret: str, redirect_uri: str, authorize_endpoint: str,
+                 token_endpoint: str, userinfo_endpoint: str, scope: str = "openid email profile"):
+        self.name = name
+        self.client_id, self.client_secret, self.redirect_uri = client_id, client_secret, redirect_uri
+        self.authorize_endpoint, self.token_endpoint = authorize_endpoint, token_endpoint
+        self.userinfo_endpoint, self.scope = userinfo_endpoint, scope
+
+    def authorization_url(self, state, nonce, code_challenge):
+        q = {"response_type": "code", "client_id": self.client_id, "redirect_uri": self.redirect_uri,
+             "scope": self.scope, "state": state, "nonce": nonce, "code_challenge": code_challenge,
+             "code_challenge_method": "S256"}
+        return f"{self.authorize_endpoint}?{urllib.parse.urlencode(q)}"
+
+    def _post(self, url, data):
+        req = urllib.request.Request(url, data=urllib.parse.urlencode(data).encode(),
+                                     headers={"Accept": "application/json"})
+        return json.loads(urllib.request.urlopen(req, timeout=15).read())
+
+    def _get(self, url, token):
+        req = urllib.request.Request(url, headers={"Authorization": f"Bearer {token}", "Accept": "application/json"})
+        return json.loads(urllib.request.urlopen(req, timeout=15).read())
+
+    def exchange_code(self, code, code_verifier, nonce):
+        tok = self._post(self.token_endpoint, {"grant_type": "authorization_code", "code": code,
+                                               "redirect_uri": self.redirect_uri, "client_id": self.client_id,
+                                               "client_secret": self.client_secret, "code_verifier": code_verifier})
+        info = self._get(self.userinfo_endpoint, tok["access_token"])
+        return {"sub": f"{self.name}:{info.get('sub') or info.get('id')}", "email": info.get("email"),
+                "name": info.get("name") or info.get("login"), "provider": self.name}
+
+
+def github_provider(github_client_id, github_client_secret, github_redirect_uri=None,
+                    github_api_base_url="https://api.github.com", **_):
+    return OIDCProvider("github", github_client_id, github_client_secret, github_redirect_uri or "",
+                        "https://github.com/login/oauth/authorize", "https://github.com/login/oauth/access_token",
+                        f"{github_api_base_url}/user", scope="read:user user:email")
+
+
+def google_provider(google_client_id, google_client_secret, google_redirect_uri=None, **_):
+    return OIDCProvider("google", google_client_id, google_client_secret, google_redirect_uri or "",
+                        "https://accounts.google.com/o/oauth2/v2/auth", "https://oauth2.googleapis.com/token",
+                        "https://openidconnect.googleapis.com/v1/userinfo")
+
+
+def microsoft_provider(microsoft_client_id, microsoft_client_secret, microsoft_redirect_uri=None,
+                       microsoft_tenant="common", **_):
+    base = f"https://login.microsoftonline.com/{microsoft_tenant}/oauth2/v2.0"
+    return OIDCProvider("microsoft", microsoft_client_id, microsoft_client_secret, microsoft_redirect_uri or "",
+                        f"{base}/authorize", f"{base}/token", "https://graph.microsoft.com/oidc/userinfo")
+
+
+class MockIdentityProvider(IdentityProvider):
+    """Deterministic provider for tests/dev (reference mock_provider.py:15): any code logs in the
+    user whose id is the code."""
+    name = "mock"
+
+    def authorization_url(self, state, nonce, code_challenge):
+        return f"/auth/callback?provider=mock&state={state}&code=mock-user"
+
+    def exchange_code(self, code, code_verifier, nonce):
+        return {"sub": f"mock:{code}", "email": f"{code}@example.com", "name": code, "provider": "mock"}
+
+
+class RoleStore:
+    """user -> roles with pending approvals (auth/app/role_store.py:28), persisted in a collection."""
+
+    def __init__(self, document_store, collection: str = "user_roles", auto_approve_roles: list[str] | None = None,
+                 first_user_auto_promotion: bool = False):
+        self.store, self.coll = document_store, collection
+        self.auto_roles = auto_approve_roles or []
+        self.first_user_admin = first_user_auto_promotion
+        self._lock = threading.Lock()
+
+    def get(self, user_id: str) -> dict | None:
+        return self.store.get_document(self.coll, user_id)
+
+    def ensure_user(self, user: dict) -> dict:
+        with self._lock:
+            doc = self.get(user["sub"])
+            if doc is None:
+                first = self.store.count_documents(self.coll) == 0
+                roles = list(self.auto_roles)
+                if first and self.first_user_admin:
+                    roles = sorted(set(roles) | {"admin"})
+                doc = {"_id": user["sub"], "user_id": user["sub"], "email": user.get("email"), "name": user.get("name"),
+                       "provider": user.get("provider"), "roles": roles, "status": "approved" if roles else "pending",
+                       "created_at": time.time()}
+                self.store.insert_document(self.coll, doc)
+            return doc
+
+    def roles(self, user_id: str) -> list[str]:
+        d = self.get(user_id)
+        return list(d.get("roles", [])) if d and d.get("status") != "denied" else []
+
+    def assign(self, user_id: str, roles: list[str]) -> dict:
+        d = self.get(user_id)
+        if d is None:
+            raise KeyError(user_id)
+        new = sorted(set(d.get("roles", [])) | set(roles))
+        self.store.update_document(self.coll, user_id, {"roles": new, "status": "approved"})
+        return self.get(user_id)
+
+    def revoke(self, user_id: str, roles: list[str]) -> dict:
+        d = self.get(user_id)
+        if d is None:
+            raise KeyError(user_id)
+        self.store.update_document(self.coll, user_id, {"roles": sorted(set(d.get("roles", [])) - set(roles))})
+        return self.get(user_id)
+
+    def deny(self, user_id: str) -> dict:
+        self.store.update_document(self.coll, user_id, {"status": "denied", "roles": []})
+        return self.get(user_id)
+
+    def pending(self) -> list[dict]:
+        return self.store.query_documents(self.coll, {"status": "pending"}, limit=1000)
+
+    def search(self, q: str) -> list[dict]:
+        ql = q.lower()
+        return [u for u in self.store.query_documents(self.coll, {}, limit=100000)
+                if ql in (u.get("email") or "").lower() or ql in (u.get("name") or "").lower()]
+
+
+class JWTMiddleware:
+    """Bearer-token verification + role check for the service APIs (middleware.py:52,424).
+
+    ``verify_key`` is the auth service's signer (in-process) or a JWKS dict fetched from
+    ``{auth_service_url}/keys`` (cached, refreshed on unknown kid)."""
+
+    def __init__(self, verify_key=None, auth_service_url: str | None = None, audience: str = "copilot-for-consensus",
+                 required_roles: list[str] | None = None, public_paths: tuple[str, ...] = ("/health", "/readyz")):
+        self.verify_key, self.auth_url = verify_key, auth_service_url
+        self.audience, self.required_roles = audience, set(required_roles or [])
+        self.public_paths = public_paths
+        self._jwks: dict | None = None
+        self._jwks_at = 0.0
+
+    def _key(self):
+        if self.verify_key is not None:
+            return self.verify_key
+        if self._jwks is None or time.time() - self._jwks_at > 300:
+            with urllib.request.urlopen(f"{self.auth_url}/keys", timeout=10) as r:
+                self._jwks = json.loads(r.read())
+            self._jwks_at = time.time()
+        return self._jwks
+
+    def verify(self, authorization: str | None) -> dict:
+        if not authorization or not authorization.lower().startswith("bearer "):
+            raise PermissionError("missing bearer token")
+        try:
+            claims = decode(authorization.split(" ", 1)[1], self._key(), audience=self.audience)
+        except JWTError as e:
+            raise PermissionError(str(e)) from e
+        if self.required_roles and not (self.required_roles & set(claims.get("roles", []))):
+            raise LookupError("insufficient role")
+        return claims
+
+    def dependency(self):
+        from fastapi import Header, HTTPException
+
+        def dep(authorization: str | None = Header(default=None)) -> dict:
+            try:
+                return self.verify(authorization)
+            except PermissionError as e:
+                raise HTTPException(401, str(e))
+            except LookupError as e:
+                raise HTTPException(403, str(e))
+        return dep
+
+
+class AuthService:
+    """Login flow state machine + token minting + role administration."""
+
+    def __init__(self, jwt_manager: JWTManager, role_store: RoleStore, providers: dict[str, IdentityProvider],
+                 require_pkce: bool = True, require_nonce: bool = True, state_ttl: int = 600):
+        self.jwt, self.roles, self.providers = jwt_manager, role_store, providers
+        self.require_pkce, self.require_nonce = require_pkce, require_nonce
+        self._pending: dict[str, dict[str, Any]] = {}
+        self.state_ttl = state_ttl
+        self._lock = threading.Lock()
+
+    def initiate_login(self, provider: str, audience: str | None = None) -> dict:
+        p = self.providers.get(provider)
+        if p is None:
+            raise KeyError(f"unknown provider {provider}")
+        state, nonce = secrets.token_urlsafe(24), secrets.token_urlsafe(24)
+        verifier, challenge = pkce_pair()
+        with self._lock:
+            now = time.time()
+            self._pending = {k: v for k, v in self._pending.items() if now - v["t"] < self.state_ttl}
+            self._pending[state] = {"provider": provider, "nonce": nonce, "verifier": verifier, "t": now,
+                                    "audience": audience}
+        return {"authorization_url": p.authorization_url(state, nonce, challenge), "state": state}
+
+    def handle_callback(self, code: str, state: str) -> dict:
+        with self._lock:
+            st = self._pending.pop(state, None)
+        if st is None or time.time() - st["t"] > self.state_ttl:
+            raise PermissionError("invalid or expired state")
+        user = self.providers[st["provider"]].exchange_code(code, st["verifier"], st["nonce"])
+        doc = self.roles.ensure_user(user)
+        token = self.jwt.mint_token(user["sub"], {"email": user.get("email"), "name": user.get("name"),
+                                                  "roles": self.roles.roles(user["sub"]),
+                                                  "provider": user.get("provider")},
+                                    audience=st.get("audience"))
+        return {"access_token": token, "token_type": "Bearer", "expires_in": self.jwt.default_expiry,
+                "user": {k: doc.get(k) for k in ("user_id", "email", "name", "roles", "status")}}
+
+    def validate_token(self, token: str, audience: str | None = None) -> dict:
+        return self.jwt.validate_token(token, audience)
+
+    def refresh(self, token: str) -> dict:
+        claims = self.jwt.validate_token(token)
+        new = self.jwt.mint_token(claims["sub"], {k: claims.get(k) for k in ("email", "name", "provider")} |
+                                  {"roles": self.roles.roles(claims["sub"])})
+        return {"access_token": new, "token_type": "Bearer", "expires_in": self.jwt.default_expiry}
+
+    def get_jwks(self) -> dict:
+        return self.jwt.get_jwks()

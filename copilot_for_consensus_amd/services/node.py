@@ -1,0 +1,113 @@
+"""Service assembly: build any service from typed config, or a whole single-node deployment.
+
+``build_service(name, cfg, ...)`` wires a service from ``get_config(name)`` exactly like the
+reference mains (e.g. parsing/main.py:152-318): adapters from their discriminant env vars, the
+validating bus decorators, JWT middleware.  :class:`Node` runs every stage in ONE process on the
+in-process broker (the MI355X single-node deployment: one node, one bus, GPU models loaded once),
+with one consumer thread per service -- the compose topology of the reference without its
+network hops.  ``python -m copilot_for_consensus_amd.services.main <service>`` runs one service
+per process (uvicorn + consumer thread) for a distributed deployment.
+"""
+from __future__ import annotations
+
+import threading
+
+from ..archive import create_archive_store
+from ..bus import InProcBroker, create_publisher, create_subscriber
+from ..chunking import create_chunker
+from ..config.loader import get_config
+from ..embedding import create_embedding_provider
+from ..observability import create_error_reporter, create_logger, create_metrics_collector
+from ..retry import RetryConfig
+from ..storage.document_store import create_document_store
+from ..summarization import create_llm_backend
+from ..vectorstore import create_vector_store
+from .ingestion import IngestionService
+from .processing import ChunkingService, EmbeddingService, OrchestratorService, ParsingService, SummarizationService
+from .reporting import ReportingService
+
+
+class Node:
+    """All pipeline services in one process, sharing the broker, stores and GPU models."""
+
+    def __init__(self, env: dict | None = None, broker: InProcBroker | None = None, document_store=None,
+                 archive_store=None, embedding_provider=None, vector_store=None, summarizer=None,
+                 retry_config: RetryConfig | None = None):
+        self.broker = broker or InProcBroker()
+        cfgs = {s: get_config(s, env=env) for s in ("ingestion", "parsing", "chunking", "embedding", "orchestrator",
+                                                    "summarization", "reporting")}
+        self.cfgs = cfgs
+        c0 = cfgs["parsing"]
+        self.store = document_store or create_document_store(c0.document_store)
+        self.archives = archive_store or create_archive_store(cfgs["ingestion"].archive_store)
+        self.metrics = create_metrics_collector(c0.metrics)
+        self.logger = create_logger(c0.logger)
+        self.errors = create_error_reporter(c0.error_reporter)
+        self.embedder = embedding_provider or create_embedding_provider(cfgs["embedding"].embedding_backend)
+        self.vectors = vector_store or create_vector_store(cfgs["embedding"].vector_store,
+                                                           dimension=int(self.embedder.dimension))
+        self.summarizer = summarizer or create_llm_backend(cfgs["summarization"].llm_backend)
+        retry = retry_config or RetryConfig.from_adapter(c0.event_retry)
+        common = dict(metrics=self.metrics, logger=self.logger, error_reporter=self.errors, retry_config=retry)
+
+        def pub(name):
+            return create_publisher(cfgs[name].message_bus, broker=self.broker)
+
+        def sub(name):
+            return create_subscriber(cfgs[name].message_bus, broker=self.broker, queue_name=name)
+
+        o, sm, r = cfgs["orchestrator"], cfgs["summarization"], cfgs["reporting"]
+        self.services = {
+            "ingestion": IngestionService(pub("ingestion"), self.store, self.archives,
+                                          max_retries=cfgs["ingestion"].max_retries, **common),
+            "parsing": ParsingService(pub("parsing"), sub("parsing"), self.store, self.archives, **common),
+            "chunking": ChunkingService(pub("chunking"), sub("chunking"), self.store,
+                                        create_chunker(cfgs["chunking"].chunker), **common),
+            "embedding": EmbeddingService(pub("embedding"), sub("embedding"), self.store, self.embedder, self.vectors,
+                                          max_retries=cfgs["embedding"].max_retries, retry_backoff_seconds=0.1,
+                                          **common),
+            "orchestrator": OrchestratorService(pub("orchestrator"), sub("orchestrator"), self.store, self.vectors,
+                                                top_k=o.top_k, context_window_tokens=o.context_window_tokens,
+                                                chunk_selection_strategy=o.chunk_selection_strategy,
+                                                system_prompt_path=o.system_prompt_path,
+                                                user_prompt_path=o.user_prompt_path, **common),
+            "summarization": SummarizationService(pub("summarization"), sub("summarization"), self.store,
+                                                  self.summarizer, citation_count=sm.citation_count,
+                                                  context_window_tokens=sm.context_window_tokens,
+                                                  max_batch_threads=sm.max_batch_threads,
+                                                  batch_wait_ms=sm.batch_wait_ms, retry_delay_seconds=0.1, **common),
+            "reporting": ReportingService(pub("reporting"), sub("reporting"), self.store, self.vectors, self.embedder,
+                                          notify_enabled=r.notify_enabled, notify_webhook_url=r.notify_webhook_url,
+                                          **common),
+        }
+        self._threads: list[threading.Thread] = []
+
+    def start(self, threaded: bool = True) -> None:
+        for s in self.services.values():
+            s.start()
+        if threaded:
+            for name, s in self.services.items():
+                if s.subscriber is not None:
+                    t = threading.Thread(target=s.subscriber.start_consuming, name=f"{name}-consumer", daemon=True)
+                    t.start()
+                    self._threads.append(t)
+
+    def stop(self) -> None:
+        for s in self.services.values():
+            if s.subscriber is not None:
+                s.subscriber.stop_consuming()
+        for t in self._threads:
+            t.join(timeout=5)
+
+    def drain(self, max_rounds: int = 1000) -> int:
+        """Synchronous mode: process queued events stage by stage until the bus is quiet."""
+        total = 0
+        for _ in range(max_rounds):
+            n = 0
+            for s in self.services.values():
+                if s.subscriber is not None:
+                    n += s.subscriber.drain()
+            total += n
+            if n == 0:
+                break
+        return total
