@@ -34,7 +34,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="mistral-7b")
     ap.add_argument("--encoder", default="minilm-l6")
-    ap.add_argument("--threads-per-gpu", type=int, default=128, help="threads summarized per GPU per step")
+    ap.add_argument("--threads-per-gpu", type=int, default=128, help="threads summarized per engine (GPU, or TP group) per step")
     ap.add_argument("--max-new", type=int, default=512, help="generated tokens per summary (llama.cpp n_predict)")
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--prefill-tokens", type=int, default=16384)
@@ -52,19 +52,19 @@ def main(argv=None):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-
+    from copilot_for_consensus_amd.parallel import init_distributed, make_groups
     from copilot_for_consensus_amd.pipeline.bench_pipeline import BenchPipeline
 
+    env = init_distributed()
+    dev = env.device
+    # TP groups of args.tp consecutive ranks (one engine per group), DP across groups
+    groups = make_groups(env, args.tp)
     pipe = BenchPipeline(model=args.model, encoder=args.encoder, device=dev, threads_per_step=args.threads_per_gpu,
                          max_new_tokens=args.max_new, tp=args.tp, prefill_tokens=args.prefill_tokens,
-                         llm_only=args.llm_only, use_graph=not args.no_graph, seed=args.seed + 7919 * rank)
+                         llm_only=args.llm_only, use_graph=not args.no_graph,
+                         seed=args.seed + 7919 * groups.dp_rank, groups=groups if args.tp > 1 else None)
 
     pipe.prepare_sources(list(range(args.warmup + args.steps)))
 
@@ -123,7 +123,7 @@ def main(argv=None):
             "config": {
                 "model": args.model,
                 "encoder": args.encoder,
-                "global_batch": args.threads_per_gpu * world,
+                "global_batch": args.threads_per_gpu * groups.dp_size,
                 "seq_len": round(prompt_tokens / max(threads, 1)),
                 "max_new_tokens": args.max_new,
                 "parallelism": f"dp{world}" + (f"xtp{args.tp}" if args.tp > 1 else ""),

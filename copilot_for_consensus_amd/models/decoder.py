@@ -114,9 +114,13 @@ class DecoderWeights:
         gen.manual_seed(seed * 1000003 + tp_rank)
         D = cfg.head_dim
 
-        def rnd(*shape, scale=std):
+        # replicated tensors come from a rank-independent stream so every TP rank holds the same copy
+        gen_rep = torch.Generator(device=w.device)
+        gen_rep.manual_seed(seed * 1000003 + 999983)
+
+        def rnd(*shape, scale=std, g=gen):
             t = torch.empty(*shape, dtype=w.dtype, device=w.device)
-            t.normal_(0.0, scale, generator=gen)
+            t.normal_(0.0, scale, generator=g)
             return t
 
         h = cfg.hidden
@@ -130,7 +134,7 @@ class DecoderWeights:
                 "gate_up": rnd(2 * w.ffn, h),
                 "down": rnd(h, w.ffn, scale=out_std),
             })
-        w.embed = rnd(cfg.vocab_size, h, scale=1.0)  # embeddings replicated (gather is cheap)
+        w.embed = rnd(cfg.vocab_size, h, scale=1.0, g=gen_rep)  # embeddings replicated (gather is cheap)
         w.final_norm = torch.ones(h, dtype=w.dtype, device=w.device)
         w.lm_head = rnd(w.vocab_shard, h)
         return w

@@ -1,0 +1,137 @@
+"""Vector index sharded over ranks (one HBM-resident :class:`HipFlatIndex` shard per GPU).
+
+A 288 GB MI355X holds ~350M x 384 bf16 vectors, so sharding is about aggregate scan bandwidth
+(8 x 8 TB/s) more than capacity.  Query = every rank scans its shard with the fused MFMA kernel
+and keeps its exact local top-k; the k candidates (score, owner rank, row) are all-gathered as one
+small fp32 tensor over RCCL and merged with a top-k over world*k -- exact global top-k, traffic
+O(world * nq * k) independent of the index size.  Ids/metadata of the winners are resolved with
+one all_gather_object of the local candidates.
+
+Insert modes:
+  * ``add_embeddings`` -- replicated input (every rank sees the same batch); each rank stores only
+    the ids it owns (sha1(id) % world), so upserts of an id always land on the same shard;
+  * ``add_local`` -- rank-local input (each rank embedded its own chunks); owner = producer.
+All query methods are collectives: every rank of the group must call them with the same nq / k.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ..vectorstore import HipFlatIndex, SearchResult, VectorStore, _as_matrix
+from .dp import owner_of
+
+
+class ShardedVectorIndex(VectorStore):
+    def __init__(self, local: HipFlatIndex, group=None):
+        self.local = local
+        self.group = group
+        self.dist = dist.is_initialized()
+        self.rank = dist.get_rank(group) if self.dist else 0
+        self.world = dist.get_world_size(group) if self.dist else 1
+        self.dim = local.dim
+
+    # ---------------------------------------------------------------- writes
+    def add_embeddings(self, ids, vectors, metadatas=None):
+        vecs = _as_matrix(vectors, self.dim)
+        metadatas = list(metadatas) if metadatas is not None else [{} for _ in ids]
+        mine = [j for j, i in enumerate(ids) if owner_of(i, self.world) == self.rank]
+        if mine:
+            self.local.add_embeddings([ids[j] for j in mine], vecs[mine], [metadatas[j] for j in mine])
+
+    def add_local(self, ids, vectors, metadatas=None):
+        self.local.add_embeddings(ids, vectors, metadatas)
+
+    def delete(self, id):
+        if id in self.local._row:
+            self.local.delete(id)
+
+    def clear(self):
+        self.local.clear()
+
+    def count(self) -> int:
+        """Global count (collective)."""
+        t = torch.tensor([self.local.count()], dtype=torch.int64, device=self._comm_device())
+        if self.world > 1:
+            dist.all_reduce(t, group=self.group)
+        return int(t.item())
+
+    def get(self, id):
+        """Collective: the owner returns the vector, every rank receives it."""
+        res = self.local.get(id) if id in self.local._row else None
+        if self.world == 1:
+            if res is None:
+                raise KeyError(id)
+            return res
+        out = [None] * self.world
+        dist.all_gather_object(out, res, group=self.group)
+        for r in out:
+            if r is not None:
+                return r
+        raise KeyError(id)
+
+    # ---------------------------------------------------------------- search
+    def _comm_device(self):
+        backend = dist.get_backend(self.group) if self.dist else None
+        return self.local.device if backend == "nccl" else torch.device("cpu")
+
+    def search(self, Q, k: int):
+        """Global exact top-k: (scores [nq,k], owner rank [nq,k], local row [nq,k]); collective."""
+        Q = _as_matrix(Q, self.dim)
+        nq = Q.shape[0]
+        kk = min(k, self.local.count())
+        if kk > 0:
+            v, i = self.local.search(Q, kk)
+        else:
+            v = torch.empty(nq, 0, device=self.local.device)
+            i = torch.empty(nq, 0, dtype=torch.long, device=self.local.device)
+        cand = torch.full((nq, k, 2), float("-inf"), dtype=torch.float32, device=self.local.device)
+        cand[:, :v.shape[1], 0] = v.float()
+        cand[:, :v.shape[1], 1] = i.float()  # rows < 2^24 per shard are exact in fp32
+        cand[:, v.shape[1]:, 1] = -1
+        dev = self._comm_device()
+        cand = cand.to(dev)
+        if self.world > 1:
+            allc = [torch.empty_like(cand) for _ in range(self.world)]
+            dist.all_gather(allc, cand, group=self.group)
+            allc = torch.stack(allc, 0)              # [world, nq, k, 2]
+        else:
+            allc = cand[None]
+        scores = allc[..., 0].permute(1, 0, 2).reshape(nq, self.world * k)
+        rows = allc[..., 1].permute(1, 0, 2).reshape(nq, self.world * k)
+        top = min(k, scores.shape[1])
+        sv, si = torch.topk(scores, top, dim=1)
+        owner = torch.div(si, k, rounding_mode="floor")
+        row = torch.gather(rows, 1, si).long()
+        return sv, owner, row
+
+    def query_batch(self, query_vectors, top_k: int = 10, with_vectors: bool = False) -> list[list[SearchResult]]:
+        sv, owner, row = self.search(query_vectors, top_k)
+        sv, owner, row = sv.cpu(), owner.cpu(), row.cpu()
+        # resolve winners owned here, then share the resolved records
+        local: dict[int, tuple] = {}
+        for r in row[owner == self.rank].tolist():
+            if r >= 0 and r not in local and self.local._ids[r] is not None:
+                vec = self.local._X[r].float().cpu().tolist() if with_vectors else []
+                local[r] = (self.local._ids[r], vec, dict(self.local._meta[r] or {}))
+        tables = [local]
+        if self.world > 1:
+            tables = [None] * self.world
+            dist.all_gather_object(tables, local, group=self.group)
+        out = []
+        for q in range(sv.shape[0]):
+            res = []
+            for s, o, r in zip(sv[q].tolist(), owner[q].tolist(), row[q].tolist()):
+                if s == float("-inf") or r < 0:
+                    continue
+                rec = tables[o].get(r)
+                if rec is None:
+                    continue
+                if self.local.metric == "l2":
+                    s = 1.0 / (1.0 + max(0.0, -s)) if self.local.faiss_scores else -s
+                res.append(SearchResult(rec[0], float(s), rec[1], rec[2]))
+            out.append(res)
+        return out
+
+    def query(self, query_vector, top_k: int = 10):
+        return self.query_batch(_as_matrix(query_vector, self.dim), top_k)[0]

@@ -25,13 +25,19 @@ class StepResult:
 class BenchPipeline:
     def __init__(self, model="mistral-7b", encoder="minilm-l6", device="cuda", threads_per_step=128,
                  max_new_tokens=512, tp=1, prefill_tokens=16384, llm_only=False, use_graph=True, seed=0,
-                 index_prefill=1_000_000):
+                 index_prefill=1_000_000, groups=None):
         from ..models.decoder import DecoderModel, DecoderWeights, get_config
         from ..runtime.engine import LLMEngine
         from ..runtime.kv_cache import PagedKVCache, blocks_needed
 
-        if tp != 1:
-            raise NotImplementedError("bench TP>1 is launched through parallel.tp (DP bench uses tp=1)")
+        self.groups = groups
+        tp_rank = groups.tp_rank if groups is not None else 0
+        if groups is not None and groups.tp_size != tp:
+            raise ValueError("groups.tp_size != tp")
+        if tp > 1 and groups is None:
+            raise ValueError("tp > 1 needs process groups (parallel.make_groups)")
+        # TP followers run the LLM only; the leader prepares the batch and broadcasts the prompts
+        self.follower = tp > 1 and tp_rank != 0
         self.device = torch.device(device)
         self.cfg = get_config(model)
         self.threads_per_step = threads_per_step
@@ -39,8 +45,8 @@ class BenchPipeline:
         self.llm_only = llm_only
         self.rng = random.Random(seed)
         self.seed = seed
-        w = DecoderWeights.random(self.cfg, self.device, seed=1234)
-        self.model = DecoderModel(w)
+        w = DecoderWeights.random(self.cfg, self.device, seed=1234, tp_rank=tp_rank, tp_size=tp)
+        self.model = DecoderModel(w, tp_group=groups.tp_group if tp > 1 else None)
         # KV budget: every thread of a step at the longest prompt we generate (3k) + max_new, x1.1
         max_prompt = 4096
         nblk = int(1.1 * threads_per_step * blocks_needed(max_prompt + max_new_tokens)) + 64
@@ -50,7 +56,7 @@ class BenchPipeline:
         self.side_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         self._last_gen_s: float | None = None
         self._last_prep_s = 0.0
-        if not llm_only:
+        if not llm_only and not self.follower:
             from ..bus import CountingPublisher
             from .rag import RagPipeline
             self.events = CountingPublisher()
@@ -61,7 +67,7 @@ class BenchPipeline:
 
     def prepare_sources(self, steps: list[int]) -> None:
         """Generate the synthetic archives of the given steps up front (outside the timed region)."""
-        if self.rag is not None:
+        if self.rag is not None and not self.follower:
             self.rag.prepare_sources(self.threads_per_step, steps)
 
     def _synthetic_prompts(self, n):
@@ -80,8 +86,27 @@ class BenchPipeline:
             if delay > 0:
                 time.sleep(delay)
         t0 = time.perf_counter()
+        if self.groups is not None and self.groups.tp_size > 1:
+            return self._prepare_tp(t0, step)
         if self.rag is None:
             return t0, None, self._synthetic_prompts(self.threads_per_step), {}
+        return self._prepare_rag(t0, step)
+
+    def _prepare_tp(self, t0, step):
+        import torch.distributed as dist
+        g = self.groups
+        if self.follower:
+            box = [None]
+            dist.broadcast_object_list(box, src=g.tp_src, group=g.tp_cpu_group)
+            return t0, None, box[0], {}
+        if self.rag is None:
+            t0, ctx, prompts, stages = t0, None, self._synthetic_prompts(self.threads_per_step), {}
+        else:
+            t0, ctx, prompts, stages = self._prepare_rag(t0, step)
+        dist.broadcast_object_list([prompts], src=g.tp_src, group=g.tp_cpu_group)
+        return t0, ctx, prompts, stages
+
+    def _prepare_rag(self, t0, step):
         if self.device.type == "cuda":
             # the encoder / kNN work of this batch runs on its own stream, beside the decode graph
             with torch.cuda.stream(self.side_stream):
@@ -122,7 +147,8 @@ class BenchPipeline:
                     stages["report"] = time.perf_counter() - t2
                 t3 = time.perf_counter()
                 stages["total"] = t3 - t0
-                results.append(StepResult(len(prompts), [t3 - t0] * len(prompts), sum(len(t) for t in res.tokens),
+                n_thr = 0 if self.follower else len(prompts)  # a TP group counts its threads once
+                results.append(StepResult(n_thr, [t3 - t0] * n_thr, sum(len(t) for t in res.tokens),
                                           sum(res.prompt_lens), stages))
                 if fut is not None:
                     pending = fut.result()
