@@ -16,6 +16,11 @@ import zipfile
 from datetime import datetime, timezone
 from pathlib import Path
 
+try:  # route annotations are resolved against module globals (postponed evaluation)
+    from fastapi import Request
+except ImportError:  # pragma: no cover - services without the HTTP layer
+    Request = None
+
 from ..archive import SourceConfig, calculate_file_hash, create_fetcher
 from ..contracts.events import utc_now_iso
 from ..contracts.ids import archive_id_from_bytes

@@ -16,6 +16,7 @@ from ..archive import create_archive_store
 from ..bus import InProcBroker, create_publisher, create_subscriber
 from ..chunking import create_chunker
 from ..config.loader import get_config
+from ..consensus import create_consensus_detector
 from ..embedding import create_embedding_provider
 from ..observability import create_error_reporter, create_logger, create_metrics_collector
 from ..retry import RetryConfig
@@ -70,7 +71,9 @@ class Node:
                                                 top_k=o.top_k, context_window_tokens=o.context_window_tokens,
                                                 chunk_selection_strategy=o.chunk_selection_strategy,
                                                 system_prompt_path=o.system_prompt_path,
-                                                user_prompt_path=o.user_prompt_path, **common),
+                                                user_prompt_path=o.user_prompt_path,
+                                                consensus_detector=create_consensus_detector(o.consensus_detector),
+                                                **common),
             "summarization": SummarizationService(pub("summarization"), sub("summarization"), self.store,
                                                   self.summarizer, citation_count=sm.citation_count,
                                                   context_window_tokens=sm.context_window_tokens,

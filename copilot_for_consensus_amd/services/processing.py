@@ -256,9 +256,13 @@ class OrchestratorService(BaseService):
 
     def __init__(self, publisher, subscriber, document_store, vector_store=None, top_k: int = 5,
                  context_window_tokens: int = 2048, chunk_selection_strategy: str = "top_k_relevance",
-                 system_prompt_path: str | None = None, user_prompt_path: str | None = None, **kw):
+                 system_prompt_path: str | None = None, user_prompt_path: str | None = None,
+                 consensus_detector=None, **kw):
         super().__init__(publisher, subscriber, document_store, **kw)
         self.vectors = vector_store
+        # optional: annotate threads with has_consensus / consensus_type (the threads schema carries
+        # these fields; the reference ships the detector but never calls it)
+        self.consensus = consensus_detector
         self.top_k, self.budget = top_k, context_window_tokens
         self.selector = create_context_selector(chunk_selection_strategy)
         self.template = prompt_template(system_prompt_path, user_prompt_path)
@@ -310,10 +314,23 @@ class OrchestratorService(BaseService):
             self.metrics.increment("orchestrator_summary_skipped_total")
             return None
         self.metrics.increment("orchestrator_summary_triggered_total")
+        if self.consensus is not None:
+            self._annotate_consensus(thread_id)
         return self.publish("SummarizationRequested", thread_ids=[thread_id], top_k=self.top_k,
                             prompt_template=self.template,
                             selected_chunks=[s.to_dict() for s in sel.selected_chunks],
                             context_selection=sel.metadata())
+
+    def _annotate_consensus(self, thread_id: str) -> None:
+        from ..consensus import ConsensusLevel, Thread
+        thread = self.store.get_document("threads", thread_id)
+        if thread is None:
+            return
+        msgs = self.store.query_documents("messages", {"thread_id": thread_id}, limit=1 << 20)
+        sig = self.consensus.detect(Thread.from_documents(thread, msgs))
+        agreed = sig.level in (ConsensusLevel.STRONG_CONSENSUS, ConsensusLevel.CONSENSUS)
+        self.store.update_document("threads", thread_id, {"has_consensus": agreed, "consensus_type": sig.level.value})
+        self.metrics.increment("orchestrator_consensus_total", tags={"level": sig.level.value})
 
     def process_embeddings(self, chunk_ids: list[str]) -> int:
         n = 0
