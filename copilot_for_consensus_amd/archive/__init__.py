@@ -146,6 +146,48 @@ class LocalVolumeArchiveStore(ArchiveStore):
         return [dict(m) for m in self._meta.values() if m["source_name"] == source_name]
 
 
+class DocumentStoreArchiveStore(ArchiveStore):
+    """Archives kept in a DocumentStore collection (base64 content) -- the reference's MongoDB
+    archive store is a stub (mongodb_archive_store.py:13); this one works on any DocumentStore."""
+
+    def __init__(self, document_store=None, collection: str = "raw_archives", **_):
+        from ..storage.document_store import InMemoryDocumentStore
+        self.store = document_store or InMemoryDocumentStore()
+        self.coll = collection
+
+    def store_archive(self, source_name, file_path, content):
+        import base64
+        aid = hashlib.sha256(content).hexdigest()[:16]
+        if self.store.get_document(self.coll, aid) is None:
+            self.store.insert_document(self.coll, {"_id": aid, "source_name": source_name, "file_path": file_path,
+                                                   "file_hash": hashlib.sha256(content).hexdigest(),
+                                                   "size_bytes": len(content),
+                                                   "content_b64": base64.b64encode(content).decode()})
+        return aid
+
+    def get_archive(self, archive_id):
+        import base64
+        d = self.store.get_document(self.coll, archive_id)
+        return None if d is None else base64.b64decode(d["content_b64"])
+
+    def get_archive_by_hash(self, content_hash):
+        r = self.store.query_documents(self.coll, {"file_hash": content_hash}, limit=1)
+        return r[0]["_id"] if r else None
+
+    def archive_exists(self, archive_id):
+        return self.store.get_document(self.coll, archive_id) is not None
+
+    def delete_archive(self, archive_id):
+        if self.store.get_document(self.coll, archive_id) is None:
+            return False
+        self.store.delete_document(self.coll, archive_id)
+        return True
+
+    def list_archives(self, source_name):
+        return [{k: v for k, v in d.items() if k != "content_b64"}
+                for d in self.store.query_documents(self.coll, {"source_name": source_name}, limit=1 << 30)]
+
+
 def create_archive_store(cfg=None) -> ArchiveStore:
     name = getattr(cfg, "driver_name", cfg) or "local"
     kw = dict(getattr(cfg, "driver_config", {}) or {})
@@ -154,7 +196,10 @@ def create_archive_store(cfg=None) -> ArchiveStore:
     if name == "inmemory":
         return InMemoryArchiveStore()
     if name == "azureblob":
-        raise ImportError("azureblob archive store needs azure-storage-blob (not in this image)")
+        from ..cloud.azure import AzureBlobArchiveStore
+        return AzureBlobArchiveStore(**{k: v for k, v in kw.items() if v is not None})
+    if name in ("mongodb", "document_store"):
+        return DocumentStoreArchiveStore(**kw)
     raise ValueError(f"unknown archive_store driver {name!r}")
 
 

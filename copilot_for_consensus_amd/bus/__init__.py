@@ -34,8 +34,9 @@ def create_publisher(cfg=None, enable_validation: bool = True, broker: InProcBro
     elif name == "rabbitmq":
         from .rabbitmq import RabbitMQPublisher
         pub = RabbitMQPublisher(**kw)
-    elif name == "azure_service_bus":
-        raise ImportError("azure_service_bus driver needs azure-servicebus (not in this image)")
+    elif name in ("azure_service_bus", "azureservicebus"):
+        from ..cloud.azure import AzureServiceBusPublisher
+        pub = AzureServiceBusPublisher(**kw)
     else:
         raise ValueError(f"unknown message_bus driver {name!r}")
     return ValidatingEventPublisher(pub, schema_provider) if enable_validation else pub
@@ -53,8 +54,9 @@ def create_subscriber(cfg=None, enable_validation: bool = True, broker: InProcBr
     elif name == "rabbitmq":
         from .rabbitmq import RabbitMQSubscriber
         sub = RabbitMQSubscriber(**kw)
-    elif name == "azure_service_bus":
-        raise ImportError("azure_service_bus driver needs azure-servicebus (not in this image)")
+    elif name in ("azure_service_bus", "azureservicebus"):
+        from ..cloud.azure import AzureServiceBusSubscriber
+        sub = AzureServiceBusSubscriber(**kw)
     else:
         raise ValueError(f"unknown message_bus driver {name!r}")
     return ValidatingEventSubscriber(sub, schema_provider) if enable_validation else sub

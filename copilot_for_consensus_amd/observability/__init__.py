@@ -234,7 +234,8 @@ def create_metrics_collector(cfg=None, **overrides) -> MetricsCollector:
     if name == "pushgateway":
         return PushGatewayMetricsCollector(**kw)
     if name == "azure_monitor":
-        raise ImportError("azure_monitor metrics need the OpenTelemetry Azure exporter (not in this image)")
+        from ..cloud.azure import AzureMonitorMetricsCollector
+        return AzureMonitorMetricsCollector(**kw)
     raise ValueError(f"unknown metrics driver {name!r}")
 
 
@@ -266,6 +267,28 @@ class SilentErrorReporter(ErrorReporter):
         self.reported.append((error, dict(context or {})))
 
 
+class SentryErrorReporter(ErrorReporter):
+    """Sentry (sentry_error_reporter.py:13 of the reference); sentry-sdk is imported on construction."""
+
+    def __init__(self, dsn: str | None = None, environment: str = "production", traces_sample_rate: float = 0.0,
+                 **_):
+        try:
+            import sentry_sdk
+        except ImportError as e:
+            raise ImportError("sentry error reporting needs the 'sentry-sdk' package, which is not installed") from e
+        self._sdk = sentry_sdk
+        sentry_sdk.init(dsn=dsn, environment=environment, traces_sample_rate=traces_sample_rate)
+
+    def report(self, error, context=None):
+        with self._sdk.push_scope() as scope:
+            for k, v in (context or {}).items():
+                scope.set_extra(k, v)
+            self._sdk.capture_exception(error)
+
+    def capture_message(self, message, level="info", context=None):
+        self._sdk.capture_message(message, level=level)
+
+
 def create_error_reporter(cfg=None, **overrides) -> ErrorReporter:
     name = getattr(cfg, "driver_name", cfg) or "console"
     kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
@@ -275,7 +298,7 @@ def create_error_reporter(cfg=None, **overrides) -> ErrorReporter:
     if name == "silent":
         return SilentErrorReporter()
     if name == "sentry":
-        raise ImportError("sentry error reporting needs sentry-sdk (not in this image)")
+        return SentryErrorReporter(**kw)
     raise ValueError(f"unknown error reporter {name!r}")
 
 

@@ -90,6 +90,16 @@ def microsoft_provider(microsoft_client_id, microsoft_client_secret, microsoft_r
                         f"{base}/authorize", f"{base}/token", "https://graph.microsoft.com/oidc/userinfo")
 
 
+def datatracker_provider(datatracker_client_id, datatracker_client_secret, datatracker_redirect_uri=None,
+                         datatracker_issuer="https://auth.ietf.org/api/openid", **_):
+    """IETF Datatracker login through its OpenID Connect provider (the reference ships only a
+    scaffold that raises NotImplementedError, datatracker_provider.py:14)."""
+    base = datatracker_issuer.rstrip("/")
+    return OIDCProvider("datatracker", datatracker_client_id, datatracker_client_secret,
+                        datatracker_redirect_uri or "", f"{base}/authorize", f"{base}/token", f"{base}/userinfo",
+                        scope="openid profile email roles")
+
+
 class MockIdentityProvider(IdentityProvider):
     """Deterministic provider for tests/dev (reference mock_provider.py:15): any code logs in the
     user whose id is the code."""

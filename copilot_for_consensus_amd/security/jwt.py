@@ -4,6 +4,9 @@ Reference: adapters/copilot_jwt_signer (LocalJWTSigner RSA/EC/HMAC, local_signer
 copilot_auth/jwt_manager.py (mint :154, validate :265, JWKS :322).
 
 * HS256 -- stdlib ``hmac``.
+* ES256 -- ECDSA over NIST P-256 with SHA-256, deterministic nonces (RFC 6979), Jacobian point
+  arithmetic on Python integers, JWK ``kty=EC, crv=P-256, x, y``; signatures in the JOSE raw
+  ``r || s`` form (RFC 7518 §3.4).
 * RS256 -- RSASSA-PKCS1-v1_5 with SHA-256 implemented on Python integers: key generation
   (Miller-Rabin primes, e = 65537), CRT signing, public verification, JWK / JWKS export
   (``kty=RSA, n, e, kid``) so services can verify tokens from the auth service's JWKS exactly as
@@ -136,6 +139,153 @@ class RSAKey:
         return cls(d["n"], d["e"], d["d"], d.get("p"), d.get("q"))
 
 
+# ------------------------------------------------------------------------------------ P-256 math
+
+_P = 0xffffffff00000001000000000000000000000000ffffffffffffffffffffffff
+_A = _P - 3
+_B = 0x5ac635d8aa3a93e7b3ebbd55769886bc651d06b0cc53b0f63bce3c3e27d2604b
+_N = 0xffffffff00000000ffffffffffffffffbce6faada7179e84f3b9cac2fc632551
+_G = (0x6b17d1f2e12c4247f8bce6e563a440f277037d812deb33a0f4a13945d898c296,
+      0x4fe342e2fe1a7f9b8ee7eb4a7c0f9e162bce33576b315ececbb6406837bf51f5)
+
+
+def _jdouble(P):
+    X, Y, Z = P
+    if Y == 0:
+        return (0, 1, 0)
+    YY = Y * Y % _P
+    S = 4 * X * YY % _P
+    ZZ = Z * Z % _P
+    M = 3 * (X - ZZ) * (X + ZZ) % _P          # a = -3
+    X3 = (M * M - 2 * S) % _P
+    return (X3, (M * (S - X3) - 8 * YY * YY) % _P, 2 * Y * Z % _P)
+
+
+def _jadd(P, Q):
+    if P[2] == 0:
+        return Q
+    if Q[2] == 0:
+        return P
+    X1, Y1, Z1 = P
+    X2, Y2, Z2 = Q
+    Z1Z1, Z2Z2 = Z1 * Z1 % _P, Z2 * Z2 % _P
+    U1, U2 = X1 * Z2Z2 % _P, X2 * Z1Z1 % _P
+    S1, S2 = Y1 * Z2 * Z2Z2 % _P, Y2 * Z1 * Z1Z1 % _P
+    if U1 == U2:
+        return _jdouble(P) if S1 == S2 else (0, 1, 0)
+    H, R = (U2 - U1) % _P, (S2 - S1) % _P
+    HH = H * H % _P
+    HHH = H * HH % _P
+    V = U1 * HH % _P
+    X3 = (R * R - HHH - 2 * V) % _P
+    return (X3, (R * (V - X3) - S1 * HHH) % _P, H * Z1 * Z2 % _P)
+
+
+def _jmul(k: int, pt) -> tuple[int, int] | None:
+    R, Q = (0, 1, 0), (pt[0], pt[1], 1)
+    while k:
+        if k & 1:
+            R = _jadd(R, Q)
+        Q = _jdouble(Q)
+        k >>= 1
+    if R[2] == 0:
+        return None
+    zi = pow(R[2], -1, _P)
+    return (R[0] * zi * zi % _P, R[1] * zi * zi * zi % _P)
+
+
+def _on_curve(x: int, y: int) -> bool:
+    return 0 <= x < _P and 0 <= y < _P and (y * y - (x * x * x + _A * x + _B)) % _P == 0
+
+
+def _rfc6979_k(d: int, h1: bytes) -> int:
+    """Deterministic nonce (RFC 6979 §3.2) for P-256 / SHA-256."""
+    x = _int_to_b(d, 32)
+    h = _int_to_b(int.from_bytes(h1, "big") % _N, 32)
+    V, K = b"\x01" * 32, b"\x00" * 32
+    K = hmac.new(K, V + b"\x00" + x + h, hashlib.sha256).digest()
+    V = hmac.new(K, V, hashlib.sha256).digest()
+    K = hmac.new(K, V + b"\x01" + x + h, hashlib.sha256).digest()
+    V = hmac.new(K, V, hashlib.sha256).digest()
+    while True:
+        V = hmac.new(K, V, hashlib.sha256).digest()
+        k = int.from_bytes(V, "big")
+        if 1 <= k < _N:
+            return k
+        K = hmac.new(K, V + b"\x00", hashlib.sha256).digest()
+        V = hmac.new(K, V, hashlib.sha256).digest()
+
+
+class ECKey:
+    """P-256 key: private scalar ``d`` (optional) and public point ``(x, y)``."""
+
+    def __init__(self, x: int, y: int, d: int | None = None):
+        if not _on_curve(x, y):
+            raise JWTError("point not on P-256")
+        self.x, self.y, self.d = x, y, d
+
+    @classmethod
+    def generate(cls) -> "ECKey":
+        d = _secrets.randbelow(_N - 1) + 1
+        x, y = _jmul(d, _G)
+        return cls(x, y, d)
+
+    def sign(self, msg: bytes) -> bytes:
+        if self.d is None:
+            raise JWTError("private key required")
+        h = hashlib.sha256(msg).digest()
+        e = int.from_bytes(h, "big")
+        while True:
+            k = _rfc6979_k(self.d, h)
+            r = _jmul(k, _G)[0] % _N
+            s = pow(k, -1, _N) * (e + r * self.d) % _N
+            if r and s:
+                return _int_to_b(r, 32) + _int_to_b(s, 32)
+            h = hashlib.sha256(h).digest()   # practically unreachable; keep determinism
+
+    def verify(self, msg: bytes, sig: bytes) -> bool:
+        if len(sig) != 64:
+            return False
+        r, s = int.from_bytes(sig[:32], "big"), int.from_bytes(sig[32:], "big")
+        if not (1 <= r < _N and 1 <= s < _N):
+            return False
+        e = int.from_bytes(hashlib.sha256(msg).digest(), "big")
+        w = pow(s, -1, _N)
+        u1, u2 = e * w % _N, r * w % _N
+        P1, P2 = _jmul(u1, _G), _jmul(u2, (self.x, self.y))
+        if P1 is None or P2 is None:
+            pt = P1 or P2
+        else:
+            R = _jadd((P1[0], P1[1], 1), (P2[0], P2[1], 1))
+            if R[2] == 0:
+                return False
+            zi = pow(R[2], -1, _P)
+            pt = (R[0] * zi * zi % _P, 0)
+        return pt is not None and pt[0] % _N == r
+
+    def public_jwk(self, kid: str) -> dict:
+        return {"kty": "EC", "crv": "P-256", "use": "sig", "alg": "ES256", "kid": kid,
+                "x": b64u(_int_to_b(self.x, 32)), "y": b64u(_int_to_b(self.y, 32))}
+
+    def public_pem(self) -> str:
+        spki = bytes.fromhex("3059301306072a8648ce3d020106082a8648ce3d030107034200") + b"\x04" + \
+            _int_to_b(self.x, 32) + _int_to_b(self.y, 32)
+        body = base64.encodebytes(spki).decode().replace("\n", "")
+        lines = [body[i:i + 64] for i in range(0, len(body), 64)]
+        return "-----BEGIN PUBLIC KEY-----\n" + "\n".join(lines) + "\n-----END PUBLIC KEY-----\n"
+
+    @classmethod
+    def from_jwk(cls, jwk: dict) -> "ECKey":
+        if jwk.get("crv") != "P-256":
+            raise JWTError("only P-256 EC keys are supported")
+        d = int.from_bytes(b64u_dec(jwk["d"]), "big") if "d" in jwk else None
+        return cls(int.from_bytes(b64u_dec(jwk["x"]), "big"), int.from_bytes(b64u_dec(jwk["y"]), "big"), d)
+
+    def private_json(self) -> str:
+        return json.dumps({"kty": "EC", "crv": "P-256", "x": b64u(_int_to_b(self.x, 32)),
+                           "y": b64u(_int_to_b(self.y, 32)), "d": b64u(_int_to_b(self.d, 32))})
+
+
 # ------------------------------------------------------------------------------------ signers
 
 class JWTSigner(ABC):
@@ -193,6 +343,28 @@ class RSASigner(JWTSigner):
         return self.key.public_jwk(self.key_id)
 
 
+class ECSigner(JWTSigner):
+    algorithm = "ES256"
+
+    def __init__(self, private_key: str | ECKey | None = None, key_id: str = "default", **_):
+        if isinstance(private_key, ECKey):
+            self.key = private_key
+        elif private_key:
+            self.key = ECKey.from_jwk(json.loads(private_key))
+        else:
+            self.key = ECKey.generate()
+        self.key_id = key_id
+
+    def sign(self, message):
+        return self.key.sign(message)
+
+    def verify(self, message, signature):
+        return self.key.verify(message, signature)
+
+    def get_public_key_jwk(self):
+        return self.key.public_jwk(self.key_id)
+
+
 def create_jwt_signer(cfg=None, **overrides) -> JWTSigner:
     kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
     kw.update(overrides)
@@ -201,6 +373,8 @@ def create_jwt_signer(cfg=None, **overrides) -> JWTSigner:
         return HMACSigner(**kw)
     if alg == "RS256":
         return RSASigner(**kw)
+    if alg == "ES256":
+        return ECSigner(**kw)
     raise JWTError(f"unsupported JWT algorithm {alg}")
 
 
@@ -233,9 +407,11 @@ def decode(token: str, verify_key, audience: str | list[str] | None = None, issu
         jwk = next((k for k in verify_key["keys"] if k.get("kid") == header.get("kid")), None)
         if jwk is None:
             raise JWTError("unknown kid")
-        verify_key = RSAKey.from_jwk(jwk)
+        verify_key = ECKey.from_jwk(jwk) if jwk.get("kty") == "EC" else RSAKey.from_jwk(jwk)
     if isinstance(verify_key, RSAKey):
         ok = alg == "RS256" and verify_key.verify(msg, sig)
+    elif isinstance(verify_key, ECKey):
+        ok = alg == "ES256" and verify_key.verify(msg, sig)
     elif isinstance(verify_key, JWTSigner):
         ok = alg == verify_key.algorithm and verify_key.verify(msg, sig)
     else:

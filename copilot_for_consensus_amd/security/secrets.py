@@ -3,7 +3,7 @@
 * LocalFileSecretProvider -- one file per secret under ``base_path`` (``/run/secrets`` in compose,
   local_provider.py:17); names are sanitised so a secret name cannot escape the directory.
 * EnvSecretProvider -- ``<PREFIX><NAME>`` environment variables (upper-cased).
-* AzureKeyVaultProvider -- needs azure-keyvault-secrets (not in this image).
+* AzureKeyVaultSecretProvider -- cloud/azure.py (imports azure-keyvault-secrets on construction).
 """
 from __future__ import annotations
 
@@ -85,6 +85,7 @@ def create_secret_provider(cfg=None, **overrides) -> SecretProvider:
         return LocalFileSecretProvider(**kw)
     if name == "env":
         return EnvSecretProvider(**kw)
-    if name == "azure_key_vault":
-        raise ImportError("azure_key_vault secrets need azure-keyvault-secrets (not in this image)")
+    if name in ("azure_key_vault", "azurekeyvault"):
+        from ..cloud.azure import AzureKeyVaultSecretProvider
+        return AzureKeyVaultSecretProvider(**kw)
     raise ValueError(f"unknown secret provider {name!r}")

@@ -30,7 +30,7 @@ def main(argv=None) -> int:
 
     if args.service == "auth":
         from ..security.auth import AuthService, MockIdentityProvider, RoleStore, github_provider, google_provider
-        from ..security.auth import microsoft_provider
+        from ..security.auth import datatracker_provider, microsoft_provider
         from ..security.jwt import JWTManager, create_jwt_signer
         from ..storage.document_store import create_document_store
         from .auth import create_auth_app
@@ -38,7 +38,8 @@ def main(argv=None) -> int:
         cfg = get_config("auth")
         store = create_document_store(cfg.document_store)
         provs = {"mock": MockIdentityProvider()} if os.environ.get("AUTH_ENABLE_MOCK_PROVIDER") else {}
-        for name, fn in (("github", github_provider), ("google", google_provider), ("microsoft", microsoft_provider)):
+        for name, fn in (("github", github_provider), ("google", google_provider), ("microsoft", microsoft_provider),
+                         ("datatracker", datatracker_provider)):
             pc = cfg.oidc_providers.driver_config.get(name, {})
             if pc.get(f"{name}_client_id"):
                 provs[name] = fn(**pc)

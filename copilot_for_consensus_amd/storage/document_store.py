@@ -437,8 +437,9 @@ def create_document_store(cfg=None, enable_validation: bool = False, strict: boo
         store: DocumentStore = InMemoryDocumentStore()
     elif name == "mongodb":
         store = MongoDocumentStore(**kw)
-    elif name == "azure_cosmosdb":
-        raise ImportError("azure_cosmosdb driver needs azure-cosmos (not in this image)")
+    elif name in ("azure_cosmosdb", "azurecosmos"):
+        from ..cloud.azure import AzureCosmosDocumentStore
+        store = AzureCosmosDocumentStore(**{k: v for k, v in kw.items() if v is not None})
     else:
         raise ValueError(f"unknown document_store driver {name!r}")
     return ValidatingDocumentStore(store, strict=strict) if enable_validation else store

@@ -433,7 +433,10 @@ def create_vector_store(cfg=None, **overrides) -> VectorStore:
             HipIVFIndex(faiss_scores=True, **kw)
     if name == "inmemory":
         return InMemoryVectorStore(**kw)
-    if name in ("qdrant", "azure_ai_search"):
-        raise ImportError(f"vector_store driver {name!r} needs an external service client not in this image; "
-                          "use VECTOR_STORE_TYPE=hip (HBM-resident index)")
+    if name == "qdrant":
+        from .remote import QdrantVectorStore
+        return QdrantVectorStore(**kw)
+    if name in ("azure_ai_search", "aisearch"):
+        from .remote import AzureAISearchVectorStore
+        return AzureAISearchVectorStore(**kw)
     raise ValueError(f"unknown vector_store driver {name!r}")
