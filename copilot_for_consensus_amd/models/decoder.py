@@ -19,13 +19,14 @@ from __future__ import annotations
 import dataclasses
 import json
 import math
+import os
 from pathlib import Path
 
 import torch
 import torch.nn.functional as F
 
 from ..ops import kernels as K
-from ..ops.reference import rope_cos_sin
+from ..ops.reference import interleave_gate_up, rope_cos_sin
 
 
 @dataclasses.dataclass(frozen=True)
@@ -101,6 +102,8 @@ class DecoderWeights:
         self.ffn = cfg.ffn // tp_size
         self.vocab_shard = cfg.vocab_size // tp_size
         self.layers: list[dict[str, torch.Tensor]] = []
+        # gate_up rows: [gate; up] (False) or 32-row interleaved groups (True, see interleave_gate_up)
+        self.gate_up_interleaved = False
         self.embed: torch.Tensor | None = None
         self.final_norm: torch.Tensor | None = None
         self.lm_head: torch.Tensor | None = None
@@ -137,7 +140,7 @@ class DecoderWeights:
         w.embed = rnd(cfg.vocab_size, h, scale=1.0, g=gen_rep)  # embeddings replicated (gather is cheap)
         w.final_norm = torch.ones(h, dtype=w.dtype, device=w.device)
         w.lm_head = rnd(w.vocab_shard, h)
-        return w
+        return w.finalize()
 
     @classmethod
     def from_safetensors(cls, cfg, ckpt_dir, device, tp_rank: int = 0, tp_size: int = 1):
@@ -183,7 +186,16 @@ class DecoderWeights:
         w.final_norm = dev(tensors["model.norm.weight"])
         head = tensors.get("lm_head.weight", tensors["model.embed_tokens.weight"])
         w.lm_head = dev(shard_rows(head, w.vocab_shard))
-        return w
+        return w.finalize()
+
+    def finalize(self) -> "DecoderWeights":
+        """Put gate/up rows in the 32-row interleaved order the fused decode SwiGLU GEMM reads (the
+        prefill path's silu_mul reads the same layout, so one copy of the weights serves both)."""
+        if not self.gate_up_interleaved and self.ffn % 32 == 0:
+            for layer in self.layers:
+                layer["gate_up"] = interleave_gate_up(layer["gate_up"])
+            self.gate_up_interleaved = True
+        return self
 
     def nbytes(self) -> int:
         n = sum(t.numel() * t.element_size() for layer in self.layers for t in layer.values())
@@ -206,11 +218,16 @@ def load_config_json(path) -> DecoderConfig:
 class DecoderModel:
     """Stateless forward functions over :class:`DecoderWeights` + a paged KV cache."""
 
-    def __init__(self, weights: DecoderWeights, tp_group=None):
+    def __init__(self, weights: DecoderWeights, tp_group=None, fused_decode: bool | None = None):
         self.w = weights
         self.cfg = weights.cfg
         self.tp_group = tp_group
         self.scale = 1.0 / math.sqrt(self.cfg.head_dim)
+        # decode projections on the split-K skinny MFMA GEMM with fused epilogues (TP=1; with TP>1
+        # the all-reduce sits between the projection and the residual/norm)
+        if fused_decode is None:
+            fused_decode = os.environ.get("CFC_FUSED_DECODE", "0") == "1"
+        self.fused_decode = fused_decode and weights.tp_size == 1 and weights.gate_up_interleaved
 
     def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.w.tp_size > 1:
@@ -231,7 +248,7 @@ class DecoderModel:
         lw = self.w.layers[i]
         h = K.rmsnorm(attn_out, lw["mlp_norm"], self.cfg.rms_eps, residual=residual)
         gu = F.linear(h, lw["gate_up"])
-        a = K.silu_mul(gu)
+        a = K.silu_mul(gu, interleaved=self.w.gate_up_interleaved)
         return self._all_reduce(F.linear(a, lw["down"]))
 
     def forward_prefill(self, ids, positions, slots, cu_q, ctx_lens, block_tables, kv, tiles=None,
@@ -259,8 +276,11 @@ class DecoderModel:
         """One token per sequence. Returns final-normed hidden [B, H]."""
         cfg, w = self.cfg, self.w
         x = K.embedding(w.embed, ids)
-        residual = None
         B = ids.shape[0]
+        if self.fused_decode and x.is_cuda and B <= K.SKINNY_MAX_M:
+            return self._forward_decode_fused(x, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
+                                              part_blocks)
+        residual = None
         for i in range(cfg.layers):
             lw = w.layers[i]
             h, residual = self._layer_pre(i, x, residual)
@@ -272,6 +292,28 @@ class DecoderModel:
             o = self._all_reduce(F.linear(attn.view(B, -1), lw["o"]))
             x = self._mlp(i, o, residual)
         return K.rmsnorm(x, w.final_norm, cfg.rms_eps, residual=residual)
+
+    def _forward_decode_fused(self, x, positions, slots, ctx_lens, block_tables, kv, attn_workspace, part_blocks):
+        """Decode layer as 4 skinny GEMMs whose epilogues carry the elementwise work:
+        qkv -> RoPE/KV write -> attention -> [o + residual + mlp RMSNorm] -> [gate_up + SwiGLU] ->
+        [down + residual + next layer's RMSNorm].  Same rounding points as the unfused path."""
+        cfg, w = self.cfg, self.w
+        B = x.shape[0]
+        eps = cfg.rms_eps
+        residual = x.clone()
+        h = K.rmsnorm(x, w.layers[0]["attn_norm"], eps)
+        for i in range(cfg.layers):
+            lw = w.layers[i]
+            qkv = K.skinny_linear(h, lw["qkv"])
+            q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
+                                cfg.head_dim)
+            attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
+                                            part_blocks=part_blocks, workspace=attn_workspace)
+            h = K.skinny_linear_residual_rmsnorm(attn.view(B, -1), lw["o"], residual, lw["mlp_norm"], eps)
+            a = K.skinny_swiglu(h, lw["gate_up"])
+            nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm
+            h = K.skinny_linear_residual_rmsnorm(a, lw["down"], residual, nxt, eps)
+        return h
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """[B, V] logits (all-gathered over the vocab-parallel shards)."""

@@ -30,7 +30,7 @@ _KERNEL_SIGS = {
     "cfc_prefill_attention": [P, P, P, P, P, P, P, P, I, I, I, I, I, F, P, P],
     "cfc_encoder_attention": [P, P, P, P, I, I, I, I, F, P, P],
     "cfc_rope_kv_write": [P, P, P, P, P, P, P, I, I, I, I, P],
-    "cfc_silu_mul": [P, P, I, I, P],
+    "cfc_silu_mul": [P, P, I, I, I, P],
     "cfc_bias_gelu": [P, P, P, I, I, P],
     "cfc_embedding": [P, P, P, I, I, P],
     "cfc_sample": [P, I, I, F, c_uint32, P, P, P],
@@ -40,8 +40,9 @@ _KERNEL_SIGS = {
     "cfc_topk_chunk_size": [],
     "cfc_l2_normalize": [P, P, P, I, I, P],
     "cfc_pool": [P, P, P, P, I, I, I, I, P],
-    "cfc_gemm_bf16": [P, P, P, P, P, I, I, I, I, I, P],
-    "cfc_allreduce_oneshot": [P, P, I, I, I, c_int64, P],
+    "cfc_skinny_gemm": [P, P, I, I, I, I, I, P, P, I, P],
+    "cfc_splitk_reduce": [P, I, I, I, I, P, I, P],
+    "cfc_splitk_residual_rmsnorm": [P, I, I, I, P, P, F, P, P],
 }
 
 _RUNTIME_SIGS = {

@@ -190,13 +190,110 @@ def encoder_attention(qkv, cu_seqlens, H, D, scale, max_seqlen, tiles=None, out=
     return out
 
 
-def silu_mul(gu, out=None):
+# ----------------------------------------------------------------------------- skinny GEMM (decode)
+
+SKINNY_MAX_M = 256          # above this the library GEMMs win (prefill shapes)
+_workspaces: dict = {}
+
+
+def _workspace(device, numel: int) -> torch.Tensor:
+    """Grow-only fp32 split-K workspace per device (sized during the eager warm-up, so hipGraph
+    capture sees a fixed pointer)."""
+    ws = _workspaces.get(device)
+    if ws is None or ws.numel() < numel:
+        ws = torch.empty(max(numel, 1 << 20), dtype=torch.float32, device=device)
+        _workspaces[device] = ws
+    return ws
+
+
+def skinny_split(M: int, N: int, K: int, target_blocks: int = 512) -> int:
+    """Split-K factor: enough blocks to cover the 256 CUs twice, K slices of whole 64-deep stages."""
+    tiles = (N // 64) * ((M + 127) // 128)
+    stages = K // 64
+    best = 1
+    for s in (1, 2, 4, 7, 8, 14, 16):
+        if stages % s == 0 and tiles * s <= target_blocks * 1.25:
+            best = s
+    return best
+
+
+def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dim() == 2 and x.shape[0] <= SKINNY_MAX_M and w.shape[0] % 64 == 0
+            and x.shape[1] % 64 == 0 and x.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous())
+
+
+def skinny_linear(x: torch.Tensor, w: torch.Tensor, split: int | None = None, out: torch.Tensor | None = None):
+    """x [M, K] @ w[N, K]^T -> bf16 [M, N] with the decode GEMM (split-K + reduce)."""
+    if not x.is_cuda:
+        return torch.nn.functional.linear(x, w)
+    M, K = x.shape
+    N = w.shape[0]
+    split = split or skinny_split(M, N, K)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device) if out is None else out
+    st = _stream(x)
+    if split == 1:
+        check(kernels().cfc_skinny_gemm(x.data_ptr(), w.data_ptr(), M, N, K, 1, 1, None, out.data_ptr(), N, st),
+              "cfc_skinny_gemm")
+        return out
+    ws = _workspace(x.device, split * M * N)
+    check(kernels().cfc_skinny_gemm(x.data_ptr(), w.data_ptr(), M, N, K, split, 0, ws.data_ptr(), None, 0, st),
+          "cfc_skinny_gemm")
+    check(kernels().cfc_splitk_reduce(ws.data_ptr(), split, M, N, 0, out.data_ptr(), N, st), "cfc_splitk_reduce")
+    return out
+
+
+def skinny_swiglu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, split: int | None = None):
+    """silu(x @ gate^T) * (x @ up^T) for gate/up weights interleaved in 32-row groups."""
+    if not x.is_cuda:
+        return ref.silu_mul_interleaved(torch.nn.functional.linear(x, w_gu_interleaved))
+    M, K = x.shape
+    N = w_gu_interleaved.shape[0]
+    split = split or skinny_split(M, N, K)
+    out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=x.device)
+    st = _stream(x)
+    if split == 1:
+        check(kernels().cfc_skinny_gemm(x.data_ptr(), w_gu_interleaved.data_ptr(), M, N, K, 1, 2, None,
+                                        out.data_ptr(), N // 2, st), "cfc_skinny_gemm")
+        return out
+    ws = _workspace(x.device, split * M * N)
+    check(kernels().cfc_skinny_gemm(x.data_ptr(), w_gu_interleaved.data_ptr(), M, N, K, split, 0, ws.data_ptr(),
+                                    None, 0, st), "cfc_skinny_gemm")
+    check(kernels().cfc_splitk_reduce(ws.data_ptr(), split, M, N, 1, out.data_ptr(), N // 2, st), "cfc_splitk_reduce")
+    return out
+
+
+def skinny_linear_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor,
+                                   eps: float, split: int | None = None) -> torch.Tensor:
+    """residual += x @ w^T (bf16-rounded projection); returns RMSNorm(residual) * norm_w."""
+    if not x.is_cuda:
+        y = torch.nn.functional.linear(x, w)
+        o, r = ref.rmsnorm(y, norm_w, eps, residual)
+        residual.copy_(r)
+        return o
+    M, K = x.shape
+    N = w.shape[0]
+    split = split or skinny_split(M, N, K)
+    ws = _workspace(x.device, split * M * N)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    st = _stream(x)
+    check(kernels().cfc_skinny_gemm(x.data_ptr(), w.data_ptr(), M, N, K, split, 0, ws.data_ptr(), None, 0, st),
+          "cfc_skinny_gemm")
+    check(kernels().cfc_splitk_residual_rmsnorm(ws.data_ptr(), split, M, N, residual.data_ptr(), norm_w.data_ptr(),
+                                                float(eps), out.data_ptr(), st), "cfc_splitk_residual_rmsnorm")
+    return out
+
+
+def silu_mul(gu, out=None, interleaved: bool = False):
+    """silu(gate) * up; ``interleaved``: gate/up in 32-column groups (see ref.interleave_gate_up)."""
     if not gu.is_cuda:
-        return ref.silu_mul(gu)
+        return ref.silu_mul_interleaved(gu) if interleaved else ref.silu_mul(gu)
     _req(gu, torch.bfloat16, "gu")
     T, F2 = gu.shape
     out = torch.empty(T, F2 // 2, dtype=gu.dtype, device=gu.device) if out is None else out
-    check(kernels().cfc_silu_mul(out.data_ptr(), gu.data_ptr(), T, F2 // 2, _stream(gu)), "cfc_silu_mul")
+    for t0 in range(0, T, 65535):
+        t1 = min(T, t0 + 65535)
+        check(kernels().cfc_silu_mul(out[t0:t1].data_ptr(), gu[t0:t1].data_ptr(), t1 - t0, F2 // 2,
+                                     1 if interleaved else 0, _stream(gu)), "cfc_silu_mul")
     return out
 
 

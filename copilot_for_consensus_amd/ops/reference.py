@@ -149,6 +149,25 @@ def silu_mul(gu):
     return (torch.nn.functional.silu(g) * u).to(gu.dtype)
 
 
+def interleave_gate_up(gu_w: torch.Tensor) -> torch.Tensor:
+    """[gate; up] rows (2F, H) -> 32-row groups [gate 32t..32t+31; up 32t..32t+31] (F % 32 == 0)."""
+    F = gu_w.shape[0] // 2
+    g, u = gu_w[:F].reshape(F // 32, 32, -1), gu_w[F:].reshape(F // 32, 32, -1)
+    return torch.stack([g, u], 1).reshape(2 * F, -1).contiguous()
+
+
+def deinterleave_gate_up(w: torch.Tensor) -> torch.Tensor:
+    F = w.shape[0] // 2
+    v = w.reshape(F // 32, 2, 32, -1)
+    return torch.cat([v[:, 0].reshape(F, -1), v[:, 1].reshape(F, -1)]).contiguous()
+
+
+def silu_mul_interleaved(gu):
+    F = gu.shape[-1] // 2
+    v = gu.reshape(*gu.shape[:-1], F // 32, 2, 32).float()
+    return (torch.nn.functional.silu(v[..., 0, :]) * v[..., 1, :]).reshape(*gu.shape[:-1], F).to(gu.dtype)
+
+
 def bias_gelu(x, bias):
     xf = x.float() + (bias.float() if bias is not None else 0.0)
     return torch.nn.functional.gelu(xf).to(x.dtype)

@@ -30,12 +30,13 @@ def shard_weights(full: DecoderWeights, tp_rank: int, tp_size: int, device=None)
     def rows(t, start, n):
         return t[start:start + n]
 
+    from ..ops.reference import deinterleave_gate_up
     for layer in full.layers:
         qkv = layer["qkv"]
         q = rows(qkv, tp_rank * hq * D, hq * D)
         k = rows(qkv, Hq * D + tp_rank * hk * D, hk * D)
         v = rows(qkv, (Hq + Hkv) * D + tp_rank * hk * D, hk * D)
-        gu = layer["gate_up"]
+        gu = deinterleave_gate_up(layer["gate_up"]) if full.gate_up_interleaved else layer["gate_up"]
         g = rows(gu, tp_rank * f, f)
         u = rows(gu, F + tp_rank * f, f)
         w.layers.append({
@@ -50,7 +51,7 @@ def shard_weights(full: DecoderWeights, tp_rank: int, tp_size: int, device=None)
     w.final_norm = full.final_norm.to(dev)
     vs = cfg.vocab_size // tp_size
     w.lm_head = full.lm_head[tp_rank * vs:(tp_rank + 1) * vs].contiguous().to(dev)
-    return w
+    return w.finalize()
 
 
 def random_sharded(cfg: DecoderConfig, device, seed: int, tp_rank: int, tp_size: int) -> DecoderWeights:

@@ -18,74 +18,83 @@ __device__ __forceinline__ int v_slot(int key_in_block) {
   return 8 * g + j;
 }
 
-// grid = T tokens, block = 256.
 // qkv: [T, (Hq + 2*Hkv) * D] (q heads | k heads | v heads), positions [T], slots [T] (-1 = skip
 // cache write), cos_sin [max_pos][D/2][2] fp32 (cos, sin interleaved).
-__global__ void __launch_bounds__(256) rope_kv_kernel(const uint16_t* __restrict__ qkv, const int32_t* __restrict__ positions,
-                                                      const int32_t* __restrict__ slots, const float* __restrict__ cos_sin,
-                                                      uint16_t* __restrict__ q_out, uint16_t* __restrict__ k_cache,
-                                                      uint16_t* __restrict__ v_cache, int Hq, int Hkv, int D) {
+__global__ void __launch_bounds__(64) rope_kv_kernel(const uint16_t* __restrict__ qkv, const int32_t* __restrict__ positions,
+                                                     const int32_t* __restrict__ slots, const float* __restrict__ cos_sin,
+                                                     uint16_t* __restrict__ q_out, uint16_t* __restrict__ k_cache,
+                                                     uint16_t* __restrict__ v_cache, int Hq, int Hkv, int D) {
+  // grid = (T, ceil(items / 64)): one 8-element item per thread -- (Hq + Hkv) * D/16 rotation
+  // items then Hkv * D/8 V items -- so a decode batch of 128 tokens is ~900 blocks, not 128.
   const int tok = blockIdx.x;
   const int half = D / 2, nv = half / 8;  // 8-element vectors per half-head
-  const int stride = (Hq + 2 * Hkv) * D;
-  const uint16_t* row = qkv + (size_t)tok * stride;
-  const int pos = positions[tok];
-  const int slot = slots[tok];
-  const float* cs = cos_sin + (size_t)pos * half * 2;
   const int n_rot = (Hq + Hkv) * nv;
   const int n_v = Hkv * (D / 8);
-  for (int it = threadIdx.x; it < n_rot + n_v; it += blockDim.x) {
-    if (it < n_rot) {
-      const int head = it / nv, c = it % nv;  // head < Hq: query, else key (head - Hq)
-      const uint16_t* src = row + head * D;
-      float a[8], b[8], ra[8], rb[8];
-      unpack8(*reinterpret_cast<const uint4*>(src + c * 8), a);
-      unpack8(*reinterpret_cast<const uint4*>(src + half + c * 8), b);
+  const int it = blockIdx.y * 64 + threadIdx.x;
+  if (it >= n_rot + n_v) return;
+  const int stride = (Hq + 2 * Hkv) * D;
+  const uint16_t* row = qkv + (size_t)tok * stride;
+  const int slot = slots[tok];
+  if (it < n_rot) {
+    const int head = it / nv, c = it - head * nv;  // head < Hq: query, else key (head - Hq)
+    const float4* cs = reinterpret_cast<const float4*>(cos_sin + ((size_t)positions[tok] * half + c * 8) * 2);
+    float csv[16];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float cv = cs[(c * 8 + j) * 2], sv = cs[(c * 8 + j) * 2 + 1];
-        ra[j] = a[j] * cv - b[j] * sv;
-        rb[j] = b[j] * cv + a[j] * sv;
-      }
-      const uint4 pa = pack8(ra), pb = pack8(rb);
-      if (head < Hq) {
-        uint16_t* dst = q_out + ((size_t)tok * Hq + head) * D;
-        *reinterpret_cast<uint4*>(dst + c * 8) = pa;
-        *reinterpret_cast<uint4*>(dst + half + c * 8) = pb;
-      } else if (slot >= 0) {
-        const int kh = head - Hq;
-        const int blk = slot / KV_BS, off = slot % KV_BS;
-        uint16_t* dst = k_cache + (((size_t)blk * Hkv + kh) * KV_BS + off) * D;
-        *reinterpret_cast<uint4*>(dst + c * 8) = pa;
-        *reinterpret_cast<uint4*>(dst + half + c * 8) = pb;
-      }
-    } else if (slot >= 0) {
-      const int v = it - n_rot;
-      const int kh = v / (D / 8), c = v % (D / 8);
-      const uint4 val = *reinterpret_cast<const uint4*>(row + (Hq + Hkv + kh) * D + c * 8);
-      const int blk = slot / KV_BS, off = slot % KV_BS;
-      const int sl = v_slot(off);
-      uint16_t* dst = v_cache + (((size_t)blk * Hkv + kh) * D + c * 8) * KV_BS + sl;
-      const uint16_t* e = reinterpret_cast<const uint16_t*>(&val);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dst[j * KV_BS] = e[j];
+    for (int j = 0; j < 4; ++j) {
+      const float4 t = cs[j];
+      csv[4 * j] = t.x; csv[4 * j + 1] = t.y; csv[4 * j + 2] = t.z; csv[4 * j + 3] = t.w;
     }
+    const uint16_t* src = row + head * D;
+    float a[8], b[8], ra[8], rb[8];
+    unpack8(*reinterpret_cast<const uint4*>(src + c * 8), a);
+    unpack8(*reinterpret_cast<const uint4*>(src + half + c * 8), b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float cv = csv[2 * j], sv = csv[2 * j + 1];
+      ra[j] = a[j] * cv - b[j] * sv;
+      rb[j] = b[j] * cv + a[j] * sv;
+    }
+    const uint4 pa = pack8(ra), pb = pack8(rb);
+    if (head < Hq) {
+      uint16_t* dst = q_out + ((size_t)tok * Hq + head) * D;
+      *reinterpret_cast<uint4*>(dst + c * 8) = pa;
+      *reinterpret_cast<uint4*>(dst + half + c * 8) = pb;
+    } else if (slot >= 0) {
+      const int kh = head - Hq;
+      const int blk = slot / KV_BS, off = slot % KV_BS;
+      uint16_t* dst = k_cache + (((size_t)blk * Hkv + kh) * KV_BS + off) * D;
+      *reinterpret_cast<uint4*>(dst + c * 8) = pa;
+      *reinterpret_cast<uint4*>(dst + half + c * 8) = pb;
+    }
+  } else if (slot >= 0) {
+    const int v = it - n_rot;
+    const int kh = v / (D / 8), c = v % (D / 8);
+    const uint4 val = *reinterpret_cast<const uint4*>(row + (Hq + Hkv + kh) * D + c * 8);
+    const int blk = slot / KV_BS, off = slot % KV_BS;
+    const int sl = v_slot(off);
+    uint16_t* dst = v_cache + (((size_t)blk * Hkv + kh) * D + c * 8) * KV_BS + sl;
+    const uint16_t* e = reinterpret_cast<const uint16_t*>(&val);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dst[j * KV_BS] = e[j];
   }
 }
 
-// out[t, f] = silu(gu[t, f]) * gu[t, F + f]
-__global__ void silu_mul_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ gu, int T, int F) {
-  const int nvec = F / 8;
-  const size_t total = (size_t)T * nvec;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const size_t t = i / nvec, c = i % nvec;
-    float a[8], b[8], r[8];
-    unpack8(*reinterpret_cast<const uint4*>(gu + t * 2 * F + c * 8), a);
-    unpack8(*reinterpret_cast<const uint4*>(gu + t * 2 * F + F + c * 8), b);
+// out[t, f] = silu(gate[t, f]) * up[t, f].  Layout of gu[t]: [gate | up] halves, or (interleave)
+// 32-column groups [gate 32t..32t+31 | up 32t..32t+31] -- the layout the decode GEMM's fused
+// SwiGLU epilogue needs, so prefill and decode share one weight copy.  grid = (cols/8/256, T).
+__global__ void silu_mul_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ gu, int F, int interleave) {
+  const int t = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;   // 8-column group of the output
+  if (c >= (F >> 3)) return;
+  const int gc = interleave ? ((c >> 2) << 3) + (c & 3) : c;
+  const int uc = interleave ? gc + 4 : c + (F >> 3);
+  const uint4* row = reinterpret_cast<const uint4*>(gu + (size_t)t * 2 * F);
+  float a[8], b[8], r[8];
+  unpack8(row[gc], a);
+  unpack8(row[uc], b);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = a[j] / (1.f + __expf(-a[j])) * b[j];
-    *reinterpret_cast<uint4*>(out + t * F + c * 8) = pack8(r);
-  }
+  for (int j = 0; j < 8; ++j) r[j] = a[j] / (1.f + __expf(-a[j])) * b[j];
+  reinterpret_cast<uint4*>(out + (size_t)t * F)[c] = pack8(r);
 }
 
 // out[t, f] = gelu_erf(x[t, f] + bias[f])   (in place allowed)
@@ -218,15 +227,16 @@ CFC_API int cfc_rope_kv_write(const void* qkv, const int32_t* positions, const i
                               hipStream_t stream) {
   if (head_dim % 16 != 0 || T < 0) return -1;
   if (T == 0) return 0;
-  rope_kv_kernel<<<T, 256, 0, stream>>>((const uint16_t*)qkv, positions, slots, cos_sin, (uint16_t*)q_out,
+  const int items = (Hq + Hkv) * (head_dim / 16) + Hkv * (head_dim / 8);
+  rope_kv_kernel<<<dim3(T, (items + 63) / 64), 64, 0, stream>>>((const uint16_t*)qkv, positions, slots, cos_sin, (uint16_t*)q_out,
                                          (uint16_t*)k_cache, (uint16_t*)v_cache, Hq, Hkv, head_dim);
   return CFC_CHECK_LAUNCH();
 }
 
-CFC_API int cfc_silu_mul(void* out, const void* gu, int T, int F, hipStream_t stream) {
-  if (F % 8 != 0) return -1;
+CFC_API int cfc_silu_mul(void* out, const void* gu, int T, int F, int interleave, hipStream_t stream) {
+  if (F % 8 != 0 || (interleave && F % 32 != 0) || T > 65535) return -1;
   if (T == 0) return 0;
-  silu_mul_kernel<<<ew_grid((size_t)T * F / 8), 256, 0, stream>>>((uint16_t*)out, (const uint16_t*)gu, T, F);
+  silu_mul_kernel<<<dim3((F / 8 + 255) / 256, T), 256, 0, stream>>>((uint16_t*)out, (const uint16_t*)gu, F, interleave);
   return CFC_CHECK_LAUNCH();
 }
 

@@ -11,7 +11,7 @@
 namespace {
 
 template <int VPT>
-__global__ void __launch_bounds__(256) rmsnorm_kernel(uint16_t* __restrict__ out, uint16_t* __restrict__ residual,
+__global__ void __launch_bounds__(1024) rmsnorm_kernel(uint16_t* __restrict__ out, uint16_t* __restrict__ residual,
                                                       const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                       int dim, float eps, int add_residual) {
   __shared__ float red[16];
@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(uint16_t* __restrict__ out
 //   mode 1: y = LN(x + bias + residual)          (post-LN BERT block: dense out + residual)
 //   mode 2: y = LN(word_emb[ids] + pos_emb[pos] + type_emb[0])   (BERT embedding layer)
 template <int VPT>
-__global__ void __launch_bounds__(256) layernorm_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ x,
+__global__ void __launch_bounds__(1024) layernorm_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ x,
                                                         const uint16_t* __restrict__ bias, const uint16_t* __restrict__ residual,
                                                         const uint16_t* __restrict__ gamma, const uint16_t* __restrict__ beta,
                                                         const int32_t* __restrict__ ids, const int32_t* __restrict__ pos,
@@ -124,7 +124,9 @@ __global__ void __launch_bounds__(256) layernorm_kernel(uint16_t* __restrict__ o
   }
 }
 
-inline int pick_block(int nvec) { return nvec >= 1024 ? 256 : (nvec >= 256 ? 128 : 64); }
+// One 16-B vector per thread whenever the row fits in a 1024-thread block: at decode (128 rows)
+// a row is a single load round trip instead of VPT dependent ones (10 us -> ~3 us per call).
+inline int pick_block(int nvec) { return nvec >= 1024 ? 1024 : ((nvec + 63) / 64) * 64; }
 
 }  // namespace
 

@@ -14,6 +14,7 @@ def _to_cpu_fp32_model(w: DecoderWeights):
     c = DecoderWeights(w.cfg, "cpu")
     c.layers = [{k: v.cpu() for k, v in layer.items()} for layer in w.layers]
     c.embed, c.final_norm, c.lm_head = w.embed.cpu(), w.final_norm.cpu(), w.lm_head.cpu()
+    c.gate_up_interleaved = w.gate_up_interleaved
     return c
 
 
@@ -43,6 +44,19 @@ def test_graph_and_eager_decode_agree():
         kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, "cuda")
         res.append(LLMEngine(m, kv, use_graph=g).generate([[1, 2, 3] * 30, [4, 5] * 70], 40, ignore_eos=True).tokens)
     assert res[0] == res[1]
+
+
+def test_fused_decode_matches_unfused():
+    cfg = get_config("tiny")
+    w = DecoderWeights.random(cfg, "cuda", seed=7)
+    res = []
+    for fused in (True, False):
+        m = DecoderModel(w, fused_decode=fused)
+        assert m.fused_decode == fused
+        kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, "cuda")
+        res.append(LLMEngine(m, kv).generate([[1, 2, 3] * 30, [4, 5] * 70, [1, 7]], 24, ignore_eos=True).tokens)
+    agree = sum(a == b for x, y in zip(*res) for a, b in zip(x, y))
+    assert [t[0] for t in res[0]] == [t[0] for t in res[1]] and agree >= 0.9 * 72, res
 
 
 def test_encoder_gpu_vs_cpu():

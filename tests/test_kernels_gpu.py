@@ -200,3 +200,47 @@ def test_pool():
     for mode in ("mean", "cls"):
         _close(K.pool(h.to(DEV), cu.to(DEV), mode, True), R.pool(h, cu, mode, True), 1e-3)
     del lens
+
+
+def test_silu_mul_interleaved():
+    gu = torch.randn(33, 2 * 512, device=DEV).bfloat16()
+    _close(K.silu_mul(gu, interleaved=True), R.silu_mul_interleaved(gu.cpu()), 2e-2)
+    w = torch.randn(2 * 64, 16)
+    assert torch.equal(R.deinterleave_gate_up(R.interleave_gate_up(w)), w)
+
+
+def _ref_linear(x, w):
+    return (x.float() @ w.float().T).cpu()
+
+
+@pytest.mark.parametrize("M,N,Kd,split", [(1, 6144, 4096, None), (8, 4096, 4096, 8), (77, 1024, 512, 2),
+                                         (128, 4096, 14336, None), (128, 6144, 4096, 4), (200, 512, 1024, 1),
+                                         (128, 32000, 4096, 1)])
+def test_skinny_linear(M, N, Kd, split):
+    x = torch.randn(M, Kd, device=DEV).bfloat16()
+    w = (torch.randn(N, Kd, device=DEV) * 0.02).bfloat16()
+    y = K.skinny_linear(x, w, split=split)
+    _close(y, _ref_linear(x, w), 3e-2)
+
+
+@pytest.mark.parametrize("M,split", [(128, 1), (5, 1), (128, 2), (130, 4)])
+def test_skinny_swiglu(M, split):
+    F, Kd = 1024, 512
+    x = torch.randn(M, Kd, device=DEV).bfloat16()
+    gu = (torch.randn(2 * F, Kd, device=DEV) * 0.05).bfloat16()
+    wi = R.interleave_gate_up(gu)
+    ref = R.silu_mul(_ref_linear(x, gu).bfloat16())
+    _close(K.skinny_swiglu(x, wi, split=split), ref, 3e-2)
+
+
+@pytest.mark.parametrize("M,N,Kd,split", [(128, 4096, 4096, 8), (3, 256, 512, 1), (128, 4096, 14336, 8)])
+def test_skinny_linear_residual_rmsnorm(M, N, Kd, split):
+    x = torch.randn(M, Kd, device=DEV).bfloat16()
+    w = (torch.randn(N, Kd, device=DEV) * 0.02).bfloat16()
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    nw = (1 + 0.1 * torch.randn(N, device=DEV)).bfloat16()
+    ref_o, ref_r = R.rmsnorm(_ref_linear(x, w).bfloat16(), nw.cpu(), 1e-5, r.cpu())
+    rr = r.clone()
+    o = K.skinny_linear_residual_rmsnorm(x, w, rr, nw, 1e-5, split=split)
+    _close(rr, ref_r, 3e-2)
+    _close(o, ref_o, 5e-2)
