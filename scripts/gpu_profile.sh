@@ -9,4 +9,7 @@ timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
   python bench.py "$@" > gpurun_out/prof_bench.log 2>&1; rc=$?
 tail -3 gpurun_out/prof_bench.log
 [ $rc -eq 0 ] || exit $rc
-python scripts/prof_summary.py gpurun_out/prof gpurun_out/prof_summary.txt | head -40
+python scripts/prof_summary.py gpurun_out/prof gpurun_out/prof_summary.txt > /dev/null
+cat gpurun_out/prof_summary.txt | head -40
+# the raw per-dispatch trace is hundreds of MB: keep only the stats so gpurun_out/ is copied back
+find gpurun_out/prof -name '*kernel_trace.csv' -delete
