@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 import time
 
 import torch
@@ -23,6 +24,7 @@ import torch
 from ..ops import kernels as K
 from ..ops.reference import KV_BLOCK
 from .kv_cache import PagedKVCache, blocks_needed
+from .prefix_cache import PrefixCache
 
 
 @dataclasses.dataclass
@@ -33,6 +35,7 @@ class GenerationResult:
     decode_s: float = 0.0
     ttft_s: float = 0.0
     decode_steps: int = 0
+    cached_prompt_tokens: int = 0    # prompt tokens served from the prefix cache
 
     @property
     def total_s(self) -> float:
@@ -64,7 +67,7 @@ class _DecodeState:
 
 class LLMEngine:
     def __init__(self, model, kv: PagedKVCache, max_prefill_tokens: int = 16384, use_graph: bool = True,
-                 stop_check_interval: int = 64):
+                 stop_check_interval: int = 64, prefix_cache: bool | None = None):
         self.model = model
         self.cfg = model.cfg
         self.kv = kv
@@ -73,6 +76,10 @@ class LLMEngine:
         self.use_graph = use_graph and kv.device.type == "cuda"
         self.stop_check_interval = stop_check_interval
         self._states: dict[tuple, _DecodeState] = {}
+        # shared-prefix reuse of whole KV blocks (system prompt + template head of every thread)
+        if prefix_cache is None:
+            prefix_cache = os.environ.get("CFC_PREFIX_CACHE", "1") != "0"
+        self.prefix_cache = PrefixCache(kv.pool) if prefix_cache else None
         if self.device.type == "cuda":
             from .gemm_tuning import enable_tuned_gemms
             self.tuned_gemms = enable_tuned_gemms()
@@ -86,11 +93,12 @@ class LLMEngine:
     def _i32(self, x):
         return torch.tensor(x, dtype=torch.int32, device=self.device)
 
-    def _prefill(self, prompts, tables, temperature, seed):
-        """Chunked packed prefill; returns first sampled token per prompt."""
+    def _prefill(self, prompts, tables, temperature, seed, start=None):
+        """Chunked packed prefill; returns first sampled token per prompt.  ``start[s]`` tokens of
+        prompt s are already in the cache (shared prefix blocks)."""
         n = len(prompts)
         first = [0] * n
-        pos = [0] * n  # tokens of each prompt already in the cache
+        pos = list(start) if start is not None else [0] * n  # tokens of each prompt already in the cache
         order = list(range(n))
         while order:
             chunk, budget = [], self.max_prefill_tokens
@@ -191,13 +199,28 @@ class LLMEngine:
         # round the block-table width up so graphs are reused across batches of similar length
         need = [blocks_needed(n + max_new_tokens) for n in lens]
         max_blocks = 8 * math.ceil(max(need) / 8)
-        tables = [self.kv.pool.alloc(n) for n in need]
+        pc = self.prefix_cache
+        tables, start, fresh = [], [], []
+        try:
+            for p, n in zip(prompts, need):
+                shared = pc.acquire(p) if pc is not None else []
+                tables.append(shared)       # registered before alloc so a failure releases it
+                new = pc.alloc(n - len(shared)) if pc is not None else self.kv.pool.alloc(n)
+                fresh.append(new)
+                tables[-1] = shared + new
+                start.append(len(shared) * KV_BLOCK)
+                if pc is not None:
+                    pc.insert(p, tables[-1])
+        except BaseException:
+            self._release(tables, fresh, failed=True)
+            raise
+        ok = False
         try:
             sync = self.device.type == "cuda"
             if sync:
                 torch.cuda.synchronize(self.device)
             t0 = time.perf_counter()
-            first = self._prefill(prompts, tables, temperature, seed)
+            first = self._prefill(prompts, tables, temperature, seed, start)
             if sync:
                 torch.cuda.synchronize(self.device)
             t1 = time.perf_counter()
@@ -236,9 +259,9 @@ class LLMEngine:
             if sync:
                 torch.cuda.synchronize(self.device)
             t2 = time.perf_counter()
+            ok = True
         finally:
-            for t in tables:
-                self.kv.pool.free(t)
+            self._release(tables, fresh, failed=not ok)
         out = []
         stop = set(stop_ids)
         for b in range(B):
@@ -248,4 +271,16 @@ class LLMEngine:
                     row = row[:j]
                     break
             out.append(row)
-        return GenerationResult(out, lens, prefill_s=t1 - t0, decode_s=t2 - t1, ttft_s=t1 - t0, decode_steps=steps)
+        return GenerationResult(out, lens, prefill_s=t1 - t0, decode_s=t2 - t1, ttft_s=t1 - t0, decode_steps=steps,
+                                cached_prompt_tokens=sum(start))
+
+    def _release(self, tables, fresh, failed: bool = False):
+        if self.prefix_cache is None:
+            for t in tables:
+                self.kv.pool.free(t)
+            return
+        if failed:  # this call's own blocks may have been published before their prefill ran
+            for t in fresh:
+                self.prefix_cache.invalidate(t)
+        for t in tables:
+            self.prefix_cache.release(t)

@@ -20,7 +20,8 @@ def test_generate_shapes_and_block_reuse():
     free0 = eng.kv.pool.num_free()
     res = eng.generate([[1, 2, 3, 4], [1] * 50], max_new_tokens=5, ignore_eos=True)
     assert [len(t) for t in res.tokens] == [5, 5]
-    assert eng.kv.pool.num_free() == free0
+    # every block is back in the pool except the one full prompt block kept by the prefix cache
+    assert eng.kv.pool.num_free() + eng.prefix_cache.cached_blocks() == free0 == 32
 
 
 def test_chunked_prefill_equals_full_prefill():
@@ -77,3 +78,41 @@ def test_v_slot_perm_is_permutation():
     for g in range(4):
         for j in range(8):
             assert inv[8 * g + j] == (4 * g + j if j < 4 else 16 + 4 * g + j - 4)
+
+
+def test_prefix_cache_reuse_matches_uncached():
+    from copilot_for_consensus_amd.runtime.prefix_cache import PrefixCache
+    system = [1] + list(range(20, 120))          # 101 shared tokens -> 3 shareable blocks
+    prompts = [system + [5, 6, 7], system + list(range(200, 260)), system + [9]]
+    cfg = get_config("tiny")
+    w = DecoderWeights.random(cfg, "cpu", seed=4)
+    ref = LLMEngine(DecoderModel(w), PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, "cpu"),
+                    prefix_cache=False).generate(prompts, 5, ignore_eos=True)
+    eng = LLMEngine(DecoderModel(w), PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, "cpu"))
+    free0 = eng.kv.pool.num_free()
+    a = eng.generate(prompts, 5, ignore_eos=True)
+    assert a.tokens == ref.tokens
+    assert a.cached_prompt_tokens == 2 * 3 * 32           # dedupe inside the first batch
+    b = eng.generate(prompts[::-1], 5, ignore_eos=True)  # second batch: every prompt hits
+    # prompt 2 (161 tokens) also hits its own 2 further full blocks
+    assert b.tokens == ref.tokens[::-1] and b.cached_prompt_tokens == (3 * 3 + 2) * 32
+    pc: PrefixCache = eng.prefix_cache
+    assert pc.cached_blocks() == 3 + 2                   # system blocks + prompt 2's own full blocks
+    # cached blocks are held back from the pool until an allocation needs them
+    assert eng.kv.pool.num_free() == free0 - pc.cached_blocks()
+    eng.generate([[1] + [3] * 1500], 2, ignore_eos=True)  # needs nearly the whole pool -> evicts
+    assert eng.kv.pool.num_free() + pc.cached_blocks() == free0
+
+
+def test_prefix_cache_invalidates_on_failure():
+    eng = _engine()
+    big = [[1] + [2] * 100] * 30                           # 30 x 4 blocks > 32-block cache
+    try:
+        eng.generate(big, 40, ignore_eos=True)
+        raise AssertionError("expected MemoryError")
+    except MemoryError:
+        pass
+    # nothing leaked, and no entry of the failed call (never prefilled) can be hit
+    assert eng.kv.pool.num_free() == 32 and eng.prefix_cache.cached_blocks() == 0
+    again = eng.generate([[1] + [2] * 100], 3, ignore_eos=True)
+    assert again.cached_prompt_tokens == 0
