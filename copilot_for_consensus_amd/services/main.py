@@ -60,8 +60,10 @@ def main(argv=None) -> int:
         from .ingestion import ingestion_routes
         from .reporting import reporting_routes
         node.start(threaded=True)
+        from ..ui import ui_routes
         app = create_app(node.services["reporting"], extra_routes=reporting_routes)
         ingestion_routes(app, node.services["ingestion"], None)
+        ui_routes(app)
         uvicorn.run(app, host="0.0.0.0", port=args.port or 8080)
         node.stop()
         return 0
@@ -73,6 +75,9 @@ def main(argv=None) -> int:
     elif args.service == "ingestion":
         from .ingestion import ingestion_routes as extra
     app = create_app(svc, extra_routes=extra, auth_dependency=_auth_dep(cfg))
+    if args.service == "reporting":
+        from ..ui import ui_routes
+        ui_routes(app)
     run_service(svc, app, cfg.http_host, args.port or cfg.http_port)
     return 0
 

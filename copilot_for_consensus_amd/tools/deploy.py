@@ -1,0 +1,147 @@
+"""Deployment artefacts derived from the code, so they cannot drift from it.
+
+Parity target: infra/rabbitmq/definitions.json (one topic exchange ``copilot.events``, a durable
+queue per consumer bound to its routing keys), infra/prometheus/prometheus.yml (+ alert rules for
+the documented SLOs, infra/prometheus/alerts/slo_latency.yml) and the docker-compose service
+topology of the reference.  Here:
+
+* RabbitMQ definitions come from each service's ``subscriptions()`` (queue = service name, one
+  binding per subscribed event's routing key) plus one ``<routing key>`` queue per *Failed event
+  for the failed-queue tooling, and dead-letter policies (the reference has none);
+* Prometheus config scrapes every service's ``/metrics`` and the pipeline exporter; alert rules
+  carry the reference's SLO thresholds (parse P95 > 5 s, chunk > 2 s, embed > 10 s, summarize
+  > 30 s, reporting API > 0.5 s);
+* docker-compose: one MI355X node runs the whole pipeline in one process (``node``) with the GPU
+  devices mapped; the per-service form is emitted too for multi-host deployments.
+
+    python -m copilot_for_consensus_amd.tools.deploy --out deploy
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+from ..contracts.events import EVENT_SPECS, EXCHANGE, routing_key_for
+
+SERVICE_PORTS = {"ingestion": 8001, "parsing": 8002, "chunking": 8003, "embedding": 8004, "orchestrator": 8005,
+                 "summarization": 8006, "reporting": 8007, "auth": 8090}
+
+SLO_RULES = [  # (service, histogram, p95 threshold seconds) from the reference's alert rules
+    ("parsing", "parsing_event_processing_seconds", 5.0),
+    ("chunking", "chunking_event_processing_seconds", 2.0),
+    ("embedding", "embedding_event_processing_seconds", 10.0),
+    ("summarization", "summarization_event_processing_seconds", 30.0),
+    ("reporting", "reporting_event_processing_seconds", 0.5),
+]
+
+
+def _subscriptions() -> dict[str, list[str]]:
+    from .gateway import _MOCK_ENV
+    from ..services.node import Node
+    node = Node(env=_MOCK_ENV)
+    return {name: sorted(svc.subscriptions()) for name, svc in node.services.items() if svc.subscriptions()}
+
+
+def rabbitmq_definitions() -> dict:
+    subs = _subscriptions()
+    queues, bindings = [], []
+    dlx = f"{EXCHANGE}.dlx"
+    for svc, events in sorted(subs.items()):
+        queues.append({"name": svc, "vhost": "/", "durable": True, "auto_delete": False,
+                       "arguments": {"x-dead-letter-exchange": dlx, "x-dead-letter-routing-key": f"{svc}.dlq"}})
+        queues.append({"name": f"{svc}.dlq", "vhost": "/", "durable": True, "auto_delete": False, "arguments": {}})
+        bindings.append({"source": dlx, "vhost": "/", "destination": f"{svc}.dlq", "destination_type": "queue",
+                         "routing_key": f"{svc}.dlq", "arguments": {}})
+        for et in events:
+            bindings.append({"source": EXCHANGE, "vhost": "/", "destination": svc, "destination_type": "queue",
+                             "routing_key": routing_key_for(et), "arguments": {}})
+    for et in sorted(EVENT_SPECS):
+        if et.endswith("Failed"):
+            rk = routing_key_for(et)
+            queues.append({"name": rk, "vhost": "/", "durable": True, "auto_delete": False, "arguments": {}})
+            bindings.append({"source": EXCHANGE, "vhost": "/", "destination": rk, "destination_type": "queue",
+                             "routing_key": rk, "arguments": {}})
+    return {"vhosts": [{"name": "/"}],
+            "exchanges": [{"name": EXCHANGE, "vhost": "/", "type": "topic", "durable": True, "auto_delete": False,
+                           "internal": False, "arguments": {}},
+                          {"name": dlx, "vhost": "/", "type": "direct", "durable": True, "auto_delete": False,
+                           "internal": False, "arguments": {}}],
+            "queues": queues, "bindings": bindings,
+            "policies": [{"vhost": "/", "name": "delivery-limit", "pattern": "^(?!.*\\.dlq$).*",
+                          "apply-to": "queues", "definition": {"delivery-limit": 8}, "priority": 0}]}
+
+
+def prometheus_config() -> str:
+    lines = ["global:", "  scrape_interval: 15s", "  evaluation_interval: 15s", "rule_files:", "  - alerts.yml",
+             "scrape_configs:"]
+    for svc, port in SERVICE_PORTS.items():
+        lines += [f"  - job_name: {svc}", "    static_configs:", f"      - targets: ['{svc}:{port}']"]
+    lines += ["  - job_name: pipeline-exporter", "    static_configs:", "      - targets: ['exporter:9502']",
+              "  - job_name: pushgateway", "    honor_labels: true", "    static_configs:",
+              "      - targets: ['pushgateway:9091']"]
+    return "\n".join(lines) + "\n"
+
+
+def alert_rules() -> str:
+    lines = ["groups:", "  - name: slo_latency", "    rules:"]
+    for svc, hist, thr in SLO_RULES:
+        lines += [f"      - alert: {svc.capitalize()}LatencyP95High",
+                  f"        expr: histogram_quantile(0.95, sum(rate({hist}_bucket[5m])) by (le)) > {thr}",
+                  "        for: 5m", "        labels: {severity: warning}",
+                  f"        annotations: {{summary: '{svc} p95 latency above {thr}s'}}"]
+    lines += ["  - name: pipeline_health", "    rules:",
+              "      - alert: DocumentsStuck",
+              "        expr: max(copilot_document_age_seconds{status=~'pending|processing'}) > 3600",
+              "        for: 15m", "        labels: {severity: warning}",
+              "        annotations: {summary: 'documents pending/processing for over an hour'}"]
+    return "\n".join(lines) + "\n"
+
+
+def compose() -> str:
+    gpu = ["    devices: ['/dev/kfd', '/dev/dri']", "    group_add: ['video', 'render']", "    ipc: host",
+           "    shm_size: 64g", "    environment:", "      - HSA_ENABLE_IPC_MODE_LEGACY=0"]
+    base_env = ["      - MESSAGE_BUS_TYPE=rabbitmq", "      - RABBITMQ_HOST=messagebus", "      - DOCUMENT_STORE_TYPE=mongodb",
+                "      - MONGODB_HOST=documentdb", "      - METRICS_TYPE=prometheus"]
+    out = ["services:",
+           "  # single MI355X node: every stage in one process on the in-process bus (recommended)",
+           "  node:", "    image: copilot-for-consensus-amd:latest", "    profiles: ['node']",
+           "    command: python -m copilot_for_consensus_amd.services.main node --port 8080",
+           "    ports: ['8080:8080']"] + gpu + ["      - DOCUMENT_STORE_TYPE=inmemory", "      - MESSAGE_BUS_TYPE=inproc"]
+    out += ["  messagebus:", "    image: rabbitmq:3-management", "    profiles: ['services']",
+            "    volumes: ['./rabbitmq/definitions.json:/etc/rabbitmq/definitions.json:ro']",
+            "    environment:", "      - RABBITMQ_SERVER_ADDITIONAL_ERL_ARGS=-rabbitmq_management load_definitions "
+            "\"/etc/rabbitmq/definitions.json\"",
+            "  documentdb:", "    image: mongo:7", "    profiles: ['services']"]
+    for svc, port in SERVICE_PORTS.items():
+        out += [f"  {svc}:", "    image: copilot-for-consensus-amd:latest", "    profiles: ['services']",
+                f"    command: python -m copilot_for_consensus_amd.services.main {svc} --port {port}",
+                f"    ports: ['{port}:{port}']"]
+        if svc in ("embedding", "summarization", "reporting"):
+            out += gpu + base_env[:]
+        else:
+            out += ["    environment:"] + base_env
+        out += ["    depends_on: [messagebus, documentdb]"]
+    out += ["  prometheus:", "    image: prom/prometheus", "    profiles: ['services', 'node']",
+            "    volumes: ['./prometheus:/etc/prometheus:ro']", "    ports: ['9090:9090']"]
+    return "\n".join(out) + "\n"
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="Write RabbitMQ definitions, Prometheus config/alerts, compose file")
+    ap.add_argument("--out", default="deploy")
+    a = ap.parse_args(argv)
+    out = Path(a.out)
+    (out / "rabbitmq").mkdir(parents=True, exist_ok=True)
+    (out / "prometheus").mkdir(parents=True, exist_ok=True)
+    (out / "rabbitmq" / "definitions.json").write_text(json.dumps(rabbitmq_definitions(), indent=2) + "\n")
+    (out / "prometheus" / "prometheus.yml").write_text(prometheus_config())
+    (out / "prometheus" / "alerts.yml").write_text(alert_rules())
+    (out / "docker-compose.yml").write_text(compose())
+    print(f"wrote deployment files under {out}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -119,3 +119,27 @@ def test_startup_requeue_generic():
                        chunking_strategy="requeue", avg_chunk_size_tokens=0))
     assert n == 1 and default_provider().validate_event(pub.get_events()[0]) == []
     assert "startup_requeue_documents_total" in m.render()
+
+
+def test_ui_served():
+    from fastapi import FastAPI
+    from fastapi.testclient import TestClient
+    from copilot_for_consensus_amd.ui import ui_routes
+    app = FastAPI()
+    ui_routes(app)
+    c = TestClient(app)
+    r = c.get("/ui")
+    assert r.status_code == 200 and "Copilot for Consensus" in r.text and "/api/reports/search" in r.text
+    assert c.get("/", follow_redirects=False).status_code in (302, 307)
+
+
+def test_deploy_artifacts(tmp_path):
+    from copilot_for_consensus_amd.tools.deploy import main, rabbitmq_definitions
+    d = rabbitmq_definitions()
+    b = {(x["destination"], x["routing_key"]) for x in d["bindings"]}
+    assert ("parsing", "archive.ingested") in b and ("summarization", "summarization.requested") in b
+    assert ("parsing.failed", "parsing.failed") in b
+    assert any(e["type"] == "topic" and e["name"] == "copilot.events" for e in d["exchanges"])
+    assert main(["--out", str(tmp_path)]) == 0
+    assert "histogram_quantile(0.95" in (tmp_path / "prometheus" / "alerts.yml").read_text()
+    assert "services.main node" in (tmp_path / "docker-compose.yml").read_text()
