@@ -4,6 +4,8 @@ import json
 import sys
 import time
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -32,10 +34,11 @@ def bench(M, N, K, iters=50):
 
 def main():
     lib = sys.argv[1] if len(sys.argv) > 1 else "default"
+    Ms = [int(a) for a in sys.argv[2:]] or [1, 8, 32, 64, 128, 256, 16384]
     if lib in ("cublas", "cublaslt"):
         torch.backends.cuda.preferred_blas_library(lib)
     res = {}
-    for M in (1, 8, 32, 64, 128, 256, 16384):
+    for M in Ms:
         for name, (N, K) in SHAPES.items():
             us, tbs, tf = bench(M, N, K, iters=20 if M > 1000 else 50)
             res[f"{name}_M{M}"] = (round(us, 1), round(tbs, 2), round(tf, 1))
