@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import json
+import os
 import threading
 from pathlib import Path
 
@@ -140,7 +141,7 @@ def synthetic_bpe(vocab_size: int = 32000, corpus_words: int = 800_000) -> BPETo
             from ..utils.synthetic import SyntheticArchive
             vocab, pairs = train_bpe(SyntheticArchive(seed=777).corpus(corpus_words), vocab_size)
             CACHE_DIR.mkdir(parents=True, exist_ok=True)
-            tmp = path.with_suffix(".tmp")
+            tmp = path.with_suffix(f".{os.getpid()}.tmp")  # per-process: ranks may build it together
             tmp.write_text(json.dumps({"vocab": vocab, "merges": pairs}))
             tmp.replace(path)
             tok = BPETokenizer(vocab, pairs)

@@ -51,7 +51,21 @@ __device__ __forceinline__ bf16x8_t pack_p(const f32x4_t& a, const f32x4_t& b) {
 // The G = Hq/Hkv query heads of the kv-head share every K/V byte (GQA packing: the G heads are
 // the MFMA's B columns).
 // ------------------------------------------------------------------------------------------
-template <int G>
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// 16-byte KV load; NT = non-temporal (streamed once per step: keep it out of the caches' LRU so the
+// shared-prefix blocks and the weights stay resident)
+template <bool NT>
+__device__ __forceinline__ uint4 kv_load(const uint16_t* p) {
+  if constexpr (NT) {
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *reinterpret_cast<const uint4*>(p);
+  }
+}
+
+template <int G, bool NT>
 __global__ void __launch_bounds__(256) paged_decode_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, const int32_t* __restrict__ ctx_lens, float scale_log2, int Hkv,
@@ -99,10 +113,10 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
     for (int st = 0; st < 2; ++st)
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        kk[st * 4 + c] = *reinterpret_cast<const uint4*>(kb + (16 * st + col) * D + 32 * c + 8 * g);
+        kk[st * 4 + c] = kv_load<NT>(kb + (16 * st + col) * D + 32 * c + 8 * g);
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt)
-      vv[dt] = *reinterpret_cast<const uint4*>(vb + (16 * dt + col) * KV_BS + 8 * g);
+      vv[dt] = kv_load<NT>(vb + (16 * dt + col) * KV_BS + 8 * g);
   };
 
   int bi = blk0 + w;
@@ -537,14 +551,17 @@ CFC_API int cfc_paged_decode_attention(const void* q, const void* k_cache, const
   const float sl2 = scale * LOG2E;
 #define DEC_ARGS (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, ctx_lens, sl2, \
     Hkv, max_blocks, part_blocks, P, part_o, part_ml, (uint16_t*)out
+  static const bool nt = [] { const char* e = getenv("CFC_DECODE_NT"); return e && atoi(e) != 0; }();
+#define DEC_CASE(GG) \
+  case GG: \
+    if (nt) paged_decode_kernel<GG, true><<<grid, 256, 0, stream>>>(DEC_ARGS); \
+    else paged_decode_kernel<GG, false><<<grid, 256, 0, stream>>>(DEC_ARGS); \
+    break;
   switch (G) {
-    case 1: paged_decode_kernel<1><<<grid, 256, 0, stream>>>(DEC_ARGS); break;
-    case 2: paged_decode_kernel<2><<<grid, 256, 0, stream>>>(DEC_ARGS); break;
-    case 4: paged_decode_kernel<4><<<grid, 256, 0, stream>>>(DEC_ARGS); break;
-    case 8: paged_decode_kernel<8><<<grid, 256, 0, stream>>>(DEC_ARGS); break;
-    case 16: paged_decode_kernel<16><<<grid, 256, 0, stream>>>(DEC_ARGS); break;
+    DEC_CASE(1) DEC_CASE(2) DEC_CASE(4) DEC_CASE(8) DEC_CASE(16)
     default: return -3;
   }
+#undef DEC_CASE
 #undef DEC_ARGS
   if (P > 1) decode_combine_kernel<<<dim3(Hq, B), 128, 0, stream>>>(part_o, part_ml, P, Hq, (uint16_t*)out);
   return CFC_CHECK_LAUNCH();

@@ -41,8 +41,67 @@ def gemm_scan(out):
         print(f"M={M:6d} layer GEMMs {tot*1e6:8.1f} us  {flops/tot/1e15:.3f} PF/s  {tot*1e6/M:.3f} us/token", flush=True)
 
 
+def kernel_overlap(out):
+    """Decode-like stream (paged attention B=128 ctx 2900 + the 4 projection GEMMs at M=128, per
+    layer) vs prefill-like stream (the 4 projection GEMMs at M=4096) alone and on two streams."""
+    import math
+    B, L, Hq, Hkv, D = 128, 2900, 32, 8, 128
+    nb_per = math.ceil(L / 32) + 1
+    kc = torch.randn(B * nb_per, Hkv, 32, D, device="cuda").bfloat16()
+    vc = torch.randn(B * nb_per, Hkv, D, 32, device="cuda").bfloat16()
+    bt = torch.randperm(B * nb_per, device="cuda").int().view(B, nb_per)
+    ctx = torch.full((B,), L, device="cuda", dtype=torch.int32)
+    q = torch.randn(B, Hq, D, device="cuda").bfloat16()
+    ao = torch.empty_like(q)
+    ws = torch.empty(B * Hq * 4 * (D + 2), device="cuda")
+    shapes = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]
+    Ws = [torch.randn(n, k, device="cuda").bfloat16() for n, k in shapes]
+    xd = [torch.randn(128, k, device="cuda").bfloat16() for _, k in shapes]
+    xp = [torch.randn(4096, k, device="cuda").bfloat16() for _, k in shapes]
+
+    def dec(layers=32):
+        for _ in range(layers):
+            for x, w in zip(xd, Ws):
+                F.linear(x, w)
+            K.paged_decode_attention(q, kc, vc, bt, ctx, 1 / math.sqrt(D), out=ao, part_blocks=26, workspace=ws)
+
+    def pre(layers=8):
+        for _ in range(layers):
+            for x, w in zip(xp, Ws):
+                F.linear(x, w)
+
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for fn in (dec, pre):
+        fn()
+    torch.cuda.synchronize()
+
+    def timed(fn):
+        t = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t
+
+    def both():
+        with torch.cuda.stream(s1):
+            dec()
+        with torch.cuda.stream(s2):
+            pre()
+
+    a, b = timed(dec), timed(pre)
+    c = timed(both)
+    out["overlap_decode_alone_ms"] = round(a * 1e3, 2)
+    out["overlap_prefill_alone_ms"] = round(b * 1e3, 2)
+    out["overlap_both_ms"] = round(c * 1e3, 2)
+    out["overlap_saved_frac_of_prefill"] = round((a + b - c) / b, 3)
+    print(f"decode-like {a*1e3:.2f} ms, prefill-like {b*1e3:.2f} ms, both on 2 streams {c*1e3:.2f} ms", flush=True)
+
+
 def main():
     res = {}
+    kernel_overlap(res)
+    if os.environ.get("OVERLAP_ONLY"):
+        print(json.dumps(res, indent=1))
+        return
     gemm_scan(res)
     cfg = get_config("mistral-7b")
     w = DecoderWeights.random(cfg, "cuda", seed=1)
