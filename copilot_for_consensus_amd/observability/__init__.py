@@ -18,6 +18,7 @@ import collections
 import contextlib
 import json
 import logging
+import os
 import sys
 import threading
 import time
@@ -304,10 +305,21 @@ def create_error_reporter(cfg=None, **overrides) -> ErrorReporter:
 
 # ------------------------------------------------------------------------------------- tracing
 
-try:  # pragma: no cover - only on ROCm builds that ship roctx python bindings
-    from roctx import rangePop as _rpop, rangePush as _rpush  # type: ignore
-except Exception:  # noqa: BLE001
-    _rpush = _rpop = None
+def _load_roctx():
+    """roctx ranges (shown by ``rocprofv3 --marker-trace``) through the ROCm tracer library."""
+    import ctypes
+    import os
+    for name in ("libroctx64.so", os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib", "libroctx64.so")):
+        try:
+            lib = ctypes.CDLL(name)
+            lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+            return (lambda n: lib.roctxRangePushA(n.encode())), (lambda: lib.roctxRangePop())
+        except (OSError, AttributeError):
+            continue
+    return None, None
+
+
+_rpush, _rpop = _load_roctx() if os.environ.get("CFC_ROCTX", "1") != "0" else (None, None)
 
 
 @contextlib.contextmanager

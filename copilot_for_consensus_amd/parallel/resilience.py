@@ -1,0 +1,166 @@
+"""Failure detection and forward progress for multi-GPU summarization workers (SURVEY §5.3 rebuild:
+per-GPU heartbeat watchdog, requeue of a dead worker's in-flight threads, RCCL timeouts that raise
+instead of hanging).
+
+All state lives in a ``torch.distributed`` key-value Store (the job's TCPStore under torchrun, a
+FileStore / HashStore otherwise), so any surviving rank -- or an external supervisor -- can see it:
+
+* :class:`Heartbeat` -- a daemon thread per rank writing ``hb/<rank>`` = wall time every
+  ``interval`` seconds, plus the rank's GPU step counter so a hung kernel (process alive, no
+  progress) is distinguishable from a dead process;
+* :class:`WorkLedger` -- which thread ids each rank owns and which are done;
+* :class:`Watchdog` -- ranks whose heartbeat is older than ``timeout`` (or whose progress counter
+  has not moved for ``stall_timeout``) are dead; :meth:`reclaim` redistributes their unfinished
+  thread ids over the live ranks with the same LPT balancing the orchestrator uses;
+* :func:`configure_collective_timeouts` -- RCCL async error handling + a finite collective timeout,
+  so a peer that dies mid-all-reduce turns into an exception on the survivors (which then abort
+  the communicator and restart through torchrun's elastic agent, resuming from the ledger).
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+import time
+from typing import Iterable
+
+from .dp import balanced_shard
+
+
+def _get(store, key: str, default=None):
+    try:
+        if hasattr(store, "check") and not store.check([key]):
+            return default
+        return store.get(key)
+    except Exception:  # missing key (stores without check) / store unreachable
+        return default
+
+
+class Heartbeat:
+    def __init__(self, store, rank: int, interval: float = 2.0, clock=time.time):
+        self.store, self.rank, self.interval, self.clock = store, rank, interval, clock
+        self.progress = 0
+        self._stop = threading.Event()
+        self._t: threading.Thread | None = None
+
+    def beat(self) -> None:
+        self.store.set(f"hb/{self.rank}", json.dumps({"t": self.clock(), "progress": self.progress,
+                                                       "pid": os.getpid()}))
+
+    def tick(self, n: int = 1) -> None:
+        """Record forward progress (e.g. one decode step / one finished batch)."""
+        self.progress += n
+
+    def start(self) -> "Heartbeat":
+        self.beat()
+
+        def loop():
+            while not self._stop.wait(self.interval):
+                try:
+                    self.beat()
+                except Exception:  # store gone: the job is ending
+                    return
+
+        self._t = threading.Thread(target=loop, name=f"heartbeat-{self.rank}", daemon=True)
+        self._t.start()
+        return self
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._t is not None:
+            self._t.join(timeout=self.interval * 2)
+
+
+class WorkLedger:
+    def __init__(self, store):
+        self.store = store
+
+    def assign(self, rank: int, items: Iterable[str]) -> None:
+        cur = self.owned(rank)
+        cur.extend(i for i in items if i not in cur)
+        self.store.set(f"ledger/own/{rank}", json.dumps(cur))
+
+    def owned(self, rank: int) -> list[str]:
+        v = _get(self.store, f"ledger/own/{rank}")
+        return json.loads(v) if v else []
+
+    def complete(self, rank: int, items: Iterable[str]) -> None:
+        done = set(self.done(rank)) | set(items)
+        self.store.set(f"ledger/done/{rank}", json.dumps(sorted(done)))
+
+    def done(self, rank: int) -> list[str]:
+        v = _get(self.store, f"ledger/done/{rank}")
+        return json.loads(v) if v else []
+
+    def pending(self, rank: int) -> list[str]:
+        d = set(self.done(rank))
+        return [i for i in self.owned(rank) if i not in d]
+
+    def release(self, rank: int) -> list[str]:
+        """Take the unfinished items away from ``rank`` (after it was declared dead)."""
+        p = self.pending(rank)
+        self.store.set(f"ledger/own/{rank}", json.dumps(self.done(rank)))
+        return p
+
+
+class Watchdog:
+    def __init__(self, store, world: int, timeout: float = 30.0, stall_timeout: float | None = None,
+                 clock=time.time):
+        self.store, self.world, self.timeout, self.stall_timeout, self.clock = store, world, timeout, stall_timeout, clock
+        self._last_progress: dict[int, tuple[int, float]] = {}
+
+    def status(self, rank: int) -> dict:
+        v = _get(self.store, f"hb/{rank}")
+        if v is None:
+            return {"alive": False, "reason": "no heartbeat"}
+        hb = json.loads(v)
+        now = self.clock()
+        if now - hb["t"] > self.timeout:
+            return {"alive": False, "reason": f"heartbeat {now - hb['t']:.1f}s old", **hb}
+        if self.stall_timeout is not None:
+            prev = self._last_progress.get(rank)
+            if prev is None or hb["progress"] != prev[0]:
+                self._last_progress[rank] = (hb["progress"], now)
+            elif now - prev[1] > self.stall_timeout:
+                return {"alive": False, "reason": f"no progress for {now - prev[1]:.1f}s", **hb}
+        return {"alive": True, **hb}
+
+    def dead_ranks(self) -> list[int]:
+        return [r for r in range(self.world) if not self.status(r)["alive"]]
+
+    def reclaim(self, ledger: WorkLedger, costs: dict[str, float] | None = None) -> dict[int, list[str]]:
+        """Move every dead rank's unfinished items to the live ranks; returns {rank: new items}."""
+        dead = self.dead_ranks()
+        live = [r for r in range(self.world) if r not in dead]
+        if not dead or not live:
+            return {}
+        orphans = [i for r in dead for i in ledger.release(r)]
+        bins = balanced_shard([(costs or {}).get(i, 1.0) for i in orphans], len(live))
+        out = {}
+        for r, idx in zip(live, bins):
+            items = [orphans[j] for j in idx]
+            if items:
+                ledger.assign(r, items)
+                out[r] = items
+        return out
+
+
+def configure_collective_timeouts(timeout_s: int = 300) -> dict:
+    """Environment for RCCL so a lost peer raises on the survivors instead of hanging forever
+    (must run before init_process_group); returns the settings applied."""
+    env = {"TORCH_NCCL_ASYNC_ERROR_HANDLING": "1", "TORCH_NCCL_DUMP_ON_TIMEOUT": "0",
+           "TORCH_NCCL_HEARTBEAT_TIMEOUT_SEC": str(max(60, timeout_s))}
+    for k, v in env.items():
+        os.environ.setdefault(k, v)
+    return {**env, "collective_timeout_s": timeout_s}
+
+
+def abort_process_group() -> None:
+    """Tear the communicator down after a peer failure (the elastic agent then restarts the
+    group; the ledger lets the restarted ranks resume where the failed ones stopped)."""
+    import torch.distributed as dist
+    if dist.is_initialized():
+        try:
+            dist.destroy_process_group()
+        except Exception:
+            pass

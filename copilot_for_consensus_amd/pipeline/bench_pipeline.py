@@ -7,6 +7,8 @@ import time
 
 import torch
 
+from ..observability import span
+
 
 @dataclasses.dataclass
 class StepResult:
@@ -90,7 +92,8 @@ class BenchPipeline:
             return self._prepare_tp(t0, step)
         if self.rag is None:
             return t0, None, self._synthetic_prompts(self.threads_per_step), {}
-        return self._prepare_rag(t0, step)
+        with span(f"bench.prepare.step{step}"):
+            return self._prepare_rag(t0, step)
 
     def _prepare_tp(self, t0, step):
         import torch.distributed as dist
@@ -136,7 +139,8 @@ class BenchPipeline:
                         start_at = time.perf_counter() + max(0.0, self._last_gen_s - 2.0 * self._last_prep_s - 0.25)
                     fut = pool.submit(self._prepare, steps[n + 1], start_at)
                 tg = time.perf_counter()
-                res = self.engine.generate(prompts, self.max_new, temperature=0.0, ignore_eos=True)
+                with span(f"bench.llm.step{step}"):
+                    res = self.engine.generate(prompts, self.max_new, temperature=0.0, ignore_eos=True)
                 self._last_gen_s = time.perf_counter() - tg
                 self._last_prep_s = sum(v for k, v in stages.items())
                 stages["prefill"] = res.prefill_s

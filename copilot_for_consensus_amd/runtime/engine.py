@@ -21,6 +21,7 @@ import time
 
 import torch
 
+from ..observability import span
 from ..ops import kernels as K
 from ..ops.reference import KV_BLOCK
 from .kv_cache import PagedKVCache, blocks_needed
@@ -220,7 +221,8 @@ class LLMEngine:
             if sync:
                 torch.cuda.synchronize(self.device)
             t0 = time.perf_counter()
-            first = self._prefill(prompts, tables, temperature, seed, start)
+            with span("llm.prefill"):
+                first = self._prefill(prompts, tables, temperature, seed, start)
             if sync:
                 torch.cuda.synchronize(self.device)
             t1 = time.perf_counter()
@@ -245,6 +247,8 @@ class LLMEngine:
             st.done.copy_(torch.isin(f, st.stop_ids.cpu()).to(torch.int32) if stop_ids else torch.zeros(B, dtype=torch.int32))
 
             steps = 0
+            rng = span("llm.decode")
+            rng.__enter__()
             if self.use_graph and (st.graph is None or st.graph[1:] != (part_blocks, temperature, seed)):
                 self._capture(st, part_blocks, temperature, seed)
             for i in range(1, max_new_tokens):
@@ -258,6 +262,7 @@ class LLMEngine:
             tokens = st.tokens.cpu()
             if sync:
                 torch.cuda.synchronize(self.device)
+            rng.__exit__(None, None, None)
             t2 = time.perf_counter()
             ok = True
         finally:

@@ -411,6 +411,8 @@ class SummarizationService(BaseService):
         summaries = retry_with_backoff(lambda: self.summarizer.summarize_batch(threads), self.max_retries,
                                        self.retry_delay)
         self.metrics.observe("summarization_latency_seconds", time.perf_counter() - t0)
+        for k, v in (getattr(self.summarizer, "last_stats", None) or {}).items():
+            self.metrics.gauge(f"summarization_gpu_{k}", float(v))
         out = []
         for (tid, ctx, _), s in zip(prepared, summaries):
             cites = format_citations(ctx["chunks"], self.citation_count)

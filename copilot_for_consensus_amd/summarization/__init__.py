@@ -102,6 +102,21 @@ class HipLLMSummarizer(Summarizer):
         self.max_batch = int(max_batch)
         self.ignore_eos = ignore_eos
         self.context_limit = cfg.max_positions - self.max_new_tokens
+        self.last_stats: dict = {}
+
+    def gpu_stats(self, res) -> dict:
+        """Engine/GPU figures of the last batch (tokens/s, TTFT, HBM use)."""
+        gen = sum(len(t) for t in res.tokens)
+        st = {"ttft_seconds": res.ttft_s, "prefill_seconds": res.prefill_s, "decode_seconds": res.decode_s,
+              "decode_tokens_per_second": gen / res.decode_s if res.decode_s > 0 else 0.0,
+              "prefill_tokens_per_second": sum(res.prompt_lens) / res.prefill_s if res.prefill_s > 0 else 0.0,
+              "prefix_cached_tokens": res.cached_prompt_tokens, "batch_threads": len(res.tokens)}
+        if torch.cuda.is_available() and self.kv.device.type == "cuda":
+            free, total = torch.cuda.mem_get_info(self.kv.device)
+            st["hbm_used_bytes"] = total - free
+            st["hbm_total_bytes"] = total
+            st["kv_cache_bytes"] = self.kv.nbytes()
+        return st
 
     def _tokens(self, prompt: str) -> list[int]:
         ids = self.tokenizer.encode(prompt)
@@ -119,6 +134,7 @@ class HipLLMSummarizer(Summarizer):
             res = self.engine.generate(ids, self.max_new_tokens, temperature=self.temperature,
                                        ignore_eos=self.ignore_eos)
             ms = int(1000 * (time.perf_counter() - t0))
+            self.last_stats = self.gpu_stats(res)
             for t, p, g in zip(part, ids, res.tokens):
                 text = self.tokenizer.decode(g).strip() or "(empty summary)"
                 out.append(Summary(t.thread_id, text, [], self.backend, self.model, len(p), len(g), ms))

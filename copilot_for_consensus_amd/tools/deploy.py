@@ -99,6 +99,33 @@ def alert_rules() -> str:
     return "\n".join(lines) + "\n"
 
 
+def grafana_dashboard() -> dict:
+    """One dashboard over the pipeline + GPU metrics (the reference ships 11 Grafana JSON files;
+    the panels here cover its service-health, latency and document-state views plus the MI355X
+    engine figures)."""
+    def panel(i, title, expr, unit="short", kind="timeseries"):
+        return {"id": i, "type": kind, "title": title, "gridPos": {"h": 8, "w": 12, "x": 12 * (i % 2), "y": 8 * (i // 2)},
+                "fieldConfig": {"defaults": {"unit": unit}, "overrides": []},
+                "targets": [{"expr": e, "refId": chr(65 + j)} for j, e in enumerate([expr] if isinstance(expr, str) else expr)]}
+    ps = [
+        panel(0, "Threads summarized / s", "sum(rate(summarization_tokens_total{type='completion'}[5m])) / 512"),
+        panel(1, "Summarization batch latency p50 / p95",
+              ["histogram_quantile(0.5, sum(rate(summarization_latency_seconds_bucket[5m])) by (le))",
+               "histogram_quantile(0.95, sum(rate(summarization_latency_seconds_bucket[5m])) by (le))"], "s"),
+        panel(2, "Decode tokens / s (GPU)", "summarization_gpu_decode_tokens_per_second"),
+        panel(3, "Prefill tokens / s (GPU)", "summarization_gpu_prefill_tokens_per_second"),
+        panel(4, "Time to first token", "summarization_gpu_ttft_seconds", "s"),
+        panel(5, "HBM used", ["summarization_gpu_hbm_used_bytes", "summarization_gpu_kv_cache_bytes"], "bytes"),
+        panel(6, "Stage latency p95", [f"histogram_quantile(0.95, sum(rate({h}_bucket[5m])) by (le))"
+                                       for _, h, _ in SLO_RULES], "s"),
+        panel(7, "Documents by status", "sum by (collection, status) (copilot_document_status_count)"),
+        panel(8, "Chunks awaiting embedding", "copilot_chunks_embedding_status_count{embedding_generated='false'}"),
+        panel(9, "Prefix-cache hit tokens / batch", "summarization_gpu_prefix_cached_tokens"),
+    ]
+    return {"title": "Copilot for Consensus - MI355X", "uid": "cfc-mi355x", "schemaVersion": 39, "version": 1,
+            "time": {"from": "now-6h", "to": "now"}, "refresh": "30s", "panels": ps}
+
+
 def compose() -> str:
     gpu = ["    devices: ['/dev/kfd', '/dev/dri']", "    group_add: ['video', 'render']", "    ipc: host",
            "    shm_size: 64g", "    environment:", "      - HSA_ENABLE_IPC_MODE_LEGACY=0"]
@@ -139,6 +166,8 @@ def main(argv=None) -> int:
     (out / "prometheus" / "prometheus.yml").write_text(prometheus_config())
     (out / "prometheus" / "alerts.yml").write_text(alert_rules())
     (out / "docker-compose.yml").write_text(compose())
+    (out / "grafana" / "dashboards").mkdir(parents=True, exist_ok=True)
+    (out / "grafana" / "dashboards" / "copilot-mi355x.json").write_text(json.dumps(grafana_dashboard(), indent=2) + "\n")
     print(f"wrote deployment files under {out}")
     return 0
 

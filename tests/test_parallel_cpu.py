@@ -188,3 +188,45 @@ def test_tp2_bench_pipeline_leader_broadcasts_prompts():
     lead, fol = outs
     assert [t for t, _, _ in lead] == [2, 2] and [t for t, _, _ in fol] == [0, 0]
     assert [x[1:] for x in lead] == [x[1:] for x in fol]  # same prompts, same generation length
+
+
+# ---------------------------------------------------------------- failure detection / recovery
+def test_watchdog_detects_dead_rank_and_reclaims_work():
+    from copilot_for_consensus_amd.parallel.resilience import Heartbeat, Watchdog, WorkLedger
+    store = dist.HashStore()
+    now = [1000.0]
+    clock = lambda: now[0]  # noqa: E731
+    hbs = [Heartbeat(store, r, clock=clock) for r in range(3)]
+    for h in hbs:
+        h.beat()
+    ledger = WorkLedger(store)
+    for r in range(3):
+        ledger.assign(r, [f"t{r}-{i}" for i in range(4)])
+    ledger.complete(1, ["t1-0"])
+    wd = Watchdog(store, 3, timeout=10.0, stall_timeout=20.0, clock=clock)
+    assert wd.dead_ranks() == []
+    now[0] += 15.0                      # rank 1 stops beating (process died)
+    hbs[0].beat(); hbs[2].beat()
+    assert wd.dead_ranks() == [1]
+    moved = wd.reclaim(ledger)
+    assert sorted(i for v in moved.values() for i in v) == ["t1-1", "t1-2", "t1-3"]
+    assert set(moved) <= {0, 2} and ledger.pending(1) == []
+    assert set(ledger.pending(0)) >= {"t0-0"} and len(ledger.pending(0)) + len(ledger.pending(2)) == 11
+    # hung-but-alive: heartbeat keeps coming, progress counter stuck -> declared dead after stall_timeout
+    for _ in range(3):
+        now[0] += 8.0
+        hbs[0].tick(); hbs[0].beat(); hbs[2].beat()
+    assert wd.status(2)["alive"] is False and "no progress" in wd.status(2)["reason"]
+    assert wd.status(0)["alive"] is True
+
+
+def test_heartbeat_thread_and_timeouts():
+    import time as _t
+    from copilot_for_consensus_amd.parallel.resilience import Heartbeat, Watchdog, configure_collective_timeouts
+    store = dist.HashStore()
+    hb = Heartbeat(store, 0, interval=0.05).start()
+    _t.sleep(0.2)
+    assert Watchdog(store, 1, timeout=1.0).dead_ranks() == []
+    hb.stop()
+    env = configure_collective_timeouts(120)
+    assert os.environ["TORCH_NCCL_ASYNC_ERROR_HANDLING"] == "1" and env["collective_timeout_s"] == 120
