@@ -87,7 +87,7 @@ class HipEncoderProvider(EmbeddingProvider):
         """[n, dim] fp32 L2-normalised embeddings, on the encoder's device."""
         for t in texts:
             _check_text(t)
-        ids = [self.tokenizer.encode(t) for t in texts]
+        ids = self.tokenizer.encode_batch(texts)
         return self.model.encode_ids(ids, max_tokens_per_forward=self.max_tokens_per_forward)
 
     def embed_batch(self, texts: list[str]) -> list[list[float]]:

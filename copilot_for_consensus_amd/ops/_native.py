@@ -54,6 +54,8 @@ _RUNTIME_SIGS = {
     "cfc_bpe_encode": [P, ctypes.c_char_p, I, P, I],
     "cfc_bpe_decode": [P, P, I, ctypes.c_char_p, I],
     "cfc_bpe_train": [ctypes.c_char_p, I, I, P, P, I],
+    "cfc_bpe_encode_batch": [P, ctypes.c_char_p, P, I, I, P, P, I],
+    "cfc_wp_encode_batch": [P, ctypes.c_char_p, P, I, I, P, P, I],
     "cfc_wp_create": [I, I, I, I],
     "cfc_wp_destroy": [P],
     "cfc_wp_add_token": [P, ctypes.c_char_p, I, I],

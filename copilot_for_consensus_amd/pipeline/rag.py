@@ -203,7 +203,7 @@ class RagPipeline:
         st["select"] = time.perf_counter() - t
 
         t = time.perf_counter()
-        prompts = [self._clip(self.bpe.encode(p)) for p in texts]
+        prompts = [self._clip(ids) for ids in self.bpe.encode_batch(texts)]
         st["tokenize"] = time.perf_counter() - t
         return PreparedBatch(prepared_threads, prompts, texts, sels, ctxs, st, aid)
 

@@ -30,6 +30,23 @@ def _c(s: str) -> tuple[bytes, int]:
     return b, len(b)
 
 
+ENCODE_THREADS = max(1, min(16, int(os.environ.get("CFC_TOKENIZER_THREADS", "0")) or (os.cpu_count() or 1)))
+
+
+def _batch(fn, handle, texts: list[str], cap: int, truncate: bool = False) -> list[list[int] | None]:
+    """Thread-parallel C++ encode of many texts.  Results longer than ``cap`` come back as None
+    (caller re-encodes them singly) unless ``truncate``, which keeps their first ``cap`` ids."""
+    bs = [t.encode("utf-8") for t in texts]
+    offs = np.zeros(len(bs) + 1, dtype=np.int64)
+    np.cumsum([len(b) for b in bs], out=offs[1:])
+    buf = b"".join(bs)
+    out = np.empty((len(bs), cap), dtype=np.int32)
+    lens = np.empty(len(bs), dtype=np.int32)
+    fn(handle, buf, offs.ctypes.data, len(bs), cap, out.ctypes.data, lens.ctypes.data,
+       min(ENCODE_THREADS, max(1, len(bs) // 4)))
+    return [out[i, :min(lens[i], cap)].tolist() if (truncate or lens[i] <= cap) else None for i in range(len(bs))]
+
+
 class BPETokenizer:
     def __init__(self, vocab: list[str], merges: list[tuple[int, int]], bos_id: int = 1, eos_id: int = 2):
         self.vocab = vocab
@@ -68,6 +85,16 @@ class BPETokenizer:
                 k = self._lib.cfc_bpe_encode(self._h, b, n, self._buf.ctypes.data, len(self._buf))
             ids = self._buf[:k].tolist()
         return ([self.bos_id] + ids) if add_bos else ids
+
+    def encode_batch(self, texts: list[str], add_bos: bool = True, cap: int = 16384) -> list[list[int]]:
+        res = _batch(self._lib.cfc_bpe_encode_batch, self._h, texts, cap)
+        out = []
+        for t, ids in zip(texts, res):
+            if ids is None:
+                out.append(self.encode(t, add_bos))
+            else:
+                out.append(([self.bos_id] + ids) if add_bos else ids)
+        return out
 
     def decode(self, ids: list[int]) -> str:
         arr = np.asarray([i for i in ids if i not in (self.bos_id, self.eos_id)], dtype=np.int32)
@@ -186,7 +213,10 @@ class WordPieceTokenizer:
         return [self.cls_id] + ids + [self.sep_id]
 
     def encode_batch(self, texts: list[str], max_length: int | None = None) -> list[list[int]]:
-        return [self.encode(t, max_length) for t in texts]
+        L = max_length or self.max_length
+        # truncation makes every result fit: ask for L-2 pieces, longer texts are simply cut
+        res = _batch(self._lib.cfc_wp_encode_batch, self._h, texts, max(1, L - 2), truncate=True)
+        return [[self.cls_id] + ids + [self.sep_id] for ids in res]
 
     @classmethod
     def from_vocab_txt(cls, path, **kw) -> "WordPieceTokenizer":

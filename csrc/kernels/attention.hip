@@ -410,6 +410,199 @@ __global__ void __launch_bounds__(512, MINW) prefill_paged_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// Prefill v4: 4 waves x 32 query rows on v_mfma_f32_32x32x16_bf16 (128-row tiles, as v3).
+//   * S^T = K . Q^T per 32-key half-tile: A = K rows from LDS, B = Q^T from registers (8 k-steps
+//     over D = 128).  C/D of 32x32: col = lane & 31 (query), row = 8(i>>2) + 4(lane>>5) + (i&3)
+//     (key), so each lane owns one query row's scores for 16 of every 32 keys (the other 16 in
+//     lane ^ 32): row max / sum = 31 local ops + one xor-32 shuffle.
+//   * O^T = V^T . P^T: the S^T accumulator IS the P^T B-operand (guide §3: k-step s of a 32-key
+//     tile = registers 8s..8s+7, key order 16s + 8(j>>2) + 4h + (j&3)); the V^T LDS image stores
+//     each d row's 64 keys in exactly that slot order, so the A fragment is one ds_read_b128.
+//     The cache's V^T blocks are in the decode (16x16) slot order; the permutation to the 32x32
+//     order is applied while writing the LDS image (two 8-byte stores per 16-byte load).
+//   * K / V^T tiles (64 keys) double-buffered in LDS, register-staged (loads for tile t+1 issued
+//     before tile t's MFMAs, LDS writes after), one barrier per tile; deferred rescale as in v3.
+//   * vs v3 (16x16x32, 16 rows/wave): every LDS fragment byte now feeds twice the FLOPs.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ f32x16_t mfma32(bf16x8_t a, bf16x8_t b, f32x16_t c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// V^T image: row d (64 keys = 128 B), 16-byte chunk c at d*128 + ((c ^ (d & 7)) << 4)
+__device__ __forceinline__ int v4_off(int d, int c) { return d * 128 + ((c ^ (d & 7)) << 4); }
+
+template <int MINW>
+__global__ void __launch_bounds__(256, MINW) prefill_paged_kernel_v4(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    const int32_t* __restrict__ block_tables, const int32_t* __restrict__ cu_q, const int32_t* __restrict__ ctx_lens,
+    const int32_t* __restrict__ tile_seq, const int32_t* __restrict__ tile_q0, float scale_log2, int Hq, int Hkv,
+    int max_blocks, uint16_t* __restrict__ out) {
+  constexpr int D = 128;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // LDS: [K buf0 16K][K buf1 16K][V buf0 16K][V buf1 16K]
+  const int t = blockIdx.x, hq = blockIdx.y;
+  const int G = Hq / Hkv, hk = hq / G;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
+  const int l32 = lane & 31, hi = lane >> 5;
+  const int s = tile_seq[t], qs = tile_q0[t];
+  const int q_begin = cu_q[s], q_len = cu_q[s + 1] - q_begin;
+  const int ctx = ctx_lens[s];
+  const int pos_base = ctx - q_len;
+  const int row_last = min(qs + PF_ROWS - 1, q_len - 1);
+  const int kend = pos_base + row_last + 1;
+  const int ntiles = (kend + PF_KT - 1) / PF_KT;
+  const int32_t* bt = block_tables + (size_t)s * max_blocks;
+
+  const int my_row = qs + 32 * w + l32;
+  const int my_pos = pos_base + my_row;
+  const int wave_min_pos = pos_base + qs + 32 * w;
+  // Q^T B-operand, pre-scaled into the exp2 domain: k-step ks holds Q[row][16ks + 8hi .. +7]
+  bf16x8_t qf[8];
+  {
+    const int rr = min(my_row, q_len - 1);
+    const uint16_t* qr = q + ((size_t)(q_begin + rr) * Hq + hq) * D;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(qr + 16 * ks + 8 * hi), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= scale_log2;
+      qf[ks] = as_bf16x8(pack8(f));
+    }
+  }
+
+  // staging: 1024 16-B pieces of K + 1024 of V per tile, 4 + 4 per thread
+  uint4 kst[4], vst[4];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = tid + 256 * i;
+      {  // K: row = id >> 4 (key in tile), chunk = id & 15
+        const int row = id >> 4, ch = id & 15, key = kt * PF_KT + row;
+        kst[i] = key < kend ? *reinterpret_cast<const uint4*>(
+                                  kc + (((size_t)bt[key / KV_BS] * Hkv + hk) * KV_BS + (key % KV_BS)) * D + ch * 8)
+                            : make_uint4(0, 0, 0, 0);
+      }
+      {  // V^T: block bi = id >> 9, d = (id >> 2) & 127, cache chunk g = id & 3 (slots 8g..8g+7)
+        const int bi = id >> 9, d = (id >> 2) & 127, g = id & 3;
+        const int key0 = kt * PF_KT + bi * KV_BS;
+        vst[i] = key0 < kend ? *reinterpret_cast<const uint4*>(
+                                   vc + (((size_t)bt[key0 / KV_BS] * Hkv + hk) * D + d) * KV_BS + g * 8)
+                             : make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto lwrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int id = tid + 256 * i;
+      *reinterpret_cast<uint4*>(smem + buf * 16384 + k_lds_off(id >> 4, id & 15)) = kst[i];
+      // cache slots 8g..8g+3 hold keys 4g..4g+3 and 8g+4..8g+7 hold keys 16+4g..16+4g+3; in the
+      // 32x32 order key k of a 32-block sits at slot 16(k>>4) + 8((k>>2)&1) + 4((k&15)>>3) + (k&3)
+      const int bi = id >> 9, d = (id >> 2) & 127, g = id & 3;
+      const int base = 32 * bi + 8 * (g & 1) + 4 * (g >> 1);        // slot of key 4g (s = 0)
+      char* vrow = smem + 32768 + buf * 16384;
+      const uint2 lo = make_uint2(vst[i].x, vst[i].y), hi2 = make_uint2(vst[i].z, vst[i].w);
+      *reinterpret_cast<uint2*>(vrow + v4_off(d, base >> 3) + (base & 7) * 2) = lo;
+      *reinterpret_cast<uint2*>(vrow + v4_off(d, (base + 16) >> 3) + ((base + 16) & 7) * 2) = hi2;
+    }
+  };
+
+  f32x16_t o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  gload(0);
+  lwrite(0);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < ntiles;
+    if (more) gload(kt + 1);
+
+    const char* kb = smem + cur * 16384;
+    const char* vb = smem + 32768 + cur * 16384;
+    const int key0 = kt * PF_KT;
+    if (key0 <= wave_min_pos + 31) {
+      f32x16_t sc[2];
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[hf][r] = 0.f;
+        const int row = 32 * hf + l32;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks)
+          sc[hf] = mfma32(as_bf16x8(*reinterpret_cast<const uint4*>(kb + k_lds_off(row, 2 * ks + hi))), qf[ks], sc[hf]);
+      }
+      if (key0 + PF_KT - 1 > wave_min_pos) {  // diagonal tile: causal mask
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (key0 + 32 * hf + 8 * (r >> 2) + 4 * hi + (r & 3) > my_pos) sc[hf][r] = -INFINITY;
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sc[hf][r]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      if (!__all(tmax - m <= RESCALE_THR)) {
+        const float mn = fmaxf(m, tmax);
+        const float mref = mn == -INFINITY ? 0.f : mn;
+        const float alpha = exp2f(m - mref);
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+        m = mn;
+      }
+      const float mref = m == -INFINITY ? 0.f : m;
+      float rs = 0.f;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { const float e = exp2f(sc[hf][r] - mref); sc[hf][r] = e; rs += e; }
+      rs += __shfl_xor(rs, 32, 64);
+      l += rs;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          uint4 u;
+          u.x = pack2bf(sc[hf][8 * ss + 0], sc[hf][8 * ss + 1]);
+          u.y = pack2bf(sc[hf][8 * ss + 2], sc[hf][8 * ss + 3]);
+          u.z = pack2bf(sc[hf][8 * ss + 4], sc[hf][8 * ss + 5]);
+          u.w = pack2bf(sc[hf][8 * ss + 6], sc[hf][8 * ss + 7]);
+          const bf16x8_t pf = as_bf16x8(u);
+          const int c = 4 * hf + 2 * ss + hi;     // V^T chunk of slots 32hf + 16ss + 8hi .. +7
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt)
+            o[dt] = mfma32(as_bf16x8(*reinterpret_cast<const uint4*>(vb + v4_off(32 * dt + l32, c))), pf, o[dt]);
+        }
+    }
+    if (more) lwrite(cur ^ 1);
+    __syncthreads();
+  }
+
+  if (my_row < q_len) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    uint16_t* orow = out + ((size_t)(q_begin + my_row) * Hq + hq) * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {   // registers 4rg..4rg+3 = d 32dt + 8rg + 4hi + 0..3
+        uint2 pk;
+        pk.x = pack2bf(o[dt][4 * rg] * inv, o[dt][4 * rg + 1] * inv);
+        pk.y = pack2bf(o[dt][4 * rg + 2] * inv, o[dt][4 * rg + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * rg + 4 * hi) = pk;
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Varlen bidirectional encoder attention (BERT family), D in {32, 64}, S <= 512.
 // Input qkv is the fused projection output [T, 3*H*D] (q | k | v, head-major inside each).
 // grid = (n_tiles, H); block = 256 = 4 waves x 16 query rows.  The WHOLE key/value range of
@@ -576,11 +769,13 @@ CFC_API int cfc_prefill_attention(const void* q, const void* k_cache, const void
   if (head_dim != 128 || Hq % Hkv != 0) return -1;
   if (n_tiles <= 0) return 0;
   const size_t lds = 65536;
-  // variant 0: <=128 VGPRs (2 workgroups / CU); variant 1: <=256 VGPRs (1 workgroup / CU)
+  // variant 0: v3 <=128 VGPRs (2 workgroups / CU); 1: v3 <=256 VGPRs; 2/3: v4 (32x32 MFMA, 2 / 1 WG per CU)
   static const int variant = [] { const char* e = getenv("CFC_PREFILL_VARIANT"); return e ? atoi(e) : 0; }();
 #define PF_ARGS (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, cu_q, ctx_lens, \
     tile_seq, tile_q0, scale * LOG2E, Hq, Hkv, max_blocks, (uint16_t*)out
   if (variant == 1) prefill_paged_kernel<2><<<dim3(n_tiles, Hq), 512, lds, stream>>>(PF_ARGS);
+  else if (variant == 2) prefill_paged_kernel_v4<2><<<dim3(n_tiles, Hq), 256, lds, stream>>>(PF_ARGS);
+  else if (variant == 3) prefill_paged_kernel_v4<1><<<dim3(n_tiles, Hq), 256, lds, stream>>>(PF_ARGS);
   else prefill_paged_kernel<4><<<dim3(n_tiles, Hq), 512, lds, stream>>>(PF_ARGS);
 #undef PF_ARGS
   return CFC_CHECK_LAUNCH();

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <queue>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -75,9 +76,15 @@ struct BPE {
     cache.clear();
   }
 
-  void encode_word(const std::string& word, std::vector<int>& out) {
-    auto hit = cache.find(word);
-    if (hit != cache.end()) {
+  using WordCache = std::unordered_map<std::string, std::vector<int>>;
+
+  void encode_word(const std::string& word, std::vector<int>& out) { encode_word(word, out, cache); }
+
+  // `wc` is the caller's word cache: the member cache for the single-text API (serialised by the
+  // Python binding's lock), a thread-local one per worker in encode_batch
+  void encode_word(const std::string& word, std::vector<int>& out, WordCache& wc) const {
+    auto hit = wc.find(word);
+    if (hit != wc.end()) {
       out.insert(out.end(), hit->second.begin(), hit->second.end());
       return;
     }
@@ -105,18 +112,20 @@ struct BPE {
       sym[best] = best_id;
       sym.erase(sym.begin() + best + 1);
     }
-    if (cache.size() < 1000000) cache.emplace(word, sym);
+    if (wc.size() < 1000000) wc.emplace(word, sym);
     out.insert(out.end(), sym.begin(), sym.end());
   }
 
-  void encode(const std::string& text, std::vector<int>& out) {
+  void encode(const std::string& text, std::vector<int>& out) { encode(text, out, cache); }
+
+  void encode(const std::string& text, std::vector<int>& out, WordCache& wc) const {
     // SentencePiece normalisation: spaces -> "▁", dummy prefix; newlines are their own pieces
     size_t i = 0;
     bool first = true;
     while (i < text.size()) {
       if (text[i] == '\n') {
         std::string nl = "\n";
-        encode_word(nl, out);
+        encode_word(nl, out, wc);
         ++i;
         first = true;
         continue;
@@ -126,17 +135,17 @@ struct BPE {
       size_t k = j;
       while (k < text.size() && text[k] != ' ' && text[k] != '\n') ++k;
       if (k == j) {  // trailing spaces
-        for (size_t s = i; s < j; ++s) encode_word(kSpaceMark, out);
+        for (size_t s = i; s < j; ++s) encode_word(kSpaceMark, out, wc);
         i = j;
         continue;
       }
       std::string w;
       // one "▁" per preceding space (first word gets the dummy prefix)
       const size_t spaces = (j - i) + (first && j == i ? 1 : 0);
-      for (size_t s = 1; s < spaces; ++s) encode_word(kSpaceMark, out);
+      for (size_t s = 1; s < spaces; ++s) encode_word(kSpaceMark, out, wc);
       if (spaces > 0) w = kSpaceMark;
       w.append(text, j, k - j);
-      encode_word(w, out);
+      encode_word(w, out, wc);
       first = false;
       i = k;
     }
@@ -391,4 +400,52 @@ CFC_API int cfc_wp_encode(void* h, const char* text, int len, int32_t* out, int 
   const int n = (int)ids.size();
   for (int i = 0; i < std::min(n, cap); ++i) out[i] = ids[i];
   return n;
+}
+
+// ------------------------------------------------------------------------------------ batch encode
+// texts = buf[offs[i], offs[i+1]); ids of text i go to out[i*cap ...] (at most cap), its FULL length
+// to lens[i] (re-encode singly when lens[i] > cap).  nthreads workers, text i on worker i % nthreads.
+template <class F>
+static void parallel_texts(int n, int nthreads, F&& fn) {
+  nthreads = std::max(1, std::min(nthreads, n));
+  if (nthreads == 1) {
+    fn(0, 1);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t) th.emplace_back([&fn, t, nthreads] { fn(t, nthreads); });
+  for (auto& x : th) x.join();
+}
+
+CFC_API int cfc_bpe_encode_batch(void* h, const char* buf, const int64_t* offs, int n, int cap, int32_t* out,
+                                 int32_t* lens, int nthreads) {
+  const auto* b = static_cast<const BPE*>(h);
+  parallel_texts(n, nthreads, [&](int t, int nt) {
+    BPE::WordCache wc;
+    std::vector<int> ids;
+    for (int i = t; i < n; i += nt) {
+      ids.clear();
+      b->encode(std::string(buf + offs[i], (size_t)(offs[i + 1] - offs[i])), ids, wc);
+      lens[i] = (int32_t)ids.size();
+      const int m = std::min((int)ids.size(), cap);
+      for (int k = 0; k < m; ++k) out[(size_t)i * cap + k] = ids[k];
+    }
+  });
+  return 0;
+}
+
+CFC_API int cfc_wp_encode_batch(void* h, const char* buf, const int64_t* offs, int n, int cap, int32_t* out,
+                                int32_t* lens, int nthreads) {
+  const auto* w = static_cast<const WordPiece*>(h);
+  parallel_texts(n, nthreads, [&](int t, int nt) {
+    std::vector<int> ids;
+    for (int i = t; i < n; i += nt) {
+      ids.clear();
+      w->encode(std::string(buf + offs[i], (size_t)(offs[i + 1] - offs[i])), ids);
+      lens[i] = (int32_t)ids.size();
+      const int m = std::min((int)ids.size(), cap);
+      for (int k = 0; k < m; ++k) out[(size_t)i * cap + k] = ids[k];
+    }
+  });
+  return 0;
 }
