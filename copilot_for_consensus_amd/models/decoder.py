@@ -225,9 +225,16 @@ class DecoderModel:
         self.scale = 1.0 / math.sqrt(self.cfg.head_dim)
         # decode projections on the split-K skinny MFMA GEMM with fused epilogues (TP=1; with TP>1
         # the all-reduce sits between the projection and the residual/norm)
-        if fused_decode is None:
-            fused_decode = os.environ.get("CFC_FUSED_DECODE", "0") == "1"
-        self.fused_decode = fused_decode and weights.tp_size == 1 and weights.gate_up_interleaved
+        # decode GEMM mode (TP=1): "splitk" = library GEMMs, with o/down as batched split-K whose
+        # reduce carries residual+RMSNorm (default); "skinny" = the hand-written split-K kernel
+        # with fused SwiGLU too; "lib" = plain library GEMMs + separate norm kernels
+        mode = os.environ.get("CFC_DECODE_GEMM", "skinny" if os.environ.get("CFC_FUSED_DECODE") == "1" else "splitk")
+        if fused_decode is not None:
+            mode = "skinny" if fused_decode else "lib"
+        if weights.tp_size != 1 or (mode == "skinny" and not weights.gate_up_interleaved):
+            mode = "lib"
+        self.decode_gemm = mode
+        self.fused_decode = mode == "skinny"
 
     def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.w.tp_size > 1:
@@ -280,6 +287,9 @@ class DecoderModel:
         if self.fused_decode and x.is_cuda and B <= K.SKINNY_MAX_M:
             return self._forward_decode_fused(x, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
                                               part_blocks)
+        if self.decode_gemm == "splitk" and x.is_cuda:
+            return self._forward_decode_splitk(x, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
+                                               part_blocks)
         residual = None
         for i in range(cfg.layers):
             lw = w.layers[i]
@@ -313,6 +323,28 @@ class DecoderModel:
             a = K.skinny_swiglu(h, lw["gate_up"])
             nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm
             h = K.skinny_linear_residual_rmsnorm(a, lw["down"], residual, nxt, eps)
+        return h
+
+    def _forward_decode_splitk(self, x, positions, slots, ctx_lens, block_tables, kv, attn_workspace, part_blocks):
+        """Library GEMMs; o and down as batched split-K with residual + next RMSNorm in the reduce."""
+        cfg, w = self.cfg, self.w
+        B = x.shape[0]
+        eps = cfg.rms_eps
+        residual = x.clone()
+        h = K.rmsnorm(x, w.layers[0]["attn_norm"], eps)
+        s_o = K.lib_split_for(w.heads * cfg.head_dim, cfg.hidden)
+        s_d = K.lib_split_for(w.ffn, cfg.hidden)
+        for i in range(cfg.layers):
+            lw = w.layers[i]
+            qkv = F.linear(h, lw["qkv"])
+            q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
+                                cfg.head_dim)
+            attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
+                                            part_blocks=part_blocks, workspace=attn_workspace)
+            h = K.lib_splitk_linear_residual_rmsnorm(attn.view(B, -1), lw["o"], s_o, residual, lw["mlp_norm"], eps)
+            a = K.silu_mul(F.linear(h, lw["gate_up"]), interleaved=w.gate_up_interleaved)
+            nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm
+            h = K.lib_splitk_linear_residual_rmsnorm(a, lw["down"], s_d, residual, nxt, eps)
         return h
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:

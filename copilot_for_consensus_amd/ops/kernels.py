@@ -283,6 +283,39 @@ def skinny_linear_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, residual: t
     return out
 
 
+def lib_splitk_linear_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, split: int, residual: torch.Tensor,
+                                       norm_w: torch.Tensor, eps: float) -> torch.Tensor:
+    """Decode projection as a strided-batched library GEMM over ``split`` K slices (fp32 partials:
+    ``split`` x more output tiles for the small-N shapes that leave most CUs idle as one GEMM), then
+    one kernel that sums the partials, adds the residual and applies the next RMSNorm:
+    residual += bf16(x @ w^T); returns RMSNorm(residual) * norm_w."""
+    if not x.is_cuda:
+        return skinny_linear_residual_rmsnorm(x, w, residual, norm_w, eps)
+    M, Kd = x.shape
+    N = w.shape[0]
+    if Kd % split:
+        raise ValueError(f"K={Kd} not divisible by split={split}")
+    Ks = Kd // split
+    part = _workspace(x.device, split * M * N)[:split * M * N].view(split, M, N)
+    torch.bmm(x.view(M, split, Ks).permute(1, 0, 2), w.view(N, split, Ks).permute(1, 2, 0),
+              out_dtype=torch.float32, out=part)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    check(kernels().cfc_splitk_residual_rmsnorm(part.data_ptr(), split, M, N, residual.data_ptr(), norm_w.data_ptr(),
+                                                float(eps), out.data_ptr(), _stream(x)), "cfc_splitk_residual_rmsnorm")
+    return out
+
+
+def lib_split_for(K: int, N: int) -> int:
+    """Split factor for the batched split-K decode GEMM (measured on MI355X at M=128:
+    down 4096x14336 -> 8 (29 vs 42 us), o 4096x4096 -> 4); 1 = not worth splitting."""
+    if N > 8192:
+        return 1
+    for s in ((8, 4, 2) if K >= 8192 else (4, 2)):
+        if K % s == 0 and K // s >= 512:
+            return s
+    return 1
+
+
 def silu_mul(gu, out=None, interleaved: bool = False):
     """silu(gate) * up; ``interleaved``: gate/up in 32-column groups (see ref.interleave_gate_up)."""
     if not gu.is_cuda:

@@ -60,6 +60,26 @@ def main():
                 nw = torch.ones(N, device="cuda").bfloat16()
                 row["fused_norm_us"] = round(timed(lambda: K.skinny_linear_residual_rmsnorm(x, w, r, nw, 1e-5)), 1)
                 row["lib_plus_norm_us"] = round(timed(lambda: K.rmsnorm(F.linear(x, w), nw, 1e-5, residual=r)), 1)
+            for S in (2, 4, 8):
+                if Kd % S:
+                    continue
+                Ks = Kd // S
+                xa = x.view(M, S, Ks).permute(1, 0, 2)          # [S, M, Ks]
+                wb = w.view(N, S, Ks).permute(1, 2, 0)          # [S, Ks, N] (column-major slices)
+                part = torch.empty(S, M, N, device="cuda", dtype=torch.float32)
+                outb = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+
+                def bmm_split():
+                    torch.bmm(xa, wb, out_dtype=torch.float32, out=part)
+                    K.kernels().cfc_splitk_reduce(part.data_ptr(), S, M, N, 0, outb.data_ptr(), N,
+                                                  torch.cuda.current_stream().cuda_stream)
+                try:
+                    row[f"bmm_s{S}_us"] = round(timed(bmm_split), 1)
+                    if S == 4:
+                        ref = F.linear(x, w).float()
+                        row["bmm_err"] = round(float((outb.float() - ref).abs().max()), 4)
+                except Exception as e:  # out_dtype / out= combination unsupported
+                    row[f"bmm_s{S}_err"] = repr(e)[:80]
             best = min(v for k, v in row.items() if k.startswith("s") and k.endswith("_us"))
             row["best_skinny_TBs"] = round(wbytes / best / 1e6, 2)
             res[f"{name}_M{M}"] = row

@@ -244,3 +244,16 @@ def test_skinny_linear_residual_rmsnorm(M, N, Kd, split):
     o = K.skinny_linear_residual_rmsnorm(x, w, rr, nw, 1e-5, split=split)
     _close(rr, ref_r, 3e-2)
     _close(o, ref_o, 5e-2)
+
+
+@pytest.mark.parametrize("M,N,Kd,split", [(128, 4096, 14336, 8), (5, 256, 512, 2)])
+def test_lib_splitk_linear_residual_rmsnorm(M, N, Kd, split):
+    x = torch.randn(M, Kd, device=DEV).bfloat16()
+    w = (torch.randn(N, Kd, device=DEV) * 0.02).bfloat16()
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    nw = (1 + 0.1 * torch.randn(N, device=DEV)).bfloat16()
+    ref_o, ref_r = R.rmsnorm(_ref_linear(x, w).bfloat16(), nw.cpu(), 1e-5, r.cpu())
+    rr = r.clone()
+    o = K.lib_splitk_linear_residual_rmsnorm(x, w, split, rr, nw, 1e-5)
+    _close(rr, ref_r, 3e-2)
+    _close(o, ref_o, 5e-2)
