@@ -37,14 +37,20 @@ def init_distributed(backend: str | None = None, timeout_s: int = 600) -> DistEn
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    backend = backend or os.environ.get("CFC_DIST_BACKEND") or None
+    use_gpu = torch.cuda.is_available() and (backend != "gloo" or os.environ.get("CFC_DIST_BACKEND") == "gloo")
     if use_gpu:
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        # ranks beyond the visible GPUs share them (rehearsing N ranks on fewer GPUs with gloo)
+        dev_idx = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev_idx)
+        device = torch.device("cuda", dev_idx)
     else:
         device = torch.device("cpu")
     be = backend or ("nccl" if use_gpu else "gloo")
     if world > 1 and not dist.is_initialized():
+        if be == "nccl":
+            from .resilience import configure_collective_timeouts
+            configure_collective_timeouts(timeout_s)
         kw = {"device_id": device} if be == "nccl" else {}
         dist.init_process_group(be, timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return DistEnv(rank, world, local, device, be if world > 1 else None)
