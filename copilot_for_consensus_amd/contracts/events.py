@@ -70,6 +70,10 @@ CONTEXT_SELECTION = obj({"selector_type": {"type": "string"}, "selector_version"
 CITATION = obj({"message_id": s(1), "chunk_id": HEX_ID, "offset": i(0), "text": {"type": "string"}},
                ["message_id", "chunk_id", "offset"], closed=True)
 
+IDS1 = arr(HEX_ID, minItems=1, uniqueItems=True)  # non-empty, duplicate-free id lists
+IDS0 = arr(HEX_ID, minItems=0, uniqueItems=True)
+COUNTS = {"type": "object", "additionalProperties": {"type": "integer", "minimum": 0}}  # collection -> n deleted
+
 # event type -> (required fields, optional fields); every payload is additionalProperties:false
 EVENT_SPECS: dict[str, tuple[dict, dict]] = {
     "ArchiveIngested": ({
@@ -81,44 +85,44 @@ EVENT_SPECS: dict[str, tuple[dict, dict]] = {
         "retry_count": i(), "ingestion_started_at": DT, "failed_at": DT,
     }, {}),
     "JSONParsed": ({
-        "archive_id": ARCHIVE_ID, "message_count": i(), "message_doc_ids": arr(HEX_ID), "thread_count": i(),
-        "thread_ids": arr(HEX_ID), "parsing_duration_seconds": num(),
+        "archive_id": ARCHIVE_ID, "message_count": i(), "message_doc_ids": IDS1, "thread_count": i(),
+        "thread_ids": IDS0, "parsing_duration_seconds": num(),
     }, {}),
     "ParsingFailed": ({
         "archive_id": ARCHIVE_ID, "error_message": s(), "error_type": s(), "messages_parsed_before_failure": i(),
         "retry_count": i(), "failed_at": DT,
     }, {"file_path": s()}),
     "ChunksPrepared": ({
-        "message_doc_ids": arr(HEX_ID), "chunk_count": i(), "chunk_ids": arr(HEX_ID), "chunks_ready": BOOL,
+        "message_doc_ids": IDS1, "chunk_count": i(), "chunk_ids": IDS1, "chunks_ready": BOOL,
         "chunking_strategy": s(), "avg_chunk_size_tokens": i(),
     }, {}),
     "ChunkingFailed": ({
-        "message_doc_ids": arr(HEX_ID), "error_message": s(), "error_type": s(), "retry_count": i(), "failed_at": DT,
+        "message_doc_ids": IDS1, "error_message": s(), "error_type": s(), "retry_count": i(), "failed_at": DT,
     }, {}),
     "EmbeddingsGenerated": ({
-        "chunk_ids": arr(HEX_ID), "embedding_count": i(), "embedding_model": s(), "embedding_backend": s(),
+        "chunk_ids": IDS1, "embedding_count": i(), "embedding_model": s(), "embedding_backend": s(),
         "embedding_dimension": i(1), "vector_store_collection": s(), "vector_store_updated": BOOL,
         "avg_generation_time_ms": num(),
     }, {}),
     "EmbeddingGenerationFailed": ({
-        "chunk_ids": arr(s()), "error_message": s(), "error_type": s(), "embedding_backend": s(), "retry_count": i(),
+        "chunk_ids": arr(s(), minItems=1, uniqueItems=True), "error_message": s(), "error_type": s(), "embedding_backend": s(), "retry_count": i(),
         "failed_at": DT,
     }, {}),
     "SummarizationRequested": ({
-        "thread_ids": arr(HEX_ID), "top_k": i(1), "prompt_template": s(),
+        "thread_ids": IDS1, "top_k": i(1), "prompt_template": s(),
     }, {"selected_chunks": arr(SELECTED_CHUNK), "context_selection": CONTEXT_SELECTION}),
     "OrchestrationFailed": ({
-        "thread_ids": arr(HEX_ID), "error_type": s(), "error_message": s(), "retry_count": i(),
+        "thread_ids": IDS1, "error_type": s(), "error_message": s(), "retry_count": i(),
     }, {}),
     "SummaryComplete": ({
-        "summary_id": HEX_ID, "thread_id": HEX_ID, "summary_markdown": s(), "citations": arr(CITATION, minItems=0),
+        "summary_id": HEX_ID, "thread_id": HEX_ID, "summary_markdown": s(), "citations": arr(CITATION, minItems=0, uniqueItems=False),
         "llm_backend": s(), "llm_model": s(), "tokens_prompt": i(), "tokens_completion": i(), "latency_ms": i(),
     }, {}),
     "SummarizationFailed": ({
         "thread_id": HEX_ID, "error_type": s(), "error_message": s(), "retry_count": i(),
     }, {}),
     "ReportPublished": ({
-        "thread_id": HEX_ID, "report_id": s(), "format": s(), "notified": BOOL, "delivery_channels": arr(s()),
+        "thread_id": HEX_ID, "report_id": s(), "format": s(), "notified": BOOL, "delivery_channels": arr(s(), minItems=0, uniqueItems=True),
         "summary_url": s(),
     }, {}),
     "ReportDeliveryFailed": ({
@@ -132,9 +136,9 @@ EVENT_SPECS: dict[str, tuple[dict, dict]] = {
     "SourceCleanupProgress": ({
         "source_name": s(), "correlation_id": UUID, "service_name": s(),
         "status": {"type": "string", "enum": ["started", "in_progress", "completed", "failed"]},
-    }, {"deletion_counts": obj(), "error_summary": {"type": "string"}, "completed_at": DT}),
+    }, {"deletion_counts": COUNTS, "error_summary": {"type": "string"}, "completed_at": DT}),
     "SourceCleanupCompleted": ({
-        "source_name": s(), "correlation_id": UUID, "completed_at": DT, "total_deletion_counts": obj(),
+        "source_name": s(), "correlation_id": UUID, "completed_at": DT, "total_deletion_counts": COUNTS,
         "services_completed": arr({"type": "string"}), "services_failed": arr({"type": "string"}),
         "overall_status": {"type": "string", "enum": ["success", "partial_success", "failed"]},
     }, {}),

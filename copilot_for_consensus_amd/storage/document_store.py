@@ -113,6 +113,9 @@ DEFAULT_INDEXES = {
 }
 
 
+_ABSENT = ("__absent__",)
+
+
 def _hashable(v):
     if isinstance(v, list):
         return None
@@ -131,6 +134,7 @@ class InMemoryDocumentStore(DocumentStore):
         self.collections: dict[str, dict[str, dict]] = defaultdict(dict)
         self._index_fields = dict(DEFAULT_INDEXES if indexes is None else indexes)
         self._idx: dict[tuple[str, str], dict[Any, set]] = defaultdict(lambda: defaultdict(set))
+        self._overflow: dict[tuple[str, str], set] = defaultdict(set)
         self.connected = False
 
     @classmethod
@@ -144,32 +148,67 @@ class InMemoryDocumentStore(DocumentStore):
         self.connected = False
 
     # ---------------------------------------------------------------- index maintenance
+    # Multikey hash index like Mongo's: a scalar is indexed under itself, an array under each of
+    # its elements, an absent field under ``_ABSENT`` (an equality-to-None query matches both null
+    # and absent).  Values that cannot be hashed go to a per-field overflow set that every lookup
+    # on that field includes, so the index only ever narrows the scan, never changes its result.
+    def _index_keys(self, doc, f):
+        if f not in doc:
+            return [_ABSENT], True
+        v = doc[f]
+        vals = v if isinstance(v, list) else [v]
+        keys = [_hashable(x) for x in vals]
+        ok = all(k is not None or x is None for k, x in zip(keys, vals))
+        return keys, ok
+
     def _index_add(self, coll, doc):
         for f in self._index_fields.get(coll, ()):
-            v = _hashable(doc.get(f))
-            if f in doc and (v is not None or doc.get(f) is None):
-                self._idx[(coll, f)][v].add(doc["_id"])
+            keys, ok = self._index_keys(doc, f)
+            idx = self._idx[(coll, f)]
+            for k in keys:
+                idx[k].add(doc["_id"])
+            if not ok or isinstance(doc.get(f), list):
+                self._overflow[(coll, f)].add(doc["_id"])
 
     def _index_remove(self, coll, doc):
         for f in self._index_fields.get(coll, ()):
-            v = _hashable(doc.get(f))
-            if f in doc:
-                self._idx[(coll, f)][v].discard(doc["_id"])
+            keys, _ = self._index_keys(doc, f)
+            idx = self._idx[(coll, f)]
+            for k in keys:
+                idx.get(k, set()).discard(doc["_id"])
+            self._overflow[(coll, f)].discard(doc["_id"])
+
+    def _lookup(self, coll, f, val):
+        idx = self._idx[(coll, f)]
+        hv = _hashable(val)
+        if hv is None and val is not None:
+            return None  # unhashable query value: no index answer, scan
+        ids = set(idx.get(hv, ()))
+        if val is None:
+            ids |= idx.get(_ABSENT, set())
+        return ids
 
     def _candidates(self, coll, flt):
         best = None
         for f, (kind, val) in simple_equality_keys(flt).items():
             if f == "_id":
-                ids = set(val) if kind == "in" else {val}
+                try:
+                    ids = set(val) if kind == "in" else {val}
+                except TypeError:
+                    continue
             elif f in self._index_fields.get(coll, ()):
-                idx = self._idx[(coll, f)]
-                if kind == "in":
-                    ids = set()
-                    for v in val:
-                        hv = _hashable(v)
-                        ids |= idx.get(hv, set())
-                else:
-                    ids = set(idx.get(_hashable(val), set()))
+                ids = set()
+                for v in (val if kind == "in" else [val]):
+                    got = self._lookup(coll, f, v)
+                    if got is None:
+                        ids = None
+                        break
+                    ids |= got
+                if ids is None:
+                    continue
+                # arrays / unhashable values may match in ways a hash lookup cannot see
+                # (element of a list-valued query, nested dicts): always re-check those docs
+                ids |= self._overflow[(coll, f)]
             else:
                 continue
             if best is None or len(ids) < len(best):
@@ -261,11 +300,14 @@ class InMemoryDocumentStore(DocumentStore):
             self.collections[collection].clear()
             for k in [k for k in self._idx if k[0] == collection]:
                 del self._idx[k]
+            for k in [k for k in self._overflow if k[0] == collection]:
+                del self._overflow[k]
 
     def clear_all(self) -> None:
         with self._lock:
             self.collections.clear()
             self._idx.clear()
+            self._overflow.clear()
 
     def aggregate_documents(self, collection: str, pipeline: list[dict]) -> list[dict]:
         """$match / $lookup / $project / $sort / $limit / $skip / $count / $group(count|sum)."""
