@@ -36,6 +36,7 @@ class InProcBroker:
         self.max_redeliveries = max_redeliveries
         self.published = 0
         self.dead_letters: dict[str, list] = collections.defaultdict(list)
+        self._consumers: collections.Counter = collections.Counter()
 
     def declare_queue(self, name: str) -> _Queue:
         with self._lock:
@@ -64,6 +65,15 @@ class InProcBroker:
 
     def queues(self) -> dict[str, int]:
         return {n: len(q.items) for n, q in self._queues.items()}
+
+    def consumer_counts(self) -> dict[str, int]:
+        """Active consumers per queue (management-API ``consumers`` field)."""
+        with self._lock:
+            return {n: self._consumers[n] for n in self._queues}
+
+    def _consumer(self, queue: str, delta: int) -> None:
+        with self._lock:
+            self._consumers[queue] = max(0, self._consumers[queue] + delta)
 
 
 _default_broker: InProcBroker | None = None
@@ -159,10 +169,14 @@ class InProcSubscriber(EventSubscriber):
 
     def start_consuming(self) -> None:
         self._stop.clear()
-        while not self._stop.is_set():
-            item = self._pop(0.05)
-            if item is not None:
-                self._handle(item)
+        self.broker._consumer(self.queue_name, +1)
+        try:
+            while not self._stop.is_set():
+                item = self._pop(0.05)
+                if item is not None:
+                    self._handle(item)
+        finally:
+            self.broker._consumer(self.queue_name, -1)
 
     def stop_consuming(self) -> None:
         self._stop.set()

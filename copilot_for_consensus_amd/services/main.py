@@ -6,7 +6,6 @@
 from __future__ import annotations
 
 import argparse
-import os
 import sys
 
 from ..config.loader import get_config
@@ -37,7 +36,7 @@ def main(argv=None) -> int:
         import uvicorn
         cfg = get_config("auth")
         store = create_document_store(cfg.document_store)
-        provs = {"mock": MockIdentityProvider()} if os.environ.get("AUTH_ENABLE_MOCK_PROVIDER") else {}
+        provs = {"mock": MockIdentityProvider()} if cfg.enable_mock_provider else {}
         for name, fn in (("github", github_provider), ("google", google_provider), ("microsoft", microsoft_provider),
                          ("datatracker", datatracker_provider)):
             pc = cfg.oidc_providers.driver_config.get(name, {})

@@ -457,7 +457,8 @@ class MongoDocumentStore(DocumentStore):
         cur = self._c(collection).find(filter_dict or {})
         if sort_by:
             cur = cur.sort(sort_by, -1 if sort_order == "desc" else 1)
-        return list(cur.skip(skip).limit(limit))
+        cur = cur.skip(skip)
+        return list(cur.limit(limit) if limit else cur)
 
     def update_document(self, collection, doc_id, patch):
         upd = patch if any(k.startswith("$") for k in patch) else {"$set": patch}
