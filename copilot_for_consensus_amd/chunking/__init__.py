@@ -120,6 +120,11 @@ class FixedSizeChunker(ThreadChunker):
 
 
 class SemanticChunker(ThreadChunker):
+    """Sentence-boundary chunking up to ``target_chunk_size`` words (reference chunkers.py:352).
+
+    ``split_on_speaker`` (declared but "not yet implemented" in the reference, chunkers.py:361):
+    when the thread carries its ``messages`` (each with ``from``), a chunk never spans two
+    consecutive messages by different senders, and each chunk records its ``speaker``."""
     strategy = "semantic"
     _SENT = re.compile(r"(?<=[.!?])\s+")
 
@@ -130,25 +135,48 @@ class SemanticChunker(ThreadChunker):
     def _sentences(self, text: str) -> list[str]:
         return [s.strip() for s in self._SENT.split(text) if s.strip()]
 
+    @staticmethod
+    def _speaker(m: dict) -> str:
+        f = m.get("from")
+        if isinstance(f, dict):
+            return str(f.get("email") or f.get("name") or "")
+        return str(f or m.get("sender") or "")
+
     def chunk(self, thread: Thread) -> list[Chunk]:
-        _require(thread)
+        by_speaker = self.split_on_speaker and bool(thread.messages)
+        if by_speaker:
+            _require(thread, need_text=False)
+            turns = [(self._speaker(m), m.get("text", m.get("body", ""))) for m in thread.messages]
+        else:
+            _require(thread)
+            turns = [(None, thread.text)]
         out, cur, count, idx = [], [], 0, 0
+        cur_speaker = None
 
         def flush():
             nonlocal cur, count, idx
-            out.append(Chunk(chunk_id(thread.message_doc_id, idx), " ".join(cur), idx, count, dict(thread.metadata),
+            md = dict(thread.metadata)
+            if by_speaker:
+                md["speaker"] = cur_speaker
+            out.append(Chunk(chunk_id(thread.message_doc_id, idx), " ".join(cur), idx, count, md,
                              thread.message_doc_id, thread.thread_id))
             idx += 1
             cur, count = [], 0
 
-        for s in self._sentences(thread.text):
-            n = len(s.split())
-            if cur and count + n > self.target_chunk_size:
+        for speaker, text in turns:
+            if cur and by_speaker and speaker != cur_speaker:
                 flush()
-            cur.append(s)
-            count += n
+            cur_speaker = speaker
+            for s in self._sentences(text or ""):
+                n = len(s.split())
+                if cur and count + n > self.target_chunk_size:
+                    flush()
+                cur.append(s)
+                count += n
         if cur:
             flush()
+        if not out and by_speaker:
+            raise ValueError("Thread messages contain no text")
         return out
 
 

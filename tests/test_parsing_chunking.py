@@ -1,0 +1,379 @@
+"""Parsing (mbox split, MIME bodies, normalizer, draft detector, thread builder), chunking (token
+window / fixed size / semantic incl. speaker turns), orchestration (context selection, prompt
+substitution, citations) and the retry policy.
+
+Mirrors the reference's parsing/tests/test_parser.py, test_thread_builder.py,
+adapters/copilot_chunking/tests/test_chunkers.py, orchestrator/tests/test_context_selectors.py,
+adapters/copilot_event_retry/tests, plus Hypothesis fuzzing of the parser (fuzzing/tests, corpus
+``mbox`` / ``adversarial_text``).  The reference's own 10-message fixture
+(tests/fixtures/mailbox_sample/test-archive.mbox) is used when the checkout is mounted.
+"""
+from __future__ import annotations
+
+import random
+from pathlib import Path
+
+import pytest
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+from copilot_for_consensus_amd.chunking import (FixedSizeChunker, SemanticChunker, Thread, TokenWindowChunker,
+                                                create_chunker)
+from copilot_for_consensus_amd.contracts.ids import chunk_id, message_doc_id
+from copilot_for_consensus_amd.orchestration import (TopKCohesiveSelector, TopKRelevanceSelector, build_context,
+                                                     create_context_selector, estimate_tokens, format_citations,
+                                                     prompt_template, substitute_prompt)
+from copilot_for_consensus_amd.parsing import (DraftDetector, MessageParser, MessageParsingError, TextNormalizer,
+                                               ThreadBuilder, clean_subject, split_mbox)
+from copilot_for_consensus_amd.retry import (DocumentNotFoundError, RetryConfig, RetryExhaustedError, RetryPolicy,
+                                             handle_event_with_retry, retry_with_backoff)
+
+FIX = Path(__file__).parent / "fixtures" / "sample.mbox"
+REF_MBOX = Path("/root/reference/tests/fixtures/mailbox_sample/test-archive.mbox")
+
+
+def _msg(mid, body="hello world.", irt=None, frm="a@example.com", subject="Topic", date="Mon, 1 Jan 2024 10:00:00 +0000",
+         extra=""):
+    hdr = f"From: A <{frm}>\nTo: wg@example.org\nSubject: {subject}\nDate: {date}\nMessage-ID: <{mid}>\n"
+    if irt:
+        hdr += f"In-Reply-To: <{irt}>\nReferences: <{irt}>\n"
+    return f"From {frm} Mon Jan  1 00:00:00 2024\n{hdr}{extra}\n{body}\n\n"
+
+
+# ------------------------------------------------------------------ mbox + parser
+def test_split_mbox_native_matches_python_fallback(monkeypatch):
+    data = FIX.read_bytes()
+    native = split_mbox(data)
+    import copilot_for_consensus_amd.ops._native as nat
+    monkeypatch.setattr(nat, "runtime", lambda: (_ for _ in ()).throw(OSError("no lib")))
+    assert split_mbox(data) == native
+    assert len(native) == 10
+
+
+def test_split_mbox_edge_cases():
+    assert split_mbox(b"") == []
+    assert split_mbox(b"From x\n\n\n") == []  # separator only: no message
+    two = _msg("1@x").encode() + _msg("2@x").encode()
+    assert len(split_mbox(two)) == 2
+    # a body line starting with "From " that is not at a line start does not split
+    assert len(split_mbox(_msg("1@x", body="see From the top").encode())) == 1
+
+
+def test_parse_fixture_threads():
+    msgs, errs = MessageParser().parse_mbox_bytes(FIX.read_bytes(), "0123456789abcdef")
+    assert errs == [] and len(msgs) == 10
+    threads = ThreadBuilder().build_threads(msgs)
+    assert sum(t["message_count"] for t in threads) == 10
+    for m in msgs:
+        assert m["_id"] == message_doc_id("0123456789abcdef", m["message_id"], m["date"], m["from"]["email"],
+                                          m["subject"])
+        assert m["thread_id"] in {t["_id"] for t in threads}
+    for t in threads:
+        assert not t["subject"].lower().startswith("re:")
+        assert t["first_message_date"] <= t["last_message_date"]
+
+
+@pytest.mark.skipif(not REF_MBOX.exists(), reason="reference checkout not mounted")
+def test_reference_fixture_threads():
+    msgs, errs = MessageParser().parse_mbox_bytes(REF_MBOX.read_bytes(), "0123456789abcdef")
+    assert errs == [] and len(msgs) == 10
+    threads = ThreadBuilder().build_threads(msgs)
+    by_mid = {m["message_id"]: m for m in msgs}
+    # msg001 <- msg002 <- msg003 <- msg009 all land in msg001's thread
+    root = by_mid["msg001@example.com"]["_id"]
+    for mid in ("msg002@example.com", "msg003@example.com", "msg009@example.com"):
+        assert by_mid[mid]["thread_id"] == root
+    assert by_mid["msg005@example.com"]["thread_id"] == by_mid["msg004@example.com"]["_id"]
+    assert by_mid["msg008@example.com"]["thread_id"] == by_mid["msg006@example.com"]["_id"]
+    sizes = sorted(t["message_count"] for t in threads)
+    assert sum(sizes) == 10 and sizes[-1] == 4
+
+
+def test_parse_message_fields_and_mime():
+    raw = (_msg("m1@x", extra="Content-Type: multipart/alternative; boundary=BB\nMIME-Version: 1.0\n",
+                body="--BB\nContent-Type: text/plain\n\nplain part mentions draft-ietf-quic-http-34 and RFC 9000.\n"
+                     "--BB\nContent-Type: text/html\n\n<p>html part</p>\n--BB--")).encode()
+    m = MessageParser().parse_mbox_bytes(raw, "a" * 16)[0][0]
+    assert m["message_id"] == "m1@x" and m["from"] == {"name": "A", "email": "a@example.com"}
+    assert "plain part" in m["body_normalized"] and "<p>" not in m["body_normalized"]
+    assert m["draft_mentions"] == ["draft-ietf-quic-http-34", "RFC 9000"]
+    assert m["date"].startswith("2024-01-01T10:00:00")
+    assert m["headers"]["mime-version"] == "1.0"
+
+
+def test_missing_message_id_collected_as_error():
+    good = _msg("ok@x")
+    bad = "From x Mon Jan  1 00:00:00 2024\nFrom: b@x\nSubject: no id\n\nbody\n\n"
+    msgs, errs = MessageParser().parse_mbox_bytes((good + bad).encode(), "a" * 16)
+    assert len(msgs) == 1 and len(errs) == 1 and "Message-ID" in errs[0]
+    with pytest.raises(MessageParsingError):
+        MessageParser().parse_mbox_bytes(bad.encode(), "a" * 16)
+
+
+def test_normalizer():
+    n = TextNormalizer()
+    assert n.normalize("") == ""
+    txt = "Hi all,\n\n> quoted line\n| piped\nreal   text\t\there\n\n\n\nmore\n-- \nSig Nature"
+    assert n.normalize(txt) == "Hi all,\n\nreal text here\n\nmore"
+    assert n.normalize("<html><body><style>x{}</style><p>a &amp; b</p></body></html>") == "a & b"
+    keep = TextNormalizer(strip_quoted=False, strip_signatures=False)
+    assert "> quoted" in keep.normalize("a\n> quoted\n-- \nsig") and "sig" in keep.normalize("a\n-- \nsig")
+
+
+def test_draft_detector():
+    d = DraftDetector()
+    assert d.detect("see draft-ietf-tls-esni-18, rfc8446 and RFC 8446 and draft-ietf-tls-esni-18") == \
+        ["draft-ietf-tls-esni-18", "RFC 8446"]
+    assert d.detect("") == [] and d.detect("nothing here") == []
+    assert DraftDetector(r"(foo-\d+)").detect("foo-1 foo-2 foo-1") == ["foo-1", "foo-2"]
+
+
+def test_clean_subject():
+    assert clean_subject("Re: RE: Fwd: [quic] [wg] Hello") == "Hello"
+    assert clean_subject("") == ""
+
+
+def test_thread_builder_cycles_and_missing_parents():
+    msgs = [{"_id": f"id{i}", "message_id": f"m{i}", "archive_id": "a", "subject": "s", "date": f"2024-01-0{i+1}",
+             "from": {"email": f"u{i % 2}@x", "name": ""}, "draft_mentions": []} for i in range(5)]
+    msgs[1]["in_reply_to"] = "m0"
+    msgs[2]["in_reply_to"] = "m3"   # m2 <-> m3 cycle
+    msgs[3]["in_reply_to"] = "m2"
+    msgs[4]["in_reply_to"] = "not-in-archive"
+    threads = ThreadBuilder().build_threads(msgs)
+    assert msgs[1]["thread_id"] == "id0"
+    assert sum(t["message_count"] for t in threads) == 5
+    t0 = next(t for t in threads if t["_id"] == "id0")
+    assert t0["message_count"] == 2 and len(t0["participants"]) == 2
+    assert ThreadBuilder().build_threads([]) == []
+
+
+_mbox_line = st.one_of(st.text(max_size=60), st.sampled_from(["From x", "From: a@b", "Message-ID: <q@w>",
+                                                               "In-Reply-To: <q@w>", "Content-Type: multipart/mixed",
+                                                               "--", "", ">From quoted", "=?utf-8?b?w6k=?="]))
+
+
+@settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(st.lists(_mbox_line, max_size=40))
+def test_parser_never_crashes_on_arbitrary_mbox(lines):
+    data = "\n".join(lines).encode("utf-8", "surrogatepass")
+    try:
+        msgs, errs = MessageParser().parse_mbox_bytes(data, "f" * 16)
+    except MessageParsingError:
+        return
+    for m in msgs:
+        assert m["message_id"] and len(m["_id"]) == 16
+    ThreadBuilder().build_threads(msgs)
+
+
+@settings(max_examples=100, deadline=None)
+@given(st.text(max_size=400))
+def test_normalizer_is_idempotent(text):
+    n = TextNormalizer()
+    once = n.normalize(text)
+    assert n.normalize(once) == once
+
+
+# ------------------------------------------------------------------ chunkers
+def _thread(words=1000, **kw):
+    rng = random.Random(0)
+    text = " ".join(f"w{rng.randint(0, 99)}" for _ in range(words))
+    return Thread("t" * 16, text, {"subject": "s"}, message_doc_id="d" * 16, **kw)
+
+
+def test_token_window_sizes_overlap_and_ids():
+    ch = TokenWindowChunker(chunk_size=384, overlap=50, min_chunk_size=100)
+    th = _thread(1000)
+    chunks = ch.chunk(th)
+    words = th.text.split()
+    assert [c.token_count for c in chunks] == [384, 384, 332]
+    assert chunks[1].text.split()[:50] == chunks[0].text.split()[-50:]
+    assert [c.chunk_id for c in chunks] == [chunk_id("d" * 16, i) for i in range(3)]
+    assert " ".join(chunks[-1].text.split()[-5:]) == " ".join(words[-5:])
+    assert len(ch.chunk(_thread(20))) == 1   # a short thread is one chunk even below min size
+    with pytest.raises(ValueError):
+        ch.chunk(Thread("t", "  ", {}, message_doc_id="d"))
+    with pytest.raises(ValueError):
+        ch.chunk(Thread("t", "x", {}, message_doc_id=None))
+    with pytest.raises(ValueError):
+        TokenWindowChunker(chunk_size=0)
+
+
+@settings(max_examples=80, deadline=None)
+@given(st.integers(1, 1500), st.integers(1, 400), st.integers(0, 399))
+def test_token_window_covers_every_word(n, size, overlap):
+    overlap = min(overlap, size - 1) if size > 1 else 0
+    th = Thread("t", " ".join(f"w{i}" for i in range(n)), {}, message_doc_id="d")  # unique words
+    chunks = TokenWindowChunker(chunk_size=size, overlap=overlap, min_chunk_size=1).chunk(th)
+    words = th.text.split()
+    pos, covered = 0, set()
+    for c in chunks:
+        cw = c.text.split()
+        assert len(cw) <= size
+        # every chunk is a contiguous window of the text
+        start = words.index(cw[0])
+        assert words[start:start + len(cw)] == cw and start >= pos
+        covered.update(range(start, start + len(cw)))
+        pos = start + 1
+    assert covered == set(range(n))
+
+
+def test_fixed_size_chunker():
+    msgs = [{"message_doc_id": f"m{i}", "text": f"body {i}"} for i in range(7)]
+    th = Thread("t", "", {"k": 1}, message_doc_id="d" * 16, messages=msgs)
+    chunks = FixedSizeChunker(messages_per_chunk=3).chunk(th)
+    assert [c.metadata["message_count"] for c in chunks] == [3, 3, 1]
+    assert chunks[0].metadata["message_doc_ids"] == ["m0", "m1", "m2"]
+    blocks = Thread("t", "a\n\nb\n\nc", {}, message_doc_id="d")
+    assert [c.text for c in FixedSizeChunker(2).chunk(blocks)] == ["a\n\nb", "c"]
+    with pytest.raises(ValueError):
+        FixedSizeChunker(0)
+    with pytest.raises(ValueError):
+        FixedSizeChunker(2).chunk(Thread("t", "", {}, message_doc_id="d", messages=[{"text": "x"}]))
+
+
+def test_semantic_chunker_sentences_and_speakers():
+    text = "One two three. Four five! Six seven eight nine? Ten."
+    chunks = SemanticChunker(target_chunk_size=5).chunk(Thread("t", text, {}, message_doc_id="d"))
+    assert [c.text for c in chunks] == ["One two three. Four five!", "Six seven eight nine? Ten."]
+    msgs = [{"from": {"email": "a@x"}, "text": "Alpha one. Alpha two."},
+            {"from": {"email": "a@x"}, "text": "Alpha three."},
+            {"from": {"email": "b@x"}, "text": "Beta one."}]
+    th = Thread("t", "", {}, message_doc_id="d", messages=msgs)
+    sp = SemanticChunker(target_chunk_size=100, split_on_speaker=True).chunk(th)
+    assert [(c.metadata["speaker"], c.text) for c in sp] == [("a@x", "Alpha one. Alpha two. Alpha three."),
+                                                             ("b@x", "Beta one.")]
+    # without split_on_speaker the speaker turns are ignored (reference behaviour)
+    flat = SemanticChunker(100).chunk(Thread("t", "Alpha one. Beta one.", {}, message_doc_id="d"))
+    assert len(flat) == 1 and "speaker" not in flat[0].metadata
+
+
+def test_create_chunker_from_config():
+    class Cfg:
+        driver_name = "token_window"
+        driver_config = {"chunk_size": 10, "overlap": 2, "min_chunk_size": None}
+    c = create_chunker(Cfg)
+    assert isinstance(c, TokenWindowChunker) and c.chunk_size == 10 and c.min_chunk_size == 100
+    assert isinstance(create_chunker("semantic", split_on_speaker=True), SemanticChunker)
+    assert isinstance(create_chunker("fixed_size"), FixedSizeChunker)
+    with pytest.raises(ValueError):
+        create_chunker("paragraph")
+
+
+# ------------------------------------------------------------------ orchestration
+def _cands():
+    return [{"_id": "c3", "text": "a " * 100, "similarity_score": 0.9, "date": "2024-01-03", "chunk_index": 0},
+            {"_id": "c1", "text": "b " * 100, "similarity_score": 0.5, "date": "2024-01-01", "chunk_index": 1},
+            {"_id": "c2", "text": "c " * 100, "similarity_score": 0.5, "date": "2024-01-01", "chunk_index": 0},
+            {"_id": None, "text": "x", "similarity_score": 1.0}]
+
+
+def test_topk_relevance_order_budget_and_ties():
+    sel = TopKRelevanceSelector().select("t", _cands(), top_k=3)
+    assert [s.chunk_id for s in sel.selected_chunks] == ["c3", "c1"]  # id-less candidate skipped after ranking
+    sel = TopKRelevanceSelector().select("t", _cands(), top_k=4)
+    assert [s.chunk_id for s in sel.selected_chunks] == ["c3", "c1", "c2"]  # score desc, id asc
+    assert [s.rank for s in sel.selected_chunks] == [0, 1, 2]
+    budget = TopKRelevanceSelector().select("t", _cands(), top_k=4, context_window_tokens=270)
+    assert [s.chunk_id for s in budget.selected_chunks] == ["c3", "c1"] and budget.total_tokens == 260
+    md = budget.metadata()
+    assert md["selector_type"] == "top_k_relevance" and md["total_candidates"] == 4
+    assert estimate_tokens("a b c d e f g h i j") == 13
+
+
+def test_cohesive_selector_orders_chronologically():
+    sel = TopKCohesiveSelector().select("t", _cands(), top_k=4)
+    assert [s.chunk_id for s in sel.selected_chunks] == ["c2", "c1", "c3"]
+    assert sel.selector_type == "top_k_cohesive"
+    assert isinstance(create_context_selector("cohesive"), TopKCohesiveSelector)
+    with pytest.raises(ValueError):
+        create_context_selector("random")
+
+
+def test_prompt_substitution_and_citations():
+    tmpl = prompt_template()
+    assert "{email_chunks}" in tmpl and "{thread_id}" in tmpl
+    chunks = [{"_id": "c1", "text": "first", "message_doc_id": "m1", "message_id": "<1@x>", "offset": 3},
+              {"_id": "c2", "text": "second", "message_doc_id": "m2"}]
+    msgs = {"m1": {"from": {"name": "Ann", "email": "ann@x"}, "date": "2024-01-02", "draft_mentions": ["RFC 1"]},
+            "m2": {"from": {"name": "", "email": "bob@x"}, "date": "2024-01-01", "draft_mentions": []}}
+    ctx = build_context(chunks, msgs)
+    out = substitute_prompt(tmpl, "tid", ctx)
+    assert "Message 1:\nfirst" in out and "Message 2:\nsecond" in out
+    assert "Ann <ann@x>" in out and "bob@x <bob@x>" in out and "RFC 1" in out
+    assert "2024-01-01 to 2024-01-02" in out
+    with pytest.raises(ValueError, match="unexpected placeholders"):
+        substitute_prompt("{thread_id} {secret}", "t", ctx)
+    empty = substitute_prompt("{email_chunks}|{participants}|{date_range}", "t", {"chunks": [], "messages": []})
+    assert empty == "(No messages available)|Multiple participants|Unknown"
+    cit = format_citations(chunks + [{"text": "no id"}])
+    assert cit == [{"message_id": "<1@x>", "chunk_id": "c1", "offset": 3, "text": "first"},
+                   {"message_id": "unknown", "chunk_id": "c2", "offset": 0, "text": "second"}]
+
+
+# ------------------------------------------------------------------ retry
+def test_retry_policy_delays():
+    p = RetryPolicy(RetryConfig(base_delay_ms=100, backoff_factor=2, max_delay_ms=500, use_jitter=False))
+    assert [p.calculate_delay_ms(n) for n in range(1, 7)] == [0, 200, 400, 500, 500, 500]
+    j = RetryPolicy(RetryConfig(base_delay_ms=100, max_delay_ms=500), rng=random.Random(1))
+    assert all(0 <= j.calculate_delay_ms(4) <= 500 for _ in range(50))
+
+
+class _Metrics:
+    def __init__(self):
+        self.calls = []
+
+    def increment(self, name, value=1, tags=None):
+        self.calls.append(name)
+
+    def observe(self, name, value, tags=None):
+        self.calls.append(name)
+
+
+def test_handle_event_with_retry_recovers_then_exhausts():
+    sleeps, metrics = [], _Metrics()
+    attempts = {"n": 0}
+
+    def flaky(ev):
+        attempts["n"] += 1
+        if attempts["n"] < 3:
+            raise DocumentNotFoundError("not yet")
+
+    pol = RetryPolicy(RetryConfig(max_attempts=5, use_jitter=False, base_delay_ms=10), sleeper=sleeps.append)
+    handle_event_with_retry(flaky, {"event_type": "JSONParsed"}, policy=pol, metrics_collector=metrics,
+                            service_name="chunking")
+    assert attempts["n"] == 3 and sleeps == [0.02, 0.04]
+    assert "chunking_event_retry_success_total" in metrics.calls
+
+    reported = []
+
+    class Rep:
+        def report(self, e, context=None):
+            reported.append(context)
+
+    def never(ev):
+        raise DocumentNotFoundError("never")
+
+    with pytest.raises(RetryExhaustedError) as ei:
+        handle_event_with_retry(never, {"event_type": "X", "event_id": "e1"}, policy=pol, error_reporter=Rep())
+    assert ei.value.dlq_info["attempts"] == 5 and reported[0]["event_id"] == "e1"
+
+    def fatal(ev):
+        raise KeyError("bug")
+
+    with pytest.raises(KeyError):
+        handle_event_with_retry(fatal, {"event_type": "X"}, policy=pol)
+
+
+def test_retry_with_backoff():
+    sleeps, n = [], {"k": 0}
+
+    def f():
+        n["k"] += 1
+        if n["k"] < 3:
+            raise IOError("x")
+        return "ok"
+
+    assert retry_with_backoff(f, 3, 5, 60, sleeper=sleeps.append) == "ok" and sleeps == [5, 10]
+    with pytest.raises(IOError):
+        retry_with_backoff(lambda: (_ for _ in ()).throw(IOError("y")), 2, 1, sleeper=sleeps.append)
