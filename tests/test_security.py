@@ -1,0 +1,206 @@
+"""JWT signing/verification (HS256 against the RFC 7515 A.1 vector, RS256, ES256), claim checks,
+JWKS, secrets providers, role store, the OIDC login state machine and the bearer-token middleware.
+Mirrors adapters/copilot_jwt_signer/tests, copilot_auth/tests (test_jwt_manager.py,
+test_middleware.py, test_mock_provider.py), copilot_secrets/tests and auth/tests of the reference."""
+from __future__ import annotations
+
+import base64
+import time
+
+import pytest
+
+from copilot_for_consensus_amd.security import jwt as J
+from copilot_for_consensus_amd.security.auth import (AuthService, JWTMiddleware, MockIdentityProvider, RoleStore,
+                                                     pkce_pair)
+from copilot_for_consensus_amd.security.secrets import (EnvSecretProvider, LocalFileSecretProvider, SecretNotFoundError,
+                                                        create_secret_provider)
+from copilot_for_consensus_amd.storage.document_store import InMemoryDocumentStore
+
+
+def _b64d(s):
+    return base64.urlsafe_b64decode(s + "=" * (-len(s) % 4))
+
+
+def test_hs256_rfc7515_appendix_a1_vector():
+    key = _b64d("AyM1SysPpbyDfgZld3umj1qzKObwVMkoqQ-EstJQLr_T-1qS0gZH75aKtMN3Yj0iPS4hcgUuTwjAzZr1Z9CAow")
+    signing_input = (b"eyJ0eXAiOiJKV1QiLA0KICJhbGciOiJIUzI1NiJ9."
+                     b"eyJpc3MiOiJqb2UiLA0KICJleHAiOjEzMDA4MTkzODAsDQogImh0dHA6Ly9leGFtcGxlLmNvbS9pc19yb290Ijp0cnVlfQ")
+    signer = J.HMACSigner(key)
+    assert J.b64u(signer.sign(signing_input)) == "dBjftJeZ4CVP-mB92K27uhbUJU1p1r_wW1gFWFOEjXk"
+    token = signing_input.decode() + ".dBjftJeZ4CVP-mB92K27uhbUJU1p1r_wW1gFWFOEjXk"
+    claims = J.decode(token, signer, now=1300819380 - 10)
+    assert claims["iss"] == "joe" and claims["http://example.com/is_root"] is True
+    with pytest.raises(J.JWTError, match="expired"):
+        J.decode(token, signer, now=1300819380 + 1000)
+
+
+@pytest.mark.parametrize("alg", ["HS256", "RS256", "ES256"])
+def test_sign_verify_roundtrip_and_tamper(alg):
+    kw = {"bits": 1024} if alg == "RS256" else {}
+    signer = J.create_jwt_signer(None, algorithm=alg, key_id="k1", **kw)
+    mgr = J.JWTManager(signer, issuer="iss", audience="aud", default_expiry=60)
+    tok = mgr.mint_token("user-1", {"roles": ["reader"]})
+    claims = mgr.validate_token(tok)
+    assert claims["sub"] == "user-1" and claims["roles"] == ["reader"] and claims["exp"] - claims["iat"] == 60
+    h, p, s = tok.split(".")
+    forged = J.b64u(b'{"sub":"admin","iss":"iss","aud":"aud","roles":["admin"]}')
+    with pytest.raises(J.JWTError, match="signature"):
+        J.decode(f"{h}.{forged}.{s}", signer)
+    with pytest.raises(J.JWTError, match="audience"):
+        mgr.validate_token(tok, audience="other")
+    with pytest.raises(J.JWTError, match="issuer"):
+        J.decode(tok, signer, issuer="someone-else")
+    if alg != "HS256":
+        jwks = mgr.get_jwks()
+        assert jwks["keys"][0]["kid"] == "k1"
+        assert J.decode(tok, jwks)["sub"] == "user-1"      # verify with only the public JWKS
+        with pytest.raises(J.JWTError, match="kid"):
+            J.decode(tok, {"keys": []})
+    else:
+        assert mgr.get_jwks() == {"keys": []}  # symmetric keys are never published
+
+
+def test_algorithm_confusion_is_rejected():
+    rs = J.RSASigner(bits=1024)
+    tok = J.encode({"sub": "x"}, rs)
+    # a token claiming HS256 must not verify against an RSA key (alg confusion)
+    h, p, s = tok.split(".")
+    hs_header = J.b64u(b'{"alg":"HS256","typ":"JWT","kid":"default"}')
+    with pytest.raises(J.JWTError):
+        J.decode(f"{hs_header}.{p}.{s}", rs.key)
+    with pytest.raises(J.JWTError):
+        J.decode("not.a.token", rs)
+    with pytest.raises(J.JWTError):
+        J.create_jwt_signer(None, algorithm="none")
+
+
+def test_nbf_and_leeway():
+    s = J.HMACSigner("k")
+    now = time.time()
+    tok = J.encode({"sub": "x", "nbf": now + 100, "exp": now + 200}, s)
+    with pytest.raises(J.JWTError, match="not yet"):
+        J.decode(tok, s, leeway=10)
+    assert J.decode(tok, s, leeway=120)["sub"] == "x"
+
+
+def test_rsa_key_serialisation_roundtrip():
+    k = J.RSAKey.generate(1024)
+    k2 = J.RSAKey.from_private_json(k.private_json())
+    sig = k2.sign(b"msg")
+    assert k.verify(b"msg", sig) and not k.verify(b"msg2", sig)
+    pub = J.RSAKey.from_jwk(k.public_jwk("x"))
+    assert pub.verify(b"msg", sig)
+
+
+def test_ec_key_serialisation_and_pem():
+    k = J.ECKey.generate()
+    signer = J.ECSigner(k.private_json(), key_id="e")
+    sig = signer.sign(b"m")
+    assert len(sig) == 64 and k.verify(b"m", sig) and not k.verify(b"n", sig)
+    assert k.public_pem().startswith("-----BEGIN PUBLIC KEY-----")
+
+
+# ------------------------------------------------------------------ secrets
+def test_local_file_secrets(tmp_path):
+    (tmp_path / "jwt_private_key").write_text("s3cret\n")
+    p = create_secret_provider("local", base_path=str(tmp_path))
+    assert isinstance(p, LocalFileSecretProvider)
+    assert p.get_secret("jwt_private_key") == "s3cret" and p.get_secret_bytes("jwt_private_key") == b"s3cret\n"
+    assert p.secret_exists("jwt_private_key") and not p.secret_exists("nope")
+    with pytest.raises(SecretNotFoundError):
+        p.get_secret("nope")
+    for bad in ("../etc/passwd", "a/b", "..", ""):
+        with pytest.raises(ValueError):
+            p.get_secret(bad)
+        assert not p.secret_exists(bad)
+
+
+def test_env_secrets():
+    p = EnvSecretProvider(prefix="app-", env={"APP_DB_PASSWORD": "pw"})
+    assert p.get_secret("db.password") == "pw" and p.secret_exists("db-password")
+    with pytest.raises(SecretNotFoundError):
+        p.get_secret("other")
+    with pytest.raises(ValueError):
+        create_secret_provider("vault9000")
+
+
+# ------------------------------------------------------------------ roles + login flow
+def _auth(first_admin=True):
+    store = InMemoryDocumentStore()
+    roles = RoleStore(store, first_user_auto_promotion=first_admin)
+    mgr = J.JWTManager(J.HMACSigner("k"), issuer="copilot-auth", audience="copilot-for-consensus")
+    return AuthService(mgr, roles, {"mock": MockIdentityProvider()}), roles, mgr
+
+
+def test_role_store_lifecycle():
+    _, roles, _ = _auth()
+    admin = roles.ensure_user({"sub": "u1", "email": "a@x", "name": "Ann"})
+    assert admin["roles"] == ["admin"] and admin["status"] == "approved"
+    second = roles.ensure_user({"sub": "u2", "email": "b@x", "name": "Bob"})
+    assert second["status"] == "pending" and [u["_id"] for u in roles.pending()] == ["u2"]
+    assert roles.assign("u2", ["reader", "processor"])["roles"] == ["processor", "reader"]
+    assert roles.revoke("u2", ["processor"])["roles"] == ["reader"]
+    assert [u["_id"] for u in roles.search("BOB")] == ["u2"]
+    roles.deny("u2")
+    assert roles.roles("u2") == []
+    with pytest.raises(KeyError):
+        roles.assign("ghost", ["reader"])
+    assert roles.ensure_user({"sub": "u1"})["roles"] == ["admin"]  # idempotent
+
+
+def test_pkce_pair_is_s256():
+    import hashlib
+    v, c = pkce_pair()
+    assert 43 <= len(v) <= 128 and c == J.b64u(hashlib.sha256(v.encode()).digest())
+
+
+def test_login_flow_and_refresh():
+    svc, roles, mgr = _auth()
+    start = svc.initiate_login("mock")
+    assert "state=" in start["authorization_url"]
+    res = svc.handle_callback("mock-user", start["state"])
+    claims = svc.validate_token(res["access_token"])
+    assert claims["sub"] == "mock:mock-user" and claims["roles"] == ["admin"]
+    with pytest.raises(PermissionError):
+        svc.handle_callback("mock-user", start["state"])  # state is single-use
+    with pytest.raises(PermissionError):
+        svc.handle_callback("x", "forged-state")
+    with pytest.raises(KeyError):
+        svc.initiate_login("myspace")
+    roles.revoke("mock:mock-user", ["admin"])
+    roles.assign("mock:mock-user", ["reader"])
+    refreshed = svc.validate_token(svc.refresh(res["access_token"])["access_token"])
+    assert refreshed["roles"] == ["reader"]  # refresh picks up role changes
+
+
+def test_state_expiry():
+    svc, _, _ = _auth()
+    svc.state_ttl = 0
+    st = svc.initiate_login("mock")["state"]
+    time.sleep(0.01)
+    with pytest.raises(PermissionError):
+        svc.handle_callback("c", st)
+
+
+def test_middleware_roles_and_http_codes():
+    from fastapi import Depends, FastAPI
+    from fastapi.testclient import TestClient
+
+    mgr = J.JWTManager(J.HMACSigner("k"), audience="copilot-for-consensus")
+    mw = JWTMiddleware(verify_key=mgr.signer, required_roles=["admin"])
+    app = FastAPI()
+
+    @app.get("/secret")
+    def secret(claims=Depends(mw.dependency())):
+        return {"sub": claims["sub"]}
+
+    c = TestClient(app)
+    assert c.get("/secret").status_code == 401
+    assert c.get("/secret", headers={"Authorization": "Bearer garbage"}).status_code == 401
+    reader = mgr.mint_token("r", {"roles": ["reader"]})
+    assert c.get("/secret", headers={"Authorization": f"Bearer {reader}"}).status_code == 403
+    admin = mgr.mint_token("a", {"roles": ["admin"]})
+    r = c.get("/secret", headers={"Authorization": f"Bearer {admin}"})
+    assert r.status_code == 200 and r.json() == {"sub": "a"}
+    other_aud = mgr.mint_token("a", {"roles": ["admin"]}, audience="elsewhere")
+    assert c.get("/secret", headers={"Authorization": f"Bearer {other_aud}"}).status_code == 401
