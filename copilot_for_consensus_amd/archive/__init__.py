@@ -159,9 +159,12 @@ class DocumentStoreArchiveStore(ArchiveStore):
         import base64
         aid = hashlib.sha256(content).hexdigest()[:16]
         if self.store.get_document(self.coll, aid) is None:
-            self.store.insert_document(self.coll, {"_id": aid, "source_name": source_name, "file_path": file_path,
+            self.store.insert_document(self.coll, {"_id": aid, "archive_id": aid, "source_name": source_name,
+                                                   "file_path": file_path, "original_path": file_path,
                                                    "file_hash": hashlib.sha256(content).hexdigest(),
+                                                   "content_hash": hashlib.sha256(content).hexdigest(),
                                                    "size_bytes": len(content),
+                                                   "stored_at": datetime.now(timezone.utc).isoformat(),
                                                    "content_b64": base64.b64encode(content).decode()})
         return aid
 
@@ -184,7 +187,7 @@ class DocumentStoreArchiveStore(ArchiveStore):
         return True
 
     def list_archives(self, source_name):
-        return [{k: v for k, v in d.items() if k != "content_b64"}
+        return [{**{k: v for k, v in d.items() if k not in ("content_b64", "_id")}, "archive_id": d["_id"]}
                 for d in self.store.query_documents(self.coll, {"source_name": source_name}, limit=1 << 30)]
 
 

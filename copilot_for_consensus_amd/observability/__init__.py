@@ -205,6 +205,10 @@ class PushGatewayMetricsCollector(PrometheusMetricsCollector):
                  raise_on_error: bool = False, grouping_key: dict | None = None, **_):
         super().__init__(namespace)
         self.gateway, self.job = gateway, job
+        if isinstance(grouping_key, str):  # env/config form: JSON object or "k=v,k2=v2"
+            gk = grouping_key.strip()
+            grouping_key = json.loads(gk) if gk.startswith("{") else dict(
+                kv.split("=", 1) for kv in gk.split(",") if "=" in kv)
         self.grouping_key = grouping_key or {}
         self.raise_on_error = raise_on_error
 
