@@ -218,10 +218,12 @@ def load_config_json(path) -> DecoderConfig:
 class DecoderModel:
     """Stateless forward functions over :class:`DecoderWeights` + a paged KV cache."""
 
-    def __init__(self, weights: DecoderWeights, tp_group=None, fused_decode: bool | None = None):
+    def __init__(self, weights: DecoderWeights, tp_group=None, fused_decode: bool | None = None, custom_ar=None):
         self.w = weights
         self.cfg = weights.cfg
         self.tp_group = tp_group
+        # validated one-shot IPC all-reduce (parallel/custom_ar.py) for decode-size tensors; RCCL otherwise
+        self.custom_ar = custom_ar
         self.scale = 1.0 / math.sqrt(self.cfg.head_dim)
         # decode projections on the split-K skinny MFMA GEMM with fused epilogues (TP=1; with TP>1
         # the all-reduce sits between the projection and the residual/norm)
@@ -238,6 +240,8 @@ class DecoderModel:
 
     def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.w.tp_size > 1:
+            if self.custom_ar is not None and self.custom_ar.supports(x):
+                return self.custom_ar(x)
             torch.distributed.all_reduce(x, group=self.tp_group)
         return x
 

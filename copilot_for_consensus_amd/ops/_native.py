@@ -43,6 +43,15 @@ _KERNEL_SIGS = {
     "cfc_skinny_gemm": [P, P, I, I, I, I, I, P, P, I, P],
     "cfc_splitk_reduce": [P, I, I, I, I, P, I, P],
     "cfc_splitk_residual_rmsnorm": [P, I, I, I, P, P, F, P, P],
+    "cfc_ar_region_bytes": [c_int64, P],
+    "cfc_ar_alloc": [c_int64, P],
+    "cfc_ar_free": [P],
+    "cfc_ar_ipc_handle_size": [],
+    "cfc_ar_ipc_handle": [P, P],
+    "cfc_ar_ipc_open": [P, P],
+    "cfc_ar_ipc_close": [P],
+    "cfc_ar_max_blocks": [],
+    "cfc_oneshot_allreduce": [P, P, c_int64, P, I, I, c_int64, I, P, P, P],
 }
 
 _RUNTIME_SIGS = {

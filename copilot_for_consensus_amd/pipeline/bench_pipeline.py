@@ -48,7 +48,11 @@ class BenchPipeline:
         self.rng = random.Random(seed)
         self.seed = seed
         w = DecoderWeights.random(self.cfg, self.device, seed=1234, tp_rank=tp_rank, tp_size=tp)
-        self.model = DecoderModel(w, tp_group=groups.tp_group if tp > 1 else None)
+        custom_ar = None
+        if tp > 1:
+            from ..parallel.custom_ar import maybe_create
+            custom_ar = maybe_create(groups.tp_group, self.device, exchange_group=groups.tp_cpu_group)
+        self.model = DecoderModel(w, tp_group=groups.tp_group if tp > 1 else None, custom_ar=custom_ar)
         # KV budget: every thread of a step at the longest prompt we generate (3k) + max_new, x1.1
         max_prompt = 4096
         nblk = int(1.1 * threads_per_step * blocks_needed(max_prompt + max_new_tokens)) + 64

@@ -95,7 +95,11 @@ class HipLLMSummarizer(Summarizer):
             self.tokenizer = synthetic_bpe(cfg.vocab_size)
         self.cfg = cfg
         self.model = cfg.name
-        self.decoder = DecoderModel(w, tp_group=tp_group)
+        custom_ar = None
+        if tp_group is not None and tensor_parallel > 1:
+            from ..parallel.custom_ar import maybe_create
+            custom_ar = maybe_create(tp_group, dev)
+        self.decoder = DecoderModel(w, tp_group=tp_group, custom_ar=custom_ar)
         self.kv = PagedKVCache.for_budget(cfg.layers, w.kv_heads, cfg.head_dim, dev, kv_cache_tokens)
         self.engine = LLMEngine(self.decoder, self.kv)
         self.max_new_tokens, self.temperature = int(max_new_tokens), float(temperature)
