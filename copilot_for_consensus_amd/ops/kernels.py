@@ -112,7 +112,10 @@ def decode_partitions(max_ctx: int, part_blocks: int) -> int:
 
 def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out=None, part_blocks=16,
                            num_partitions=None, workspace=None):
-    """q [B, Hq, D]; caches [nblk, Hkv, 32, D] / [nblk, Hkv, D, 32]; returns [B, Hq, D]."""
+    """q [B, Hq, D]; caches [nblk, Hkv, 32, D] / [nblk, Hkv, D, 32]; returns [B, Hq, D].
+
+    ``part_blocks`` > 0: split-KV partitions of that many blocks; ``part_blocks`` = -P: P balanced
+    partitions of each sequence's own context (what the engine uses)."""
     if not q.is_cuda:
         return ref.paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale)
     B, Hq, D = q.shape
@@ -120,6 +123,10 @@ def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, o
     _req(block_tables, torch.int32, "block_tables")
     _req(ctx_lens, torch.int32, "ctx_lens")
     max_blocks = block_tables.shape[1]
+    if part_blocks < 0:          # -P: every sequence's own blocks split into P balanced ranges
+        num_partitions, part_blocks = -part_blocks, 0
+    if part_blocks == 0 and not num_partitions:
+        raise ValueError("balanced partitioning needs num_partitions (or part_blocks=-P)")
     Pn = num_partitions or math.ceil(max_blocks / part_blocks)
     out = torch.empty_like(q) if out is None else out
     if Pn > 1:

@@ -87,9 +87,13 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ helpers
     def _part_blocks(self, B, max_blocks):
-        target = 4096
+        """Split-KV partitioning of the decode attention, as ``-P``: each sequence's own blocks in
+        P balanced ranges, P the smallest giving >= CFC_DECODE_WGS workgroups (default 512, two per
+        CU).  Long KV runs per workgroup win: at B=128 P=1 streams 6.5 TB/s vs 5.0-5.4 for fixed
+        26-block partitions (scripts/bench_decode_attn.py, profiles/decode_attn_partitions_r01.log)."""
+        target = int(os.environ.get("CFC_DECODE_WGS", "512"))
         P = max(1, math.ceil(target / max(1, B * self.model.w.kv_heads)))
-        return max(4, math.ceil(max_blocks / P))
+        return -min(P, max(1, max_blocks // 2))
 
     def _i32(self, x):
         return torch.tensor(x, dtype=torch.int32, device=self.device)
@@ -156,7 +160,7 @@ class LLMEngine:
         key = (B, max_blocks, max_new, tuple(stop_ids))
         st = self._states.get(key)
         if st is None:
-            P = math.ceil(max_blocks / part_blocks)
+            P = -part_blocks if part_blocks < 0 else math.ceil(max_blocks / part_blocks)
             ws = B * self.model.w.heads * P * (self.cfg.head_dim + 2) if P > 1 else 1
             st = _DecodeState(B, max_blocks, max_new, self.device, ws)
             # persistent: a captured graph holds this pointer

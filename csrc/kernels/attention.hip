@@ -78,8 +78,11 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   const int Hq = Hkv * G;
   const int ctx = ctx_lens[b];
   const int nblk = (ctx + KV_BS - 1) / KV_BS;
-  const int blk0 = p * part_blocks;
-  const int blk1 = min(nblk, blk0 + part_blocks);
+  // part_blocks > 0: fixed-size partitions of the block table; <= 0: the sequence's OWN blocks
+  // split into P near-equal ranges (balanced per sequence whatever its length -- no nearly empty
+  // tail partitions, and P can stay small, so each workgroup streams a long run of KV)
+  const int blk0 = part_blocks > 0 ? p * part_blocks : (int)(((int64_t)p * nblk) / P);
+  const int blk1 = part_blocks > 0 ? min(nblk, blk0 + part_blocks) : (int)(((int64_t)(p + 1) * nblk) / P);
 
   __shared__ float sm_o[4][D][17];
   __shared__ float sm_m[4][16], sm_l[4][16];
@@ -744,7 +747,10 @@ CFC_API int cfc_paged_decode_attention(const void* q, const void* k_cache, const
   const float sl2 = scale * LOG2E;
 #define DEC_ARGS (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, ctx_lens, sl2, \
     Hkv, max_blocks, part_blocks, P, part_o, part_ml, (uint16_t*)out
-  static const bool nt = [] { const char* e = getenv("CFC_DECODE_NT"); return e && atoi(e) != 0; }();
+  // nontemporal KV loads for large batches (B=128: 6.5 vs 5.9 TB/s; B=8: 3.8 vs 4.2 -- there the
+  // plain loads win), profiles/decode_attn_partitions_r01.log; CFC_DECODE_NT=0/1 forces either
+  static const int nt_env = [] { const char* e = getenv("CFC_DECODE_NT"); return e ? atoi(e) : -1; }();
+  const bool nt = nt_env >= 0 ? nt_env != 0 : B >= 32;
 #define DEC_CASE(GG) \
   case GG: \
     if (nt) paged_decode_kernel<GG, true><<<grid, 256, 0, stream>>>(DEC_ARGS); \
