@@ -111,7 +111,7 @@ class ParsingService(_CleanupMixin, BaseService):
         n = 0
         for a in self.store.query_documents("archives", {"status": {"$in": ["pending", "processing"]}}, limit=10000):
             self.publish("ArchiveIngested", archive_id=a["_id"], source_name=a.get("source", "unknown"),
-                         source_type="local", source_url=a.get("source_url") or a.get("file_path") or "requeue",
+                         source_type=a.get("source_type") or "local", source_url=a.get("source_url") or a.get("file_path") or "requeue",
                          file_size_bytes=int(a.get("file_size_bytes", 0)), file_hash_sha256=a.get("file_hash", "-"),
                          ingestion_started_at=a.get("ingestion_date") or utc_now_iso(),
                          ingestion_completed_at=utc_now_iso())
@@ -151,6 +151,9 @@ class ChunkingService(_CleanupMixin, BaseService):
                              "thread_id": c.thread_id, "archive_id": m.get("archive_id"),
                              "chunk_index": c.chunk_index, "text": c.text, "token_count": c.token_count,
                              "metadata": c.metadata, "created_at": now, "embedding_generated": False})
+        if not docs:  # only empty bodies: nothing to embed (and ChunksPrepared needs >= 1 chunk id)
+            self.metrics.increment("chunking_empty_messages_total", len(msgs))
+            return []
         self.store.insert_many("chunks", docs)  # duplicate ids tolerated (idempotent)
         self.metrics.increment("chunking_chunks_created_total", len(docs))
         self.publish("ChunksPrepared", message_doc_ids=list(message_doc_ids), chunk_count=len(docs),
@@ -345,6 +348,9 @@ class OrchestratorService(BaseService):
                 tids = self._resolve_threads(event["data"]["chunk_ids"])
             except Exception:
                 tids = []
+            if not tids:  # chunks never became visible: nothing to name (the event needs >= 1 thread)
+                self.log.error("orchestration failed before threads resolved", error=repr(error))
+                return
             self.publish("OrchestrationFailed", thread_ids=tids, error_type=type(error).__name__,
                          error_message=str(error) or type(error).__name__, retry_count=0)
 
@@ -447,8 +453,10 @@ class SummarizationService(BaseService):
                     batch, self._queue = self._queue[:self.max_batch], self._queue[self.max_batch:]
                 try:
                     self.summarize_events(batch)
-                except Exception as e:
+                except Exception as e:  # engine failure after retries: every thread of the batch fails
                     self.log.error("summarization batch failed", error=repr(e))
+                    for ev in batch:
+                        self.on_failure("SummarizationRequested", ev, e)
         self._worker = threading.Thread(target=loop, name="summarization-batcher", daemon=True)
         self._worker.start()
 

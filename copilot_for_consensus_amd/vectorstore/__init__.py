@@ -60,6 +60,9 @@ class VectorStore(ABC):
     @abstractmethod
     def get(self, id: str) -> SearchResult: ...
 
+    def __len__(self) -> int:
+        return self.count()
+
     def query_batch(self, query_vectors, top_k: int = 10) -> list[list[SearchResult]]:
         return [self.query(q, top_k) for q in query_vectors]
 
