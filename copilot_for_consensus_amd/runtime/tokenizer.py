@@ -14,7 +14,9 @@ from __future__ import annotations
 import ctypes
 import json
 import os
+import re
 import threading
+import unicodedata
 from pathlib import Path
 
 import numpy as np
@@ -48,11 +50,19 @@ def _batch(fn, handle, texts: list[str], cap: int, truncate: bool = False) -> li
 
 
 class BPETokenizer:
-    def __init__(self, vocab: list[str], merges: list[tuple[int, int]], bos_id: int = 1, eos_id: int = 2):
+    SPLIT_EVERY_MARK, SPLIT_SENTENCEPIECE = 0, 1
+    PREPEND_UNLESS_PRESENT, PREPEND_ALWAYS, PREPEND_NEVER = 0, 1, 2
+
+    def __init__(self, vocab: list[str], merges: list[tuple[int, int]], bos_id: int = 1, eos_id: int = 2,
+                 split_mode: int = 0, prepend_mode: int = 0):
+        """``split_mode`` / ``prepend_mode``: see csrc/runtime/tokenizer.cpp (HF Metaspace(split) =
+        0/0, HF Llama-2/Mistral files with Prepend+Replace normalizers and no pre-tokenizer = 1/1)."""
         self.vocab = vocab
         self.bos_id, self.eos_id = bos_id, eos_id
         self._lib = runtime()
         self._h = self._lib.cfc_bpe_create()
+        if self._lib.cfc_bpe_set_mode(self._h, int(split_mode), int(prepend_mode)) != 0:
+            raise ValueError(f"bad BPE modes split={split_mode} prepend={prepend_mode}")
         for i, t in enumerate(vocab):
             b, n = _c(t)
             self._lib.cfc_bpe_add_token(self._h, b, n, i)
@@ -124,12 +134,39 @@ class BPETokenizer:
             if a in v and b in v:
                 merges.append((v[a], v[b]))
         specials = {at["content"]: at["id"] for at in d.get("added_tokens", [])}
-        return cls(vocab, merges, specials.get("<s>", 1), specials.get("</s>", 2))
+        split_mode, prepend_mode = _sentencepiece_modes(d)
+        return cls(vocab, merges, specials.get("<s>", 1), specials.get("</s>", 2), split_mode, prepend_mode)
 
     @classmethod
     def train(cls, corpus: str, vocab_size: int = 32000) -> "BPETokenizer":
         vocab, pairs = train_bpe(corpus, vocab_size)
         return cls(vocab, pairs)
+
+
+def _flatten_steps(node: dict | None, key: str) -> list[dict]:
+    if not node:
+        return []
+    if node.get("type") == "Sequence":
+        return [x for sub in node.get(key, []) for x in _flatten_steps(sub, key)]
+    return [node]
+
+
+def _sentencepiece_modes(d: dict) -> tuple[int, int]:
+    """(split_mode, prepend_mode) of an HF tokenizer.json's SentencePiece-style pipeline."""
+    pre = _flatten_steps(d.get("pre_tokenizer"), "pretokenizers")
+    norm = _flatten_steps(d.get("normalizer"), "normalizers")
+    kinds = {p.get("type") for p in pre}
+    if kinds - {"Metaspace"}:
+        raise NotImplementedError(f"pre-tokenizers {sorted(kinds)} are not SentencePiece-style (byte-level BPE "
+                                  "tokenizer.json files are not supported by BPETokenizer)")
+    if pre:
+        m = pre[0]
+        scheme = m.get("prepend_scheme") or ("always" if m.get("add_prefix_space", True) else "never")
+        prepend = BPETokenizer.PREPEND_NEVER if scheme == "never" else BPETokenizer.PREPEND_UNLESS_PRESENT
+        split = BPETokenizer.SPLIT_EVERY_MARK if m.get("split", True) else BPETokenizer.SPLIT_SENTENCEPIECE
+        return split, prepend
+    prepends = [n for n in norm if n.get("type") == "Prepend"]
+    return BPETokenizer.SPLIT_SENTENCEPIECE, (BPETokenizer.PREPEND_ALWAYS if prepends else BPETokenizer.PREPEND_NEVER)
 
 
 def train_bpe(corpus: str, vocab_size: int) -> tuple[list[str], list[tuple[int, int]]]:
@@ -176,12 +213,41 @@ def synthetic_bpe(vocab_size: int = 32000, corpus_words: int = 800_000) -> BPETo
         return tok
 
 
+_ASCII_CTRL = re.compile(r"[\x00-\x08\x0b\x0c\x0e-\x1f\x7f]")
+
+
+def bert_normalize(text: str, lowercase: bool = True) -> str:
+    """HF BertNormalizer + the Unicode part of BertPreTokenizer, for non-ASCII text: drop control
+    characters, map Unicode spaces to ' ', strip accents (NFD, drop Mn) and lower-case (uncased
+    models), and space-pad Unicode punctuation so the C++ splitter isolates it.  Pure-ASCII text
+    without control characters is returned unchanged -- the C++ tokenizer handles it natively."""
+    if text.isascii() and not _ASCII_CTRL.search(text):
+        return text
+    out = []
+    for c in text:
+        cp = ord(c)
+        if cp == 0 or cp == 0xFFFD:
+            continue
+        cat = unicodedata.category(c)
+        if c in "\t\n\r" or cat == "Zs":
+            out.append(" ")
+        elif cat in ("Cc", "Cf"):
+            continue
+        else:
+            out.append(c)
+    t = "".join(out)
+    if lowercase:
+        t = "".join(c for c in unicodedata.normalize("NFD", t) if unicodedata.category(c) != "Mn").lower()
+    return "".join(f" {c} " if ord(c) > 127 and unicodedata.category(c).startswith("P") else c for c in t)
+
+
 class WordPieceTokenizer:
     PAD, UNK, CLS, SEP, MASK = 0, 100, 101, 102, 103
 
     def __init__(self, vocab: list[str], lowercase: bool = True, max_length: int = 512):
         self.vocab = vocab
         self.max_length = max_length
+        self.lowercase = lowercase
         self._lib = runtime()
         tok2id = {t: i for i, t in enumerate(vocab)}
         self.unk_id = tok2id.get("[UNK]", self.UNK)
@@ -203,7 +269,7 @@ class WordPieceTokenizer:
     def encode(self, text: str, max_length: int | None = None) -> list[int]:
         """[CLS] pieces [SEP], truncated to max_length (sentence-transformers behaviour)."""
         L = max_length or self.max_length
-        b, n = _c(text)
+        b, n = _c(bert_normalize(text, self.lowercase))
         with self._enc_lock:
             k = self._lib.cfc_wp_encode(self._h, b, n, self._buf.ctypes.data, len(self._buf))
             if k > len(self._buf):
@@ -215,6 +281,7 @@ class WordPieceTokenizer:
     def encode_batch(self, texts: list[str], max_length: int | None = None) -> list[list[int]]:
         L = max_length or self.max_length
         # truncation makes every result fit: ask for L-2 pieces, longer texts are simply cut
+        texts = [bert_normalize(t, self.lowercase) for t in texts]
         res = _batch(self._lib.cfc_wp_encode_batch, self._h, texts, max(1, L - 2), truncate=True)
         return [[self.cls_id] + ids + [self.sep_id] for ids in res]
 

@@ -118,37 +118,39 @@ struct BPE {
 
   void encode(const std::string& text, std::vector<int>& out) { encode(text, out, cache); }
 
+  // HF tokenizer.json semantics of the SentencePiece-style pipelines:
+  //   split_mode 0 -- Metaspace(split=true): a new piece starts at EVERY "▁" ("▁▁▁a" -> ▁ ▁ ▁a);
+  //   split_mode 1 -- no pre-tokenizer (Llama-2/Mistral files: Prepend + Replace normalizers):
+  //                   the whole text is one sequence; splitting where a "▁" follows a non-"▁"
+  //                   character is exact for SentencePiece vocabularies, whose pieces carry "▁"
+  //                   only as a prefix (runs like "▁▁▁" still merge);
+  //   prepend_mode 0 -- prepend "▁" unless the text already starts with one (Metaspace "always"),
+  //                1 -- always (Prepend normalizer), 2 -- never.
+  // Newlines are ordinary characters inside a piece (SentencePiece: "a\nb" -> ▁a <0x0A> b).
+  int split_mode = 0, prepend_mode = 0;
+
   void encode(const std::string& text, std::vector<int>& out, WordCache& wc) const {
-    // SentencePiece normalisation: spaces -> "▁", dummy prefix; newlines are their own pieces
-    size_t i = 0;
-    bool first = true;
-    while (i < text.size()) {
-      if (text[i] == '\n') {
-        std::string nl = "\n";
-        encode_word(nl, out, wc);
-        ++i;
-        first = true;
-        continue;
-      }
-      size_t j = i;
-      while (j < text.size() && text[j] == ' ') ++j;
-      size_t k = j;
-      while (k < text.size() && text[k] != ' ' && text[k] != '\n') ++k;
-      if (k == j) {  // trailing spaces
-        for (size_t s = i; s < j; ++s) encode_word(kSpaceMark, out, wc);
-        i = j;
-        continue;
-      }
-      std::string w;
-      // one "▁" per preceding space (first word gets the dummy prefix)
-      const size_t spaces = (j - i) + (first && j == i ? 1 : 0);
-      for (size_t s = 1; s < spaces; ++s) encode_word(kSpaceMark, out, wc);
-      if (spaces > 0) w = kSpaceMark;
-      w.append(text, j, k - j);
-      encode_word(w, out, wc);
-      first = false;
-      i = k;
+    if (text.empty()) return;
+    std::string norm;
+    norm.reserve(text.size() + text.size() / 2 + 3);
+    if (prepend_mode == 1 || (prepend_mode == 0 && text[0] != ' ')) norm += kSpaceMark;
+    for (char c : text) {
+      if (c == ' ') norm += kSpaceMark;
+      else norm.push_back(c);
     }
+    // kSpaceMark's lead byte 0xE2 never occurs inside another UTF-8 sequence, so a byte scan is safe
+    size_t start = 0;
+    bool prev_mark = false;
+    for (size_t p = 0; p < norm.size();) {
+      const bool mark = norm.compare(p, 3, kSpaceMark) == 0;
+      if (mark && p > start && (split_mode == 0 || !prev_mark)) {
+        encode_word(norm.substr(start, p - start), out, wc);
+        start = p;
+      }
+      prev_mark = mark;
+      p += mark ? 3 : 1;
+    }
+    if (start < norm.size()) encode_word(norm.substr(start), out, wc);
   }
 };
 
@@ -241,6 +243,15 @@ CFC_API int cfc_bpe_add_merge(void* h, int a, int b, int rank, int merged) {
 }
 
 CFC_API int cfc_bpe_finalize(void* h) { static_cast<BPE*>(h)->finalize(); return 0; }
+
+CFC_API int cfc_bpe_set_mode(void* h, int split_mode, int prepend_mode) {
+  if (split_mode < 0 || split_mode > 1 || prepend_mode < 0 || prepend_mode > 2) return -1;
+  auto* b = static_cast<BPE*>(h);
+  b->split_mode = split_mode;
+  b->prepend_mode = prepend_mode;
+  b->cache.clear();
+  return 0;
+}
 
 // Returns the number of ids produced (may exceed cap: call again with a bigger buffer).
 CFC_API int cfc_bpe_encode(void* h, const char* text, int len, int32_t* out, int cap) {

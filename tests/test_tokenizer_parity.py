@@ -1,0 +1,132 @@
+"""C++ tokenizers vs HF ``tokenizers`` (the Rust library the reference's SentenceTransformers /
+HF stacks tokenise with): vocabularies are trained here with HF trainers on mailing-list text,
+loaded into the native WordPiece / SentencePiece-BPE, and every encoding must be identical --
+fixed edge cases plus Hypothesis-generated Unicode text (accents, CJK, emoji, punctuation, runs
+of spaces and newlines).  Both tokenizer.json shapes of SentencePiece models are covered:
+Metaspace pre-tokenizer, and the Llama-2/Mistral form (Prepend + Replace normalizers, no
+pre-tokenizer)."""
+from __future__ import annotations
+
+import json
+import os
+
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+tokenizers = pytest.importorskip("tokenizers")
+from tokenizers import Tokenizer, decoders, models, normalizers, pre_tokenizers, trainers  # noqa: E402
+
+from copilot_for_consensus_amd.parsing import MessageParser  # noqa: E402
+from copilot_for_consensus_amd.runtime.tokenizer import BPETokenizer, WordPieceTokenizer  # noqa: E402
+
+FIX = os.path.join(os.path.dirname(__file__), "fixtures", "sample.mbox")
+EXTRA = ["Hello, World! Café déjà-vu naïve — “quotes” 123.45 e-mail@x.org (RFC 9000)",
+         "ÀÉÎÕÜ ß 東京 emoji 😀 tab\there ¡Hola! «citation» 1·2", "draft-ietf-quic-http-34: don't stop!!"]
+CASES = EXTRA + ["  leading   spaces  ", "", " ", "\n", "a\nb", "x\n\n  y", "UPPER lower MiXeD", "ok.\r\nnext",
+                 "zero​width", "nbsp here", "tab\tsep", "a" * 150, "ｆｕｌｌｗｉｄｔｈ"]
+
+
+@pytest.fixture(scope="module")
+def corpus():
+    msgs, _ = MessageParser().parse_mbox_bytes(open(FIX, "rb").read(), "0" * 16)
+    return [m["body_normalized"] for m in msgs] * 3 + EXTRA
+
+
+@pytest.fixture(scope="module")
+def wordpiece(corpus):
+    ref = Tokenizer(models.WordPiece(unk_token="[UNK]"))
+    ref.normalizer = normalizers.BertNormalizer(lowercase=True)
+    ref.pre_tokenizer = pre_tokenizers.BertPreTokenizer()
+    ref.train_from_iterator(corpus, trainers.WordPieceTrainer(
+        vocab_size=2000, special_tokens=["[PAD]", "[UNK]", "[CLS]", "[SEP]", "[MASK]"]))
+    vocab = [None] * ref.get_vocab_size()
+    for t, i in ref.get_vocab().items():
+        vocab[i] = t
+    return ref, WordPieceTokenizer(vocab, max_length=100000)
+
+
+def _sp_bpe(corpus, tmp_path_factory, legacy: bool):
+    ref = Tokenizer(models.BPE(byte_fallback=True, unk_token="<unk>", fuse_unk=True))
+    ref.pre_tokenizer = pre_tokenizers.Metaspace(replacement="▁", prepend_scheme="always", split=True)
+    ref.decoder = decoders.Metaspace(replacement="▁", prepend_scheme="always", split=True)
+    ref.train_from_iterator(corpus, trainers.BpeTrainer(
+        vocab_size=3000, special_tokens=["<unk>", "<s>", "</s>"] + [f"<0x{i:02X}>" for i in range(256)]))
+    d = json.loads(ref.to_str())
+    if legacy:  # the Llama-2 / Mistral tokenizer.json pipeline, same vocabulary and merges
+        d["pre_tokenizer"] = None
+        d["normalizer"] = {"type": "Sequence", "normalizers": [{"type": "Prepend", "prepend": "▁"},
+                                                               {"type": "Replace", "pattern": {"String": " "},
+                                                                "content": "▁"}]}
+        ref = Tokenizer.from_str(json.dumps(d))
+    p = tmp_path_factory.mktemp("tok") / "tokenizer.json"
+    p.write_text(json.dumps(d))
+    return ref, BPETokenizer.from_hf_json(p)
+
+
+@pytest.fixture(scope="module")
+def sp_metaspace(corpus, tmp_path_factory):
+    return _sp_bpe(corpus, tmp_path_factory, legacy=False)
+
+
+@pytest.fixture(scope="module")
+def sp_legacy(corpus, tmp_path_factory):
+    return _sp_bpe(corpus, tmp_path_factory, legacy=True)
+
+
+def _wp_ids(ref, mine, text):
+    return ref.encode(text).ids, mine.encode(text)[1:-1]
+
+
+def test_wordpiece_matches_hf(wordpiece, corpus):
+    ref, mine = wordpiece
+    for t in corpus[:10] + CASES:
+        want, got = _wp_ids(ref, mine, t)
+        assert got == want, (t, [mine.vocab[i] for i in want], [mine.vocab[i] for i in got])
+    batch = mine.encode_batch(CASES)
+    assert [b[1:-1] for b in batch] == [ref.encode(t).ids for t in CASES]
+
+
+@pytest.mark.parametrize("which", ["sp_metaspace", "sp_legacy"])
+def test_sentencepiece_bpe_matches_hf(which, request, corpus):
+    ref, mine = request.getfixturevalue(which)
+    for t in corpus[:10] + CASES:
+        want = ref.encode(t).ids
+        got = mine.encode(t, add_bos=False)
+        assert got == want, (which, t, [mine.vocab[i] for i in want], [mine.vocab[i] for i in got])
+    assert [x[1:] for x in mine.encode_batch(CASES)] == [ref.encode(t).ids for t in CASES]
+
+
+_alphabet = st.sampled_from(list("abcdefghij ABC  \n\t.,!?-'\"éèüñçÅ東京ß😀—“”«»¡·") + ["  ", "\n\n", "ing", "the"])
+_text = st.lists(_alphabet, max_size=60).map("".join)
+
+
+@settings(max_examples=300, deadline=None)
+@given(_text)
+def test_fuzz_wordpiece(wordpiece, text):
+    ref, mine = wordpiece
+    want, got = _wp_ids(ref, mine, text)
+    assert got == want
+
+
+@settings(max_examples=300, deadline=None)
+@given(_text)
+def test_fuzz_sentencepiece(sp_metaspace, sp_legacy, text):
+    for ref, mine in (sp_metaspace, sp_legacy):
+        assert mine.encode(text, add_bos=False) == ref.encode(text).ids
+
+
+def test_decode_roundtrip(sp_metaspace):
+    _, mine = sp_metaspace
+    for t in ["Hello world", "a\nb  c", "東京 😀"]:
+        assert mine.decode(mine.encode(t)) == t
+
+
+def test_byte_level_tokenizer_json_is_rejected(tmp_path):
+    bl = Tokenizer(models.BPE())
+    bl.pre_tokenizer = pre_tokenizers.ByteLevel()
+    bl.train_from_iterator(["some text here"], trainers.BpeTrainer(vocab_size=300))
+    p = tmp_path / "bl.json"
+    bl.save(str(p))
+    with pytest.raises(NotImplementedError):
+        BPETokenizer.from_hf_json(p)
