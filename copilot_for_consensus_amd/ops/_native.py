@@ -61,6 +61,7 @@ _RUNTIME_SIGS = {
     "cfc_bpe_add_merge": [P, I, I, I, I],
     "cfc_bpe_finalize": [P],
     "cfc_bpe_set_mode": [P, I, I],
+    "cfc_bpe_encode_pieces": [P, ctypes.c_char_p, P, I, P, I],
     "cfc_bpe_encode": [P, ctypes.c_char_p, I, P, I],
     "cfc_bpe_decode": [P, P, I, ctypes.c_char_p, I],
     "cfc_bpe_train": [ctypes.c_char_p, I, I, P, P, I],

@@ -191,6 +191,163 @@ def train_bpe(corpus: str, vocab_size: int) -> tuple[list[str], list[tuple[int, 
 _SYNTH_TOKENIZERS: dict = {}
 
 
+# ------------------------------------------------------------------------------ byte-level BPE
+
+# Llama-3's pre-tokenisation regex (tiktoken cl100k-style, digits in groups of up to 3)
+LLAMA3_PATTERN = (r"(?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}{1,3}| ?[^\s\p{L}\p{N}]+[\r\n]*"
+                  r"|\s*[\r\n]+|\s+(?!\S)|\s+")
+GPT2_PATTERN = r"""'s|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+"""
+
+
+def bytes_to_unicode() -> dict[int, str]:
+    """GPT-2's reversible byte -> printable character map used by ByteLevel BPE vocabularies."""
+    bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("¡"), ord("¬") + 1)) + list(range(ord("®"), ord("ÿ") + 1))
+    cs = bs[:]
+    n = 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    return {b: chr(c) for b, c in zip(bs, cs)}
+
+
+class ByteLevelBPETokenizer:
+    """Byte-level BPE (Llama-3 / GPT-style tokenizer.json): regex pre-tokenisation (``regex``
+    module, Unicode classes), bytes mapped to printable stand-ins, then the native merge loop
+    (csrc/runtime/tokenizer.cpp ``cfc_bpe_encode_pieces``).  Added/special tokens are matched
+    verbatim before pre-tokenisation, as HF does."""
+
+    def __init__(self, vocab: list[str], merges: list[tuple[int, int]], pattern: str = LLAMA3_PATTERN,
+                 special_tokens: dict[str, int] | None = None, bos_id: int | None = None, eos_id: int | None = None,
+                 add_prefix_space: bool = False):
+        import regex
+        self.vocab = vocab
+        self._pat = regex.compile(pattern)
+        self.special = dict(special_tokens or {})
+        self._special_re = (regex.compile("|".join(regex.escape(t) for t in sorted(self.special, key=len, reverse=True)))
+                            if self.special else None)
+        self.bos_id, self.eos_id = bos_id, eos_id
+        self.add_prefix_space = add_prefix_space
+        self._b2u = bytes_to_unicode()
+        self._u2b = {c: b for b, c in self._b2u.items()}
+        self._lib = runtime()
+        self._h = self._lib.cfc_bpe_create()
+        for i, t in enumerate(vocab):
+            b, n = _c(t)
+            self._lib.cfc_bpe_add_token(self._h, b, n, i)
+        tok2id = {t: i for i, t in enumerate(vocab)}
+        for rank, (a, b) in enumerate(merges):
+            merged = tok2id.get(vocab[a] + vocab[b])
+            if merged is not None:
+                self._lib.cfc_bpe_add_merge(self._h, a, b, rank, merged)
+        self._lib.cfc_bpe_finalize(self._h)
+        self._buf = np.empty(1 << 16, dtype=np.int32)
+        self._enc_lock = threading.Lock()
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._lib.cfc_bpe_destroy(h)
+            self._h = None
+
+    @property
+    def vocab_size(self) -> int:
+        return len(self.vocab)
+
+    def _pieces(self, text: str) -> list[str]:
+        if self.add_prefix_space and text and not text.startswith(" "):
+            text = " " + text
+        b2u = self._b2u
+        return ["".join(b2u[x] for x in m.encode("utf-8")) for m in self._pat.findall(text)]
+
+    def _encode_plain(self, text: str) -> list[int]:
+        pieces = self._pieces(text)
+        if not pieces:
+            return []
+        bs = [p.encode("utf-8") for p in pieces]
+        offs = np.zeros(len(bs) + 1, dtype=np.int64)
+        np.cumsum([len(b) for b in bs], out=offs[1:])
+        with self._enc_lock:
+            k = self._lib.cfc_bpe_encode_pieces(self._h, b"".join(bs), offs.ctypes.data, len(bs),
+                                                self._buf.ctypes.data, len(self._buf))
+            if k > len(self._buf):
+                self._buf = np.empty(2 * k, dtype=np.int32)
+                k = self._lib.cfc_bpe_encode_pieces(self._h, b"".join(bs), offs.ctypes.data, len(bs),
+                                                    self._buf.ctypes.data, len(self._buf))
+            return self._buf[:k].tolist()
+
+    def encode(self, text: str, add_bos: bool = True) -> list[int]:
+        ids: list[int] = [self.bos_id] if (add_bos and self.bos_id is not None) else []
+        if self._special_re is None:
+            return ids + self._encode_plain(text)
+        pos = 0
+        for m in self._special_re.finditer(text):
+            ids += self._encode_plain(text[pos:m.start()])
+            ids.append(self.special[m.group()])
+            pos = m.end()
+        return ids + self._encode_plain(text[pos:])
+
+    def encode_batch(self, texts: list[str], add_bos: bool = True, cap: int = 16384) -> list[list[int]]:
+        return [self.encode(t, add_bos) for t in texts]
+
+    def decode(self, ids: list[int]) -> str:
+        skip = {i for i in (self.bos_id, self.eos_id) if i is not None}
+        inv_special = {v: k for k, v in self.special.items()}
+        out = bytearray()
+        for i in ids:
+            if i in skip:
+                continue
+            if i in inv_special:
+                out += inv_special[i].encode("utf-8")
+                continue
+            out += bytes(self._u2b[c] for c in self.vocab[i] if c in self._u2b)
+        return out.decode("utf-8", errors="replace")
+
+    @classmethod
+    def from_hf_json(cls, path) -> "ByteLevelBPETokenizer":
+        d = json.loads(Path(path).read_text())
+        model = d["model"]
+        if model.get("type") != "BPE":
+            raise ValueError("tokenizer.json is not a BPE model")
+        pre = _flatten_steps(d.get("pre_tokenizer"), "pretokenizers")
+        kinds = [p.get("type") for p in pre]
+        if "ByteLevel" not in kinds:
+            raise NotImplementedError("not a byte-level BPE tokenizer.json (use BPETokenizer)")
+        pattern, add_prefix = GPT2_PATTERN, False
+        for p in pre:
+            if p.get("type") == "Split":
+                pat = p.get("pattern", {})
+                pattern = pat.get("Regex") or __import__("regex").escape(pat.get("String", ""))
+            elif p.get("type") == "ByteLevel":
+                add_prefix = bool(p.get("add_prefix_space", False))
+                if p.get("use_regex", True) and "Split" not in kinds:
+                    pattern = GPT2_PATTERN
+        v = model["vocab"]
+        added = {at["content"]: at["id"] for at in d.get("added_tokens", [])}
+        size = max(list(v.values()) + list(added.values())) + 1
+        vocab = [f"<unused{i}>" for i in range(size)]
+        for t, i in v.items():
+            vocab[i] = t
+        for t, i in added.items():
+            vocab[i] = t
+        merges = []
+        for m in model["merges"]:
+            a, b = m.split(" ", 1) if isinstance(m, str) else m
+            if a in v and b in v:
+                merges.append((v[a], v[b]))
+        bos = added.get("<|begin_of_text|>", added.get("<s>"))
+        eos = added.get("<|end_of_text|>", added.get("</s>", added.get("<|endoftext|>")))
+        return cls(vocab, merges, pattern, added, bos, eos, add_prefix)
+
+
+def load_hf_tokenizer(path):
+    """BPETokenizer (SentencePiece-style) or ByteLevelBPETokenizer, from the tokenizer.json's pipeline."""
+    d = json.loads(Path(path).read_text())
+    kinds = {p.get("type") for p in _flatten_steps(d.get("pre_tokenizer"), "pretokenizers")}
+    return ByteLevelBPETokenizer.from_hf_json(path) if "ByteLevel" in kinds else BPETokenizer.from_hf_json(path)
+
+
 def synthetic_bpe(vocab_size: int = 32000, corpus_words: int = 800_000) -> BPETokenizer:
     """Deterministic BPE trained on the synthetic mailing-list distribution (cached on disk)."""
     key = ("bpe", vocab_size)

@@ -82,13 +82,13 @@ class HipLLMSummarizer(Summarizer):
         from ..models.decoder import DecoderModel, DecoderWeights, get_config, load_config_json
         from ..runtime.engine import LLMEngine
         from ..runtime.kv_cache import PagedKVCache
-        from ..runtime.tokenizer import BPETokenizer, synthetic_bpe
+        from ..runtime.tokenizer import load_hf_tokenizer, synthetic_bpe
         dev = torch.device(device if (not str(device).startswith("cuda") or torch.cuda.is_available()) else "cpu")
         if checkpoint_dir:
             from pathlib import Path
             cfg = load_config_json(Path(checkpoint_dir) / "config.json")
             w = DecoderWeights.from_safetensors(cfg, checkpoint_dir, dev, tp_rank, tensor_parallel)
-            self.tokenizer = BPETokenizer.from_hf_json(Path(checkpoint_dir) / "tokenizer.json")
+            self.tokenizer = load_hf_tokenizer(Path(checkpoint_dir) / "tokenizer.json")
         else:
             cfg = get_config(model)
             w = DecoderWeights.random(cfg, dev, seed=seed, tp_rank=tp_rank, tp_size=tensor_parallel)

@@ -445,6 +445,20 @@ CFC_API int cfc_bpe_encode_batch(void* h, const char* buf, const int64_t* offs, 
   return 0;
 }
 
+// Byte-level BPE (GPT-2 / tiktoken / Llama-3 tokenizer.json): the caller has already split the text
+// with the model's regex and mapped every byte to its printable stand-in character; each piece is
+// merged independently (no "▁" handling, no byte fallback needed).  Concatenated ids into out;
+// returns their count (may exceed cap).
+CFC_API int cfc_bpe_encode_pieces(void* h, const char* buf, const int64_t* offs, int n, int32_t* out, int cap) {
+  auto* b = static_cast<BPE*>(h);
+  std::vector<int> ids;
+  for (int i = 0; i < n; ++i)
+    b->encode_word(std::string(buf + offs[i], (size_t)(offs[i + 1] - offs[i])), ids);
+  const int m = (int)ids.size();
+  for (int k = 0; k < std::min(m, cap); ++k) out[k] = ids[k];
+  return m;
+}
+
 CFC_API int cfc_wp_encode_batch(void* h, const char* buf, const int64_t* offs, int n, int cap, int32_t* out,
                                 int32_t* lens, int nthreads) {
   const auto* w = static_cast<const WordPiece*>(h);

@@ -1,6 +1,7 @@
 """C++ tokenizers vs HF ``tokenizers`` (the Rust library the reference's SentenceTransformers /
 HF stacks tokenise with): vocabularies are trained here with HF trainers on mailing-list text,
-loaded into the native WordPiece / SentencePiece-BPE, and every encoding must be identical --
+loaded into the native WordPiece / SentencePiece-BPE / byte-level BPE (Llama-3 regex), and every
+encoding must be identical --
 fixed edge cases plus Hypothesis-generated Unicode text (accents, CJK, emoji, punctuation, runs
 of spaces and newlines).  Both tokenizer.json shapes of SentencePiece models are covered:
 Metaspace pre-tokenizer, and the Llama-2/Mistral form (Prepend + Replace normalizers, no
@@ -130,3 +131,38 @@ def test_byte_level_tokenizer_json_is_rejected(tmp_path):
     bl.save(str(p))
     with pytest.raises(NotImplementedError):
         BPETokenizer.from_hf_json(p)
+
+
+# ------------------------------------------------------------------ byte-level BPE (Llama-3 style)
+@pytest.fixture(scope="module")
+def bytelevel(corpus, tmp_path_factory):
+    from copilot_for_consensus_amd.runtime.tokenizer import LLAMA3_PATTERN, load_hf_tokenizer
+    ref = Tokenizer(models.BPE())
+    ref.pre_tokenizer = pre_tokenizers.Sequence([
+        pre_tokenizers.Split(tokenizers.Regex(LLAMA3_PATTERN), behavior="isolated", invert=False),
+        pre_tokenizers.ByteLevel(add_prefix_space=False, use_regex=False)])
+    ref.decoder = decoders.ByteLevel()
+    ref.train_from_iterator(corpus, trainers.BpeTrainer(
+        vocab_size=1500, special_tokens=["<|begin_of_text|>", "<|end_of_text|>"],
+        initial_alphabet=pre_tokenizers.ByteLevel.alphabet()))
+    p = tmp_path_factory.mktemp("bl") / "tokenizer.json"
+    ref.save(str(p))
+    return ref, load_hf_tokenizer(p)
+
+
+def test_bytelevel_bpe_matches_hf(bytelevel, corpus):
+    from copilot_for_consensus_amd.runtime.tokenizer import ByteLevelBPETokenizer
+    ref, mine = bytelevel
+    assert isinstance(mine, ByteLevelBPETokenizer)
+    for t in corpus[:10] + CASES + ["<|begin_of_text|>Hi<|end_of_text|> there 12345 I'LL go"]:
+        want = ref.encode(t).ids
+        got = mine.encode(t, add_bos=False)
+        assert got == want, (t, [mine.vocab[i] for i in want], [mine.vocab[i] for i in got])
+        assert mine.decode(got) == ref.decode(want, skip_special_tokens=False) or "<|" in t
+
+
+@settings(max_examples=300, deadline=None)
+@given(_text)
+def test_fuzz_bytelevel(bytelevel, text):
+    ref, mine = bytelevel
+    assert mine.encode(text, add_bos=False) == ref.encode(text).ids
