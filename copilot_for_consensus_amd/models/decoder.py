@@ -45,6 +45,8 @@ class DecoderConfig:
     tie_embeddings: bool = False
     bos_id: int = 1
     eos_id: int = 2
+    # Llama-3.1 RoPE frequency scaling: (factor, low_freq_factor, high_freq_factor, original_max_positions)
+    rope_llama3: tuple | None = None
 
     @property
     def q_size(self) -> int:
@@ -107,7 +109,8 @@ class DecoderWeights:
         self.embed: torch.Tensor | None = None
         self.final_norm: torch.Tensor | None = None
         self.lm_head: torch.Tensor | None = None
-        self.cos_sin = rope_cos_sin(cfg.max_positions, cfg.head_dim, cfg.rope_theta, device=self.device)
+        self.cos_sin = rope_cos_sin(cfg.max_positions, cfg.head_dim, cfg.rope_theta, device=self.device,
+                                    llama3_scaling=cfg.rope_llama3)
 
     # ---------------------------------------------------------------- init
     @classmethod
@@ -203,16 +206,29 @@ class DecoderWeights:
 
 
 def load_config_json(path) -> DecoderConfig:
-    """DecoderConfig from an HF ``config.json``."""
+    """DecoderConfig from an HF ``config.json`` (transformers 4.x ``rope_theta`` / ``rope_scaling``
+    and 5.x ``rope_parameters`` spellings)."""
     c = json.loads(Path(path).read_text())
+    rope = dict(c.get("rope_parameters") or {})
+    scaling = c.get("rope_scaling") or (rope if rope.get("rope_type") not in (None, "default") else None)
+    theta = c.get("rope_theta") or rope.get("rope_theta") or 10000.0
+    llama3 = None
+    if scaling:
+        kind = scaling.get("rope_type") or scaling.get("type")
+        if kind == "llama3":
+            llama3 = (float(scaling["factor"]), float(scaling["low_freq_factor"]), float(scaling["high_freq_factor"]),
+                      int(scaling["original_max_position_embeddings"]))
+        elif kind not in (None, "default"):
+            raise NotImplementedError(f"RoPE scaling {kind!r} is not supported")
+    eos = c.get("eos_token_id", 2)
     return DecoderConfig(
         name=c.get("_name_or_path", "hf"), vocab_size=c["vocab_size"], hidden=c["hidden_size"],
         layers=c["num_hidden_layers"], heads=c["num_attention_heads"],
         kv_heads=c.get("num_key_value_heads", c["num_attention_heads"]),
-        head_dim=c.get("head_dim", c["hidden_size"] // c["num_attention_heads"]), ffn=c["intermediate_size"],
-        rope_theta=c.get("rope_theta", 10000.0), rms_eps=c.get("rms_norm_eps", 1e-5),
+        head_dim=c.get("head_dim") or c["hidden_size"] // c["num_attention_heads"], ffn=c["intermediate_size"],
+        rope_theta=float(theta), rms_eps=c.get("rms_norm_eps", 1e-5),
         max_positions=c.get("max_position_embeddings", 4096), tie_embeddings=c.get("tie_word_embeddings", False),
-        bos_id=c.get("bos_token_id", 1) or 1, eos_id=c.get("eos_token_id", 2) if isinstance(c.get("eos_token_id", 2), int) else c["eos_token_id"][0])
+        bos_id=c.get("bos_token_id", 1) or 1, eos_id=eos if isinstance(eos, int) else eos[0], rope_llama3=llama3)
 
 
 class DecoderModel:

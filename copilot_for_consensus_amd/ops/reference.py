@@ -50,9 +50,21 @@ def embed_layernorm(ids, positions, word_emb, pos_emb, type_emb, gamma, beta, ep
     return torch.nn.functional.layer_norm(x, (x.shape[-1],), gamma.float(), beta.float(), eps).to(word_emb.dtype)
 
 
-def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None) -> torch.Tensor:
-    """[max_pos, D/2, 2] fp32 table of (cos, sin) for rotate-half RoPE."""
+def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None, llama3_scaling=None) -> torch.Tensor:
+    """[max_pos, D/2, 2] fp32 table of (cos, sin) for rotate-half RoPE.
+
+    ``llama3_scaling`` = (factor, low_freq_factor, high_freq_factor, original_max_positions): the
+    Llama-3.1 frequency rescaling (long wavelengths divided by ``factor``, short ones kept, a
+    smooth blend in between)."""
     inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if llama3_scaling is not None:
+        factor, low, high, orig = llama3_scaling
+        wavelen = 2 * math.pi / inv
+        scaled = torch.where(wavelen > orig / low, inv / factor, inv)
+        smooth = (orig / wavelen - low) / (high - low)
+        blend = (1 - smooth) * scaled / factor + smooth * scaled
+        medium = ~(wavelen < orig / high) & ~(wavelen > orig / low)
+        inv = torch.where(medium, blend, scaled)
     t = torch.arange(max_pos, dtype=torch.float64)
     ang = torch.outer(t, inv)
     return torch.stack([ang.cos(), ang.sin()], -1).float().to(device)
