@@ -126,7 +126,7 @@ def main(argv=None):
                 "global_batch": args.threads_per_gpu * groups.dp_size,
                 "seq_len": round(prompt_tokens / max(threads, 1)),
                 "max_new_tokens": args.max_new,
-                "parallelism": f"dp{world}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
+                "parallelism": f"dp{groups.dp_size}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
                 "pipeline": "llm-only" if args.llm_only else "parse+chunk+embed+knn+select+prefill+decode",
             },
             "p50_summary_latency_s": round(p50, 3) if p50 is not None else None,

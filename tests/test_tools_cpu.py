@@ -108,6 +108,31 @@ def test_gateway_generation(tmp_path):
         assert p in g["paths"], p
     conf = (tmp_path / "nginx.conf").read_text()
     assert "location /reporting/" in conf and "client_max_body_size 100m" in conf
+    # cloud gateways (reference infra/gateway/{aws,azure,gcp}_adapter.py): every operation routed
+    cf = json.loads((tmp_path / "aws" / "cloudformation.json").read_text())
+    body = cf["Resources"]["Api"]["Properties"]["Body"]
+    trig = body["paths"]["/ingestion/api/sources/{name}/trigger"]["post"]["x-amazon-apigateway-integration"]
+    assert trig["uri"] == "http://ingestion:8080/api/sources/{name}/trigger"
+    assert trig["requestParameters"] == {"integration.request.path.name": "method.request.path.name"}
+    apim = json.loads((tmp_path / "azure" / "apim.json").read_text())
+    assert "validate-jwt" in apim["resources"][1]["properties"]["value"]
+    assert json.loads(apim["resources"][0]["properties"]["value"])["paths"] == g["paths"]
+    gcp = json.loads((tmp_path / "gcp" / "api_config.json").read_text())
+    search = gcp["paths"]["/reporting/api/reports/search"]["get"]
+    assert search["x-google-backend"]["address"] == "http://reporting:8080/api/reports/search"
+    assert search["security"] == [{"copilot_jwt": []}]
+    assert "security" not in gcp["paths"]["/auth/.well-known/jwks.json"]["get"]
+
+
+def test_cloud_gateway_with_public_backend(tmp_path):
+    from copilot_for_consensus_amd.tools import gateway as G
+    spec = {"openapi": "3.1.0", "paths": {"/reporting/api/reports/{report_id}": {"get": {
+        "parameters": [{"name": "report_id", "in": "path"}]}}}}
+    cf = G.aws_cloudformation(spec, "https://api.example.org")
+    op = cf["Resources"]["Api"]["Properties"]["Body"]["paths"]["/reporting/api/reports/{report_id}"]["get"]
+    assert op["x-amazon-apigateway-integration"]["uri"] == "https://api.example.org/reporting/api/reports/{report_id}"
+    assert G.validate_cloud_config(spec, "aws", cf) == []
+    assert G.validate_cloud_config(spec, "gcp", {"paths": {"/x": {"get": {}}}}) == ["GET /x"]
 
 
 def test_startup_requeue_generic():
