@@ -155,6 +155,10 @@ def test_ui_served():
     c = TestClient(app)
     r = c.get("/ui")
     assert r.status_code == 200 and "Copilot for Consensus" in r.text and "/api/reports/search" in r.text
+    # reference ui/src/routes: Login, Callback, AdminDashboard / PendingAssignments / UserRolesList
+    for route in ("async login()", "async callback(q)", "async admin(q)", "/admin/role-assignments/pending",
+                  "/admin/users/search"):
+        assert route in r.text, route
     assert c.get("/", follow_redirects=False).status_code in (302, 307)
 
 
