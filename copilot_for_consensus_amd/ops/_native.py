@@ -34,6 +34,7 @@ _KERNEL_SIGS = {
     "cfc_bias_gelu": [P, P, P, I, I, P],
     "cfc_embedding": [P, P, P, I, I, P],
     "cfc_sample": [P, I, I, F, c_uint32, P, P, P],
+    "cfc_sample_truncated": [P, I, I, F, I, F, F, c_uint32, P, P, P],
     "cfc_decode_advance": [P, P, I, P, P, P, P, P, P, I, P, P, I, I, P],
     "cfc_knn_scores": [P, P, I, I, I, P, P, P, P],
     "cfc_topk_pass": [P, P, I, I, I, I, P, P, P],

@@ -7,6 +7,7 @@ fallback for GPU tensors: a missing native library raises.
 """
 from __future__ import annotations
 
+import dataclasses
 import math
 
 import torch
@@ -358,19 +359,49 @@ def embedding(table, ids, out=None):
     return out
 
 
+@dataclasses.dataclass(frozen=True)
+class SamplingParams:
+    """Decoding controls.  ``temperature <= 0`` is greedy (the truncation knobs are then moot);
+    otherwise top-k -> top-p -> min-p cut on the raw logits, then temperature, as llama.cpp's
+    default sampler chain (the reference's /completion call sets only temperature 0.7 and runs
+    with the server defaults top_k 40, top_p 0.95, min_p 0.05)."""
+    temperature: float = 0.0
+    top_k: int = 0
+    top_p: float = 1.0
+    min_p: float = 0.0
+
+    @classmethod
+    def of(cls, t) -> "SamplingParams":
+        return t if isinstance(t, SamplingParams) else cls(float(t))
+
+    @property
+    def truncated(self) -> bool:
+        return self.temperature > 0 and (self.top_k > 0 or self.top_p < 1.0 or self.min_p > 0.0)
+
+
 def sample(logits, out_ids, temperature=0.0, seed=0, step=None):
-    """Greedy (temperature <= 0) or Gumbel-max sampling of one token per row into out_ids (int32)."""
+    """One token per row into out_ids (int32): greedy, Gumbel-max over the full softmax, or the
+    truncated chain of :class:`SamplingParams` (``temperature`` may be a float or SamplingParams)."""
+    sp = SamplingParams.of(temperature)
     if not logits.is_cuda:
-        if temperature <= 0:
+        if sp.temperature <= 0:
             out_ids.copy_(ref.sample_greedy(logits))
         else:
             g = torch.Generator().manual_seed(int(seed) + int(step[0]) if step is not None else int(seed))
-            p = torch.softmax(logits.float() / temperature, -1)
-            out_ids.copy_(torch.multinomial(p, 1, generator=g)[:, 0].to(torch.int32))
+            if sp.truncated:
+                out_ids.copy_(ref.sample_truncated(logits, sp.temperature, sp.top_k, sp.top_p, sp.min_p, g))
+            else:
+                p = torch.softmax(logits.float() / sp.temperature, -1)
+                out_ids.copy_(torch.multinomial(p, 1, generator=g)[:, 0].to(torch.int32))
         return out_ids
     _req(logits, torch.bfloat16, "logits")
     B, V = logits.shape
-    check(kernels().cfc_sample(logits.data_ptr(), B, V, float(temperature), int(seed) & 0xFFFFFFFF, _p(step),
+    if sp.truncated:
+        check(kernels().cfc_sample_truncated(logits.data_ptr(), B, V, sp.temperature, int(sp.top_k), float(sp.top_p),
+                                             float(sp.min_p), int(seed) & 0xFFFFFFFF, _p(step), out_ids.data_ptr(),
+                                             _stream(logits)), "cfc_sample_truncated")
+        return out_ids
+    check(kernels().cfc_sample(logits.data_ptr(), B, V, float(sp.temperature), int(seed) & 0xFFFFFFFF, _p(step),
                                out_ids.data_ptr(), _stream(logits)), "cfc_sample")
     return out_ids
 

@@ -189,6 +189,38 @@ def sample_greedy(logits):
     return torch.argmax(logits.float(), -1).to(torch.int32)
 
 
+def truncation_keep(sorted_logits: torch.Tensor, top_p: float, min_p: float) -> int:
+    """How many of the (descending) top-k logits survive top-p then min-p (at least one)."""
+    v = sorted_logits.float()
+    p = torch.softmax(v, -1)
+    minp_logit = float(v[0]) + math.log(min_p) if min_p > 0 else -math.inf
+    cum, keep = 0.0, 0
+    while keep < v.numel():
+        if keep > 0 and float(v[keep]) < minp_logit:
+            break
+        cum += float(p[keep])
+        keep += 1
+        if cum >= top_p:
+            break
+    return max(1, keep)
+
+
+def sample_truncated(logits, temperature, top_k, top_p, min_p, generator=None, cap: int = 256):
+    """top-k -> top-p -> min-p -> temperature -> draw (ties ordered by index), one id per row."""
+    out = []
+    for row in logits.float():
+        k = min(top_k if top_k > 0 else cap, cap, row.numel())
+        vals, idx = torch.sort(row, descending=True, stable=True)
+        vals, idx = vals[:k], idx[:k]
+        keep = truncation_keep(vals, top_p, min_p)
+        if temperature <= 0:
+            out.append(int(idx[0]))
+            continue
+        p = torch.softmax(vals[:keep] / temperature, -1)
+        out.append(int(idx[torch.multinomial(p, 1, generator=generator)[0]]))
+    return torch.tensor(out, dtype=torch.int32)
+
+
 def knn_scores(X, Q, xnorm2=None, qnorm2=None):
     dots = Q.float() @ X.float().T
     if xnorm2 is None:

@@ -188,7 +188,14 @@ class LLMEngine:
     # ------------------------------------------------------------------ API
     @torch.inference_mode()
     def generate(self, prompts: list[list[int]], max_new_tokens: int, temperature: float = 0.0, seed: int = 0,
-                 stop_ids: tuple[int, ...] = (), ignore_eos: bool = False) -> GenerationResult:
+                 stop_ids: tuple[int, ...] = (), ignore_eos: bool = False, top_k: int = 0, top_p: float = 1.0,
+                 min_p: float = 0.0) -> GenerationResult:
+        """``temperature`` (or a :class:`ops.kernels.SamplingParams`) with optional top-k / top-p /
+        min-p truncation -- all applied on device inside the captured decode step."""
+        if top_k or top_p < 1.0 or min_p > 0.0:
+            temperature = K.SamplingParams(float(temperature), int(top_k), float(top_p), float(min_p))
+        else:
+            temperature = K.SamplingParams.of(temperature)
         B = len(prompts)
         if B == 0:
             return GenerationResult([], [])

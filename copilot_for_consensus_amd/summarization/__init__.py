@@ -12,6 +12,7 @@ summarizer.py:20; models Thread / Summary / Citation, models.py).
 from __future__ import annotations
 
 import dataclasses
+import json
 import time
 from abc import ABC, abstractmethod
 
@@ -78,7 +79,8 @@ class HipLLMSummarizer(Summarizer):
     def __init__(self, model: str = "mistral-7b", checkpoint_dir: str | None = None, tensor_parallel: int = 1,
                  max_new_tokens: int = 512, temperature: float = 0.0, max_batch: int = 128,
                  kv_cache_tokens: int = 524288, device: str = "cuda", seed: int = 1234, tp_group=None,
-                 tp_rank: int = 0, ignore_eos: bool = False, **_):
+                 tp_rank: int = 0, ignore_eos: bool = False, top_k: int = 40, top_p: float = 0.95,
+                 min_p: float = 0.05, stop_sequences=("</s>", "\n\n\n"), **_):
         from ..models.decoder import DecoderModel, DecoderWeights, get_config, load_config_json
         from ..runtime.engine import LLMEngine
         from ..runtime.kv_cache import PagedKVCache
@@ -103,6 +105,12 @@ class HipLLMSummarizer(Summarizer):
         self.kv = PagedKVCache.for_budget(cfg.layers, w.kv_heads, cfg.head_dim, dev, kv_cache_tokens)
         self.engine = LLMEngine(self.decoder, self.kv)
         self.max_new_tokens, self.temperature = int(max_new_tokens), float(temperature)
+        # llama.cpp server sampling defaults + the reference's stop sequences (llamacpp_summarizer.py:111-113)
+        from ..ops.kernels import SamplingParams
+        self.sampling = SamplingParams(float(temperature), int(top_k), float(top_p), float(min_p))
+        if isinstance(stop_sequences, str):
+            stop_sequences = json.loads(stop_sequences)
+        self.stop_sequences = tuple(s for s in (stop_sequences or ()) if s)
         self.max_batch = int(max_batch)
         self.ignore_eos = ignore_eos
         self.context_limit = cfg.max_positions - self.max_new_tokens
@@ -135,14 +143,19 @@ class HipLLMSummarizer(Summarizer):
             part = threads[s:s + self.max_batch]
             ids = token_ids[s:s + self.max_batch] if token_ids is not None else [self._tokens(t.prompt) for t in part]
             t0 = time.perf_counter()
-            res = self.engine.generate(ids, self.max_new_tokens, temperature=self.temperature,
+            res = self.engine.generate(ids, self.max_new_tokens, temperature=self.sampling,
                                        ignore_eos=self.ignore_eos)
             ms = int(1000 * (time.perf_counter() - t0))
             self.last_stats = self.gpu_stats(res)
             for t, p, g in zip(part, ids, res.tokens):
-                text = self.tokenizer.decode(g).strip() or "(empty summary)"
+                text = self.apply_stops(self.tokenizer.decode(g)).strip() or "(empty summary)"
                 out.append(Summary(t.thread_id, text, [], self.backend, self.model, len(p), len(g), ms))
         return out
+
+    def apply_stops(self, text: str) -> str:
+        """Cut at the first stop sequence (string-level stops, as the llama.cpp server applies them)."""
+        cut = min((i for i in (text.find(s) for s in self.stop_sequences) if i >= 0), default=-1)
+        return text if cut < 0 else text[:cut]
 
     def summarize(self, thread: Thread) -> Summary:
         return self.summarize_batch([thread])[0]

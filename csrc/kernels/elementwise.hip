@@ -187,6 +187,152 @@ __global__ void __launch_bounds__(256) sample_kernel(const uint16_t* __restrict_
   }
 }
 
+// Truncated sampling with llama.cpp's default chain (its server's /completion, which the reference
+// calls with only temperature 0.7): top-k -> top-p -> min-p on the raw logits, then temperature
+// and a draw from the survivors (Gumbel-max with the same counter-based RNG as sample_kernel).
+// One 256-thread workgroup per row, no host sync (graph-capturable):
+//   1. radix-select the key of the k-th largest logit (4 passes of 256-bin LDS histograms over the
+//      order-preserving uint32 image of the float), 2. gather the k largest into LDS (ties at the
+//      threshold by ascending index), 3. sort them (value desc, index asc), 4. top-p / min-p cut on
+//      the sorted survivors, 5. Gumbel-max over the kept ones.
+#define SK_CAP 256
+
+__device__ __forceinline__ uint32_t order_key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__global__ void __launch_bounds__(256) sample_topk_kernel(const uint16_t* __restrict__ logits, int V, float temperature,
+                                                          int top_k, float top_p, float min_p, uint32_t seed,
+                                                          const int32_t* __restrict__ step_ptr,
+                                                          int32_t* __restrict__ out_ids) {
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const uint16_t* lr = logits + (size_t)row * V;
+  const uint32_t step = step_ptr ? (uint32_t)*step_ptr : 0u;
+  const int K = max(1, min(top_k > 0 ? top_k : SK_CAP, min(V, SK_CAP)));
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t s_prefix, s_remaining;
+  __shared__ float cv[SK_CAP];
+  __shared__ int ci[SK_CAP];
+  __shared__ int s_n;
+  __shared__ float sv[SK_CAP];
+  __shared__ int si[SK_CAP];
+  __shared__ int s_keep;
+  __shared__ int tie_i[4][SK_CAP];
+  __shared__ int tie_n[4];
+
+  // 1. radix select: key of the K-th largest element
+  uint32_t prefix = 0, mask = 0, remaining = (uint32_t)K;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    hist[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < V; i += 256) {
+      const uint32_t k = order_key(bf2f(lr[i]));
+      if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 0xFF], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t cum = 0;
+      int b = 255;
+      for (; b > 0; --b) {
+        if (cum + hist[b] >= remaining) break;
+        cum += hist[b];
+      }
+      s_prefix = prefix | ((uint32_t)b << shift);
+      s_remaining = remaining - cum;
+    }
+    __syncthreads();
+    prefix = s_prefix;
+    remaining = s_remaining;
+    mask |= 0xFFu << shift;
+  }
+  // 2. gather: every key > threshold (fewer than K, any order: ranked below), then the `remaining`
+  //    lowest-index keys == threshold -- each wave scans a quarter of the row in index order with
+  //    ballots, so ties are taken by ascending index exactly like the reference
+  if (tid == 0) s_n = 0;
+  __syncthreads();
+  for (int i = tid; i < V; i += 256) {
+    const float f = bf2f(lr[i]);
+    if (order_key(f) > prefix) {
+      const int slot = atomicAdd(&s_n, 1);
+      cv[slot] = f;
+      ci[slot] = i;
+    }
+  }
+  {
+    const int w = tid >> 6, lane = tid & 63;
+    const int lo = (int)(((int64_t)V * w) / 4), hi = (int)(((int64_t)V * (w + 1)) / 4);
+    int found = 0;
+    for (int base = lo; base < hi && found < (int)remaining; base += 64) {
+      const int i = base + lane;
+      const bool tie = i < hi && order_key(bf2f(lr[i])) == prefix;
+      const unsigned long long m = __ballot(tie);
+      if (tie) {
+        const int pos = found + __popcll(m & ((1ull << lane) - 1ull));
+        if (pos < (int)remaining) tie_i[w][pos] = i;
+      }
+      found += __popcll(m);
+    }
+    if (lane == 0) tie_n[w] = min(found, (int)remaining);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int n0 = s_n;
+    for (int w = 0; w < 4 && n0 < K; ++w)
+      for (int j = 0; j < tie_n[w] && n0 < K; ++j) { ci[n0] = tie_i[w][j]; cv[n0] = bf2f(lr[tie_i[w][j]]); ++n0; }
+    s_n = n0;
+  }
+  __syncthreads();
+  const int n = s_n;
+  // 3. rank = position in (value desc, index asc); keep rank < K
+  if (tid < n) {
+    const float v = cv[tid];
+    const int id = ci[tid];
+    int rank = 0;
+    for (int j = 0; j < n; ++j) rank += (cv[j] > v) || (cv[j] == v && ci[j] < id);
+    if (rank < K) { sv[rank] = v; si[rank] = id; }
+  }
+  __syncthreads();
+  const int kk = min(n, K);
+  // 4. top-p over softmax(logits) of the sorted survivors, min-p relative to the best (always >= 1 kept)
+  if (tid == 0) {
+    const float top = sv[0];
+    float z = 0.f;
+    for (int j = 0; j < kk; ++j) z += __expf(sv[j] - top);
+    const float minp_logit = min_p > 0.f ? top + __logf(min_p) : -INFINITY;
+    float cum = 0.f;
+    int keep = 0;
+    for (; keep < kk; ++keep) {
+      if (keep > 0 && sv[keep] < minp_logit) break;
+      cum += __expf(sv[keep] - top) / z;
+      if (cum >= top_p) { ++keep; break; }
+    }
+    s_keep = max(1, min(keep, kk));
+  }
+  __syncthreads();
+  // 5. temperature + Gumbel-max over the kept candidates (greedy if temperature <= 0)
+  if (tid < 64) {
+    float best = -INFINITY;
+    int best_i = 0x7fffffff;
+    for (int j = tid; j < s_keep; j += 64) {
+      float x = sv[j];
+      if (temperature > 0.f) {
+        const uint32_t h = hash_u32(seed ^ hash_u32(step * 0x9E3779B9u ^ hash_u32(row * 0x85EBCA6Bu ^ (uint32_t)si[j])));
+        const float u = ((h >> 8) + 0.5f) * (1.f / 16777216.f);
+        x = x / temperature - __logf(-__logf(u));
+      }
+      if (x > best || (x == best && si[j] < best_i)) { best = x; best_i = si[j]; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(best_i, o, 64);
+      if (ob > best || (ob == best && oi < best_i)) { best = ob; best_i = oi; }
+    }
+    if (tid == 0) out_ids[row] = best_i;
+  }
+}
+
 // Advance the per-sequence decode state after sampling (one thread per sequence):
 //   tokens[b][step] = next[b]; input_ids[b] = next[b]; positions[b]++; ctx_lens[b]++;
 //   slots[b] = block_tables[b][pos/32]*32 + pos%32; done[b] |= next[b] in stop_ids.
@@ -252,6 +398,17 @@ CFC_API int cfc_embedding(void* out, const void* table, const int32_t* ids, int 
   if (dim % 8 != 0) return -1;
   if (T == 0) return 0;
   embedding_kernel<<<T, 256, 0, stream>>>((uint16_t*)out, (const uint16_t*)table, ids, T, dim);
+  return CFC_CHECK_LAUNCH();
+}
+
+// top_k <= 0: no top-k cut (candidates still capped at SK_CAP = 256); top_p >= 1 / min_p <= 0 disable those.
+CFC_API int cfc_sample_truncated(const void* logits, int B, int V, float temperature, int top_k, float top_p,
+                                 float min_p, uint32_t seed, const int32_t* step_ptr, int32_t* out_ids,
+                                 hipStream_t stream) {
+  if (B == 0) return 0;
+  if (V <= 0 || top_p <= 0.f) return -1;
+  sample_topk_kernel<<<B, 256, 0, stream>>>((const uint16_t*)logits, V, temperature, top_k, top_p, min_p, seed,
+                                            step_ptr, out_ids);
   return CFC_CHECK_LAUNCH();
 }
 
