@@ -4,7 +4,8 @@ A one-GPU box cannot show xGMI, but it does exercise everything else: two proces
 other's uncached regions through IPC handles, synchronise through the cross-process signal
 slots and read each other's staging buffers.  Results are checked against gloo's all-reduce of the
 same tensors (fp32 reference), eager and under hipGraph capture (the epochs advance on device, so a
-replayed graph keeps working)."""
+replayed graph keeps working), and a TP=2 decoder whose decode all-reduces run on the kernel must
+generate the unsharded model's tokens."""
 from __future__ import annotations
 
 import os
@@ -105,3 +106,70 @@ def test_two_processes_share_regions_over_ipc():
         # bf16(fp32 sum of 2 bf16 values) vs bf16(exact fp32 sum): at most 1 ulp apart
         assert res["eager_max_err"] <= 0.0625, res
         assert res["graph_max_err"] <= 0.0625, res
+
+
+def _tp_worker(rank, world, port, q, prompts, n_new):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(rank), CFC_DIST_BACKEND="gloo")
+        from copilot_for_consensus_amd.models.decoder import DecoderModel, DecoderWeights, get_config
+        from copilot_for_consensus_amd.parallel import init_distributed, make_groups
+        from copilot_for_consensus_amd.parallel.custom_ar import maybe_create
+        from copilot_for_consensus_amd.parallel.tp import shard_weights
+        from copilot_for_consensus_amd.runtime.engine import LLMEngine
+        from copilot_for_consensus_amd.runtime.kv_cache import PagedKVCache
+        env = init_distributed(backend="gloo")
+        g = make_groups(env, tp=world)
+        cfg = get_config("tiny")
+        full = DecoderWeights.random(cfg, env.device, seed=5)
+        w = shard_weights(full, g.tp_rank, g.tp_size)
+        ar = maybe_create(g.tp_group, env.device)
+        m = DecoderModel(w, tp_group=g.tp_group, custom_ar=ar)
+        kv = PagedKVCache(cfg.layers, 64, w.kv_heads, cfg.head_dim, env.device)
+        toks = LLMEngine(m, kv, use_graph=False).generate(prompts, n_new, ignore_eos=True).tokens
+        q.put((rank, {"tokens": toks, "custom_ar": ar is not None and ar.enabled,
+                      "errors": ar.errors() if ar is not None else -1}))
+        import torch.distributed as dist
+        dist.barrier()
+        if ar is not None:
+            ar.close()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, {"exception": traceback.format_exc()}))
+
+
+def test_tp2_decoder_with_oneshot_allreduce_matches_tp1():
+    """TP=2 (two processes sharing the GPU, decode all-reduces on the one-shot IPC kernel) generates
+    the same greedy tokens as the unsharded model."""
+    import torch.multiprocessing as mp
+    from copilot_for_consensus_amd.models.decoder import DecoderModel, DecoderWeights, get_config
+    from copilot_for_consensus_amd.runtime.engine import LLMEngine
+    from copilot_for_consensus_amd.runtime.kv_cache import PagedKVCache
+    prompts = [[1, 5, 9, 200, 17, 33], [1] + list(range(40, 110)), [1, 2]]
+    cfg = get_config("tiny")
+    ref = LLMEngine(DecoderModel(DecoderWeights.random(cfg, "cuda:0", seed=5)),
+                    PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, "cuda:0"), use_graph=False).generate(
+        prompts, 8, ignore_eos=True).tokens
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, q, prompts, 8)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in procs:
+            r, out = q.get(timeout=200)
+            res[r] = out
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(2):
+        assert "exception" not in res[r], res[r]
+        assert res[r]["custom_ar"] and res[r]["errors"] == 0, res[r]
+    assert res[0]["tokens"] == res[1]["tokens"]
+    agree = sum(a == b for x, y in zip(res[0]["tokens"], ref) for a, b in zip(x, y))
+    assert agree >= 0.9 * sum(len(x) for x in ref), (res[0]["tokens"], ref)
