@@ -27,7 +27,8 @@ _KERNEL_SIGS = {
     "cfc_rmsnorm": [P, P, P, P, I, I, F, I, P],
     "cfc_layernorm": [P, P, P, P, P, P, P, P, P, P, I, I, F, I, P],
     "cfc_paged_decode_attention": [P, P, P, P, P, I, I, I, I, I, I, I, F, P, P, P, P],
-    "cfc_prefill_attention": [P, P, P, P, P, P, P, P, I, I, I, I, I, F, P, P],
+    "cfc_prefill_attention": [P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, P, P],
+    "cfc_prefill_rows": [I, I],
     "cfc_encoder_attention": [P, P, P, P, I, I, I, I, F, P, P],
     "cfc_rope_kv_write": [P, P, P, P, P, P, P, I, I, I, I, P],
     "cfc_silu_mul": [P, P, I, I, I, P],

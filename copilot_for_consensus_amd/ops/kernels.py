@@ -144,8 +144,18 @@ def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, o
     return out
 
 
-PREFILL_TILE_ROWS = 128   # query rows per workgroup of the decoder prefill kernel
+PREFILL_TILE_ROWS = 128   # query rows per workgroup of the legacy single-head prefill kernels
 ENCODER_TILE_ROWS = 64    # query rows per workgroup of the encoder attention kernel
+
+
+def prefill_rows(Hq: int, Hkv: int) -> int:
+    """Query rows per tile the decoder prefill kernel expects: the default GQA-packed kernel takes
+    256 / G rows of all G = Hq / Hkv heads of one kv-head per workgroup (attention.hip:
+    prefill_gqa_kernel), the legacy kernels 128 rows of one head."""
+    lib = kernels() if torch.cuda.is_available() else None
+    if lib is None:
+        return PREFILL_TILE_ROWS
+    return int(lib.cfc_prefill_rows(int(Hq), int(Hkv)))
 
 
 def prefill_tiles(cu_q: list[int], tile: int = PREFILL_TILE_ROWS, ctx_lens: list[int] | None = None):
@@ -169,15 +179,16 @@ def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, 
         return ref.prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale)
     T, Hq, D = q.shape
     Hkv = k_cache.shape[1]
+    rows = prefill_rows(Hq, Hkv)
     if tiles is None:
-        seqs, q0 = prefill_tiles(cu_q.tolist(), PREFILL_TILE_ROWS, ctx_lens.tolist())
+        seqs, q0 = prefill_tiles(cu_q.tolist(), rows, ctx_lens.tolist())
         tiles = (torch.tensor(seqs, dtype=torch.int32, device=q.device),
                  torch.tensor(q0, dtype=torch.int32, device=q.device))
     tile_seq, tile_q0 = tiles
     out = torch.empty_like(q) if out is None else out
     check(kernels().cfc_prefill_attention(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                           block_tables.data_ptr(), cu_q.data_ptr(), ctx_lens.data_ptr(),
-                                          tile_seq.data_ptr(), tile_q0.data_ptr(), tile_seq.numel(), Hq, Hkv, D,
+                                          tile_seq.data_ptr(), tile_q0.data_ptr(), tile_seq.numel(), rows, Hq, Hkv, D,
                                           block_tables.shape[1], float(scale), out.data_ptr(), _stream(q)),
           "cfc_prefill_attention")
     return out

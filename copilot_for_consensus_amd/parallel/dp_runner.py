@@ -47,6 +47,12 @@ class ResilientDPRunner:
     # ---------------------------------------------------------------- setup
     def _init_assignment(self, items: dict[str, float], wait_s: float) -> list[str]:
         all_ids = sorted(items)
+        # rendezvous: a rank that has not started yet has no heartbeat and would look dead to an
+        # early finisher; wait (bounded) for every rank's first heartbeat before the loop starts
+        self.store.add(f"{self.job}/arrived", 1)
+        deadline = time.monotonic() + wait_s
+        while int(self.store.add(f"{self.job}/arrived", 0)) < self.world and time.monotonic() < deadline:
+            time.sleep(self.poll)
         if int(self.store.add(f"{self.job}/init_ticket", 1)) == 1:
             ids = list(items)
             bins = balanced_shard([float(items[i]) for i in ids], self.world)

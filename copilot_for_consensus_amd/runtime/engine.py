@@ -75,6 +75,9 @@ class LLMEngine:
         self.device = kv.device
         self.max_prefill_tokens = max_prefill_tokens
         self.use_graph = use_graph and kv.device.type == "cuda"
+        # query rows per prefill attention tile (the GQA-packed kernel takes 256 / G)
+        self._prefill_rows = (K.prefill_rows(model.w.heads, model.w.kv_heads) if kv.device.type == "cuda"
+                              else K.PREFILL_TILE_ROWS)
         self.stop_check_interval = stop_check_interval
         self._states: dict[tuple, _DecodeState] = {}
         # shared-prefix reuse of whole KV blocks (system prompt + template head of every thread)
@@ -135,7 +138,7 @@ class LLMEngine:
             bt = torch.zeros(len(rows), maxb, dtype=torch.int32)
             for r, s in enumerate(rows):
                 bt[r, :len(tables[s])] = torch.tensor(tables[s], dtype=torch.int32)
-            tseq, tq0 = K.prefill_tiles(cu, K.PREFILL_TILE_ROWS, ctx)
+            tseq, tq0 = K.prefill_tiles(cu, self._prefill_rows, ctx)
             hidden = self.model.forward_prefill(
                 self._i32(ids), self._i32(positions), self._i32(slots), self._i32(cu), self._i32(ctx),
                 bt.to(self.device), self.kv, tiles=(self._i32(tseq), self._i32(tq0)),

@@ -606,6 +606,211 @@ __global__ void __launch_bounds__(256, MINW) prefill_paged_kernel_v4(
 }
 
 // ------------------------------------------------------------------------------------------
+// Prefill v5 (default): GQA-packed 8-wave tiles on v_mfma_f32_32x32x16_bf16.
+// grid = (n_tiles, Hkv); block = 512 = 8 waves, 2 per SIMD.  A tile is QR = 256 / G query rows of
+// ONE sequence for ALL G query heads of kv-head hk: wave w takes head hk*G + (w % G) and rows
+// 32 (w / G) .. +31.  Every K/V byte staged in LDS therefore feeds 256 query rows (8 waves), and
+// the tile spans only 256/G positions, so at G = 4 the causal diagonal idles 4x fewer rows than a
+// 256-row single-head tile would.
+//   * LDS per KV tile (64 keys): K 64 x 256 B (16-B chunk c of key r at r*256 + ((c ^ (r&15))<<4))
+//     and V^T 128 d-rows x 128 B copied AS STORED in the cache (decode slot order).  The decode
+//     order already fits the 32x32 PV: cache chunk g of a 32-key block holds keys {4g..4g+3,
+//     16+4g..16+4g+3}, all with key bit 2 == g&1, which is exactly the half-wave (lane>>5) that holds
+//     them in the S^T accumulator; so k-step s of half hf uses chunk 4hf + 2s + hi for the A operand
+//     and accumulator registers {4s..4s+3, 8+4s..8+4s+3} as the B operand -- one ds_read_b128 and
+//     one in-lane pack, no permutation anywhere.  V swizzle c ^ ((d>>1)&7) ^ ((d&1)<<2): the
+//     ds_read_b128 lane groups and the 8-lane ds_write_b128 groups are both conflict-free.
+//   * register-staged double buffer, one barrier per tile (loads for tile t+1 issued before tile
+//     t's MFMAs, LDS writes after); Q pre-scaled into the exp2 domain; deferred rescale
+//     (RESCALE_THR); row max / sum across the two half-waves with v_permlane32_swap (no LDS
+//     bpermute); per-lane partial row sums combined once at the end; v_exp_f32 / v_cvt_pk_bf16_f32
+//     directly; waves 4-7 at static priority 1 (the younger half loses VALU arbitration otherwise).
+// ------------------------------------------------------------------------------------------
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
+}
+// value of lane l ^ 32 combined with lane l's own (both halves get the same result)
+__device__ __forceinline__ float pair_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float pair_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ int v5_off(int d, int c) { return d * 128 + ((c ^ ((d >> 1) & 7) ^ ((d & 1) << 2)) << 4); }
+
+template <int G>
+__global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    const int32_t* __restrict__ block_tables, const int32_t* __restrict__ cu_q, const int32_t* __restrict__ ctx_lens,
+    const int32_t* __restrict__ tile_seq, const int32_t* __restrict__ tile_q0, float scale_log2, int Hq, int Hkv,
+    int max_blocks, uint16_t* __restrict__ out) {
+  constexpr int D = 128;
+  constexpr int QR = 256 / G;      // query rows per tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // LDS: [K buf0 16K][K buf1 16K][V buf0 16K][V buf1 16K]
+  const int t = blockIdx.x, hk = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
+  const int l32 = lane & 31, hi = lane >> 5;
+  const int hq = hk * G + (w % G);
+  const int rsub = w / G;
+  const int s = tile_seq[t], qs = tile_q0[t];
+  const int q_begin = cu_q[s], q_len = cu_q[s + 1] - q_begin;
+  const int ctx = ctx_lens[s];
+  const int pos_base = ctx - q_len;
+  const int row_last = min(qs + QR - 1, q_len - 1);
+  const int kend = pos_base + row_last + 1;         // keys [0, kend) are needed by this tile
+  const int ntiles = (kend + PF_KT - 1) / PF_KT;
+  const int32_t* bt = block_tables + (size_t)s * max_blocks;
+
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+
+  const int my_row = qs + 32 * rsub + l32;
+  const int my_pos = pos_base + my_row;
+  const int wave_min_pos = pos_base + qs + 32 * rsub;
+  // Q^T B-operand, pre-scaled: k-step ks holds Q[row][16ks + 8hi .. +7]
+  bf16x8_t qf[8];
+  {
+    const int rr = min(my_row, q_len - 1);
+    const uint16_t* qr = q + ((size_t)(q_begin + rr) * Hq + hq) * D;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(qr + 16 * ks + 8 * hi), f);
+      uint4 u;
+      u.x = cvt_pk_bf16(f[0] * scale_log2, f[1] * scale_log2);
+      u.y = cvt_pk_bf16(f[2] * scale_log2, f[3] * scale_log2);
+      u.z = cvt_pk_bf16(f[4] * scale_log2, f[5] * scale_log2);
+      u.w = cvt_pk_bf16(f[6] * scale_log2, f[7] * scale_log2);
+      qf[ks] = as_bf16x8(u);
+    }
+  }
+
+  // staging: tile kt = cache blocks 2kt, 2kt+1; piece i of a thread is block 2kt+i, bytes 16 tid ..
+  // of both its K image [32][128] and its V^T image [128][32] (each 8 KB contiguous).  The block id
+  // is workgroup-uniform (scalar load) and the data loads are UNCONDITIONAL (a block past kend
+  // re-reads the last needed block; its V is zeroed at the LDS write), so no per-lane select
+  // makes the compiler wait for the loads inside the issue sequence -- they stay in flight across
+  // the tile's MFMAs.
+  const int nb_need = (kend + KV_BS - 1) / KV_BS;
+  uint4 ks0, ks1, vs0, vs1;     // named (not an array): an array here is kept in scratch
+  auto gload = [&](int kt) {
+    const int b0 = bt[min(2 * kt, nb_need - 1)], b1 = bt[min(2 * kt + 1, nb_need - 1)];
+    const size_t base0 = ((size_t)b0 * Hkv + hk) * (KV_BS * D) + 8 * tid;
+    const size_t base1 = ((size_t)b1 * Hkv + hk) * (KV_BS * D) + 8 * tid;
+    ks0 = *reinterpret_cast<const uint4*>(kc + base0);
+    vs0 = *reinterpret_cast<const uint4*>(vc + base0);
+    ks1 = *reinterpret_cast<const uint4*>(kc + base1);
+    vs1 = *reinterpret_cast<const uint4*>(vc + base1);
+  };
+  auto lwrite = [&](int buf, int kt) {
+    char* kb = smem + buf * 16384;
+    char* vb = smem + 32768 + buf * 16384;
+    *reinterpret_cast<uint4*>(kb + k_lds_off(tid >> 4, tid & 15)) = ks0;
+    *reinterpret_cast<uint4*>(kb + k_lds_off((tid >> 4) + 32, tid & 15)) = ks1;
+    const bool z0 = kt * PF_KT >= kend, z1 = kt * PF_KT + KV_BS >= kend;
+    *reinterpret_cast<uint4*>(vb + v5_off((tid >> 2) & 127, tid & 3)) = z0 ? make_uint4(0, 0, 0, 0) : vs0;
+    *reinterpret_cast<uint4*>(vb + v5_off((tid >> 2) & 127, 4 + (tid & 3))) = z1 ? make_uint4(0, 0, 0, 0) : vs1;
+  };
+
+  f32x16_t o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m = -INFINITY, l = 0.f;   // l: this lane's partial row sum (its 32 of every 64 keys)
+
+  gload(0);
+  lwrite(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < ntiles;
+    if (more) gload(kt + 1);
+
+    const char* kb = smem + cur * 16384;
+    const char* vb = smem + 32768 + cur * 16384;
+    const int key0 = kt * PF_KT;
+    if (key0 <= wave_min_pos + 31) {     // else every key of the tile is after all of this wave's rows
+      f32x16_t sc[2];
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[hf][r] = 0.f;
+        const int row = 32 * hf + l32;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks)
+          sc[hf] = mfma32(as_bf16x8(*reinterpret_cast<const uint4*>(kb + k_lds_off(row, 2 * ks + hi))), qf[ks], sc[hf]);
+      }
+      if (key0 + PF_KT - 1 > wave_min_pos) {  // diagonal tile: causal mask
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (key0 + 32 * hf + 8 * (r >> 2) + 4 * hi + (r & 3) > my_pos) sc[hf][r] = -INFINITY;
+      }
+      float tmax = fmaxf(sc[0][0], sc[1][0]);
+#pragma unroll
+      for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, fmaxf(sc[0][r], sc[1][r]));
+      tmax = pair_max(tmax);
+      if (!__all(tmax - m <= RESCALE_THR)) {
+        const float mn = fmaxf(m, tmax);
+        const float alpha = __builtin_amdgcn_exp2f(m - (mn == -INFINITY ? 0.f : mn));
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+        m = mn;
+      }
+      const float mref = m == -INFINITY ? 0.f : m;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = __builtin_amdgcn_exp2f(sc[hf][r] - mref);
+          sc[hf][r] = e;
+          l += e;
+        }
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          uint4 u;
+          u.x = cvt_pk_bf16(sc[hf][4 * ss + 0], sc[hf][4 * ss + 1]);
+          u.y = cvt_pk_bf16(sc[hf][4 * ss + 2], sc[hf][4 * ss + 3]);
+          u.z = cvt_pk_bf16(sc[hf][8 + 4 * ss + 0], sc[hf][8 + 4 * ss + 1]);
+          u.w = cvt_pk_bf16(sc[hf][8 + 4 * ss + 2], sc[hf][8 + 4 * ss + 3]);
+          const bf16x8_t pf = as_bf16x8(u);
+          const int c = 4 * hf + 2 * ss + hi;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt)
+            o[dt] = mfma32(as_bf16x8(*reinterpret_cast<const uint4*>(vb + v5_off(32 * dt + l32, c))), pf, o[dt]);
+        }
+    }
+    if (more) lwrite(cur ^ 1, kt + 1);
+    __syncthreads();
+  }
+
+  l = pair_sum(l);
+  if (my_row < q_len) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    uint16_t* orow = out + ((size_t)(q_begin + my_row) * Hq + hq) * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {   // registers 4rg..4rg+3 = d 32dt + 8rg + 4hi + 0..3
+        uint2 pk;
+        pk.x = cvt_pk_bf16(o[dt][4 * rg] * inv, o[dt][4 * rg + 1] * inv);
+        pk.y = cvt_pk_bf16(o[dt][4 * rg + 2] * inv, o[dt][4 * rg + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * rg + 4 * hi) = pk;
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Varlen bidirectional encoder attention (BERT family), D in {32, 64}, S <= 512.
 // Input qkv is the fused projection output [T, 3*H*D] (q | k | v, head-major inside each).
 // grid = (n_tiles, H); block = 256 = 4 waves x 16 query rows.  The WHOLE key/value range of
@@ -768,17 +973,46 @@ CFC_API int cfc_paged_decode_attention(const void* q, const void* k_cache, const
 
 CFC_API int cfc_prefill_tile_rows() { return PF_ROWS; }
 
+static int prefill_variant() {
+  static const int v = [] { const char* e = getenv("CFC_PREFILL_VARIANT"); return e ? atoi(e) : 5; }();
+  return v;
+}
+
+// Query rows per tile the default prefill kernel expects for Hq / Hkv heads (the host tiler's
+// granularity): 256 / G on the GQA-packed kernel, else PF_ROWS.
+CFC_API int cfc_prefill_rows(int Hq, int Hkv) {
+  if (Hkv <= 0 || Hq % Hkv) return PF_ROWS;
+  const int G = Hq / Hkv;
+  const bool v5 = prefill_variant() == 5 && (G == 1 || G == 2 || G == 4 || G == 8);
+  return v5 ? 256 / G : PF_ROWS;
+}
+
 CFC_API int cfc_prefill_attention(const void* q, const void* k_cache, const void* v_cache, const int32_t* block_tables,
                                   const int32_t* cu_q, const int32_t* ctx_lens, const int32_t* tile_seq,
-                                  const int32_t* tile_q0, int n_tiles, int Hq, int Hkv, int head_dim, int max_blocks,
-                                  float scale, void* out, hipStream_t stream) {
-  if (head_dim != 128 || Hq % Hkv != 0) return -1;
+                                  const int32_t* tile_q0, int n_tiles, int tile_rows, int Hq, int Hkv, int head_dim,
+                                  int max_blocks, float scale, void* out, hipStream_t stream) {
+  if (head_dim != 128 || Hkv <= 0 || Hq % Hkv != 0) return -1;
+  if (tile_rows != cfc_prefill_rows(Hq, Hkv)) return -2;     // tiles cut for another kernel
   if (n_tiles <= 0) return 0;
   const size_t lds = 65536;
-  // variant 0: v3 <=128 VGPRs (2 workgroups / CU); 1: v3 <=256 VGPRs; 2/3: v4 (32x32 MFMA, 2 / 1 WG per CU)
-  static const int variant = [] { const char* e = getenv("CFC_PREFILL_VARIANT"); return e ? atoi(e) : 0; }();
+  const int G = Hq / Hkv;
 #define PF_ARGS (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, cu_q, ctx_lens, \
     tile_seq, tile_q0, scale * LOG2E, Hq, Hkv, max_blocks, (uint16_t*)out
+  if (tile_rows != PF_ROWS || (G * tile_rows == 256 && prefill_variant() == 5)) {
+    // 5: GQA-packed 8-wave kernel (default)
+    const dim3 grid(n_tiles, Hkv);
+    switch (G) {
+      case 1: prefill_gqa_kernel<1><<<grid, 512, lds, stream>>>(PF_ARGS); break;
+      case 2: prefill_gqa_kernel<2><<<grid, 512, lds, stream>>>(PF_ARGS); break;
+      case 4: prefill_gqa_kernel<4><<<grid, 512, lds, stream>>>(PF_ARGS); break;
+      case 8: prefill_gqa_kernel<8><<<grid, 512, lds, stream>>>(PF_ARGS); break;
+      default: return -3;
+    }
+    return CFC_CHECK_LAUNCH();
+  }
+  // legacy single-head 128-row kernels: 0 = v3 <=128 VGPRs (2 workgroups / CU); 1 = v3 <=256 VGPRs;
+  // 2/3 = v4 (32x32 MFMA, 2 / 1 WG per CU)
+  const int variant = prefill_variant();
   if (variant == 1) prefill_paged_kernel<2><<<dim3(n_tiles, Hq), 512, lds, stream>>>(PF_ARGS);
   else if (variant == 2) prefill_paged_kernel_v4<2><<<dim3(n_tiles, Hq), 256, lds, stream>>>(PF_ARGS);
   else if (variant == 3) prefill_paged_kernel_v4<1><<<dim3(n_tiles, Hq), 256, lds, stream>>>(PF_ARGS);

@@ -21,7 +21,7 @@ def prefill_case(nseq=6, L=2800, Hq=32, Hkv=8, D=128, iters=10):
     cu = torch.arange(0, nseq + 1, device="cuda", dtype=torch.int32) * L
     ctx = torch.full((nseq,), L, device="cuda", dtype=torch.int32)
     q = torch.randn(nseq * L, Hq, D, device="cuda").bfloat16()
-    seqs, q0 = K.prefill_tiles(cu.tolist(), K.PREFILL_TILE_ROWS, ctx.tolist())
+    seqs, q0 = K.prefill_tiles(cu.tolist(), K.prefill_rows(Hq, Hkv), ctx.tolist())
     tiles = (torch.tensor(seqs, dtype=torch.int32, device="cuda"), torch.tensor(q0, dtype=torch.int32, device="cuda"))
     out = torch.empty_like(q)
     for _ in range(2):

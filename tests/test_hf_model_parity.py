@@ -89,7 +89,7 @@ def _our_logits(ckpt, device, ids):
     i32 = lambda x: torch.tensor(x, dtype=torch.int32, device=device)  # noqa: E731
     slots = [table[p // KV_BLOCK] * KV_BLOCK + p % KV_BLOCK for p in range(n)]
     cu, ctx = [0, n], [n]
-    tseq, tq0 = K.prefill_tiles(cu, K.PREFILL_TILE_ROWS, ctx)
+    tseq, tq0 = K.prefill_tiles(cu, K.prefill_rows(w.heads, w.kv_heads), ctx)
     hidden = model.forward_prefill(i32(ids), i32(list(range(n))), i32(slots), i32(cu), i32(ctx),
                                    i32([table]), kv, tiles=(i32(tseq), i32(tq0)))
     return model.logits(hidden).float().cpu()

@@ -110,12 +110,13 @@ def test_paged_decode(G, part_blocks):
     _close(out, ref, 2e-2)
 
 
-@pytest.mark.parametrize("G", [1, 4])
+@pytest.mark.parametrize("G", [1, 2, 4, 8])
 def test_prefill_attention(G):
     Hkv, D = 2, 128
     Hq = Hkv * G
-    # (q_len, ctx_len): fresh prompts and chunked continuation (ctx > q_len)
-    seqs = [(1, 1), (17, 17), (64, 64), (200, 200), (70, 300), (129, 1000)]
+    # (q_len, ctx_len): fresh prompts and chunked continuation (ctx > q_len), tile edges of every
+    # G's tile height (256 / G rows) and a long prompt
+    seqs = [(1, 1), (17, 17), (64, 64), (200, 200), (70, 300), (129, 1000), (256, 256), (33, 33), (1100, 1100)]
     kc, vc, bt = _fill_cache([c for _, c in seqs], Hkv, D)
     cu = [0]
     for qn, _ in seqs:
