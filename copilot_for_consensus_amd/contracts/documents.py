@@ -71,7 +71,8 @@ COLLECTION_SPECS: dict[str, dict] = {
                        "updated_at": ANY_STR, "last_run_at": ANY_STR,
                        "last_run_status": {"type": ["string", "null"], "enum": ["success", "failure", None]},
                        "last_error": ANY_STR, "next_run_at": ANY_STR, "files_processed": i(0), "files_skipped": i(0)},
-        "indexes": ["name"],
+        "indexes": ["name", "enabled", "source_type"],
+        "unique": ["name"],
     },
 }
 
@@ -95,5 +96,7 @@ def document_schema(collection: str) -> dict:
 def collections_config() -> dict:
     return {"collections": [
         {"name": c, "schema": f"/schemas/documents/v1/{c}.schema.json",
-         "indexes": [{"keys": {f: 1}, "options": {"name": f"{f}_idx"}} for f in spec["indexes"]]}
+         "indexes": [{"keys": {f: 1}, "options": {"name": f"{f}_idx", **({"unique": True}
+                                                                         if f in spec.get("unique", ()) else {})}}
+                     for f in spec["indexes"]]}
         for c, spec in COLLECTION_SPECS.items()]}

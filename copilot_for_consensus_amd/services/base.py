@@ -61,14 +61,17 @@ class BaseService:
                 with self._lock:
                     self.stats["events_processed"] += 1
                     self.stats["last_event_at"] = time.time()
+                self.metrics.increment(f"{self.name}_events_processed_total", tags={"event_type": event_type})
             except RetryExhaustedError as e:
                 with self._lock:
                     self.stats["events_failed"] += 1
+                self.metrics.increment(f"{self.name}_events_failed_total", tags={"event_type": event_type})
                 self.log.error("retry exhausted", event_type=event_type, error=str(e))
                 self.on_failure(event_type, event, e)
             except Exception as e:
                 with self._lock:
                     self.stats["events_failed"] += 1
+                self.metrics.increment(f"{self.name}_events_failed_total", tags={"event_type": event_type})
                 self.log.error("handler failed", event_type=event_type, error=repr(e))
                 self.on_failure(event_type, event, e)
                 raise
@@ -113,6 +116,21 @@ def create_app(service: BaseService, extra_routes: Callable | None = None, confi
     from fastapi.responses import PlainTextResponse
 
     app = FastAPI(title=f"copilot-for-consensus {service.name}")
+
+    @app.middleware("http")
+    async def _request_metrics(request, call_next):
+        # per-route latency + status counts (the API latency / error-rate SLO alerts read these)
+        t = time.perf_counter()
+        status = 500
+        try:
+            resp = await call_next(request)
+            status = resp.status_code
+            return resp
+        finally:
+            route = getattr(request.scope.get("route"), "path", "unmatched")
+            tags = {"method": request.method, "route": route}
+            service.metrics.observe(f"{service.name}_http_request_duration_seconds", time.perf_counter() - t, tags=tags)
+            service.metrics.increment(f"{service.name}_http_requests_total", tags={**tags, "status": str(status)})
 
     @app.get("/health")
     def health():

@@ -425,7 +425,8 @@ class ValidatingDocumentStore(DocumentStore):
 class MongoDocumentStore(DocumentStore):
     """MongoDB driver (reference mongo_document_store.py:33); needs ``pymongo``."""
 
-    def __init__(self, host="documentdb", port=27017, database="copilot", username=None, password=None, **_):
+    def __init__(self, host="documentdb", port=27017, database="copilot", username=None, password=None,
+                 ensure_indexes=True, **_):
         try:
             import pymongo  # type: ignore
         except ImportError as e:  # pragma: no cover
@@ -433,11 +434,29 @@ class MongoDocumentStore(DocumentStore):
         self._pymongo = pymongo
         self._args = dict(host=host, port=int(port), username=username, password=password)
         self._dbname = database
+        self.ensure_indexes = ensure_indexes
         self.db = None
 
     def connect(self):
         self.client = self._pymongo.MongoClient(**{k: v for k, v in self._args.items() if v is not None})
         self.db = self.client[self._dbname]
+        if self.ensure_indexes:
+            self.ensure_collections()
+
+    def ensure_collections(self, config: dict | None = None) -> int:
+        """Create the collections and indexes of collections.config.json (what the reference's
+        infra/init/mongo-init.js does at container start); idempotent.  Returns indexes ensured."""
+        from ..contracts.documents import collections_config
+        cfg = config or collections_config()
+        existing = set(self.db.list_collection_names())
+        n = 0
+        for d in cfg.get("collections", []):
+            if d["name"] not in existing:
+                self.db.create_collection(d["name"])
+            for spec in d.get("indexes", []):
+                self.db[d["name"]].create_index(list(spec["keys"].items()), **spec.get("options", {}))
+                n += 1
+        return n
 
     def _c(self, collection):
         if self.db is None:

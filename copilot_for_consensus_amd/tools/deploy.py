@@ -12,7 +12,9 @@ topology of the reference.  Here:
   carry the reference's SLO thresholds (parse P95 > 5 s, chunk > 2 s, embed > 10 s, summarize
   > 30 s, reporting API > 0.5 s);
 * docker-compose: one MI355X node runs the whole pipeline in one process (``node``) with the GPU
-  devices mapped; the per-service form is emitted too for multi-host deployments.
+  devices mapped; the per-service form is emitted too for multi-host deployments;
+* the eight alert groups, eleven Grafana dashboards, Loki/Promtail, the Mongo bootstrap script and
+  the Kubernetes manifests come from :mod:`.ops_assets`.
 
     python -m copilot_for_consensus_amd.tools.deploy --out deploy
 """
@@ -75,7 +77,7 @@ def rabbitmq_definitions() -> dict:
 
 def prometheus_config() -> str:
     lines = ["global:", "  scrape_interval: 15s", "  evaluation_interval: 15s", "rule_files:", "  - alerts.yml",
-             "scrape_configs:"]
+             "  - alerts/*.yml", "scrape_configs:"]
     for svc, port in SERVICE_PORTS.items():
         lines += [f"  - job_name: {svc}", "    static_configs:", f"      - targets: ['{svc}:{port}']"]
     lines += ["  - job_name: pipeline-exporter", "    static_configs:", "      - targets: ['exporter:9502']",
@@ -140,7 +142,8 @@ def compose() -> str:
             "    volumes: ['./rabbitmq/definitions.json:/etc/rabbitmq/definitions.json:ro']",
             "    environment:", "      - RABBITMQ_SERVER_ADDITIONAL_ERL_ARGS=-rabbitmq_management load_definitions "
             "\"/etc/rabbitmq/definitions.json\"",
-            "  documentdb:", "    image: mongo:7", "    profiles: ['services']"]
+            "  documentdb:", "    image: mongo:7", "    profiles: ['services']",
+            "    volumes: ['./mongo/mongo-init.js:/docker-entrypoint-initdb.d/mongo-init.js:ro']"]
     for svc, port in SERVICE_PORTS.items():
         out += [f"  {svc}:", "    image: copilot-for-consensus-amd:latest", "    profiles: ['services']",
                 f"    command: python -m copilot_for_consensus_amd.services.main {svc} --port {port}",
@@ -151,7 +154,15 @@ def compose() -> str:
             out += ["    environment:"] + base_env
         out += ["    depends_on: [messagebus, documentdb]"]
     out += ["  prometheus:", "    image: prom/prometheus", "    profiles: ['services', 'node']",
-            "    volumes: ['./prometheus:/etc/prometheus:ro']", "    ports: ['9090:9090']"]
+            "    volumes: ['./prometheus:/etc/prometheus:ro']", "    ports: ['9090:9090']",
+            "  grafana:", "    image: grafana/grafana", "    profiles: ['services', 'node']",
+            "    volumes: ['./grafana/dashboards:/var/lib/grafana/dashboards:ro']", "    ports: ['3000:3000']",
+            "  loki:", "    image: grafana/loki", "    profiles: ['services', 'node']",
+            "    command: -config.file=/etc/loki/loki-config.yml",
+            "    volumes: ['./loki:/etc/loki:ro']", "    ports: ['3100:3100']",
+            "  promtail:", "    image: grafana/promtail", "    profiles: ['services', 'node']",
+            "    command: -config.file=/etc/promtail/promtail-config.yml",
+            "    volumes: ['./promtail:/etc/promtail:ro', '/var/run/docker.sock:/var/run/docker.sock:ro']"]
     return "\n".join(out) + "\n"
 
 
@@ -168,6 +179,21 @@ def main(argv=None) -> int:
     (out / "docker-compose.yml").write_text(compose())
     (out / "grafana" / "dashboards").mkdir(parents=True, exist_ok=True)
     (out / "grafana" / "dashboards" / "copilot-mi355x.json").write_text(json.dumps(grafana_dashboard(), indent=2) + "\n")
+    from . import ops_assets as ops
+    import yaml
+    (out / "prometheus" / "alerts").mkdir(parents=True, exist_ok=True)
+    for stem, rules in ops.alert_groups().items():
+        (out / "prometheus" / "alerts" / f"{stem}.yml").write_text(yaml.safe_dump(rules, sort_keys=False))
+    for stem, dash in ops.dashboards().items():
+        (out / "grafana" / "dashboards" / f"{stem}.json").write_text(json.dumps(dash, indent=2) + "\n")
+    for sub, fname, body in (("loki", "loki-config.yml", ops.loki_config()),
+                             ("promtail", "promtail-config.yml", ops.promtail_config())):
+        (out / sub).mkdir(parents=True, exist_ok=True)
+        (out / sub / fname).write_text(yaml.safe_dump(body, sort_keys=False))
+    (out / "mongo").mkdir(parents=True, exist_ok=True)
+    (out / "mongo" / "mongo-init.js").write_text(ops.mongo_init_js())
+    (out / "k8s").mkdir(parents=True, exist_ok=True)
+    (out / "k8s" / "copilot-mi355x.yaml").write_text(ops.k8s_yaml())
     print(f"wrote deployment files under {out}")
     return 0
 

@@ -38,8 +38,10 @@ def _fmt(name, labels: dict, value) -> str:
 
 
 class PipelineExporter:
-    def __init__(self, store, vector_store=None, database: str = "copilot"):
+    def __init__(self, store, vector_store=None, database: str = "copilot", broker=None, gpus: bool = False):
         self.store, self.vectors, self.db = store, vector_store, database
+        self.broker = broker          # in-process broker: queue depth / consumer gauges
+        self.gpus = gpus              # per-device HBM gauges (torch.cuda.mem_get_info)
         self.scrape_errors = 0
 
     def collect(self) -> list[str]:
@@ -80,6 +82,23 @@ class PipelineExporter:
                 if X is not None:
                     out.append(_fmt("copilot_vectorstore_device_bytes", {"device": str(X.device)},
                                     X.numel() * X.element_size()))
+            except Exception:
+                self.scrape_errors += 1
+        if self.broker is not None:
+            try:
+                consumers = self.broker.consumer_counts()
+                for q, depth in sorted(self.broker.queues().items()):
+                    out.append(_fmt("copilot_queue_messages", {"queue": q}, depth))
+                    out.append(_fmt("copilot_queue_consumers", {"queue": q}, consumers.get(q, 0)))
+            except Exception:
+                self.scrape_errors += 1
+        if self.gpus:
+            try:
+                import torch
+                for i in range(torch.cuda.device_count()):
+                    free, total = torch.cuda.mem_get_info(i)
+                    out.append(_fmt("copilot_gpu_hbm_used_bytes", {"device": i}, total - free))
+                    out.append(_fmt("copilot_gpu_hbm_total_bytes", {"device": i}, total))
             except Exception:
                 self.scrape_errors += 1
         out.append(_fmt("copilot_document_exporter_scrape_errors_total", {}, self.scrape_errors))
