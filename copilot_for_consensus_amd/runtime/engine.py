@@ -19,6 +19,7 @@ import math
 import os
 import time
 
+import numpy as np
 import torch
 
 from ..observability import span
@@ -105,7 +106,7 @@ class LLMEngine:
         """Chunked packed prefill; returns first sampled token per prompt.  ``start[s]`` tokens of
         prompt s are already in the cache (shared prefix blocks)."""
         n = len(prompts)
-        first = [0] * n
+        first_dev = torch.zeros(n, dtype=torch.int32, device=self.device)
         pos = list(start) if start is not None else [0] * n  # tokens of each prompt already in the cache
         order = list(range(n))
         while order:
@@ -120,13 +121,13 @@ class LLMEngine:
                     order.remove(s)
                 else:
                     break  # a split sequence ends the chunk
-            ids, positions, slots, cu, ctx, rows, last_rows, finishing = [], [], [], [0], [], [], [], []
+            cu, ctx, rows, last_rows, finishing = [0], [], [], [], []
+            ids_np, pos_np, slot_np = [], [], []
             for (s, a, b) in chunk:
-                toks = prompts[s][a:b]
-                ids.extend(toks)
-                positions.extend(range(a, b))
-                bt = tables[s]
-                slots.extend(bt[p // KV_BLOCK] * KV_BLOCK + p % KV_BLOCK for p in range(a, b))
+                ids_np.append(np.asarray(prompts[s][a:b], dtype=np.int32))
+                p = np.arange(a, b, dtype=np.int32)
+                pos_np.append(p)
+                slot_np.append(np.asarray(tables[s], dtype=np.int32)[p // KV_BLOCK] * KV_BLOCK + p % KV_BLOCK)
                 cu.append(cu[-1] + (b - a))
                 ctx.append(b)
                 rows.append(s)
@@ -135,20 +136,37 @@ class LLMEngine:
                     finishing.append(s)
                 pos[s] = b
             maxb = max(len(tables[s]) for s in rows)
-            bt = torch.zeros(len(rows), maxb, dtype=torch.int32)
+            bt = np.zeros((len(rows), maxb), dtype=np.int32)
             for r, s in enumerate(rows):
-                bt[r, :len(tables[s])] = torch.tensor(tables[s], dtype=torch.int32)
+                bt[r, :len(tables[s])] = tables[s]
             tseq, tq0 = K.prefill_tiles(cu, self._prefill_rows, ctx)
+            # everything the chunk needs in ONE pinned host buffer and one non-blocking copy: a
+            # pageable torch.tensor(..., device=cuda) synchronises the stream, so the GPU would idle
+            # while the host builds the next chunk
+            parts = [np.concatenate(ids_np), np.concatenate(pos_np), np.concatenate(slot_np),
+                     np.asarray(cu, np.int32), np.asarray(ctx, np.int32), np.asarray(tseq, np.int32),
+                     np.asarray(tq0, np.int32), np.asarray(last_rows, np.int32),
+                     np.asarray(finishing, np.int32), bt.reshape(-1)]
+            dev = self._h2d(np.concatenate(parts))
+            offs = np.cumsum([0] + [len(x) for x in parts]).tolist()
+            d_ids, d_pos, d_slots, d_cu, d_ctx, d_tseq, d_tq0, d_last, d_fin, d_bt = (
+                dev[offs[i]:offs[i + 1]] for i in range(len(parts)))
             hidden = self.model.forward_prefill(
-                self._i32(ids), self._i32(positions), self._i32(slots), self._i32(cu), self._i32(ctx),
-                bt.to(self.device), self.kv, tiles=(self._i32(tseq), self._i32(tq0)),
-                last_idx=torch.tensor(last_rows, dtype=torch.long, device=self.device) if last_rows else None)
+                d_ids, d_pos, d_slots, d_cu, d_ctx, d_bt.view(len(rows), maxb), self.kv, tiles=(d_tseq, d_tq0),
+                last_idx=d_last.long() if last_rows else None)
             if finishing:
                 logits = self.model.logits(hidden)
                 out = torch.empty(len(finishing), dtype=torch.int32, device=self.device)
                 K.sample(logits, out, temperature, seed, torch.zeros(1, dtype=torch.int32, device=self.device))
-                for s, t in zip(finishing, out.tolist()):
-                    first[s] = t
+                first_dev.index_copy_(0, d_fin.long(), out)
+        return first_dev.tolist()      # the one host sync of the prefill
+
+    def _h2d(self, a: np.ndarray) -> torch.Tensor:
+        t = torch.from_numpy(a)
+        if self.device.type != "cuda":
+            return t.clone()
+        return t.pin_memory().to(self.device, non_blocking=True)
+
         return first
 
     def _decode_step(self, st: _DecodeState, part_blocks, temperature, seed):
