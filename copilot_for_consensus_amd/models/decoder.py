@@ -279,8 +279,9 @@ class DecoderModel:
         return self._all_reduce(F.linear(a, lw["down"]))
 
     def forward_prefill(self, ids, positions, slots, cu_q, ctx_lens, block_tables, kv, tiles=None,
-                        last_idx=None) -> torch.Tensor:
-        """Packed varlen prefill. Returns hidden states of rows ``last_idx`` (or all rows)."""
+                        last_idx=None, v_runs=None) -> torch.Tensor:
+        """Packed varlen prefill. Returns hidden states of rows ``last_idx`` (or all rows).
+        ``v_runs`` (ops.kernels.v_runs of the slots, on device): V written per cache block."""
         cfg, w = self.cfg, self.w
         x = K.embedding(w.embed, ids)
         residual = None
@@ -289,7 +290,7 @@ class DecoderModel:
             h, residual = self._layer_pre(i, x, residual)
             qkv = F.linear(h, lw["qkv"])
             q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
-                                cfg.head_dim)
+                                cfg.head_dim, runs=v_runs)
             attn = K.prefill_attention(q, kv.k[i], kv.v[i], block_tables, cu_q, ctx_lens, self.scale, tiles=tiles)
             o = self._all_reduce(F.linear(attn.view(attn.shape[0], -1), lw["o"]))
             x = self._mlp(i, o, residual)

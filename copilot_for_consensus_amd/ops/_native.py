@@ -30,7 +30,8 @@ _KERNEL_SIGS = {
     "cfc_prefill_attention": [P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, P, P],
     "cfc_prefill_rows": [I, I],
     "cfc_encoder_attention": [P, P, P, P, I, I, I, I, F, P, P],
-    "cfc_rope_kv_write": [P, P, P, P, P, P, P, I, I, I, I, P],
+    "cfc_rope_kv_write": [P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "cfc_v_cache_write_runs": [P, P, I, P, I, I, I, P],
     "cfc_silu_mul": [P, P, I, I, I, P],
     "cfc_bias_gelu": [P, P, P, I, I, P],
     "cfc_embedding": [P, P, P, I, I, P],

@@ -87,7 +87,24 @@ def embed_layernorm(ids, positions, word_emb, pos_emb, type_emb, gamma, beta, ep
 
 # ----------------------------------------------------------------------------- decoder ops
 
-def rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D, q_out=None):
+def v_runs(slots) -> "np.ndarray":
+    """Host-side run list for :func:`rope_kv_write`'s prefill V path: maximal groups of consecutive
+    tokens whose slots fall in one cache block at consecutive offsets -> int32 [R, 4]
+    {first token, count, block, first offset}."""
+    import numpy as np
+    s = np.asarray(slots, dtype=np.int64)
+    if s.size == 0:
+        return np.zeros((0, 4), np.int32)
+    blk, off = s // KV_BLOCK, s % KV_BLOCK
+    brk = np.flatnonzero((np.diff(blk) != 0) | (np.diff(off) != 1)) + 1
+    starts = np.concatenate([[0], brk])
+    ends = np.concatenate([brk, [s.size]])
+    return np.stack([starts, ends - starts, blk[starts], off[starts]], 1).astype(np.int32)
+
+
+def rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D, q_out=None, runs=None):
+    """RoPE on q/k + paged K/V cache write.  ``runs`` (device int32 [R, 4] from :func:`v_runs`):
+    write V per whole cache block (prefill); without it V is written per token (decode)."""
     if not qkv.is_cuda:
         q = ref.rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D)
         if q_out is not None:
@@ -100,10 +117,15 @@ def rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D, 
     T = qkv.shape[0]
     if qkv.shape[1] != (Hq + 2 * Hkv) * D:
         raise ValueError("rope_kv_write: qkv width mismatch")
+    if runs is not None:
+        _req(runs, torch.int32, "runs")
     q_out = torch.empty(T, Hq, D, dtype=qkv.dtype, device=qkv.device) if q_out is None else q_out
     check(kernels().cfc_rope_kv_write(qkv.data_ptr(), positions.data_ptr(), slots.data_ptr(), cos_sin.data_ptr(),
                                       q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), T, Hq, Hkv, D,
-                                      _stream(qkv)), "cfc_rope_kv_write")
+                                      0 if runs is not None else 1, _stream(qkv)), "cfc_rope_kv_write")
+    if runs is not None:
+        check(kernels().cfc_v_cache_write_runs(qkv.data_ptr(), runs.data_ptr(), runs.shape[0], v_cache.data_ptr(),
+                                               Hq, Hkv, D, _stream(qkv)), "cfc_v_cache_write_runs")
     return q_out
 
 

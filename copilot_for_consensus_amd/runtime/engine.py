@@ -143,17 +143,19 @@ class LLMEngine:
             # everything the chunk needs in ONE pinned host buffer and one non-blocking copy: a
             # pageable torch.tensor(..., device=cuda) synchronises the stream, so the GPU would idle
             # while the host builds the next chunk
-            parts = [np.concatenate(ids_np), np.concatenate(pos_np), np.concatenate(slot_np),
+            slots_np = np.concatenate(slot_np)
+            runs = K.v_runs(slots_np)
+            parts = [np.concatenate(ids_np), np.concatenate(pos_np), slots_np,
                      np.asarray(cu, np.int32), np.asarray(ctx, np.int32), np.asarray(tseq, np.int32),
                      np.asarray(tq0, np.int32), np.asarray(last_rows, np.int32),
-                     np.asarray(finishing, np.int32), bt.reshape(-1)]
+                     np.asarray(finishing, np.int32), bt.reshape(-1), runs.reshape(-1)]
             dev = self._h2d(np.concatenate(parts))
             offs = np.cumsum([0] + [len(x) for x in parts]).tolist()
-            d_ids, d_pos, d_slots, d_cu, d_ctx, d_tseq, d_tq0, d_last, d_fin, d_bt = (
+            d_ids, d_pos, d_slots, d_cu, d_ctx, d_tseq, d_tq0, d_last, d_fin, d_bt, d_runs = (
                 dev[offs[i]:offs[i + 1]] for i in range(len(parts)))
             hidden = self.model.forward_prefill(
                 d_ids, d_pos, d_slots, d_cu, d_ctx, d_bt.view(len(rows), maxb), self.kv, tiles=(d_tseq, d_tq0),
-                last_idx=d_last.long() if last_rows else None)
+                last_idx=d_last.long() if last_rows else None, v_runs=d_runs.view(-1, 4))
             if finishing:
                 logits = self.model.logits(hidden)
                 out = torch.empty(len(finishing), dtype=torch.int32, device=self.device)

@@ -23,13 +23,15 @@ __device__ __forceinline__ int v_slot(int key_in_block) {
 __global__ void __launch_bounds__(64) rope_kv_kernel(const uint16_t* __restrict__ qkv, const int32_t* __restrict__ positions,
                                                      const int32_t* __restrict__ slots, const float* __restrict__ cos_sin,
                                                      uint16_t* __restrict__ q_out, uint16_t* __restrict__ k_cache,
-                                                     uint16_t* __restrict__ v_cache, int Hq, int Hkv, int D) {
+                                                     uint16_t* __restrict__ v_cache, int Hq, int Hkv, int D,
+                                                     int write_v) {
   // grid = (T, ceil(items / 64)): one 8-element item per thread -- (Hq + Hkv) * D/16 rotation
   // items then Hkv * D/8 V items -- so a decode batch of 128 tokens is ~900 blocks, not 128.
+  // write_v = 0: V goes through v_cache_runs_kernel instead (prefill: whole blocks, 16-B stores)
   const int tok = blockIdx.x;
   const int half = D / 2, nv = half / 8;  // 8-element vectors per half-head
   const int n_rot = (Hq + Hkv) * nv;
-  const int n_v = Hkv * (D / 8);
+  const int n_v = write_v ? Hkv * (D / 8) : 0;
   const int it = blockIdx.y * 64 + threadIdx.x;
   if (it >= n_rot + n_v) return;
   const int stride = (Hq + 2 * Hkv) * D;
@@ -76,6 +78,47 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const uint16_t* __restrict_
     const uint16_t* e = reinterpret_cast<const uint16_t*>(&val);
 #pragma unroll
     for (int j = 0; j < 8; ++j) dst[j * KV_BS] = e[j];
+  }
+}
+
+// Prefill V-cache writer.  One workgroup per (run, kv-head); a run = consecutive tokens that land
+// in ONE cache block at consecutive offsets (runs[r] = {first token, count, block, first offset},
+// built on the host from the slots).  The run's V rows are staged in LDS and written out as the
+// block's transposed, slot-permuted image: a full run (32 tokens) as 16-byte stores of whole
+// 8-slot chunks, a partial run (chunk edges, prefix-cache continuations) per element so the
+// block's other slots are left untouched.  Replaces the 2-byte scattered stores of the per-token
+// path (1.85 TB/s effective for rope_kv at a prefill chunk, profiles/elementwise_bw_probe_r01.log).
+__global__ void __launch_bounds__(256) v_cache_runs_kernel(const uint16_t* __restrict__ qkv,
+                                                           const int32_t* __restrict__ runs,
+                                                           uint16_t* __restrict__ v_cache, int Hq, int Hkv, int D) {
+  __shared__ __attribute__((aligned(16))) uint16_t sv[KV_BS][256 + 8];
+  const int r = blockIdx.x, kh = blockIdx.y, tid = threadIdx.x;
+  const int t0 = runs[4 * r], n = runs[4 * r + 1], blk = runs[4 * r + 2], off0 = runs[4 * r + 3];
+  const int nc = D / 8;
+  const size_t stride = (size_t)(Hq + 2 * Hkv) * D;
+  for (int i = tid; i < n * nc; i += 256) {
+    const int j = i / nc, c = i - j * nc;
+    *reinterpret_cast<uint4*>(&sv[off0 + j][c * 8]) =
+        *reinterpret_cast<const uint4*>(qkv + (size_t)(t0 + j) * stride + (size_t)(Hq + Hkv + kh) * D + c * 8);
+  }
+  __syncthreads();
+  uint16_t* dst = v_cache + ((size_t)blk * Hkv + kh) * D * KV_BS;   // [D][32 slots]
+  if (n == KV_BS) {
+    for (int i = tid; i < D * 4; i += 256) {
+      const int d = i >> 2, g = i & 3;
+      uint16_t e[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) e[j] = sv[16 * (j >> 2) + 4 * g + (j & 3)][d];   // key held by slot 8g + j
+      uint4 v;
+      v.x = e[0] | ((uint32_t)e[1] << 16); v.y = e[2] | ((uint32_t)e[3] << 16);
+      v.z = e[4] | ((uint32_t)e[5] << 16); v.w = e[6] | ((uint32_t)e[7] << 16);
+      *reinterpret_cast<uint4*>(dst + d * KV_BS + 8 * g) = v;
+    }
+  } else {
+    for (int i = tid; i < n * D; i += 256) {
+      const int j = i / D, d = i - j * D, off = off0 + j;
+      dst[d * KV_BS + v_slot(off)] = sv[off][d];
+    }
   }
 }
 
@@ -370,12 +413,22 @@ inline int ew_grid(size_t total) {
 
 CFC_API int cfc_rope_kv_write(const void* qkv, const int32_t* positions, const int32_t* slots, const float* cos_sin,
                               void* q_out, void* k_cache, void* v_cache, int T, int Hq, int Hkv, int head_dim,
-                              hipStream_t stream) {
+                              int write_v, hipStream_t stream) {
   if (head_dim % 16 != 0 || T < 0) return -1;
   if (T == 0) return 0;
-  const int items = (Hq + Hkv) * (head_dim / 16) + Hkv * (head_dim / 8);
+  const int items = (Hq + Hkv) * (head_dim / 16) + (write_v ? Hkv * (head_dim / 8) : 0);
   rope_kv_kernel<<<dim3(T, (items + 63) / 64), 64, 0, stream>>>((const uint16_t*)qkv, positions, slots, cos_sin, (uint16_t*)q_out,
-                                         (uint16_t*)k_cache, (uint16_t*)v_cache, Hq, Hkv, head_dim);
+                                         (uint16_t*)k_cache, (uint16_t*)v_cache, Hq, Hkv, head_dim, write_v);
+  return CFC_CHECK_LAUNCH();
+}
+
+// runs: [R][4] int32 {first token, count (1..32), cache block, first offset (count + offset <= 32)}
+CFC_API int cfc_v_cache_write_runs(const void* qkv, const int32_t* runs, int R, void* v_cache, int Hq, int Hkv,
+                                   int head_dim, hipStream_t stream) {
+  if (head_dim % 8 != 0 || head_dim > 256 || R < 0) return -1;
+  if (R == 0) return 0;
+  v_cache_runs_kernel<<<dim3(R, Hkv), 256, 0, stream>>>((const uint16_t*)qkv, runs, (uint16_t*)v_cache, Hq, Hkv,
+                                                        head_dim);
   return CFC_CHECK_LAUNCH();
 }
 

@@ -37,6 +37,9 @@ def main():
         us = timeit(lambda: K.rope_kv_write(qkv, pos, slots, cs, kc, vc, Hq, Hkv, D))
         byts = qkv.numel() * 2 + T * Hq * D * 2 + 2 * T * Hkv * D * 2
         print(f"rope_kv T={T}: {us:.1f} us  {byts / us / 1e6:.2f} TB/s", flush=True)
+        runs = torch.from_numpy(K.v_runs(slots.cpu().numpy())).cuda()
+        us = timeit(lambda: K.rope_kv_write(qkv, pos, slots, cs, kc, vc, Hq, Hkv, D, runs=runs))
+        print(f"rope_kv+v_runs T={T}: {us:.1f} us  {byts / us / 1e6:.2f} TB/s", flush=True)
         gu = torch.randn(T, 2 * FF, device="cuda").bfloat16()
         us = timeit(lambda: K.silu_mul(gu))
         print(f"silu_mul T={T}: {us:.1f} us  {gu.numel() * 3 / us / 1e6:.2f} TB/s", flush=True)

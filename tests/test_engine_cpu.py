@@ -116,3 +116,12 @@ def test_prefix_cache_invalidates_on_failure():
     assert eng.kv.pool.num_free() == 32 and eng.prefix_cache.cached_blocks() == 0
     again = eng.generate([[1] + [2] * 100], 3, ignore_eos=True)
     assert again.cached_prompt_tokens == 0
+
+
+def test_v_runs_split_on_block_and_offset_breaks():
+    from copilot_for_consensus_amd.ops import kernels as K
+    slots = [3 * 32 + 30, 3 * 32 + 31, 7 * 32, 7 * 32 + 1, 7 * 32 + 3, 2 * 32 + 0]
+    assert K.v_runs(slots).tolist() == [[0, 2, 3, 30], [2, 2, 7, 0], [4, 1, 7, 3], [5, 1, 2, 0]]
+    full = K.v_runs([5 * 32 + i for i in range(32)] + [6 * 32 + i for i in range(32)])
+    assert full.tolist() == [[0, 32, 5, 0], [32, 32, 6, 0]]
+    assert K.v_runs([]).shape == (0, 4)

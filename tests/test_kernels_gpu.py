@@ -76,6 +76,32 @@ def test_rope_kv_write():
     _close(vc, vc2, 1e-6, 0)
 
 
+def test_rope_kv_write_prefill_runs():
+    """The prefill V path (whole-block runs, 16-B stores; partial runs per element) writes exactly
+    what the per-token path writes and leaves the other slots of partially written blocks alone."""
+    Hq, Hkv, D = 8, 2, 128
+    # seq A continues at offset 5 of block 3 (prefix in cache) for 70 tokens; seq B: 40 tokens from 0
+    slots = [3 * 32 + 5 + i for i in range(27)] + [9 * 32 + i for i in range(32)] + [4 * 32 + i for i in range(11)]
+    slots += [12 * 32 + i for i in range(32)] + [1 * 32 + i for i in range(8)]
+    T = len(slots)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV).bfloat16()
+    pos = torch.arange(T, device=DEV, dtype=torch.int32)
+    cs = R.rope_cos_sin(4096, D, 1e6, device=DEV)
+    kc0 = torch.randn(16, Hkv, 32, D, device=DEV).bfloat16()
+    vc0 = torch.randn(16, Hkv, D, 32, device=DEV).bfloat16()
+    kc1, vc1, kc2, vc2 = kc0.clone(), vc0.clone(), kc0.clone(), vc0.clone()
+    sl = torch.tensor(slots, dtype=torch.int32, device=DEV)
+    runs_np = K.v_runs(slots)
+    assert runs_np[:, 1].tolist() == [27, 32, 11, 32, 8]
+    runs = torch.from_numpy(runs_np).to(DEV)
+    q1 = K.rope_kv_write(qkv, pos, sl, cs, kc1, vc1, Hq, Hkv, D)
+    q2 = K.rope_kv_write(qkv, pos, sl, cs, kc2, vc2, Hq, Hkv, D, runs=runs)
+    torch.cuda.synchronize()
+    assert torch.equal(q1, q2) and torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
+    untouched = [b for b in range(16) if b not in (1, 3, 4, 9, 12)]
+    assert torch.equal(vc2[untouched], vc0[untouched])
+
+
 def _fill_cache(ctx_lens, Hkv, D, extra_blocks=3):
     """Random K/V for every sequence, written through the reference writer; returns tables."""
     tables, nblk = [], 0
