@@ -201,25 +201,48 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 // Reduce partials + residual add + RMSNorm, one block per row (N = hidden, N / 8 <= 1024 threads):
 //   h = sum_p part[p][m] + residual[m];  residual[m] <- bf16(h);  out[m] = bf16(norm(bf16(h)) * w)
 // (the rounding sequence of rmsnorm_kernel with add_residual, so fused and unfused decode agree).
-__global__ void __launch_bounds__(1024) splitk_residual_rmsnorm_kernel(const float* __restrict__ part, int split,
+// SPLIT is a template parameter so every partial, the residual and the norm weight are loaded
+// up front with no per-split branch: a runtime-count loop made the compiler wait for each split's
+// loads before issuing the next (one dependent L2/HBM round trip per split).
+template <int SPLIT>
+__global__ void __launch_bounds__(1024) splitk_residual_rmsnorm_kernel(const float* __restrict__ part, int split_rt,
                                                                        int M, int N, uint16_t* __restrict__ residual,
                                                                        const uint16_t* __restrict__ w, float eps,
                                                                        uint16_t* __restrict__ out) {
   __shared__ float red[16];
   const int m = blockIdx.x, c = threadIdx.x;      // c: 8-column group
+  const int split = SPLIT > 0 ? SPLIT : split_rt;
   const bool act = c * 8 < N;
   float v[8];
   float ss = 0.f;
+  uint4 rr = make_uint4(0, 0, 0, 0), wv = make_uint4(0, 0, 0, 0);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  uint4* rp = reinterpret_cast<uint4*>(residual + (size_t)m * N) + c;
   if (act) {
-    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int p = 0; p < split; ++p) {
-      const float4* row = reinterpret_cast<const float4*>(part + ((size_t)p * M + m) * N + c * 8);
-      const float4 a = row[0], b = row[1];
-      s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w; s[4] += b.x; s[5] += b.y; s[6] += b.z; s[7] += b.w;
+    rr = *rp;
+    wv = reinterpret_cast<const uint4*>(w)[c];
+    if constexpr (SPLIT > 0) {
+      float4 a[SPLIT], b[SPLIT];
+#pragma unroll
+      for (int p = 0; p < SPLIT; ++p) {
+        const float4* row = reinterpret_cast<const float4*>(part + ((size_t)p * M + m) * N + c * 8);
+        a[p] = row[0];
+        b[p] = row[1];
+      }
+#pragma unroll
+      for (int p = 0; p < SPLIT; ++p) {
+        s[0] += a[p].x; s[1] += a[p].y; s[2] += a[p].z; s[3] += a[p].w;
+        s[4] += b[p].x; s[5] += b[p].y; s[6] += b[p].z; s[7] += b[p].w;
+      }
+    } else {
+      for (int p = 0; p < split; ++p) {
+        const float4* row = reinterpret_cast<const float4*>(part + ((size_t)p * M + m) * N + c * 8);
+        const float4 a = row[0], b = row[1];
+        s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w; s[4] += b.x; s[5] += b.y; s[6] += b.z; s[7] += b.w;
+      }
     }
-    uint4* rp = reinterpret_cast<uint4*>(residual + (size_t)m * N) + c;
     float r[8];
-    unpack8(*rp, r);
+    unpack8(rr, r);
     // the projection output is rounded to bf16 first (as the unfused path stores it), then added
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(s[j])) + r[j];
@@ -233,7 +256,7 @@ __global__ void __launch_bounds__(1024) splitk_residual_rmsnorm_kernel(const flo
   const float inv = rsqrtf(ss / (float)N + eps);
   if (act) {
     float gw[8], o[8];
-    unpack8(reinterpret_cast<const uint4*>(w)[c], gw);
+    unpack8(wv, gw);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = v[j] * inv * gw[j];
     reinterpret_cast<uint4*>(out + (size_t)m * N)[c] = pack8(o);
@@ -273,9 +296,16 @@ CFC_API int cfc_splitk_reduce(const float* part, int split, int M, int N, int mo
 
 CFC_API int cfc_splitk_residual_rmsnorm(const float* part, int split, int M, int N, void* residual, const void* w,
                                         float eps, void* out, hipStream_t stream) {
-  if (N % 8 || N / 8 > 1024 || M <= 0) return -1;
+  if (N % 8 || N / 8 > 1024 || M <= 0 || split <= 0) return -1;
   const int threads = ((N / 8 + 63) / 64) * 64;
-  splitk_residual_rmsnorm_kernel<<<M, threads, 0, stream>>>(part, split, M, N, (uint16_t*)residual,
-                                                            (const uint16_t*)w, eps, (uint16_t*)out);
+#define SRR_ARGS part, split, M, N, (uint16_t*)residual, (const uint16_t*)w, eps, (uint16_t*)out
+  switch (split) {
+    case 1: splitk_residual_rmsnorm_kernel<1><<<M, threads, 0, stream>>>(SRR_ARGS); break;
+    case 2: splitk_residual_rmsnorm_kernel<2><<<M, threads, 0, stream>>>(SRR_ARGS); break;
+    case 4: splitk_residual_rmsnorm_kernel<4><<<M, threads, 0, stream>>>(SRR_ARGS); break;
+    case 8: splitk_residual_rmsnorm_kernel<8><<<M, threads, 0, stream>>>(SRR_ARGS); break;
+    default: splitk_residual_rmsnorm_kernel<0><<<M, threads, 0, stream>>>(SRR_ARGS); break;
+  }
+#undef SRR_ARGS
   return CFC_CHECK_LAUNCH();
 }

@@ -25,6 +25,52 @@ def timeit(fn, iters=20):
     return (time.perf_counter() - t) / iters * 1e6
 
 
+def graph_us(fn, iters=200):
+    """Per-call time inside one replayed hipGraph (launch overhead excluded, as in decode)."""
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    g.replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / iters * 1e6
+
+
+def decode_sizes():
+    """The per-layer elementwise kernels of one B=128 decode step, graph-replayed."""
+    B = 128
+    cs = R.rope_cos_sin(32768, D, 1e6, device="cuda")
+    kc = torch.zeros(B * 100, Hkv, 32, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.zeros(B * 100, Hkv, D, 32, device="cuda", dtype=torch.bfloat16)
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
+    pos = (torch.arange(B, device="cuda", dtype=torch.int32) * 37 + 2000) % 4000
+    slots = torch.arange(B, device="cuda", dtype=torch.int32) * 3200 + 2900
+    print(f"[graph] rope_kv B={B}: {graph_us(lambda: K.rope_kv_write(qkv, pos, slots, cs, kc, vc, Hq, Hkv, D)):.2f} us")
+    gu = torch.randn(B, 2 * FF, device="cuda").bfloat16()
+    print(f"[graph] silu_mul B={B}: {graph_us(lambda: K.silu_mul(gu)):.2f} us")
+    for K_, split in ((Hq * D, 4), (FF, 8)):
+        a = torch.randn(B, K_, device="cuda").bfloat16()
+        w = torch.randn(H, K_, device="cuda").bfloat16()
+        res = torch.randn(B, H, device="cuda").bfloat16()
+        nw = torch.randn(H, device="cuda").bfloat16()
+        part = torch.randn(split, B, H, device="cuda")
+        out = torch.empty(B, H, device="cuda").bfloat16()
+        f = lambda: K.kernels().cfc_splitk_residual_rmsnorm(part.data_ptr(), split, B, H, res.data_ptr(),  # noqa: E731
+                                                             nw.data_ptr(), 1e-5, out.data_ptr(), K._stream(a))
+        print(f"[graph] splitk_residual_rmsnorm split={split}: {graph_us(f):.2f} us")
+        g = lambda: K.lib_splitk_linear_residual_rmsnorm(a, w, split, res, nw, 1e-5)  # noqa: E731
+        print(f"[graph] lib split-K GEMM + reduce K={K_} split={split}: {graph_us(g, 50):.2f} us")
+    x = torch.randn(B, H, device="cuda").bfloat16()
+    res = torch.randn(B, H, device="cuda").bfloat16()
+    nw = torch.randn(H, device="cuda").bfloat16()
+    print(f"[graph] add+rmsnorm B={B}: {graph_us(lambda: K.rmsnorm(x, nw, 1e-5, residual=res)):.2f} us")
+
+
 def main():
     cs = R.rope_cos_sin(32768, D, 1e6, device="cuda")
     for T in (18432, 128):
@@ -52,3 +98,4 @@ def main():
 
 if __name__ == "__main__":
     main()
+    decode_sizes()
