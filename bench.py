@@ -87,10 +87,12 @@ def main(argv=None):
         for i, r in enumerate(results):
             print(f"[bench] step {i}: {r.summary()}", file=sys.stderr, flush=True)
 
-    threads_local = sum(r.threads for r in results)
-    lat_local = [x for r in results for x in r.latencies_s]
-    gen_tokens_local = sum(r.generated_tokens for r in results)
-    prompt_tokens_local = sum(r.prompt_tokens for r in results)
+    # one report per DP replica: TP followers ran the same threads as their leader
+    lead = groups.tp_rank == 0
+    threads_local = sum(r.threads for r in results) if lead else 0
+    lat_local = [x for r in results for x in r.latencies_s] if lead else []
+    gen_tokens_local = sum(r.generated_tokens for r in results) if lead else 0
+    prompt_tokens_local = sum(r.prompt_tokens for r in results) if lead else 0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

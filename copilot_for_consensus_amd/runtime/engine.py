@@ -76,6 +76,12 @@ class LLMEngine:
         self.device = kv.device
         self.max_prefill_tokens = max_prefill_tokens
         self.use_graph = use_graph and kv.device.type == "cuda"
+        tp_group = getattr(model, "tp_group", None)
+        if self.use_graph and tp_group is not None:
+            import torch.distributed as dist
+            # gloo collectives cannot be captured in a hipGraph (RCCL's can): eager decode steps
+            if dist.get_backend(tp_group) == "gloo":
+                self.use_graph = False
         # query rows per prefill attention tile (the GQA-packed kernel takes 256 / G)
         self._prefill_rows = (K.prefill_rows(model.w.heads, model.w.kv_heads) if kv.device.type == "cuda"
                               else K.PREFILL_TILE_ROWS)
