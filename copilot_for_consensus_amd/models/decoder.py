@@ -47,6 +47,8 @@ class DecoderConfig:
     eos_id: int = 2
     # Llama-3.1 RoPE frequency scaling: (factor, low_freq_factor, high_freq_factor, original_max_positions)
     rope_llama3: tuple | None = None
+    # sliding-window attention (Mistral v0.1: 4096): a token sees the previous `sliding_window` positions
+    sliding_window: int | None = None
 
     @property
     def q_size(self) -> int:
@@ -73,6 +75,9 @@ PRESETS: dict[str, DecoderConfig] = {
     # mistral-7b-instruct-v0.2 (what docker-compose.infra.yml:296 serves): no sliding window, theta 1e6
     "mistral-7b": DecoderConfig("mistral-7b", 32000, 4096, 32, 32, 8, 128, 14336, rope_theta=1e6,
                                 max_positions=32768),
+    # mistral-7b v0.1: sliding-window attention over 4096 positions, theta 1e4
+    "mistral-7b-v0.1": DecoderConfig("mistral-7b-v0.1", 32000, 4096, 32, 32, 8, 128, 14336, rope_theta=1e4,
+                                     max_positions=32768, sliding_window=4096),
     "llama-3-8b": DecoderConfig("llama-3-8b", 128256, 4096, 32, 32, 8, 128, 14336, rope_theta=5e5,
                                 max_positions=8192, bos_id=128000, eos_id=128009),
     "llama-3-70b": DecoderConfig("llama-3-70b", 128256, 8192, 80, 64, 8, 128, 28672, rope_theta=5e5,
@@ -221,6 +226,7 @@ def load_config_json(path) -> DecoderConfig:
         elif kind not in (None, "default"):
             raise NotImplementedError(f"RoPE scaling {kind!r} is not supported")
     eos = c.get("eos_token_id", 2)
+    window = c.get("sliding_window") if c.get("use_sliding_window", True) else None
     return DecoderConfig(
         name=c.get("_name_or_path", "hf"), vocab_size=c["vocab_size"], hidden=c["hidden_size"],
         layers=c["num_hidden_layers"], heads=c["num_attention_heads"],
@@ -228,7 +234,8 @@ def load_config_json(path) -> DecoderConfig:
         head_dim=c.get("head_dim") or c["hidden_size"] // c["num_attention_heads"], ffn=c["intermediate_size"],
         rope_theta=float(theta), rms_eps=c.get("rms_norm_eps", 1e-5),
         max_positions=c.get("max_position_embeddings", 4096), tie_embeddings=c.get("tie_word_embeddings", False),
-        bos_id=c.get("bos_token_id", 1) or 1, eos_id=eos if isinstance(eos, int) else eos[0], rope_llama3=llama3)
+        bos_id=c.get("bos_token_id", 1) or 1, eos_id=eos if isinstance(eos, int) else eos[0], rope_llama3=llama3,
+        sliding_window=int(window) if window else None)
 
 
 class DecoderModel:
@@ -241,6 +248,7 @@ class DecoderModel:
         # validated one-shot IPC all-reduce (parallel/custom_ar.py) for decode-size tensors; RCCL otherwise
         self.custom_ar = custom_ar
         self.scale = 1.0 / math.sqrt(self.cfg.head_dim)
+        self.window = int(self.cfg.sliding_window or 0)
         # decode projections on the split-K skinny MFMA GEMM with fused epilogues (TP=1; with TP>1
         # the all-reduce sits between the projection and the residual/norm)
         # decode GEMM mode (TP=1): "splitk" = library GEMMs, with o/down as batched split-K whose
@@ -291,7 +299,8 @@ class DecoderModel:
             qkv = F.linear(h, lw["qkv"])
             q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
                                 cfg.head_dim, runs=v_runs)
-            attn = K.prefill_attention(q, kv.k[i], kv.v[i], block_tables, cu_q, ctx_lens, self.scale, tiles=tiles)
+            attn = K.prefill_attention(q, kv.k[i], kv.v[i], block_tables, cu_q, ctx_lens, self.scale, tiles=tiles,
+                                       window=self.window)
             o = self._all_reduce(F.linear(attn.view(attn.shape[0], -1), lw["o"]))
             x = self._mlp(i, o, residual)
         if last_idx is not None:
@@ -319,7 +328,7 @@ class DecoderModel:
             q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
                                 cfg.head_dim)
             attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
-                                            part_blocks=part_blocks, workspace=attn_workspace)
+                                            part_blocks=part_blocks, workspace=attn_workspace, window=self.window)
             o = self._all_reduce(F.linear(attn.view(B, -1), lw["o"]))
             x = self._mlp(i, o, residual)
         return K.rmsnorm(x, w.final_norm, cfg.rms_eps, residual=residual)
@@ -339,7 +348,7 @@ class DecoderModel:
             q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
                                 cfg.head_dim)
             attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
-                                            part_blocks=part_blocks, workspace=attn_workspace)
+                                            part_blocks=part_blocks, workspace=attn_workspace, window=self.window)
             h = K.skinny_linear_residual_rmsnorm(attn.view(B, -1), lw["o"], residual, lw["mlp_norm"], eps)
             a = K.skinny_swiglu(h, lw["gate_up"])
             nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm
@@ -361,7 +370,7 @@ class DecoderModel:
             q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
                                 cfg.head_dim)
             attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
-                                            part_blocks=part_blocks, workspace=attn_workspace)
+                                            part_blocks=part_blocks, workspace=attn_workspace, window=self.window)
             h = K.lib_splitk_linear_residual_rmsnorm(attn.view(B, -1), lw["o"], s_o, residual, lw["mlp_norm"], eps)
             a = K.silu_mul(F.linear(h, lw["gate_up"]), interleaved=w.gate_up_interleaved)
             nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm

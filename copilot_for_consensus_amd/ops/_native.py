@@ -26,8 +26,8 @@ F = c_float
 _KERNEL_SIGS = {
     "cfc_rmsnorm": [P, P, P, P, I, I, F, I, P],
     "cfc_layernorm": [P, P, P, P, P, P, P, P, P, P, I, I, F, I, P],
-    "cfc_paged_decode_attention": [P, P, P, P, P, I, I, I, I, I, I, I, F, P, P, P, P],
-    "cfc_prefill_attention": [P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, P, P],
+    "cfc_paged_decode_attention": [P, P, P, P, P, I, I, I, I, I, I, I, F, I, P, P, P, P],
+    "cfc_prefill_attention": [P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P, P],
     "cfc_prefill_rows": [I, I],
     "cfc_encoder_attention": [P, P, P, P, I, I, I, I, F, P, P],
     "cfc_rope_kv_write": [P, P, P, P, P, P, P, I, I, I, I, I, P],

@@ -134,13 +134,14 @@ def decode_partitions(max_ctx: int, part_blocks: int) -> int:
 
 
 def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out=None, part_blocks=16,
-                           num_partitions=None, workspace=None):
+                           num_partitions=None, workspace=None, window=0):
     """q [B, Hq, D]; caches [nblk, Hkv, 32, D] / [nblk, Hkv, D, 32]; returns [B, Hq, D].
 
     ``part_blocks`` > 0: split-KV partitions of that many blocks; ``part_blocks`` = -P: P balanced
-    partitions of each sequence's own context (what the engine uses)."""
+    partitions of each sequence's own context (what the engine uses).  ``window`` > 0: sliding-window
+    attention over the last ``window`` keys (Mistral v0.1)."""
     if not q.is_cuda:
-        return ref.paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale)
+        return ref.paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, window=window)
     B, Hq, D = q.shape
     Hkv = k_cache.shape[1]
     _req(block_tables, torch.int32, "block_tables")
@@ -161,8 +162,8 @@ def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, o
         part_o = part_ml = None
     check(kernels().cfc_paged_decode_attention(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                                block_tables.data_ptr(), ctx_lens.data_ptr(), B, Hq, Hkv, D,
-                                               max_blocks, part_blocks, Pn, float(scale), _p(part_o), _p(part_ml),
-                                               out.data_ptr(), _stream(q)), "cfc_paged_decode_attention")
+                                               max_blocks, part_blocks, Pn, float(scale), int(window or 0), _p(part_o),
+                                               _p(part_ml), out.data_ptr(), _stream(q)), "cfc_paged_decode_attention")
     return out
 
 
@@ -195,10 +196,11 @@ def prefill_tiles(cu_q: list[int], tile: int = PREFILL_TILE_ROWS, ctx_lens: list
     return [t[1] for t in tiles], [t[2] for t in tiles]
 
 
-def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, tiles=None, out=None):
-    """q [T, Hq, D] (packed varlen); cu_q [S+1] int32; ctx_lens [S] int32 (cached + new)."""
+def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, tiles=None, out=None, window=0):
+    """q [T, Hq, D] (packed varlen); cu_q [S+1] int32; ctx_lens [S] int32 (cached + new);
+    ``window`` > 0: sliding-window attention (needs the GQA-packed kernel's G in {1, 2, 4, 8})."""
     if not q.is_cuda:
-        return ref.prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale)
+        return ref.prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, window=window)
     T, Hq, D = q.shape
     Hkv = k_cache.shape[1]
     rows = prefill_rows(Hq, Hkv)
@@ -211,7 +213,8 @@ def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, 
     check(kernels().cfc_prefill_attention(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                           block_tables.data_ptr(), cu_q.data_ptr(), ctx_lens.data_ptr(),
                                           tile_seq.data_ptr(), tile_q0.data_ptr(), tile_seq.numel(), rows, Hq, Hkv, D,
-                                          block_tables.shape[1], float(scale), out.data_ptr(), _stream(q)),
+                                          block_tables.shape[1], float(scale), int(window or 0), out.data_ptr(),
+                                          _stream(q)),
           "cfc_prefill_attention")
     return out
 

@@ -106,32 +106,37 @@ def gather_kv(k_cache, v_cache, block_table, n):
     return k[:n], v[:n]
 
 
-def _attend(q, k, v, scale, causal_offset=None):
-    """q [m, Hq, D], k/v [n, Hkv, D] -> [m, Hq, D] fp32 (GQA)."""
+def _attend(q, k, v, scale, causal_offset=None, window=0):
+    """q [m, Hq, D], k/v [n, Hkv, D] -> [m, Hq, D] fp32 (GQA).  ``window`` > 0: sliding-window
+    attention as HF Mistral masks it -- a query at position p sees keys k with p - window < k <= p."""
     Hq, Hkv = q.shape[1], k.shape[1]
     G = Hq // Hkv
     kk = k.float().repeat_interleave(G, 1)
     vv = v.float().repeat_interleave(G, 1)
     s = torch.einsum("mhd,nhd->hmn", q.float(), kk) * scale
-    if causal_offset is not None:
-        m, n = q.shape[0], k.shape[0]
-        pos = torch.arange(m, device=q.device)[:, None] + causal_offset
-        mask = torch.arange(n, device=q.device)[None, :] > pos
+    m, n = q.shape[0], k.shape[0]
+    if causal_offset is not None or window:
+        off = causal_offset if causal_offset is not None else n - m
+        pos = torch.arange(m, device=q.device)[:, None] + off
+        keys = torch.arange(n, device=q.device)[None, :]
+        mask = keys > pos
+        if window:
+            mask = mask | (keys <= pos - window)
         s = s.masked_fill(mask[None], float("-inf"))
     p = torch.softmax(s, -1)
     return torch.einsum("hmn,nhd->mhd", p, vv)
 
 
-def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale):
+def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, window=0):
     out = torch.empty_like(q)
     for b in range(q.shape[0]):
         n = int(ctx_lens[b])
         k, v = gather_kv(k_cache, v_cache, block_tables[b], n)
-        out[b] = _attend(q[b:b + 1], k, v, scale)[0].to(q.dtype)
+        out[b] = _attend(q[b:b + 1], k, v, scale, window=window)[0].to(q.dtype)
     return out
 
 
-def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale):
+def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, window=0):
     out = torch.empty_like(q)
     for s in range(len(cu_q) - 1):
         a, b = int(cu_q[s]), int(cu_q[s + 1])
@@ -139,7 +144,7 @@ def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale):
             continue
         n = int(ctx_lens[s])
         k, v = gather_kv(k_cache, v_cache, block_tables[s], n)
-        out[a:b] = _attend(q[a:b], k, v, scale, causal_offset=n - (b - a)).to(q.dtype)
+        out[a:b] = _attend(q[a:b], k, v, scale, causal_offset=n - (b - a), window=window).to(q.dtype)
     return out
 
 

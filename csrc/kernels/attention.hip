@@ -69,7 +69,7 @@ template <int G, bool NT>
 __global__ void __launch_bounds__(256) paged_decode_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, const int32_t* __restrict__ ctx_lens, float scale_log2, int Hkv,
-    int max_blocks, int part_blocks, int P, float* __restrict__ part_o, float* __restrict__ part_ml,
+    int max_blocks, int part_blocks, int P, int window, float* __restrict__ part_o, float* __restrict__ part_ml,
     uint16_t* __restrict__ out) {
   constexpr int D = 128;
   const int p = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
@@ -78,11 +78,16 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   const int Hq = Hkv * G;
   const int ctx = ctx_lens[b];
   const int nblk = (ctx + KV_BS - 1) / KV_BS;
+  // sliding window (window > 0): the query at position ctx-1 sees keys [ctx - window, ctx)
+  const int key_lo = window > 0 ? max(0, ctx - window) : 0;
+  const int blk_lo = key_lo / KV_BS;
   // part_blocks > 0: fixed-size partitions of the block table; <= 0: the sequence's OWN blocks
   // split into P near-equal ranges (balanced per sequence whatever its length -- no nearly empty
   // tail partitions, and P can stay small, so each workgroup streams a long run of KV)
-  const int blk0 = part_blocks > 0 ? p * part_blocks : (int)(((int64_t)p * nblk) / P);
-  const int blk1 = part_blocks > 0 ? min(nblk, blk0 + part_blocks) : (int)(((int64_t)(p + 1) * nblk) / P);
+  const int blk0 = part_blocks > 0 ? max(blk_lo, p * part_blocks)
+                                   : blk_lo + (int)(((int64_t)p * (nblk - blk_lo)) / P);
+  const int blk1 = part_blocks > 0 ? min(nblk, p * part_blocks + part_blocks)
+                                   : blk_lo + (int)(((int64_t)(p + 1) * (nblk - blk_lo)) / P);
 
   __shared__ float sm_o[4][D][17];
   __shared__ float sm_m[4][16], sm_l[4][16];
@@ -144,7 +149,7 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
       for (int i = 0; i < 4; ++i) {
         const int key = key0 + 16 * st + 4 * g + i;
         float v = s[st][i] * scale_log2;
-        v = key < ctx ? v : -INFINITY;
+        v = key < ctx && key >= key_lo ? v : -INFINITY;
         s[st][i] = v;
         tmax = fmaxf(tmax, v);
       }
@@ -648,7 +653,7 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
     const int32_t* __restrict__ block_tables, const int32_t* __restrict__ cu_q, const int32_t* __restrict__ ctx_lens,
     const int32_t* __restrict__ tile_seq, const int32_t* __restrict__ tile_q0, float scale_log2, int Hq, int Hkv,
-    int max_blocks, uint16_t* __restrict__ out) {
+    int max_blocks, int window, uint16_t* __restrict__ out) {
   constexpr int D = 128;
   constexpr int QR = 256 / G;      // query rows per tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -665,6 +670,8 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
   const int row_last = min(qs + QR - 1, q_len - 1);
   const int kend = pos_base + row_last + 1;         // keys [0, kend) are needed by this tile
   const int ntiles = (kend + PF_KT - 1) / PF_KT;
+  // sliding window: row at position p sees keys (p - window, p]; the tile's first row bounds it
+  const int kt_begin = window > 0 ? max(0, pos_base + qs - window + 1) / PF_KT : 0;
   const int32_t* bt = block_tables + (size_t)s * max_blocks;
 
   if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
@@ -724,10 +731,10 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
     for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
   float m = -INFINITY, l = 0.f;   // l: this lane's partial row sum (its 32 of every 64 keys)
 
-  gload(0);
-  lwrite(0, 0);
+  gload(kt_begin);
+  lwrite(kt_begin & 1, kt_begin);
   __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
+  for (int kt = kt_begin; kt < ntiles; ++kt) {
     const int cur = kt & 1;
     const bool more = kt + 1 < ntiles;
     if (more) gload(kt + 1);
@@ -735,7 +742,8 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
     const char* kb = smem + cur * 16384;
     const char* vb = smem + 32768 + cur * 16384;
     const int key0 = kt * PF_KT;
-    if (key0 <= wave_min_pos + 31) {     // else every key of the tile is after all of this wave's rows
+    const bool below = window > 0 && key0 + PF_KT - 1 <= wave_min_pos - window;  // all keys out of window
+    if (key0 <= wave_min_pos + 31 && !below) {     // else every key of the tile is masked for this wave
       f32x16_t sc[2];
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
@@ -752,6 +760,13 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
 #pragma unroll
           for (int r = 0; r < 16; ++r)
             if (key0 + 32 * hf + 8 * (r >> 2) + 4 * hi + (r & 3) > my_pos) sc[hf][r] = -INFINITY;
+      }
+      if (window > 0 && key0 <= wave_min_pos + 31 - window) {  // window edge: keys <= pos - window
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (key0 + 32 * hf + 8 * (r >> 2) + 4 * hi + (r & 3) <= my_pos - window) sc[hf][r] = -INFINITY;
       }
       float tmax = fmaxf(sc[0][0], sc[1][0]);
 #pragma unroll
@@ -944,14 +959,14 @@ __global__ void __launch_bounds__(256) encoder_attn_kernel(const uint16_t* __res
 // part_o / part_ml: fp32 workspaces of B*Hq*P*128 and B*Hq*P*2 floats (unused when P == 1).
 CFC_API int cfc_paged_decode_attention(const void* q, const void* k_cache, const void* v_cache,
                                        const int32_t* block_tables, const int32_t* ctx_lens, int B, int Hq, int Hkv,
-                                       int head_dim, int max_blocks, int part_blocks, int P, float scale,
+                                       int head_dim, int max_blocks, int part_blocks, int P, float scale, int window,
                                        float* part_o, float* part_ml, void* out, hipStream_t stream) {
-  if (head_dim != 128 || Hq % Hkv != 0 || B <= 0 || P <= 0) return -1;
+  if (head_dim != 128 || Hq % Hkv != 0 || B <= 0 || P <= 0 || window < 0) return -1;
   const int G = Hq / Hkv;
   dim3 grid(P, Hkv, B);
   const float sl2 = scale * LOG2E;
 #define DEC_ARGS (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, ctx_lens, sl2, \
-    Hkv, max_blocks, part_blocks, P, part_o, part_ml, (uint16_t*)out
+    Hkv, max_blocks, part_blocks, P, window, part_o, part_ml, (uint16_t*)out
   // nontemporal KV loads for large batches (B=128: 6.5 vs 5.9 TB/s; B=8: 3.8 vs 4.2 -- there the
   // plain loads win), profiles/decode_attn_partitions_r01.log; CFC_DECODE_NT=0/1 forces either
   static const int nt_env = [] { const char* e = getenv("CFC_DECODE_NT"); return e ? atoi(e) : -1; }();
@@ -990,26 +1005,29 @@ CFC_API int cfc_prefill_rows(int Hq, int Hkv) {
 CFC_API int cfc_prefill_attention(const void* q, const void* k_cache, const void* v_cache, const int32_t* block_tables,
                                   const int32_t* cu_q, const int32_t* ctx_lens, const int32_t* tile_seq,
                                   const int32_t* tile_q0, int n_tiles, int tile_rows, int Hq, int Hkv, int head_dim,
-                                  int max_blocks, float scale, void* out, hipStream_t stream) {
-  if (head_dim != 128 || Hkv <= 0 || Hq % Hkv != 0) return -1;
+                                  int max_blocks, float scale, int window, void* out, hipStream_t stream) {
+  if (head_dim != 128 || Hkv <= 0 || Hq % Hkv != 0 || window < 0) return -1;
   if (tile_rows != cfc_prefill_rows(Hq, Hkv)) return -2;     // tiles cut for another kernel
   if (n_tiles <= 0) return 0;
   const size_t lds = 65536;
   const int G = Hq / Hkv;
 #define PF_ARGS (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, cu_q, ctx_lens, \
     tile_seq, tile_q0, scale * LOG2E, Hq, Hkv, max_blocks, (uint16_t*)out
+#define PF5_ARGS (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, cu_q, ctx_lens, \
+    tile_seq, tile_q0, scale * LOG2E, Hq, Hkv, max_blocks, window, (uint16_t*)out
   if (tile_rows != PF_ROWS || (G * tile_rows == 256 && prefill_variant() == 5)) {
     // 5: GQA-packed 8-wave kernel (default)
     const dim3 grid(n_tiles, Hkv);
     switch (G) {
-      case 1: prefill_gqa_kernel<1><<<grid, 512, lds, stream>>>(PF_ARGS); break;
-      case 2: prefill_gqa_kernel<2><<<grid, 512, lds, stream>>>(PF_ARGS); break;
-      case 4: prefill_gqa_kernel<4><<<grid, 512, lds, stream>>>(PF_ARGS); break;
-      case 8: prefill_gqa_kernel<8><<<grid, 512, lds, stream>>>(PF_ARGS); break;
+      case 1: prefill_gqa_kernel<1><<<grid, 512, lds, stream>>>(PF5_ARGS); break;
+      case 2: prefill_gqa_kernel<2><<<grid, 512, lds, stream>>>(PF5_ARGS); break;
+      case 4: prefill_gqa_kernel<4><<<grid, 512, lds, stream>>>(PF5_ARGS); break;
+      case 8: prefill_gqa_kernel<8><<<grid, 512, lds, stream>>>(PF5_ARGS); break;
       default: return -3;
     }
     return CFC_CHECK_LAUNCH();
   }
+  if (window > 0) return -4;     // sliding window: GQA-packed kernel only
   // legacy single-head 128-row kernels: 0 = v3 <=128 VGPRs (2 workgroups / CU); 1 = v3 <=256 VGPRs;
   // 2/3 = v4 (32x32 MFMA, 2 / 1 WG per CU)
   const int variant = prefill_variant();
@@ -1018,6 +1036,7 @@ CFC_API int cfc_prefill_attention(const void* q, const void* k_cache, const void
   else if (variant == 3) prefill_paged_kernel_v4<1><<<dim3(n_tiles, Hq), 256, lds, stream>>>(PF_ARGS);
   else prefill_paged_kernel<4><<<dim3(n_tiles, Hq), 512, lds, stream>>>(PF_ARGS);
 #undef PF_ARGS
+#undef PF5_ARGS
   return CFC_CHECK_LAUNCH();
 }
 

@@ -125,3 +125,22 @@ def test_v_runs_split_on_block_and_offset_breaks():
     full = K.v_runs([5 * 32 + i for i in range(32)] + [6 * 32 + i for i in range(32)])
     assert full.tolist() == [[0, 32, 5, 0], [32, 32, 6, 0]]
     assert K.v_runs([]).shape == (0, 4)
+
+
+def test_reference_sliding_window_is_attention_over_the_last_keys():
+    import math
+
+    from copilot_for_consensus_amd.ops import reference as R
+    g = torch.Generator().manual_seed(0)
+    q = torch.randn(5, 4, 16, generator=g)
+    k = torch.randn(40, 2, 16, generator=g)
+    v = torch.randn(40, 2, 16, generator=g)
+    W = 7
+    got = R._attend(q, k, v, 1 / math.sqrt(16), causal_offset=35, window=W)
+    for i in range(5):
+        p = 35 + i
+        want = R._attend(q[i:i + 1], k[p - W + 1:p + 1], v[p - W + 1:p + 1], 1 / math.sqrt(16))
+        assert torch.allclose(got[i:i + 1], want, atol=1e-5)
+    # decode form: the last query sees the last W keys
+    dec = R._attend(q[:1], k, v, 0.25, window=W)
+    assert torch.allclose(dec, R._attend(q[:1], k[-W:], v[-W:], 0.25), atol=1e-5)

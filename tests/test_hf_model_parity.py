@@ -59,6 +59,9 @@ def _hf_decoder(kind, tmp_path_factory):
     if kind == "mistral":
         cfg = transformers.MistralConfig(rope_theta=1e6, sliding_window=None, **common)
         model = transformers.MistralForCausalLM(cfg)
+    elif kind == "mistral_swa":    # Mistral v0.1-style sliding-window attention (window << prompt)
+        cfg = transformers.MistralConfig(rope_theta=1e4, sliding_window=24, **common)
+        model = transformers.MistralForCausalLM(cfg)
     elif kind == "llama":
         cfg = transformers.LlamaConfig(rope_theta=5e5, **common)
         model = transformers.LlamaForCausalLM(cfg)
@@ -73,7 +76,7 @@ def _hf_decoder(kind, tmp_path_factory):
     return d, model
 
 
-@pytest.fixture(scope="module", params=["mistral", "llama", "llama31"])
+@pytest.fixture(scope="module", params=["mistral", "mistral_swa", "llama", "llama31"])
 def decoder_dir(request, tmp_path_factory):
     return _hf_decoder(request.param, tmp_path_factory)
 

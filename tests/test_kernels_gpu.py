@@ -136,6 +136,41 @@ def test_paged_decode(G, part_blocks):
     _close(out, ref, 2e-2)
 
 
+@pytest.mark.parametrize("G", [1, 4])
+@pytest.mark.parametrize("part_blocks", [4, -1, -3])
+@pytest.mark.parametrize("window", [1, 33, 100])
+def test_paged_decode_sliding_window(G, part_blocks, window):
+    Hkv, D = 2, 128
+    Hq = Hkv * G
+    ctx = [1, 31, 32, 33, 100, 517, 2049, 64]
+    kc, vc, bt = _fill_cache(ctx, Hkv, D)
+    q = torch.randn(len(ctx), Hq, D).bfloat16()
+    cl = torch.tensor(ctx, dtype=torch.int32)
+    ref = R.paged_decode_attention(q, kc, vc, bt, cl, 1 / math.sqrt(D), window=window)
+    out = K.paged_decode_attention(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), cl.to(DEV), 1 / math.sqrt(D),
+                                   part_blocks=part_blocks, window=window)
+    _close(out, ref, 2e-2)
+
+
+@pytest.mark.parametrize("G", [1, 4, 8])
+@pytest.mark.parametrize("window", [1, 40, 100])
+def test_prefill_attention_sliding_window(G, window):
+    Hkv, D = 2, 128
+    Hq = Hkv * G
+    seqs = [(1, 1), (17, 17), (200, 200), (70, 300), (129, 1000), (600, 600)]
+    kc, vc, bt = _fill_cache([c for _, c in seqs], Hkv, D)
+    cu = [0]
+    for qn, _ in seqs:
+        cu.append(cu[-1] + qn)
+    q = torch.randn(cu[-1], Hq, D).bfloat16()
+    cu_t = torch.tensor(cu, dtype=torch.int32)
+    cl = torch.tensor([c for _, c in seqs], dtype=torch.int32)
+    ref = R.prefill_attention(q, kc, vc, bt, cu_t, cl, 1 / math.sqrt(D), window=window)
+    out = K.prefill_attention(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), cu_t.to(DEV), cl.to(DEV),
+                              1 / math.sqrt(D), window=window)
+    _close(out, ref, 2e-2)
+
+
 @pytest.mark.parametrize("G", [1, 2, 4, 8])
 def test_prefill_attention(G):
     Hkv, D = 2, 128
