@@ -38,6 +38,8 @@ def parse_args(argv=None):
     ap.add_argument("--max-new", type=int, default=512, help="generated tokens per summary (llama.cpp n_predict)")
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--prefill-tokens", type=int, default=16384)
+    ap.add_argument("--kv-dtype", choices=["bf16", "fp8"], default="bf16",
+                    help="KV-cache storage; fp8 (e4m3fn) is an opt-in precision trade-off, not the headline")
     ap.add_argument("--llm-only", action="store_true", help="skip the CPU/encoder/kNN stages (diagnostic)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
@@ -62,7 +64,7 @@ def main(argv=None):
     # TP groups of args.tp consecutive ranks (one engine per group), DP across groups
     groups = make_groups(env, args.tp)
     pipe = BenchPipeline(model=args.model, encoder=args.encoder, device=dev, threads_per_step=args.threads_per_gpu,
-                         max_new_tokens=args.max_new, tp=args.tp, prefill_tokens=args.prefill_tokens,
+                         max_new_tokens=args.max_new, tp=args.tp, prefill_tokens=args.prefill_tokens, kv_dtype=args.kv_dtype,
                          llm_only=args.llm_only, use_graph=not args.no_graph,
                          seed=args.seed + 7919 * groups.dp_rank, groups=groups if args.tp > 1 else None)
 
@@ -128,6 +130,7 @@ def main(argv=None):
                 "global_batch": args.threads_per_gpu * groups.dp_size,
                 "seq_len": round(prompt_tokens / max(threads, 1)),
                 "max_new_tokens": args.max_new,
+                "kv_cache": "bf16" if args.kv_dtype == "bf16" else "fp8_e4m3fn (opt-in, reduced-precision KV)",
                 "parallelism": f"dp{groups.dp_size}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
                 "pipeline": "llm-only" if args.llm_only else "parse+chunk+embed+knn+select+prefill+decode",
             },

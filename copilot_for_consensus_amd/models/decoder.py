@@ -298,9 +298,9 @@ class DecoderModel:
             h, residual = self._layer_pre(i, x, residual)
             qkv = F.linear(h, lw["qkv"])
             q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
-                                cfg.head_dim, runs=v_runs)
+                                cfg.head_dim, runs=v_runs, k_scale=kv.k_scale, v_scale=kv.v_scale)
             attn = K.prefill_attention(q, kv.k[i], kv.v[i], block_tables, cu_q, ctx_lens, self.scale, tiles=tiles,
-                                       window=self.window)
+                                       window=self.window, k_scale=kv.k_scale, v_scale=kv.v_scale)
             o = self._all_reduce(F.linear(attn.view(attn.shape[0], -1), lw["o"]))
             x = self._mlp(i, o, residual)
         if last_idx is not None:
@@ -326,9 +326,10 @@ class DecoderModel:
             h, residual = self._layer_pre(i, x, residual)
             qkv = F.linear(h, lw["qkv"])
             q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
-                                cfg.head_dim)
+                                cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
             attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
-                                            part_blocks=part_blocks, workspace=attn_workspace, window=self.window)
+                                            part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
+                                            k_scale=kv.k_scale, v_scale=kv.v_scale)
             o = self._all_reduce(F.linear(attn.view(B, -1), lw["o"]))
             x = self._mlp(i, o, residual)
         return K.rmsnorm(x, w.final_norm, cfg.rms_eps, residual=residual)
@@ -346,9 +347,10 @@ class DecoderModel:
             lw = w.layers[i]
             qkv = K.skinny_linear(h, lw["qkv"])
             q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
-                                cfg.head_dim)
+                                cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
             attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
-                                            part_blocks=part_blocks, workspace=attn_workspace, window=self.window)
+                                            part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
+                                            k_scale=kv.k_scale, v_scale=kv.v_scale)
             h = K.skinny_linear_residual_rmsnorm(attn.view(B, -1), lw["o"], residual, lw["mlp_norm"], eps)
             a = K.skinny_swiglu(h, lw["gate_up"])
             nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm
@@ -368,9 +370,10 @@ class DecoderModel:
             lw = w.layers[i]
             qkv = F.linear(h, lw["qkv"])
             q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
-                                cfg.head_dim)
+                                cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
             attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
-                                            part_blocks=part_blocks, workspace=attn_workspace, window=self.window)
+                                            part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
+                                            k_scale=kv.k_scale, v_scale=kv.v_scale)
             h = K.lib_splitk_linear_residual_rmsnorm(attn.view(B, -1), lw["o"], s_o, residual, lw["mlp_norm"], eps)
             a = K.silu_mul(F.linear(h, lw["gate_up"]), interleaved=w.gate_up_interleaved)
             nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm

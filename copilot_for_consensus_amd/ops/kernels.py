@@ -102,11 +102,17 @@ def v_runs(slots) -> "np.ndarray":
     return np.stack([starts, ends - starts, blk[starts], off[starts]], 1).astype(np.int32)
 
 
-def rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D, q_out=None, runs=None):
+def _fp8(cache) -> bool:
+    return cache.dtype == torch.float8_e4m3fn
+
+
+def rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D, q_out=None, runs=None,
+                  k_scale=1.0, v_scale=1.0):
     """RoPE on q/k + paged K/V cache write.  ``runs`` (device int32 [R, 4] from :func:`v_runs`):
-    write V per whole cache block (prefill); without it V is written per token (decode)."""
+    write V per whole cache block (prefill); without it V is written per token (decode).
+    float8_e4m3fn caches store K / k_scale and V / v_scale."""
     if not qkv.is_cuda:
-        q = ref.rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D)
+        q = ref.rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D, k_scale, v_scale)
         if q_out is not None:
             q_out.view_as(q).copy_(q)
             return q_out
@@ -120,9 +126,20 @@ def rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D, 
     if runs is not None:
         _req(runs, torch.int32, "runs")
     q_out = torch.empty(T, Hq, D, dtype=qkv.dtype, device=qkv.device) if q_out is None else q_out
+    write_v = 0 if runs is not None else 1
+    if _fp8(k_cache):
+        check(kernels().cfc_rope_kv_write_fp8(qkv.data_ptr(), positions.data_ptr(), slots.data_ptr(),
+                                              cos_sin.data_ptr(), q_out.data_ptr(), k_cache.data_ptr(),
+                                              v_cache.data_ptr(), T, Hq, Hkv, D, write_v, 1.0 / k_scale,
+                                              1.0 / v_scale, _stream(qkv)), "cfc_rope_kv_write_fp8")
+        if runs is not None:
+            check(kernels().cfc_v_cache_write_runs_fp8(qkv.data_ptr(), runs.data_ptr(), runs.shape[0],
+                                                       v_cache.data_ptr(), Hq, Hkv, D, 1.0 / v_scale, _stream(qkv)),
+                  "cfc_v_cache_write_runs_fp8")
+        return q_out
     check(kernels().cfc_rope_kv_write(qkv.data_ptr(), positions.data_ptr(), slots.data_ptr(), cos_sin.data_ptr(),
                                       q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), T, Hq, Hkv, D,
-                                      0 if runs is not None else 1, _stream(qkv)), "cfc_rope_kv_write")
+                                      write_v, _stream(qkv)), "cfc_rope_kv_write")
     if runs is not None:
         check(kernels().cfc_v_cache_write_runs(qkv.data_ptr(), runs.data_ptr(), runs.shape[0], v_cache.data_ptr(),
                                                Hq, Hkv, D, _stream(qkv)), "cfc_v_cache_write_runs")
@@ -134,14 +151,15 @@ def decode_partitions(max_ctx: int, part_blocks: int) -> int:
 
 
 def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out=None, part_blocks=16,
-                           num_partitions=None, workspace=None, window=0):
+                           num_partitions=None, workspace=None, window=0, k_scale=1.0, v_scale=1.0):
     """q [B, Hq, D]; caches [nblk, Hkv, 32, D] / [nblk, Hkv, D, 32]; returns [B, Hq, D].
 
     ``part_blocks`` > 0: split-KV partitions of that many blocks; ``part_blocks`` = -P: P balanced
     partitions of each sequence's own context (what the engine uses).  ``window`` > 0: sliding-window
     attention over the last ``window`` keys (Mistral v0.1)."""
     if not q.is_cuda:
-        return ref.paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, window=window)
+        return ref.paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, window=window,
+                                          k_scale=k_scale, v_scale=v_scale)
     B, Hq, D = q.shape
     Hkv = k_cache.shape[1]
     _req(block_tables, torch.int32, "block_tables")
@@ -160,6 +178,13 @@ def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, o
         part_ml = workspace[B * Hq * Pn * D:]
     else:
         part_o = part_ml = None
+    if _fp8(k_cache):
+        check(kernels().cfc_paged_decode_attention_fp8(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                                                       block_tables.data_ptr(), ctx_lens.data_ptr(), B, Hq, Hkv, D,
+                                                       max_blocks, part_blocks, Pn, float(scale), int(window or 0),
+                                                       float(k_scale), float(v_scale), _p(part_o), _p(part_ml),
+                                                       out.data_ptr(), _stream(q)), "cfc_paged_decode_attention_fp8")
+        return out
     check(kernels().cfc_paged_decode_attention(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                                block_tables.data_ptr(), ctx_lens.data_ptr(), B, Hq, Hkv, D,
                                                max_blocks, part_blocks, Pn, float(scale), int(window or 0), _p(part_o),
@@ -196,11 +221,13 @@ def prefill_tiles(cu_q: list[int], tile: int = PREFILL_TILE_ROWS, ctx_lens: list
     return [t[1] for t in tiles], [t[2] for t in tiles]
 
 
-def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, tiles=None, out=None, window=0):
+def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, tiles=None, out=None, window=0,
+                      k_scale=1.0, v_scale=1.0):
     """q [T, Hq, D] (packed varlen); cu_q [S+1] int32; ctx_lens [S] int32 (cached + new);
     ``window`` > 0: sliding-window attention (needs the GQA-packed kernel's G in {1, 2, 4, 8})."""
     if not q.is_cuda:
-        return ref.prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, window=window)
+        return ref.prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, window=window,
+                                     k_scale=k_scale, v_scale=v_scale)
     T, Hq, D = q.shape
     Hkv = k_cache.shape[1]
     rows = prefill_rows(Hq, Hkv)
@@ -210,6 +237,14 @@ def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, 
                  torch.tensor(q0, dtype=torch.int32, device=q.device))
     tile_seq, tile_q0 = tiles
     out = torch.empty_like(q) if out is None else out
+    if _fp8(k_cache):
+        check(kernels().cfc_prefill_attention_fp8(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                                                  block_tables.data_ptr(), cu_q.data_ptr(), ctx_lens.data_ptr(),
+                                                  tile_seq.data_ptr(), tile_q0.data_ptr(), tile_seq.numel(), rows, Hq,
+                                                  Hkv, D, block_tables.shape[1], float(scale), int(window or 0),
+                                                  float(k_scale), float(v_scale), out.data_ptr(), _stream(q)),
+              "cfc_prefill_attention_fp8")
+        return out
     check(kernels().cfc_prefill_attention(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                           block_tables.data_ptr(), cu_q.data_ptr(), ctx_lens.data_ptr(),
                                           tile_seq.data_ptr(), tile_q0.data_ptr(), tile_seq.numel(), rows, Hq, Hkv, D,

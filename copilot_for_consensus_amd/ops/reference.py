@@ -70,7 +70,14 @@ def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None, llama3_
     return torch.stack([ang.cos(), ang.sin()], -1).float().to(device)
 
 
-def rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D):
+def _to_cache(x, cache, scale):
+    """Value as stored in a cache of ``cache.dtype`` (fp8 e4m3fn caches hold x / scale, clamped)."""
+    if cache.dtype == torch.float8_e4m3fn:
+        return (x.float() / scale).clamp(-448.0, 448.0).to(torch.float8_e4m3fn)
+    return x.to(cache.dtype)
+
+
+def rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D, k_scale=1.0, v_scale=1.0):
     """Apply RoPE to q/k of the fused projection, write k/v into the paged cache. Returns q."""
     T = qkv.shape[0]
     x = qkv.float().view(T, Hq + 2 * Hkv, D)
@@ -91,18 +98,21 @@ def rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D):
         if s < 0:
             continue
         blk, off = divmod(s, KV_BLOCK)
-        k_cache[blk, :, off, :] = k[t]
-        v_cache[blk, :, :, int(perm[off])] = v[t]
+        k_cache[blk, :, off, :] = _to_cache(k[t], k_cache, k_scale)
+        v_cache[blk, :, :, int(perm[off])] = _to_cache(v[t], v_cache, v_scale)
     return q
 
 
-def gather_kv(k_cache, v_cache, block_table, n):
-    """Contiguous K, V [n, Hkv, D] of one sequence from the paged caches."""
+def gather_kv(k_cache, v_cache, block_table, n, k_scale=1.0, v_scale=1.0):
+    """Contiguous K, V [n, Hkv, D] of one sequence from the paged caches (fp8 caches dequantized
+    to fp32 with their scales)."""
     perm = v_slot_perm(k_cache.device)
     nb = (n + KV_BLOCK - 1) // KV_BLOCK
     blocks = block_table[:nb].long()
     k = k_cache[blocks].permute(0, 2, 1, 3).reshape(nb * KV_BLOCK, k_cache.shape[1], k_cache.shape[3])
     v = v_cache[blocks][..., perm].permute(0, 3, 1, 2).reshape(nb * KV_BLOCK, v_cache.shape[1], v_cache.shape[2])
+    if k_cache.dtype == torch.float8_e4m3fn:
+        k, v = k.float() * k_scale, v.float() * v_scale
     return k[:n], v[:n]
 
 
@@ -127,23 +137,23 @@ def _attend(q, k, v, scale, causal_offset=None, window=0):
     return torch.einsum("hmn,nhd->mhd", p, vv)
 
 
-def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, window=0):
+def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, window=0, k_scale=1.0, v_scale=1.0):
     out = torch.empty_like(q)
     for b in range(q.shape[0]):
         n = int(ctx_lens[b])
-        k, v = gather_kv(k_cache, v_cache, block_tables[b], n)
+        k, v = gather_kv(k_cache, v_cache, block_tables[b], n, k_scale, v_scale)
         out[b] = _attend(q[b:b + 1], k, v, scale, window=window)[0].to(q.dtype)
     return out
 
 
-def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, window=0):
+def prefill_attention(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, scale, window=0, k_scale=1.0, v_scale=1.0):
     out = torch.empty_like(q)
     for s in range(len(cu_q) - 1):
         a, b = int(cu_q[s]), int(cu_q[s + 1])
         if b == a:
             continue
         n = int(ctx_lens[s])
-        k, v = gather_kv(k_cache, v_cache, block_tables[s], n)
+        k, v = gather_kv(k_cache, v_cache, block_tables[s], n, k_scale, v_scale)
         out[a:b] = _attend(q[a:b], k, v, scale, causal_offset=n - (b - a), window=window).to(q.dtype)
     return out
 

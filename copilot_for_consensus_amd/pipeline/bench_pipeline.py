@@ -27,7 +27,7 @@ class StepResult:
 class BenchPipeline:
     def __init__(self, model="mistral-7b", encoder="minilm-l6", device="cuda", threads_per_step=128,
                  max_new_tokens=512, tp=1, prefill_tokens=16384, llm_only=False, use_graph=True, seed=0,
-                 index_prefill=1_000_000, groups=None):
+                 index_prefill=1_000_000, groups=None, kv_dtype="bf16"):
         from ..models.decoder import DecoderModel, DecoderWeights, get_config
         from ..runtime.engine import LLMEngine
         from ..runtime.kv_cache import PagedKVCache, blocks_needed
@@ -56,7 +56,8 @@ class BenchPipeline:
         # KV budget: every thread of a step at the longest prompt we generate (3k) + max_new, x1.1
         max_prompt = 4096
         nblk = int(1.1 * threads_per_step * blocks_needed(max_prompt + max_new_tokens)) + 64
-        self.kv = PagedKVCache(self.cfg.layers, nblk, w.kv_heads, self.cfg.head_dim, self.device)
+        kvd = {"bf16": torch.bfloat16, "fp8": torch.float8_e4m3fn}[kv_dtype]
+        self.kv = PagedKVCache(self.cfg.layers, nblk, w.kv_heads, self.cfg.head_dim, self.device, dtype=kvd)
         self.engine = LLMEngine(self.model, self.kv, max_prefill_tokens=prefill_tokens, use_graph=use_graph)
         self.rag = None
         self.side_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None

@@ -71,8 +71,18 @@ class BlockPool:
 
 
 class PagedKVCache:
-    def __init__(self, layers: int, num_blocks: int, kv_heads: int, head_dim: int, device, dtype=torch.bfloat16):
+    """K [layers][blocks, kv_heads, 32, D] and V^T [layers][blocks, kv_heads, D, 32] (slot-permuted).
+
+    ``dtype`` bf16 (default) or ``torch.float8_e4m3fn``: the FP8 cache halves the bytes the decode
+    attention streams; it holds K / ``k_scale`` and V / ``v_scale`` (clamped to +-448) and the
+    kernels scale back.  Opt-in: it is a precision trade-off, not the default."""
+
+    def __init__(self, layers: int, num_blocks: int, kv_heads: int, head_dim: int, device, dtype=torch.bfloat16,
+                 k_scale: float = 1.0, v_scale: float = 1.0):
+        if dtype not in (torch.bfloat16, torch.float8_e4m3fn):
+            raise ValueError(f"KV cache dtype {dtype} not supported (bfloat16 or float8_e4m3fn)")
         self.layers, self.num_blocks, self.kv_heads, self.head_dim = layers, num_blocks, kv_heads, head_dim
+        self.dtype, self.k_scale, self.v_scale = dtype, float(k_scale), float(v_scale)
         self.device = torch.device(device)
         # zero-initialised: slots of a partially filled block are read (then masked) by the kernels
         self._k = torch.zeros(layers, num_blocks, kv_heads, KV_BLOCK, head_dim, dtype=dtype, device=self.device)

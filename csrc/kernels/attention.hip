@@ -65,12 +65,35 @@ __device__ __forceinline__ uint4 kv_load(const uint16_t* p) {
   }
 }
 
-template <int G, bool NT>
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+// 8-byte load of 8 fp8 KV values (the FP8 cache's fragment)
+template <bool NT>
+__device__ __forceinline__ uint2 kv_load8(const uint8_t* p) {
+  if constexpr (NT) {
+    const u32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p));
+    return make_uint2(v.x, v.y);
+  } else {
+    return *reinterpret_cast<const uint2*>(p);
+  }
+}
+
+// Raw KV fragment as loaded (bf16: 16 B; fp8: 8 B) and its bf16x8 MFMA operand.  The fp8 ->
+// bf16 conversion happens at the MFMA, so a prefetched block's loads stay in flight.
+template <bool F8> struct KvFrag { typedef uint4 raw; };
+template <> struct KvFrag<true> { typedef uint2 raw; };
+__device__ __forceinline__ bf16x8_t kv_operand(uint4 r) { return as_bf16x8(r); }
+__device__ __forceinline__ bf16x8_t kv_operand(uint2 r) { return as_bf16x8(fp8x8_to_bf16x8(r)); }
+
+template <int G, bool NT, bool F8 = false>
 __global__ void __launch_bounds__(256) paged_decode_kernel(
-    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    const uint16_t* __restrict__ q, const void* __restrict__ kc, const void* __restrict__ vc,
     const int32_t* __restrict__ block_tables, const int32_t* __restrict__ ctx_lens, float scale_log2, int Hkv,
-    int max_blocks, int part_blocks, int P, int window, float* __restrict__ part_o, float* __restrict__ part_ml,
-    uint16_t* __restrict__ out) {
+    int max_blocks, int part_blocks, int P, int window, float v_scale, float* __restrict__ part_o,
+    float* __restrict__ part_ml, uint16_t* __restrict__ out) {
+  // F8: kc / vc hold e4m3 of K / k_scale and V / v_scale; k_scale is folded into scale_log2 by the
+  // host, v_scale multiplies the output here
+  typedef typename KvFrag<F8>::raw Raw;
   constexpr int D = 128;
   const int p = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -112,25 +135,27 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   const int32_t* bt = block_tables + (size_t)b * max_blocks;
   const size_t head_stride = (size_t)KV_BS * D;  // elements per (block, kv-head)
 
-  uint4 kr[8], vr[8];
-  auto load_blk = [&](int bi, uint4* kk, uint4* vv) {
+  Raw kr[8], vr[8];
+  auto ld = [&](const void* base, size_t e) -> Raw {
+    if constexpr (F8) return kv_load8<NT>(reinterpret_cast<const uint8_t*>(base) + e);
+    else return kv_load<NT>(reinterpret_cast<const uint16_t*>(base) + e);
+  };
+  auto load_blk = [&](int bi, Raw* kk, Raw* vv) {
     const size_t base = ((size_t)bt[bi] * Hkv + h) * head_stride;
-    const uint16_t* kb = kc + base;
-    const uint16_t* vb = vc + base;
 #pragma unroll
     for (int st = 0; st < 2; ++st)
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        kk[st * 4 + c] = kv_load<NT>(kb + (16 * st + col) * D + 32 * c + 8 * g);
+        kk[st * 4 + c] = ld(kc, base + (16 * st + col) * D + 32 * c + 8 * g);
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt)
-      vv[dt] = kv_load<NT>(vb + (16 * dt + col) * KV_BS + 8 * g);
+      vv[dt] = ld(vc, base + (16 * dt + col) * KV_BS + 8 * g);
   };
 
   int bi = blk0 + w;
   if (bi < blk1) load_blk(bi, kr, vr);
   for (; bi < blk1; bi += 4) {
-    uint4 kn[8], vn[8];
+    Raw kn[8], vn[8];
     const bool more = bi + 4 < blk1;
     if (more) load_blk(bi + 4, kn, vn);
 
@@ -139,7 +164,7 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
     for (int st = 0; st < 2; ++st) {
       s[st] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < 4; ++c) s[st] = mfma16(as_bf16x8(kr[st * 4 + c]), qf[c], s[st]);
+      for (int c = 0; c < 4; ++c) s[st] = mfma16(kv_operand(kr[st * 4 + c]), qf[c], s[st]);
     }
     const int key0 = bi * KV_BS;
     float tmax = -INFINITY;
@@ -170,7 +195,7 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) {
       o[dt] *= alpha;
-      o[dt] = mfma16(as_bf16x8(vr[dt]), pf, o[dt]);
+      o[dt] = mfma16(kv_operand(vr[dt]), pf, o[dt]);
     }
     if (more) {
 #pragma unroll
@@ -201,6 +226,7 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
       }
     }
     const int head = h * G + qh;
+    O *= v_scale;
     if (P == 1) {
       out[((size_t)b * Hq + head) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
     } else {
@@ -648,12 +674,14 @@ __device__ __forceinline__ float pair_sum(float x) {
 }
 __device__ __forceinline__ int v5_off(int d, int c) { return d * 128 + ((c ^ ((d >> 1) & 7) ^ ((d & 1) << 2)) << 4); }
 
-template <int G>
+template <int G, bool F8 = false>
 __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
-    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    const uint16_t* __restrict__ q, const void* __restrict__ kc, const void* __restrict__ vc,
     const int32_t* __restrict__ block_tables, const int32_t* __restrict__ cu_q, const int32_t* __restrict__ ctx_lens,
     const int32_t* __restrict__ tile_seq, const int32_t* __restrict__ tile_q0, float scale_log2, int Hq, int Hkv,
-    int max_blocks, int window, uint16_t* __restrict__ out) {
+    int max_blocks, int window, float v_scale, uint16_t* __restrict__ out) {
+  // F8: e4m3 caches (K / k_scale folded into scale_log2 by the host, V / v_scale rescaled at the
+  // output); tiles are widened to bf16 at the LDS write, so the MFMA loop is the bf16 one
   constexpr int D = 128;
   constexpr int QR = 256 / G;      // query rows per tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -707,21 +735,40 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
   uint4 ks0, ks1, vs0, vs1;     // named (not an array): an array here is kept in scratch
   auto gload = [&](int kt) {
     const int b0 = bt[min(2 * kt, nb_need - 1)], b1 = bt[min(2 * kt + 1, nb_need - 1)];
-    const size_t base0 = ((size_t)b0 * Hkv + hk) * (KV_BS * D) + 8 * tid;
-    const size_t base1 = ((size_t)b1 * Hkv + hk) * (KV_BS * D) + 8 * tid;
-    ks0 = *reinterpret_cast<const uint4*>(kc + base0);
-    vs0 = *reinterpret_cast<const uint4*>(vc + base0);
-    ks1 = *reinterpret_cast<const uint4*>(kc + base1);
-    vs1 = *reinterpret_cast<const uint4*>(vc + base1);
+    if constexpr (F8) {
+      // 8 KB of K and 8 KB of V per tile: one 16-B piece of each per thread; block = tid >> 8
+      const size_t base = ((size_t)(tid >> 8 ? b1 : b0) * Hkv + hk) * (KV_BS * D) + 16 * (tid & 255);
+      ks0 = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(kc) + base);
+      vs0 = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(vc) + base);
+    } else {
+      const size_t base0 = ((size_t)b0 * Hkv + hk) * (KV_BS * D) + 8 * tid;
+      const size_t base1 = ((size_t)b1 * Hkv + hk) * (KV_BS * D) + 8 * tid;
+      ks0 = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(kc) + base0);
+      vs0 = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(vc) + base0);
+      ks1 = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(kc) + base1);
+      vs1 = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(vc) + base1);
+    }
   };
   auto lwrite = [&](int buf, int kt) {
     char* kb = smem + buf * 16384;
     char* vb = smem + 32768 + buf * 16384;
-    *reinterpret_cast<uint4*>(kb + k_lds_off(tid >> 4, tid & 15)) = ks0;
-    *reinterpret_cast<uint4*>(kb + k_lds_off((tid >> 4) + 32, tid & 15)) = ks1;
     const bool z0 = kt * PF_KT >= kend, z1 = kt * PF_KT + KV_BS >= kend;
-    *reinterpret_cast<uint4*>(vb + v5_off((tid >> 2) & 127, tid & 3)) = z0 ? make_uint4(0, 0, 0, 0) : vs0;
-    *reinterpret_cast<uint4*>(vb + v5_off((tid >> 2) & 127, 4 + (tid & 3))) = z1 ? make_uint4(0, 0, 0, 0) : vs1;
+    if constexpr (F8) {
+      const int b = tid >> 8, e = tid & 255;
+      const int key = (e >> 3) + 32 * b, ch = 2 * (e & 7);          // 16 d values = bf16 chunks ch, ch+1
+      *reinterpret_cast<uint4*>(kb + k_lds_off(key, ch)) = fp8x8_to_bf16x8(make_uint2(ks0.x, ks0.y));
+      *reinterpret_cast<uint4*>(kb + k_lds_off(key, ch + 1)) = fp8x8_to_bf16x8(make_uint2(ks0.z, ks0.w));
+      const int d = e >> 1, c = 4 * b + 2 * (e & 1);                  // 16 slots = cache chunks c, c+1
+      const bool z = b ? z1 : z0;
+      const uint4 zero = make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(vb + v5_off(d, c)) = z ? zero : fp8x8_to_bf16x8(make_uint2(vs0.x, vs0.y));
+      *reinterpret_cast<uint4*>(vb + v5_off(d, c + 1)) = z ? zero : fp8x8_to_bf16x8(make_uint2(vs0.z, vs0.w));
+    } else {
+      *reinterpret_cast<uint4*>(kb + k_lds_off(tid >> 4, tid & 15)) = ks0;
+      *reinterpret_cast<uint4*>(kb + k_lds_off((tid >> 4) + 32, tid & 15)) = ks1;
+      *reinterpret_cast<uint4*>(vb + v5_off((tid >> 2) & 127, tid & 3)) = z0 ? make_uint4(0, 0, 0, 0) : vs0;
+      *reinterpret_cast<uint4*>(vb + v5_off((tid >> 2) & 127, 4 + (tid & 3))) = z1 ? make_uint4(0, 0, 0, 0) : vs1;
+    }
   };
 
   f32x16_t o[4];
@@ -811,7 +858,7 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
 
   l = pair_sum(l);
   if (my_row < q_len) {
-    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const float inv = l > 0.f ? v_scale / l : 0.f;
     uint16_t* orow = out + ((size_t)(q_begin + my_row) * Hq + hq) * D;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
@@ -957,24 +1004,25 @@ __global__ void __launch_bounds__(256) encoder_attn_kernel(const uint16_t* __res
 
 // q: [B, Hq, 128] bf16; caches per layer as documented above; out: [B, Hq, 128] bf16.
 // part_o / part_ml: fp32 workspaces of B*Hq*P*128 and B*Hq*P*2 floats (unused when P == 1).
-CFC_API int cfc_paged_decode_attention(const void* q, const void* k_cache, const void* v_cache,
-                                       const int32_t* block_tables, const int32_t* ctx_lens, int B, int Hq, int Hkv,
-                                       int head_dim, int max_blocks, int part_blocks, int P, float scale, int window,
-                                       float* part_o, float* part_ml, void* out, hipStream_t stream) {
+template <bool F8>
+static int launch_paged_decode(const void* q, const void* k_cache, const void* v_cache, const int32_t* block_tables,
+                               const int32_t* ctx_lens, int B, int Hq, int Hkv, int head_dim, int max_blocks,
+                               int part_blocks, int P, float scale, int window, float v_scale, float* part_o,
+                               float* part_ml, void* out, hipStream_t stream) {
   if (head_dim != 128 || Hq % Hkv != 0 || B <= 0 || P <= 0 || window < 0) return -1;
   const int G = Hq / Hkv;
   dim3 grid(P, Hkv, B);
   const float sl2 = scale * LOG2E;
-#define DEC_ARGS (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, ctx_lens, sl2, \
-    Hkv, max_blocks, part_blocks, P, window, part_o, part_ml, (uint16_t*)out
+#define DEC_ARGS (const uint16_t*)q, k_cache, v_cache, block_tables, ctx_lens, sl2, Hkv, max_blocks, part_blocks, P, \
+    window, v_scale, part_o, part_ml, (uint16_t*)out
   // nontemporal KV loads for large batches (B=128: 6.5 vs 5.9 TB/s; B=8: 3.8 vs 4.2 -- there the
   // plain loads win), profiles/decode_attn_partitions_r01.log; CFC_DECODE_NT=0/1 forces either
   static const int nt_env = [] { const char* e = getenv("CFC_DECODE_NT"); return e ? atoi(e) : -1; }();
   const bool nt = nt_env >= 0 ? nt_env != 0 : B >= 32;
 #define DEC_CASE(GG) \
   case GG: \
-    if (nt) paged_decode_kernel<GG, true><<<grid, 256, 0, stream>>>(DEC_ARGS); \
-    else paged_decode_kernel<GG, false><<<grid, 256, 0, stream>>>(DEC_ARGS); \
+    if (nt) paged_decode_kernel<GG, true, F8><<<grid, 256, 0, stream>>>(DEC_ARGS); \
+    else paged_decode_kernel<GG, false, F8><<<grid, 256, 0, stream>>>(DEC_ARGS); \
     break;
   switch (G) {
     DEC_CASE(1) DEC_CASE(2) DEC_CASE(4) DEC_CASE(8) DEC_CASE(16)
@@ -984,6 +1032,26 @@ CFC_API int cfc_paged_decode_attention(const void* q, const void* k_cache, const
 #undef DEC_ARGS
   if (P > 1) decode_combine_kernel<<<dim3(Hq, B), 128, 0, stream>>>(part_o, part_ml, P, Hq, (uint16_t*)out);
   return CFC_CHECK_LAUNCH();
+}
+
+// q: [B, Hq, 128] bf16; caches per layer as documented above; out: [B, Hq, 128] bf16.
+// part_o / part_ml: fp32 workspaces of B*Hq*P*128 and B*Hq*P*2 floats (unused when P == 1).
+CFC_API int cfc_paged_decode_attention(const void* q, const void* k_cache, const void* v_cache,
+                                       const int32_t* block_tables, const int32_t* ctx_lens, int B, int Hq, int Hkv,
+                                       int head_dim, int max_blocks, int part_blocks, int P, float scale, int window,
+                                       float* part_o, float* part_ml, void* out, hipStream_t stream) {
+  return launch_paged_decode<false>(q, k_cache, v_cache, block_tables, ctx_lens, B, Hq, Hkv, head_dim, max_blocks,
+                                    part_blocks, P, scale, window, 1.f, part_o, part_ml, out, stream);
+}
+
+// FP8 (e4m3fn) caches holding K / k_scale and V / v_scale
+CFC_API int cfc_paged_decode_attention_fp8(const void* q, const void* k_cache, const void* v_cache,
+                                           const int32_t* block_tables, const int32_t* ctx_lens, int B, int Hq,
+                                           int Hkv, int head_dim, int max_blocks, int part_blocks, int P, float scale,
+                                           int window, float k_scale, float v_scale, float* part_o, float* part_ml,
+                                           void* out, hipStream_t stream) {
+  return launch_paged_decode<true>(q, k_cache, v_cache, block_tables, ctx_lens, B, Hq, Hkv, head_dim, max_blocks,
+                                   part_blocks, P, scale * k_scale, window, v_scale, part_o, part_ml, out, stream);
 }
 
 CFC_API int cfc_prefill_tile_rows() { return PF_ROWS; }
@@ -1013,8 +1081,8 @@ CFC_API int cfc_prefill_attention(const void* q, const void* k_cache, const void
   const int G = Hq / Hkv;
 #define PF_ARGS (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, cu_q, ctx_lens, \
     tile_seq, tile_q0, scale * LOG2E, Hq, Hkv, max_blocks, (uint16_t*)out
-#define PF5_ARGS (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, cu_q, ctx_lens, \
-    tile_seq, tile_q0, scale * LOG2E, Hq, Hkv, max_blocks, window, (uint16_t*)out
+#define PF5_ARGS (const uint16_t*)q, k_cache, v_cache, block_tables, cu_q, ctx_lens, \
+    tile_seq, tile_q0, scale * LOG2E, Hq, Hkv, max_blocks, window, 1.f, (uint16_t*)out
   if (tile_rows != PF_ROWS || (G * tile_rows == 256 && prefill_variant() == 5)) {
     // 5: GQA-packed 8-wave kernel (default)
     const dim3 grid(n_tiles, Hkv);
@@ -1037,6 +1105,29 @@ CFC_API int cfc_prefill_attention(const void* q, const void* k_cache, const void
   else prefill_paged_kernel<4><<<dim3(n_tiles, Hq), 512, lds, stream>>>(PF_ARGS);
 #undef PF_ARGS
 #undef PF5_ARGS
+  return CFC_CHECK_LAUNCH();
+}
+
+// FP8 (e4m3fn) caches holding K / k_scale and V / v_scale; GQA-packed kernel only (G in 1,2,4,8)
+CFC_API int cfc_prefill_attention_fp8(const void* q, const void* k_cache, const void* v_cache,
+                                      const int32_t* block_tables, const int32_t* cu_q, const int32_t* ctx_lens,
+                                      const int32_t* tile_seq, const int32_t* tile_q0, int n_tiles, int tile_rows,
+                                      int Hq, int Hkv, int head_dim, int max_blocks, float scale, int window,
+                                      float k_scale, float v_scale, void* out, hipStream_t stream) {
+  if (head_dim != 128 || Hkv <= 0 || Hq % Hkv != 0 || window < 0) return -1;
+  const int G = Hq / Hkv;
+  if (!(G == 1 || G == 2 || G == 4 || G == 8) || tile_rows * G != 256) return -2;
+  if (n_tiles <= 0) return 0;
+  const dim3 grid(n_tiles, Hkv);
+#define PF8_ARGS (const uint16_t*)q, k_cache, v_cache, block_tables, cu_q, ctx_lens, tile_seq, tile_q0, \
+    scale * k_scale * LOG2E, Hq, Hkv, max_blocks, window, v_scale, (uint16_t*)out
+  switch (G) {
+    case 1: prefill_gqa_kernel<1, true><<<grid, 512, 65536, stream>>>(PF8_ARGS); break;
+    case 2: prefill_gqa_kernel<2, true><<<grid, 512, 65536, stream>>>(PF8_ARGS); break;
+    case 4: prefill_gqa_kernel<4, true><<<grid, 512, 65536, stream>>>(PF8_ARGS); break;
+    default: prefill_gqa_kernel<8, true><<<grid, 512, 65536, stream>>>(PF8_ARGS); break;
+  }
+#undef PF8_ARGS
   return CFC_CHECK_LAUNCH();
 }
 

@@ -77,4 +77,35 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
+// ---------------------------------------------------------------------------------------------
+// FP8 KV cache (OCP e4m3fn -- gfx950's v_cvt_pk_fp8_f32 / v_cvt_pk_f32_fp8 format, max 448; NOT
+// MI300's fnuz).  Values are clamped to +-448 before conversion so the cache never holds NaN.
+// fp8 -> f32 -> bf16 is exact (e4m3's 3 mantissa bits and exponent range fit bf16).
+typedef __bf16 bf16x2v_t __attribute__((ext_vector_type(2)));
+typedef float f32x2v_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t cvt_pk_bf16_f32(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v_t{a, b}, bf16x2v_t));
+}
+__device__ __forceinline__ float fp8_clamp(float x) { return fminf(fmaxf(x, -448.f), 448.f); }
+__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
+  const uint32_t r = __builtin_amdgcn_cvt_pk_fp8_f32(fp8_clamp(a), fp8_clamp(b), 0, false);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(fp8_clamp(c), fp8_clamp(d), r, true);
+}
+__device__ __forceinline__ uint2 pack8_fp8(const float* f) {
+  return make_uint2(pack4_fp8(f[0], f[1], f[2], f[3]), pack4_fp8(f[4], f[5], f[6], f[7]));
+}
+__device__ __forceinline__ uint8_t f2fp8(float x) {
+  return (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(fp8_clamp(x), 0.f, 0, false) & 0xff);
+}
+// 8 fp8 (in a uint2) -> 8 bf16 (bits, in a uint4), same element order
+__device__ __forceinline__ uint4 fp8x8_to_bf16x8(uint2 v) {
+  const auto a = __builtin_amdgcn_cvt_pk_f32_fp8(v.x, false), b = __builtin_amdgcn_cvt_pk_f32_fp8(v.x, true);
+  const auto c = __builtin_amdgcn_cvt_pk_f32_fp8(v.y, false), d = __builtin_amdgcn_cvt_pk_f32_fp8(v.y, true);
+  uint4 r;
+  r.x = cvt_pk_bf16_f32(a[0], a[1]); r.y = cvt_pk_bf16_f32(b[0], b[1]);
+  r.z = cvt_pk_bf16_f32(c[0], c[1]); r.w = cvt_pk_bf16_f32(d[0], d[1]);
+  return r;
+}
+
 #define CFC_CHECK_LAUNCH() (int)hipGetLastError()

@@ -20,14 +20,16 @@ __device__ __forceinline__ int v_slot(int key_in_block) {
 
 // qkv: [T, (Hq + 2*Hkv) * D] (q heads | k heads | v heads), positions [T], slots [T] (-1 = skip
 // cache write), cos_sin [max_pos][D/2][2] fp32 (cos, sin interleaved).
+template <bool F8>
 __global__ void __launch_bounds__(64) rope_kv_kernel(const uint16_t* __restrict__ qkv, const int32_t* __restrict__ positions,
                                                      const int32_t* __restrict__ slots, const float* __restrict__ cos_sin,
-                                                     uint16_t* __restrict__ q_out, uint16_t* __restrict__ k_cache,
-                                                     uint16_t* __restrict__ v_cache, int Hq, int Hkv, int D,
-                                                     int write_v) {
+                                                     uint16_t* __restrict__ q_out, void* __restrict__ k_cache,
+                                                     void* __restrict__ v_cache, int Hq, int Hkv, int D,
+                                                     int write_v, float inv_k, float inv_v) {
   // grid = (T, ceil(items / 64)): one 8-element item per thread -- (Hq + Hkv) * D/16 rotation
   // items then Hkv * D/8 V items -- so a decode batch of 128 tokens is ~900 blocks, not 128.
-  // write_v = 0: V goes through v_cache_runs_kernel instead (prefill: whole blocks, 16-B stores)
+  // write_v = 0: V goes through v_cache_runs_kernel instead (prefill: whole blocks, 16-B stores).
+  // F8: the caches hold e4m3 of value * inv_k / inv_v (the attention kernels scale back).
   const int tok = blockIdx.x;
   const int half = D / 2, nv = half / 8;  // 8-element vectors per half-head
   const int n_rot = (Hq + Hkv) * nv;
@@ -64,9 +66,21 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const uint16_t* __restrict_
     } else if (slot >= 0) {
       const int kh = head - Hq;
       const int blk = slot / KV_BS, off = slot % KV_BS;
-      uint16_t* dst = k_cache + (((size_t)blk * Hkv + kh) * KV_BS + off) * D;
-      *reinterpret_cast<uint4*>(dst + c * 8) = pa;
-      *reinterpret_cast<uint4*>(dst + half + c * 8) = pb;
+      const size_t e0 = (((size_t)blk * Hkv + kh) * KV_BS + off) * D;
+      if constexpr (F8) {
+        float qa[8], qb[8];
+        unpack8(pa, qa);     // round to bf16 first: the same values the bf16 cache would hold
+        unpack8(pb, qb);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { qa[j] *= inv_k; qb[j] *= inv_k; }
+        uint8_t* dst = reinterpret_cast<uint8_t*>(k_cache) + e0;
+        *reinterpret_cast<uint2*>(dst + c * 8) = pack8_fp8(qa);
+        *reinterpret_cast<uint2*>(dst + half + c * 8) = pack8_fp8(qb);
+      } else {
+        uint16_t* dst = reinterpret_cast<uint16_t*>(k_cache) + e0;
+        *reinterpret_cast<uint4*>(dst + c * 8) = pa;
+        *reinterpret_cast<uint4*>(dst + half + c * 8) = pb;
+      }
     }
   } else if (slot >= 0) {
     const int v = it - n_rot;
@@ -74,10 +88,17 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const uint16_t* __restrict_
     const uint4 val = *reinterpret_cast<const uint4*>(row + (Hq + Hkv + kh) * D + c * 8);
     const int blk = slot / KV_BS, off = slot % KV_BS;
     const int sl = v_slot(off);
-    uint16_t* dst = v_cache + (((size_t)blk * Hkv + kh) * D + c * 8) * KV_BS + sl;
+    const size_t e0 = (((size_t)blk * Hkv + kh) * D + c * 8) * KV_BS + sl;
     const uint16_t* e = reinterpret_cast<const uint16_t*>(&val);
+    if constexpr (F8) {
+      uint8_t* dst = reinterpret_cast<uint8_t*>(v_cache) + e0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dst[j * KV_BS] = e[j];
+      for (int j = 0; j < 8; ++j) dst[j * KV_BS] = f2fp8(bf2f(e[j]) * inv_v);
+    } else {
+      uint16_t* dst = reinterpret_cast<uint16_t*>(v_cache) + e0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dst[j * KV_BS] = e[j];
+    }
   }
 }
 
@@ -88,9 +109,11 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const uint16_t* __restrict_
 // 8-slot chunks, a partial run (chunk edges, prefix-cache continuations) per element so the
 // block's other slots are left untouched.  Replaces the 2-byte scattered stores of the per-token
 // path (1.85 TB/s effective for rope_kv at a prefill chunk, profiles/elementwise_bw_probe_r01.log).
+template <bool F8>
 __global__ void __launch_bounds__(256) v_cache_runs_kernel(const uint16_t* __restrict__ qkv,
                                                            const int32_t* __restrict__ runs,
-                                                           uint16_t* __restrict__ v_cache, int Hq, int Hkv, int D) {
+                                                           void* __restrict__ v_cache, int Hq, int Hkv, int D,
+                                                           float inv_v) {
   __shared__ __attribute__((aligned(16))) uint16_t sv[KV_BS][256 + 8];
   const int r = blockIdx.x, kh = blockIdx.y, tid = threadIdx.x;
   const int t0 = runs[4 * r], n = runs[4 * r + 1], blk = runs[4 * r + 2], off0 = runs[4 * r + 3];
@@ -102,22 +125,32 @@ __global__ void __launch_bounds__(256) v_cache_runs_kernel(const uint16_t* __res
         *reinterpret_cast<const uint4*>(qkv + (size_t)(t0 + j) * stride + (size_t)(Hq + Hkv + kh) * D + c * 8);
   }
   __syncthreads();
-  uint16_t* dst = v_cache + ((size_t)blk * Hkv + kh) * D * KV_BS;   // [D][32 slots]
+  const size_t e0 = ((size_t)blk * Hkv + kh) * D * KV_BS;   // [D][32 slots]
   if (n == KV_BS) {
     for (int i = tid; i < D * 4; i += 256) {
       const int d = i >> 2, g = i & 3;
       uint16_t e[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) e[j] = sv[16 * (j >> 2) + 4 * g + (j & 3)][d];   // key held by slot 8g + j
-      uint4 v;
-      v.x = e[0] | ((uint32_t)e[1] << 16); v.y = e[2] | ((uint32_t)e[3] << 16);
-      v.z = e[4] | ((uint32_t)e[5] << 16); v.w = e[6] | ((uint32_t)e[7] << 16);
-      *reinterpret_cast<uint4*>(dst + d * KV_BS + 8 * g) = v;
+      if constexpr (F8) {
+        float f[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = bf2f(e[j]) * inv_v;
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(v_cache) + e0 + d * KV_BS + 8 * g) = pack8_fp8(f);
+      } else {
+        uint4 v;
+        v.x = e[0] | ((uint32_t)e[1] << 16); v.y = e[2] | ((uint32_t)e[3] << 16);
+        v.z = e[4] | ((uint32_t)e[5] << 16); v.w = e[6] | ((uint32_t)e[7] << 16);
+        *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(v_cache) + e0 + d * KV_BS + 8 * g) = v;
+      }
     }
   } else {
     for (int i = tid; i < n * D; i += 256) {
       const int j = i / D, d = i - j * D, off = off0 + j;
-      dst[d * KV_BS + v_slot(off)] = sv[off][d];
+      if constexpr (F8)
+        reinterpret_cast<uint8_t*>(v_cache)[e0 + d * KV_BS + v_slot(off)] = f2fp8(bf2f(sv[off][d]) * inv_v);
+      else
+        reinterpret_cast<uint16_t*>(v_cache)[e0 + d * KV_BS + v_slot(off)] = sv[off][d];
     }
   }
 }
@@ -417,8 +450,22 @@ CFC_API int cfc_rope_kv_write(const void* qkv, const int32_t* positions, const i
   if (head_dim % 16 != 0 || T < 0) return -1;
   if (T == 0) return 0;
   const int items = (Hq + Hkv) * (head_dim / 16) + (write_v ? Hkv * (head_dim / 8) : 0);
-  rope_kv_kernel<<<dim3(T, (items + 63) / 64), 64, 0, stream>>>((const uint16_t*)qkv, positions, slots, cos_sin, (uint16_t*)q_out,
-                                         (uint16_t*)k_cache, (uint16_t*)v_cache, Hq, Hkv, head_dim, write_v);
+  rope_kv_kernel<false><<<dim3(T, (items + 63) / 64), 64, 0, stream>>>(
+      (const uint16_t*)qkv, positions, slots, cos_sin, (uint16_t*)q_out, k_cache, v_cache, Hq, Hkv, head_dim, write_v,
+      1.f, 1.f);
+  return CFC_CHECK_LAUNCH();
+}
+
+// FP8 (e4m3fn) KV cache: k/v stored as value * inv_k / inv_v
+CFC_API int cfc_rope_kv_write_fp8(const void* qkv, const int32_t* positions, const int32_t* slots,
+                                  const float* cos_sin, void* q_out, void* k_cache, void* v_cache, int T, int Hq,
+                                  int Hkv, int head_dim, int write_v, float inv_k, float inv_v, hipStream_t stream) {
+  if (head_dim % 16 != 0 || T < 0) return -1;
+  if (T == 0) return 0;
+  const int items = (Hq + Hkv) * (head_dim / 16) + (write_v ? Hkv * (head_dim / 8) : 0);
+  rope_kv_kernel<true><<<dim3(T, (items + 63) / 64), 64, 0, stream>>>(
+      (const uint16_t*)qkv, positions, slots, cos_sin, (uint16_t*)q_out, k_cache, v_cache, Hq, Hkv, head_dim, write_v,
+      inv_k, inv_v);
   return CFC_CHECK_LAUNCH();
 }
 
@@ -427,8 +474,17 @@ CFC_API int cfc_v_cache_write_runs(const void* qkv, const int32_t* runs, int R, 
                                    int head_dim, hipStream_t stream) {
   if (head_dim % 8 != 0 || head_dim > 256 || R < 0) return -1;
   if (R == 0) return 0;
-  v_cache_runs_kernel<<<dim3(R, Hkv), 256, 0, stream>>>((const uint16_t*)qkv, runs, (uint16_t*)v_cache, Hq, Hkv,
-                                                        head_dim);
+  v_cache_runs_kernel<false><<<dim3(R, Hkv), 256, 0, stream>>>((const uint16_t*)qkv, runs, v_cache, Hq, Hkv,
+                                                               head_dim, 1.f);
+  return CFC_CHECK_LAUNCH();
+}
+
+CFC_API int cfc_v_cache_write_runs_fp8(const void* qkv, const int32_t* runs, int R, void* v_cache, int Hq, int Hkv,
+                                       int head_dim, float inv_v, hipStream_t stream) {
+  if (head_dim % 8 != 0 || head_dim > 256 || R < 0) return -1;
+  if (R == 0) return 0;
+  v_cache_runs_kernel<true><<<dim3(R, Hkv), 256, 0, stream>>>((const uint16_t*)qkv, runs, v_cache, Hq, Hkv, head_dim,
+                                                              inv_v);
   return CFC_CHECK_LAUNCH();
 }
 

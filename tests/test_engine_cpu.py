@@ -144,3 +144,30 @@ def test_reference_sliding_window_is_attention_over_the_last_keys():
     # decode form: the last query sees the last W keys
     dec = R._attend(q[:1], k, v, 0.25, window=W)
     assert torch.allclose(dec, R._attend(q[:1], k[-W:], v[-W:], 0.25), atol=1e-5)
+
+
+def test_fp8_reference_cache_round_trip():
+    """float8_e4m3fn caches store value / scale (clamped to +-448) and gather scales back."""
+    Hq, Hkv, D = 4, 2, 16
+    T = 40
+    qkv = (torch.randn(T, (Hq + 2 * Hkv) * D) * 4).bfloat16()
+    cs = R.rope_cos_sin(128, D, 1e4)
+    kc = torch.zeros(4, Hkv, 32, D, dtype=torch.float8_e4m3fn)
+    vc = torch.zeros(4, Hkv, D, 32, dtype=torch.float8_e4m3fn)
+    kb, vb = torch.zeros(4, Hkv, 32, D).bfloat16(), torch.zeros(4, Hkv, D, 32).bfloat16()
+    slots = torch.arange(T, dtype=torch.int32) + 32
+    pos = torch.arange(T, dtype=torch.int32)
+    R.rope_kv_write(qkv, pos, slots, cs, kc, vc, Hq, Hkv, D, k_scale=0.25, v_scale=2.0)
+    R.rope_kv_write(qkv, pos, slots, cs, kb, vb, Hq, Hkv, D)
+    bt = torch.tensor([1, 2], dtype=torch.int32)
+    k8, v8 = R.gather_kv(kc, vc, bt, T, 0.25, 2.0)
+    k16, v16 = R.gather_kv(kb, vb, bt, T)
+    # e4m3: 3 mantissa bits -> relative error <= 2^-4 (plus the clamp, not reached here)
+    assert torch.allclose(k8, k16.float(), rtol=0.07, atol=0.25 * 2 ** -9)
+    assert torch.allclose(v8, v16.float(), rtol=0.07, atol=2.0 * 2 ** -9)
+    try:
+        from copilot_for_consensus_amd.runtime.kv_cache import PagedKVCache as P
+        P(1, 2, 1, 16, "cpu", dtype=torch.float16)
+        raise AssertionError("fp16 cache accepted")
+    except ValueError:
+        pass

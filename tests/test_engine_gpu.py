@@ -35,6 +35,23 @@ def test_decoder_prefill_logits_match_reference():
     assert agree >= 10, outs
 
 
+def test_fp8_kv_engine_matches_reference_fp8_engine():
+    """The opt-in FP8 (e4m3fn) KV cache end to end: GPU engine (fp8 kernels, hipGraph decode) vs the
+    CPU reference engine over the same fp8 cache semantics."""
+    cfg = get_config("tiny")
+    w = DecoderWeights.random(cfg, "cuda", seed=3)
+    prompts = [[1] + list(range(5, 5 + 90)), [1, 9, 8, 7], [1] + list(range(300, 371))]
+    outs = []
+    for model, dev in ((DecoderModel(w), "cuda"), (DecoderModel(_to_cpu_fp32_model(w)), "cpu")):
+        kv = PagedKVCache(cfg.layers, 24, cfg.kv_heads, cfg.head_dim, dev, dtype=torch.float8_e4m3fn,
+                          k_scale=0.5, v_scale=0.5)
+        eng = LLMEngine(model, kv, max_prefill_tokens=64, use_graph=(dev == "cuda"))
+        outs.append(eng.generate(prompts, max_new_tokens=8, ignore_eos=True).tokens)
+    assert [t[0] for t in outs[0]] == [t[0] for t in outs[1]]
+    agree = sum(a == b for x, y in zip(*outs) for a, b in zip(x, y))
+    assert agree >= 0.8 * sum(len(x) for x in outs[1]), outs
+
+
 def test_graph_and_eager_decode_agree():
     cfg = get_config("tiny")
     w = DecoderWeights.random(cfg, "cuda", seed=5)

@@ -319,3 +319,70 @@ def test_lib_splitk_linear_residual_rmsnorm(M, N, Kd, split):
     o = K.lib_splitk_linear_residual_rmsnorm(x, w, split, rr, nw, 1e-5)
     _close(rr, ref_r, 3e-2)
     _close(o, ref_o, 5e-2)
+
+
+# ------------------------------------------------------------------ FP8 (e4m3fn) KV cache
+F8 = torch.float8_e4m3fn
+
+
+def _fill_cache_fp8(ctx_lens, Hkv, D, k_scale, v_scale):
+    kc, vc, bt = _fill_cache(ctx_lens, Hkv, D)
+    return ((kc.float() / k_scale).clamp(-448, 448).to(F8), (vc.float() / v_scale).clamp(-448, 448).to(F8), bt)
+
+
+@pytest.mark.parametrize("scales", [(1.0, 1.0), (0.5, 0.25)])
+def test_rope_kv_write_fp8_matches_reference_bytes(scales):
+    """The kernel writes OCP e4m3fn bytes identical to torch's float8_e4m3fn of the same values
+    (per-token and whole-block-run V paths)."""
+    ks, vs = scales
+    Hq, Hkv, D = 8, 2, 128
+    slots = [3 * 32 + 5 + i for i in range(27)] + [9 * 32 + i for i in range(32)] + [4 * 32 + i for i in range(11)]
+    T = len(slots)
+    qkv = (torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV) * 3).bfloat16()
+    pos = torch.arange(T, device=DEV, dtype=torch.int32)
+    cs = R.rope_cos_sin(4096, D, 1e6, device=DEV)
+    sl = torch.tensor(slots, dtype=torch.int32, device=DEV)
+    kr, vr = torch.zeros(16, Hkv, 32, D, dtype=F8), torch.zeros(16, Hkv, D, 32, dtype=F8)
+    qr = R.rope_kv_write(qkv.cpu(), pos.cpu(), sl.cpu(), cs.cpu(), kr, vr, Hq, Hkv, D, ks, vs)
+    for runs in (None, torch.from_numpy(K.v_runs(slots)).to(DEV)):
+        kc = torch.zeros(16, Hkv, 32, D, dtype=F8, device=DEV)
+        vc = torch.zeros(16, Hkv, D, 32, dtype=F8, device=DEV)
+        q = K.rope_kv_write(qkv, pos, sl, cs, kc, vc, Hq, Hkv, D, runs=runs, k_scale=ks, v_scale=vs)
+        _close(q, qr, 2e-2)
+        kb, kref = kc.cpu().view(torch.uint8), kr.view(torch.uint8)
+        # K goes through the rotation in fp32 on both sides: allow a 1-ulp fp8 difference on a few values
+        assert (kb.int() - kref.int()).abs().max() <= 1 and (kb != kref).float().mean() < 0.01
+        assert torch.equal(vc.cpu().view(torch.uint8), vr.view(torch.uint8))
+
+
+@pytest.mark.parametrize("G", [1, 4, 8])
+@pytest.mark.parametrize("part_blocks", [4, -1, -3])
+def test_paged_decode_fp8(G, part_blocks):
+    Hkv, D = 2, 128
+    Hq = Hkv * G
+    ctx = [1, 31, 33, 100, 517, 2049]
+    kc, vc, bt = _fill_cache_fp8(ctx, Hkv, D, 0.5, 0.25)
+    q = torch.randn(len(ctx), Hq, D).bfloat16()
+    cl = torch.tensor(ctx, dtype=torch.int32)
+    ref = R.paged_decode_attention(q, kc, vc, bt, cl, 1 / math.sqrt(D), k_scale=0.5, v_scale=0.25)
+    out = K.paged_decode_attention(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), cl.to(DEV), 1 / math.sqrt(D),
+                                   part_blocks=part_blocks, k_scale=0.5, v_scale=0.25)
+    _close(out, ref, 2e-2)
+
+
+@pytest.mark.parametrize("G", [1, 2, 4, 8])
+def test_prefill_attention_fp8(G):
+    Hkv, D = 2, 128
+    Hq = Hkv * G
+    seqs = [(1, 1), (17, 17), (200, 200), (70, 300), (129, 1000)]
+    kc, vc, bt = _fill_cache_fp8([c for _, c in seqs], Hkv, D, 0.5, 2.0)
+    cu = [0]
+    for qn, _ in seqs:
+        cu.append(cu[-1] + qn)
+    q = torch.randn(cu[-1], Hq, D).bfloat16()
+    cu_t = torch.tensor(cu, dtype=torch.int32)
+    cl = torch.tensor([c for _, c in seqs], dtype=torch.int32)
+    ref = R.prefill_attention(q, kc, vc, bt, cu_t, cl, 1 / math.sqrt(D), k_scale=0.5, v_scale=2.0)
+    out = K.prefill_attention(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), cu_t.to(DEV), cl.to(DEV),
+                              1 / math.sqrt(D), k_scale=0.5, v_scale=2.0)
+    _close(out, ref, 2e-2)
