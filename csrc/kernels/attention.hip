@@ -115,14 +115,18 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   __shared__ float sm_o[4][D][17];
   __shared__ float sm_m[4][16], sm_l[4][16];
 
-  // Q^T B-operand: lane holds Q[head h*G+col][32c + 8g .. +7]; columns >= G are zero.
+  // Q^T B-operand: lane holds Q[head h*G+col][dq(c) .. +7]; columns >= G are zero.  bf16 cache:
+  // dq(c) = 32c + 8g.  FP8 cache: the head dim is visited in the order that lets ONE 16-byte load
+  // carry two k-steps of a key row (64 contiguous bytes per row per wave instruction, as the bf16
+  // loads have): dq(c) = 64(c >> 1) + 16g + 8(c & 1) -- any d order works as long as Q and K agree.
   bf16x8_t qf[4];
   {
     const bool valid = col < G;
     const uint16_t* qr = q + ((size_t)b * Hq + h * G + (valid ? col : 0)) * D;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      uint4 v = valid ? *reinterpret_cast<const uint4*>(qr + 32 * c + 8 * g) : make_uint4(0, 0, 0, 0);
+      const int dq = F8 ? 64 * (c >> 1) + 16 * g + 8 * (c & 1) : 32 * c + 8 * g;
+      uint4 v = valid ? *reinterpret_cast<const uint4*>(qr + dq) : make_uint4(0, 0, 0, 0);
       qf[c] = as_bf16x8(v);
     }
   }
@@ -135,27 +139,49 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   const int32_t* bt = block_tables + (size_t)b * max_blocks;
   const size_t head_stride = (size_t)KV_BS * D;  // elements per (block, kv-head)
 
-  Raw kr[8], vr[8];
+  // K fragments: bf16 -> 8 x 16 B (st, c); fp8 -> 4 x 16 B (st, pair p of k-steps 2p, 2p+1)
+  constexpr int NK = F8 ? 4 : 8;
+  uint4 kr[NK];
+  Raw vr[8];
   auto ld = [&](const void* base, size_t e) -> Raw {
     if constexpr (F8) return kv_load8<NT>(reinterpret_cast<const uint8_t*>(base) + e);
     else return kv_load<NT>(reinterpret_cast<const uint16_t*>(base) + e);
   };
-  auto load_blk = [&](int bi, Raw* kk, Raw* vv) {
+  auto load_blk = [&](int bi, uint4* kk, Raw* vv) {
     const size_t base = ((size_t)bt[bi] * Hkv + h) * head_stride;
+    if constexpr (F8) {
+      const uint8_t* kb = reinterpret_cast<const uint8_t*>(kc) + base;
 #pragma unroll
-    for (int st = 0; st < 2; ++st)
+      for (int st = 0; st < 2; ++st)
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        kk[st * 4 + c] = ld(kc, base + (16 * st + col) * D + 32 * c + 8 * g);
+        for (int pp = 0; pp < 2; ++pp)
+          kk[st * 2 + pp] = kv_load<NT>(reinterpret_cast<const uint16_t*>(kb + (16 * st + col) * D + 64 * pp + 16 * g));
+    } else {
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          kk[st * 4 + c] = kv_load<NT>(reinterpret_cast<const uint16_t*>(kc) + base + (16 * st + col) * D + 32 * c + 8 * g);
+    }
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt)
       vv[dt] = ld(vc, base + (16 * dt + col) * KV_BS + 8 * g);
+  };
+  // K operand of (st, k-step c)
+  auto kop = [&](const uint4* kk, int st, int c) -> bf16x8_t {
+    if constexpr (F8) {
+      const uint4 r = kk[st * 2 + (c >> 1)];
+      return kv_operand((c & 1) ? make_uint2(r.z, r.w) : make_uint2(r.x, r.y));
+    } else {
+      return as_bf16x8(kk[st * 4 + c]);
+    }
   };
 
   int bi = blk0 + w;
   if (bi < blk1) load_blk(bi, kr, vr);
   for (; bi < blk1; bi += 4) {
-    Raw kn[8], vn[8];
+    uint4 kn[NK];
+    Raw vn[8];
     const bool more = bi + 4 < blk1;
     if (more) load_blk(bi + 4, kn, vn);
 
@@ -164,7 +190,7 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
     for (int st = 0; st < 2; ++st) {
       s[st] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < 4; ++c) s[st] = mfma16(kv_operand(kr[st * 4 + c]), qf[c], s[st]);
+      for (int c = 0; c < 4; ++c) s[st] = mfma16(kop(kr, st, c), qf[c], s[st]);
     }
     const int key0 = bi * KV_BS;
     float tmax = -INFINITY;
@@ -199,7 +225,10 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
     }
     if (more) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) { kr[i] = kn[i]; vr[i] = vn[i]; }
+      for (int i = 0; i < 8; ++i) {
+        if (i < NK) kr[i] = kn[i];
+        vr[i] = vn[i];
+      }
     }
   }
 
