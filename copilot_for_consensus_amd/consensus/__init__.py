@@ -12,6 +12,9 @@ Differences by design:
     agreement / dissent prototype sentences -- cosine to the nearest prototype of each class,
     thresholded, replaces the keyword match; the same ladder then decides the level.  A prototype
     file (``model_path``, JSON ``{"agreement": [...], "dissent": [...]}``) overrides the built-ins.
+
+Reference: adapters/copilot_consensus/copilot_consensus/consensus.py:68 (ConsensusDetector), :90
+(heuristic), :290 (mock), :351-393 (ML detector, NotImplementedError there).
 """
 from __future__ import annotations
 

@@ -3,6 +3,9 @@
 Field names, required sets, status enum and indexes follow the reference's
 docs/schemas/documents/v1/*.schema.json and collections.config.json; like the events, the JSON
 Schemas are generated from the compact specs below.
+
+Reference: docs/schemas/documents/v1/*.schema.json and collections.config.json (read by
+infra/init/mongo-init.js:8-50).
 """
 from __future__ import annotations
 

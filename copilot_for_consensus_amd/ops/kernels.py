@@ -4,6 +4,11 @@ Every function takes torch tensors.  CUDA (= HIP on ROCm) tensors go to ``libcfc
 PyTorch's current stream (so the calls are hipGraph-capturable); CPU tensors run the fp32
 reference in :mod:`.reference` (CI / BASELINE config 1 have no GPU).  There is no silent
 fallback for GPU tensors: a missing native library raises.
+
+Reference call sites these ops replace: SentenceTransformer.encode
+(sentence_transformer_provider.py:93), the LLM servers' generation (local_llm_summarizer.py:107,
+llamacpp_summarizer.py:108-113) and the vector stores' scans (inmemory.py:106-119,
+faiss_store.py:214).
 """
 from __future__ import annotations
 

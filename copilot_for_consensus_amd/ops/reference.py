@@ -4,6 +4,9 @@ They define the exact semantics (including the paged KV-cache layouts) that the 
 ``csrc/kernels`` must reproduce; the numerics tests compare the two, and CPU-only runs (CI,
 BASELINE config 1) execute these.  Inputs/outputs use the same dtypes as the kernels (bf16
 activations), the math runs in fp32.
+
+These define the semantics the HIP kernels are tested against -- the attention/sampling the
+reference's engines run behind local_llm_summarizer.py:107 and llamacpp_summarizer.py:108-113.
 """
 from __future__ import annotations
 

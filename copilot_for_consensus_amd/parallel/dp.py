@@ -10,6 +10,9 @@ threads across them:
 * :func:`balanced_shard` -- longest-processing-time-first assignment by cost (prompt tokens), so
   ranks finish together instead of waiting on the one that drew the 10k-token threads;
 * :func:`gather_objects` -- results back to every rank (all_gather_object; small payloads).
+
+Reference scaling it replaces: competing consumers per queue, Container Apps replicas on queue
+length (infra/azure/modules/containerapps.bicep:262-263,711-730).
 """
 from __future__ import annotations
 

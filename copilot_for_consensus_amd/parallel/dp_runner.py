@@ -19,6 +19,9 @@ consumers on a durable RabbitMQ queue (unacked messages are redelivered); here t
 
 Processing is at-least-once (a rank presumed dead that was only slow may finish a batch that was
 also reassigned); the pipeline's deterministic ids make the duplicate writes idempotent.
+
+Reference counterpart: unacked messages redelivered to another consumer
+(rabbitmq_subscriber.py:537-560).
 """
 from __future__ import annotations
 

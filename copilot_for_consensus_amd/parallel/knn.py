@@ -12,6 +12,9 @@ Insert modes:
     the ids it owns (sha1(id) % world), so upserts of an id always land on the same shard;
   * ``add_local`` -- rank-local input (each rank embedded its own chunks); owner = producer.
 All query methods are collectives: every rank of the group must call them with the same nq / k.
+
+Reference query path: reporting topic search query(top_k=limit*3) (reporting/app/service.py:828),
+FAISS IndexFlat search (faiss_store.py:214).
 """
 from __future__ import annotations
 

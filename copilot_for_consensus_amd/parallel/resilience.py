@@ -15,6 +15,9 @@ FileStore / HashStore otherwise), so any surviving rank -- or an external superv
 * :func:`configure_collective_timeouts` -- RCCL async error handling + a finite collective timeout,
   so a peer that dies mid-all-reduce turns into an exception on the survivors (which then abort
   the communicator and restart through torchrun's elastic agent, resuming from the ledger).
+
+Reference recovery paths it generalises: subscriber reconnect (rabbitmq_subscriber.py:376-476),
+nack/requeue (:537-560), in-handler retry (event_handler.py:120-175).
 """
 from __future__ import annotations
 

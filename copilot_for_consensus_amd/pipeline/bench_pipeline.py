@@ -1,4 +1,9 @@
-"""The benchmark's unit of work: one batch of threads summarized end to end on one GPU."""
+"""The benchmark's unit of work: one batch of threads summarized end to end on one GPU.
+
+The reference's per-thread path it batches: summarization/app/service.py:289 ->
+local_llm_summarizer.py:107 (one thread per call); embedding one chunk per call
+(embedding/app/service.py:384-393).
+"""
 from __future__ import annotations
 
 import dataclasses

@@ -10,6 +10,10 @@ orchestrator scores candidates for 16 threads per fused HIP kNN scan.
 Stage events (ArchiveIngested, JSONParsed, ChunksPrepared, EmbeddingsGenerated,
 SummarizationRequested, SummaryComplete, ReportPublished) are built and schema-validated exactly
 as the services publish them; they go to ``publisher`` (a recording NoopPublisher by default).
+
+Reference: orchestrator context selection (orchestrator/app/context_selectors.py:17,95-107;
+context_sources.py:21,57-64) and the summarization request path
+(summarization/app/service.py:289).
 """
 from __future__ import annotations
 

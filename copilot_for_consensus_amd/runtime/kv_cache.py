@@ -6,6 +6,9 @@ Layout per layer (see csrc/kernels/attention.hip for why):
 Both live in ONE allocation per tensor kind ([layers, ...]) so the cache is a single HBM
 region; blocks are handed out by :class:`BlockPool` (the C++ free list in
 csrc/runtime/blockpool.cpp when the runtime library is available).
+
+Sized for the reference's LLM context (LLAMA_ARG_CTX_SIZE 4096, docker-compose.infra.yml:297) and
+beyond.
 """
 from __future__ import annotations
 

@@ -13,6 +13,9 @@ needs room (``alloc`` evicts).  Entries inserted for a batch are visible to late
 SAME batch: the prefill writes a layer's K/V for every token of a chunk before that layer's
 attention runs, and an owning prompt is always prefilled in the same or an earlier chunk than the
 prompts that reuse its blocks.
+
+Reference counterpart: llama.cpp's prompt cache behind llamacpp_summarizer.py:108 (the server
+reuses a matching prompt prefix).
 """
 from __future__ import annotations
 

@@ -8,6 +8,10 @@
   derives a 30522-entry vocabulary from the trained BPE pieces (word-initial pieces, ``##``
   continuations), with BERT's special-token ids ([PAD]=0 [UNK]=100 [CLS]=101 [SEP]=102).
 Trained vocabularies are cached as JSON under ``_lib/tokenizers`` (deterministic, git-ignored).
+
+Replaces the HF tokenizers that run inside SentenceTransformer.encode / AutoTokenizer
+(sentence_transformer_provider.py:93, huggingface_provider.py:92-101) and inside the llama.cpp /
+Ollama servers (llamacpp_summarizer.py:108).
 """
 from __future__ import annotations
 

@@ -2,6 +2,8 @@
 
     python -m copilot_for_consensus_amd.services.main node         # all services, in-proc bus
     python -m copilot_for_consensus_amd.services.main reporting    # one service per process
+
+Reference entry points: <service>/main.py (e.g. ingestion/main.py:179, parsing/main.py:101-124).
 """
 from __future__ import annotations
 

@@ -6,6 +6,8 @@ Parity target: adapters/copilot_startup/copilot_startup/startup_requeue.py (Star
 ``startup_requeue_errors_total``).  The services' own ``requeue_incomplete`` hooks
 (services/processing.py) group documents into batched events; this class is the generic
 per-document form the reference exposes, usable by scripts and custom services.
+
+Reference: adapters/copilot_startup/copilot_startup/startup_requeue.py:19-44 (StartupRequeue).
 """
 from __future__ import annotations
 

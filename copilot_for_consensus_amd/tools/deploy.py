@@ -17,6 +17,9 @@ topology of the reference.  Here:
   the Kubernetes manifests come from :mod:`.ops_assets`.
 
     python -m copilot_for_consensus_amd.tools.deploy --out deploy
+
+Reference lines: prometheus.yml:19-26 (push model), :23-60 (scrape jobs);
+alerts/slo_latency.yml:18-305.
 """
 from __future__ import annotations
 

@@ -6,6 +6,9 @@ scrape errors), mongo_doc_count_exporter.py / mongo_collstats_exporter.py (per-c
 and qdrant_exporter.py (vector counts) of the reference.  One collector reads any DocumentStore
 and VectorStore (in-proc or Mongo) -- plus the GPU-resident index's HBM footprint -- and renders
 the Prometheus text format; ``serve`` exposes it on /metrics (stdlib http.server).
+
+Reference: scripts/document_processing_exporter.py:37-67 (gauges), mongo_doc_count_exporter.py,
+qdrant_exporter.py.
 """
 from __future__ import annotations
 

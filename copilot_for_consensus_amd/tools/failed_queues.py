@@ -8,6 +8,8 @@ QUEUE_MAPPINGS :44-52, list :98, inspect :125, export :183, requeue :230 with --
   * :class:`RabbitMQFailedQueues` -- pika ``basic_get`` / ``basic_publish`` (import-gated).
 Requeue republishes each message on the target routing key (the mapping, ``--target``, or for a
 dead letter its own routing key) and removes it from the failed queue only after the publish.
+
+Reference: scripts/manage_failed_queues.py:98-303 (list / inspect / export / requeue / purge).
 """
 from __future__ import annotations
 

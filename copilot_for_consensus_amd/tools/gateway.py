@@ -8,6 +8,9 @@ paths (``/ingestion``, ``/reporting``, ``/auth``, ...) and an nginx config with 
 service is rendered from the same route table, so the three cannot drift apart.
 
     python -m copilot_for_consensus_amd.tools.gateway --out deploy/gateway
+
+Reference: infra/gateway/generate_gateway_config.py:34-119 (per-provider adapters),
+infra/nginx/nginx.conf:155-267 (path-prefix proxy), openapi/gateway.yaml.
 """
 from __future__ import annotations
 

@@ -5,6 +5,9 @@ Parity targets: the reference's ``scripts/check_mutable_defaults.py`` (mutable d
 configuration layer or for allow-listed names) and ``scripts/check_license_headers.py``.
 
   python -m copilot_for_consensus_amd.tools.policy [paths...]     # exit 1 on any finding
+
+Reference: scripts/check_mutable_defaults.py:47-141, check_no_runtime_env_vars.py:78-110,
+check_license_headers.py.
 """
 from __future__ import annotations
 

@@ -9,6 +9,9 @@ compose).  Differences:
     with a ``parsed_message_ids`` field its own schema rejects, one event per document);
   * "stuck" is defined per collection on this framework's document model: archives by status,
     messages without chunks, chunks not embedded, threads with embedded chunks but no summary.
+
+Reference: scripts/retry_stuck_documents.py:143 (COLLECTION_CONFIGS :147-172, failed_max_retries
+terminal state :355).
 """
 from __future__ import annotations
 

@@ -6,6 +6,8 @@ here the config schemas are generated from config/specs.py, so only export is ne
 
     python -m copilot_for_consensus_amd.tools.schemas export docs/schemas
     python -m copilot_for_consensus_amd.tools.schemas check
+
+Reference: scripts/generate_typed_configs.py:1-14 and scripts/generate_service_openapi.py.
 """
 from __future__ import annotations
 

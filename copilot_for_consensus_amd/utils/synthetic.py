@@ -7,6 +7,9 @@ ASCII headers, dates, To/CC lists, quoted reply lines, signatures, RFC and draft
 Bodies use a Zipf-distributed vocabulary of 300k words (a core of technical English plus
 syllable-built pseudo-words), so a BPE vocabulary trained on it yields a realistic ~1.3 tokens
 per word (measured 1.36) and the orchestrator's 1.3x-words budget behaves as with real mail.
+
+Message shape modelled on the reference fixture tests/fixtures/mailbox_sample/test-archive.mbox
+(mbox with RFC 5322 headers, In-Reply-To threading).
 """
 from __future__ import annotations
 
