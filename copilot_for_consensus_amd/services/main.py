@@ -55,7 +55,12 @@ def main(argv=None) -> int:
 
     from .base import create_app, run_service
     from .node import Node
-    node = Node()
+    try:
+        node = Node()
+        node.connect(None if args.service == "node" else [args.service])
+    except Exception as e:  # noqa: BLE001 -- fail fast: a service that cannot reach its bus/store exits 1
+        print(f"[{args.service}] start-up failed: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
+        return 1
     if args.service == "node":
         import uvicorn
         from .ingestion import ingestion_routes

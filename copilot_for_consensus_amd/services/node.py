@@ -84,8 +84,25 @@ class Node:
                                           **common),
         }
         self._threads: list[threading.Thread] = []
+        self._connected = False
+
+    def connect(self, services=None) -> None:
+        """Connect the document store and every (or the named) service's publisher / subscriber.
+        Raises on the first failure -- the entry point turns that into exit code 1, the reference's
+        fail-fast start-up (parsing/tests/test_startup_validation.py:115-165)."""
+        if self._connected:
+            return
+        self.store.connect()
+        for name, svc in self.services.items():
+            if services is not None and name not in services:
+                continue
+            for end in (svc.publisher, svc.subscriber):
+                if end is not None and hasattr(end, "connect"):
+                    end.connect()
+        self._connected = True
 
     def start(self, threaded: bool = True) -> None:
+        self.connect()
         for s in self.services.values():
             s.start()
         if threaded:

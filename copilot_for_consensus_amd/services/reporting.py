@@ -210,9 +210,11 @@ def reporting_routes(app, service: ReportingService, auth=None):
     def search(topic: str, limit: int = Query(10, ge=1, le=50), min_score: float = Query(0.5, ge=0.0, le=1.0)):
         try:
             r = service.search_reports_by_topic(topic, limit, min_score)
+        except ValueError as e:          # empty topic / search not configured (reporting/main.py:227-229)
+            raise HTTPException(400, str(e))
         except RuntimeError as e:
             raise HTTPException(503, str(e))
-        return {"topic": topic, "reports": r, "count": len(r)}
+        return {"topic": topic, "reports": r, "count": len(r), "min_score": min_score}
 
     @app.get("/api/reports/{report_id}", dependencies=deps)
     def report(report_id: str):
