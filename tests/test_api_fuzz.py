@@ -105,3 +105,38 @@ def test_get_operations_never_5xx(clients, service):
         assert resp.status_code < 500, (url, query, resp.status_code, resp.text[:200])
 
     run()
+
+
+_json_scalar = st.none() | st.booleans() | st.integers(-10 ** 9, 10 ** 9) | _text
+_body = st.dictionaries(st.sampled_from(["name", "source_type", "url", "enabled", "port", "username", "folder",
+                                         "schedule", "extra"]) | _text, _json_scalar | st.lists(_json_scalar, max_size=3),
+                        max_size=8)
+
+
+def test_source_writes_never_5xx(clients):
+    c = clients["ingestion"]
+
+    @settings(max_examples=150, deadline=None, suppress_health_check=list(HealthCheck))
+    @given(_body, st.sampled_from(["post", "put"]), _text)
+    def run(body, method, name):
+        if method == "post":
+            r = c.post("/api/sources", json=body)
+        else:
+            r = c.put(f"/api/sources/{name.replace('/', '_') or 'x'}", json=body)
+        assert r.status_code < 500, (method, body, r.status_code, r.text[:200])
+        if r.status_code in (200, 201) and method == "post":
+            c.delete(f"/api/sources/{body.get('name')}")
+
+    run()
+
+
+def test_uploads_never_5xx(clients):
+    c = clients["ingestion"]
+
+    @settings(max_examples=80, deadline=None, suppress_health_check=list(HealthCheck))
+    @given(st.binary(max_size=512), _text, st.sampled_from([".mbox", ".zip", ".tar.gz", ".tgz", ".tar", ".txt", ""]))
+    def run(data, stem, ext):
+        r = c.post("/api/uploads", files={"file": ((stem or "f") + ext, data, "application/octet-stream")})
+        assert r.status_code < 500, (stem + ext, len(data), r.status_code, r.text[:200])
+
+    run()
