@@ -32,6 +32,7 @@ _KERNEL_SIGS = {
     "cfc_encoder_attention": [P, P, P, P, I, I, I, I, F, P, P],
     "cfc_rope_kv_write": [P, P, P, P, P, P, P, I, I, I, I, I, P],
     "cfc_v_cache_write_runs": [P, P, I, P, I, I, I, P],
+    "cfc_decode_advance_cb": [P, P, I, P, P, P, P, P, P, P, I, P, P, I, I, P],
     "cfc_rope_kv_write_fp8": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, P],
     "cfc_v_cache_write_runs_fp8": [P, P, I, P, I, I, I, F, P],
     "cfc_paged_decode_attention_fp8": [P, P, P, P, P, I, I, I, I, I, I, I, F, I, F, F, P, P, P, P],

@@ -482,6 +482,40 @@ def sample(logits, out_ids, temperature=0.0, seed=0, step=None):
     return out_ids
 
 
+def decode_advance_cb(next_ids, tokens, gen, limit, input_ids, positions, ctx_lens, slots, block_tables, done,
+                      stop_ids):
+    """Continuous-batching bookkeeping after a decode step: per-slot token count / limit; finished
+    and empty slots (done = 1) are frozen (graph-capturable, no host sync)."""
+    B = next_ids.numel()
+    cap = tokens.shape[1]
+    if not next_ids.is_cuda:
+        act = done == 0
+        if not bool(act.any()):
+            return
+        idx = act.nonzero().flatten()
+        g = gen[idx].long()
+        rec = g < cap
+        tokens[idx[rec], g[rec]] = next_ids[idx[rec]].to(tokens.dtype)
+        gen[idx] += 1
+        fin = gen[idx] >= limit[idx]
+        if stop_ids.numel():
+            fin |= torch.isin(next_ids[idx], stop_ids)
+        done[idx] = fin.to(done.dtype)
+        go = idx[~fin]
+        input_ids[go] = next_ids[go]
+        positions[go] += 1
+        ctx_lens[go] = positions[go] + 1
+        pos = positions[go].long()
+        slots[go] = (block_tables[go, pos // KV_BLOCK] * KV_BLOCK + pos % KV_BLOCK).to(slots.dtype)
+        return
+    check(kernels().cfc_decode_advance_cb(next_ids.data_ptr(), tokens.data_ptr(), cap, gen.data_ptr(),
+                                          limit.data_ptr(), input_ids.data_ptr(), positions.data_ptr(),
+                                          ctx_lens.data_ptr(), slots.data_ptr(), block_tables.data_ptr(),
+                                          block_tables.shape[1], done.data_ptr(),
+                                          _p(stop_ids) if stop_ids.numel() else None, stop_ids.numel(), B,
+                                          _stream(next_ids)), "cfc_decode_advance_cb")
+
+
 def decode_advance(next_ids, tokens, step, input_ids, positions, ctx_lens, slots, block_tables, done, stop_ids):
     """Device-side bookkeeping after each decode step (graph-capturable, no host sync)."""
     B = next_ids.numel()

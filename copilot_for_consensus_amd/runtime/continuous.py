@@ -1,0 +1,256 @@
+"""Continuous batching over the paged KV cache ("continuous batching of
+threads"; the reference's llama.cpp / Ollama servers interleave concurrent requests the same way,
+llamacpp_summarizer.py:108 -> llama-server slots, docker-compose.infra.yml:296-298).
+
+:class:`LLMEngine.generate` runs a batch to completion; a thread that finishes early leaves its row
+idle until the slowest one is done, and a thread that arrives mid-batch waits for the whole batch.
+Here the decode batch is a fixed set of ``max_slots`` slots:
+
+* one decode step over all slots is captured ONCE in a hipGraph (fixed shapes: slots x the
+  block-table width) and replayed ``steps_per_sync`` times between host visits;
+* every slot carries its own generated-token count and limit on the device
+  (``decode_advance_cb_kernel``); a finished or empty slot is frozen -- it keeps pointing at its
+  own last KV slot, or at a scratch block when empty -- so the captured step runs over it harmlessly;
+* between bursts the host harvests finished slots (one device->host copy of their rows), returns
+  their KV blocks, and admits queued requests into the free slots: their prompts go through the
+  engine's chunked packed prefill (prefix-cache aware) and their first token, position, block table
+  and limit are written into the slot rows.
+
+Greedy outputs equal :meth:`LLMEngine.generate` on each request alone (tests/test_continuous.py).
+"""
+from __future__ import annotations
+
+import collections
+import dataclasses
+import math
+import time
+
+import numpy as np
+import torch
+
+from ..ops import kernels as K
+from ..ops.reference import KV_BLOCK
+from .kv_cache import blocks_needed
+
+
+@dataclasses.dataclass
+class Request:
+    rid: int
+    prompt: list[int]
+    max_new: int
+    submitted_s: float
+    first_token_s: float | None = None
+    finished_s: float | None = None
+    tokens: list[int] | None = None
+
+    @property
+    def latency_s(self) -> float | None:
+        return None if self.finished_s is None else self.finished_s - self.submitted_s
+
+
+class ContinuousEngine:
+    def __init__(self, engine, max_slots: int = 128, max_new_cap: int = 512, max_prompt: int = 4096,
+                 steps_per_sync: int = 16, stop_ids: tuple[int, ...] = (), temperature: float = 0.0, seed: int = 0,
+                 max_admit_tokens: int | None = None):
+        self.engine = engine
+        self.model = engine.model
+        self.kv = engine.kv
+        self.device = self.kv.device
+        self.B = int(max_slots)
+        self.cap = int(max_new_cap)
+        self.max_prompt = int(max_prompt)
+        self.steps_per_sync = max(1, int(steps_per_sync))
+        self.stop_ids = tuple(int(s) for s in stop_ids)
+        self.sampling = K.SamplingParams.of(temperature)
+        self.seed = int(seed)
+        self.max_admit_tokens = max_admit_tokens or engine.max_prefill_tokens * 4
+        self.max_blocks = 8 * math.ceil(blocks_needed(self.max_prompt + self.cap) / 8)
+        # empty slots read and write this block only
+        self.scratch = self.kv.pool.alloc(1)[0]
+        B, dev = self.B, self.device
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.ids = torch.zeros(B, **i32)
+        self.positions = torch.zeros(B, **i32)
+        self.ctx_lens = torch.ones(B, **i32)
+        self.slots = torch.full((B,), self.scratch * KV_BLOCK, **i32)
+        self.block_tables = torch.full((B, self.max_blocks), self.scratch, **i32)
+        self.tokens = torch.zeros(B, self.cap, **i32)
+        self.gen = torch.zeros(B, **i32)
+        self.limit = torch.ones(B, **i32)
+        self.done = torch.ones(B, **i32)
+        self.next_ids = torch.zeros(B, **i32)
+        self.step_t = torch.zeros(1, **i32)     # sampler RNG salt
+        self.stop_t = torch.tensor(self.stop_ids, **i32)
+        self.part_blocks = engine._part_blocks(B, self.max_blocks)
+        P = -self.part_blocks
+        ws = B * self.model.w.heads * P * (self.model.cfg.head_dim + 2) if P > 1 else 1
+        self.workspace = torch.empty(max(1, ws), dtype=torch.float32, device=dev)
+        self.use_graph = engine.use_graph
+        self.graph = None
+        self.queue: collections.deque[Request] = collections.deque()
+        self.slot_req: list[Request | None] = [None] * B
+        self.slot_tables: list[tuple[list[int], list[int]] | None] = [None] * B
+        self.free = list(range(B - 1, -1, -1))
+        self._rid = 0
+        self.stats = {"steps": 0, "admitted": 0, "finished": 0, "prefill_s": 0.0, "decode_s": 0.0}
+
+    # ------------------------------------------------------------------ API
+    def submit(self, prompt: list[int], max_new: int) -> Request:
+        if not prompt:
+            raise ValueError("empty prompt")
+        if len(prompt) > self.max_prompt or max_new > self.cap or max_new < 1:
+            raise ValueError(f"prompt {len(prompt)} > {self.max_prompt} or max_new {max_new} outside [1, {self.cap}]")
+        r = Request(self._rid, list(prompt), int(max_new), time.perf_counter())
+        self._rid += 1
+        self.queue.append(r)
+        return r
+
+    def pending(self) -> int:
+        return len(self.queue) + sum(r is not None for r in self.slot_req)
+
+    @torch.inference_mode()
+    def step(self) -> list[Request]:
+        """Admit what fits, run one burst of decode steps, harvest; returns requests finished now."""
+        self._admit()
+        if all(r is None for r in self.slot_req):
+            return []
+        t = time.perf_counter()
+        self._burst(self.steps_per_sync)
+        out = self._harvest()
+        self.stats["decode_s"] += time.perf_counter() - t
+        return out
+
+    def run(self) -> list[Request]:
+        done: list[Request] = []
+        while self.pending():
+            done.extend(self.step())
+        return done
+
+    def close(self) -> None:
+        for s in range(self.B):
+            if self.slot_tables[s] is not None:
+                self._release_slot(s)
+        self.kv.pool.free([self.scratch])
+
+    # ------------------------------------------------------------------ internals
+    def _admit(self) -> None:
+        if not self.queue or not self.free:
+            return
+        take: list[Request] = []
+        budget = self.max_admit_tokens
+        while self.queue and len(take) < len(self.free) and (not take or budget >= len(self.queue[0].prompt)):
+            r = self.queue.popleft()
+            take.append(r)
+            budget -= len(r.prompt)
+        pc = self.engine.prefix_cache
+        tables, fresh, start = [], [], []
+        try:
+            for r in take:
+                n = blocks_needed(len(r.prompt) + r.max_new)
+                shared = pc.acquire(r.prompt) if pc is not None else []
+                tables.append(shared)
+                new = pc.alloc(n - len(shared)) if pc is not None else self.kv.pool.alloc(n)
+                fresh.append(new)
+                tables[-1] = shared + new
+                start.append(len(shared) * KV_BLOCK)
+                if pc is not None:
+                    pc.insert(r.prompt, tables[-1])
+        except BaseException:
+            self.engine._release(tables, fresh, failed=True)
+            self.queue.extendleft(reversed(take))
+            raise
+        t = time.perf_counter()
+        first = self.engine._prefill([r.prompt for r in take], tables, self.sampling, self.seed, start)
+        now = time.perf_counter()
+        self.stats["prefill_s"] += now - t
+        slots = [self.free.pop() for _ in take]
+        bt = np.full((len(take), self.max_blocks), self.scratch, np.int32)
+        rows = np.zeros((len(take), 6), np.int32)       # ids, positions, ctx, slot, limit, done
+        for i, (r, s, tbl, f) in enumerate(zip(take, slots, tables, first)):
+            bt[i, :len(tbl)] = tbl
+            n = len(r.prompt)
+            rows[i] = (f, n, n + 1, tbl[n // KV_BLOCK] * KV_BLOCK + n % KV_BLOCK, r.max_new,
+                       int(r.max_new <= 1 or f in self.stop_ids))
+            r.first_token_s = now
+            self.slot_req[s] = r
+            self.slot_tables[s] = (tbl, fresh[i])
+        idx = torch.tensor(slots, dtype=torch.long, device=self.device)
+        rows_t = torch.from_numpy(rows).to(self.device)
+        self.block_tables.index_copy_(0, idx, torch.from_numpy(bt).to(self.device))
+        for j, dst in enumerate((self.ids, self.positions, self.ctx_lens, self.slots, self.limit, self.done)):
+            dst.index_copy_(0, idx, rows_t[:, j].contiguous())
+        self.gen.index_fill_(0, idx, 1)
+        self.tokens.index_copy_(0, idx, torch.nn.functional.pad(rows_t[:, :1], (0, self.cap - 1)))
+        self.stats["admitted"] += len(take)
+
+    def _decode_step(self) -> None:
+        hidden = self.model.forward_decode(self.ids, self.positions, self.slots, self.ctx_lens, self.block_tables,
+                                           self.kv, attn_workspace=self.workspace, part_blocks=self.part_blocks)
+        logits = self.model.logits(hidden)
+        K.sample(logits, self.next_ids, self.sampling, self.seed, self.step_t)
+        K.decode_advance_cb(self.next_ids, self.tokens, self.gen, self.limit, self.ids, self.positions,
+                            self.ctx_lens, self.slots, self.block_tables, self.done, self.stop_t)
+        self.step_t.add_(1)
+
+    def _state(self):
+        return [self.ids, self.positions, self.ctx_lens, self.slots, self.tokens, self.gen, self.done,
+                self.next_ids, self.step_t]
+
+    def _burst(self, n: int) -> None:
+        if self.use_graph and self.graph is None:
+            saved = [t.clone() for t in self._state()]
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                self._decode_step()        # warm-up (workspaces, library handles) outside capture
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            for t, v in zip(self._state(), saved):
+                t.copy_(v)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._decode_step()
+            for t, v in zip(self._state(), saved):
+                t.copy_(v)
+            self.graph = g
+        for _ in range(n):
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self._decode_step()
+        self.stats["steps"] += n
+
+    def _harvest(self) -> list[Request]:
+        done = self.done.cpu().numpy()
+        fin = [s for s in range(self.B) if self.slot_req[s] is not None and done[s]]
+        if not fin:
+            return []
+        idx = torch.tensor(fin, dtype=torch.long, device=self.device)
+        gen = self.gen.index_select(0, idx).cpu().tolist()
+        toks = self.tokens.index_select(0, idx).cpu()
+        now = time.perf_counter()
+        stop = set(self.stop_ids)
+        out = []
+        for i, s in enumerate(fin):
+            row = toks[i, :min(gen[i], self.cap)].tolist()
+            for j, t in enumerate(row):
+                if t in stop:
+                    row = row[:j]
+                    break
+            r = self.slot_req[s]
+            r.tokens, r.finished_s = row, now
+            out.append(r)
+            self._release_slot(s)
+        # freeze the freed rows on the scratch block before their KV blocks can be reused
+        self.block_tables.index_fill_(0, idx, self.scratch)
+        self.slots.index_fill_(0, idx, self.scratch * KV_BLOCK)
+        self.positions.index_fill_(0, idx, 0)
+        self.ctx_lens.index_fill_(0, idx, 1)
+        self.stats["finished"] += len(out)
+        return out
+
+    def _release_slot(self, s: int) -> None:
+        tbl, fresh = self.slot_tables[s]
+        self.engine._release([tbl], [fresh])
+        self.slot_tables[s] = None
+        self.slot_req[s] = None
+        self.free.append(s)

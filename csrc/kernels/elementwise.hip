@@ -437,6 +437,35 @@ __global__ void decode_advance_kernel(const int32_t* __restrict__ next, int32_t*
   if (b == 0) *step_ptr = step + 1;
 }
 
+// Continuous batching: every slot carries its own generated-token count and limit.  Active,
+// unfinished slots record the sampled token at tokens[b][gen[b]], advance their position and KV
+// slot, and finish on a stop id or when gen reaches limit.  Finished / empty slots are frozen:
+// their token, position and KV slot stay put (an empty slot points at the engine's scratch block),
+// so the fixed-shape captured step can keep running over them.
+__global__ void decode_advance_cb_kernel(const int32_t* __restrict__ next, int32_t* __restrict__ tokens, int cap,
+                                         int32_t* __restrict__ gen, const int32_t* __restrict__ limit,
+                                         int32_t* __restrict__ input_ids, int32_t* __restrict__ positions,
+                                         int32_t* __restrict__ ctx_lens, int32_t* __restrict__ slots,
+                                         const int32_t* __restrict__ block_tables, int max_blocks,
+                                         int32_t* __restrict__ done, const int32_t* __restrict__ stop_ids, int n_stop,
+                                         int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B || done[b]) return;
+  const int tok = next[b];
+  const int g = gen[b];
+  if (g < cap) tokens[(size_t)b * cap + g] = tok;
+  gen[b] = g + 1;
+  int d = g + 1 >= limit[b];
+  for (int i = 0; i < n_stop; ++i) d |= (tok == stop_ids[i]);
+  done[b] = d;
+  if (d) return;
+  input_ids[b] = tok;
+  const int pos = positions[b] + 1;
+  positions[b] = pos;
+  ctx_lens[b] = pos + 1;
+  slots[b] = block_tables[(size_t)b * max_blocks + pos / KV_BS] * KV_BS + pos % KV_BS;
+}
+
 inline int ew_grid(size_t total) {
   size_t g = (total + 255) / 256;
   return (int)(g > 4096 ? 4096 : (g == 0 ? 1 : g));
@@ -485,6 +514,17 @@ CFC_API int cfc_v_cache_write_runs_fp8(const void* qkv, const int32_t* runs, int
   if (R == 0) return 0;
   v_cache_runs_kernel<true><<<dim3(R, Hkv), 256, 0, stream>>>((const uint16_t*)qkv, runs, v_cache, Hq, Hkv, head_dim,
                                                               inv_v);
+  return CFC_CHECK_LAUNCH();
+}
+
+CFC_API int cfc_decode_advance_cb(const int32_t* next, int32_t* tokens, int cap, int32_t* gen, const int32_t* limit,
+                                  int32_t* input_ids, int32_t* positions, int32_t* ctx_lens, int32_t* slots,
+                                  const int32_t* block_tables, int max_blocks, int32_t* done, const int32_t* stop_ids,
+                                  int n_stop, int B, hipStream_t stream) {
+  if (B <= 0) return 0;
+  decode_advance_cb_kernel<<<(B + 255) / 256, 256, 0, stream>>>(next, tokens, cap, gen, limit, input_ids, positions,
+                                                                 ctx_lens, slots, block_tables, max_blocks, done,
+                                                                 stop_ids, n_stop, B);
   return CFC_CHECK_LAUNCH();
 }
 
