@@ -51,7 +51,7 @@ class Request:
 class ContinuousEngine:
     def __init__(self, engine, max_slots: int = 128, max_new_cap: int = 512, max_prompt: int = 4096,
                  steps_per_sync: int = 16, stop_ids: tuple[int, ...] = (), temperature: float = 0.0, seed: int = 0,
-                 max_admit_tokens: int | None = None):
+                 max_admit_tokens: int | None = None, min_admit: int = 1, max_wait_s: float = 0.5):
         self.engine = engine
         self.model = engine.model
         self.kv = engine.kv
@@ -64,6 +64,9 @@ class ContinuousEngine:
         self.sampling = K.SamplingParams.of(temperature)
         self.seed = int(seed)
         self.max_admit_tokens = max_admit_tokens or engine.max_prefill_tokens * 4
+        # admission batching: prefill waits for `min_admit` queued threads (or the oldest waiting
+        # `max_wait_s`, or an idle engine) -- fewer, larger prefills interrupt the decode less
+        self.min_admit, self.max_wait_s = max(1, int(min_admit)), float(max_wait_s)
         self.max_blocks = 8 * math.ceil(blocks_needed(self.max_prompt + self.cap) / 8)
         # empty slots read and write this block only
         self.scratch = self.kv.pool.alloc(1)[0]
@@ -135,6 +138,10 @@ class ContinuousEngine:
     # ------------------------------------------------------------------ internals
     def _admit(self) -> None:
         if not self.queue or not self.free:
+            return
+        idle = all(r is None for r in self.slot_req)
+        waited = time.perf_counter() - self.queue[0].submitted_s
+        if not idle and len(self.queue) < min(self.min_admit, len(self.free)) and waited < self.max_wait_s:
             return
         take: list[Request] = []
         budget = self.max_admit_tokens

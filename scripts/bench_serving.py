@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--prompt", type=int, default=2500)
     ap.add_argument("--steps-per-sync", type=int, default=16)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--min-admit", type=int, default=1)
+    ap.add_argument("--max-wait", type=float, default=0.5)
     a = ap.parse_args()
     cfg = get_config(a.model)
     dev = torch.device("cuda")
@@ -39,7 +41,7 @@ def main():
     kv = PagedKVCache(cfg.layers, nblk, cfg.kv_heads, cfg.head_dim, dev)
     eng = LLMEngine(model, kv, max_prefill_tokens=16384)
     ce = ContinuousEngine(eng, max_slots=a.slots, max_new_cap=a.max_new, max_prompt=int(a.prompt * 1.3) + 200,
-                          steps_per_sync=a.steps_per_sync)
+                          steps_per_sync=a.steps_per_sync, min_admit=a.min_admit, max_wait_s=a.max_wait)
     rng = random.Random(a.seed)
     system = [rng.randrange(3, cfg.vocab_size) for _ in range(170)]      # shared system prompt (prefix cache)
     prompts = [[1] + system + [rng.randrange(3, cfg.vocab_size) for _ in range(int(rng.uniform(0.7, 1.3) * a.prompt))]
@@ -75,7 +77,8 @@ def main():
            "p50_latency_s": round(statistics.median(lat), 3), "p95_latency_s": round(lat[int(0.95 * len(lat)) - 1], 3),
            "p50_ttft_s": round(statistics.median(ttft), 3),
            "generated_tokens_per_s": round(sum(len(h.tokens) for h in handles) / elapsed, 1),
-           "decode_steps": ce.stats["steps"], "prefill_s": round(ce.stats["prefill_s"], 2)}
+           "decode_steps": ce.stats["steps"], "prefill_s": round(ce.stats["prefill_s"], 2),
+           "min_admit": a.min_admit, "max_wait_s": a.max_wait}
     print(json.dumps(out), flush=True)
 
 
