@@ -86,7 +86,7 @@ __device__ __forceinline__ bf16x8_t kv_operand(uint4 r) { return as_bf16x8(r); }
 __device__ __forceinline__ bf16x8_t kv_operand(uint2 r) { return as_bf16x8(fp8x8_to_bf16x8(r)); }
 
 template <int G, bool NT, bool F8 = false>
-__global__ void __launch_bounds__(256, 2) paged_decode_kernel(
+__global__ void __launch_bounds__(256, F8 ? 2 : 1) paged_decode_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ kc, const void* __restrict__ vc,
     const int32_t* __restrict__ block_tables, const int32_t* __restrict__ ctx_lens, float scale_log2, int Hkv,
     int max_blocks, int part_blocks, int P, int window, float v_scale, float* __restrict__ part_o,
