@@ -167,7 +167,13 @@ class ContinuousEngine:
             self.queue.extendleft(reversed(take))
             raise
         t = time.perf_counter()
-        first = self.engine._prefill([r.prompt for r in take], tables, self.sampling, self.seed, start)
+        try:
+            first = self.engine._prefill([r.prompt for r in take], tables, self.sampling, self.seed, start)
+        except BaseException:
+            # nothing was installed in a slot yet: return the blocks, put the requests back in front
+            self.engine._release(tables, fresh, failed=True)
+            self.queue.extendleft(reversed(take))
+            raise
         now = time.perf_counter()
         self.stats["prefill_s"] += now - t
         slots = [self.free.pop() for _ in take]

@@ -77,3 +77,21 @@ def test_continuous_gpu_graph_matches_generate():
     agree = sum(a == b for x, y in zip(got, want) for a, b in zip(x, y))
     assert [len(x) for x in got] == [len(x) for x in want]
     assert agree >= 0.95 * sum(len(x) for x in want), (got, want)
+
+
+def test_failed_admission_returns_blocks_and_requeues(monkeypatch):
+    model, kv = _setup("cpu")
+    eng = LLMEngine(model, kv, max_prefill_tokens=128, use_graph=False)
+    ce = ContinuousEngine(eng, max_slots=2, max_new_cap=8, max_prompt=64, steps_per_sync=2)
+    free0 = kv.pool.num_free()
+    ce.submit([1, 2, 3, 4], 4)
+
+    def boom(*a, **k):
+        raise RuntimeError("HIP out of memory")
+    monkeypatch.setattr(eng, "_prefill", boom)
+    with pytest.raises(RuntimeError):
+        ce.step()
+    cached = eng.prefix_cache.cached_blocks() if eng.prefix_cache else 0
+    assert kv.pool.num_free() + cached == free0 and len(ce.queue) == 1 and len(ce.free) == 2
+    monkeypatch.undo()
+    assert len(ce.run()) == 1
