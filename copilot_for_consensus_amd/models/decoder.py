@@ -82,7 +82,15 @@ PRESETS: dict[str, DecoderConfig] = {
                                 max_positions=8192, bos_id=128000, eos_id=128009),
     "llama-3-70b": DecoderConfig("llama-3-70b", 128256, 8192, 80, 64, 8, 128, 28672, rope_theta=5e5,
                                  max_positions=8192, bos_id=128000, eos_id=128009),
+    # Llama-2 7B / 13B (the reference's Ollama / llama.cpp docs quote decode speeds for both:
+    # docs/operations/ollama-gpu-setup.md:151-152, docs/operations/llm-gpu-setup.md:467,476).
+    # Plain multi-head attention: kv_heads == heads, i.e. G = 1 in the GQA-packed prefill kernel.
+    "llama-2-7b": DecoderConfig("llama-2-7b", 32000, 4096, 32, 32, 32, 128, 11008, rope_theta=1e4,
+                                max_positions=4096),
+    "llama-2-13b": DecoderConfig("llama-2-13b", 32000, 5120, 40, 40, 40, 128, 13824, rope_theta=1e4,
+                                 max_positions=4096),
     # small configs for tests / smoke runs
+    "tiny-mha": DecoderConfig("tiny-mha", 512, 256, 2, 2, 2, 128, 512, rope_theta=1e4, max_positions=4096),
     "tiny": DecoderConfig("tiny", 512, 256, 2, 4, 2, 128, 512, rope_theta=1e4, max_positions=4096),
     "small": DecoderConfig("small", 32000, 1024, 4, 8, 2, 128, 2816, rope_theta=1e6, max_positions=8192),
 }

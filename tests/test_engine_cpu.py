@@ -171,3 +171,21 @@ def test_fp8_reference_cache_round_trip():
         raise AssertionError("fp16 cache accepted")
     except ValueError:
         pass
+
+
+def test_llama2_presets_match_published_parameter_counts():
+    # HF Llama-2 checkpoints: 6,738,415,616 and 13,015,864,320 parameters
+    assert get_config("llama-2-7b").num_params() == 6_738_415_616
+    assert get_config("llama-2-13b").num_params() == 13_015_864_320
+    assert get_config("llama-2-13b").kv_heads == get_config("llama-2-13b").heads   # MHA, G = 1
+
+
+def test_mha_incremental_decode_matches_full_recompute():
+    """Multi-head attention (kv_heads == heads, the Llama-2 layout) through the paged engine."""
+    cfg = get_config("tiny-mha")
+    m = DecoderModel(DecoderWeights.random(cfg, "cpu", seed=4))
+    eng = LLMEngine(m, PagedKVCache(cfg.layers, 32, cfg.kv_heads, cfg.head_dim, "cpu"))
+    p = [1] + list(range(20, 60))
+    gen = eng.generate([p], 4, ignore_eos=True).tokens[0]
+    for t in range(1, 4):
+        assert eng.generate([p + gen[:t]], 1, ignore_eos=True).tokens[0][0] == gen[t]

@@ -120,3 +120,19 @@ def test_long_context_generation_matches_reference():
     assert [t[0] for t in outs[0]] == [t[0] for t in outs[1]]
     agree = sum(a == b for x, y in zip(*outs) for a, b in zip(x, y))
     assert agree >= 12, outs
+
+
+def test_mha_generation_matches_reference():
+    """Llama-2 layout (kv_heads == heads: G = 1 in the GQA-packed prefill kernel, one query head per
+    kv-head in split-KV decode) on the GPU engine vs the CPU reference engine."""
+    cfg = get_config("tiny-mha")
+    w = DecoderWeights.random(cfg, "cuda", seed=7)
+    prompts = [[1] + list(range(5, 5 + 300)), [1, 9, 8, 7], [1] + list(range(100, 171))]
+    outs = []
+    for model, dev in ((DecoderModel(w), "cuda"), (DecoderModel(_to_cpu_fp32_model(w)), "cpu")):
+        kv = PagedKVCache(cfg.layers, 40, cfg.kv_heads, cfg.head_dim, dev)
+        eng = LLMEngine(model, kv, max_prefill_tokens=128, use_graph=(dev == "cuda"))
+        outs.append(eng.generate(prompts, max_new_tokens=8, ignore_eos=True).tokens)
+    assert [t[0] for t in outs[0]] == [t[0] for t in outs[1]]
+    agree = sum(a == b for x, y in zip(*outs) for a, b in zip(x, y))
+    assert agree >= 0.8 * sum(len(x) for x in outs[1]), outs
