@@ -268,6 +268,9 @@ class DecoderModel:
         if weights.tp_size != 1 or (mode == "skinny" and not weights.gate_up_interleaved):
             mode = "lib"
         self.decode_gemm = mode
+        # B <= 4 decode steps on the GEMV kernel (needs the interleaved gate/up layout for SwiGLU)
+        self.decode_gemv = (os.environ.get("CFC_DECODE_GEMV", "1") != "0" and weights.gate_up_interleaved
+                            and mode == "splitk")
         self.fused_decode = mode == "skinny"
 
     def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
@@ -374,6 +377,9 @@ class DecoderModel:
         h = K.rmsnorm(x, w.layers[0]["attn_norm"], eps)
         s_o = K.lib_split_for(w.heads * cfg.head_dim, cfg.hidden)
         s_d = K.lib_split_for(w.ffn, cfg.hidden)
+        if self.decode_gemv and B <= K.GEMV_MAX_M:
+            return self._forward_decode_gemv(h, residual, positions, slots, ctx_lens, block_tables, kv,
+                                             attn_workspace, part_blocks)
         for i in range(cfg.layers):
             lw = w.layers[i]
             qkv = F.linear(h, lw["qkv"])
@@ -386,6 +392,27 @@ class DecoderModel:
             a = K.silu_mul(F.linear(h, lw["gate_up"]), interleaved=w.gate_up_interleaved)
             nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm
             h = K.lib_splitk_linear_residual_rmsnorm(a, lw["down"], s_d, residual, nxt, eps)
+        return h
+
+    def _forward_decode_gemv(self, h, residual, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
+                             part_blocks):
+        """Single-stream / small-batch decode (B <= 4): every projection on the weight-streaming GEMV
+        kernel (gemm.hip: gemv_kernel), SwiGLU in the gate/up GEMV's epilogue, o and down feeding the
+        residual + next-RMSNorm reduce.  Same rounding points as _forward_decode_splitk."""
+        cfg, w = self.cfg, self.w
+        B, eps = h.shape[0], cfg.rms_eps
+        for i in range(cfg.layers):
+            lw = w.layers[i]
+            qkv = K.gemv(h, lw["qkv"])
+            q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
+                                cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
+            attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
+                                            part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
+                                            k_scale=kv.k_scale, v_scale=kv.v_scale)
+            h = K.gemv_residual_rmsnorm(attn.view(B, -1), lw["o"], residual, lw["mlp_norm"], eps)
+            a = K.gemv(h, lw["gate_up"], "swiglu")
+            nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm
+            h = K.gemv_residual_rmsnorm(a, lw["down"], residual, nxt, eps)
         return h
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:

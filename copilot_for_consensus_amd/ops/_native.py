@@ -50,6 +50,7 @@ _KERNEL_SIGS = {
     "cfc_pool": [P, P, P, P, I, I, I, I, P],
     "cfc_skinny_gemm": [P, P, I, I, I, I, I, P, P, I, P],
     "cfc_splitk_reduce": [P, I, I, I, I, P, I, P],
+    "cfc_gemv": [P, P, I, I, I, I, P, P, I, P],
     "cfc_splitk_residual_rmsnorm": [P, I, I, I, P, P, F, P, P],
     "cfc_ar_region_bytes": [c_int64, P],
     "cfc_ar_alloc": [c_int64, P],

@@ -389,6 +389,48 @@ def lib_splitk_linear_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, split: 
     return out
 
 
+GEMV_MAX_M = 4   # decode batches up to this size take the weight-streaming GEMV (gemm.hip: gemv_kernel)
+
+
+def gemv(x: torch.Tensor, w: torch.Tensor, epi: str = "bf16", out: torch.Tensor | None = None) -> torch.Tensor:
+    """x [M <= 4, K] @ w[N, K]^T on the GEMV kernel.  ``epi``: "bf16" -> bf16 [M, N]; "f32" -> fp32
+    [M, N]; "swiglu" -> bf16 [M, N/2] = silu(gate) * up for 32-row interleaved gate/up weights."""
+    if not x.is_cuda:
+        y = torch.nn.functional.linear(x.float(), w.float())
+        if epi == "swiglu":
+            return ref.silu_mul_interleaved(y.to(x.dtype))
+        return y if epi == "f32" else y.to(x.dtype)
+    _req(x, torch.bfloat16, "x")
+    _req(w, torch.bfloat16, "w")
+    M, Kd = x.shape
+    N = w.shape[0]
+    if w.shape[1] != Kd or not (1 <= M <= GEMV_MAX_M) or not x.is_contiguous() or not w.is_contiguous():
+        raise ValueError(f"gemv: x {tuple(x.shape)} w {tuple(w.shape)} (M <= {GEMV_MAX_M}, contiguous)")
+    mode = {"f32": 0, "bf16": 1, "swiglu": 2}[epi]
+    if out is None:
+        shape = (M, N // 2) if epi == "swiglu" else (M, N)
+        out = torch.empty(shape, dtype=torch.float32 if epi == "f32" else torch.bfloat16, device=x.device)
+    yf, yb = (out.data_ptr(), None) if epi == "f32" else (None, out.data_ptr())
+    check(kernels().cfc_gemv(x.data_ptr(), w.data_ptr(), M, N, Kd, mode, yf, yb, out.shape[1], _stream(x)),
+          "cfc_gemv")
+    return out
+
+
+def gemv_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor,
+                          eps: float) -> torch.Tensor:
+    """residual += bf16(x @ w^T) via the GEMV (fp32 out) and the split = 1 residual + RMSNorm reduce;
+    returns RMSNorm(residual) * norm_w (same rounding points as lib_splitk_linear_residual_rmsnorm)."""
+    if not x.is_cuda:
+        return skinny_linear_residual_rmsnorm(x, w, residual, norm_w, eps)
+    M, N = x.shape[0], w.shape[0]
+    part = _workspace(x.device, M * N)[:M * N].view(M, N)
+    gemv(x, w, "f32", out=part)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    check(kernels().cfc_splitk_residual_rmsnorm(part.data_ptr(), 1, M, N, residual.data_ptr(), norm_w.data_ptr(),
+                                                float(eps), out.data_ptr(), _stream(x)), "cfc_splitk_residual_rmsnorm")
+    return out
+
+
 def lib_split_for(K: int, N: int) -> int:
     """Split factor for the batched split-K decode GEMM (measured on MI355X at M=128:
     down 4096x14336 -> 8 (29 vs 42 us), o 4096x4096 -> 4); 1 = not worth splitting."""

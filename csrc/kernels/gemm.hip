@@ -263,6 +263,102 @@ __global__ void __launch_bounds__(1024) splitk_residual_rmsnorm_kernel(const flo
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// GEMV for single-stream / small-batch decode (M <= 4): Y[M, N] = X[M, K] . W[N, K]^T.
+//
+// At M <= 4 a projection is a pure weight stream (0.5-2 flop per byte): no MFMA, no LDS.  Each
+// wave owns GV_RW = 2 rows of W and walks K in 512-element chunks (one 16-B load per lane per row);
+// GV_CPI = 8 chunks (16 x 16 B per lane, 16 KB per wave) are issued before any FMA so every wave
+// keeps its whole K=4096 slice in flight at once, and nontemporal loads keep the once-read weights
+// out of L2.  X rows are read from global (L2-resident, re-read once per wave = M/2 of W's bytes).
+// The 64 lane partials are summed with a butterfly.  Epilogues: fp32 store (feeds the residual +
+// RMSNorm reduce kernel with split = 1), bf16 store, or SwiGLU over the 32-row interleaved gate/up
+// weights (the wave's two rows are gate row j and up row j of output column j).
+// Grid: one 4-wave block per 8 W rows (4 output columns for SwiGLU) -> 512-3584 blocks for the
+// 7B shapes, i.e. >= 2 blocks per CU.
+constexpr int GV_RW = 2;
+constexpr int GV_CPI = 8;   // chunks in flight per row (4 for M > 2, to stay within 128 VGPRs + AGPRs)
+constexpr int GV_CHUNK = 512;
+enum { GV_F32 = 0, GV_BF16 = 1, GV_SWIGLU = 2 };
+typedef unsigned int gv_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 gv_stream(const uint16_t* p) {
+  const gv_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const gv_u32x4*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ float dot8(const uint4 a, const uint4 b) {
+  float fa[8], fb[8];
+  unpack8(a, fa);
+  unpack8(b, fb);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s = fmaf(fa[j], fb[j], s);
+  return s;
+}
+
+template <int MT, int EPI, int CPI = (MT > 2 ? GV_CPI / 2 : GV_CPI)>
+__global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W,
+                                                   int N, int K, float* __restrict__ yf, uint16_t* __restrict__ yb,
+                                                   int ldo, int ncols) {
+  const int lane = threadIdx.x & 63;
+  const int col = blockIdx.x * 4 + (threadIdx.x >> 6);   // output column group of this wave
+  if (col >= ncols) return;
+  int rows[GV_RW];
+  if constexpr (EPI == GV_SWIGLU) {
+    rows[0] = 64 * (col >> 5) + (col & 31);   // gate row of output column `col`
+    rows[1] = rows[0] + 32;                   // matching up row
+  } else {
+    rows[0] = GV_RW * col;
+    rows[1] = GV_RW * col + 1;
+  }
+  float acc[GV_RW][MT];
+#pragma unroll
+  for (int r = 0; r < GV_RW; ++r)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[r][m] = 0.f;
+
+  for (int k0 = 0; k0 < K; k0 += CPI * GV_CHUNK) {
+    uint4 w[GV_RW][CPI], x[MT][CPI];
+#pragma unroll
+    for (int c = 0; c < CPI; ++c) {
+      const int k = k0 + c * GV_CHUNK + lane * 8;
+#pragma unroll
+      for (int r = 0; r < GV_RW; ++r)
+        w[r][c] = k < K ? gv_stream(W + (size_t)rows[r] * K + k) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int c = 0; c < CPI; ++c) {
+      const int k = k0 + c * GV_CHUNK + lane * 8;
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        x[m][c] = k < K ? *reinterpret_cast<const uint4*>(X + (size_t)m * K + k) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int c = 0; c < CPI; ++c)
+#pragma unroll
+      for (int r = 0; r < GV_RW; ++r)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[r][m] += dot8(w[r][c], x[m][c]);
+  }
+#pragma unroll
+  for (int r = 0; r < GV_RW; ++r)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[r][m] = wave_sum(acc[r][m]);
+  if (lane != 0) return;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    if constexpr (EPI == GV_SWIGLU) {
+      const float g = bf2f(f2bf(acc[0][m])), u = bf2f(f2bf(acc[1][m]));   // bf16 GEMM output, as unfused
+      yb[(size_t)m * ldo + col] = f2bf(g / (1.f + __expf(-g)) * u);
+    } else if constexpr (EPI == GV_BF16) {
+      *reinterpret_cast<uint32_t*>(yb + (size_t)m * ldo + rows[0]) = pack2bf(acc[0][m], acc[1][m]);
+    } else {
+      *reinterpret_cast<float2*>(yf + (size_t)m * N + rows[0]) = make_float2(acc[0][m], acc[1][m]);
+    }
+  }
+}
 }  // namespace
 
 // epi: 0 = fp32 partials into `part` ([split][M][N]), 1 = bf16 into out (split must be 1),
@@ -307,5 +403,28 @@ CFC_API int cfc_splitk_residual_rmsnorm(const float* part, int split, int M, int
     default: splitk_residual_rmsnorm_kernel<0><<<M, threads, 0, stream>>>(SRR_ARGS); break;
   }
 #undef SRR_ARGS
+  return CFC_CHECK_LAUNCH();
+}
+
+// M <= 4 GEMV. epi 0: fp32 [M, N] into yf; 1: bf16 into yb (row stride ldo); 2: SwiGLU over the
+// interleaved gate/up W -> bf16 [M, N/2] into yb.  N even (epi 2: N % 64 == 0), K % 8 == 0.
+CFC_API int cfc_gemv(const void* x, const void* w, int M, int N, int K, int epi, float* yf, void* yb, int ldo,
+                     hipStream_t stream) {
+  if (M < 1 || M > 4 || N <= 0 || N % 2 || K <= 0 || K % 8) return -1;
+  if (epi == GV_SWIGLU && N % 64) return -1;
+  if ((epi == GV_F32 && !yf) || (epi != GV_F32 && !yb)) return -2;
+  const int ncols = epi == GV_SWIGLU ? N / 2 : N / GV_RW;
+  const dim3 grid((ncols + 3) / 4);
+#define GV_ARGS (const uint16_t*)x, (const uint16_t*)w, N, K, yf, (uint16_t*)yb, ldo, ncols
+#define GV_CASE(MT)                                                                          \
+  case MT:                                                                                   \
+    if (epi == GV_F32) gemv_kernel<MT, GV_F32><<<grid, 256, 0, stream>>>(GV_ARGS);           \
+    else if (epi == GV_BF16) gemv_kernel<MT, GV_BF16><<<grid, 256, 0, stream>>>(GV_ARGS);    \
+    else if (epi == GV_SWIGLU) gemv_kernel<MT, GV_SWIGLU><<<grid, 256, 0, stream>>>(GV_ARGS); \
+    else return -3;                                                                          \
+    break;
+  switch (M) { GV_CASE(1) GV_CASE(2) GV_CASE(3) GV_CASE(4) }
+#undef GV_CASE
+#undef GV_ARGS
   return CFC_CHECK_LAUNCH();
 }

@@ -136,3 +136,18 @@ def test_mha_generation_matches_reference():
     assert [t[0] for t in outs[0]] == [t[0] for t in outs[1]]
     agree = sum(a == b for x, y in zip(*outs) for a, b in zip(x, y))
     assert agree >= 0.8 * sum(len(x) for x in outs[1]), outs
+
+
+def test_gemv_decode_matches_splitk_decode(monkeypatch):
+    """B <= 4 decode on the GEMV kernel vs the library split-K decode path, same weights."""
+    cfg = get_config("small")
+    w = DecoderWeights.random(cfg, "cuda", seed=13)
+    res = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("CFC_DECODE_GEMV", flag)
+        model = DecoderModel(w)
+        assert model.decode_gemv == (flag == "1")
+        kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, "cuda")
+        res.append(LLMEngine(model, kv).generate([[1, 2, 3] * 100, [1, 7]], 24, ignore_eos=True).tokens)
+    agree = sum(a == b for x, y in zip(*res) for a, b in zip(x, y))
+    assert [t[0] for t in res[0]] == [t[0] for t in res[1]] and agree >= 0.75 * 48, res

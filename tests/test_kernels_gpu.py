@@ -386,3 +386,37 @@ def test_prefill_attention_fp8(G):
     out = K.prefill_attention(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), cu_t.to(DEV), cl.to(DEV),
                               1 / math.sqrt(D), k_scale=0.5, v_scale=2.0)
     _close(out, ref, 2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,Kd", [(6144, 4096), (512, 11008), (258, 1000)])
+def test_gemv_bf16_and_f32(M, N, Kd):
+    """GEMV (gemm.hip: gemv_kernel) vs fp32 matmul; K not a multiple of the 512-wide chunk included."""
+    x = torch.randn(M, Kd, device=DEV).bfloat16()
+    w = (torch.randn(N, Kd, device=DEV) / math.sqrt(Kd)).bfloat16()
+    ref = x.float() @ w.float().t()
+    _close(K.gemv(x, w, "f32"), ref, atol=2e-3, rtol=1e-3)
+    _close(K.gemv(x, w, "bf16"), ref, atol=2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 4])
+def test_gemv_swiglu_interleaved(M):
+    Kd, F = 4096, 1024
+    x = torch.randn(M, Kd, device=DEV).bfloat16()
+    gu = (torch.randn(2 * F, Kd, device=DEV) / math.sqrt(Kd)).bfloat16()
+    y = (x.float() @ gu.float().t()).bfloat16().float()
+    ref = torch.nn.functional.silu(y[:, :F]) * y[:, F:]
+    _close(K.gemv(x, R.interleave_gate_up(gu), "swiglu"), ref, atol=2e-2)
+
+
+def test_gemv_residual_rmsnorm_matches_reference():
+    M, Kd, N = 2, 14336, 4096
+    x = torch.randn(M, Kd, device=DEV).bfloat16()
+    w = (torch.randn(N, Kd, device=DEV) / math.sqrt(Kd)).bfloat16()
+    res = torch.randn(M, N, device=DEV).bfloat16()
+    g = torch.rand(N, device=DEV).bfloat16() + 0.5
+    r2 = res.clone()
+    out = K.gemv_residual_rmsnorm(x, w, r2, g, 1e-5)
+    ref_o, ref_r = R.rmsnorm((x.float() @ w.float().t()).bfloat16(), g, 1e-5, res)
+    _close(r2, ref_r, atol=3e-2)
+    _close(out, ref_o, atol=5e-2)
