@@ -270,22 +270,50 @@ __global__ void __launch_bounds__(256, F8 ? 2 : 1) paged_decode_kernel(
 __global__ void __launch_bounds__(128) decode_combine_kernel(const float* __restrict__ part_o,
                                                              const float* __restrict__ part_ml, int P, int Hq,
                                                              uint16_t* __restrict__ out) {
-  constexpr int D = 128;
+  // Small-batch decode runs with up to ~64 partitions per head: the (m, l) pairs are loaded by all
+  // 128 threads at once and the weights exp2(m_p - M) / L go through LDS, so the only per-thread
+  // loop is P independent part_o loads (unrolled) instead of three dependent P-long chains.
+  constexpr int D = 128, PMAX = 256;
+  __shared__ float wsh[PMAX];
+  __shared__ float red[2];
   const int head = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
   const size_t base = ((size_t)b * Hq + head) * P;
-  float M = -INFINITY;
-  for (int p = 0; p < P; ++p) M = fmaxf(M, part_ml[(base + p) * 2]);
-  float L = 0.f, O = 0.f;
-  if (M != -INFINITY) {
-    for (int p = 0; p < P; ++p) {
-      const float mp = part_ml[(base + p) * 2];
-      if (mp == -INFINITY) continue;
-      const float f = exp2f(mp - M);
-      L += part_ml[(base + p) * 2 + 1] * f;
-      O += part_o[(base + p) * D + d] * f;
+  const int lane = d & 63, wid = d >> 6;
+  float O = 0.f, Ltot = 0.f, Mrun = -INFINITY;
+  for (int p0 = 0; p0 < P; p0 += PMAX) {   // one pass for P <= 256
+    const int np = min(PMAX, P - p0);
+    float mloc = -INFINITY;
+    for (int i = d; i < np; i += 128) mloc = fmaxf(mloc, part_ml[(base + p0 + i) * 2]);
+    mloc = wave_max(mloc);
+    if (lane == 0) red[wid] = mloc;
+    __syncthreads();
+    const float M = fmaxf(red[0], red[1]);
+    __syncthreads();
+    float lsum = 0.f;
+    for (int i = d; i < np; i += 128) {
+      const float mp = part_ml[(base + p0 + i) * 2];
+      const float f = (M == -INFINITY || mp == -INFINITY) ? 0.f : exp2f(mp - M);
+      wsh[i] = f;
+      lsum += part_ml[(base + p0 + i) * 2 + 1] * f;
+    }
+    lsum = wave_sum(lsum);
+    if (lane == 0) red[wid] = lsum;
+    __syncthreads();
+    const float L = red[0] + red[1];
+    float o = 0.f;
+#pragma unroll 8
+    for (int i = 0; i < np; ++i) o += part_o[(base + p0 + i) * D + d] * wsh[i];
+    __syncthreads();
+    // merge this pass into the running (O, L, Mrun); every thread holds the same M, L
+    if (p0 == 0) {
+      O = o; Ltot = L; Mrun = M;
+    } else {
+      const float Mn = fmaxf(Mrun, M);
+      const float a = Mrun == -INFINITY ? 0.f : exp2f(Mrun - Mn), c = M == -INFINITY ? 0.f : exp2f(M - Mn);
+      O = O * a + o * c; Ltot = Ltot * a + L * c; Mrun = Mn;
     }
   }
-  out[((size_t)b * Hq + head) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+  out[((size_t)b * Hq + head) * D + d] = f2bf(Ltot > 0.f ? O / Ltot : 0.f);
 }
 
 // ------------------------------------------------------------------------------------------

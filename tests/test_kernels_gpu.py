@@ -122,7 +122,7 @@ def _fill_cache(ctx_lens, Hkv, D, extra_blocks=3):
 
 
 @pytest.mark.parametrize("G", [1, 4, 8])
-@pytest.mark.parametrize("part_blocks", [4, 1000, -1, -2, -3, -7])
+@pytest.mark.parametrize("part_blocks", [4, 1000, -1, -2, -3, -7, -300])
 def test_paged_decode(G, part_blocks):
     Hkv, D = 2, 128
     Hq = Hkv * G
