@@ -417,7 +417,11 @@ class DecoderModel:
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """[B, V] logits (all-gathered over the vocab-parallel shards)."""
-        local = F.linear(hidden, self.w.lm_head)
+        if (self.decode_gemv and hidden.is_cuda and hidden.shape[0] <= K.GEMV_MAX_M
+                and hidden.is_contiguous()):
+            local = K.gemv(hidden, self.w.lm_head)   # 262 MB weight stream: 4.6 -> ~6 TB/s at B=1
+        else:
+            local = F.linear(hidden, self.w.lm_head)
         if self.w.tp_size == 1:
             return local
         parts = [torch.empty_like(local) for _ in range(self.w.tp_size)]
