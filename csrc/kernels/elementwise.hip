@@ -214,7 +214,7 @@ __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
 // One workgroup per row. temperature <= 0 => greedy argmax (lowest index wins ties);
 // otherwise Gumbel-max sampling: argmax(logit/T + Gumbel(seed, step, row, idx)), which draws
 // exactly from softmax(logit/T).  `step` is read from device memory so graph replays advance it.
-__global__ void __launch_bounds__(256) sample_kernel(const uint16_t* __restrict__ logits, int V, float temperature,
+__global__ void __launch_bounds__(1024) sample_kernel(const uint16_t* __restrict__ logits, int V, float temperature,
                                                      uint32_t seed, const int32_t* __restrict__ step_ptr,
                                                      int32_t* __restrict__ out_ids) {
   const int row = blockIdx.x;
@@ -231,22 +231,35 @@ __global__ void __launch_bounds__(256) sample_kernel(const uint16_t* __restrict_
     const float u = ((h >> 8) + 0.5f) * (1.f / 16777216.f);
     return x * inv_t - __logf(-__logf(u));
   };
-  for (int c = threadIdx.x; c < nvec; c += blockDim.x) {
-    float v[8];
-    unpack8(reinterpret_cast<const uint4*>(lr)[c], v);
+  // 1024 threads x 4 independent 16-B loads in flight: a 32k-vocab row is one memory round trip
+  // (the previous 256-thread loop was 16 dependent ones: 16 us per decode step at B = 1)
+  for (int c0 = threadIdx.x; c0 < nvec; c0 += 4 * blockDim.x) {
+    uint4 raw[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int idx = c * 8 + j;
-      const float x = score(v[j], idx);
-      if (x > best || (x == best && idx < best_i)) { best = x; best_i = idx; }
+    for (int u = 0; u < 4; ++u) {
+      const int c = c0 + u * blockDim.x;
+      raw[u] = c < nvec ? reinterpret_cast<const uint4*>(lr)[c] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = c0 + u * blockDim.x;
+      if (c >= nvec) break;
+      float v[8];
+      unpack8(raw[u], v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int idx = c * 8 + j;
+        const float x = score(v[j], idx);
+        if (x > best || (x == best && idx < best_i)) { best = x; best_i = idx; }
+      }
     }
   }
   for (int idx = nvec * 8 + threadIdx.x; idx < V; idx += blockDim.x) {  // tail (V % 8)
     const float x = score(bf2f(lr[idx]), idx);
     if (x > best || (x == best && idx < best_i)) { best = x; best_i = idx; }
   }
-  __shared__ float sb[4];
-  __shared__ int si[4];
+  __shared__ float sb[16];
+  __shared__ int si[16];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float ob = __shfl_xor(best, o, 64);
@@ -564,7 +577,7 @@ CFC_API int cfc_sample_truncated(const void* logits, int B, int V, float tempera
 CFC_API int cfc_sample(const void* logits, int B, int V, float temperature, uint32_t seed, const int32_t* step_ptr,
                        int32_t* out_ids, hipStream_t stream) {
   if (B == 0) return 0;
-  sample_kernel<<<B, 256, 0, stream>>>((const uint16_t*)logits, V, temperature, seed, step_ptr, out_ids);
+  sample_kernel<<<B, 1024, 0, stream>>>((const uint16_t*)logits, V, temperature, seed, step_ptr, out_ids);
   return CFC_CHECK_LAUNCH();
 }
 

@@ -420,3 +420,15 @@ def test_gemv_residual_rmsnorm_matches_reference():
     ref_o, ref_r = R.rmsnorm((x.float() @ w.float().t()).bfloat16(), g, 1e-5, res)
     _close(r2, ref_r, atol=3e-2)
     _close(out, ref_o, atol=5e-2)
+
+
+@pytest.mark.parametrize("V", [32000, 32003, 128256, 7])
+def test_greedy_sample_vocab_sizes_and_ties(V):
+    """1024-thread sampler: 4 loads in flight per thread, scalar tail when V % 8 != 0, lowest index on ties."""
+    logits = torch.randn(5, V, device=DEV).bfloat16()
+    logits[1] = 0.0                                   # all tied -> index 0
+    logits[2, V - 1] = 100.0                          # maximum in the last (tail) element
+    out = torch.empty(5, dtype=torch.int32, device=DEV)
+    K.sample(logits, out)
+    assert out.cpu().tolist() == R.sample_greedy(logits.cpu()).tolist()
+    assert out[1].item() == 0 and out[2].item() == V - 1
