@@ -269,8 +269,10 @@ class DecoderModel:
             mode = "lib"
         self.decode_gemm = mode
         # B <= 4 decode steps on the GEMV kernel (needs the interleaved gate/up layout for SwiGLU)
+        gemv_shapes = (self.cfg.hidden % 8 == 0 and (weights.heads * self.cfg.head_dim) % 8 == 0
+                       and weights.ffn % 32 == 0 and self.cfg.head_dim % 2 == 0)
         self.decode_gemv = (os.environ.get("CFC_DECODE_GEMV", "1") != "0" and weights.gate_up_interleaved
-                            and mode == "splitk")
+                            and mode == "splitk" and gemv_shapes)
         self.fused_decode = mode == "skinny"
 
     def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
@@ -417,8 +419,11 @@ class DecoderModel:
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """[B, V] logits (all-gathered over the vocab-parallel shards)."""
+        head = self.w.lm_head
         if (self.decode_gemv and hidden.is_cuda and hidden.shape[0] <= K.GEMV_MAX_M
-                and hidden.is_contiguous()):
+                and hidden.is_contiguous() and head.shape[0] % 2 == 0 and head.shape[1] % 8 == 0):
+            # (the GEMV takes row pairs and 16-byte K slices: odd vocabularies, e.g. 32001-token
+            # fine-tunes, stay on the library GEMM)
             local = K.gemv(hidden, self.w.lm_head)   # 262 MB weight stream: 4.6 -> ~6 TB/s at B=1
         else:
             local = F.linear(hidden, self.w.lm_head)

@@ -278,14 +278,22 @@ def encoder_attention(qkv, cu_seqlens, H, D, scale, max_seqlen, tiles=None, out=
 
 SKINNY_MAX_M = 256          # above this the library GEMMs win (prefill shapes)
 _workspaces: dict = {}
+# Superseded workspaces are never freed: a hipGraph captured while one of them was current keeps
+# its raw pointer and writes fp32 partials through it on every replay.  Growth at least doubles,
+# so the retired buffers add up to less than the live one.
+_retired_workspaces: list = []
 
 
 def _workspace(device, numel: int) -> torch.Tensor:
     """Grow-only fp32 split-K workspace per device (sized during the eager warm-up, so hipGraph
-    capture sees a fixed pointer)."""
+    capture sees a fixed pointer; see _retired_workspaces for why old ones stay allocated)."""
+    device = torch.device(device)
     ws = _workspaces.get(device)
     if ws is None or ws.numel() < numel:
-        ws = torch.empty(max(numel, 1 << 20), dtype=torch.float32, device=device)
+        size = max(numel, 1 << 20, 2 * ws.numel() if ws is not None else 0)
+        if ws is not None:
+            _retired_workspaces.append(ws)
+        ws = torch.empty(size, dtype=torch.float32, device=device)
         _workspaces[device] = ws
     return ws
 

@@ -204,7 +204,9 @@ def bias_gelu(x, bias):
 
 
 def sample_greedy(logits):
-    return torch.argmax(logits.float(), -1).to(torch.int32)
+    """argmax, NaN ranked as -inf (as the HIP sampler): an all-NaN row gives token 0."""
+    x = logits.float()
+    return torch.argmax(torch.nan_to_num(x, nan=-math.inf, posinf=math.inf, neginf=-math.inf), -1).to(torch.int32)
 
 
 def truncation_keep(sorted_logits: torch.Tensor, top_p: float, min_p: float) -> int:
@@ -227,6 +229,7 @@ def sample_truncated(logits, temperature, top_k, top_p, min_p, generator=None, c
     """top-k -> top-p -> min-p -> temperature -> draw (ties ordered by index), one id per row."""
     out = []
     for row in logits.float():
+        row = torch.nan_to_num(row, nan=-math.inf, posinf=math.inf, neginf=-math.inf)
         k = min(top_k if top_k > 0 else cap, cap, row.numel())
         vals, idx = torch.sort(row, descending=True, stable=True)
         vals, idx = vals[:k], idx[:k]

@@ -61,12 +61,41 @@ class OIDCProvider(IdentityProvider):
         req = urllib.request.Request(url, headers={"Authorization": f"Bearer {token}", "Accept": "application/json"})
         return json.loads(urllib.request.urlopen(req, timeout=15).read())
 
+    require_nonce = True
+
+    @staticmethod
+    def id_token_claims(id_token: str) -> dict:
+        """Payload of an ID token received straight from the token endpoint over TLS (OIDC Core
+        3.1.3.7 lets the code-flow client rely on the TLS server check instead of the signature)."""
+        try:
+            body = id_token.split(".")[1]
+            return json.loads(base64.urlsafe_b64decode(body + "=" * (-len(body) % 4)))
+        except (IndexError, ValueError) as e:
+            raise PermissionError("malformed id_token") from e
+
     def exchange_code(self, code, code_verifier, nonce):
         tok = self._post(self.token_endpoint, {"grant_type": "authorization_code", "code": code,
                                                "redirect_uri": self.redirect_uri, "client_id": self.client_id,
                                                "client_secret": self.client_secret, "code_verifier": code_verifier})
+        if "access_token" not in tok:
+            raise PermissionError(f"token endpoint refused the code: {tok.get('error', 'no access_token')}")
+        id_token = tok.get("id_token")
+        if id_token:
+            claims = self.id_token_claims(id_token)
+            if claims.get("nonce") != nonce:
+                raise PermissionError("id_token nonce mismatch")
+            aud = claims.get("aud")
+            if aud is not None and self.client_id not in (aud if isinstance(aud, list) else [aud]):
+                raise PermissionError("id_token audience mismatch")
+        elif self.require_nonce and "openid" in self.scope.split():
+            # an OpenID provider must return an id_token carrying our nonce (plain OAuth providers
+            # such as GitHub do not request the openid scope and have no nonce to check)
+            raise PermissionError("OpenID provider returned no id_token to check the nonce against")
         info = self._get(self.userinfo_endpoint, tok["access_token"])
-        return {"sub": f"{self.name}:{info.get('sub') or info.get('id')}", "email": info.get("email"),
+        subject = info.get("sub") or info.get("id")
+        if subject in (None, ""):
+            raise PermissionError("userinfo has no subject (sub / id)")
+        return {"sub": f"{self.name}:{subject}", "email": info.get("email"),
                 "name": info.get("name") or info.get("login"), "provider": self.name}
 
 
@@ -225,6 +254,9 @@ class AuthService:
                  require_pkce: bool = True, require_nonce: bool = True, state_ttl: int = 600):
         self.jwt, self.roles, self.providers = jwt_manager, role_store, providers
         self.require_pkce, self.require_nonce = require_pkce, require_nonce
+        for p in providers.values():   # the nonce is checked inside OIDCProvider.exchange_code
+            if isinstance(p, OIDCProvider):
+                p.require_nonce = require_nonce
         self._pending: dict[str, dict[str, Any]] = {}
         self.state_ttl = state_ttl
         self._lock = threading.Lock()

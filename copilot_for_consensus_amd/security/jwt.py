@@ -113,6 +113,10 @@ class RSAKey:
         if self.p:
             s1, s2 = pow(m, self.dp, self.p), pow(m, self.dq, self.q)
             s = s2 + self.q * ((self.qinv * (s1 - s2)) % self.p)
+            # a fault in either half-exponentiation leaks a factor of n through gcd(s^e - m, n)
+            # (Boneh-DeMillo-Lipton): check the signature before it leaves
+            if pow(s, self.e, self.n) != m:
+                raise JWTError("RSA-CRT signature failed its self-check")
         else:
             s = pow(m, self.d, self.n)
         return _int_to_b(s, self.size)
@@ -182,12 +186,20 @@ def _jadd(P, Q):
 
 
 def _jmul(k: int, pt) -> tuple[int, int] | None:
-    R, Q = (0, 1, 0), (pt[0], pt[1], 1)
-    while k:
-        if k & 1:
-            R = _jadd(R, Q)
-        Q = _jdouble(Q)
-        k >>= 1
+    """k * pt by a Montgomery ladder over a fixed 258-bit schedule: k is first replaced by k + N
+    or k + 2N (same point, since N * pt = O), so the top bit and the number of steps never depend
+    on the scalar, and every step does one add and one double whatever the bit is (the bit only
+    selects which register receives which result)."""
+    k %= _N
+    k += _N
+    if k.bit_length() <= 256:
+        k += _N
+    R0, R1 = (0, 1, 0), (pt[0], pt[1], 1)
+    for i in range(257, -1, -1):
+        b = (k >> i) & 1
+        S, D = _jadd(R0, R1), _jdouble(R1 if b else R0)
+        R0, R1 = (S, D) if b else (D, S)
+    R = R0
     if R[2] == 0:
         return None
     zi = pow(R[2], -1, _P)

@@ -211,6 +211,10 @@ __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
   return x;
 }
 
+// NaN logits rank as -inf in both samplers, so an all-NaN row still yields a defined token (the
+// lowest index) instead of an index that matched no comparison.
+__device__ __forceinline__ float logit_nan_as_ninf(float x) { return x != x ? -INFINITY : x; }
+
 // One workgroup per row. temperature <= 0 => greedy argmax (lowest index wins ties);
 // otherwise Gumbel-max sampling: argmax(logit/T + Gumbel(seed, step, row, idx)), which draws
 // exactly from softmax(logit/T).  `step` is read from device memory so graph replays advance it.
@@ -226,6 +230,7 @@ __global__ void __launch_bounds__(1024) sample_kernel(const uint16_t* __restrict
   const bool sample = temperature > 0.f;
   const float inv_t = sample ? 1.f / temperature : 1.f;
   auto score = [&](float x, int idx) -> float {
+    x = logit_nan_as_ninf(x);
     if (!sample) return x;
     const uint32_t h = hash_u32(seed ^ hash_u32(step * 0x9E3779B9u ^ hash_u32(row * 0x85EBCA6Bu ^ (uint32_t)idx)));
     const float u = ((h >> 8) + 0.5f) * (1.f / 16777216.f);
@@ -272,7 +277,9 @@ __global__ void __launch_bounds__(1024) sample_kernel(const uint16_t* __restrict
   if (threadIdx.x == 0) {
     for (int i = 1; i < (int)(blockDim.x >> 6); ++i)
       if (sb[i] > best || (sb[i] == best && si[i] < best_i)) { best = sb[i]; best_i = si[i]; }
-    out_ids[row] = best_i;
+    // an all-NaN / all -inf row matches no comparison: emit token 0 instead of an index past the
+    // vocabulary (the next step's embedding gather would read outside the table)
+    out_ids[row] = (unsigned)best_i < (unsigned)V ? best_i : 0;
   }
 }
 
@@ -316,7 +323,7 @@ __global__ void __launch_bounds__(256) sample_topk_kernel(const uint16_t* __rest
     hist[tid] = 0;
     __syncthreads();
     for (int i = tid; i < V; i += 256) {
-      const uint32_t k = order_key(bf2f(lr[i]));
+      const uint32_t k = order_key(logit_nan_as_ninf(bf2f(lr[i])));
       if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 0xFF], 1u);
     }
     __syncthreads();
@@ -341,7 +348,7 @@ __global__ void __launch_bounds__(256) sample_topk_kernel(const uint16_t* __rest
   if (tid == 0) s_n = 0;
   __syncthreads();
   for (int i = tid; i < V; i += 256) {
-    const float f = bf2f(lr[i]);
+    const float f = logit_nan_as_ninf(bf2f(lr[i]));
     if (order_key(f) > prefix) {
       const int slot = atomicAdd(&s_n, 1);
       cv[slot] = f;
@@ -354,7 +361,7 @@ __global__ void __launch_bounds__(256) sample_topk_kernel(const uint16_t* __rest
     int found = 0;
     for (int base = lo; base < hi && found < (int)remaining; base += 64) {
       const int i = base + lane;
-      const bool tie = i < hi && order_key(bf2f(lr[i])) == prefix;
+      const bool tie = i < hi && order_key(logit_nan_as_ninf(bf2f(lr[i]))) == prefix;
       const unsigned long long m = __ballot(tie);
       if (tie) {
         const int pos = found + __popcll(m & ((1ull << lane) - 1ull));
@@ -368,7 +375,7 @@ __global__ void __launch_bounds__(256) sample_topk_kernel(const uint16_t* __rest
   if (tid == 0) {
     int n0 = s_n;
     for (int w = 0; w < 4 && n0 < K; ++w)
-      for (int j = 0; j < tie_n[w] && n0 < K; ++j) { ci[n0] = tie_i[w][j]; cv[n0] = bf2f(lr[tie_i[w][j]]); ++n0; }
+      for (int j = 0; j < tie_n[w] && n0 < K; ++j) { ci[n0] = tie_i[w][j]; cv[n0] = logit_nan_as_ninf(bf2f(lr[tie_i[w][j]])); ++n0; }
     s_n = n0;
   }
   __syncthreads();
@@ -418,7 +425,7 @@ __global__ void __launch_bounds__(256) sample_topk_kernel(const uint16_t* __rest
       const int oi = __shfl_xor(best_i, o, 64);
       if (ob > best || (ob == best && oi < best_i)) { best = ob; best_i = oi; }
     }
-    if (tid == 0) out_ids[row] = best_i;
+    if (tid == 0) out_ids[row] = (unsigned)best_i < (unsigned)V ? best_i : 0;  // never outside the vocabulary
   }
 }
 

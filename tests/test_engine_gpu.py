@@ -151,3 +151,45 @@ def test_gemv_decode_matches_splitk_decode(monkeypatch):
         res.append(LLMEngine(model, kv).generate([[1, 2, 3] * 100, [1, 7]], 24, ignore_eos=True).tokens)
     agree = sum(a == b for x, y in zip(*res) for a, b in zip(x, y))
     assert [t[0] for t in res[0]] == [t[0] for t in res[1]] and agree >= 0.75 * 48, res
+
+
+def test_small_graph_survives_workspace_growth():
+    """A B=2 hipGraph (GEMV decode, fp32 partials in the shared split-K workspace) captured before a
+    large batch grows the workspace must still be correct when replayed afterwards (the superseded
+    buffer stays allocated)."""
+    from copilot_for_consensus_amd.ops import kernels as K
+
+    cfg = get_config("small")
+    w = DecoderWeights.random(cfg, "cuda", seed=17)
+    m = DecoderModel(w)
+    small = [[1, 2, 3] * 40, [1, 9, 4] * 11]
+    kv = PagedKVCache(cfg.layers, 1024, cfg.kv_heads, cfg.head_dim, "cuda")
+    eng = LLMEngine(m, kv, use_graph=True)
+    first = eng.generate(small, 16, ignore_eos=True).tokens
+    g = torch.Generator().manual_seed(4)
+    big = [[1] + torch.randint(3, cfg.vocab_size, (200,), generator=g).tolist() for _ in range(64)]
+    eng.generate(big, 4, ignore_eos=True)
+    ws = K._workspaces[torch.device("cuda", torch.cuda.current_device())]
+    K._workspace(ws.device, 4 * ws.numel())           # force a growth past anything captured so far
+    junk = torch.full((ws.numel(),), float("nan"), device="cuda")   # likely reuses freed memory
+    again = eng.generate(small, 16, ignore_eos=True).tokens
+    del junk
+    kv2 = PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, "cuda")
+    eager = LLMEngine(m, kv2, use_graph=False).generate(small, 16, ignore_eos=True).tokens
+    assert again == first == eager
+
+
+def test_odd_vocab_lm_head_single_stream():
+    """An odd vocabulary (e.g. 32001-token fine-tunes) keeps the lm_head off the row-pair GEMV."""
+    from copilot_for_consensus_amd.models.decoder import DecoderConfig
+
+    cfg = DecoderConfig("tiny-odd", 517, 256, 2, 4, 2, 128, 512, rope_theta=1e4, max_positions=4096)
+    w = DecoderWeights.random(cfg, "cuda", seed=21)
+    prompts = [[1] + list(range(5, 60))]
+    outs = []
+    for model, dev in ((DecoderModel(w), "cuda"), (DecoderModel(_to_cpu_fp32_model(w)), "cpu")):
+        kv = PagedKVCache(cfg.layers, 16, cfg.kv_heads, cfg.head_dim, dev)
+        outs.append(LLMEngine(model, kv, use_graph=(dev == "cuda")).generate(prompts, 8, ignore_eos=True).tokens)
+    assert all(0 <= t < cfg.vocab_size for t in outs[0][0])
+    assert outs[0][0][0] == outs[1][0][0]
+    assert sum(a == b for a, b in zip(outs[0][0], outs[1][0])) >= 6, outs

@@ -432,3 +432,16 @@ def test_greedy_sample_vocab_sizes_and_ties(V):
     K.sample(logits, out)
     assert out.cpu().tolist() == R.sample_greedy(logits.cpu()).tolist()
     assert out[1].item() == 0 and out[2].item() == V - 1
+
+
+@pytest.mark.parametrize("V", [32000, 517])
+def test_sample_all_nan_row_stays_in_vocab(V):
+    """A row of NaN logits matches no comparison; the sampler must still emit an index inside the
+    vocabulary (the next embedding gather reads it)."""
+    logits = torch.randn(3, V, device=DEV).bfloat16()
+    logits[1] = float("nan")
+    for t in (0.0, 0.7, K.SamplingParams(0.7, top_k=40, top_p=0.95, min_p=0.05)):
+        out = torch.empty(3, dtype=torch.int32, device=DEV)
+        K.sample(logits, out, temperature=t, seed=3)
+        ids = out.cpu().tolist()
+        assert all(0 <= i < V for i in ids), (t, ids)

@@ -204,3 +204,80 @@ def test_middleware_roles_and_http_codes():
     assert r.status_code == 200 and r.json() == {"sub": "a"}
     other_aud = mgr.mint_token("a", {"roles": ["admin"]}, audience="elsewhere")
     assert c.get("/secret", headers={"Authorization": f"Bearer {other_aud}"}).status_code == 401
+
+
+class _FakeOIDC:
+    """OIDCProvider with the two HTTP calls stubbed out."""
+
+    @staticmethod
+    def make(token_resp: dict, userinfo: dict, scope: str = "openid email profile"):
+        from copilot_for_consensus_amd.security.auth import OIDCProvider
+
+        p = OIDCProvider("acme", "client-1", "secret", "https://app/cb", "https://idp/authorize", "https://idp/token",
+                         "https://idp/userinfo", scope=scope)
+        p._post = lambda url, data: dict(token_resp)
+        p._get = lambda url, token: dict(userinfo)
+        return p
+
+
+def _id_token(claims: dict) -> str:
+    import json
+
+    def enc(d):
+        return base64.urlsafe_b64encode(json.dumps(d).encode()).rstrip(b"=").decode()
+    return f"{enc({'alg': 'RS256'})}.{enc(claims)}.sig"
+
+
+def test_oidc_exchange_checks_nonce_audience_and_subject():
+    ok = {"access_token": "at", "id_token": _id_token({"nonce": "n1", "aud": "client-1", "sub": "u"})}
+    p = _FakeOIDC.make(ok, {"sub": "u", "email": "u@x"})
+    assert p.exchange_code("c", "v", "n1")["sub"] == "acme:u"
+    with pytest.raises(PermissionError, match="nonce"):
+        p.exchange_code("c", "v", "other-nonce")
+    bad_aud = {"access_token": "at", "id_token": _id_token({"nonce": "n1", "aud": ["someone-else"]})}
+    with pytest.raises(PermissionError, match="audience"):
+        _FakeOIDC.make(bad_aud, {"sub": "u"}).exchange_code("c", "v", "n1")
+    # an OpenID provider that returns no id_token cannot prove the nonce
+    with pytest.raises(PermissionError, match="id_token"):
+        _FakeOIDC.make({"access_token": "at"}, {"sub": "u"}).exchange_code("c", "v", "n1")
+    # plain OAuth (GitHub-style, no openid scope): no id_token expected
+    gh = _FakeOIDC.make({"access_token": "at"}, {"id": 42, "login": "octo"}, scope="read:user")
+    assert gh.exchange_code("c", "v", "n1") == {"sub": "acme:42", "email": None, "name": "octo", "provider": "acme"}
+    # userinfo without sub / id must not collapse every such user into "acme:None"
+    with pytest.raises(PermissionError, match="subject"):
+        _FakeOIDC.make({"access_token": "at"}, {"email": "x@y"}, scope="read:user").exchange_code("c", "v", "n")
+
+
+def test_auth_service_require_nonce_flag_reaches_providers():
+    p = _FakeOIDC.make({"access_token": "at"}, {"sub": "u"})
+    store = InMemoryDocumentStore()
+    mgr = J.JWTManager(J.HMACSigner("k"))
+    svc = AuthService(mgr, RoleStore(store), {"acme": p}, require_nonce=False)
+    assert p.require_nonce is False
+    st = svc.initiate_login("acme")["state"]
+    assert svc.handle_callback("code", st)["user"]["user_id"] == "acme:u"
+
+
+def test_es256_ladder_matches_double_and_add():
+    import secrets as _s
+
+    def naive(k, pt):
+        R, Q = (0, 1, 0), (pt[0], pt[1], 1)
+        while k:
+            if k & 1:
+                R = J._jadd(R, Q)
+            Q = J._jdouble(Q)
+            k >>= 1
+        zi = pow(R[2], -1, J._P)
+        return (R[0] * zi * zi % J._P, R[1] * zi * zi * zi % J._P)
+
+    for k in (1, 2, 3, J._N - 1, _s.randbelow(J._N - 1) + 1):
+        assert J._jmul(k, J._G) == naive(k, J._G)
+    assert J._jmul(J._N, J._G) is None
+
+
+def test_rsa_crt_fault_is_caught():
+    key = J.RSAKey.generate(1024)
+    key.dp ^= 1 << 5          # simulate a faulty half-exponentiation
+    with pytest.raises(J.JWTError, match="self-check"):
+        key.sign(b"payload")
