@@ -439,6 +439,33 @@ def gemv_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tens
     return out
 
 
+def splitk_reduce(part: torch.Tensor, out: torch.Tensor | None = None, swiglu: bool = False) -> torch.Tensor:
+    """Sum fp32 slabs [split, M, N] -> bf16 [M, N] (or silu(gate) * up [M, N/2] for interleaved gate/up)."""
+    split, M, N = part.shape
+    if not part.is_cuda:
+        y = part.sum(0).to(torch.bfloat16)
+        return ref.silu_mul_interleaved(y) if swiglu else y
+    cols = N // 2 if swiglu else N
+    out = torch.empty(M, cols, dtype=torch.bfloat16, device=part.device) if out is None else out
+    check(kernels().cfc_splitk_reduce(part.data_ptr(), split, M, N, 1 if swiglu else 0, out.data_ptr(), out.shape[1],
+                                      _stream(part)), "cfc_splitk_reduce")
+    return out
+
+
+def splitk_residual_rmsnorm(part: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor, eps: float) -> torch.Tensor:
+    """residual += bf16(sum of fp32 slabs [split, M, N]); returns RMSNorm(residual) * norm_w."""
+    split, M, N = part.shape
+    if not part.is_cuda:
+        y = part.sum(0).to(residual.dtype)
+        o, r = ref.rmsnorm(y, norm_w, eps, residual)
+        residual.copy_(r)
+        return o
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=part.device)
+    check(kernels().cfc_splitk_residual_rmsnorm(part.data_ptr(), split, M, N, residual.data_ptr(), norm_w.data_ptr(),
+                                                float(eps), out.data_ptr(), _stream(part)), "cfc_splitk_residual_rmsnorm")
+    return out
+
+
 def lib_split_for(K: int, N: int) -> int:
     """Split factor for the batched split-K decode GEMM (measured on MI355X at M=128:
     down 4096x14336 -> 8 (29 vs 42 us), o 4096x4096 -> 4); 1 = not worth splitting."""
