@@ -122,6 +122,9 @@ class DecoderWeights:
         self.embed: torch.Tensor | None = None
         self.final_norm: torch.Tensor | None = None
         self.lm_head: torch.Tensor | None = None
+        # ggml-quantized copies of the projections for the B <= 4 decode GEMV (GGUF checkpoints)
+        self.qlayers: list[dict] | None = None
+        self.q_lm_head = None
         self.cos_sin = rope_cos_sin(cfg.max_positions, cfg.head_dim, cfg.rope_theta, device=self.device,
                                     llama3_scaling=cfg.rope_llama3)
 
@@ -204,6 +207,69 @@ class DecoderWeights:
         w.lm_head = dev(shard_rows(head, w.vocab_shard))
         return w.finalize()
 
+    @classmethod
+    def from_gguf(cls, path, device, cfg=None, quantized_decode: bool = True):
+        """Load a llama-architecture GGUF (llama.cpp / Ollama files: Mistral, Llama).  Every tensor
+        is dequantized to bf16 (GPU kernel on CUDA devices) for the batched paths; with
+        ``quantized_decode`` the Q4_K / Q6_K / Q8_0 projection weights are ALSO kept in their
+        block format for the B <= 4 decode GEMV (``qlayers`` / ``q_lm_head``).  q/k rows are
+        un-permuted from llama.cpp's interleaved-RoPE order to this framework's rotate-half order.
+        TP is not supported for GGUF checkpoints (one GPU holds any GGUF model)."""
+        from ..ops.kernels import QGEMV_TYPES, QWeight, dequant_bf16
+        from ..runtime import gguf as G
+
+        r = G.GGUFReader(path)
+        cfg = cfg or G.config_from_gguf(r.metadata, tensor_names=r.tensors.keys(), name=Path(path).stem)
+        w = cls(cfg, device)
+        D = cfg.head_dim
+        qrows = G.unpermute_qk_rows(cfg.heads * D, cfg.heads)
+        krows = G.unpermute_qk_rows(cfg.kv_heads * D, cfg.kv_heads)
+
+        def info(name):
+            if name not in r.tensors:
+                raise KeyError(f"{path}: tensor {name} missing")
+            return r.tensors[name]
+
+        def bf16(name, rows=None):
+            ti = info(name)
+            t = dequant_bf16(ti.data, ti.ggml_type, ti.shape, w.device)
+            if rows is not None:
+                t = t.index_select(0, torch.as_tensor(rows, device=t.device))
+            return t.contiguous()
+
+        def quant(name, rows=None):
+            ti = info(name)
+            if not quantized_decode or ti.ggml_type not in QGEMV_TYPES or len(ti.shape) != 2:
+                return None
+            N, Kd = ti.shape
+            return QWeight.from_raw(ti.data, ti.ggml_type, N, Kd, w.device, rows=rows)
+
+        qlayers = []
+        for i in range(cfg.layers):
+            p = f"blk.{i}."
+            q, k, v = bf16(p + "attn_q.weight", qrows), bf16(p + "attn_k.weight", krows), bf16(p + "attn_v.weight")
+            w.layers.append({
+                "attn_norm": bf16(p + "attn_norm.weight"),
+                "qkv": torch.cat([q, k, v], 0).contiguous(),
+                "o": bf16(p + "attn_output.weight"),
+                "mlp_norm": bf16(p + "ffn_norm.weight"),
+                "gate_up": torch.cat([bf16(p + "ffn_gate.weight"), bf16(p + "ffn_up.weight")], 0).contiguous(),
+                "down": bf16(p + "ffn_down.weight"),
+            })
+            qlayers.append({"q": quant(p + "attn_q.weight", qrows), "k": quant(p + "attn_k.weight", krows),
+                            "v": quant(p + "attn_v.weight"), "o": quant(p + "attn_output.weight"),
+                            "gate": quant(p + "ffn_gate.weight"), "up": quant(p + "ffn_up.weight"),
+                            "down": quant(p + "ffn_down.weight")})
+        w.embed = bf16("token_embd.weight")
+        w.final_norm = bf16("output_norm.weight")
+        head = "output.weight" if "output.weight" in r.tensors else "token_embd.weight"
+        w.lm_head = w.embed if head == "token_embd.weight" else bf16(head)
+        if quantized_decode:
+            w.qlayers = qlayers
+            w.q_lm_head = quant(head)
+        w.gguf_types = sorted({t.type_name for t in r.tensors.values()})
+        return w.finalize()
+
     def finalize(self) -> "DecoderWeights":
         """Put gate/up rows in the 32-row interleaved order the fused decode SwiGLU GEMM reads (the
         prefill path's silu_mul reads the same layout, so one copy of the weights serves both)."""
@@ -274,6 +340,9 @@ class DecoderModel:
         self.decode_gemv = (os.environ.get("CFC_DECODE_GEMV", "1") != "0" and weights.gate_up_interleaved
                             and mode == "splitk" and gemv_shapes)
         self.fused_decode = mode == "skinny"
+        # B <= 4 decode on the ggml-quantized weights (GGUF checkpoints; csrc/kernels/quant.hip)
+        self.decode_qgemv = (weights.qlayers is not None and os.environ.get("CFC_DECODE_QGEMV", "1") != "0"
+                             and weights.tp_size == 1 and weights.gate_up_interleaved)
 
     def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.w.tp_size > 1:
@@ -379,6 +448,9 @@ class DecoderModel:
         h = K.rmsnorm(x, w.layers[0]["attn_norm"], eps)
         s_o = K.lib_split_for(w.heads * cfg.head_dim, cfg.hidden)
         s_d = K.lib_split_for(w.ffn, cfg.hidden)
+        if self.decode_qgemv and B <= K.GEMV_MAX_M:
+            return self._forward_decode_qgemv(h, residual, positions, slots, ctx_lens, block_tables, kv,
+                                              attn_workspace, part_blocks)
         if self.decode_gemv and B <= K.GEMV_MAX_M:
             return self._forward_decode_gemv(h, residual, positions, slots, ctx_lens, block_tables, kv,
                                              attn_workspace, part_blocks)
@@ -417,10 +489,57 @@ class DecoderModel:
             h = K.gemv_residual_rmsnorm(a, lw["down"], residual, nxt, eps)
         return h
 
+    def _forward_decode_qgemv(self, h, residual, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
+                              part_blocks):
+        """B <= 4 decode straight from the GGUF blocks (Q4_K / Q6_K / Q8_0 weight stream, 3.6x fewer
+        bytes than bf16 at Q4_K).  Projections without a quantized copy use the bf16 GEMV.  Same
+        rounding points as _forward_decode_gemv."""
+        cfg, w = self.cfg, self.w
+        B, eps = h.shape[0], cfg.rms_eps
+        qs, ks = w.heads * cfg.head_dim, w.kv_heads * cfg.head_dim
+        for i in range(cfg.layers):
+            lw, ql = w.layers[i], w.qlayers[i]
+            if ql["q"] is not None and ql["k"] is not None and ql["v"] is not None:
+                qkv = torch.empty(B, qs + 2 * ks, dtype=torch.bfloat16, device=h.device)
+                ld = qkv.shape[1]   # q, k, v write their column slices (types may differ: Q4_K_M's v is often Q6_K)
+                K.qgemv(h, ql["q"], out=qkv, ldo=ld)
+                K.qgemv(h, ql["k"], out=qkv[:, qs:], ldo=ld)
+                K.qgemv(h, ql["v"], out=qkv[:, qs + ks:], ldo=ld)
+            else:
+                qkv = K.gemv(h, lw["qkv"])
+            q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
+                                cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
+            attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
+                                            part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
+                                            k_scale=kv.k_scale, v_scale=kv.v_scale)
+            a2 = attn.view(B, -1)
+            if ql["o"] is not None:
+                part = K._workspace(h.device, B * cfg.hidden)[:B * cfg.hidden].view(1, B, cfg.hidden)
+                K.qgemv(a2, ql["o"], "f32", out=part[0])
+                h = K.splitk_residual_rmsnorm(part, residual, lw["mlp_norm"], eps)
+            else:
+                h = K.gemv_residual_rmsnorm(a2, lw["o"], residual, lw["mlp_norm"], eps)
+            g, u = ql["gate"], ql["up"]
+            if g is not None and u is not None and g.qtype == u.qtype:
+                a = K.qgemv(h, g, "swiglu", qw2=u)
+            else:
+                a = K.gemv(h, lw["gate_up"], "swiglu")
+            nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm
+            if ql["down"] is not None:
+                part = K._workspace(h.device, B * cfg.hidden)[:B * cfg.hidden].view(1, B, cfg.hidden)
+                K.qgemv(a, ql["down"], "f32", out=part[0])
+                h = K.splitk_residual_rmsnorm(part, residual, nxt, eps)
+            else:
+                h = K.gemv_residual_rmsnorm(a, lw["down"], residual, nxt, eps)
+        return h
+
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """[B, V] logits (all-gathered over the vocab-parallel shards)."""
         head = self.w.lm_head
-        if (self.decode_gemv and hidden.is_cuda and hidden.shape[0] <= K.GEMV_MAX_M
+        if (self.decode_qgemv and self.w.q_lm_head is not None and hidden.is_cuda
+                and hidden.shape[0] <= K.GEMV_MAX_M and hidden.is_contiguous() and self.w.q_lm_head.N % 4 == 0):
+            local = K.qgemv(hidden, self.w.q_lm_head)
+        elif (self.decode_gemv and hidden.is_cuda and hidden.shape[0] <= K.GEMV_MAX_M
                 and hidden.is_contiguous() and head.shape[0] % 2 == 0 and head.shape[1] % 8 == 0):
             # (the GEMV takes row pairs and 16-byte K slices: odd vocabularies, e.g. 32001-token
             # fine-tunes, stay on the library GEMM)

@@ -51,6 +51,8 @@ _KERNEL_SIGS = {
     "cfc_skinny_gemm": [P, P, I, I, I, I, I, P, P, I, P],
     "cfc_splitk_reduce": [P, I, I, I, I, P, I, P],
     "cfc_gemv": [P, P, I, I, I, I, P, P, I, P],
+    "cfc_qgemv": [P, I, I, I, I, P, P, c_int64, c_int64, c_int64, I, P, P, I, P],
+    "cfc_dequant_bf16": [P, I, c_int64, P, P],
     "cfc_splitk_residual_rmsnorm": [P, I, I, I, P, P, F, P, P],
     "cfc_ar_region_bytes": [c_int64, P],
     "cfc_ar_alloc": [c_int64, P],

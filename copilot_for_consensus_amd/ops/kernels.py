@@ -466,6 +466,194 @@ def splitk_residual_rmsnorm(part: torch.Tensor, residual: torch.Tensor, norm_w: 
     return out
 
 
+# ----------------------------------------------------------------------------- ggml-quantized weights
+
+QGEMV_TYPES = (8, 12, 14)    # Q8_0, Q4_K, Q6_K: the types the quantized GEMV streams (quant.hip)
+
+
+def _planar(qtype: int, blocks):
+    """ggml blocks [N, nb, size] (numpy uint8) -> the planes of the GPU layout (quant.hip header):
+    every plane is row-major [N, ...] so a wave's 16-B loads of one plane are contiguous.
+      Q4_K: NIB [N, K/2] (32-weight chunk c, byte i = q[32c+i] | q[32c+16+i] << 4), HDR [N, nb, 16]
+            (the ggml fp16 d, fp16 dmin, 12 scale bytes);
+      Q6_K: NIB [N, K/2] (low 4 bits, same order), HI [N, K/4] (chunk c: dword h, byte b, bits
+            2f..2f+1 = the top 2 bits of weight 16h + 4f + b), SC [N, K/16] int8, D [N, nb] fp16;
+      Q8_0: Q [N, K] int8, D [N, K/32] fp16."""
+    import numpy as np
+    N, nb, _ = blocks.shape
+    if qtype == 8:
+        return [np.ascontiguousarray(blocks[:, :, 2:34]).reshape(N, -1),
+                np.ascontiguousarray(blocks[:, :, 0:2]).reshape(N, -1)]
+    if qtype == 12:
+        qs = blocks[:, :, 16:144]                                   # ggml: qs[32j + l] = q[64j+l] | q[64j+32+l] << 4
+        lo, hi = qs & 0xF, qs >> 4
+        q = np.empty((N, nb, 256), np.uint8)
+        for j in range(4):
+            q[:, :, 64 * j:64 * j + 32] = lo[:, :, 32 * j:32 * j + 32]
+            q[:, :, 64 * j + 32:64 * j + 64] = hi[:, :, 32 * j:32 * j + 32]
+        q = q.reshape(N, -1, 32)
+        nib = (q[:, :, :16] | (q[:, :, 16:] << 4)).reshape(N, -1)
+        return [np.ascontiguousarray(nib), np.ascontiguousarray(blocks[:, :, 0:16]).reshape(N, -1)]
+    if qtype == 14:
+        ql, qh = blocks[:, :, 0:128], blocks[:, :, 128:192]
+        q6 = np.empty((N, nb, 256), np.uint8)
+        for h in range(2):
+            L, H = ql[:, :, 64 * h:64 * h + 64], qh[:, :, 32 * h:32 * h + 32]
+            q6[:, :, 128 * h:128 * h + 32] = (L[:, :, :32] & 0xF) | ((H & 3) << 4)
+            q6[:, :, 128 * h + 32:128 * h + 64] = (L[:, :, 32:] & 0xF) | (((H >> 2) & 3) << 4)
+            q6[:, :, 128 * h + 64:128 * h + 96] = (L[:, :, :32] >> 4) | (((H >> 4) & 3) << 4)
+            q6[:, :, 128 * h + 96:128 * h + 128] = (L[:, :, 32:] >> 4) | (((H >> 6) & 3) << 4)
+        c = q6.reshape(N, -1, 32)                                   # 32-weight chunks
+        nib = ((c[:, :, :16] & 0xF) | ((c[:, :, 16:] & 0xF) << 4)).reshape(N, -1)
+        top = (c >> 4).reshape(N, -1, 2, 4, 4)                       # [chunk, half h, f, b]
+        hi = (top[:, :, :, 0] | (top[:, :, :, 1] << 2) | (top[:, :, :, 2] << 4) | (top[:, :, :, 3] << 6))
+        return [np.ascontiguousarray(nib), np.ascontiguousarray(hi.reshape(N, -1)),
+                np.ascontiguousarray(blocks[:, :, 192:208]).reshape(N, -1),
+                np.ascontiguousarray(blocks[:, :, 208:210]).reshape(N, -1)]
+    raise ValueError(f"ggml type {qtype} has no quantized GEMV layout")
+
+
+@dataclasses.dataclass
+class QWeight:
+    """One ggml-quantized weight [N, K] in the planar GPU layout of csrc/kernels/quant.hip (see
+    :func:`_planar`): all planes in ONE device buffer ``buf``, plane p at byte ``offs[p]``."""
+    qtype: int
+    N: int
+    K: int
+    buf: torch.Tensor
+    offs: tuple
+
+    @classmethod
+    def _from_planes(cls, qtype, N, K, planes, device) -> "QWeight":
+        import numpy as np
+        offs, pos = [], 0
+        for pl in planes:
+            offs.append(pos)
+            pos += (pl.nbytes + 255) // 256 * 256                      # every plane 256-B aligned
+        host = np.zeros(pos, np.uint8)
+        for o, pl in zip(offs, planes):
+            host[o:o + pl.nbytes] = np.ascontiguousarray(pl).view(np.uint8).reshape(-1)
+        offs += [0] * (3 - len(offs))
+        return cls(qtype, N, K, torch.from_numpy(host).to(device), tuple(offs[:4]))
+
+    @classmethod
+    def from_raw(cls, raw, qtype: int, N: int, K: int, device, rows=None) -> "QWeight":
+        """``raw``: the tensor's ggml blocks (numpy uint8, file layout); ``rows``: optional row
+        permutation applied to whole block rows (llama q/k un-permute)."""
+        import numpy as np
+        from ..runtime import gguf as G
+        per, size = G.BLOCK[qtype]
+        blocks = np.asarray(raw, dtype=np.uint8).reshape(N, K // per, size)
+        if rows is not None:
+            blocks = blocks[np.asarray(rows)]
+        return cls._from_planes(qtype, N, K, _planar(qtype, blocks), device)
+
+    @classmethod
+    def random(cls, qtype: int, N: int, K: int, device, generator=None) -> "QWeight":
+        """Random planes with small fixed scales (benchmarks: the bytes, not the values, matter)."""
+        import numpy as np
+        rng = np.random.default_rng(int(torch.randint(0, 2 ** 31, (1,), generator=generator).item())
+                                    if generator is not None and generator.device.type == "cpu" else None)
+        nb = K // 256
+        half = np.frombuffer(np.float16(0.001).tobytes(), np.uint8)
+        if qtype == 8:
+            planes = [rng.integers(0, 256, (N, K), dtype=np.uint8), np.tile(half, (N, K // 32))]
+        elif qtype == 12:
+            hdr = rng.integers(0, 256, (N, nb, 16), dtype=np.uint8)
+            hdr[:, :, 0:2] = half
+            hdr[:, :, 2:4] = half
+            planes = [rng.integers(0, 256, (N, K // 2), dtype=np.uint8), hdr.reshape(N, -1)]
+        elif qtype == 14:
+            planes = [rng.integers(0, 256, (N, K // 2), dtype=np.uint8),
+                      rng.integers(0, 256, (N, K // 4), dtype=np.uint8),
+                      rng.integers(0, 256, (N, K // 16), dtype=np.uint8), np.tile(half, (N, nb))]
+        else:
+            raise ValueError(f"ggml type {qtype} has no quantized GEMV layout")
+        return cls._from_planes(qtype, N, K, planes, device)
+
+    @property
+    def nbytes(self) -> int:
+        from ..runtime import gguf as G
+        per, size = G.BLOCK[self.qtype]
+        return self.N * self.K // per * size
+
+
+def llama_cpp_q4km_types(layers: int) -> list[dict]:
+    """Per-layer ggml types of llama.cpp's Q4_K_M recipe: Q4_K everywhere except attn_v and
+    ffn_down in the "more bits" layers (first and last eighth, every third in between), which
+    are Q6_K; the output projection is Q6_K."""
+    def more_bits(i):
+        return i < layers // 8 or i >= 7 * layers // 8 or (i - layers // 8) % 3 == 2
+    out = []
+    for i in range(layers):
+        t6 = 14 if more_bits(i) else 12
+        out.append({"q": 12, "k": 12, "v": t6, "o": 12, "gate": 12, "up": 12, "down": t6})
+    return out
+
+
+def attach_random_quant(weights, recipe: str = "q4_k_m", seed: int = 0):
+    """Give random-init DecoderWeights ggml-quantized projection copies (random blocks) so the
+    quantized decode path can be benchmarked on a model of the right shape without a file."""
+    cfg = weights.cfg
+    dev = weights.device
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    D = cfg.head_dim
+    shapes = {"q": (weights.heads * D, cfg.hidden), "k": (weights.kv_heads * D, cfg.hidden),
+              "v": (weights.kv_heads * D, cfg.hidden), "o": (cfg.hidden, weights.heads * D),
+              "gate": (weights.ffn, cfg.hidden), "up": (weights.ffn, cfg.hidden), "down": (cfg.hidden, weights.ffn)}
+    if recipe == "q4_k_m":
+        types, head_t = llama_cpp_q4km_types(cfg.layers), 14
+    elif recipe == "q8_0":
+        types, head_t = [{k: 8 for k in shapes} for _ in range(cfg.layers)], 8
+    else:
+        raise ValueError(f"unknown quantization recipe {recipe!r}")
+    weights.qlayers = [{k: QWeight.random(t[k], *shapes[k], dev, g) for k in shapes} for t in types]
+    weights.q_lm_head = QWeight.random(head_t, weights.vocab_shard, cfg.hidden, dev, g)
+    return weights
+
+
+def qgemv(x: torch.Tensor, qw: QWeight, epi: str = "bf16", qw2: QWeight | None = None,
+          out: torch.Tensor | None = None, ldo: int | None = None) -> torch.Tensor:
+    """x [M <= 4, K] bf16 @ dequant(qw)^T on the quantized GEMV (quant.hip).  ``epi``: "bf16" ->
+    [M, N] bf16; "f32" -> [M, N] fp32; "swiglu" -> bf16 [M, N] = silu(x @ qw^T) * (x @ qw2^T).
+    ``out`` may be a column slice of a wider buffer (row stride ``ldo``)."""
+    M, Kd = x.shape
+    if Kd != qw.K or not (1 <= M <= GEMV_MAX_M):
+        raise ValueError(f"qgemv: x {tuple(x.shape)} vs weight K={qw.K} (M <= {GEMV_MAX_M})")
+    if epi == "swiglu" and (qw2 is None or qw2.qtype != qw.qtype or qw2.N != qw.N or qw2.K != qw.K):
+        raise ValueError("qgemv swiglu: gate and up weights must share type and shape")
+    _req(x, torch.bfloat16, "x")
+    mode = {"f32": 0, "bf16": 1, "swiglu": 2}[epi]
+    if out is None:
+        out = torch.empty(M, qw.N, dtype=torch.float32 if epi == "f32" else torch.bfloat16, device=x.device)
+        ldo = qw.N
+    elif ldo is None:
+        ldo = out.stride(0)
+    yf, yb = (out.data_ptr(), None) if epi == "f32" else (None, out.data_ptr())
+    o = tuple(qw.offs) + (0,) * (4 - len(qw.offs))
+    check(kernels().cfc_qgemv(x.data_ptr(), M, qw.N, Kd, qw.qtype, qw.buf.data_ptr(),
+                              qw2.buf.data_ptr() if qw2 is not None else None, o[1], o[2], o[3],
+                              mode, yf, yb, int(ldo), _stream(x)), "cfc_qgemv")
+    return out
+
+
+def dequant_bf16(raw, qtype: int, shape, device) -> torch.Tensor:
+    """ggml blocks (numpy uint8, file layout) -> bf16 tensor of ``shape`` on ``device`` (GPU
+    kernel for CUDA devices, numpy reference otherwise)."""
+    import numpy as np
+    from ..runtime import gguf as G
+    device = torch.device(device)
+    if device.type != "cuda":
+        return torch.from_numpy(G.dequantize(raw, qtype, tuple(shape))).to(torch.bfloat16)
+    n = int(np.prod(shape))
+    src = torch.from_numpy(np.array(raw, dtype=np.uint8, copy=True).reshape(-1)).to(device)
+    out = torch.empty(tuple(shape), dtype=torch.bfloat16, device=device)
+    check(kernels().cfc_dequant_bf16(src.data_ptr(), int(qtype), n, out.data_ptr(), _stream(out)),
+          "cfc_dequant_bf16")
+    return out
+
+
 def lib_split_for(K: int, N: int) -> int:
     """Split factor for the batched split-K decode GEMM (measured on MI355X at M=128:
     down 4096x14336 -> 8 (29 vs 42 us), o 4096x4096 -> 4); 1 = not worth splitting."""

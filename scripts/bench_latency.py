@@ -33,10 +33,20 @@ PUBLISHED = {
 }
 
 
-def run_model(name, prompt_lens, new, reps, seed):
+def run_model(name, prompt_lens, new, reps, seed, weights="bf16"):
     cfg = get_config(name)
     dev = torch.device("cuda")
-    model = DecoderModel(DecoderWeights.random(cfg, dev, seed=seed))
+    w = DecoderWeights.random(cfg, dev, seed=seed)
+    wbytes = cfg.num_params() * 2
+    if weights != "bf16":
+        # ggml-quantized projections (llama.cpp's Q4_K_M type recipe, or all Q8_0), random blocks:
+        # decode streams them (csrc/kernels/quant.hip); prefill keeps the bf16 copies
+        from copilot_for_consensus_amd.ops.kernels import attach_random_quant
+        attach_random_quant(w, weights, seed)
+        wbytes = sum(q.nbytes for layer in w.qlayers for q in layer.values()) + w.q_lm_head.nbytes
+    model = DecoderModel(w)
+    if weights != "bf16":
+        assert model.decode_qgemv
     kv = PagedKVCache(cfg.layers, blocks_needed(max(prompt_lens) + new) + 8, cfg.kv_heads, cfg.head_dim, dev)
     eng = LLMEngine(model, kv, max_prefill_tokens=16384, prefix_cache=False)
     g = torch.Generator().manual_seed(seed)
@@ -56,10 +66,10 @@ def run_model(name, prompt_lens, new, reps, seed):
         row = {"model": name, "prompt_tokens": plen, "new_tokens": new, "ttft_s": round(statistics.median(ttft), 4),
                "decode_tok_s": round(statistics.median(tps), 1),
                "ms_per_token": round(1000.0 / statistics.median(tps), 3),
-               "weight_gb": round(cfg.num_params() * 2 / 1e9, 2)}
+               "weights": weights, "weight_gb": round(wbytes / 1e9, 2)}
         # HBM bytes one decode step must read: all weights + the KV of the context so far
         kv_bytes = 2 * cfg.layers * cfg.kv_heads * cfg.head_dim * 2 * (plen + new / 2)
-        row["achieved_TB_s"] = round((cfg.num_params() * 2 + kv_bytes) * statistics.median(tps) / 1e12, 2)
+        row["achieved_TB_s"] = round((wbytes + kv_bytes) * statistics.median(tps) / 1e12, 2)
         pub = PUBLISHED.get(name)
         if pub:
             row["published_tok_s"] = pub["tok_s"]
@@ -79,9 +89,11 @@ def main():
     ap.add_argument("--new", type=int, default=256)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--weights", choices=["bf16", "q4_k_m", "q8_0"], default="bf16",
+                    help="decode weight format (q4_k_m / q8_0: ggml blocks streamed by the quantized GEMV)")
     a = ap.parse_args()
     for name in a.models:
-        run_model(name, a.prompt, a.new, a.reps, a.seed)
+        run_model(name, a.prompt, a.new, a.reps, a.seed, a.weights)
 
 
 if __name__ == "__main__":

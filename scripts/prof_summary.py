@@ -8,8 +8,18 @@ from collections import defaultdict
 
 def main(root, out=None, top=30):
     stats = glob.glob(f"{root}/**/*kernel_stats.csv", recursive=True)
+    dbs = glob.glob(f"{root}/**/*results.db", recursive=True)
     lines = []
-    if stats:
+    if not stats and dbs:   # rocprofv3's default rocpd SQLite output (ROCm 7.x)
+        import sqlite3
+        con = sqlite3.connect(dbs[0])
+        rows = con.execute("select name, total_calls, total_duration, average from top_kernels").fetchall()
+        tot = sum(r[2] for r in rows) or 1
+        lines.append(f"# {dbs[0]}\n# total kernel time {tot/1e6:.1f} ms over {sum(r[1] for r in rows)} dispatches")
+        lines.append(f"{'pct':>6} {'total_ms':>10} {'calls':>7} {'avg_us':>9}  kernel")
+        for name, calls, total, avg in sorted(rows, key=lambda r: -r[2])[:top]:
+            lines.append(f"{100*total/tot:6.2f} {total/1e6:10.2f} {calls:7d} {avg/1e3:9.1f}  {name[:150]}")
+    elif stats:
         rows = list(csv.DictReader(open(stats[0])))
         tot = sum(float(r["TotalDurationNs"]) for r in rows)
         lines.append(f"# {stats[0]}\n# total kernel time {tot/1e6:.1f} ms over {sum(int(r['Calls']) for r in rows)} dispatches")
