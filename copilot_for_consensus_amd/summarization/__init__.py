@@ -76,7 +76,8 @@ class MockSummarizer(Summarizer):
 class HipLLMSummarizer(Summarizer):
     backend = "hip"
 
-    def __init__(self, model: str = "mistral-7b", checkpoint_dir: str | None = None, tensor_parallel: int = 1,
+    def __init__(self, model: str = "mistral-7b", checkpoint_dir: str | None = None, gguf_path: str | None = None,
+                 tensor_parallel: int = 1,
                  max_new_tokens: int = 512, temperature: float = 0.0, max_batch: int = 128,
                  kv_cache_tokens: int = 524288, device: str = "cuda", seed: int = 1234, tp_group=None,
                  tp_rank: int = 0, ignore_eos: bool = False, top_k: int = 40, top_p: float = 0.95,
@@ -86,7 +87,18 @@ class HipLLMSummarizer(Summarizer):
         from ..runtime.kv_cache import PagedKVCache
         from ..runtime.tokenizer import load_hf_tokenizer, synthetic_bpe
         dev = torch.device(device if (not str(device).startswith("cuda") or torch.cuda.is_available()) else "cpu")
-        if checkpoint_dir:
+        if gguf_path is None and checkpoint_dir and str(checkpoint_dir).endswith(".gguf"):
+            gguf_path, checkpoint_dir = checkpoint_dir, None
+        if gguf_path:
+            # llama.cpp / Ollama weights: bf16 copies for prefill and batches, the ggml blocks kept
+            # for the quantized B <= 4 decode GEMV (runtime/gguf.py, csrc/kernels/quant.hip)
+            from ..runtime import gguf as G
+            if tensor_parallel > 1:
+                raise ValueError("GGUF checkpoints run on one GPU (tensor_parallel must be 1)")
+            w = DecoderWeights.from_gguf(gguf_path, dev)
+            cfg = w.cfg
+            self.tokenizer = G.tokenizer_from_gguf(G.GGUFReader(gguf_path).metadata)
+        elif checkpoint_dir:
             from pathlib import Path
             cfg = load_config_json(Path(checkpoint_dir) / "config.json")
             w = DecoderWeights.from_safetensors(cfg, checkpoint_dir, dev, tp_rank, tensor_parallel)

@@ -394,3 +394,39 @@ def test_gpu_gguf_q4km_model_quantized_decode_matches_dequantized(tmp_path):
     cos = torch.nn.functional.cosine_similarity(a, b, dim=-1)
     assert float(cos.min()) > 0.999, cos
     assert float((a - b).abs().max()) < 0.05 * float(b.std()) * 10, (a - b).abs().max()
+
+
+def test_hip_summarizer_loads_gguf(tmp_path, monkeypatch):
+    """LLM_BACKEND_TYPE=hip with LLAMA_ARG_MODEL pointing at a GGUF (the reference compose's
+    variable): weights and tokenizer come from the file; summaries decode through the engine."""
+    from copilot_for_consensus_amd.config import loader
+    from copilot_for_consensus_amd.summarization import Thread, create_llm_backend
+
+    toks = ["<unk>", "<s>", "</s>"] + [f"<0x{i:02X}>" for i in range(256)]
+    chars = sorted(set("abcdefghijklmnopqrstuvwxyz:.,"))
+    toks += ["▁"] + chars + ["▁" + c for c in chars]
+    types = [2, 3, 3] + [6] * 256 + [1] * (len(toks) - 259)
+    cfg = DecoderConfig("tiny-gguf", len(toks), 128, 2, 2, 1, 64, 256, max_positions=1024)
+    rng = np.random.default_rng(0)
+    sd = {"model.embed_tokens.weight": rng.standard_normal((cfg.vocab_size, 128)).astype(np.float32),
+          "lm_head.weight": rng.standard_normal((cfg.vocab_size, 128)).astype(np.float32) * 0.05,
+          "model.norm.weight": np.ones(128, np.float32)}
+    for i in range(2):
+        p = f"model.layers.{i}."
+        for n, shape in (("self_attn.q_proj", (128, 128)), ("self_attn.k_proj", (64, 128)),
+                         ("self_attn.v_proj", (64, 128)), ("self_attn.o_proj", (128, 128)),
+                         ("mlp.gate_proj", (256, 128)), ("mlp.up_proj", (256, 128)), ("mlp.down_proj", (128, 256))):
+            sd[p + n + ".weight"] = rng.standard_normal(shape).astype(np.float32) * 0.05
+        sd[p + "input_layernorm.weight"] = np.ones(128, np.float32)
+        sd[p + "post_attention_layernorm.weight"] = np.ones(128, np.float32)
+    path = tmp_path / "tiny.gguf"
+    G.write_llama_gguf(path, cfg, sd, tokens=toks, token_types=types, default_qtype=G.F32)
+    monkeypatch.setenv("LLAMA_ARG_MODEL", str(path))
+    monkeypatch.setenv("LLM_DEVICE", "cpu")
+    monkeypatch.setenv("LLM_MAX_NEW_TOKENS", "6")
+    adapter = loader.load_adapter_config("llm_backend")
+    assert adapter.driver_config["gguf_path"] == str(path)   # LLAMA_ARG_MODEL maps onto the hip driver
+    s = create_llm_backend(adapter, kv_cache_tokens=4096)
+    assert s.cfg.name == "tiny-gguf" and s.tokenizer.vocab_size == len(toks)
+    out = s.summarize(Thread("t1", ["alpha beta"], prompt="summarize: the thread."))
+    assert out.tokens_prompt > 3 and 1 <= out.tokens_completion <= 6 and out.llm_backend == "hip"
