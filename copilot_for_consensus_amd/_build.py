@@ -7,6 +7,8 @@ the GPU box with the gpurun snapshot):
   (CDNA4 / MI355X only; no other offload arch, no CUDA path).
 * ``_lib/libcfc_runtime.so`` -- the host-side C++ runtime (``csrc/runtime/*.cpp``): BPE and
   WordPiece tokenizers, paged-KV block allocator, mbox splitter.
+* ``_lib/cfc-broker`` -- the native message broker executable (``csrc/broker/cfc_broker.cpp``),
+  the RabbitMQ replacement for multi-process deployments (``bus/cfcbroker.py``).
 
 The build is incremental (object files are rebuilt only when their source or a header changed)
 and compiles translation units in parallel.
@@ -36,6 +38,7 @@ CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
 
 KERNELS_LIB = LIB_DIR / "libcfc_kernels.so"
 RUNTIME_LIB = LIB_DIR / "libcfc_runtime.so"
+BROKER_BIN = LIB_DIR / "cfc-broker"
 
 
 def _digest(paths: list[Path], extra: list[str]) -> str:
@@ -100,8 +103,27 @@ def build_runtime(jobs: int | None = None, verbose: bool = True) -> Path:
                       jobs or min(8, os.cpu_count() or 4), verbose)
 
 
-def build_all(verbose: bool = True) -> tuple[Path, Path]:
-    return build_kernels(verbose=verbose), build_runtime(verbose=verbose)
+def build_broker(verbose: bool = True, out: Path | None = None, extra_flags: list[str] | None = None) -> Path:
+    """Single-TU executable; rebuilt when the source or the flags change."""
+    src = CSRC / "broker" / "cfc_broker.cpp"
+    out = out or BROKER_BIN
+    flags = ["-O2", "-std=c++17", "-Wall", "-Wextra", *(extra_flags or [])]
+    stamp = out.with_name(out.name + ".stamp")
+    digest = _digest([src], flags)
+    if out.exists() and stamp.exists() and stamp.read_text() == digest:
+        return out
+    out.parent.mkdir(parents=True, exist_ok=True)
+    res = subprocess.run([CXX, *flags, str(src), "-o", str(out)], capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"broker build failed\n{res.stderr[-8000:]}")
+    stamp.write_text(digest)
+    if verbose:
+        print(f"[cfc-build] linked {out}")
+    return out
+
+
+def build_all(verbose: bool = True) -> tuple[Path, Path, Path]:
+    return build_kernels(verbose=verbose), build_runtime(verbose=verbose), build_broker(verbose=verbose)
 
 
 if __name__ == "__main__":

@@ -86,19 +86,50 @@ class InMemoryArchiveStore(ArchiveStore):
 
 
 class LocalVolumeArchiveStore(ArchiveStore):
-    """Files under ``<base>/<source>/<archive_id>.mbox`` + JSON metadata sidecar index."""
+    """Files under ``<base>/<source>/<archive_id>.mbox`` + one JSON metadata sidecar per archive
+    (``<base>/.meta/<archive_id>.json``, written atomically).  Several processes share the volume
+    (the reference mounts one ``raw_archives`` volume into ingestion and parsing): an archive stored
+    by one process is visible to the others on their next lookup, with no shared index file to race
+    on."""
 
     def __init__(self, archive_base_path: str = "/data/raw_archives", **_):
         self.base = Path(archive_base_path)
         self.base.mkdir(parents=True, exist_ok=True)
-        self._index_path = self.base / "metadata.json"
+        self._meta_dir = self.base / ".meta"
+        self._meta_dir.mkdir(exist_ok=True)
         self._lock = threading.Lock()
-        self._meta: dict[str, dict] = json.loads(self._index_path.read_text()) if self._index_path.exists() else {}
+        self._meta: dict[str, dict] = {}
+        legacy = self.base / "metadata.json"          # single-index layout of earlier versions
+        if legacy.exists():
+            for aid, m in json.loads(legacy.read_text()).items():
+                if not (self._meta_dir / f"{aid}.json").exists():
+                    self._write_meta(aid, m)
+        self._refresh()
 
-    def _save(self):
-        tmp = self._index_path.with_suffix(".tmp")
-        tmp.write_text(json.dumps(self._meta, indent=1))
-        os.replace(tmp, self._index_path)
+    def _write_meta(self, aid: str, m: dict) -> None:
+        tmp = self._meta_dir / f".{aid}.{os.getpid()}.tmp"
+        tmp.write_text(json.dumps(m))
+        os.replace(tmp, self._meta_dir / f"{aid}.json")
+        self._meta[aid] = m
+
+    def _read_meta(self, aid: str) -> dict | None:
+        m = self._meta.get(aid)
+        if m is None:
+            try:
+                m = json.loads((self._meta_dir / f"{aid}.json").read_text())
+            except (OSError, ValueError):
+                return None
+            self._meta[aid] = m
+        return m
+
+    def _refresh(self) -> None:
+        seen = {}
+        for f in self._meta_dir.glob("*.json"):
+            try:
+                seen[f.stem] = json.loads(f.read_text())
+            except (OSError, ValueError):
+                continue
+        self._meta = seen
 
     def store_archive(self, source_name, file_path, content):
         aid = archive_id_from_bytes(content)
@@ -107,42 +138,44 @@ class LocalVolumeArchiveStore(ArchiveStore):
         p = d / f"{aid}.mbox"
         with self._lock:
             if not p.exists():
-                tmp = p.with_suffix(".part")
+                tmp = p.with_suffix(f".{os.getpid()}.part")
                 tmp.write_bytes(content)
                 os.replace(tmp, p)
-            self._meta[aid] = {"archive_id": aid, "source_name": source_name, "file_path": str(p),
-                               "original_path": file_path, "content_hash": hashlib.sha256(content).hexdigest(),
-                               "size_bytes": len(content), "stored_at": datetime.now(timezone.utc).isoformat()}
-            self._save()
+            self._write_meta(aid, {"archive_id": aid, "source_name": source_name, "file_path": str(p),
+                                   "original_path": file_path, "content_hash": hashlib.sha256(content).hexdigest(),
+                                   "size_bytes": len(content), "stored_at": datetime.now(timezone.utc).isoformat()})
         return aid
 
     def get_archive(self, archive_id):
-        m = self._meta.get(archive_id)
+        m = self._read_meta(archive_id)
         if not m:
             return None
         p = Path(m["file_path"])
         return p.read_bytes() if p.exists() else None
 
     def get_archive_by_hash(self, content_hash):
+        self._refresh()
         for aid, m in self._meta.items():
             if m["content_hash"] == content_hash:
                 return aid
         return None
 
     def archive_exists(self, archive_id):
-        m = self._meta.get(archive_id)
+        m = self._read_meta(archive_id)
         return bool(m) and Path(m["file_path"]).exists()
 
     def delete_archive(self, archive_id):
         with self._lock:
-            m = self._meta.pop(archive_id, None)
+            m = self._read_meta(archive_id)
+            self._meta.pop(archive_id, None)
             if not m:
                 return False
             Path(m["file_path"]).unlink(missing_ok=True)
-            self._save()
+            (self._meta_dir / f"{archive_id}.json").unlink(missing_ok=True)
             return True
 
     def list_archives(self, source_name):
+        self._refresh()
         return [dict(m) for m in self._meta.values() if m["source_name"] == source_name]
 
 

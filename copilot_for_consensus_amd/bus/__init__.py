@@ -1,4 +1,4 @@
-"""Event transport: publisher/subscriber API + drivers (inproc, noop, rabbitmq) + validation.
+"""Event transport: publisher/subscriber API + drivers (inproc, noop, cfcbroker, rabbitmq) + validation.
 
 Factories mirror create_publisher / create_subscriber (adapters/copilot_message_bus/
 copilot_message_bus/factory.py:94,147): the validating decorator wraps the driver by default.
@@ -31,6 +31,9 @@ def create_publisher(cfg=None, enable_validation: bool = True, broker: InProcBro
         pub = InProcPublisher(broker=broker, **kw)
     elif name == "noop":
         pub = NoopPublisher()
+    elif name == "cfcbroker":
+        from .cfcbroker import CfcBrokerPublisher
+        pub = CfcBrokerPublisher(**kw)
     elif name == "rabbitmq":
         from .rabbitmq import RabbitMQPublisher
         pub = RabbitMQPublisher(**kw)
@@ -51,6 +54,9 @@ def create_subscriber(cfg=None, enable_validation: bool = True, broker: InProcBr
         sub = InProcSubscriber(broker=broker, **kw)
     elif name == "noop":
         sub = NoopSubscriber()
+    elif name == "cfcbroker":
+        from .cfcbroker import CfcBrokerSubscriber
+        sub = CfcBrokerSubscriber(**kw)
     elif name == "rabbitmq":
         from .rabbitmq import RabbitMQSubscriber
         sub = RabbitMQSubscriber(**kw)

@@ -100,6 +100,11 @@ class StaticConfigProvider(EnvConfigProvider):
         super().__init__({k: str(v) for k, v in values.items()})
 
 
+def env_is_set(name: str, env: Mapping[str, str] | None = None) -> bool:
+    """True when the variable is explicitly set (to tell a deployment's choice from a spec default)."""
+    return bool((os.environ if env is None else env).get(name))
+
+
 def load_adapter_config(adapter: str, env: Mapping[str, str] | None = None, driver: str | None = None,
                         secrets=None, overrides: Mapping[str, Any] | None = None) -> AdapterConfig:
     env = os.environ if env is None else env

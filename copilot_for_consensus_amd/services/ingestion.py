@@ -48,7 +48,14 @@ class IngestionService(BaseService):
                  max_retries: int = 3, **kw):
         super().__init__(publisher, None, document_store, **kw)
         self.archives = archive_store
-        self.storage_path = Path(storage_path or tempfile.mkdtemp(prefix="cfc-ingest-"))
+        path = None
+        if storage_path:
+            try:   # INGESTION_STORAGE_PATH (uploads + fetch scratch); a temp dir if it cannot be created
+                Path(storage_path).mkdir(parents=True, exist_ok=True)
+                path = Path(storage_path)
+            except OSError:
+                path = None
+        self.storage_path = path or Path(tempfile.mkdtemp(prefix="cfc-ingest-"))
         self.max_retries = max_retries
         self.stats.update(files_ingested=0, files_skipped=0, files_failed=0)
 

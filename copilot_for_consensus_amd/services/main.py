@@ -1,7 +1,11 @@
-"""Run one service (uvicorn + consumer thread) or the whole single-node pipeline.
+"""Run one service (uvicorn + consumer thread), the whole single-node pipeline, or the shared
+infrastructure a one-process-per-service deployment needs.
 
     python -m copilot_for_consensus_amd.services.main node         # all services, in-proc bus
     python -m copilot_for_consensus_amd.services.main reporting    # one service per process
+    python -m copilot_for_consensus_amd.services.main broker       # native message broker (RabbitMQ role)
+    python -m copilot_for_consensus_amd.services.main docstore     # document store server (MongoDB role)
+    python -m copilot_for_consensus_amd.services.main vectorstore  # HIP kNN behind Qdrant's REST API
 
 Reference entry points: <service>/main.py (e.g. ingestion/main.py:179, parsing/main.py:101-124).
 """
@@ -25,9 +29,14 @@ def _auth_dep(cfg):
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("service", choices=["node", "ingestion", "parsing", "chunking", "embedding", "orchestrator",
-                                        "summarization", "reporting", "auth"])
+                                        "summarization", "reporting", "auth", "broker", "docstore", "vectorstore"])
     ap.add_argument("--port", type=int, default=None)
+    ap.add_argument("--host", default=None)
+    ap.add_argument("--data-dir", default=None, help="broker journal / docstore WAL / vector index directory")
     args = ap.parse_args(argv)
+
+    if args.service in ("broker", "docstore", "vectorstore"):
+        return _infra(args)
 
     if args.service == "auth":
         from ..security.auth import AuthService, MockIdentityProvider, RoleStore, github_provider, google_provider
@@ -85,6 +94,56 @@ def main(argv=None) -> int:
         from ..ui import ui_routes
         ui_routes(app)
     run_service(svc, app, cfg.http_host, args.port or cfg.http_port)
+    return 0
+
+
+def _infra(args) -> int:
+    import os
+    host = args.host or "0.0.0.0"
+    if args.service == "broker":
+        import subprocess
+
+        from ..bus.cfcbroker import BROKER_BIN, DEFAULT_PORT
+        if not BROKER_BIN.exists():
+            from .._build import build_broker
+            build_broker(verbose=False)
+        cmd = [str(BROKER_BIN), "--host", host, "--port", str(args.port or int(os.environ.get("CFC_BROKER_PORT",
+                                                                                               DEFAULT_PORT)))]
+        data = args.data_dir or os.environ.get("CFC_BROKER_DATA_DIR")
+        if data:
+            cmd += ["--data-dir", data]
+        cmd += ["--max-redeliveries", os.environ.get("CFC_BROKER_MAX_REDELIVERIES", "5"),
+                "--fsync", os.environ.get("CFC_BROKER_FSYNC", "always")]
+        proc = subprocess.Popen(cmd)   # a child, not an exec: the broker's exit code is ours
+        try:
+            return proc.wait()
+        except KeyboardInterrupt:
+            proc.terminate()
+            return proc.wait()
+    if args.service == "docstore":
+        from ..storage.server import DocumentStoreServer
+        srv = DocumentStoreServer(host=host, port=args.port or int(os.environ.get("CFC_DOCSTORE_PORT", 27027)),
+                                  data_dir=args.data_dir or os.environ.get("CFC_DOCSTORE_DATA_DIR"),
+                                  fsync=os.environ.get("CFC_DOCSTORE_FSYNC", "false").lower() == "true")
+        print(f"cfc-docstore listening on {host}:{srv.port} (replayed {srv.replayed} log records)", flush=True)
+        import signal
+        import threading
+        # serve_forever() returns once shutdown() runs (from another thread); close() then snapshots
+        signal.signal(signal.SIGTERM, lambda *_: threading.Thread(target=srv.server.shutdown, daemon=True).start())
+        try:
+            srv.serve_forever()
+        except KeyboardInterrupt:
+            pass
+        return 0
+    import uvicorn
+
+    from ..vectorstore.server import create_vector_app
+    from ..config.loader import load_adapter_config
+    hip = load_adapter_config("vector_store", driver="hip").driver_config     # VECTOR_STORE_* of the hip driver
+    port = args.port or load_adapter_config("vector_store", driver="qdrant").driver_config["port"]   # QDRANT_PORT
+    app = create_vector_app(device=hip["device"], capacity=hip["capacity"], index_type=hip["index_type"],
+                            nlist=hip["nlist"], nprobe=hip["nprobe"], persist_dir=args.data_dir or hip["persist_path"])
+    uvicorn.run(app, host=host, port=port, log_level="warning")
     return 0
 
 

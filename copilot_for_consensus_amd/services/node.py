@@ -15,7 +15,7 @@ import threading
 from ..archive import create_archive_store
 from ..bus import InProcBroker, create_publisher, create_subscriber
 from ..chunking import create_chunker
-from ..config.loader import get_config
+from ..config.loader import env_is_set, get_config
 from ..consensus import create_consensus_detector
 from ..embedding import create_embedding_provider
 from ..observability import create_error_reporter, create_logger, create_metrics_collector
@@ -60,6 +60,8 @@ class Node:
         o, sm, r = cfgs["orchestrator"], cfgs["summarization"], cfgs["reporting"]
         self.services = {
             "ingestion": IngestionService(pub("ingestion"), self.store, self.archives,
+                                          storage_path=cfgs["ingestion"].storage_path if env_is_set(
+                                              "INGESTION_STORAGE_PATH", env) else None,
                                           max_retries=cfgs["ingestion"].max_retries, **common),
             "parsing": ParsingService(pub("parsing"), sub("parsing"), self.store, self.archives, **common),
             "chunking": ChunkingService(pub("chunking"), sub("chunking"), self.store,

@@ -499,6 +499,9 @@ def create_document_store(cfg=None, enable_validation: bool = False, strict: boo
         store: DocumentStore = InMemoryDocumentStore()
     elif name == "mongodb":
         store = MongoDocumentStore(**kw)
+    elif name == "cfcstore":
+        from .server import RemoteDocumentStore
+        store = RemoteDocumentStore(**{k: v for k, v in kw.items() if v is not None})
     elif name in ("azure_cosmosdb", "azurecosmos"):
         from ..cloud.azure import AzureCosmosDocumentStore
         store = AzureCosmosDocumentStore(**{k: v for k, v in kw.items() if v is not None})

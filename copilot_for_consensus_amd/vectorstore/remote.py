@@ -70,9 +70,12 @@ class QdrantVectorStore(VectorStore):
     def _ensure_collection(self):
         code, data = self.http("GET", f"/collections/{self.collection}", ok=(200, 404))
         if code == 404:
-            self.http("PUT", f"/collections/{self.collection}",
-                      {"vectors": {"size": self.dim, "distance": self.distance}})
-            return
+            # several services start at once: another one may create it between our GET and PUT
+            code, _ = self.http("PUT", f"/collections/{self.collection}",
+                                {"vectors": {"size": self.dim, "distance": self.distance}}, ok=(200, 400, 409))
+            if code == 200:
+                return
+            code, data = self.http("GET", f"/collections/{self.collection}")
         vec = data["result"]["config"]["params"]["vectors"]
         if int(vec["size"]) != self.dim:
             raise ValueError(f"collection {self.collection} has vector size {vec['size']}, expected {self.dim}")

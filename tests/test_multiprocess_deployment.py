@@ -1,0 +1,220 @@
+"""The reference's compose topology as separate OS processes, talking only over TCP.
+
+Infrastructure: the native broker (RabbitMQ's role), the document store server (MongoDB's role)
+and the Qdrant-REST vector store (Qdrant's role).  Services: ingestion, parsing, chunking,
+embedding, orchestrator, summarization and reporting, each one ``python -m
+copilot_for_consensus_amd.services.main <service>`` process with its own uvicorn + consumer thread
+(reference <service>/main.py).  The flow is the reference's docker-compose CI job
+(.github/workflows/docker-compose-ci.yml:339-521): create a source and trigger it through the
+ingestion REST API, then poll the reporting API until the reports exist.  Then the chunking
+service is killed with SIGKILL, a second archive is uploaded while it is down (its events wait in
+the broker's durable ``chunking`` queue), the service is restarted and the pipeline completes.
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import signal
+import socket
+import subprocess
+import sys
+import time
+import urllib.error
+import urllib.request
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIX = os.path.join(ROOT, "tests", "fixtures", "sample.mbox")
+SERVICES = ("ingestion", "parsing", "chunking", "embedding", "orchestrator", "summarization", "reporting")
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _http(method: str, url: str, body=None, headers=None, timeout=10):
+    data = body if isinstance(body, (bytes, type(None))) else json.dumps(body).encode()
+    h = {"Content-Type": "application/json"} if isinstance(body, (dict, list)) else {}
+    h.update(headers or {})
+    req = urllib.request.Request(url, data=data, method=method, headers=h)
+    try:
+        with urllib.request.urlopen(req, timeout=timeout) as r:
+            return r.status, json.loads(r.read() or b"null")
+    except urllib.error.HTTPError as e:
+        return e.code, e.read().decode(errors="replace")
+
+
+class Deployment:
+    def __init__(self, tmp):
+        self.tmp = tmp
+        self.procs: dict[str, subprocess.Popen] = {}
+        self.ports = {n: _free_port() for n in ("broker", "docstore", "vectorstore", *SERVICES)}
+        self.env = {**os.environ, "PYTHONPATH": ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""),
+                    "MESSAGE_BUS_TYPE": "cfcbroker", "CFC_BROKER_HOST": "127.0.0.1",
+                    "CFC_BROKER_PORT": str(self.ports["broker"]),
+                    "DOCUMENT_STORE_TYPE": "cfcstore", "CFC_DOCSTORE_HOST": "127.0.0.1",
+                    "CFC_DOCSTORE_PORT": str(self.ports["docstore"]),
+                    "VECTOR_STORE_TYPE": "qdrant", "QDRANT_HOST": "127.0.0.1",
+                    "QDRANT_PORT": str(self.ports["vectorstore"]), "VECTOR_STORE_DEVICE": "cpu",
+                    "EMBEDDING_BACKEND_TYPE": "mock", "LLM_BACKEND_TYPE": "mock", "MOCK_LATENCY_MS": "0",
+                    "ARCHIVE_STORE_TYPE": "local", "ARCHIVE_BASE_PATH": str(tmp / "archives"),
+                    "INGESTION_STORAGE_PATH": str(tmp / "ingestion"),
+                    "METRICS_TYPE": "noop", "LOG_TYPE": "silent", "ERROR_REPORTER_TYPE": "silent",
+                    "SECRET_PROVIDER_TYPE": "env", "JWT_AUTH_ENABLED": "false", "CUDA_VISIBLE_DEVICES": "",
+                    "HIP_VISIBLE_DEVICES": "", "OMP_NUM_THREADS": "1"}
+
+    def start(self, name: str, *extra: str) -> None:
+        log = open(self.tmp / f"{name}.log", "ab")
+        cmd = [sys.executable, "-m", "copilot_for_consensus_amd.services.main", name, "--port", str(self.ports[name]),
+               *extra]
+        self.procs[name] = subprocess.Popen(cmd, env=self.env, stdout=log, stderr=subprocess.STDOUT,
+                                            start_new_session=True)
+
+    def wait_tcp(self, name: str, timeout=60) -> None:
+        deadline = time.time() + timeout
+        while time.time() < deadline:
+            self._alive(name)
+            try:
+                socket.create_connection(("127.0.0.1", self.ports[name]), timeout=1).close()
+                return
+            except OSError:
+                time.sleep(0.1)
+        raise TimeoutError(f"{name} did not listen: {self.log(name)}")
+
+    def wait_ready(self, name: str, timeout=120) -> None:
+        deadline = time.time() + timeout
+        while time.time() < deadline:
+            self._alive(name)
+            try:
+                if _http("GET", self.url(name, "/readyz"), timeout=2)[0] == 200:
+                    return
+            except OSError:
+                pass
+            time.sleep(0.2)
+        raise TimeoutError(f"{name} not ready: {self.log(name)}")
+
+    def _alive(self, name):
+        p = self.procs[name]
+        if p.poll() is not None:
+            raise RuntimeError(f"{name} exited {p.returncode}: {self.log(name)}")
+
+    def url(self, name: str, path: str) -> str:
+        return f"http://127.0.0.1:{self.ports[name]}{path}"
+
+    def log(self, name: str) -> str:
+        try:
+            lines = (self.tmp / f"{name}.log").read_text(errors="replace").splitlines()
+            return "\n".join(ln for ln in lines if "uvicorn.access" not in ln)[-3000:]
+        except OSError:
+            return ""
+
+    def kill(self, name: str, sig=signal.SIGKILL) -> None:
+        p = self.procs.pop(name)
+        os.killpg(p.pid, sig)
+        p.wait(30)
+
+    def stop_all(self) -> None:
+        for name in list(self.procs):
+            p = self.procs.pop(name)
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                    p.wait(15)
+                except Exception:
+                    os.killpg(p.pid, signal.SIGKILL)
+                    p.wait(5)
+
+
+@pytest.fixture
+def deployment(tmp_path):
+    d = Deployment(tmp_path)
+    yield d
+    d.stop_all()
+
+
+def _reports(d) -> list:
+    code, body = _http("GET", d.url("reporting", "/api/reports?limit=100"))
+    return body["reports"] if code == 200 else []
+
+
+def _wait_reports(d, n, timeout=180) -> list:
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        r = _reports(d)
+        if len(r) >= n:
+            return r
+        for s in list(d.procs):
+            d._alive(s)
+        time.sleep(0.3)
+    from copilot_for_consensus_amd.bus.cfcbroker import Connection
+    stats = Connection("127.0.0.1", d.ports["broker"]).stats()["queues"]
+    logs = "\n".join(f"--- {s}\n{d.log(s)}" for s in SERVICES)
+    raise TimeoutError(f"{len(_reports(d))} of {n} reports; queues {stats}\n{logs}")
+
+
+@pytest.mark.timeout(600)
+def test_services_as_processes_over_broker_and_stores(deployment, tmp_path):
+    from copilot_for_consensus_amd.bus.cfcbroker import Connection
+    from copilot_for_consensus_amd.utils.synthetic import SyntheticArchive
+
+    d = deployment
+    d.start("broker", "--data-dir", str(tmp_path / "broker"))
+    d.start("docstore", "--data-dir", str(tmp_path / "docstore"))
+    d.start("vectorstore")
+    for n in ("broker", "docstore", "vectorstore"):
+        d.wait_tcp(n)
+    for s in SERVICES:
+        d.start(s)
+    for s in SERVICES:
+        d.wait_ready(s)
+
+    src = tmp_path / "src"
+    src.mkdir()
+    shutil.copy(FIX, src / "list.mbox")
+    code, body = _http("POST", d.url("ingestion", "/api/sources"), {"name": "wg", "source_type": "local",
+                                                                     "url": str(src)})
+    assert code == 201, body
+    code, body = _http("POST", d.url("ingestion", "/api/sources/wg/trigger"))
+    assert code == 200 and len(body["archive_ids"]) == 1, body
+    reports = _wait_reports(d, 2)
+    code, threads = _http("GET", d.url("reporting", "/api/threads"))
+    assert all(t["summary_id"] for t in threads["threads"])
+    code, rep = _http("GET", d.url("reporting", f"/api/reports/{reports[0]['_id']}"))
+    assert code == 200 and rep["content_markdown"]
+    # semantic topic search: reporting embeds the topic, the vector store answers over REST
+    code, msgs = _http("GET", d.url("reporting", f"/api/messages?thread_id={rep['thread_id']}"))
+    topic = urllib.request.quote(msgs["messages"][0]["body_normalized"][:120])
+    code, hits = _http("GET", d.url("reporting", f"/api/reports/search?topic={topic}&min_score=0.0"))
+    assert code == 200 and hits["count"] >= 1, hits
+
+    # chunking dies; a second archive arrives while it is down; its events wait in the broker
+    d.kill("chunking")
+    mbox = SyntheticArchive(seed=7).mbox(3)
+    boundary = "cfcboundary"
+    form = (f"--{boundary}\r\nContent-Disposition: form-data; name=\"file\"; filename=\"late.mbox\"\r\n"
+            f"Content-Type: application/mbox\r\n\r\n").encode() + mbox + f"\r\n--{boundary}--\r\n".encode()
+    code, body = _http("POST", d.url("ingestion", "/api/uploads"), form,
+                       headers={"Content-Type": f"multipart/form-data; boundary={boundary}"})
+    assert code == 201, body
+    code, body = _http("POST", d.url("ingestion", "/api/sources"),
+                       {"name": "late", "source_type": "local", "url": body.get("server_path") or body.get("path")})
+    code, body = _http("POST", d.url("ingestion", "/api/sources/late/trigger"))
+    assert code == 200 and len(body["archive_ids"]) == 1, body
+    admin = Connection("127.0.0.1", d.ports["broker"])
+    deadline = time.time() + 60
+    while time.time() < deadline and admin.stats()["queues"]["chunking"]["ready"] == 0:
+        time.sleep(0.2)
+    assert admin.stats()["queues"]["chunking"]["ready"] > 0      # parsed, waiting for chunking
+    assert len(_reports(d)) == 2
+    d.start("chunking")
+    reports = _wait_reports(d, 5)
+    assert len(reports) == 5
+    st = admin.stats()["queues"]
+    assert all(st[q]["ready"] == 0 and st[q]["unacked"] == 0 for q in SERVICES if q in st)
+    assert not any(q.endswith(".dlq") and v["ready"] for q, v in st.items())
