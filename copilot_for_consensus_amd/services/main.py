@@ -65,8 +65,9 @@ def main(argv=None) -> int:
     from .base import create_app, run_service
     from .node import Node
     try:
-        node = Node()
-        node.connect(None if args.service == "node" else [args.service])
+        only = None if args.service == "node" else [args.service]
+        node = Node(services=only)
+        node.connect(only)
     except Exception as e:  # noqa: BLE001 -- fail fast: a service that cannot reach its bus/store exits 1
         print(f"[{args.service}] start-up failed: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
         return 1

@@ -31,24 +31,41 @@ from .reporting import ReportingService
 class Node:
     """All pipeline services in one process, sharing the broker, stores and GPU models."""
 
+    # adapters each service needs (so a one-service process builds only its own: the summarization
+    # process alone loads the LLM, only embedding / reporting load the encoder)
+    NEEDS = {"ingestion": {"archives"}, "parsing": {"archives"}, "chunking": set(),
+             "embedding": {"embedder", "vectors"}, "orchestrator": {"vectors"}, "summarization": {"summarizer"},
+             "reporting": {"embedder", "vectors"}}
+
     def __init__(self, env: dict | None = None, broker: InProcBroker | None = None, document_store=None,
                  archive_store=None, embedding_provider=None, vector_store=None, summarizer=None,
-                 retry_config: RetryConfig | None = None):
+                 retry_config: RetryConfig | None = None, services=None):
+        names = [s for s in self.NEEDS if services is None or s in services]
+        need = set().union(*(self.NEEDS[s] for s in names))
         self.broker = broker or InProcBroker()
-        cfgs = {s: get_config(s, env=env) for s in ("ingestion", "parsing", "chunking", "embedding", "orchestrator",
-                                                    "summarization", "reporting")}
+        cfgs = {s: get_config(s, env=env) for s in names}
         self.cfgs = cfgs
-        c0 = cfgs["parsing"]
+        c0 = cfgs[names[0]]
         self.store = document_store or create_document_store(c0.document_store)
-        self.archives = archive_store or create_archive_store(cfgs["ingestion"].archive_store)
+        self.archives = archive_store or (create_archive_store(cfgs.get("ingestion", c0).archive_store)
+                                          if "archives" in need else None)
         self.metrics = create_metrics_collector(c0.metrics)
         self.logger = create_logger(c0.logger)
         self.errors = create_error_reporter(c0.error_reporter)
-        self.embedder = embedding_provider or create_embedding_provider(cfgs["embedding"].embedding_backend)
-        self.vectors = vector_store or create_vector_store(cfgs["embedding"].vector_store,
-                                                           dimension=int(self.embedder.dimension))
-        self.summarizer = summarizer or create_llm_backend(cfgs["summarization"].llm_backend)
-        retry = retry_config or RetryConfig.from_adapter(c0.event_retry)
+        ecfg = cfgs.get("embedding", c0)
+        self.embedder = embedding_provider or (create_embedding_provider(ecfg.embedding_backend)
+                                               if "embedder" in need else None)
+        if vector_store is not None or "vectors" not in need:
+            self.vectors = vector_store
+        else:
+            dim = int(self.embedder.dimension) if self.embedder is not None else \
+                int(ecfg.vector_store.driver_config.get("dimension") or
+                    ecfg.vector_store.driver_config.get("vector_size") or 384)
+            self.vectors = create_vector_store(ecfg.vector_store, dimension=dim)
+        self.summarizer = summarizer or (create_llm_backend(cfgs["summarization"].llm_backend)
+                                         if "summarizer" in need else None)
+        rcfg = next((c.event_retry for c in cfgs.values() if hasattr(c, "event_retry")), None)
+        retry = retry_config or (RetryConfig.from_adapter(rcfg) if rcfg is not None else RetryConfig())
         common = dict(metrics=self.metrics, logger=self.logger, error_reporter=self.errors, retry_config=retry)
 
         def pub(name):
@@ -57,34 +74,36 @@ class Node:
         def sub(name):
             return create_subscriber(cfgs[name].message_bus, broker=self.broker, queue_name=name)
 
-        o, sm, r = cfgs["orchestrator"], cfgs["summarization"], cfgs["reporting"]
-        self.services = {
-            "ingestion": IngestionService(pub("ingestion"), self.store, self.archives,
-                                          storage_path=cfgs["ingestion"].storage_path if env_is_set(
-                                              "INGESTION_STORAGE_PATH", env) else None,
-                                          max_retries=cfgs["ingestion"].max_retries, **common),
-            "parsing": ParsingService(pub("parsing"), sub("parsing"), self.store, self.archives, **common),
-            "chunking": ChunkingService(pub("chunking"), sub("chunking"), self.store,
-                                        create_chunker(cfgs["chunking"].chunker), **common),
-            "embedding": EmbeddingService(pub("embedding"), sub("embedding"), self.store, self.embedder, self.vectors,
-                                          max_retries=cfgs["embedding"].max_retries, retry_backoff_seconds=0.1,
-                                          **common),
-            "orchestrator": OrchestratorService(pub("orchestrator"), sub("orchestrator"), self.store, self.vectors,
-                                                top_k=o.top_k, context_window_tokens=o.context_window_tokens,
-                                                chunk_selection_strategy=o.chunk_selection_strategy,
-                                                system_prompt_path=o.system_prompt_path,
-                                                user_prompt_path=o.user_prompt_path,
-                                                consensus_detector=create_consensus_detector(o.consensus_detector),
-                                                **common),
-            "summarization": SummarizationService(pub("summarization"), sub("summarization"), self.store,
-                                                  self.summarizer, citation_count=sm.citation_count,
-                                                  context_window_tokens=sm.context_window_tokens,
-                                                  max_batch_threads=sm.max_batch_threads,
-                                                  batch_wait_ms=sm.batch_wait_ms, retry_delay_seconds=0.1, **common),
-            "reporting": ReportingService(pub("reporting"), sub("reporting"), self.store, self.vectors, self.embedder,
-                                          notify_enabled=r.notify_enabled, notify_webhook_url=r.notify_webhook_url,
-                                          **common),
+        build = {
+            "ingestion": lambda: IngestionService(
+                pub("ingestion"), self.store, self.archives,
+                storage_path=cfgs["ingestion"].storage_path if env_is_set("INGESTION_STORAGE_PATH", env) else None,
+                max_retries=cfgs["ingestion"].max_retries, **common),
+            "parsing": lambda: ParsingService(pub("parsing"), sub("parsing"), self.store, self.archives, **common),
+            "chunking": lambda: ChunkingService(pub("chunking"), sub("chunking"), self.store,
+                                                create_chunker(cfgs["chunking"].chunker), **common),
+            "embedding": lambda: EmbeddingService(pub("embedding"), sub("embedding"), self.store, self.embedder,
+                                                  self.vectors, max_retries=cfgs["embedding"].max_retries,
+                                                  retry_backoff_seconds=0.1, **common),
+            "orchestrator": lambda: OrchestratorService(
+                pub("orchestrator"), sub("orchestrator"), self.store, self.vectors, top_k=cfgs["orchestrator"].top_k,
+                context_window_tokens=cfgs["orchestrator"].context_window_tokens,
+                chunk_selection_strategy=cfgs["orchestrator"].chunk_selection_strategy,
+                system_prompt_path=cfgs["orchestrator"].system_prompt_path,
+                user_prompt_path=cfgs["orchestrator"].user_prompt_path,
+                consensus_detector=create_consensus_detector(cfgs["orchestrator"].consensus_detector), **common),
+            "summarization": lambda: SummarizationService(
+                pub("summarization"), sub("summarization"), self.store, self.summarizer,
+                citation_count=cfgs["summarization"].citation_count,
+                context_window_tokens=cfgs["summarization"].context_window_tokens,
+                max_batch_threads=cfgs["summarization"].max_batch_threads,
+                batch_wait_ms=cfgs["summarization"].batch_wait_ms, retry_delay_seconds=0.1, **common),
+            "reporting": lambda: ReportingService(
+                pub("reporting"), sub("reporting"), self.store, self.vectors, self.embedder,
+                notify_enabled=cfgs["reporting"].notify_enabled,
+                notify_webhook_url=cfgs["reporting"].notify_webhook_url, **common),
         }
+        self.services = {n: build[n]() for n in names}
         self._threads: list[threading.Thread] = []
         self._connected = False
 

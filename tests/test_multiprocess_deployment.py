@@ -51,7 +51,7 @@ def _http(method: str, url: str, body=None, headers=None, timeout=10):
 
 
 class Deployment:
-    def __init__(self, tmp):
+    def __init__(self, tmp, overrides: dict | None = None):
         self.tmp = tmp
         self.procs: dict[str, subprocess.Popen] = {}
         self.ports = {n: _free_port() for n in ("broker", "docstore", "vectorstore", *SERVICES)}
@@ -68,6 +68,11 @@ class Deployment:
                     "METRICS_TYPE": "noop", "LOG_TYPE": "silent", "ERROR_REPORTER_TYPE": "silent",
                     "SECRET_PROVIDER_TYPE": "env", "JWT_AUTH_ENABLED": "false", "CUDA_VISIBLE_DEVICES": "",
                     "HIP_VISIBLE_DEVICES": "", "OMP_NUM_THREADS": "1"}
+        for k, v in (overrides or {}).items():
+            if v is None:
+                self.env.pop(k, None)
+            else:
+                self.env[k] = v
 
     def start(self, name: str, *extra: str) -> None:
         log = open(self.tmp / f"{name}.log", "ab")
@@ -133,9 +138,15 @@ class Deployment:
 
 @pytest.fixture
 def deployment(tmp_path):
-    d = Deployment(tmp_path)
-    yield d
-    d.stop_all()
+    made = []
+
+    def make(overrides=None):
+        made.append(Deployment(tmp_path, overrides))
+        return made[-1]
+
+    yield make
+    for d in made:
+        d.stop_all()
 
 
 def _reports(d) -> list:
@@ -160,10 +171,26 @@ def _wait_reports(d, n, timeout=180) -> list:
 
 @pytest.mark.timeout(600)
 def test_services_as_processes_over_broker_and_stores(deployment, tmp_path):
+    """CPU: mock embedding + mock LLM (the reference CI's configuration), HIP index on the CPU path."""
+    _run(deployment(), tmp_path)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_services_as_processes_on_the_gpu(deployment, tmp_path):
+    """MI355X: the embedding and reporting processes run the HIP MiniLM encoder, the vector store
+    process holds the index in HBM behind the Qdrant REST API, the summarization process runs the
+    HIP decoder (tiny preset, random init) -- four processes sharing the GPU."""
+    _run(deployment({"CUDA_VISIBLE_DEVICES": None, "HIP_VISIBLE_DEVICES": None, "EMBEDDING_BACKEND_TYPE": "hip",
+                     "EMBEDDING_DEVICE": "cuda", "VECTOR_STORE_DEVICE": "cuda", "LLM_BACKEND_TYPE": "hip",
+                     "LLM_MODEL_PRESET": "tiny", "LLM_MAX_NEW_TOKENS": "32", "LLM_KV_CACHE_TOKENS": "65536"}),
+         tmp_path)
+
+
+def _run(d, tmp_path):
     from copilot_for_consensus_amd.bus.cfcbroker import Connection
     from copilot_for_consensus_amd.utils.synthetic import SyntheticArchive
 
-    d = deployment
     d.start("broker", "--data-dir", str(tmp_path / "broker"))
     d.start("docstore", "--data-dir", str(tmp_path / "docstore"))
     d.start("vectorstore")
