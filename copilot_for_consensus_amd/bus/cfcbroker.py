@@ -420,6 +420,36 @@ class CfcBrokerFailedQueues:
         self.conn.publish(self.exchange, routing_key, json.dumps(event).encode())
 
 
+class CfcBrokerMonitor:
+    """Queue gauges for tools/exporters.py (the reference reads them from the RabbitMQ management
+    API for its queue-lag alerts, infra/prometheus/alerts/queue_lag.yml)."""
+
+    def __init__(self, host: str = "localhost", port: int = DEFAULT_PORT):
+        self.host, self.port = host, int(port)
+        self.conn: Connection | None = None
+
+    def stats(self) -> dict:
+        for attempt in range(2):
+            try:
+                if self.conn is None or self.conn.closed:
+                    self.conn = Connection(self.host, self.port, name="monitor")
+                return self.conn.stats()
+            except (OSError, ConnectionError, TimeoutError):
+                self.conn = None
+                if attempt:
+                    raise
+        return {}
+
+    def queues(self) -> dict[str, int]:
+        return {q: v["ready"] for q, v in self.stats().get("queues", {}).items()}
+
+    def consumer_counts(self) -> dict[str, int]:
+        return {q: v["consumers"] for q, v in self.stats().get("queues", {}).items()}
+
+    def queue_details(self) -> dict[str, dict]:
+        return self.stats().get("queues", {})
+
+
 def spawn_broker(port: int = 0, data_dir: str | os.PathLike | None = None, host: str = "127.0.0.1",
                  fsync: bool = True, max_redeliveries: int = 5, binary: str | os.PathLike | None = None,
                  timeout: float = 10.0) -> tuple[subprocess.Popen, int]:

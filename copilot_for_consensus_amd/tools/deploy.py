@@ -12,7 +12,9 @@ topology of the reference.  Here:
   carry the reference's SLO thresholds (parse P95 > 5 s, chunk > 2 s, embed > 10 s, summarize
   > 30 s, reporting API > 0.5 s);
 * docker-compose: one MI355X node runs the whole pipeline in one process (``node``) with the GPU
-  devices mapped; the per-service form is emitted too for multi-host deployments;
+  devices mapped; the per-service form is emitted too for multi-host deployments, with the
+  reference's RabbitMQ + MongoDB (docker-compose.yml) or with this framework's native broker,
+  document store server and HIP vector store (docker-compose.native.yml);
 * the eight alert groups, eleven Grafana dashboards, Loki/Promtail, the Mongo bootstrap script and
   the Kubernetes manifests come from :mod:`.ops_assets`.
 
@@ -169,6 +171,41 @@ def compose() -> str:
     return "\n".join(out) + "\n"
 
 
+def compose_native() -> str:
+    """One service per container with this framework's own infrastructure in place of RabbitMQ,
+    MongoDB and Qdrant: the native broker (csrc/broker), the document store server (WAL +
+    snapshots) and the HIP index behind Qdrant's REST API, each on a persistent volume."""
+    gpu = ["    devices: ['/dev/kfd', '/dev/dri']", "    group_add: ['video', 'render']", "    ipc: host"]
+    env = ["      - MESSAGE_BUS_TYPE=cfcbroker", "      - CFC_BROKER_HOST=messagebus", "      - CFC_BROKER_PORT=5680",
+           "      - DOCUMENT_STORE_TYPE=cfcstore", "      - CFC_DOCSTORE_HOST=documentdb", "      - CFC_DOCSTORE_PORT=27027",
+           "      - VECTOR_STORE_TYPE=qdrant", "      - QDRANT_HOST=vectorstore", "      - QDRANT_PORT=6333",
+           "      - ARCHIVE_STORE_TYPE=local", "      - ARCHIVE_BASE_PATH=/data/raw_archives",
+           "      - METRICS_TYPE=prometheus", "      - HSA_ENABLE_IPC_MODE_LEGACY=0"]
+    img = "    image: copilot-for-consensus-amd:latest"
+    out = ["services:",
+           "  messagebus:", img, "    command: python -m copilot_for_consensus_amd.services.main broker --port 5680 "
+           "--data-dir /data/broker", "    volumes: ['broker:/data/broker']",
+           "    healthcheck: {test: ['CMD', 'python', '-c', \"import socket; socket.create_connection(('localhost', 5680))\"]}",
+           "  documentdb:", img, "    command: python -m copilot_for_consensus_amd.services.main docstore --port 27027 "
+           "--data-dir /data/docstore", "    volumes: ['docstore:/data/docstore']",
+           "  vectorstore:", img, "    command: python -m copilot_for_consensus_amd.services.main vectorstore --port 6333 "
+           "--data-dir /data/vectors", "    volumes: ['vectors:/data/vectors']"] + gpu + \
+          ["    environment:", "      - VECTOR_STORE_DEVICE=cuda", "      - HSA_ENABLE_IPC_MODE_LEGACY=0"]
+    for svc, port in SERVICE_PORTS.items():
+        if svc == "auth":
+            continue
+        out += [f"  {svc}:", img, f"    command: python -m copilot_for_consensus_amd.services.main {svc} --port {port}",
+                f"    ports: ['{port}:{port}']"]
+        if svc in ("embedding", "summarization", "reporting"):
+            out += gpu
+        out += ["    environment:"] + env
+        if svc in ("ingestion", "parsing"):
+            out += ["    volumes: ['archives:/data/raw_archives']"]
+        out += ["    depends_on: [messagebus, documentdb, vectorstore]", "    restart: unless-stopped"]
+    out += ["volumes:", "  broker: {}", "  docstore: {}", "  vectors: {}", "  archives: {}"]
+    return "\n".join(out) + "\n"
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description="Write RabbitMQ definitions, Prometheus config/alerts, compose file")
     ap.add_argument("--out", default="deploy")
@@ -180,6 +217,7 @@ def main(argv=None) -> int:
     (out / "prometheus" / "prometheus.yml").write_text(prometheus_config())
     (out / "prometheus" / "alerts.yml").write_text(alert_rules())
     (out / "docker-compose.yml").write_text(compose())
+    (out / "docker-compose.native.yml").write_text(compose_native())
     (out / "grafana" / "dashboards").mkdir(parents=True, exist_ok=True)
     (out / "grafana" / "dashboards" / "copilot-mi355x.json").write_text(json.dumps(grafana_dashboard(), indent=2) + "\n")
     from . import ops_assets as ops

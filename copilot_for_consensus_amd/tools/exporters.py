@@ -93,6 +93,11 @@ class PipelineExporter:
                 for q, depth in sorted(self.broker.queues().items()):
                     out.append(_fmt("copilot_queue_messages", {"queue": q}, depth))
                     out.append(_fmt("copilot_queue_consumers", {"queue": q}, consumers.get(q, 0)))
+                details = getattr(self.broker, "queue_details", None)
+                for q, v in sorted((details() if details else {}).items()):   # native broker counters
+                    out.append(_fmt("copilot_queue_messages_unacked", {"queue": q}, v["unacked"]))
+                    out.append(_fmt("copilot_queue_dead_lettered_total", {"queue": q}, v["dead_lettered"]))
+                    out.append(_fmt("copilot_queue_redelivered_total", {"queue": q}, v["redelivered"]))
             except Exception:
                 self.scrape_errors += 1
         if self.gpus:
@@ -140,7 +145,14 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description="Pipeline document-state Prometheus exporter")
     ap.add_argument("--port", type=int, default=9502)
     a = ap.parse_args(argv)
-    PipelineExporter(create_document_store(load_adapter_config("document_store"))).serve(a.port)
+    bus = load_adapter_config("message_bus")
+    broker = None
+    if bus.driver_name == "cfcbroker":
+        from ..bus.cfcbroker import CfcBrokerMonitor
+        broker = CfcBrokerMonitor(bus.driver_config["broker_host"], bus.driver_config["broker_port"])
+    store = create_document_store(load_adapter_config("document_store"))
+    store.connect()
+    PipelineExporter(store, broker=broker).serve(a.port)
     while True:
         time.sleep(3600)
 

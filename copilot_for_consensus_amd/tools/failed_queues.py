@@ -5,7 +5,8 @@ QUEUE_MAPPINGS :44-52, list :98, inspect :125, export :183, requeue :230 with --
 :303 with --limit/--confirm).  Two backends behind one manager:
   * :class:`InProcFailedQueues` -- the in-process broker: ``<queue>.dlq`` dead letters (events that
     exhausted redeliveries) plus queues bound to the ``*.failed`` routing keys;
-  * :class:`RabbitMQFailedQueues` -- pika ``basic_get`` / ``basic_publish`` (import-gated).
+  * :class:`RabbitMQFailedQueues` -- pika ``basic_get`` / ``basic_publish`` (import-gated);
+  * ``bus.cfcbroker.CfcBrokerFailedQueues`` -- the native broker (``--backend cfcbroker``).
 Requeue republishes each message on the target routing key (the mapping, ``--target``, or for a
 dead letter its own routing key) and removes it from the failed queue only after the publish.
 
@@ -167,9 +168,10 @@ class FailedQueueManager:
 
 
 def main(argv=None) -> int:
-    ap = argparse.ArgumentParser(description="Manage failed-event queues (RabbitMQ)")
+    ap = argparse.ArgumentParser(description="Manage failed-event queues (RabbitMQ or the native cfc-broker)")
+    ap.add_argument("--backend", choices=["rabbitmq", "cfcbroker"], default="rabbitmq")
     ap.add_argument("--host", default="localhost")
-    ap.add_argument("--port", type=int, default=5672)
+    ap.add_argument("--port", type=int, default=None, help="default 5672 (rabbitmq) / 5680 (cfcbroker)")
     ap.add_argument("--username", default="guest")
     ap.add_argument("--password", default="guest")
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -182,7 +184,11 @@ def main(argv=None) -> int:
     p = sub.add_parser("purge"); p.add_argument("queue"); p.add_argument("--limit", type=int)
     p.add_argument("--dry-run", action="store_true"); p.add_argument("--confirm", action="store_true")
     a = ap.parse_args(argv)
-    m = FailedQueueManager(RabbitMQFailedQueues(a.host, a.port, a.username, a.password))
+    if a.backend == "cfcbroker":
+        from ..bus.cfcbroker import CfcBrokerFailedQueues
+        m = FailedQueueManager(CfcBrokerFailedQueues(a.host, a.port or 5680))
+    else:
+        m = FailedQueueManager(RabbitMQFailedQueues(a.host, a.port or 5672, a.username, a.password))
     if a.cmd == "list":
         print(json.dumps(m.list_failed_queues(), indent=2))
     elif a.cmd == "inspect":

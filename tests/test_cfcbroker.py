@@ -226,3 +226,38 @@ def test_subscriber_drain_and_malformed(broker):
     assert sub.drain(idle_timeout=0.5) == 2
     assert seen == ["JSONParsed"] and sub.failed == 1
     assert c.stats()["queues"]["chunking"]["unacked"] == 0
+
+
+def test_exporter_reads_native_broker(broker):
+    from copilot_for_consensus_amd.bus.cfcbroker import CfcBrokerMonitor
+    from copilot_for_consensus_amd.storage.document_store import InMemoryDocumentStore
+    from copilot_for_consensus_amd.tools.exporters import PipelineExporter
+    _, port = broker(max_redeliveries=0)
+    c = Connection("127.0.0.1", port)
+    c.declare("parsing", max_redeliveries=1)
+    c.bind("parsing", EXCHANGE, "archive.ingested")
+    c.publish(EXCHANGE, "archive.ingested", b"{}")
+    c.publish(EXCHANGE, "archive.ingested", b"{}")
+    c.consume("parsing", prefetch=1)
+    d = c.next_delivery(2)
+    c.nack(d.tag, requeue=False)
+    c.ping()
+    text = PipelineExporter(InMemoryDocumentStore(), broker=CfcBrokerMonitor("127.0.0.1", port)).render()
+    assert 'copilot_queue_messages{queue="parsing"} 0' in text          # the other one is unacked
+    assert 'copilot_queue_messages_unacked{queue="parsing"} 1' in text
+    assert 'copilot_queue_dead_lettered_total{queue="parsing"} 1' in text
+    assert 'copilot_queue_messages{queue="parsing.dlq"} 1' in text
+    assert 'copilot_queue_consumers{queue="parsing"} 1' in text
+
+
+def test_failed_queues_cli_on_native_broker(broker, capsys):
+    from copilot_for_consensus_amd.tools.failed_queues import main
+    _, port = broker()
+    CfcBrokerFailedQueues("127.0.0.1", port)        # declares the *.failed queues
+    c = Connection("127.0.0.1", port)
+    c.publish(EXCHANGE, "chunking.failed", json.dumps({"event_type": "ChunkingFailed", "data": {}}).encode())
+    assert main(["--backend", "cfcbroker", "--port", str(port), "list"]) == 0
+    rows = {r["queue"]: r["message_count"] for r in json.loads(capsys.readouterr().out)}
+    assert rows["chunking.failed"] == 1
+    assert main(["--backend", "cfcbroker", "--port", str(port), "purge", "chunking.failed", "--confirm"]) == 0
+    assert capsys.readouterr().out.strip() == "1"
