@@ -38,6 +38,7 @@ class BaseService:
                                       "last_event_at": None}
         self._ready = threading.Event()
         self._lock = threading.Lock()
+        self.consumer_thread: threading.Thread | None = None   # set by whoever runs the consume loop
 
     # ---------------------------------------------------------------- events
     def publish(self, event_type: str, **data) -> dict:
@@ -104,6 +105,10 @@ class BaseService:
     def is_ready(self) -> bool:
         return self._ready.is_set()
 
+    def consumer_alive(self) -> bool | None:
+        """None when no consume thread was started (synchronous / drain mode), else its liveness."""
+        return None if self.consumer_thread is None else self.consumer_thread.is_alive()
+
     def get_stats(self) -> dict:
         with self._lock:
             return dict(self.stats)
@@ -134,13 +139,18 @@ def create_app(service: BaseService, extra_routes: Callable | None = None, confi
 
     @app.get("/health")
     def health():
-        return {"status": "healthy", "service": service.name, "events_processed": service.stats["events_processed"]}
+        # a bus-driven service whose consumer thread died is unhealthy (reference reporting/main.py:79-103)
+        alive = service.consumer_alive()
+        return {"status": "unhealthy" if alive is False else "healthy", "service": service.name,
+                "events_processed": service.stats["events_processed"], "subscriber_thread_alive": alive}
 
     @app.get("/readyz")
     def readyz():
         if not service.is_ready():
-            raise HTTPException(503, "not ready")
-        return {"status": "ready"}
+            raise HTTPException(503, "Service not initialized")
+        if service.consumer_alive() is False:
+            raise HTTPException(503, "Subscriber thread not running")
+        return {"status": "ready", "service": service.name}
 
     @app.get("/stats")
     def stats():
@@ -175,6 +185,8 @@ def run_service(service: BaseService, app, host: str = "0.0.0.0", port: int = 80
             service.subscriber.start_consuming()
 
     t = threading.Thread(target=consume, name=f"{service.name}-consumer", daemon=False)
+    if service.subscriber is not None:
+        service.consumer_thread = t
     t.start()
     try:
         uvicorn.run(app, host=host, port=port, log_config=uvicorn_log_config())

@@ -130,6 +130,7 @@ class Node:
             for name, s in self.services.items():
                 if s.subscriber is not None:
                     t = threading.Thread(target=s.subscriber.start_consuming, name=f"{name}-consumer", daemon=True)
+                    s.consumer_thread = t
                     t.start()
                     self._threads.append(t)
 

@@ -96,12 +96,19 @@ class ReportingService(BaseService):
 
     # ------------------------------------------------------------------ read path
     def _thread_filter_ok(self, t, start, end, min_p, max_p, min_m, max_m, source, archives):
+        """Reference filter semantics (reporting/app/service.py:660-699, 1066-1107): date filters keep
+        threads whose [first, last] message range overlaps [start, end] inclusively and skip threads
+        without both dates; participant / message counts inclusive; source via the thread's archive."""
         if t is None:
             return False
-        if start and (t.get("last_message_date") or "") < start:
-            return False
-        if end and (t.get("first_message_date") or "") > end:
-            return False
+        if start is not None or end is not None:
+            first, last = t.get("first_message_date"), t.get("last_message_date")
+            if not first or not last:
+                return False
+            if end is not None and first > end:
+                return False
+            if start is not None and last < start:
+                return False
         n_p = len(t.get("participants") or [])
         if (min_p is not None and n_p < min_p) or (max_p is not None and n_p > max_p):
             return False
@@ -109,34 +116,61 @@ class ReportingService(BaseService):
         if (min_m is not None and n_m < min_m) or (max_m is not None and n_m > max_m):
             return False
         if source:
-            a = archives.get(t.get("archive_id"))
-            if a is None:
-                a = self.store.get_document("archives", t.get("archive_id", ""))
-                archives[t.get("archive_id")] = a
+            a = self._archive(t.get("archive_id"), archives)
             if not a or a.get("source") != source:
                 return False
         return True
 
+    def _archive(self, archive_id, cache: dict):
+        if not archive_id:
+            return None
+        if archive_id not in cache:
+            cache[archive_id] = self.store.get_document("archives", archive_id)
+        return cache[archive_id]
+
+    @staticmethod
+    def _sort_missing_last(docs: list[dict], path: tuple[str, ...], order: str) -> list[dict]:
+        """Missing / empty values go last in either direction (reference service.py:722-741)."""
+        def val(d):
+            for k in path:
+                d = d.get(k) if isinstance(d, dict) else None
+            return d
+        present = [d for d in docs if val(d)]
+        missing = [d for d in docs if not val(d)]
+        present.sort(key=lambda d: str(val(d)), reverse=order == "desc")
+        return present + missing
+
     def get_reports(self, thread_id=None, limit=10, skip=0, message_start_date=None, message_end_date=None,
                     source=None, min_participants=None, max_participants=None, min_messages=None,
                     max_messages=None, sort_by="generated_at", sort_order="desc") -> list[dict]:
+        """Summaries enriched with ``thread_metadata`` / ``archive_metadata`` (reports whose thread is
+        gone are skipped), thread-level filters, sort by ``generated_at`` or ``thread_start_date``."""
         flt = {"thread_id": thread_id} if thread_id else {}
-        thread_filters = any(x is not None for x in (message_start_date, message_end_date, source, min_participants,
-                                                     max_participants, min_messages, max_messages))
-        docs = self.store.query_documents("summaries", flt, limit=1 << 30 if thread_filters else limit + skip,
-                                          sort_by=sort_by if sort_by in ("generated_at", "first_message_date",
-                                                                         "last_message_date", "thread_id") else
-                                          "generated_at", sort_order=sort_order)
-        if thread_filters:
-            archives: dict = {}
-            kept = []
-            for d in docs:
-                t = self.store.get_document("threads", d.get("thread_id", ""))
-                if self._thread_filter_ok(t, message_start_date, message_end_date, min_participants,
-                                          max_participants, min_messages, max_messages, source, archives):
-                    kept.append(d)
-            docs = kept
-        return docs[skip:skip + limit]
+        docs = self.store.query_documents("summaries", flt, limit=1 << 30)
+        tids = list({d.get("thread_id") for d in docs if d.get("thread_id")})
+        threads = {t["_id"]: t for t in self.store.query_documents("threads", {"_id": {"$in": tids}},
+                                                                    limit=len(tids) or 1)} if tids else {}
+        archives: dict = {}
+        out = []
+        for d in docs:
+            t = threads.get(d.get("thread_id"))
+            if t is None or not self._thread_filter_ok(t, message_start_date, message_end_date, min_participants,
+                                                       max_participants, min_messages, max_messages, source,
+                                                       archives):
+                continue
+            parts = t.get("participants") or []
+            d["thread_metadata"] = {"subject": t.get("subject", ""), "participants": parts,
+                                    "participant_count": len(parts), "message_count": t.get("message_count", 0),
+                                    "first_message_date": t.get("first_message_date"),
+                                    "last_message_date": t.get("last_message_date")}
+            a = self._archive(t.get("archive_id"), archives)
+            if a:
+                d["archive_metadata"] = {"source": a.get("source", ""), "source_url": a.get("source_url", ""),
+                                         "ingestion_date": a.get("ingestion_date")}
+            out.append(d)
+        path = ("thread_metadata", "first_message_date") if sort_by == "thread_start_date" else ("generated_at",)
+        out = self._sort_missing_last(out, path, sort_order)
+        return out[skip:skip + limit]
 
     def search_reports_by_topic(self, topic: str, limit: int = 10, min_score: float = 0.5) -> list[dict]:
         if self.vectors is None or self.embedder is None:
@@ -177,14 +211,22 @@ class ReportingService(BaseService):
 
     def get_threads(self, limit=10, skip=0, archive_id=None, message_start_date=None, message_end_date=None,
                     source=None, min_participants=None, max_participants=None, min_messages=None, max_messages=None,
-                    sort_by="first_message_date", sort_order="desc"):
+                    sort_by=None, sort_order="desc"):
+        """Threads with the reference's filters, each enriched with ``archive_source``."""
         flt = {"archive_id": archive_id} if archive_id else {}
-        docs = self.store.query_documents("threads", flt, limit=1 << 30, sort_by=sort_by, sort_order=sort_order)
+        docs = self.store.query_documents("threads", flt, limit=1 << 30)
         archives: dict = {}
-        docs = [t for t in docs if self._thread_filter_ok(t, message_start_date, message_end_date, min_participants,
-                                                           max_participants, min_messages, max_messages, source,
-                                                           archives)]
-        return docs[skip:skip + limit]
+        out = []
+        for t in docs:
+            if not self._thread_filter_ok(t, message_start_date, message_end_date, min_participants,
+                                          max_participants, min_messages, max_messages, source, archives):
+                continue
+            a = self._archive(t.get("archive_id"), archives)
+            t["archive_source"] = a.get("source") if a else None
+            out.append(t)
+        if sort_by:
+            out = self._sort_missing_last(out, (sort_by,), sort_order)
+        return out[skip:skip + limit]
 
     def get_sources(self) -> list[str]:
         return sorted({a.get("source") for a in self.store.query_documents("archives", {}, limit=1 << 30)
@@ -201,7 +243,8 @@ def reporting_routes(app, service: ReportingService, auth=None):
                 message_start_date: str | None = None, message_end_date: str | None = None, source: str | None = None,
                 min_participants: int | None = Query(None, ge=0), max_participants: int | None = Query(None, ge=0),
                 min_messages: int | None = Query(None, ge=0), max_messages: int | None = Query(None, ge=0),
-                sort_by: str = "generated_at", sort_order: str = Query("desc", pattern="^(asc|desc)$")):
+                sort_by: str = Query("generated_at", pattern="^(thread_start_date|generated_at)$"),
+                sort_order: str = Query("desc", pattern="^(asc|desc)$")):
         r = service.get_reports(thread_id, limit, skip, message_start_date, message_end_date, source,
                                 min_participants, max_participants, min_messages, max_messages, sort_by, sort_order)
         return {"reports": r, "count": len(r), "limit": limit, "skip": skip}
@@ -240,7 +283,8 @@ def reporting_routes(app, service: ReportingService, auth=None):
                 message_start_date: str | None = None, message_end_date: str | None = None, source: str | None = None,
                 min_participants: int | None = Query(None, ge=0), max_participants: int | None = Query(None, ge=0),
                 min_messages: int | None = Query(None, ge=0), max_messages: int | None = Query(None, ge=0),
-                sort_by: str = "first_message_date", sort_order: str = Query("desc", pattern="^(asc|desc)$")):
+                sort_by: str | None = Query(None, pattern="^(first_message_date|last_message_date)$"),
+                sort_order: str = Query("desc", pattern="^(asc|desc)$")):
         r = service.get_threads(limit, skip, archive_id, message_start_date, message_end_date, source,
                                 min_participants, max_participants, min_messages, max_messages, sort_by, sort_order)
         return {"threads": r, "count": len(r), "limit": limit, "skip": skip}

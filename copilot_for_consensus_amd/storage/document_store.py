@@ -135,6 +135,10 @@ class InMemoryDocumentStore(DocumentStore):
         self._index_fields = dict(DEFAULT_INDEXES if indexes is None else indexes)
         self._idx: dict[tuple[str, str], dict[Any, set]] = defaultdict(lambda: defaultdict(set))
         self._overflow: dict[tuple[str, str], set] = defaultdict(set)
+        # insertion sequence per document: index-narrowed scans return documents in insertion
+        # ("natural") order, as a full scan and MongoDB do
+        self._seq: dict[tuple[str, str], int] = {}
+        self._next_seq = 0
         self.connected = False
 
     @classmethod
@@ -225,6 +229,8 @@ class InMemoryDocumentStore(DocumentStore):
             d = copy.deepcopy(doc)
             d["_id"] = doc_id
             coll[doc_id] = d
+            self._seq[(collection, doc_id)] = self._next_seq
+            self._next_seq += 1
             self._index_add(collection, d)
             return doc_id
 
@@ -236,7 +242,11 @@ class InMemoryDocumentStore(DocumentStore):
     def _select(self, collection, filter_dict):
         coll = self.collections[collection]
         cand = self._candidates(collection, filter_dict)
-        it = (coll[i] for i in cand if i in coll) if cand is not None else coll.values()
+        if cand is not None:
+            seq = self._seq
+            it = (coll[i] for i in sorted((i for i in cand if i in coll), key=lambda i: seq.get((collection, i), 0)))
+        else:
+            it = coll.values()
         return [d for d in it if matches(d, filter_dict)]
 
     def query_documents(self, collection: str, filter_dict: dict[str, Any] | None = None, limit: int = 100,
@@ -286,6 +296,7 @@ class InMemoryDocumentStore(DocumentStore):
             if d is None:
                 raise DocumentNotFoundError(f"Document {doc_id} not found in collection {collection}")
             self._index_remove(collection, d)
+            self._seq.pop((collection, doc_id), None)
 
     def delete_many(self, collection: str, filter_dict: dict) -> int:
         with self._lock:
@@ -293,6 +304,7 @@ class InMemoryDocumentStore(DocumentStore):
             for d in docs:
                 self.collections[collection].pop(d["_id"], None)
                 self._index_remove(collection, d)
+                self._seq.pop((collection, d["_id"]), None)
             return len(docs)
 
     def clear_collection(self, collection: str) -> None:

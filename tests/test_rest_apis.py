@@ -136,9 +136,12 @@ def test_reporting_filters_pagination_sorting(stack):
     assert rep.get("/api/threads/doesnotexist/summary").status_code == 404
     assert rep.get("/api/messages/doesnotexist").status_code == 404
     assert rep.get("/api/chunks/doesnotexist").status_code == 404
-    th = rep.get("/api/threads", params={"limit": 10, "sort_by": "message_count", "sort_order": "asc"}).json()
-    counts = [t["message_count"] for t in th["threads"]]
-    assert counts == sorted(counts)
+    th = rep.get("/api/threads", params={"limit": 10, "sort_by": "first_message_date", "sort_order": "asc"}).json()
+    firsts = [t["first_message_date"] for t in th["threads"]]
+    assert firsts == sorted(firsts) and all(t["archive_source"] == "wg" for t in th["threads"])
+    # the reference accepts only these sort keys (reporting/main.py:152-156, 319-323)
+    assert rep.get("/api/threads", params={"sort_by": "message_count"}).status_code == 422
+    assert rep.get("/api/reports", params={"sort_by": "title"}).status_code == 422
     assert rep.get("/api/reports/search", params={"topic": "x", "limit": 51}).status_code == 422
 
 
