@@ -184,8 +184,16 @@ class IngestionService(BaseService):
             return False, f"Source '{name}' not found", []
         if not src.get("enabled", True):
             return False, f"Source '{name}' is disabled", []
+        # a manual trigger re-ingests everything the source holds: its archive records are dropped
+        # first so the checksum dedupe lets the files through again (reference service.py:1733-1772);
+        # downstream stages are idempotent on the deterministic ids, so nothing is duplicated
+        deleted = self.delete_archives_for_source(name)
         ids = self.ingest_archive(src)
-        return True, f"Ingested {len(ids)} archive(s)", ids
+        return True, f"Ingested {len(ids)} archive(s) ({deleted} previous record(s) reset)", ids
+
+    def delete_archives_for_source(self, name: str) -> int:
+        """Drop the source's ``archives`` records (not the stored bytes); returns how many."""
+        return self.store.delete_many("archives", {"source": name})
 
     def ingest_all_enabled_sources(self) -> dict[str, list[str]]:
         return {s["name"]: self.ingest_archive(s) for s in self.list_sources(enabled_only=True)}
@@ -201,6 +209,15 @@ class IngestionService(BaseService):
         d = self.storage_path / "uploads"
         d.mkdir(parents=True, exist_ok=True)
         p = d / name
+        if p.exists():   # never overwrite an earlier upload: name_1.mbox, name_2.tar.gz, ...
+            low = name.lower()
+            ext = next((e for e in (".tar.gz", ".tgz", ".tar", ".zip", ".mbox") if low.endswith(e)), p.suffix)
+            stem = name[:len(name) - len(ext)]
+            n = 1
+            while (d / f"{stem}_{n}{ext}").exists():
+                n += 1
+            name = f"{stem}_{n}{ext}"
+            p = d / name
         p.write_bytes(content)
         return {"filename": name, "server_path": str(p), "size_bytes": len(content),
                 "uploaded_at": datetime.now(timezone.utc).isoformat(), "suggested_source_type": "local",
@@ -249,6 +266,11 @@ def ingestion_routes(app, service: IngestionService, auth=None):
 
     @app.post("/api/sources", status_code=201, dependencies=deps)
     def create_source(body: dict):
+        # required fields missing -> 422 like the reference's pydantic request model
+        missing = [k for k in ("name", "source_type", "url") if not body.get(k)]
+        if missing:
+            raise HTTPException(422, [{"loc": ["body", k], "msg": "Field required", "type": "missing"}
+                                      for k in missing])
         try:
             return {"source": service.create_source(body)}
         except (ValueError, TypeError) as e:

@@ -310,6 +310,7 @@ class InMemoryDocumentStore(DocumentStore):
     def clear_collection(self, collection: str) -> None:
         with self._lock:
             self.collections[collection].clear()
+            self._seq = {k: v for k, v in self._seq.items() if k[0] != collection}
             for k in [k for k in self._idx if k[0] == collection]:
                 del self._idx[k]
             for k in [k for k in self._overflow if k[0] == collection]:
@@ -318,6 +319,7 @@ class InMemoryDocumentStore(DocumentStore):
     def clear_all(self) -> None:
         with self._lock:
             self.collections.clear()
+            self._seq.clear()
             self._idx.clear()
             self._overflow.clear()
 

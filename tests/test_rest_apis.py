@@ -204,3 +204,24 @@ def test_auth_token_exchange_and_jwks(auth_client):
     assert c.get("/userinfo", headers={"Authorization": f"Bearer {tok}"}).json()["roles"] == ["processor"]
     assert c.get("/keys").json() == {"keys": []}          # HMAC signer publishes nothing
     assert c.get("/.well-known/public_key.pem").status_code == 404
+
+
+def test_ingestion_api_reference_semantics(stack):
+    """Reference ingestion/tests/test_api.py behaviours: duplicate source 400 'already exists',
+    missing fields 422, uploads never overwrite each other, path parts stripped from names,
+    compound extensions accepted, re-trigger re-ingests."""
+    node, ing, _, tmp = stack
+    assert ing.post("/api/sources", json={"name": "x"}).status_code == 422
+    body = {"name": "dup", "source_type": "local", "url": str(tmp)}
+    assert ing.post("/api/sources", json=body).status_code == 201
+    r = ing.post("/api/sources", json=body)
+    assert r.status_code == 400 and "already exists" in r.json()["detail"]
+    data = open(FIX, "rb").read()
+    u1 = ing.post("/api/uploads", params={"filename": "test.mbox"}, content=data).json()
+    u2 = ing.post("/api/uploads", params={"filename": "test.mbox"}, content=data).json()
+    assert u1["filename"] == "test.mbox" and u2["filename"] == "test_1.mbox"
+    u3 = ing.post("/api/uploads", params={"filename": "../../etc/a.tar.gz"}, content=_tgz(data)).json()
+    assert ".." not in u3["filename"] and "/" not in u3["filename"] and u3["filename"].endswith(".tar.gz")
+    assert ing.post("/api/uploads", params={"filename": "x.exe"}, content=b"MZ").status_code == 400
+    assert ing.post("/api/uploads", params={"filename": "e.mbox"}, content=b"").status_code == 400
+    assert ing.post("/api/sources/nope/trigger").status_code == 404
