@@ -6,6 +6,7 @@ infrastructure a one-process-per-service deployment needs.
     python -m copilot_for_consensus_amd.services.main broker       # native message broker (RabbitMQ role)
     python -m copilot_for_consensus_amd.services.main docstore     # document store server (MongoDB role)
     python -m copilot_for_consensus_amd.services.main vectorstore  # HIP kNN behind Qdrant's REST API
+    python -m copilot_for_consensus_amd.services.main llm          # HIP decoder behind llama.cpp / Ollama / OpenAI APIs
 
 Reference entry points: <service>/main.py (e.g. ingestion/main.py:179, parsing/main.py:101-124).
 """
@@ -29,13 +30,14 @@ def _auth_dep(cfg):
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("service", choices=["node", "ingestion", "parsing", "chunking", "embedding", "orchestrator",
-                                        "summarization", "reporting", "auth", "broker", "docstore", "vectorstore"])
+                                        "summarization", "reporting", "auth", "broker", "docstore", "vectorstore",
+                                        "llm"])
     ap.add_argument("--port", type=int, default=None)
     ap.add_argument("--host", default=None)
     ap.add_argument("--data-dir", default=None, help="broker journal / docstore WAL / vector index directory")
     args = ap.parse_args(argv)
 
-    if args.service in ("broker", "docstore", "vectorstore"):
+    if args.service in ("broker", "docstore", "vectorstore", "llm"):
         return _infra(args)
 
     if args.service == "auth":
@@ -138,8 +140,15 @@ def _infra(args) -> int:
         return 0
     import uvicorn
 
-    from ..vectorstore.server import create_vector_app
     from ..config.loader import load_adapter_config
+    if args.service == "llm":
+        from ..serving import build_from_config
+        llm = load_adapter_config("llm_backend", driver="hip").driver_config     # LLM_* of the hip driver
+        app, _ = build_from_config(llm)
+        port = args.port or load_adapter_config("llm_backend", driver="llamacpp").driver_config.get("port") or 8081
+        uvicorn.run(app, host=host, port=int(port), log_level="warning")
+        return 0
+    from ..vectorstore.server import create_vector_app
     hip = load_adapter_config("vector_store", driver="hip").driver_config     # VECTOR_STORE_* of the hip driver
     port = args.port or load_adapter_config("vector_store", driver="qdrant").driver_config["port"]   # QDRANT_PORT
     app = create_vector_app(device=hip["device"], capacity=hip["capacity"], index_type=hip["index_type"],

@@ -1,0 +1,372 @@
+"""LLM inference server: the HIP decoder behind the HTTP APIs of the engines the reference calls.
+
+The reference's summarizers reach an LLM over HTTP: Ollama ``POST /api/generate``
+(local_llm_summarizer.py:107, ``stream: false``), the llama.cpp server ``POST /completion``
+(llamacpp_summarizer.py:108-113: ``n_predict`` 512, ``temperature`` 0.7, stops ``</s>`` /
+``\\n\\n\\n``) and OpenAI chat completions (openai_summarizer.py:313-317).  Its compose file runs
+those servers as containers (docker-compose.infra.yml: ``ollama``, ``llama-cpp``).  This module is
+the MI355X replacement for those containers: the same routes and JSON, served by this framework's
+engine (paged KV, GQA flash prefill, hipGraph decode, on-device sampling; GGUF or safetensors
+weights), so ``LLM_BACKEND_TYPE=local`` / ``llamacpp`` / ``openai`` deployments -- the reference's
+own drivers included -- run on the GPU without code changes.
+
+Concurrent requests are micro-batched: a scheduler thread collects requests for up to
+``batch_wait_ms``, groups those with the same sampling parameters and runs each group as one
+batched ``LLMEngine.generate`` (per-request token limits, stop strings and EOS applied per row).
+
+Routes:
+  llama.cpp  POST /completion, POST /tokenize, POST /detokenize, GET /health, GET /props
+  Ollama     POST /api/generate, POST /api/chat, GET /api/tags, GET /api/version
+  OpenAI     POST /v1/completions, POST /v1/chat/completions, GET /v1/models
+``stream: true`` is answered in each API's streaming framing (NDJSON / SSE) with the completion as
+one chunk followed by the final record.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import queue
+import threading
+import time
+import uuid
+from typing import Any
+
+from fastapi import Body, FastAPI, HTTPException
+from fastapi.responses import JSONResponse, StreamingResponse
+
+
+@dataclasses.dataclass
+class GenRequest:
+    prompt_ids: list[int]
+    max_new: int
+    temperature: float = 0.0
+    top_k: int = 0
+    top_p: float = 1.0
+    min_p: float = 0.0
+    seed: int = 0
+    stop: tuple[str, ...] = ()
+    ignore_eos: bool = False
+    submitted: float = dataclasses.field(default_factory=time.perf_counter)
+    done: threading.Event = dataclasses.field(default_factory=threading.Event)
+    text: str = ""
+    tokens: list[int] = dataclasses.field(default_factory=list)
+    finish: str = "stop"                 # stop | length
+    stopping_word: str = ""
+    prompt_s: float = 0.0
+    gen_s: float = 0.0
+    error: str | None = None
+
+    def key(self):
+        sampled = self.temperature > 0
+        return (round(self.temperature, 6), self.top_k if sampled else 0, round(self.top_p, 6) if sampled else 1.0,
+                round(self.min_p, 6) if sampled else 0.0, self.seed if sampled else 0, self.ignore_eos)
+
+
+class BatchScheduler:
+    """Collects requests and runs same-sampling groups as batched generations on the engine."""
+
+    def __init__(self, engine, tokenizer, max_batch: int = 64, batch_wait_ms: float = 5.0):
+        self.engine, self.tok = engine, tokenizer
+        self.max_batch, self.wait_s = int(max_batch), batch_wait_ms / 1000.0
+        self.q: queue.Queue[GenRequest] = queue.Queue()
+        self._stop = threading.Event()
+        self.batches = 0
+        self.served = 0
+        self.max_seen_batch = 0
+        self._t = threading.Thread(target=self._loop, name="llm-scheduler", daemon=True)
+        self._t.start()
+
+    def submit(self, r: GenRequest, timeout: float = 600.0) -> GenRequest:
+        self.q.put(r)
+        if not r.done.wait(timeout):
+            raise TimeoutError("generation timed out")
+        if r.error:
+            raise RuntimeError(r.error)
+        return r
+
+    def close(self) -> None:
+        self._stop.set()
+        self._t.join(5)
+
+    def _loop(self) -> None:
+        while not self._stop.is_set():
+            try:
+                first = self.q.get(timeout=0.1)
+            except queue.Empty:
+                continue
+            batch = [first]
+            deadline = time.perf_counter() + self.wait_s
+            while len(batch) < self.max_batch:
+                left = deadline - time.perf_counter()
+                try:
+                    batch.append(self.q.get(timeout=max(0.0, left)) if left > 0 else self.q.get_nowait())
+                except queue.Empty:
+                    break
+            groups: dict[tuple, list[GenRequest]] = {}
+            for r in batch:
+                groups.setdefault(r.key(), []).append(r)
+            for g in groups.values():
+                self._run(g)
+
+    def _run(self, group: list[GenRequest]) -> None:
+        r0 = group[0]
+        limit = self.engine.cfg.max_positions
+        if len(group) > 1 and max(len(r.prompt_ids) for r in group) + max(r.max_new for r in group) > limit:
+            for r in group:               # each fits alone; together the longest prompt + largest budget do not
+                self._run([r])
+            return
+        try:
+            t0 = time.perf_counter()
+            res = self.engine.generate([r.prompt_ids for r in group], max(r.max_new for r in group),
+                                       temperature=r0.temperature, seed=r0.seed, ignore_eos=r0.ignore_eos,
+                                       top_k=r0.top_k, top_p=r0.top_p, min_p=r0.min_p)
+            dt = time.perf_counter() - t0
+            self.batches += 1
+            self.max_seen_batch = max(self.max_seen_batch, len(group))
+            for r, toks in zip(group, res.tokens):
+                hit_limit = len(toks) >= r.max_new
+                toks = toks[:r.max_new]
+                text = self.tok.decode(toks)
+                cut, word = -1, ""
+                for s in r.stop:
+                    i = text.find(s)
+                    if i >= 0 and (cut < 0 or i < cut):
+                        cut, word = i, s
+                if cut >= 0:
+                    text, r.stopping_word, r.finish = text[:cut], word, "stop"
+                else:
+                    r.finish = "length" if hit_limit else "stop"
+                r.text, r.tokens = text, toks
+                r.prompt_s, r.gen_s = res.prefill_s, max(dt - res.prefill_s, 0.0)
+                self.served += 1
+        except Exception as e:  # noqa: BLE001 -- every waiter must be released with the failure
+            for r in group:
+                r.error = f"{type(e).__name__}: {e}"
+        finally:
+            for r in group:
+                r.done.set()
+
+
+def chat_prompt(messages: list[dict], family: str) -> str:
+    """Instruction templates of the model families this framework serves."""
+    msgs = [m for m in messages if isinstance(m, dict)]
+    if family == "llama3":
+        out = []
+        for m in msgs:
+            out.append(f"<|start_header_id|>{m.get('role', 'user')}<|end_header_id|>\n\n{m.get('content', '')}<|eot_id|>")
+        return "".join(out) + "<|start_header_id|>assistant<|end_header_id|>\n\n"
+    # Mistral / Llama-2 [INST] format; a system message is folded into the first user turn
+    system = "\n\n".join(m.get("content", "") for m in msgs if m.get("role") == "system")
+    out, pending_sys = [], system
+    for m in msgs:
+        role, content = m.get("role"), m.get("content", "")
+        if role == "user":
+            if pending_sys:
+                content, pending_sys = f"{pending_sys}\n\n{content}", ""
+            out.append(f"[INST] {content} [/INST]")
+        elif role == "assistant":
+            out.append(f" {content}</s>")
+    return "".join(out)
+
+
+def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, family: str = "mistral",
+                   max_batch: int = 64, batch_wait_ms: float = 5.0, default_n_predict: int = 512) -> FastAPI:
+    sched = BatchScheduler(engine, tokenizer, max_batch=max_batch, batch_wait_ms=batch_wait_ms)
+    app = FastAPI(title=f"copilot-for-consensus HIP LLM server ({model_name})")
+    app.state.scheduler = sched
+    started = time.time()
+
+    def encode(prompt) -> list[int]:
+        if isinstance(prompt, list) and all(isinstance(x, int) for x in prompt):
+            ids = list(prompt)
+        elif isinstance(prompt, str):
+            ids = tokenizer.encode(prompt)
+        else:
+            raise HTTPException(400, "prompt must be a string or a list of token ids")
+        if not ids:
+            raise HTTPException(400, "empty prompt")
+        return ids
+
+    def run(prompt, n_predict, temperature, top_k, top_p, min_p, seed, stop, ignore_eos=False) -> GenRequest:
+        ids = encode(prompt)
+        room = context_limit - len(ids)
+        if room <= 0:
+            raise HTTPException(400, f"prompt of {len(ids)} tokens exceeds the context ({context_limit})")
+        n = room if n_predict is None or int(n_predict) < 0 else min(int(n_predict), room)
+        if n == 0:
+            raise HTTPException(400, "n_predict must be positive")
+        if isinstance(stop, str):
+            stop = [stop]
+        r = GenRequest(ids, n, float(temperature or 0.0), int(top_k or 0), float(1.0 if top_p is None else top_p),
+                       float(min_p or 0.0), int(seed or 0), tuple(s for s in (stop or []) if s), bool(ignore_eos))
+        try:
+            return sched.submit(r)
+        except RuntimeError as e:
+            raise HTTPException(500, str(e))
+
+    # ------------------------------------------------------------------ llama.cpp server
+    @app.get("/health")
+    def health():
+        return {"status": "ok", "slots_idle": 1, "slots_processing": 0}
+
+    @app.get("/props")
+    def props():
+        return {"default_generation_settings": {"n_ctx": context_limit, "model": model_name,
+                                                "n_predict": default_n_predict},
+                "total_slots": max_batch}
+
+    @app.post("/tokenize")
+    def tokenize(body: dict = Body(...)):
+        return {"tokens": tokenizer.encode(body.get("content", ""), add_bos=bool(body.get("add_special", False)))}
+
+    @app.post("/detokenize")
+    def detokenize(body: dict = Body(...)):
+        return {"content": tokenizer.decode(list(body.get("tokens") or []))}
+
+    @app.post("/completion")
+    def completion(body: dict = Body(...)):
+        # llama.cpp defaults: temperature 0.8, top_k 40, top_p 0.95, min_p 0.05
+        r = run(body.get("prompt"), body.get("n_predict", default_n_predict), body.get("temperature", 0.8),
+                body.get("top_k", 40), body.get("top_p", 0.95), body.get("min_p", 0.05), body.get("seed"),
+                body.get("stop"), body.get("ignore_eos", False))
+        out = {"content": r.text, "model": model_name, "stop": True, "tokens_predicted": len(r.tokens),
+               "tokens_evaluated": len(r.prompt_ids), "stopped_eos": r.finish == "stop" and not r.stopping_word,
+               "stopped_word": bool(r.stopping_word), "stopped_limit": r.finish == "length",
+               "stopping_word": r.stopping_word, "truncated": False,
+               "timings": {"prompt_n": len(r.prompt_ids), "prompt_ms": 1000 * r.prompt_s,
+                           "predicted_n": len(r.tokens), "predicted_ms": 1000 * r.gen_s,
+                           "predicted_per_second": len(r.tokens) / r.gen_s if r.gen_s > 0 else 0.0}}
+        if body.get("stream"):
+            def sse():
+                yield "data: " + json.dumps({"content": r.text, "stop": False}) + "\n\n"
+                yield "data: " + json.dumps({**out, "content": ""}) + "\n\n"
+            return StreamingResponse(sse(), media_type="text/event-stream")
+        return out
+
+    # ------------------------------------------------------------------ Ollama
+    def ollama_opts(body):
+        o = dict(body.get("options") or {})
+        return (o.get("num_predict", default_n_predict), o.get("temperature", 0.8), o.get("top_k", 40),
+                o.get("top_p", 0.9), o.get("min_p", 0.0), o.get("seed"), o.get("stop"))
+
+    def ollama_record(r: GenRequest, extra: dict) -> dict:
+        return {"model": model_name, "created_at": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()), **extra,
+                "done": True, "done_reason": r.finish, "total_duration": int(1e9 * (r.prompt_s + r.gen_s)),
+                "load_duration": 0, "prompt_eval_count": len(r.prompt_ids),
+                "prompt_eval_duration": int(1e9 * r.prompt_s), "eval_count": len(r.tokens),
+                "eval_duration": int(1e9 * r.gen_s)}
+
+    def ndjson(first: dict, last: dict):
+        def gen():
+            yield json.dumps(first) + "\n"
+            yield json.dumps(last) + "\n"
+        return StreamingResponse(gen(), media_type="application/x-ndjson")
+
+    @app.post("/api/generate")
+    def ollama_generate(body: dict = Body(...)):
+        prompt = body.get("prompt", "")
+        if body.get("system") and not body.get("raw"):
+            prompt = chat_prompt([{"role": "system", "content": body["system"]}, {"role": "user", "content": prompt}],
+                                 family)
+        n, temp, k, p, mp, seed, stop = ollama_opts(body)
+        r = run(prompt, n, temp, k, p, mp, seed, stop)
+        rec = ollama_record(r, {"response": r.text, "context": []})
+        if body.get("stream", True):                 # Ollama streams unless told not to
+            return ndjson({"model": model_name, "created_at": rec["created_at"], "response": r.text, "done": False},
+                          {**rec, "response": ""})
+        return rec
+
+    @app.post("/api/chat")
+    def ollama_chat(body: dict = Body(...)):
+        n, temp, k, p, mp, seed, stop = ollama_opts(body)
+        r = run(chat_prompt(body.get("messages") or [], family), n, temp, k, p, mp, seed, stop)
+        msg = {"role": "assistant", "content": r.text}
+        rec = ollama_record(r, {"message": msg})
+        if body.get("stream", True):
+            return ndjson({"model": model_name, "created_at": rec["created_at"], "message": msg, "done": False},
+                          {**rec, "message": {"role": "assistant", "content": ""}})
+        return rec
+
+    @app.get("/api/tags")
+    def ollama_tags():
+        return {"models": [{"name": model_name, "model": model_name, "modified_at": "", "size": 0,
+                            "details": {"family": family, "format": "hip"}}]}
+
+    @app.get("/api/version")
+    def ollama_version():
+        return {"version": "0.0.0-cfc-hip"}
+
+    # ------------------------------------------------------------------ OpenAI
+    def oai_usage(r: GenRequest) -> dict:
+        return {"prompt_tokens": len(r.prompt_ids), "completion_tokens": len(r.tokens),
+                "total_tokens": len(r.prompt_ids) + len(r.tokens)}
+
+    def sse(chunks: list[dict]):
+        def gen():
+            for c in chunks:
+                yield "data: " + json.dumps(c) + "\n\n"
+            yield "data: [DONE]\n\n"
+        return StreamingResponse(gen(), media_type="text/event-stream")
+
+    @app.post("/v1/completions")
+    def oai_completions(body: dict = Body(...)):
+        if int(body.get("n", 1)) != 1:
+            raise HTTPException(400, "only n=1 is supported")
+        prompt = body.get("prompt", "")
+        if isinstance(prompt, list) and prompt and isinstance(prompt[0], str):
+            if len(prompt) != 1:
+                raise HTTPException(400, "one prompt per request")
+            prompt = prompt[0]
+        r = run(prompt, body.get("max_tokens", 16), body.get("temperature", 1.0), 0, body.get("top_p", 1.0), 0.0,
+                body.get("seed"), body.get("stop"))
+        cid, created = f"cmpl-{uuid.uuid4().hex[:24]}", int(time.time())
+        choice = {"text": r.text, "index": 0, "logprobs": None, "finish_reason": r.finish}
+        if body.get("stream"):
+            return sse([{"id": cid, "object": "text_completion", "created": created, "model": model_name,
+                         "choices": [choice]}])
+        return {"id": cid, "object": "text_completion", "created": created, "model": model_name,
+                "choices": [choice], "usage": oai_usage(r)}
+
+    @app.post("/v1/chat/completions")
+    def oai_chat(body: dict = Body(...)):
+        if int(body.get("n", 1)) != 1:
+            raise HTTPException(400, "only n=1 is supported")
+        msgs = body.get("messages")
+        if not isinstance(msgs, list) or not msgs:
+            raise HTTPException(400, "messages must be a non-empty list")
+        r = run(chat_prompt(msgs, family), body.get("max_tokens", body.get("max_completion_tokens")),
+                body.get("temperature", 1.0), 0, body.get("top_p", 1.0), 0.0, body.get("seed"), body.get("stop"))
+        cid, created = f"chatcmpl-{uuid.uuid4().hex[:24]}", int(time.time())
+        if body.get("stream"):
+            return sse([{"id": cid, "object": "chat.completion.chunk", "created": created, "model": model_name,
+                         "choices": [{"index": 0, "delta": {"role": "assistant", "content": r.text},
+                                      "finish_reason": None}]},
+                        {"id": cid, "object": "chat.completion.chunk", "created": created, "model": model_name,
+                         "choices": [{"index": 0, "delta": {}, "finish_reason": r.finish}]}])
+        return {"id": cid, "object": "chat.completion", "created": created, "model": model_name,
+                "choices": [{"index": 0, "message": {"role": "assistant", "content": r.text},
+                             "finish_reason": r.finish}], "usage": oai_usage(r)}
+
+    @app.get("/v1/models")
+    def oai_models():
+        return {"object": "list", "data": [{"id": model_name, "object": "model", "created": int(started),
+                                            "owned_by": "copilot-for-consensus-amd"}]}
+
+    @app.get("/metrics")
+    def metrics():
+        return JSONResponse({"requests_served": sched.served, "batches": sched.batches,
+                             "max_batch_seen": sched.max_seen_batch, "queue_depth": sched.q.qsize()})
+
+    return app
+
+
+def build_from_config(cfg: dict[str, Any]):
+    """(app, summarizer) from the ``llm_backend`` hip driver settings (LLM_MODEL_PRESET / LLM_GGUF_PATH /
+    LLM_CHECKPOINT_DIR / LLM_KV_CACHE_TOKENS / LLM_MAX_BATCH ...)."""
+    from ..summarization import HipLLMSummarizer
+    s = HipLLMSummarizer(**{k: v for k, v in cfg.items() if v is not None})
+    name = s.cfg.name
+    family = "llama3" if "llama-3" in name or "llama3" in name or s.cfg.vocab_size > 100000 else "mistral"
+    app = create_llm_app(s.engine, s.tokenizer, name, s.cfg.max_positions, family=family,
+                         max_batch=s.max_batch, default_n_predict=s.max_new_tokens)
+    return app, s
