@@ -10,9 +10,11 @@ engine (paged KV, GQA flash prefill, hipGraph decode, on-device sampling; GGUF o
 weights), so ``LLM_BACKEND_TYPE=local`` / ``llamacpp`` / ``openai`` deployments -- the reference's
 own drivers included -- run on the GPU without code changes.
 
-Concurrent requests are micro-batched: a scheduler thread collects requests for up to
-``batch_wait_ms``, groups those with the same sampling parameters and runs each group as one
-batched ``LLMEngine.generate`` (per-request token limits, stop strings and EOS applied per row).
+Concurrent requests share the GPU through continuous batching: each distinct sampling
+configuration gets a slot-based engine (runtime/continuous.py) whose hipGraph-captured decode step
+runs over every in-flight request, and new requests are admitted between bursts; per-request token
+limits, EOS and stop strings are applied per row.  Requests beyond the slot engine's caps fall back
+to grouped batched ``LLMEngine.generate`` calls.
 
 Routes:
   llama.cpp  POST /completion, POST /tokenize, POST /detokenize, GET /health, GET /props
@@ -55,6 +57,13 @@ class GenRequest:
     prompt_s: float = 0.0
     gen_s: float = 0.0
     error: str | None = None
+    loop: Any = None                     # asyncio loop + event of an async waiter (the HTTP handlers)
+    aevent: Any = None
+
+    def complete(self) -> None:
+        self.done.set()
+        if self.aevent is not None:
+            self.loop.call_soon_threadsafe(self.aevent.set)
 
     def key(self):
         sampled = self.temperature > 0
@@ -63,16 +72,25 @@ class GenRequest:
 
 
 class BatchScheduler:
-    """Collects requests and runs same-sampling groups as batched generations on the engine."""
+    """Runs requests on the engine: continuous batching (runtime/continuous.py: one hipGraph-captured
+    decode step over a fixed set of slots, requests admitted between bursts) for each distinct
+    sampling configuration, up to ``max_engines`` of them; requests beyond a continuous engine's
+    prompt / token caps, or past that many configurations, run as grouped batched ``generate``
+    calls (micro-batching)."""
 
-    def __init__(self, engine, tokenizer, max_batch: int = 64, batch_wait_ms: float = 5.0):
+    def __init__(self, engine, tokenizer, max_batch: int = 64, batch_wait_ms: float = 5.0, continuous: bool = True,
+                 max_engines: int = 4, max_prompt: int = 4096, max_new_cap: int = 512, steps_per_sync: int = 8):
         self.engine, self.tok = engine, tokenizer
         self.max_batch, self.wait_s = int(max_batch), batch_wait_ms / 1000.0
+        self.continuous, self.max_engines = continuous, int(max_engines)
+        self.max_prompt, self.cap, self.steps_per_sync = int(max_prompt), int(max_new_cap), int(steps_per_sync)
         self.q: queue.Queue[GenRequest] = queue.Queue()
         self._stop = threading.Event()
         self.batches = 0
         self.served = 0
         self.max_seen_batch = 0
+        self.engines: dict[tuple, Any] = {}        # sampling key -> ContinuousEngine
+        self._inflight: dict[tuple, dict[int, GenRequest]] = {}
         self._t = threading.Thread(target=self._loop, name="llm-scheduler", daemon=True)
         self._t.start()
 
@@ -84,29 +102,111 @@ class BatchScheduler:
             raise RuntimeError(r.error)
         return r
 
+    async def asubmit(self, r: GenRequest, timeout: float = 600.0) -> GenRequest:
+        """Non-blocking wait for the HTTP handlers: no worker thread is held per in-flight request."""
+        import asyncio
+        r.loop, r.aevent = asyncio.get_running_loop(), asyncio.Event()
+        self.q.put(r)
+        await asyncio.wait_for(r.aevent.wait(), timeout)
+        if r.error:
+            raise RuntimeError(r.error)
+        return r
+
     def close(self) -> None:
         self._stop.set()
         self._t.join(5)
 
+    # ------------------------------------------------------------------ scheduling
+    def _continuous_for(self, r: GenRequest):
+        if not self.continuous or len(r.prompt_ids) > self.max_prompt or r.max_new > self.cap:
+            return None
+        key = r.key()
+        ce = self.engines.get(key)
+        if ce is None:
+            if len(self.engines) >= self.max_engines:
+                return None
+            from ..ops import kernels as K
+            from ..runtime.continuous import ContinuousEngine
+            stops = () if r.ignore_eos else (self.engine.cfg.eos_id,)
+            ce = ContinuousEngine(self.engine, max_slots=self.max_batch, max_new_cap=self.cap,
+                                  max_prompt=self.max_prompt, steps_per_sync=self.steps_per_sync, stop_ids=stops,
+                                  seed=r.seed, max_wait_s=self.wait_s)
+            ce.sampling = K.SamplingParams(r.temperature, r.top_k, r.top_p, r.min_p) if r.temperature > 0 \
+                else K.SamplingParams.of(0.0)
+            self.engines[key] = ce
+            self._inflight[key] = {}
+        return ce
+
     def _loop(self) -> None:
         while not self._stop.is_set():
+            busy = any(ce.pending() for ce in self.engines.values())
+            batch: list[GenRequest] = []
             try:
-                first = self.q.get(timeout=0.1)
+                batch.append(self.q.get(timeout=0.0 if busy else 0.1) if busy else self.q.get(timeout=0.1))
             except queue.Empty:
-                continue
-            batch = [first]
-            deadline = time.perf_counter() + self.wait_s
-            while len(batch) < self.max_batch:
-                left = deadline - time.perf_counter()
+                pass
+            if batch and not busy:       # an idle engine waits a moment so a burst of arrivals shares a prefill
+                deadline = time.perf_counter() + self.wait_s
+                while len(batch) < self.max_batch:
+                    left = deadline - time.perf_counter()
+                    try:
+                        batch.append(self.q.get(timeout=left) if left > 0 else self.q.get_nowait())
+                    except queue.Empty:
+                        break
+            while True:                  # everything else already queued
                 try:
-                    batch.append(self.q.get(timeout=max(0.0, left)) if left > 0 else self.q.get_nowait())
+                    batch.append(self.q.get_nowait())
                 except queue.Empty:
                     break
-            groups: dict[tuple, list[GenRequest]] = {}
+            legacy: dict[tuple, list[GenRequest]] = {}
             for r in batch:
-                groups.setdefault(r.key(), []).append(r)
-            for g in groups.values():
-                self._run(g)
+                ce = self._continuous_for(r)
+                if ce is None:
+                    legacy.setdefault(r.key(), []).append(r)
+                else:
+                    cr = ce.submit(r.prompt_ids, r.max_new)
+                    self._inflight[r.key()][cr.rid] = r
+            for g in legacy.values():
+                for s in range(0, len(g), self.max_batch):
+                    self._run(g[s:s + self.max_batch])
+            for key, ce in list(self.engines.items()):
+                if not ce.pending():
+                    continue
+                try:
+                    active = sum(x is not None for x in ce.slot_req)
+                    finished = ce.step()
+                    self.max_seen_batch = max(self.max_seen_batch, active,
+                                              sum(x is not None for x in ce.slot_req))
+                except Exception as e:  # noqa: BLE001 -- fail every request of this engine, drop it
+                    for r in self._inflight.pop(key, {}).values():
+                        r.error = f"{type(e).__name__}: {e}"
+                        r.complete()
+                    self.engines.pop(key, None)
+                    continue
+                if finished:
+                    self.batches += 1
+                for cr in finished:
+                    r = self._inflight[key].pop(cr.rid)
+                    self._finish(r, cr.tokens, cr.tokens is not None and len(cr.tokens) >= r.max_new,
+                                 (cr.first_token_s or cr.submitted_s) - cr.submitted_s,
+                                 cr.finished_s - (cr.first_token_s or cr.submitted_s))
+                    r.complete()
+
+    def _finish(self, r: GenRequest, toks: list[int], hit_limit: bool, prompt_s: float, gen_s: float) -> None:
+        toks = list(toks[:r.max_new])
+        text = self.tok.decode(toks)
+        cut, word = -1, ""
+        for s in r.stop:
+            i = text.find(s)
+            if i >= 0 and (cut < 0 or i < cut):
+                cut, word = i, s
+        if cut >= 0:
+            text, r.stopping_word, r.finish = text[:cut], word, "stop"
+        else:
+            r.finish = "length" if hit_limit else "stop"
+        r.text, r.tokens = text, toks
+        r.prompt_s, r.gen_s = prompt_s, gen_s
+        self.served += 1
 
     def _run(self, group: list[GenRequest]) -> None:
         r0 = group[0]
@@ -124,27 +224,13 @@ class BatchScheduler:
             self.batches += 1
             self.max_seen_batch = max(self.max_seen_batch, len(group))
             for r, toks in zip(group, res.tokens):
-                hit_limit = len(toks) >= r.max_new
-                toks = toks[:r.max_new]
-                text = self.tok.decode(toks)
-                cut, word = -1, ""
-                for s in r.stop:
-                    i = text.find(s)
-                    if i >= 0 and (cut < 0 or i < cut):
-                        cut, word = i, s
-                if cut >= 0:
-                    text, r.stopping_word, r.finish = text[:cut], word, "stop"
-                else:
-                    r.finish = "length" if hit_limit else "stop"
-                r.text, r.tokens = text, toks
-                r.prompt_s, r.gen_s = res.prefill_s, max(dt - res.prefill_s, 0.0)
-                self.served += 1
+                self._finish(r, toks, len(toks) >= r.max_new, res.prefill_s, max(dt - res.prefill_s, 0.0))
         except Exception as e:  # noqa: BLE001 -- every waiter must be released with the failure
             for r in group:
                 r.error = f"{type(e).__name__}: {e}"
         finally:
             for r in group:
-                r.done.set()
+                r.complete()
 
 
 def chat_prompt(messages: list[dict], family: str) -> str:
@@ -170,8 +256,11 @@ def chat_prompt(messages: list[dict], family: str) -> str:
 
 
 def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, family: str = "mistral",
-                   max_batch: int = 64, batch_wait_ms: float = 5.0, default_n_predict: int = 512) -> FastAPI:
-    sched = BatchScheduler(engine, tokenizer, max_batch=max_batch, batch_wait_ms=batch_wait_ms)
+                   max_batch: int = 64, batch_wait_ms: float = 5.0, default_n_predict: int = 512,
+                   continuous: bool = True, max_prompt: int = 4096, max_new_cap: int = 512) -> FastAPI:
+    sched = BatchScheduler(engine, tokenizer, max_batch=max_batch, batch_wait_ms=batch_wait_ms, continuous=continuous,
+                           max_prompt=min(max_prompt, context_limit - 1),
+                           max_new_cap=max(1, min(max_new_cap, context_limit - 1)))
     app = FastAPI(title=f"copilot-for-consensus HIP LLM server ({model_name})")
     app.state.scheduler = sched
     started = time.time()
@@ -187,7 +276,7 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
             raise HTTPException(400, "empty prompt")
         return ids
 
-    def run(prompt, n_predict, temperature, top_k, top_p, min_p, seed, stop, ignore_eos=False) -> GenRequest:
+    async def run(prompt, n_predict, temperature, top_k, top_p, min_p, seed, stop, ignore_eos=False) -> GenRequest:
         ids = encode(prompt)
         room = context_limit - len(ids)
         if room <= 0:
@@ -200,7 +289,7 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
         r = GenRequest(ids, n, float(temperature or 0.0), int(top_k or 0), float(1.0 if top_p is None else top_p),
                        float(min_p or 0.0), int(seed or 0), tuple(s for s in (stop or []) if s), bool(ignore_eos))
         try:
-            return sched.submit(r)
+            return await sched.asubmit(r)
         except RuntimeError as e:
             raise HTTPException(500, str(e))
 
@@ -224,9 +313,9 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
         return {"content": tokenizer.decode(list(body.get("tokens") or []))}
 
     @app.post("/completion")
-    def completion(body: dict = Body(...)):
+    async def completion(body: dict = Body(...)):
         # llama.cpp defaults: temperature 0.8, top_k 40, top_p 0.95, min_p 0.05
-        r = run(body.get("prompt"), body.get("n_predict", default_n_predict), body.get("temperature", 0.8),
+        r = await run(body.get("prompt"), body.get("n_predict", default_n_predict), body.get("temperature", 0.8),
                 body.get("top_k", 40), body.get("top_p", 0.95), body.get("min_p", 0.05), body.get("seed"),
                 body.get("stop"), body.get("ignore_eos", False))
         out = {"content": r.text, "model": model_name, "stop": True, "tokens_predicted": len(r.tokens),
@@ -263,13 +352,13 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
         return StreamingResponse(gen(), media_type="application/x-ndjson")
 
     @app.post("/api/generate")
-    def ollama_generate(body: dict = Body(...)):
+    async def ollama_generate(body: dict = Body(...)):
         prompt = body.get("prompt", "")
         if body.get("system") and not body.get("raw"):
             prompt = chat_prompt([{"role": "system", "content": body["system"]}, {"role": "user", "content": prompt}],
                                  family)
         n, temp, k, p, mp, seed, stop = ollama_opts(body)
-        r = run(prompt, n, temp, k, p, mp, seed, stop)
+        r = await run(prompt, n, temp, k, p, mp, seed, stop)
         rec = ollama_record(r, {"response": r.text, "context": []})
         if body.get("stream", True):                 # Ollama streams unless told not to
             return ndjson({"model": model_name, "created_at": rec["created_at"], "response": r.text, "done": False},
@@ -277,9 +366,9 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
         return rec
 
     @app.post("/api/chat")
-    def ollama_chat(body: dict = Body(...)):
+    async def ollama_chat(body: dict = Body(...)):
         n, temp, k, p, mp, seed, stop = ollama_opts(body)
-        r = run(chat_prompt(body.get("messages") or [], family), n, temp, k, p, mp, seed, stop)
+        r = await run(chat_prompt(body.get("messages") or [], family), n, temp, k, p, mp, seed, stop)
         msg = {"role": "assistant", "content": r.text}
         rec = ollama_record(r, {"message": msg})
         if body.get("stream", True):
@@ -309,7 +398,7 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
         return StreamingResponse(gen(), media_type="text/event-stream")
 
     @app.post("/v1/completions")
-    def oai_completions(body: dict = Body(...)):
+    async def oai_completions(body: dict = Body(...)):
         if int(body.get("n", 1)) != 1:
             raise HTTPException(400, "only n=1 is supported")
         prompt = body.get("prompt", "")
@@ -317,7 +406,7 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
             if len(prompt) != 1:
                 raise HTTPException(400, "one prompt per request")
             prompt = prompt[0]
-        r = run(prompt, body.get("max_tokens", 16), body.get("temperature", 1.0), 0, body.get("top_p", 1.0), 0.0,
+        r = await run(prompt, body.get("max_tokens", 16), body.get("temperature", 1.0), 0, body.get("top_p", 1.0), 0.0,
                 body.get("seed"), body.get("stop"))
         cid, created = f"cmpl-{uuid.uuid4().hex[:24]}", int(time.time())
         choice = {"text": r.text, "index": 0, "logprobs": None, "finish_reason": r.finish}
@@ -328,13 +417,13 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
                 "choices": [choice], "usage": oai_usage(r)}
 
     @app.post("/v1/chat/completions")
-    def oai_chat(body: dict = Body(...)):
+    async def oai_chat(body: dict = Body(...)):
         if int(body.get("n", 1)) != 1:
             raise HTTPException(400, "only n=1 is supported")
         msgs = body.get("messages")
         if not isinstance(msgs, list) or not msgs:
             raise HTTPException(400, "messages must be a non-empty list")
-        r = run(chat_prompt(msgs, family), body.get("max_tokens", body.get("max_completion_tokens")),
+        r = await run(chat_prompt(msgs, family), body.get("max_tokens", body.get("max_completion_tokens")),
                 body.get("temperature", 1.0), 0, body.get("top_p", 1.0), 0.0, body.get("seed"), body.get("stop"))
         cid, created = f"chatcmpl-{uuid.uuid4().hex[:24]}", int(time.time())
         if body.get("stream"):
@@ -360,7 +449,7 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
     return app
 
 
-def build_from_config(cfg: dict[str, Any]):
+def build_from_config(cfg: dict[str, Any], **server_kw):
     """(app, summarizer) from the ``llm_backend`` hip driver settings (LLM_MODEL_PRESET / LLM_GGUF_PATH /
     LLM_CHECKPOINT_DIR / LLM_KV_CACHE_TOKENS / LLM_MAX_BATCH ...)."""
     from ..summarization import HipLLMSummarizer
@@ -368,5 +457,5 @@ def build_from_config(cfg: dict[str, Any]):
     name = s.cfg.name
     family = "llama3" if "llama-3" in name or "llama3" in name or s.cfg.vocab_size > 100000 else "mistral"
     app = create_llm_app(s.engine, s.tokenizer, name, s.cfg.max_positions, family=family,
-                         max_batch=s.max_batch, default_n_predict=s.max_new_tokens)
+                         max_batch=s.max_batch, default_n_predict=s.max_new_tokens, **server_kw)
     return app, s

@@ -31,7 +31,7 @@ def _serve(app):
 
 def _stack(device):
     app, s = build_from_config({"model": "tiny", "device": device, "max_new_tokens": 16, "kv_cache_tokens": 1 << 15,
-                                "max_batch": 16})
+                                "max_batch": 16}, max_prompt=256, max_new_cap=64)
     server, t, port = _serve(app)
     return app, s, server, t, f"http://127.0.0.1:{port}"
 
