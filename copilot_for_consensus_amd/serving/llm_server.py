@@ -57,6 +57,7 @@ class GenRequest:
     prompt_s: float = 0.0
     gen_s: float = 0.0
     error: str | None = None
+    truncated: bool = False              # the prompt was cut to fit the context
     loop: Any = None                     # asyncio loop + event of an async waiter (the HTTP handlers)
     aevent: Any = None
 
@@ -278,16 +279,23 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
 
     async def run(prompt, n_predict, temperature, top_k, top_p, min_p, seed, stop, ignore_eos=False) -> GenRequest:
         ids = encode(prompt)
-        room = context_limit - len(ids)
-        if room <= 0:
-            raise HTTPException(400, f"prompt of {len(ids)} tokens exceeds the context ({context_limit})")
-        n = room if n_predict is None or int(n_predict) < 0 else min(int(n_predict), room)
-        if n == 0:
+        want = None if n_predict is None or int(n_predict) < 0 else int(n_predict)
+        if want == 0:
             raise HTTPException(400, "n_predict must be positive")
+        truncated = False
+        budget = context_limit - min(want or 1, context_limit // 2)
+        if len(ids) > budget:
+            # like the llama.cpp / Ollama servers: an over-long prompt is truncated, not refused --
+            # keep the head (instructions) and the newest tail, reserve room for the generation
+            half = budget // 2
+            ids, truncated = ids[:half] + ids[len(ids) - (budget - half):], True
+        room = context_limit - len(ids)
+        n = room if want is None else min(want, room)
         if isinstance(stop, str):
             stop = [stop]
         r = GenRequest(ids, n, float(temperature or 0.0), int(top_k or 0), float(1.0 if top_p is None else top_p),
                        float(min_p or 0.0), int(seed or 0), tuple(s for s in (stop or []) if s), bool(ignore_eos))
+        r.truncated = truncated
         try:
             return await sched.asubmit(r)
         except RuntimeError as e:
@@ -321,7 +329,7 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
         out = {"content": r.text, "model": model_name, "stop": True, "tokens_predicted": len(r.tokens),
                "tokens_evaluated": len(r.prompt_ids), "stopped_eos": r.finish == "stop" and not r.stopping_word,
                "stopped_word": bool(r.stopping_word), "stopped_limit": r.finish == "length",
-               "stopping_word": r.stopping_word, "truncated": False,
+               "stopping_word": r.stopping_word, "truncated": r.truncated,
                "timings": {"prompt_n": len(r.prompt_ids), "prompt_ms": 1000 * r.prompt_s,
                            "predicted_n": len(r.tokens), "predicted_ms": 1000 * r.gen_s,
                            "predicted_per_second": len(r.tokens) / r.gen_s if r.gen_s > 0 else 0.0}}

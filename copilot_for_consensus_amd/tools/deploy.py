@@ -191,6 +191,10 @@ def compose_native() -> str:
            "  vectorstore:", img, "    command: python -m copilot_for_consensus_amd.services.main vectorstore --port 6333 "
            "--data-dir /data/vectors", "    volumes: ['vectors:/data/vectors']"] + gpu + \
           ["    environment:", "      - VECTOR_STORE_DEVICE=cuda", "      - HSA_ENABLE_IPC_MODE_LEGACY=0"]
+    out += ["  llm:", img, "    command: python -m copilot_for_consensus_amd.services.main llm --port 8081",
+            "    profiles: ['llm-server']", "    ports: ['8081:8081']"] + gpu + \
+           ["    environment:", "      - LLM_MODEL_PRESET=mistral-7b", "      - HSA_ENABLE_IPC_MODE_LEGACY=0",
+            "    # the llama-cpp / ollama containers' role: LLM_BACKEND_TYPE=llamacpp, LLAMACPP_ENDPOINT=http://llm:8081"]
     for svc, port in SERVICE_PORTS.items():
         if svc == "auth":
             continue

@@ -54,7 +54,7 @@ class Deployment:
     def __init__(self, tmp, overrides: dict | None = None):
         self.tmp = tmp
         self.procs: dict[str, subprocess.Popen] = {}
-        self.ports = {n: _free_port() for n in ("broker", "docstore", "vectorstore", *SERVICES)}
+        self.ports = {n: _free_port() for n in ("broker", "docstore", "vectorstore", "llm", *SERVICES)}
         self.env = {**os.environ, "PYTHONPATH": ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""),
                     "MESSAGE_BUS_TYPE": "cfcbroker", "CFC_BROKER_HOST": "127.0.0.1",
                     "CFC_BROKER_PORT": str(self.ports["broker"]),
@@ -187,14 +187,26 @@ def test_services_as_processes_on_the_gpu(deployment, tmp_path):
          tmp_path)
 
 
-def _run(d, tmp_path):
+@pytest.mark.timeout(600)
+def test_summarization_through_llamacpp_api_of_llm_server(deployment, tmp_path):
+    """The reference's llama.cpp topology: the summarization service uses the llama.cpp HTTP driver
+    (LLM_BACKEND_TYPE=llamacpp, /completion, temperature 0.7, stops) against this framework's LLM
+    server process (tiny random-init decoder on the CPU path)."""
+    d = deployment({"LLM_BACKEND_TYPE": "llamacpp", "LLM_MODEL_PRESET": "tiny", "LLM_DEVICE": "cpu",
+                    "LLM_MAX_BATCH": "4", "LLM_MAX_NEW_TOKENS": "24", "LLM_KV_CACHE_TOKENS": "32768"})
+    d.env["LLAMACPP_ENDPOINT"] = f"http://127.0.0.1:{d.ports['llm']}"
+    d.start("llm")
+    _run(d, tmp_path, extra_infra=("llm",), late_archive=False)
+
+
+def _run(d, tmp_path, extra_infra=(), late_archive=True):
     from copilot_for_consensus_amd.bus.cfcbroker import Connection
     from copilot_for_consensus_amd.utils.synthetic import SyntheticArchive
 
     d.start("broker", "--data-dir", str(tmp_path / "broker"))
     d.start("docstore", "--data-dir", str(tmp_path / "docstore"))
     d.start("vectorstore")
-    for n in ("broker", "docstore", "vectorstore"):
+    for n in ("broker", "docstore", "vectorstore", *extra_infra):
         d.wait_tcp(n)
     for s in SERVICES:
         d.start(s)
@@ -220,6 +232,8 @@ def _run(d, tmp_path):
     code, hits = _http("GET", d.url("reporting", f"/api/reports/search?topic={topic}&min_score=0.0"))
     assert code == 200 and hits["count"] >= 1, hits
 
+    if not late_archive:
+        return
     # chunking dies; a second archive arrives while it is down; its events wait in the broker
     d.kill("chunking")
     mbox = SyntheticArchive(seed=7).mbox(3)
