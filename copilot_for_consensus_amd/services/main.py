@@ -7,6 +7,7 @@ infrastructure a one-process-per-service deployment needs.
     python -m copilot_for_consensus_amd.services.main docstore     # document store server (MongoDB role)
     python -m copilot_for_consensus_amd.services.main vectorstore  # HIP kNN behind Qdrant's REST API
     python -m copilot_for_consensus_amd.services.main llm          # HIP decoder behind llama.cpp / Ollama / OpenAI APIs
+    python -m copilot_for_consensus_amd.services.main embedserver  # HIP encoder behind OpenAI / Ollama / TEI embeddings
 
 Reference entry points: <service>/main.py (e.g. ingestion/main.py:179, parsing/main.py:101-124).
 """
@@ -31,13 +32,13 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("service", choices=["node", "ingestion", "parsing", "chunking", "embedding", "orchestrator",
                                         "summarization", "reporting", "auth", "broker", "docstore", "vectorstore",
-                                        "llm"])
+                                        "llm", "embedserver"])
     ap.add_argument("--port", type=int, default=None)
     ap.add_argument("--host", default=None)
     ap.add_argument("--data-dir", default=None, help="broker journal / docstore WAL / vector index directory")
     args = ap.parse_args(argv)
 
-    if args.service in ("broker", "docstore", "vectorstore", "llm"):
+    if args.service in ("broker", "docstore", "vectorstore", "llm", "embedserver"):
         return _infra(args)
 
     if args.service == "auth":
@@ -147,6 +148,13 @@ def _infra(args) -> int:
         app, _ = build_from_config(llm)
         port = args.port or load_adapter_config("llm_backend", driver="llamacpp").driver_config.get("port") or 8081
         uvicorn.run(app, host=host, port=int(port), log_level="warning")
+        return 0
+    if args.service == "embedserver":
+        from ..embedding import HipEncoderProvider
+        from ..serving import create_embedding_app
+        emb = load_adapter_config("embedding_backend", driver="hip").driver_config   # EMBEDDING_MODEL_NAME / _DEVICE
+        app = create_embedding_app(HipEncoderProvider(**{k: v for k, v in emb.items() if v is not None}))
+        uvicorn.run(app, host=host, port=args.port or 8082, log_level="warning")
         return 0
     from ..vectorstore.server import create_vector_app
     hip = load_adapter_config("vector_store", driver="hip").driver_config     # VECTOR_STORE_* of the hip driver
