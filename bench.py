@@ -40,6 +40,8 @@ def parse_args(argv=None):
     ap.add_argument("--prefill-tokens", type=int, default=16384)
     ap.add_argument("--kv-dtype", choices=["bf16", "fp8"], default="bf16",
                     help="KV-cache storage; fp8 (e4m3fn) is an opt-in precision trade-off, not the headline")
+    ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16",
+                    help="decoder projections; fp8 = opt-in W8A8 e4m3fn (precision trade-off, not the headline)")
     ap.add_argument("--llm-only", action="store_true", help="skip the CPU/encoder/kNN stages (diagnostic)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
@@ -65,6 +67,7 @@ def main(argv=None):
     groups = make_groups(env, args.tp)
     pipe = BenchPipeline(model=args.model, encoder=args.encoder, device=dev, threads_per_step=args.threads_per_gpu,
                          max_new_tokens=args.max_new, tp=args.tp, prefill_tokens=args.prefill_tokens, kv_dtype=args.kv_dtype,
+                         weight_dtype=args.weights,
                          llm_only=args.llm_only, use_graph=not args.no_graph,
                          seed=args.seed + 7919 * groups.dp_rank, groups=groups if args.tp > 1 else None)
 
@@ -122,7 +125,7 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_THREADS_PER_S, 2),
-            "dtype": "bf16",
+            "dtype": "bf16" if args.weights == "bf16" else "fp8_e4m3fn W8A8 (opt-in, reduced precision)",
             "data": "synthetic .mbox threads, random-init weights",
             "config": {
                 "model": args.model,

@@ -125,6 +125,8 @@ class DecoderWeights:
         # ggml-quantized copies of the projections for the B <= 4 decode GEMV (GGUF checkpoints)
         self.qlayers: list[dict] | None = None
         self.q_lm_head = None
+        # opt-in W8A8 FP8 projections (e4m3fn + per-output-channel scales): to_fp8()
+        self.fp8_layers: list[dict] | None = None
         self.cos_sin = rope_cos_sin(cfg.max_positions, cfg.head_dim, cfg.rope_theta, device=self.device,
                                     llama3_scaling=cfg.rope_llama3)
 
@@ -279,8 +281,30 @@ class DecoderWeights:
             self.gate_up_interleaved = True
         return self
 
+    FP8_PROJECTIONS = ("qkv", "o", "gate_up", "down")
+
+    def to_fp8(self, keep_bf16: bool = False) -> "DecoderWeights":
+        """Opt-in W8A8 FP8 (OCP e4m3fn, gfx950 MFMA FP8): every projection quantised once with
+        per-output-channel scales; activations are quantised per token at run time
+        (ops.kernels.linear_fp8).  A precision trade-off like llama.cpp's Q8_0 / the reference's
+        Q4_K_M deployment -- not the bf16 headline.  The bf16 copies are dropped unless ``keep_bf16``;
+        norms, embeddings and the lm_head stay bf16."""
+        self.fp8_layers = []
+        for layer in self.layers:
+            q = {}
+            for name in self.FP8_PROJECTIONS:
+                q[name] = K.quant_fp8_weight(layer[name])
+                if not keep_bf16:
+                    layer[name] = None
+            self.fp8_layers.append(q)
+        if not keep_bf16 and self.device.type == "cuda":
+            torch.cuda.empty_cache()
+        return self
+
     def nbytes(self) -> int:
-        n = sum(t.numel() * t.element_size() for layer in self.layers for t in layer.values())
+        n = sum(t.numel() * t.element_size() for layer in self.layers for t in layer.values() if t is not None)
+        for q in self.fp8_layers or []:
+            n += sum(a.numel() * a.element_size() + b.numel() * b.element_size() for a, b in q.values())
         return n + sum(t.numel() * t.element_size() for t in (self.embed, self.final_norm, self.lm_head))
 
 
@@ -333,16 +357,26 @@ class DecoderModel:
             mode = "skinny" if fused_decode else "lib"
         if weights.tp_size != 1 or (mode == "skinny" and not weights.gate_up_interleaved):
             mode = "lib"
+        self.fp8 = weights.fp8_layers is not None
+        if self.fp8:
+            mode = "lib"          # W8A8: every projection through linear_fp8 (bf16 fused paths need bf16 weights)
         self.decode_gemm = mode
         # B <= 4 decode steps on the GEMV kernel (needs the interleaved gate/up layout for SwiGLU)
         gemv_shapes = (self.cfg.hidden % 8 == 0 and (weights.heads * self.cfg.head_dim) % 8 == 0
                        and weights.ffn % 32 == 0 and self.cfg.head_dim % 2 == 0)
         self.decode_gemv = (os.environ.get("CFC_DECODE_GEMV", "1") != "0" and weights.gate_up_interleaved
-                            and mode == "splitk" and gemv_shapes)
+                            and mode == "splitk" and gemv_shapes and not self.fp8)
         self.fused_decode = mode == "skinny"
         # B <= 4 decode on the ggml-quantized weights (GGUF checkpoints; csrc/kernels/quant.hip)
         self.decode_qgemv = (weights.qlayers is not None and os.environ.get("CFC_DECODE_QGEMV", "1") != "0"
-                             and weights.tp_size == 1 and weights.gate_up_interleaved)
+                             and weights.tp_size == 1 and weights.gate_up_interleaved and not self.fp8)
+
+    def _lin(self, i: int, name: str, x: torch.Tensor) -> torch.Tensor:
+        """Projection ``name`` of layer ``i``: bf16 library GEMM, or W8A8 FP8 in fp8 mode."""
+        if self.fp8:
+            w8, s = self.w.fp8_layers[i][name]
+            return K.linear_fp8(x, w8, s)
+        return F.linear(x, self.w.layers[i][name])
 
     def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.w.tp_size > 1:
@@ -364,9 +398,9 @@ class DecoderModel:
     def _mlp(self, i, attn_out, residual):
         lw = self.w.layers[i]
         h = K.rmsnorm(attn_out, lw["mlp_norm"], self.cfg.rms_eps, residual=residual)
-        gu = F.linear(h, lw["gate_up"])
+        gu = self._lin(i, "gate_up", h)
         a = K.silu_mul(gu, interleaved=self.w.gate_up_interleaved)
-        return self._all_reduce(F.linear(a, lw["down"]))
+        return self._all_reduce(self._lin(i, "down", a))
 
     def forward_prefill(self, ids, positions, slots, cu_q, ctx_lens, block_tables, kv, tiles=None,
                         last_idx=None, v_runs=None) -> torch.Tensor:
@@ -378,12 +412,12 @@ class DecoderModel:
         for i in range(cfg.layers):
             lw = w.layers[i]
             h, residual = self._layer_pre(i, x, residual)
-            qkv = F.linear(h, lw["qkv"])
+            qkv = self._lin(i, "qkv", h)
             q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
                                 cfg.head_dim, runs=v_runs, k_scale=kv.k_scale, v_scale=kv.v_scale)
             attn = K.prefill_attention(q, kv.k[i], kv.v[i], block_tables, cu_q, ctx_lens, self.scale, tiles=tiles,
                                        window=self.window, k_scale=kv.k_scale, v_scale=kv.v_scale)
-            o = self._all_reduce(F.linear(attn.view(attn.shape[0], -1), lw["o"]))
+            o = self._all_reduce(self._lin(i, "o", attn.view(attn.shape[0], -1)))
             x = self._mlp(i, o, residual)
         if last_idx is not None:
             x = x.index_select(0, last_idx)
@@ -406,13 +440,13 @@ class DecoderModel:
         for i in range(cfg.layers):
             lw = w.layers[i]
             h, residual = self._layer_pre(i, x, residual)
-            qkv = F.linear(h, lw["qkv"])
+            qkv = self._lin(i, "qkv", h)
             q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
                                 cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
             attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
                                             part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
                                             k_scale=kv.k_scale, v_scale=kv.v_scale)
-            o = self._all_reduce(F.linear(attn.view(B, -1), lw["o"]))
+            o = self._all_reduce(self._lin(i, "o", attn.view(B, -1)))
             x = self._mlp(i, o, residual)
         return K.rmsnorm(x, w.final_norm, cfg.rms_eps, residual=residual)
 

@@ -276,3 +276,11 @@ def pool(hidden, cu_seqlens, mode="mean", normalize=True):
 
 def softmax_scale(head_dim: int) -> float:
     return 1.0 / math.sqrt(head_dim)
+
+
+def quant_fp8_rows(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """fp32 reference of the per-row FP8 quantisation kernel."""
+    xf = x.float()
+    amax = xf.abs().amax(1, keepdim=True)
+    s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    return (xf / s).clamp(-448.0, 448.0).to(torch.float8_e4m3fn), s

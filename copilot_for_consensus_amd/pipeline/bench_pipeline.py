@@ -32,7 +32,7 @@ class StepResult:
 class BenchPipeline:
     def __init__(self, model="mistral-7b", encoder="minilm-l6", device="cuda", threads_per_step=128,
                  max_new_tokens=512, tp=1, prefill_tokens=16384, llm_only=False, use_graph=True, seed=0,
-                 index_prefill=1_000_000, groups=None, kv_dtype="bf16"):
+                 index_prefill=1_000_000, groups=None, kv_dtype="bf16", weight_dtype="bf16"):
         from ..models.decoder import DecoderModel, DecoderWeights, get_config
         from ..runtime.engine import LLMEngine
         from ..runtime.kv_cache import PagedKVCache, blocks_needed
@@ -53,6 +53,8 @@ class BenchPipeline:
         self.rng = random.Random(seed)
         self.seed = seed
         w = DecoderWeights.random(self.cfg, self.device, seed=1234, tp_rank=tp_rank, tp_size=tp)
+        if weight_dtype == "fp8":
+            w.to_fp8()           # opt-in W8A8 FP8 projections (precision trade-off, not the headline)
         custom_ar = None
         if tp > 1:
             from ..parallel.custom_ar import maybe_create

@@ -81,7 +81,8 @@ class HipLLMSummarizer(Summarizer):
                  max_new_tokens: int = 512, temperature: float = 0.0, max_batch: int = 128,
                  kv_cache_tokens: int = 524288, device: str = "cuda", seed: int = 1234, tp_group=None,
                  tp_rank: int = 0, ignore_eos: bool = False, top_k: int = 40, top_p: float = 0.95,
-                 min_p: float = 0.05, stop_sequences=("</s>", "\n\n\n"), **_):
+                 min_p: float = 0.05, stop_sequences=("</s>", "\n\n\n"), weight_dtype: str = "bf16",
+                 kv_cache_dtype: str = "bf16", **_):
         from ..models.decoder import DecoderModel, DecoderWeights, get_config, load_config_json
         from ..runtime.engine import LLMEngine
         from ..runtime.kv_cache import PagedKVCache
@@ -107,6 +108,8 @@ class HipLLMSummarizer(Summarizer):
             cfg = get_config(model)
             w = DecoderWeights.random(cfg, dev, seed=seed, tp_rank=tp_rank, tp_size=tensor_parallel)
             self.tokenizer = synthetic_bpe(cfg.vocab_size)
+        if weight_dtype == "fp8":
+            w.to_fp8()           # opt-in W8A8 FP8 projections (LLM_WEIGHT_DTYPE=fp8)
         self.cfg = cfg
         self.model = cfg.name
         custom_ar = None
@@ -114,7 +117,8 @@ class HipLLMSummarizer(Summarizer):
             from ..parallel.custom_ar import maybe_create
             custom_ar = maybe_create(tp_group, dev)
         self.decoder = DecoderModel(w, tp_group=tp_group, custom_ar=custom_ar)
-        self.kv = PagedKVCache.for_budget(cfg.layers, w.kv_heads, cfg.head_dim, dev, kv_cache_tokens)
+        kvd = torch.float8_e4m3fn if kv_cache_dtype == "fp8" else torch.bfloat16
+        self.kv = PagedKVCache.for_budget(cfg.layers, w.kv_heads, cfg.head_dim, dev, kv_cache_tokens, dtype=kvd)
         self.engine = LLMEngine(self.decoder, self.kv)
         self.max_new_tokens, self.temperature = int(max_new_tokens), float(temperature)
         # llama.cpp server sampling defaults + the reference's stop sequences (llamacpp_summarizer.py:111-113)

@@ -173,6 +173,51 @@ __global__ void silu_mul_kernel(uint16_t* __restrict__ out, const uint16_t* __re
   reinterpret_cast<uint4*>(out + (size_t)t * F)[c] = pack8(r);
 }
 
+// Per-row (per-token) FP8 quantisation for the W8A8 linear path: scale[r] = max|x[r,:]| / 448,
+// out[r,:] = e4m3fn(x[r,:] / scale[r]) (OCP e4m3 via gfx950's v_cvt_pk_fp8_f32, saturating).
+// One 256-thread workgroup per row; the row stays in registers between the amax pass and the
+// conversion (K <= 256 * 8 * QR_MAX_VEC), so it is read from HBM once.
+constexpr int QR_MAX_VEC = 16;   // up to 32768 columns
+__global__ void __launch_bounds__(256) quant_fp8_rows_kernel(const uint16_t* __restrict__ x, uint8_t* __restrict__ out,
+                                                            float* __restrict__ scale, int K) {
+  const int r = blockIdx.x, t = threadIdx.x;
+  const int nvec = K >> 3;
+  const uint4* row = reinterpret_cast<const uint4*>(x + (size_t)r * K);
+  uint4 v[QR_MAX_VEC];
+  float amax = 0.f;
+#pragma unroll
+  for (int j = 0; j < QR_MAX_VEC; ++j) {
+    const int c = t + 256 * j;
+    if (c < nvec) {
+      v[j] = row[c];
+      float f[8];
+      unpack8(v[j], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(f[e]));
+    }
+  }
+  __shared__ float red[4];
+  amax = wave_max(amax);
+  if ((t & 63) == 0) red[t >> 6] = amax;
+  __syncthreads();
+  amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float s = amax > 0.f ? amax / 448.f : 1.f;
+  const float inv = 1.f / s;
+  if (t == 0) scale[r] = s;
+  uint2* orow = reinterpret_cast<uint2*>(out + (size_t)r * K);
+#pragma unroll
+  for (int j = 0; j < QR_MAX_VEC; ++j) {
+    const int c = t + 256 * j;
+    if (c < nvec) {
+      float f[8];
+      unpack8(v[j], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] *= inv;
+      orow[c] = pack8_fp8(f);
+    }
+  }
+}
+
 // out[t, f] = gelu_erf(x[t, f] + bias[f])   (in place allowed)
 __global__ void bias_gelu_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ x,
                                  const uint16_t* __restrict__ bias, int T, int F) {
@@ -545,6 +590,13 @@ CFC_API int cfc_decode_advance_cb(const int32_t* next, int32_t* tokens, int cap,
   decode_advance_cb_kernel<<<(B + 255) / 256, 256, 0, stream>>>(next, tokens, cap, gen, limit, input_ids, positions,
                                                                  ctx_lens, slots, block_tables, max_blocks, done,
                                                                  stop_ids, n_stop, B);
+  return CFC_CHECK_LAUNCH();
+}
+
+CFC_API int cfc_quant_fp8_rows(void* out, float* scale, const void* x, int M, int K, hipStream_t stream) {
+  if (K % 8 != 0 || K > 256 * 8 * QR_MAX_VEC || M < 0) return -1;
+  if (M == 0) return 0;
+  quant_fp8_rows_kernel<<<M, 256, 0, stream>>>((const uint16_t*)x, (uint8_t*)out, scale, K);
   return CFC_CHECK_LAUNCH();
 }
 

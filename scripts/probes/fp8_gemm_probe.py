@@ -38,6 +38,16 @@ def main():
                                                                         out_dtype=torch.bfloat16)), 1)
         except Exception as e:  # noqa: BLE001
             rec["fp8_error"] = f"{type(e).__name__}: {str(e)[:200]}"
+        try:   # rowwise: per-token activation scales x per-output-channel weight scales
+            ra = (a.abs().amax(1, keepdim=True) / 448.0).float()
+            rw = (w.abs().amax(1, keepdim=True) / 448.0).float()
+            a8r, w8r = (a / ra).to(f8), (w / rw).to(f8)
+            y = torch._scaled_mm(a8r, w8r.t(), scale_a=ra, scale_b=rw.t(), out_dtype=torch.bfloat16)
+            rec["fp8_rowwise_rel_err"] = float((y.float() - ref).norm() / ref.norm())
+            rec["fp8_rowwise_us"] = round(1e6 * bench(lambda: torch._scaled_mm(
+                a8r, w8r.t(), scale_a=ra, scale_b=rw.t(), out_dtype=torch.bfloat16)), 1)
+        except Exception as e:  # noqa: BLE001
+            rec["fp8_rowwise_error"] = f"{type(e).__name__}: {str(e)[:200]}"
         rec["bf16_us"] = round(1e6 * bench(lambda: torch.nn.functional.linear(a, w)), 1)
         flops = 2 * M * N * K
         if "fp8_us" in rec:
