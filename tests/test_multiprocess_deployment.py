@@ -21,6 +21,7 @@ import subprocess
 import sys
 import time
 import urllib.error
+import urllib.parse
 import urllib.request
 
 import pytest
@@ -54,7 +55,7 @@ class Deployment:
     def __init__(self, tmp, overrides: dict | None = None):
         self.tmp = tmp
         self.procs: dict[str, subprocess.Popen] = {}
-        self.ports = {n: _free_port() for n in ("broker", "docstore", "vectorstore", "llm", *SERVICES)}
+        self.ports = {n: _free_port() for n in ("broker", "docstore", "vectorstore", "llm", "auth", *SERVICES)}
         self.env = {**os.environ, "PYTHONPATH": ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""),
                     "MESSAGE_BUS_TYPE": "cfcbroker", "CFC_BROKER_HOST": "127.0.0.1",
                     "CFC_BROKER_PORT": str(self.ports["broker"]),
@@ -259,3 +260,54 @@ def _run(d, tmp_path, extra_infra=(), late_archive=True):
     st = admin.stats()["queues"]
     assert all(st[q]["ready"] == 0 and st[q]["unacked"] == 0 for q in SERVICES if q in st)
     assert not any(q.endswith(".dlq") and v["ready"] for q, v in st.items())
+
+
+@pytest.mark.timeout(600)
+def test_jwt_auth_across_processes(deployment, tmp_path):
+    """Auth as its own process (RS256 keys, mock OIDC provider, roles in the shared document store);
+    ingestion and reporting in theirs verify bearer tokens against its JWKS (reference
+    copilot_auth/middleware.py:122-270, role checks :424; ingestion requires admin, reporting reader)."""
+    d = deployment({"JWT_AUTH_ENABLED": "true", "AUTH_ENABLE_MOCK_PROVIDER": "true",
+                    "AUTH_FIRST_USER_AUTO_PROMOTION_ENABLED": "true", "AUTH_JWT_ALGORITHM": "RS256"})
+    auth_url = f"http://127.0.0.1:{d.ports['auth']}"
+    d.env.update({"INGESTION_AUTH_SERVICE_URL": auth_url, "REPORTING_AUTH_SERVICE_URL": auth_url,
+                  "AUTH_PORT": str(d.ports["auth"])})
+    d.start("broker", "--data-dir", str(tmp_path / "broker"))
+    d.start("docstore")
+    d.start("vectorstore")
+    for n in ("broker", "docstore", "vectorstore"):
+        d.wait_tcp(n)
+    d.start("auth")
+    d.wait_tcp("auth")
+    for s in ("ingestion", "reporting"):
+        d.start(s)
+    for s in ("ingestion", "reporting"):
+        d.wait_ready(s)
+
+    def login(user):
+        code, r = _http("GET", d.url("auth", "/login?provider=mock"))
+        assert code == 200, r
+        state = urllib.parse.parse_qs(urllib.parse.urlparse(r["authorization_url"]).query)["state"][0]
+        code, tok = _http("GET", d.url("auth", f"/callback?code={user}&state={state}"))
+        assert code == 200, tok
+        return tok["access_token"]
+
+    admin = login("alice")            # first user: promoted to admin
+    nobody = login("bob")             # second user: no roles until approved
+    body = {"name": "wg", "source_type": "local", "url": str(tmp_path)}
+    assert _http("POST", d.url("ingestion", "/api/sources"), body)[0] == 401
+    assert _http("POST", d.url("ingestion", "/api/sources"), body, {"Authorization": "Bearer junk"})[0] == 401
+    assert _http("POST", d.url("ingestion", "/api/sources"), body, {"Authorization": f"Bearer {nobody}"})[0] == 403
+    assert _http("POST", d.url("ingestion", "/api/sources"), body, {"Authorization": f"Bearer {admin}"})[0] == 201
+    assert _http("GET", d.url("reporting", "/api/reports"))[0] == 401
+    code, rep = _http("GET", d.url("reporting", "/api/reports"), headers={"Authorization": f"Bearer {admin}"})
+    assert code == 200 and rep["count"] == 0
+    assert _http("GET", d.url("reporting", "/health"))[0] == 200            # health stays public
+    # the admin grants bob the reader role through the auth admin API; his NEW token reads reports
+    code, _ = _http("POST", d.url("auth", "/admin/users/mock:bob/roles"), {"roles": ["reader"]},
+                    {"Authorization": f"Bearer {admin}"})
+    assert code == 200
+    bob2 = login("bob")
+    assert _http("GET", d.url("reporting", "/api/reports"), headers={"Authorization": f"Bearer {bob2}"})[0] == 200
+    assert _http("POST", d.url("ingestion", "/api/sources"), {**body, "name": "x"},
+                 {"Authorization": f"Bearer {bob2}"})[0] == 403
