@@ -57,6 +57,10 @@ def split_mbox(data: bytes) -> list[bytes]:
         chunk = data[off:end]
         nl = chunk.find(b"\n")
         body = chunk[nl + 1:] if nl >= 0 else b""
+        # the empty line in front of the next "From " line (or at end of file) belongs to the
+        # separator, as Python's mailbox.mbox (the reference parser) reads it
+        if body.endswith(b"\n\n") and not body.endswith(b"\r\n\r\n"):
+            body = body[:-1]
         if body.strip():
             msgs.append(body)
     return msgs

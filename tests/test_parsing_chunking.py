@@ -377,3 +377,16 @@ def test_retry_with_backoff():
     assert retry_with_backoff(f, 3, 5, 60, sleeper=sleeps.append) == "ok" and sleeps == [5, 10]
     with pytest.raises(IOError):
         retry_with_backoff(lambda: (_ for _ in ()).throw(IOError("y")), 2, 1, sleeper=sleeps.append)
+
+
+def test_mbox_separator_blank_line_is_not_body():
+    """Python's mailbox.mbox (the reference parser, parsing/app/parser.py:42-62) treats the blank
+    line in front of the next ``From `` line -- and at end of file -- as part of the separator; a
+    CRLF file keeps it (its lines are not the LF line separator)."""
+    from copilot_for_consensus_amd.parsing import split_mbox
+    mb = (b"From a@x Mon Jan  1 00:00:00 2024\nSubject: one\n\nbody one\n\n"
+          b"From b@x Mon Jan  1 00:00:00 2024\nSubject: two\n\nbody two\n\n")
+    one, two = split_mbox(mb)
+    assert one.endswith(b"body one\n") and two.endswith(b"body two\n")
+    crlf = split_mbox(mb.replace(b"\n", b"\r\n"))
+    assert crlf[0].endswith(b"body one\r\n\r\n")
