@@ -114,20 +114,35 @@ class SentenceTransformerProvider(EmbeddingProvider):  # pragma: no cover - opti
         return self.model.encode(text).tolist()
 
 
-class OpenAIEmbeddingProvider(EmbeddingProvider):  # pragma: no cover - optional dependency
+class OpenAIEmbeddingProvider(EmbeddingProvider):
+    """OpenAI / Azure OpenAI embeddings over REST (reference openai_provider.py:20,124-126; no SDK
+    needed): ``POST {base}/embeddings`` with 429 backoff -- works against any OpenAI-compatible
+    endpoint, including this framework's HIP embedding server (serving/embed_server.py)."""
     backend = "openai"
 
-    def __init__(self, api_key=None, model=None, **_):
-        try:
-            import openai
-        except ImportError as e:
-            raise ImportError("openai is not installed") from e
-        self.client = openai.OpenAI(api_key=api_key)
-        self.model_name = model or "text-embedding-3-small"
+    def __init__(self, api_key=None, model=None, organization=None, base_url=None, api_base=None, api_version=None,
+                 deployment_name=None, **_):
+        from ..utils.openai_rest import OpenAIRestClient
+        azure = bool(api_base and deployment_name)
+        self.client = OpenAIRestClient(api_key=api_key, base_url=base_url, azure_endpoint=api_base if azure else None,
+                                       api_version=api_version, deployment=deployment_name, organization=organization)
+        self.model_name = model or deployment_name or "text-embedding-3-small"
+        self._dim = None
+
+    @property
+    def dimension(self) -> int:
+        if self._dim is None:            # probe once, as the reference's embedding main does (main.py:295)
+            self._dim = len(self.embed("test"))
+        return self._dim
 
     def embed(self, text):
         _check_text(text)
-        return self.client.embeddings.create(model=self.model_name, input=text).data[0].embedding
+        return self.client.embeddings(self.model_name, text)[0]
+
+    def embed_batch(self, texts: list[str]) -> list[list[float]]:
+        for t in texts:
+            _check_text(t)
+        return self.client.embeddings(self.model_name, list(texts)) if texts else []
 
 
 def create_embedding_provider(cfg=None, **overrides) -> EmbeddingProvider:

@@ -219,24 +219,35 @@ class LlamaCppSummarizer(_HTTPSummarizer):
                        len(text.split()), int(1000 * (time.perf_counter() - t0)))
 
 
-class OpenAISummarizer(Summarizer):  # pragma: no cover - optional dependency
+class OpenAISummarizer(Summarizer):
+    """OpenAI / Azure OpenAI chat completions over REST (reference openai_summarizer.py:46; no SDK
+    needed): one user message with the prompt, ``max_tokens`` = the thread's context window
+    (:313-317), 429s retried with full-jitter backoff honouring retry-after (:189-286).  Any
+    OpenAI-compatible server works, including this framework's LLM server (serving/llm_server.py)."""
     backend = "openai"
 
-    def __init__(self, openai_api_key=None, openai_model=None, openai_base_url=None, **_):
-        try:
-            import openai
-        except ImportError as e:
-            raise ImportError("openai is not installed") from e
-        self.client = openai.OpenAI(api_key=openai_api_key, base_url=openai_base_url)
-        self.model = openai_model or "gpt-4o-mini"
+    def __init__(self, openai_api_key=None, openai_model=None, openai_base_url=None, azure_openai_api_key=None,
+                 azure_openai_endpoint=None, azure_openai_deployment=None, azure_openai_model=None,
+                 azure_openai_api_version=None, max_retries: int = 3, base_backoff_seconds: float = 5.0, **_):
+        from ..utils.openai_rest import OpenAIRestClient
+        self.is_azure = bool(azure_openai_endpoint and azure_openai_deployment)
+        self.client = OpenAIRestClient(
+            api_key=azure_openai_api_key if self.is_azure else openai_api_key, base_url=openai_base_url,
+            azure_endpoint=azure_openai_endpoint if self.is_azure else None, api_version=azure_openai_api_version,
+            deployment=azure_openai_deployment, max_retries=max_retries, base_backoff_seconds=base_backoff_seconds)
+        self.model = (azure_openai_deployment if self.is_azure else openai_model) or "gpt-4o-mini"
+        self.backend = "azure" if self.is_azure else "openai"
 
     def summarize(self, thread):
         t0 = time.perf_counter()
-        r = self.client.chat.completions.create(model=self.model, messages=[{"role": "user", "content": thread.prompt}],
-                                                max_tokens=thread.context_window_tokens)
-        text = r.choices[0].message.content or ""
-        return Summary(thread.thread_id, text, [], self.backend, self.model, r.usage.prompt_tokens,
-                       r.usage.completion_tokens, int(1000 * (time.perf_counter() - t0)))
+        r = self.client.chat(self.model, [{"role": "user", "content": thread.prompt}],
+                             max_tokens=thread.context_window_tokens)
+        text = r["choices"][0]["message"].get("content")
+        if text is None:
+            raise AttributeError("OpenAI response message content was None")
+        usage = r.get("usage") or {}
+        return Summary(thread.thread_id, text, [], self.backend, self.model, int(usage.get("prompt_tokens", 0)),
+                       int(usage.get("completion_tokens", 0)), int(1000 * (time.perf_counter() - t0)))
 
 
 def create_llm_backend(cfg=None, **overrides) -> Summarizer:
