@@ -152,13 +152,22 @@ class ContinuousEngine:
         pc = self.engine.prefix_cache
         tables, fresh, start = [], [], []
         try:
-            for r in take:
+            for i, r in enumerate(take):
                 n = blocks_needed(len(r.prompt) + r.max_new)
                 shared = pc.acquire(r.prompt) if pc is not None else []
-                tables.append(shared)
-                new = pc.alloc(n - len(shared)) if pc is not None else self.kv.pool.alloc(n)
+                try:
+                    new = pc.alloc(n - len(shared)) if pc is not None else self.kv.pool.alloc(n)
+                except MemoryError:
+                    # KV cache full: admit what fits, the rest waits in the queue for running slots to
+                    # finish and return their blocks (only a request that can never fit is an error)
+                    self.engine._release([shared], [[]])
+                    if i == 0 and idle:
+                        raise
+                    self.queue.extendleft(reversed(take[i:]))
+                    take = take[:i]
+                    break
+                tables.append(shared + new)
                 fresh.append(new)
-                tables[-1] = shared + new
                 start.append(len(shared) * KV_BLOCK)
                 if pc is not None:
                     pc.insert(r.prompt, tables[-1])
@@ -166,6 +175,8 @@ class ContinuousEngine:
             self.engine._release(tables, fresh, failed=True)
             self.queue.extendleft(reversed(take))
             raise
+        if not take:
+            return
         t = time.perf_counter()
         try:
             first = self.engine._prefill([r.prompt for r in take], tables, self.sampling, self.seed, start)

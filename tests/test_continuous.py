@@ -95,3 +95,25 @@ def test_failed_admission_returns_blocks_and_requeues(monkeypatch):
     assert kv.pool.num_free() + cached == free0 and len(ce.queue) == 1 and len(ce.free) == 2
     monkeypatch.undo()
     assert len(ce.run()) == 1
+
+
+def test_admission_waits_for_kv_blocks_instead_of_failing():
+    """With a KV cache too small for every queued request at once, admission takes what fits and
+    the rest waits for finished slots to return their blocks (the LLM server's load case)."""
+    import torch
+    from copilot_for_consensus_amd.models.decoder import DecoderModel, DecoderWeights, get_config
+    from copilot_for_consensus_amd.runtime.continuous import ContinuousEngine
+    from copilot_for_consensus_amd.runtime.engine import LLMEngine
+    from copilot_for_consensus_amd.runtime.kv_cache import PagedKVCache, blocks_needed
+    cfg = get_config("tiny")
+    model = DecoderModel(DecoderWeights.random(cfg, "cpu", seed=5))
+    per = blocks_needed(60 + 8)
+    kv = PagedKVCache(cfg.layers, 2 * per + 1 + 1, model.w.kv_heads, cfg.head_dim, "cpu")   # 2 requests + scratch
+    eng = LLMEngine(model, kv, prefix_cache=False)
+    ce = ContinuousEngine(eng, max_slots=4, max_new_cap=8, max_prompt=64, steps_per_sync=4)
+    prompts = [[1] + [(3 * i + j) % 500 + 3 for j in range(59)] for i in range(5)]
+    reqs = [ce.submit(p, 8) for p in prompts]
+    done = ce.run()
+    assert len(done) == 5 and all(len(r.tokens) == 8 for r in reqs)
+    want = eng.generate([prompts[4]], 8, temperature=0.0, ignore_eos=True).tokens[0]
+    assert reqs[4].tokens == want
