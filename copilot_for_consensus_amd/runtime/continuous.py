@@ -42,6 +42,8 @@ class Request:
     first_token_s: float | None = None
     finished_s: float | None = None
     tokens: list[int] | None = None
+    slot: int | None = None              # decode slot while running
+    cancelled: bool = False
 
     @property
     def latency_s(self) -> float | None:
@@ -94,6 +96,7 @@ class ContinuousEngine:
         self.slot_req: list[Request | None] = [None] * B
         self.slot_tables: list[tuple[list[int], list[int]] | None] = [None] * B
         self.free = list(range(B - 1, -1, -1))
+        self._cancelled: list[Request] = []
         self._rid = 0
         self.stats = {"steps": 0, "admitted": 0, "finished": 0, "prefill_s": 0.0, "decode_s": 0.0}
 
@@ -109,17 +112,50 @@ class ContinuousEngine:
         return r
 
     def pending(self) -> int:
-        return len(self.queue) + sum(r is not None for r in self.slot_req)
+        return len(self.queue) + sum(r is not None for r in self.slot_req) + len(self._cancelled)
+
+    def cancel(self, r: Request) -> None:
+        """Stop a request early (client gone, stop string seen): a queued one is dropped, a running
+        one has its slot marked done on the device, so the next harvest returns its tokens so far."""
+        if r.finished_s is not None or r.cancelled:
+            return
+        r.cancelled = True
+        if r in self.queue:
+            self.queue.remove(r)
+            r.tokens, r.finished_s = [], time.perf_counter()
+            self._cancelled.append(r)
+        elif r.slot is not None and self.slot_req[r.slot] is r:
+            self.done[r.slot] = 1
+
+    def partial(self, reqs: list[Request]) -> dict[int, list[int]]:
+        """Tokens generated so far by running requests (one device->host copy): rid -> tokens."""
+        live = [r for r in reqs if r.slot is not None and self.slot_req[r.slot] is r]
+        if not live:
+            return {}
+        idx = torch.tensor([r.slot for r in live], dtype=torch.long, device=self.device)
+        gen = self.gen.index_select(0, idx).cpu().tolist()
+        toks = self.tokens.index_select(0, idx).cpu()
+        stop = set(self.stop_ids)
+        out = {}
+        for i, r in enumerate(live):
+            row = toks[i, :min(gen[i], self.cap)].tolist()
+            for j, t in enumerate(row):
+                if t in stop:
+                    row = row[:j]
+                    break
+            out[r.rid] = row
+        return out
 
     @torch.inference_mode()
     def step(self) -> list[Request]:
         """Admit what fits, run one burst of decode steps, harvest; returns requests finished now."""
         self._admit()
+        early, self._cancelled = self._cancelled, []
         if all(r is None for r in self.slot_req):
-            return []
+            return early
         t = time.perf_counter()
         self._burst(self.steps_per_sync)
-        out = self._harvest()
+        out = early + self._harvest()
         self.stats["decode_s"] += time.perf_counter() - t
         return out
 
@@ -197,6 +233,7 @@ class ContinuousEngine:
                        int(r.max_new <= 1 or f in self.stop_ids))
             r.first_token_s = now
             self.slot_req[s] = r
+            r.slot = s
             self.slot_tables[s] = (tbl, fresh[i])
         idx = torch.tensor(slots, dtype=torch.long, device=self.device)
         rows_t = torch.from_numpy(rows).to(self.device)
@@ -261,7 +298,7 @@ class ContinuousEngine:
                     row = row[:j]
                     break
             r = self.slot_req[s]
-            r.tokens, r.finished_s = row, now
+            r.tokens, r.finished_s, r.slot = row, now, None
             out.append(r)
             self._release_slot(s)
         # freeze the freed rows on the scratch block before their KV blocks can be reused

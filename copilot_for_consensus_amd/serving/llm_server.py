@@ -20,8 +20,9 @@ Routes:
   llama.cpp  POST /completion, POST /tokenize, POST /detokenize, GET /health, GET /props
   Ollama     POST /api/generate, POST /api/chat, GET /api/tags, GET /api/version
   OpenAI     POST /v1/completions, POST /v1/chat/completions, GET /v1/models
-``stream: true`` is answered in each API's streaming framing (NDJSON / SSE) with the completion as
-one chunk followed by the final record.
+``stream: true`` streams text deltas as the slot engine produces them (read after every burst of
+decode steps), in each API's framing (SSE for llama.cpp / OpenAI, NDJSON for Ollama), then the
+API's final record; a client that disconnects cancels its generation.
 """
 from __future__ import annotations
 
@@ -58,10 +59,18 @@ class GenRequest:
     gen_s: float = 0.0
     error: str | None = None
     truncated: bool = False              # the prompt was cut to fit the context
+    stream: bool = False                 # push text deltas through on_delta while generating
+    on_delta: Any = None
+    emitted: int = 0                     # characters already pushed
+    handle: Any = None                   # (engine key, continuous Request) while on a slot engine
     loop: Any = None                     # asyncio loop + event of an async waiter (the HTTP handlers)
     aevent: Any = None
 
     def complete(self) -> None:
+        if self.stream and self.on_delta is not None and not self.error:
+            if len(self.text) > self.emitted:
+                self.on_delta(self.text[self.emitted:])
+                self.emitted = len(self.text)
         self.done.set()
         if self.aevent is not None:
             self.loop.call_soon_threadsafe(self.aevent.set)
@@ -102,6 +111,10 @@ class BatchScheduler:
         if r.error:
             raise RuntimeError(r.error)
         return r
+
+    def cancel(self, r: GenRequest) -> None:
+        """Thread-safe: stop a request whose client went away."""
+        self.q.put(("cancel", r))
 
     async def asubmit(self, r: GenRequest, timeout: float = 600.0) -> GenRequest:
         """Non-blocking wait for the HTTP handlers: no worker thread is held per in-flight request."""
@@ -161,11 +174,17 @@ class BatchScheduler:
                     break
             legacy: dict[tuple, list[GenRequest]] = {}
             for r in batch:
+                if isinstance(r, tuple):          # ("cancel", request)
+                    h = r[1].handle
+                    if h is not None and h[0] in self.engines:
+                        self.engines[h[0]].cancel(h[1])
+                    continue
                 ce = self._continuous_for(r)
                 if ce is None:
                     legacy.setdefault(r.key(), []).append(r)
                 else:
                     cr = ce.submit(r.prompt_ids, r.max_new)
+                    r.handle = (r.key(), cr)
                     self._inflight[r.key()][cr.rid] = r
             for g in legacy.values():
                 for s in range(0, len(g), self.max_batch):
@@ -186,12 +205,36 @@ class BatchScheduler:
                     continue
                 if finished:
                     self.batches += 1
+                self._stream_partials(key, ce, {cr.rid for cr in finished})
                 for cr in finished:
                     r = self._inflight[key].pop(cr.rid)
                     self._finish(r, cr.tokens, cr.tokens is not None and len(cr.tokens) >= r.max_new,
                                  (cr.first_token_s or cr.submitted_s) - cr.submitted_s,
                                  cr.finished_s - (cr.first_token_s or cr.submitted_s))
                     r.complete()
+
+    def _stream_partials(self, key, ce, finishing: set[int]) -> None:
+        """Push the new text of streaming requests still running; a stop string seen mid-stream
+        cancels the slot (the text up to it is what the client gets)."""
+        live = {rid: r for rid, r in self._inflight.get(key, {}).items() if r.stream and rid not in finishing}
+        if not live:
+            return
+        parts = ce.partial([r.handle[1] for r in live.values()])
+        for rid, toks in parts.items():
+            r = live[rid]
+            text = self.tok.decode(toks[:r.max_new])
+            cut = min((i for i in (text.find(s) for s in r.stop) if i >= 0), default=-1)
+            if cut >= 0:
+                ce.cancel(r.handle[1])
+                text = text[:cut]
+            hold = max((len(s) for s in r.stop), default=1) - 1     # a stop string may be forming
+            upto = len(text) if cut >= 0 else max(r.emitted, len(text) - hold)
+            # a multi-byte character still being generated decodes as U+FFFD: wait for it
+            while upto > r.emitted and text[upto - 1] == "\ufffd":
+                upto -= 1
+            if upto > r.emitted:
+                r.on_delta(text[r.emitted:upto])
+                r.emitted = upto
 
     def _finish(self, r: GenRequest, toks: list[int], hit_limit: bool, prompt_s: float, gen_s: float) -> None:
         toks = list(toks[:r.max_new])
@@ -277,7 +320,7 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
             raise HTTPException(400, "empty prompt")
         return ids
 
-    async def run(prompt, n_predict, temperature, top_k, top_p, min_p, seed, stop, ignore_eos=False) -> GenRequest:
+    def prepare(prompt, n_predict, temperature, top_k, top_p, min_p, seed, stop, ignore_eos=False) -> GenRequest:
         ids = encode(prompt)
         want = None if n_predict is None or int(n_predict) < 0 else int(n_predict)
         if want == 0:
@@ -296,10 +339,45 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
         r = GenRequest(ids, n, float(temperature or 0.0), int(top_k or 0), float(1.0 if top_p is None else top_p),
                        float(min_p or 0.0), int(seed or 0), tuple(s for s in (stop or []) if s), bool(ignore_eos))
         r.truncated = truncated
+        return r
+
+    async def run(*args, **kw) -> GenRequest:
         try:
-            return await sched.asubmit(r)
+            return await sched.asubmit(prepare(*args, **kw))
         except RuntimeError as e:
             raise HTTPException(500, str(e))
+
+    def streamed(r: GenRequest, frame_delta, frame_final, media_type: str, tail: str | None = None):
+        """Incremental response: one frame per text delta while the slot engine generates, then the
+        API's final record; a client that disconnects cancels the generation."""
+        import asyncio
+        loop = asyncio.get_event_loop()
+        q: asyncio.Queue = asyncio.Queue()
+        r.stream, r.loop, r.aevent = True, loop, asyncio.Event()
+        r.on_delta = lambda text: loop.call_soon_threadsafe(q.put_nowait, text)
+        sched.q.put(r)
+
+        async def gen():
+            done_wait = asyncio.ensure_future(r.aevent.wait())
+            try:
+                while True:
+                    get = asyncio.ensure_future(q.get())
+                    finished, _ = await asyncio.wait({get, done_wait}, return_when=asyncio.FIRST_COMPLETED)
+                    if get in finished:
+                        yield frame_delta(get.result())
+                        continue
+                    get.cancel()
+                    while not q.empty():
+                        yield frame_delta(q.get_nowait())
+                    break
+                yield frame_final(None if r.error else r)
+                if tail:
+                    yield tail
+            finally:
+                if not r.done.is_set():
+                    sched.cancel(r)
+                done_wait.cancel()
+        return StreamingResponse(gen(), media_type=media_type)
 
     # ------------------------------------------------------------------ llama.cpp server
     @app.get("/health")
@@ -323,22 +401,24 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
     @app.post("/completion")
     async def completion(body: dict = Body(...)):
         # llama.cpp defaults: temperature 0.8, top_k 40, top_p 0.95, min_p 0.05
-        r = await run(body.get("prompt"), body.get("n_predict", default_n_predict), body.get("temperature", 0.8),
+        args = (body.get("prompt"), body.get("n_predict", default_n_predict), body.get("temperature", 0.8),
                 body.get("top_k", 40), body.get("top_p", 0.95), body.get("min_p", 0.05), body.get("seed"),
                 body.get("stop"), body.get("ignore_eos", False))
-        out = {"content": r.text, "model": model_name, "stop": True, "tokens_predicted": len(r.tokens),
+        if body.get("stream"):
+            return streamed(prepare(*args), lambda d: "data: " + json.dumps({"content": d, "stop": False}) + "\n\n",
+                            lambda r: "data: " + json.dumps({**llama_record(r), "content": ""} if r else
+                                                            {"error": "generation failed", "stop": True}) + "\n\n",
+                            "text/event-stream")
+        return llama_record(await run(*args))
+
+    def llama_record(r: GenRequest) -> dict:
+        return {"content": r.text, "model": model_name, "stop": True, "tokens_predicted": len(r.tokens),
                "tokens_evaluated": len(r.prompt_ids), "stopped_eos": r.finish == "stop" and not r.stopping_word,
                "stopped_word": bool(r.stopping_word), "stopped_limit": r.finish == "length",
                "stopping_word": r.stopping_word, "truncated": r.truncated,
                "timings": {"prompt_n": len(r.prompt_ids), "prompt_ms": 1000 * r.prompt_s,
                            "predicted_n": len(r.tokens), "predicted_ms": 1000 * r.gen_s,
                            "predicted_per_second": len(r.tokens) / r.gen_s if r.gen_s > 0 else 0.0}}
-        if body.get("stream"):
-            def sse():
-                yield "data: " + json.dumps({"content": r.text, "stop": False}) + "\n\n"
-                yield "data: " + json.dumps({**out, "content": ""}) + "\n\n"
-            return StreamingResponse(sse(), media_type="text/event-stream")
-        return out
 
     # ------------------------------------------------------------------ Ollama
     def ollama_opts(body):
@@ -353,11 +433,8 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
                 "prompt_eval_duration": int(1e9 * r.prompt_s), "eval_count": len(r.tokens),
                 "eval_duration": int(1e9 * r.gen_s)}
 
-    def ndjson(first: dict, last: dict):
-        def gen():
-            yield json.dumps(first) + "\n"
-            yield json.dumps(last) + "\n"
-        return StreamingResponse(gen(), media_type="application/x-ndjson")
+    def now_iso() -> str:
+        return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
 
     @app.post("/api/generate")
     async def ollama_generate(body: dict = Body(...)):
@@ -366,23 +443,30 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
             prompt = chat_prompt([{"role": "system", "content": body["system"]}, {"role": "user", "content": prompt}],
                                  family)
         n, temp, k, p, mp, seed, stop = ollama_opts(body)
-        r = await run(prompt, n, temp, k, p, mp, seed, stop)
-        rec = ollama_record(r, {"response": r.text, "context": []})
         if body.get("stream", True):                 # Ollama streams unless told not to
-            return ndjson({"model": model_name, "created_at": rec["created_at"], "response": r.text, "done": False},
-                          {**rec, "response": ""})
-        return rec
+            return streamed(prepare(prompt, n, temp, k, p, mp, seed, stop),
+                            lambda d: json.dumps({"model": model_name, "created_at": now_iso(), "response": d,
+                                                  "done": False}) + "\n",
+                            lambda r: json.dumps(ollama_record(r, {"response": "", "context": []}) if r else
+                                                 {"error": "generation failed"}) + "\n",
+                            "application/x-ndjson")
+        r = await run(prompt, n, temp, k, p, mp, seed, stop)
+        return ollama_record(r, {"response": r.text, "context": []})
 
     @app.post("/api/chat")
     async def ollama_chat(body: dict = Body(...)):
         n, temp, k, p, mp, seed, stop = ollama_opts(body)
-        r = await run(chat_prompt(body.get("messages") or [], family), n, temp, k, p, mp, seed, stop)
-        msg = {"role": "assistant", "content": r.text}
-        rec = ollama_record(r, {"message": msg})
+        prompt = chat_prompt(body.get("messages") or [], family)
         if body.get("stream", True):
-            return ndjson({"model": model_name, "created_at": rec["created_at"], "message": msg, "done": False},
-                          {**rec, "message": {"role": "assistant", "content": ""}})
-        return rec
+            return streamed(prepare(prompt, n, temp, k, p, mp, seed, stop),
+                            lambda d: json.dumps({"model": model_name, "created_at": now_iso(),
+                                                  "message": {"role": "assistant", "content": d},
+                                                  "done": False}) + "\n",
+                            lambda r: json.dumps(ollama_record(r, {"message": {"role": "assistant", "content": ""}})
+                                                 if r else {"error": "generation failed"}) + "\n",
+                            "application/x-ndjson")
+        r = await run(prompt, n, temp, k, p, mp, seed, stop)
+        return ollama_record(r, {"message": {"role": "assistant", "content": r.text}})
 
     @app.get("/api/tags")
     def ollama_tags():
@@ -398,12 +482,8 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
         return {"prompt_tokens": len(r.prompt_ids), "completion_tokens": len(r.tokens),
                 "total_tokens": len(r.prompt_ids) + len(r.tokens)}
 
-    def sse(chunks: list[dict]):
-        def gen():
-            for c in chunks:
-                yield "data: " + json.dumps(c) + "\n\n"
-            yield "data: [DONE]\n\n"
-        return StreamingResponse(gen(), media_type="text/event-stream")
+    def sse(obj: dict) -> str:
+        return "data: " + json.dumps(obj) + "\n\n"
 
     @app.post("/v1/completions")
     async def oai_completions(body: dict = Body(...)):
@@ -414,13 +494,19 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
             if len(prompt) != 1:
                 raise HTTPException(400, "one prompt per request")
             prompt = prompt[0]
-        r = await run(prompt, body.get("max_tokens", 16), body.get("temperature", 1.0), 0, body.get("top_p", 1.0), 0.0,
+        args = (prompt, body.get("max_tokens", 16), body.get("temperature", 1.0), 0, body.get("top_p", 1.0), 0.0,
                 body.get("seed"), body.get("stop"))
         cid, created = f"cmpl-{uuid.uuid4().hex[:24]}", int(time.time())
-        choice = {"text": r.text, "index": 0, "logprobs": None, "finish_reason": r.finish}
+        head = {"id": cid, "object": "text_completion", "created": created, "model": model_name}
         if body.get("stream"):
-            return sse([{"id": cid, "object": "text_completion", "created": created, "model": model_name,
-                         "choices": [choice]}])
+            return streamed(prepare(*args),
+                            lambda d: sse({**head, "choices": [{"text": d, "index": 0, "logprobs": None,
+                                                                "finish_reason": None}]}),
+                            lambda r: sse({**head, "choices": [{"text": "", "index": 0, "logprobs": None,
+                                                                "finish_reason": r.finish if r else "error"}]}),
+                            "text/event-stream", tail="data: [DONE]\n\n")
+        r = await run(*args)
+        choice = {"text": r.text, "index": 0, "logprobs": None, "finish_reason": r.finish}
         return {"id": cid, "object": "text_completion", "created": created, "model": model_name,
                 "choices": [choice], "usage": oai_usage(r)}
 
@@ -431,15 +517,22 @@ def create_llm_app(engine, tokenizer, model_name: str, context_limit: int, famil
         msgs = body.get("messages")
         if not isinstance(msgs, list) or not msgs:
             raise HTTPException(400, "messages must be a non-empty list")
-        r = await run(chat_prompt(msgs, family), body.get("max_tokens", body.get("max_completion_tokens")),
+        args = (chat_prompt(msgs, family), body.get("max_tokens", body.get("max_completion_tokens")),
                 body.get("temperature", 1.0), 0, body.get("top_p", 1.0), 0.0, body.get("seed"), body.get("stop"))
         cid, created = f"chatcmpl-{uuid.uuid4().hex[:24]}", int(time.time())
+        head = {"id": cid, "object": "chat.completion.chunk", "created": created, "model": model_name}
         if body.get("stream"):
-            return sse([{"id": cid, "object": "chat.completion.chunk", "created": created, "model": model_name,
-                         "choices": [{"index": 0, "delta": {"role": "assistant", "content": r.text},
-                                      "finish_reason": None}]},
-                        {"id": cid, "object": "chat.completion.chunk", "created": created, "model": model_name,
-                         "choices": [{"index": 0, "delta": {}, "finish_reason": r.finish}]}])
+            first = {"sent": False}
+
+            def delta(d):
+                dd = {"content": d} if first["sent"] else {"role": "assistant", "content": d}
+                first["sent"] = True
+                return sse({**head, "choices": [{"index": 0, "delta": dd, "finish_reason": None}]})
+            return streamed(prepare(*args), delta,
+                            lambda r: sse({**head, "choices": [{"index": 0, "delta": {},
+                                                                "finish_reason": r.finish if r else "error"}]}),
+                            "text/event-stream", tail="data: [DONE]\n\n")
+        r = await run(*args)
         return {"id": cid, "object": "chat.completion", "created": created, "model": model_name,
                 "choices": [{"index": 0, "message": {"role": "assistant", "content": r.text},
                              "finish_reason": r.finish}], "usage": oai_usage(r)}

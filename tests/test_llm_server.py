@@ -61,7 +61,8 @@ def _check_apis(app, s, base):
     assert o["done"] is True and o["response"] == r["content"] and o["eval_count"] == len(want)
     lines = [json.loads(x) for x in requests.post(f"{base}/api/generate", json={
         "prompt": prompt, "options": {"num_predict": 12, "temperature": 0}}).text.splitlines()]
-    assert lines[0]["done"] is False and lines[-1]["done"] is True and lines[0]["response"] == r["content"]
+    assert lines[0]["done"] is False and lines[-1]["done"] is True and len(lines) >= 2
+    assert "".join(x["response"] for x in lines) == r["content"]           # deltas add up to the text
     assert requests.get(f"{base}/api/tags").json()["models"][0]["name"] == s.cfg.name
     # OpenAI completions + chat (+ SSE framing)
     c = requests.post(f"{base}/v1/completions", json={"prompt": prompt, "max_tokens": 12, "temperature": 0}).json()
@@ -73,6 +74,12 @@ def _check_apis(app, s, base):
     ev = [x for x in requests.post(f"{base}/v1/chat/completions", json={
         "messages": [{"role": "user", "content": "hi"}], "max_tokens": 4, "stream": True}).text.split("\n\n") if x]
     assert ev[-1] == "data: [DONE]" and json.loads(ev[0][6:])["object"] == "chat.completion.chunk"
+    chunks = [json.loads(x[6:]) for x in ev[:-1]]
+    assert chunks[0]["choices"][0]["delta"]["role"] == "assistant" and chunks[-1]["choices"][0]["finish_reason"]
+    # llama.cpp SSE stream: several deltas while generating, then the final record
+    sse = [json.loads(x[6:]) for x in requests.post(f"{base}/completion", json={
+        "prompt": prompt, "n_predict": 12, "temperature": 0, "stream": True}).text.split("\n\n") if x]
+    assert sse[-1]["stop"] is True and "".join(x["content"] for x in sse) == r["content"]
     # errors
     assert requests.post(f"{base}/completion", json={"prompt": 42}).status_code == 400
     long = requests.post(f"{base}/completion", json={"prompt": "x " * 5000, "n_predict": 4, "temperature": 0}).json()
@@ -139,3 +146,21 @@ def test_server_on_gpu_batches_concurrent_requests():
     finally:
         server.should_exit = True
         t.join(10)
+
+
+def test_stream_cancel_on_disconnect(cpu_stack):
+    """A streaming client that goes away mid-generation frees its slot (the request is cancelled)."""
+    app, s, base = cpu_stack
+    sched = app.state.scheduler
+    with requests.post(f"{base}/completion", json={"prompt": "tell a long story", "n_predict": 60,
+                                                   "temperature": 0, "ignore_eos": True, "stream": True},
+                       stream=True) as resp:
+        for line in resp.iter_lines():
+            if line:
+                break                      # first delta arrived; drop the connection
+    deadline = time.time() + 20
+    while time.time() < deadline and any(ce.pending() for ce in sched.engines.values()):
+        time.sleep(0.05)
+    assert not any(ce.pending() for ce in sched.engines.values())
+    # the server still answers normally afterwards
+    assert requests.post(f"{base}/completion", json={"prompt": "x", "n_predict": 2, "temperature": 0}).status_code == 200
