@@ -388,15 +388,21 @@ class DecoderModel:
     def _layer_pre(self, i, x, residual):
         """Returns normed input of layer i and the residual stream."""
         lw = self.w.layers[i]
+        # fp8 mode: the norm emits the qkv projection's quantised input directly (K.rmsnorm_fp8)
+        norm = K.rmsnorm_fp8 if self.fp8 else K.rmsnorm
         if residual is None:
             residual = x.clone()
-            h = K.rmsnorm(x, lw["attn_norm"], self.cfg.rms_eps)
+            h = norm(x, lw["attn_norm"], self.cfg.rms_eps)
         else:
-            h = K.rmsnorm(x, lw["attn_norm"], self.cfg.rms_eps, residual=residual)
+            h = norm(x, lw["attn_norm"], self.cfg.rms_eps, residual=residual)
         return h, residual
 
     def _mlp(self, i, attn_out, residual):
         lw = self.w.layers[i]
+        if self.fp8:
+            h = K.rmsnorm_fp8(attn_out, lw["mlp_norm"], self.cfg.rms_eps, residual=residual)
+            a = K.silu_mul_fp8(self._lin(i, "gate_up", h), interleaved=self.w.gate_up_interleaved)
+            return self._all_reduce(self._lin(i, "down", a))
         h = K.rmsnorm(attn_out, lw["mlp_norm"], self.cfg.rms_eps, residual=residual)
         gu = self._lin(i, "gate_up", h)
         a = K.silu_mul(gu, interleaved=self.w.gate_up_interleaved)

@@ -39,6 +39,8 @@ _KERNEL_SIGS = {
     "cfc_prefill_attention_fp8": [P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, F, F, P, P],
     "cfc_silu_mul": [P, P, I, I, I, P],
     "cfc_quant_fp8_rows": [P, P, P, I, I, P],
+    "cfc_rmsnorm_fp8": [P, P, P, P, P, I, I, F, I, P],
+    "cfc_silu_mul_fp8": [P, P, P, I, I, I, P],
     "cfc_bias_gelu": [P, P, P, I, I, P],
     "cfc_embedding": [P, P, P, I, I, P],
     "cfc_sample": [P, I, I, F, c_uint32, P, P, P],

@@ -701,14 +701,42 @@ def quant_fp8_weight(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     return (w.float() / s).to(torch.float8_e4m3fn), s.t().contiguous()
 
 
-def linear_fp8(x: torch.Tensor, w8: torch.Tensor, w_scale: torch.Tensor) -> torch.Tensor:
+def rmsnorm_fp8(x: torch.Tensor, w: torch.Tensor, eps: float,
+                residual: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+    """quant_fp8_rows(rmsnorm(x, w, eps, residual)) in one kernel: (x8 [M, K] e4m3fn, scale [M, 1])."""
+    if not x.is_cuda:
+        return ref.quant_fp8_rows(rmsnorm(x, w, eps, residual))
+    _req(x, torch.bfloat16, "x")
+    dim = x.shape[-1]
+    rows = x.numel() // dim
+    out = torch.empty(rows, dim, dtype=torch.float8_e4m3fn, device=x.device)
+    scale = torch.empty(rows, 1, dtype=torch.float32, device=x.device)
+    check(kernels().cfc_rmsnorm_fp8(out.data_ptr(), scale.data_ptr(), _p(residual), x.data_ptr(), w.data_ptr(), rows,
+                                    dim, float(eps), 1 if residual is not None else 0, _stream(x)), "cfc_rmsnorm_fp8")
+    return out, scale
+
+
+def silu_mul_fp8(gu: torch.Tensor, interleaved: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
+    """quant_fp8_rows(silu_mul(gu)) in one kernel: (a8 [T, F] e4m3fn, scale [T, 1])."""
+    if not gu.is_cuda or gu.shape[1] // 2 > 32768:
+        return quant_fp8_rows(silu_mul(gu, interleaved=interleaved))
+    _req(gu, torch.bfloat16, "gu")
+    T, F2 = gu.shape
+    out = torch.empty(T, F2 // 2, dtype=torch.float8_e4m3fn, device=gu.device)
+    scale = torch.empty(T, 1, dtype=torch.float32, device=gu.device)
+    check(kernels().cfc_silu_mul_fp8(out.data_ptr(), scale.data_ptr(), gu.data_ptr(), T, F2 // 2,
+                                     1 if interleaved else 0, _stream(gu)), "cfc_silu_mul_fp8")
+    return out, scale
+
+
+def linear_fp8(x, w8: torch.Tensor, w_scale: torch.Tensor) -> torch.Tensor:
     """W8A8 FP8 linear on the MFMA FP8 path (hipBLASLt through torch._scaled_mm): per-token
     activation scales x per-output-channel weight scales, bf16 out.  ~1.8-1.9x the bf16 GEMM rate
-    at prefill shapes on gfx950 (profiles/fp8_gemm_probe_r02.log)."""
-    if not x.is_cuda:
-        x8, sx = ref.quant_fp8_rows(x)
+    at prefill shapes on gfx950 (profiles/fp8_gemm_probe_r02.log).  ``x`` is a bf16 activation
+    (quantised here) or an already-quantised (x8, scale) pair from rmsnorm_fp8 / silu_mul_fp8."""
+    x8, sx = x if isinstance(x, tuple) else (ref.quant_fp8_rows(x) if not x.is_cuda else quant_fp8_rows(x))
+    if not x8.is_cuda:
         return ((x8.float() * sx) @ (w8.float() * w_scale.t()).T).to(torch.bfloat16)
-    x8, sx = quant_fp8_rows(x)
     return torch._scaled_mm(x8, w8.t(), scale_a=sx, scale_b=w_scale, out_dtype=torch.bfloat16)
 
 

@@ -70,6 +70,18 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
+// Block-wide max, same contract as block_sum.
+__device__ __forceinline__ float block_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = red[0];
+  for (int i = 1; i < nw; ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+
 // XCD-aware bijective remap of a 1-D block id (guide §5 "XCD swizzle must be bijective"):
 // consecutive logical tiles land on the same XCD so neighbouring tiles share that XCD's L2.
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {

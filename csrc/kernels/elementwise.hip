@@ -173,6 +173,49 @@ __global__ void silu_mul_kernel(uint16_t* __restrict__ out, const uint16_t* __re
   reinterpret_cast<uint4*>(out + (size_t)t * F)[c] = pack8(r);
 }
 
+// SwiGLU fused with the per-row FP8 quantisation of its output (the down projection's input in
+// W8A8 mode): one 1024-thread workgroup per row, the row's products held in registers between
+// the amax reduction and the e4m3 conversion.  Values are rounded to bf16 first, so the result
+// equals silu_mul -> quant_fp8_rows bit for bit.  F <= 1024 * 8 * SQ_MAX_VEC.
+constexpr int SQ_MAX_VEC = 4;
+__global__ void __launch_bounds__(1024) silu_mul_fp8_kernel(uint8_t* __restrict__ out, float* __restrict__ scale,
+                                                           const uint16_t* __restrict__ gu, int F, int interleave) {
+  __shared__ float red[16];
+  const int t = blockIdx.x;
+  const uint4* row = reinterpret_cast<const uint4*>(gu + (size_t)t * 2 * F);
+  float r[SQ_MAX_VEC][8];
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < SQ_MAX_VEC; ++i) {
+    const int c = threadIdx.x + i * 1024;
+    if (c < (F >> 3)) {
+      const int gc = interleave ? ((c >> 2) << 3) + (c & 3) : c;
+      const int uc = interleave ? gc + 4 : c + (F >> 3);
+      float a[8], b[8];
+      unpack8(row[gc], a);
+      unpack8(row[uc], b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        r[i][j] = bf2f(f2bf(a[j] / (1.f + __expf(-a[j])) * b[j]));
+        amax = fmaxf(amax, fabsf(r[i][j]));
+      }
+    }
+  }
+  amax = block_max(amax, red);
+  const float s = amax > 0.f ? amax / 448.f : 1.f, rs = 1.f / s;
+  if (threadIdx.x == 0) scale[t] = s;
+  uint2* orow = reinterpret_cast<uint2*>(out + (size_t)t * F);
+#pragma unroll
+  for (int i = 0; i < SQ_MAX_VEC; ++i) {
+    const int c = threadIdx.x + i * 1024;
+    if (c < (F >> 3)) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[i][j] *= rs;
+      orow[c] = pack8_fp8(r[i]);
+    }
+  }
+}
+
 // Per-row (per-token) FP8 quantisation for the W8A8 linear path: scale[r] = max|x[r,:]| / 448,
 // out[r,:] = e4m3fn(x[r,:] / scale[r]) (OCP e4m3 via gfx950's v_cvt_pk_fp8_f32, saturating).
 // One 256-thread workgroup per row; the row stays in registers between the amax pass and the
@@ -604,6 +647,14 @@ CFC_API int cfc_silu_mul(void* out, const void* gu, int T, int F, int interleave
   if (F % 8 != 0 || (interleave && F % 32 != 0) || T > 65535) return -1;
   if (T == 0) return 0;
   silu_mul_kernel<<<dim3((F / 8 + 255) / 256, T), 256, 0, stream>>>((uint16_t*)out, (const uint16_t*)gu, F, interleave);
+  return CFC_CHECK_LAUNCH();
+}
+
+CFC_API int cfc_silu_mul_fp8(void* out, float* scale, const void* gu, int T, int F, int interleave,
+                             hipStream_t stream) {
+  if (F % 8 != 0 || (interleave && F % 32 != 0) || F > 1024 * 8 * SQ_MAX_VEC || T < 0) return -1;
+  if (T == 0) return 0;
+  silu_mul_fp8_kernel<<<T, 1024, 0, stream>>>((uint8_t*)out, scale, (const uint16_t*)gu, F, interleave);
   return CFC_CHECK_LAUNCH();
 }
 

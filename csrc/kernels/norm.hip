@@ -10,8 +10,12 @@
 
 namespace {
 
-template <int VPT>
-__global__ void __launch_bounds__(1024) rmsnorm_kernel(uint16_t* __restrict__ out, uint16_t* __restrict__ residual,
+// F8: out is e4m3fn of the bf16-rounded normalised row divided by a per-row scale
+// (scale[row] = amax / 448) -- the W8A8 projection's activation quantisation fused into the norm
+// that produces it, so the row makes no extra HBM round trip through a bf16 tensor.
+template <int VPT, bool F8>
+__global__ void __launch_bounds__(1024) rmsnorm_kernel(void* __restrict__ out, float* __restrict__ scale,
+                                                      uint16_t* __restrict__ residual,
                                                       const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                       int dim, float eps, int add_residual) {
   __shared__ float red[16];
@@ -43,16 +47,46 @@ __global__ void __launch_bounds__(1024) rmsnorm_kernel(uint16_t* __restrict__ ou
   ss = block_sum(ss, red);
   const float inv = rsqrtf(ss / (float)dim + eps);
   const uint4* wr = reinterpret_cast<const uint4*>(w);
-  uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * dim);
+  if constexpr (!F8) {
+    uint4* orow = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(out) + (size_t)row * dim);
 #pragma unroll
-  for (int i = 0; i < VPT; ++i) {
-    const int c = threadIdx.x + i * blockDim.x;
-    if (c < nvec) {
-      float g[8], o[8];
-      unpack8(wr[c], g);
+    for (int i = 0; i < VPT; ++i) {
+      const int c = threadIdx.x + i * blockDim.x;
+      if (c < nvec) {
+        float g[8], o[8];
+        unpack8(wr[c], g);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = v[i][j] * inv * g[j];
-      orow[c] = pack8(o);
+        for (int j = 0; j < 8; ++j) o[j] = v[i][j] * inv * g[j];
+        orow[c] = pack8(o);
+      }
+    }
+  } else {
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = threadIdx.x + i * blockDim.x;
+      if (c < nvec) {
+        float g[8];
+        unpack8(wr[c], g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          v[i][j] = bf2f(f2bf(v[i][j] * inv * g[j]));   // the bf16 value the unfused norm would store
+          amax = fmaxf(amax, fabsf(v[i][j]));
+        }
+      }
+    }
+    amax = block_max(amax, red);
+    const float s = amax > 0.f ? amax / 448.f : 1.f, rs = 1.f / s;
+    if (threadIdx.x == 0) scale[row] = s;
+    uint2* orow = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(out) + (size_t)row * dim);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = threadIdx.x + i * blockDim.x;
+      if (c < nvec) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] *= rs;
+        orow[c] = pack8_fp8(v[i]);
+      }
     }
   }
 }
@@ -128,6 +162,24 @@ __global__ void __launch_bounds__(1024) layernorm_kernel(uint16_t* __restrict__ 
 // a row is a single load round trip instead of VPT dependent ones (10 us -> ~3 us per call).
 inline int pick_block(int nvec) { return nvec >= 1024 ? 1024 : ((nvec + 63) / 64) * 64; }
 
+template <bool F8>
+int launch_rmsnorm(void* out, float* scale, void* residual, const void* x, const void* w, int rows, int dim, float eps,
+                   int add_residual, hipStream_t stream) {
+  const int nvec = dim / 8, block = pick_block(nvec);
+  const int vpt = (nvec + block - 1) / block;
+  auto r = (uint16_t*)residual;
+  auto xi = (const uint16_t*)x; auto wi = (const uint16_t*)w;
+  switch (vpt) {
+    case 1: rmsnorm_kernel<1, F8><<<rows, block, 0, stream>>>(out, scale, r, xi, wi, dim, eps, add_residual); break;
+    case 2: rmsnorm_kernel<2, F8><<<rows, block, 0, stream>>>(out, scale, r, xi, wi, dim, eps, add_residual); break;
+    case 3: case 4: rmsnorm_kernel<4, F8><<<rows, block, 0, stream>>>(out, scale, r, xi, wi, dim, eps, add_residual); break;
+    case 5: case 6: case 7: case 8:
+      rmsnorm_kernel<8, F8><<<rows, block, 0, stream>>>(out, scale, r, xi, wi, dim, eps, add_residual); break;
+    default: return -2;
+  }
+  return CFC_CHECK_LAUNCH();
+}
+
 }  // namespace
 
 // out = RMSNorm(x [+ residual]) * w.  When add_residual != 0, residual is updated in place to
@@ -135,18 +187,14 @@ inline int pick_block(int nvec) { return nvec >= 1024 ? 1024 : ((nvec + 63) / 64
 CFC_API int cfc_rmsnorm(void* out, void* residual, const void* x, const void* w, int rows, int dim, float eps,
                         int add_residual, hipStream_t stream) {
   if (dim % 8 != 0 || rows <= 0) return -1;
-  const int nvec = dim / 8, block = pick_block(nvec);
-  const int vpt = (nvec + block - 1) / block;
-  auto o = (uint16_t*)out; auto r = (uint16_t*)residual;
-  auto xi = (const uint16_t*)x; auto wi = (const uint16_t*)w;
-  switch (vpt) {
-    case 1: rmsnorm_kernel<1><<<rows, block, 0, stream>>>(o, r, xi, wi, dim, eps, add_residual); break;
-    case 2: rmsnorm_kernel<2><<<rows, block, 0, stream>>>(o, r, xi, wi, dim, eps, add_residual); break;
-    case 3: case 4: rmsnorm_kernel<4><<<rows, block, 0, stream>>>(o, r, xi, wi, dim, eps, add_residual); break;
-    case 5: case 6: case 7: case 8: rmsnorm_kernel<8><<<rows, block, 0, stream>>>(o, r, xi, wi, dim, eps, add_residual); break;
-    default: return -2;
-  }
-  return CFC_CHECK_LAUNCH();
+  return launch_rmsnorm<false>(out, nullptr, residual, x, w, rows, dim, eps, add_residual, stream);
+}
+
+// FP8 output: out [rows, dim] e4m3fn, scale [rows] f32 with RMSNorm(...) ~= out * scale.
+CFC_API int cfc_rmsnorm_fp8(void* out, float* scale, void* residual, const void* x, const void* w, int rows, int dim,
+                            float eps, int add_residual, hipStream_t stream) {
+  if (dim % 8 != 0 || rows <= 0) return -1;
+  return launch_rmsnorm<true>(out, scale, residual, x, w, rows, dim, eps, add_residual, stream);
 }
 
 CFC_API int cfc_layernorm(void* out, const void* x, const void* bias, const void* residual, const void* gamma,

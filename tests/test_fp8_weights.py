@@ -31,6 +31,24 @@ def test_fp8_reference_and_linear_cpu():
     assert y.dtype == torch.bfloat16 and _rel(y, x.float() @ w.float().T) < 0.06
 
 
+def test_fused_quant_ops_cpu():
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(6, 512, generator=g).bfloat16()
+    w = (1 + 0.1 * torch.randn(512, generator=g)).bfloat16()
+    r1, r2 = torch.randn(6, 512, generator=g).bfloat16(), None
+    r2 = r1.clone()
+    x8, s = K.rmsnorm_fp8(x, w, 1e-5, residual=r1)
+    e8, es = ref.quant_fp8_rows(K.rmsnorm(x, w, 1e-5, residual=r2))
+    assert torch.equal(r1, r2) and torch.equal(s, es) and torch.equal(x8.float(), e8.float())
+    gu = torch.randn(6, 2 * 256, generator=g).bfloat16()
+    a8, sa = K.silu_mul_fp8(gu, interleaved=True)
+    b8, sb = ref.quant_fp8_rows(K.silu_mul(gu, interleaved=True))
+    assert torch.equal(sa, sb) and torch.equal(a8.float(), b8.float())
+    wl = torch.randn(64, 512, generator=g).bfloat16()
+    wq, ws = K.quant_fp8_weight(wl)
+    assert torch.equal(K.linear_fp8((x8, s), wq, ws), K.linear_fp8((e8, es), wq, ws))
+
+
 def _models(device, seed=3):
     cfg = get_config("tiny")
     wb = DecoderWeights.random(cfg, device, seed=seed)
@@ -72,6 +90,40 @@ def test_quant_fp8_rows_kernel_matches_reference():
         assert bool((diff <= step + 1e-6).all()) and float((diff > 0).float().mean()) < 0.01
     z8, zs = K.quant_fp8_rows(torch.zeros(2, 64, device="cuda", dtype=torch.bfloat16))
     assert float(zs.min()) == 1.0 and float(z8.float().abs().max()) == 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,dim", [(1, 4096), (128, 4096), (37, 8192), (4, 64), (200, 5120)])
+def test_rmsnorm_fp8_kernel_matches_unfused(rows, dim):
+    g = torch.Generator(device="cuda").manual_seed(rows)
+    x = torch.randn(rows, dim, device="cuda", generator=g).bfloat16()
+    w = (1 + 0.1 * torch.randn(dim, device="cuda", generator=g)).bfloat16()
+    res = torch.randn(rows, dim, device="cuda", generator=g).bfloat16()
+    r1, r2 = res.clone(), res.clone()
+    x8, s = K.rmsnorm_fp8(x, w, 1e-5, residual=r1)
+    e8, es = K.quant_fp8_rows(K.rmsnorm(x, w, 1e-5, residual=r2))
+    assert torch.equal(r1, r2)
+    torch.testing.assert_close(s, es, rtol=1e-6, atol=0)
+    assert float((x8.float() != e8.float()).float().mean()) < 1e-3
+    # and against the fp32 reference of the whole op
+    rn, _ = ref.rmsnorm(x.float(), w.float(), 1e-5, res.float())
+    assert _rel(x8.float() * s, rn) < 0.04
+    n8, ns = K.rmsnorm_fp8(x, w, 1e-5)
+    f8, fs = K.quant_fp8_rows(K.rmsnorm(x, w, 1e-5))
+    torch.testing.assert_close(ns, fs, rtol=1e-6, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,F,inter", [(1, 14336, True), (128, 14336, True), (33, 4096, False), (3, 28672, False)])
+def test_silu_mul_fp8_kernel_matches_unfused(T, F, inter):
+    g = torch.Generator(device="cuda").manual_seed(T + F)
+    gu = (torch.randn(T, 2 * F, device="cuda", generator=g) * 2).bfloat16()
+    a8, s = K.silu_mul_fp8(gu, interleaved=inter)
+    b8, sb = K.quant_fp8_rows(K.silu_mul(gu, interleaved=inter))
+    torch.testing.assert_close(s, sb, rtol=1e-6, atol=0)
+    assert float((a8.float() != b8.float()).float().mean()) < 1e-3
+    want = ref.silu_mul_interleaved(gu.float()) if inter else ref.silu_mul(gu.float())
+    assert _rel(a8.float() * s, want) < 0.04
 
 
 @pytest.mark.gpu
