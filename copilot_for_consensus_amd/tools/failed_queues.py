@@ -89,7 +89,13 @@ class RabbitMQFailedQueues:
         return sorted(QUEUE_MAPPINGS)
 
     def count(self, name):
-        return self.ch.queue_declare(queue=name, passive=True).method.message_count
+        """Ready messages, or None when the queue does not exist.  A passive declare of a missing
+        queue makes the broker close the channel (404), so a fresh one is opened for the next call."""
+        try:
+            return self.ch.queue_declare(queue=name, durable=True, passive=True).method.message_count
+        except Exception:  # noqa: BLE001 -- pika's ChannelClosedByBroker; the SDK is optional
+            self.ch = self.conn.channel()
+            return None
 
     def peek(self, name, limit):
         out, tags = [], []
@@ -117,7 +123,8 @@ class FailedQueueManager:
         self.b = backend
 
     def list_failed_queues(self) -> list[dict[str, Any]]:
-        return [{"queue": n, "message_count": self.b.count(n), "target": QUEUE_MAPPINGS.get(n)} for n in self.b.names()]
+        rows = [{"queue": n, "message_count": self.b.count(n), "target": QUEUE_MAPPINGS.get(n)} for n in self.b.names()]
+        return [r for r in rows if r["message_count"] is not None]     # absent queues skipped, as the reference
 
     def inspect_messages(self, queue: str, limit: int = 10) -> list[dict]:
         return self.b.peek(queue, limit)
