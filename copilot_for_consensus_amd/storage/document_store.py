@@ -437,25 +437,56 @@ class ValidatingDocumentStore(DocumentStore):
 
 
 class MongoDocumentStore(DocumentStore):
-    """MongoDB driver (reference mongo_document_store.py:33); needs ``pymongo``."""
+    """MongoDB driver (reference mongo_document_store.py:33-452); needs ``pymongo``.
+
+    Same contract as the reference's driver: ``connect`` pings the server and authenticates
+    against ``admin`` unless ``authSource`` is given, failures raise DocumentStoreConnectionError;
+    ids that parse as ObjectIds are matched as ObjectIds and every ``_id`` (nested ones in
+    aggregation results too) comes back as a string; results are sanitised of backend fields;
+    ``sort_order`` must be asc / desc; driver errors surface as DocumentStoreError.  The batched
+    helpers run as single server-side operations (insert_many unordered, update_many, delete_many,
+    count_documents) instead of the base class's per-document loops."""
 
     def __init__(self, host="documentdb", port=27017, database="copilot", username=None, password=None,
-                 ensure_indexes=True, **_):
+                 ensure_indexes=True, client_options: dict | None = None, **_):
+        if not host:
+            raise ValueError("MongoDB host is required")
+        if not port:
+            raise ValueError("MongoDB port is required")
+        if not database:
+            raise ValueError("MongoDB database is required")
         try:
             import pymongo  # type: ignore
         except ImportError as e:  # pragma: no cover
-            raise ImportError("DOCUMENT_STORE_TYPE=mongodb needs 'pymongo'; use 'inmemory'") from e
+            raise ImportError("DOCUMENT_STORE_TYPE=mongodb needs 'pymongo'; use 'cfcstore' (native store server) "
+                              "or 'inmemory'") from e
         self._pymongo = pymongo
-        self._args = dict(host=host, port=int(port), username=username, password=password)
+        self.host, self.port, self.username, self.password = host, int(port), username, password
+        self.client_options = dict(client_options or {})
         self._dbname = database
         self.ensure_indexes = ensure_indexes
-        self.db = None
+        self.client = self.db = None
 
     def connect(self):
-        self.client = self._pymongo.MongoClient(**{k: v for k, v in self._args.items() if v is not None})
-        self.db = self.client[self._dbname]
+        params: dict[str, Any] = {"host": self.host, "port": self.port}
+        if self.username and self.password:
+            params.update(username=self.username, password=self.password)
+            params.setdefault("authSource", self.client_options.get("authSource", "admin"))
+        params.update(self.client_options)
+        try:
+            self.client = self._pymongo.MongoClient(**params)
+            self.client.admin.command("ping")
+            self.db = self.client[self._dbname]
+        except Exception as e:  # noqa: BLE001 -- ConnectionFailure, auth errors, DNS: one typed error
+            self.client = self.db = None
+            raise DocumentStoreConnectionError(f"cannot connect to MongoDB at {self.host}:{self.port}: {e}") from e
         if self.ensure_indexes:
             self.ensure_collections()
+
+    def disconnect(self):
+        if self.client is not None:
+            self.client.close()
+        self.client = self.db = None
 
     def ensure_collections(self, config: dict | None = None) -> int:
         """Create the collections and indexes of collections.config.json (what the reference's
@@ -472,38 +503,121 @@ class MongoDocumentStore(DocumentStore):
                 n += 1
         return n
 
+    # -- helpers ---------------------------------------------------------------------------------
     def _c(self, collection):
         if self.db is None:
-            raise DocumentStoreNotConnectedError("call connect() first")
+            raise DocumentStoreNotConnectedError("not connected to MongoDB: call connect() first")
         return self.db[collection]
 
-    def insert_document(self, collection, doc):
+    def _oid_query(self, doc_id) -> dict:
+        """{"_id": ObjectId(doc_id)} when doc_id is a valid ObjectId string, else the raw id."""
         try:
-            return str(self._c(collection).insert_one(dict(doc)).inserted_id)
-        except self._pymongo.errors.DuplicateKeyError as e:
-            raise DocumentAlreadyExistsError(str(e)) from e
+            from bson import ObjectId  # type: ignore  (ships with pymongo)
+            if isinstance(doc_id, str) and ObjectId.is_valid(doc_id):
+                return {"_id": ObjectId(doc_id)}
+        except ImportError:
+            pass
+        return {"_id": doc_id}
+
+    @classmethod
+    def _stringify_ids(cls, obj):
+        """ObjectId -> str, recursively (aggregation results carry nested ids from $lookup)."""
+        if isinstance(obj, dict):
+            for k, v in obj.items():
+                obj[k] = cls._stringify_ids(v)
+            return obj
+        if isinstance(obj, list):
+            return [cls._stringify_ids(v) for v in obj]
+        if type(obj).__name__ == "ObjectId":
+            return str(obj)
+        return obj
+
+    def _out(self, doc):
+        if doc is None:
+            return None
+        if "_id" in doc:
+            doc["_id"] = str(doc["_id"])
+        return sanitize_document(doc)
+
+    def _run(self, what: str, fn):
+        try:
+            return fn()
+        except (DocumentStoreError, ValueError):
+            raise
+        except Exception as e:  # noqa: BLE001 -- pymongo OperationFailure / AutoReconnect / ...
+            if isinstance(e, self._pymongo.errors.DuplicateKeyError):
+                raise DocumentAlreadyExistsError(str(e)) from e
+            raise DocumentStoreError(f"MongoDB {what} failed: {e}") from e
+
+    # -- DocumentStore ---------------------------------------------------------------------------
+    def insert_document(self, collection, doc):
+        c = self._c(collection)
+        return self._run("insert", lambda: str(c.insert_one(dict(doc)).inserted_id))
+
+    def insert_many(self, collection, docs, ignore_duplicates: bool = True):
+        c, docs = self._c(collection), [dict(d) for d in docs]
+        if not docs:
+            return []
+        try:
+            res = c.insert_many(docs, ordered=False)
+            return [str(i) for i in res.inserted_ids]
+        except self._pymongo.errors.BulkWriteError as e:
+            errs = e.details.get("writeErrors", [])
+            if any(w.get("code") != 11000 for w in errs):       # 11000 = duplicate key
+                raise DocumentStoreError(f"MongoDB insert_many failed: {e}") from e
+            if not ignore_duplicates:
+                raise DocumentAlreadyExistsError(str(e)) from e
+            failed = {w["index"] for w in errs}
+            return [str(d["_id"]) for i, d in enumerate(docs) if i not in failed]
 
     def get_document(self, collection, doc_id):
-        return self._c(collection).find_one({"_id": doc_id})
+        c = self._c(collection)
+        return self._out(self._run("get", lambda: c.find_one(self._oid_query(doc_id))))
 
     def query_documents(self, collection, filter_dict=None, limit=100, sort_by=None, sort_order="desc", skip=0):
-        cur = self._c(collection).find(filter_dict or {})
-        if sort_by:
-            cur = cur.sort(sort_by, -1 if sort_order == "desc" else 1)
-        cur = cur.skip(skip)
-        return list(cur.limit(limit) if limit else cur)
+        if sort_order not in ("asc", "desc"):
+            raise DocumentStoreError(f"Invalid sort_order {sort_order!r}: must be 'asc' or 'desc'")
+        c = self._c(collection)
+
+        def run():
+            cur = c.find(filter_dict or {})
+            if sort_by:
+                cur = cur.sort(sort_by, self._pymongo.DESCENDING if sort_order == "desc" else self._pymongo.ASCENDING)
+            if skip:
+                cur = cur.skip(int(skip))
+            if limit:
+                cur = cur.limit(int(limit))
+            return [self._out(d) for d in cur]
+        return self._run("query", run)
+
+    def count_documents(self, collection, filter_dict=None):
+        c = self._c(collection)
+        return int(self._run("count", lambda: c.count_documents(filter_dict or {})))
 
     def update_document(self, collection, doc_id, patch):
+        c = self._c(collection)
         upd = patch if any(k.startswith("$") for k in patch) else {"$set": patch}
-        if self._c(collection).update_one({"_id": doc_id}, upd).matched_count == 0:
-            raise DocumentNotFoundError(doc_id)
+        if self._run("update", lambda: c.update_one(self._oid_query(doc_id), upd)).matched_count == 0:
+            raise DocumentNotFoundError(f"document {doc_id} not found in {collection}")
+
+    def update_many(self, collection, filter_dict, patch):
+        c = self._c(collection)
+        upd = patch if any(k.startswith("$") for k in patch) else {"$set": patch}
+        return int(self._run("update_many", lambda: c.update_many(filter_dict, upd)).modified_count)
 
     def delete_document(self, collection, doc_id):
-        if self._c(collection).delete_one({"_id": doc_id}).deleted_count == 0:
-            raise DocumentNotFoundError(doc_id)
+        c = self._c(collection)
+        if self._run("delete", lambda: c.delete_one(self._oid_query(doc_id))).deleted_count == 0:
+            raise DocumentNotFoundError(f"document {doc_id} not found in {collection}")
+
+    def delete_many(self, collection, filter_dict):
+        c = self._c(collection)
+        return int(self._run("delete_many", lambda: c.delete_many(filter_dict)).deleted_count)
 
     def aggregate_documents(self, collection, pipeline):
-        return list(self._c(collection).aggregate(pipeline))
+        c = self._c(collection)
+        docs = self._run("aggregate", lambda: list(c.aggregate(pipeline)))
+        return [sanitize_document(self._stringify_ids(d)) for d in docs]
 
 
 def create_document_store(cfg=None, enable_validation: bool = False, strict: bool = True) -> DocumentStore:

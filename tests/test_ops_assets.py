@@ -5,10 +5,9 @@ from __future__ import annotations
 
 import json
 import re
-import sys
-import types
 from pathlib import Path
 
+import pytest
 import yaml
 
 from copilot_for_consensus_amd.contracts.documents import collections_config
@@ -101,40 +100,20 @@ def test_mongo_init_and_store_indexes():
         assert f'"name": "{c["name"]}"' in js
         for i in c.get("indexes", []):
             assert i["options"]["name"] in js
-    # MongoDocumentStore.ensure_collections against a stand-in pymongo
-    calls = []
-
-    class Coll:
-        def __init__(self, n):
-            self.n = n
-
-        def create_index(self, keys, **opt):
-            calls.append((self.n, tuple(keys), opt.get("name"), opt.get("unique", False)))
-
-    class DB(dict):
-        def list_collection_names(self):
-            return ["messages"]
-
-        def create_collection(self, n):
-            calls.append(("create", n))
-
-        def __getitem__(self, n):
-            return Coll(n)
-
-    fake = types.ModuleType("pymongo")
-    fake.MongoClient = lambda **kw: {"copilot": DB()}
-    fake.errors = types.SimpleNamespace(DuplicateKeyError=KeyError)
-    sys.modules["pymongo"] = fake
+    # MongoDocumentStore.ensure_collections against the stand-in pymongo (tests/fake_pymongo.py)
+    import fake_pymongo
+    mp = pytest.MonkeyPatch()
     try:
+        server = fake_pymongo.install(mp)
+        server.dbs["copilot"] = {"messages": fake_pymongo._CollData()}
         from copilot_for_consensus_amd.storage.document_store import MongoDocumentStore
         st = MongoDocumentStore(host="h")
         st.connect()
+        assert st.ensure_collections() == sum(len(c.get("indexes", [])) for c in cfg["collections"])
     finally:
-        del sys.modules["pymongo"]
-    created = {c[1] for c in calls if c[0] == "create"}
-    assert "messages" not in created and "archives" in created
-    assert ("sources", (("name", 1),), "name_idx", True) in calls
-    assert sum(1 for c in calls if c[0] != "create") == sum(len(c.get("indexes", [])) for c in cfg["collections"])
+        mp.undo()
+    assert {c["name"] for c in cfg["collections"]} <= set(server.dbs["copilot"])
+    assert "name" in server.dbs["copilot"]["sources"].unique
 
 
 def test_k8s_manifests():
