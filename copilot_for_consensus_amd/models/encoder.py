@@ -54,6 +54,20 @@ ENCODER_PRESETS = {
 }
 
 
+def encoder_config_from_hf(config_json, name: str | None = None, **over) -> EncoderConfig:
+    """EncoderConfig from an HF BertConfig ``config.json`` (BERT / MiniLM / BGE checkpoints)."""
+    import json
+    c = json.loads(Path(config_json).read_text())
+    if c.get("model_type", "bert") not in ("bert", "xlm-roberta", "roberta") and "hidden_size" not in c:
+        raise ValueError(f"{config_json}: not a BERT-family config")
+    kw = dict(vocab_size=int(c["vocab_size"]), hidden=int(c["hidden_size"]), layers=int(c["num_hidden_layers"]),
+              heads=int(c["num_attention_heads"]), ffn=int(c["intermediate_size"]),
+              max_positions=int(c.get("max_position_embeddings", 512)), ln_eps=float(c.get("layer_norm_eps", 1e-12)),
+              max_seq_length=min(512, int(c.get("max_position_embeddings", 512))))
+    kw.update(over)
+    return EncoderConfig(name or Path(config_json).parent.name, **kw)
+
+
 def get_encoder_config(name) -> EncoderConfig:
     if isinstance(name, EncoderConfig):
         return name
