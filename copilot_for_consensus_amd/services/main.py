@@ -76,14 +76,8 @@ def main(argv=None) -> int:
         return 1
     if args.service == "node":
         import uvicorn
-        from .ingestion import ingestion_routes
-        from .reporting import reporting_routes
         node.start(threaded=True)
-        from ..ui import ui_routes
-        app = create_app(node.services["reporting"], extra_routes=reporting_routes)
-        ingestion_routes(app, node.services["ingestion"], None)
-        ui_routes(app)
-        uvicorn.run(app, host="0.0.0.0", port=args.port or 8080)
+        uvicorn.run(node.http_app(), host="0.0.0.0", port=args.port or 8080)
         node.stop()
         return 0
     svc = node.services[args.service]
@@ -96,7 +90,7 @@ def main(argv=None) -> int:
     app = create_app(svc, extra_routes=extra, auth_dependency=_auth_dep(cfg))
     if args.service == "reporting":
         from ..ui import ui_routes
-        ui_routes(app)
+        ui_routes(app, bases={"reporting": ""})       # its own API at the root; ingestion / auth via the gateway
     run_service(svc, app, cfg.http_host, args.port or cfg.http_port)
     return 0
 

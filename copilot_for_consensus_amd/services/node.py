@@ -141,6 +141,23 @@ class Node:
         for t in self._threads:
             t.join(timeout=5)
 
+    def http_app(self, auth_base: str = "/auth"):
+        """The all-in-one HTTP front in the gateway's layout (deploy/gateway/nginx.conf):
+        ``/reporting/...`` and ``/ingestion/...`` are the two services' APIs (both define
+        ``/api/sources`` -- thread-source names vs the ingestion source records -- so they cannot
+        share one path space), ``/ui`` the web UI wired to those prefixes.  The reporting API also
+        answers at the root for clients of a single reporting service."""
+        from ..ui import ui_routes
+        from .base import create_app
+        from .ingestion import ingestion_routes
+        from .reporting import reporting_routes
+        root = create_app(self.services["reporting"], extra_routes=reporting_routes)
+        root.mount("/reporting", create_app(self.services["reporting"], extra_routes=reporting_routes))
+        if "ingestion" in self.services:
+            root.mount("/ingestion", create_app(self.services["ingestion"], extra_routes=ingestion_routes))
+        ui_routes(root, bases={"reporting": "/reporting", "ingestion": "/ingestion", "auth": auth_base})
+        return root
+
     def drain(self, max_rounds: int = 1000) -> int:
         """Synchronous mode: process queued events stage by stage until the bus is quiet."""
         total = 0

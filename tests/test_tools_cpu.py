@@ -3,6 +3,8 @@ gateway generation, StartupRequeue."""
 import json
 from datetime import datetime, timedelta, timezone
 
+import pytest
+
 from copilot_for_consensus_amd.bus import InProcBroker, InProcPublisher, InProcSubscriber, NoopPublisher
 from copilot_for_consensus_amd.contracts.registry import default_provider
 from copilot_for_consensus_amd.observability import PrometheusMetricsCollector
@@ -159,7 +161,28 @@ def test_ui_served():
     for route in ("async login()", "async callback(q)", "async admin(q)", "/admin/role-assignments/pending",
                   "/admin/users/search"):
         assert route in r.text, route
+    # ReportsList / DiscussionsList filters + paging, MessageDetail chunks, UserRolesList
+    for needle in ("message_start_date", "max_participants", "sort_order", "thread_start_date", "first_message_date",
+                   "/api/chunks?message_doc_id=", "/roles`", "function pager"):
+        assert needle in r.text, needle
     assert c.get("/", follow_redirects=False).status_code in (302, 307)
+
+
+def test_ui_script_parses(tmp_path):
+    """The page's script is valid JavaScript (node --check; ``??`` rewritten for old node versions)."""
+    import re
+    import shutil
+    import subprocess
+    node = shutil.which("node")
+    if node is None:
+        pytest.skip("node not installed")
+    from copilot_for_consensus_amd.ui import INDEX
+    html = INDEX.read_text(encoding="utf-8")
+    js = re.search(r"<script>(.*)</script>", html, re.S).group(1).replace("??", "||")
+    f = tmp_path / "ui.js"
+    f.write_text(js)
+    r = subprocess.run([node, "--check", str(f)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
 
 
 def test_deploy_artifacts(tmp_path):
