@@ -134,8 +134,10 @@ class AzureServiceBusSubscriber(EventSubscriber):
 class AzureCosmosDocumentStore:
     """DocumentStore over Cosmos DB (NoSQL API); Mongo-style filters translated to a SQL subset."""
 
-    def __init__(self, endpoint: str, key: str | None = None, database: str = "copilot",
+    def __init__(self, endpoint: str | None = None, key: str | None = None, database: str = "copilot",
                  use_managed_identity: bool = False, partition_key: str = "/id", **_):
+        if not endpoint:
+            raise ValueError("azure_cosmosdb document store: endpoint is required (COSMOS_ENDPOINT)")
         cosmos = _need("azure.cosmos", "azure-cosmos")
         self._cosmos = cosmos
         cred = key if key else _credential(True)
@@ -288,7 +290,11 @@ class AzureBlobArchiveStore:
 # ----------------------------------------------------------------------------- Key Vault
 
 class AzureKeyVaultSecretProvider:
-    def __init__(self, vault_url: str, **_):
+    def __init__(self, vault_url: str | None = None, vault_name: str | None = None, **_):
+        vault_url = vault_url or (f"https://{vault_name}.vault.azure.net" if vault_name else None)
+        if not vault_url:
+            raise ValueError("azure_key_vault secret provider: vault_url (AZURE_KEY_VAULT_URI) or vault_name "
+                             "(AZURE_KEY_VAULT_NAME) is required")
         sec = _need("azure.keyvault.secrets", "azure-keyvault-secrets")
         self.client = sec.SecretClient(vault_url=vault_url, credential=_credential(True))
 
@@ -349,7 +355,11 @@ class KeyVaultJWTSigner:
 class AzureMonitorMetricsCollector:
     """OpenTelemetry metrics exported to Azure Monitor (counters / histograms / observable gauges)."""
 
-    def __init__(self, connection_string: str, namespace: str = "copilot", export_interval_ms: int = 60000, **_):
+    def __init__(self, connection_string: str | None = None, namespace: str = "copilot", export_interval_ms: int = 60000,
+                 **_):
+        if not connection_string:
+            raise ValueError("azure_monitor metrics: connection_string is required "
+                             "(the Application Insights connection string, a secret)")
         otel = _need("opentelemetry.metrics", "opentelemetry-api")
         sdk = _need("opentelemetry.sdk.metrics", "opentelemetry-sdk")
         reader_mod = _need("opentelemetry.sdk.metrics.export", "opentelemetry-sdk")

@@ -128,8 +128,10 @@ class QdrantVectorStore(VectorStore):
 class AzureAISearchVectorStore(VectorStore):
     API = "2023-11-01"
 
-    def __init__(self, endpoint: str, api_key: str, index_name: str = "embeddings", vector_size: int = 384,
-                 transport: Callable | None = None, batch: int = 1000, **_):
+    def __init__(self, endpoint: str | None = None, api_key: str | None = None, index_name: str = "embeddings",
+                 vector_size: int = 384, transport: Callable | None = None, batch: int = 1000, **_):
+        if not endpoint or not api_key:
+            raise ValueError("azure_ai_search vector store: endpoint (AZURE_SEARCH_ENDPOINT) and api_key are required")
         self.index, self.dim, self.batch = index_name, int(vector_size), batch
         self.http = _Http(endpoint, {"api-key": api_key}, transport=transport)
         self._ensure_index()
