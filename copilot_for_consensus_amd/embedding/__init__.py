@@ -101,8 +101,8 @@ class HipEncoderProvider(EmbeddingProvider):
         """[n, dim] fp32 embeddings (L2-normalised unless configured otherwise), on the encoder's device."""
         for t in texts:
             _check_text(t)
-        ids = self.tokenizer.encode_batch(texts)
-        return self.model.encode_ids(ids, max_tokens_per_forward=self.max_tokens_per_forward)
+        ids, cu = self.tokenizer.encode_packed(texts)
+        return self.model.encode_packed(ids, cu, max_tokens_per_forward=self.max_tokens_per_forward)
 
     def embed_batch(self, texts: list[str]) -> list[list[float]]:
         return self.embed_tensor(texts).cpu().tolist()

@@ -164,30 +164,43 @@ class EncoderModel:
     def encode_ids(self, batch: list[list[int]], pooling: str | None = None, normalize: bool | None = None,
                    max_tokens_per_forward: int = 65536) -> torch.Tensor:
         """Sentence embeddings [n, H] fp32 for pre-tokenised sequences (truncated to max_seq_length)."""
+        import numpy as np
+        seqs = [s[:self.cfg.max_seq_length] for s in batch]
+        cu = np.zeros(len(seqs) + 1, dtype=np.int32)
+        np.cumsum([len(s) for s in seqs], out=cu[1:])
+        ids = np.fromiter((t for s in seqs for t in s), dtype=np.int32, count=int(cu[-1]))
+        return self.encode_packed(ids, cu, pooling, normalize, max_tokens_per_forward)
+
+    @torch.inference_mode()
+    def encode_packed(self, ids, cu_seqlens, pooling: str | None = None, normalize: bool | None = None,
+                      max_tokens_per_forward: int = 65536) -> torch.Tensor:
+        """Sentence embeddings [n, H] fp32 for sequences already packed (numpy int32 ``ids`` [T],
+        ``cu_seqlens`` [n+1], each at most max_seq_length long): positions, forward groups and the
+        device copies are built with array operations, no per-token Python."""
+        import numpy as np
         c = self.cfg
         pooling = pooling or c.pooling
         normalize = c.normalize if normalize is None else normalize
-        seqs = [s[:c.max_seq_length] for s in batch]
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        cu = np.ascontiguousarray(cu_seqlens, dtype=np.int64)
+        lens = np.diff(cu)
+        if len(lens) and int(lens.max()) > c.max_seq_length:
+            raise ValueError(f"sequence of {int(lens.max())} tokens > max_seq_length {c.max_seq_length}")
+        pos_all = (np.arange(int(cu[-1]), dtype=np.int64) - np.repeat(cu[:-1], lens)).astype(np.int32)
+        dev = self.device
         outs = []
-        i = 0
-        while i < len(seqs):
-            j, tok = i, 0
-            while j < len(seqs) and (tok + len(seqs[j]) <= max_tokens_per_forward or j == i):
-                tok += len(seqs[j])
-                j += 1
-            part = seqs[i:j]
-            ids = [t for s in part for t in s]
-            pos = [p for s in part for p in range(len(s))]
-            cu = [0]
-            for s in part:
-                cu.append(cu[-1] + len(s))
-            dev = self.device
-            cu_t = torch.tensor(cu, dtype=torch.int32, device=dev)
-            seq_t, q0_t = K.prefill_tiles(cu, K.ENCODER_TILE_ROWS)
+        i, n = 0, len(lens)
+        while i < n:
+            # as many whole sequences as fit in max_tokens_per_forward (at least one)
+            j = int(np.searchsorted(cu, cu[i] + max_tokens_per_forward, side="right")) - 1
+            j = min(max(j, i + 1), n)
+            t0, t1 = int(cu[i]), int(cu[j])
+            cu_part = (cu[i:j + 1] - t0).astype(np.int32)
+            seq_t, q0_t = K.prefill_tiles(cu_part.tolist(), K.ENCODER_TILE_ROWS)
             tiles = (torch.tensor(seq_t, dtype=torch.int32, device=dev), torch.tensor(q0_t, dtype=torch.int32, device=dev))
-            h = self.forward_packed(torch.tensor(ids, dtype=torch.int32, device=dev),
-                                    torch.tensor(pos, dtype=torch.int32, device=dev), cu_t,
-                                    max(len(s) for s in part), tiles=tiles)
+            cu_t = torch.from_numpy(cu_part).to(dev)
+            h = self.forward_packed(torch.from_numpy(ids[t0:t1]).to(dev), torch.from_numpy(pos_all[t0:t1]).to(dev),
+                                    cu_t, int(lens[i:j].max()), tiles=tiles)
             outs.append(K.pool(h, cu_t, pooling, normalize))
             i = j
         return torch.cat(outs, 0)

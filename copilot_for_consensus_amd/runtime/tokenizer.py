@@ -39,9 +39,8 @@ def _c(s: str) -> tuple[bytes, int]:
 ENCODE_THREADS = max(1, min(16, int(os.environ.get("CFC_TOKENIZER_THREADS", "0")) or (os.cpu_count() or 1)))
 
 
-def _batch(fn, handle, texts: list[str], cap: int, truncate: bool = False) -> list[list[int] | None]:
-    """Thread-parallel C++ encode of many texts.  Results longer than ``cap`` come back as None
-    (caller re-encodes them singly) unless ``truncate``, which keeps their first ``cap`` ids."""
+def _batch_raw(fn, handle, texts: list[str], cap: int) -> tuple[np.ndarray, np.ndarray]:
+    """Thread-parallel C++ encode of many texts: (ids [n, cap] int32, full lengths [n] int32)."""
     bs = [t.encode("utf-8") for t in texts]
     offs = np.zeros(len(bs) + 1, dtype=np.int64)
     np.cumsum([len(b) for b in bs], out=offs[1:])
@@ -50,7 +49,14 @@ def _batch(fn, handle, texts: list[str], cap: int, truncate: bool = False) -> li
     lens = np.empty(len(bs), dtype=np.int32)
     fn(handle, buf, offs.ctypes.data, len(bs), cap, out.ctypes.data, lens.ctypes.data,
        min(ENCODE_THREADS, max(1, len(bs) // 4)))
-    return [out[i, :min(lens[i], cap)].tolist() if (truncate or lens[i] <= cap) else None for i in range(len(bs))]
+    return out, lens
+
+
+def _batch(fn, handle, texts: list[str], cap: int, truncate: bool = False) -> list[list[int] | None]:
+    """As _batch_raw, as lists.  Results longer than ``cap`` come back as None (caller re-encodes
+    them singly) unless ``truncate``, which keeps their first ``cap`` ids."""
+    out, lens = _batch_raw(fn, handle, texts, cap)
+    return [out[i, :min(lens[i], cap)].tolist() if (truncate or lens[i] <= cap) else None for i in range(len(texts))]
 
 
 class BPETokenizer:
@@ -445,6 +451,24 @@ class WordPieceTokenizer:
         texts = [bert_normalize(t, self.lowercase) for t in texts]
         res = _batch(self._lib.cfc_wp_encode_batch, self._h, texts, max(1, L - 2), truncate=True)
         return [[self.cls_id] + ids + [self.sep_id] for ids in res]
+
+    def encode_packed(self, texts: list[str], max_length: int | None = None) -> tuple[np.ndarray, np.ndarray]:
+        """encode_batch as the encoder consumes it, with no per-token Python work: every text's
+        [CLS] pieces [SEP] concatenated (ids int32 [T]) and the boundaries (cu_seqlens int32 [n+1])."""
+        L = max_length or self.max_length
+        cap = max(1, L - 2)
+        texts = [bert_normalize(t, self.lowercase) for t in texts]
+        out, lens = _batch_raw(self._lib.cfc_wp_encode_batch, self._h, texts, cap)
+        lens = np.minimum(lens, cap)
+        cu = np.zeros(len(texts) + 1, dtype=np.int32)
+        np.cumsum(lens + 2, out=cu[1:])
+        ids = np.empty(int(cu[-1]), dtype=np.int32)
+        ids[cu[:-1]] = self.cls_id
+        ids[cu[1:] - 1] = self.sep_id
+        body = np.arange(cap, dtype=np.int32)[None, :]
+        mask = body < lens[:, None]
+        ids[((cu[:-1] + 1)[:, None] + body)[mask]] = out[mask]
+        return ids, cu
 
     @classmethod
     def from_vocab_txt(cls, path, **kw) -> "WordPieceTokenizer":

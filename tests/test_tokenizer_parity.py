@@ -86,6 +86,12 @@ def test_wordpiece_matches_hf(wordpiece, corpus):
         assert got == want, (t, [mine.vocab[i] for i in want], [mine.vocab[i] for i in got])
     batch = mine.encode_batch(CASES)
     assert [b[1:-1] for b in batch] == [ref.encode(t).ids for t in CASES]
+    # the packed form the encoder consumes: same ids, concatenated, with cu_seqlens; truncation too
+    for L in (100000, 7):
+        ids, cu = mine.encode_packed(CASES + corpus[:5], max_length=L)
+        want = mine.encode_batch(CASES + corpus[:5], max_length=L)
+        assert cu.tolist() == [0] + list(__import__("itertools").accumulate(len(w) for w in want))
+        assert ids.tolist() == [t for w in want for t in w]
 
 
 @pytest.mark.parametrize("which", ["sp_metaspace", "sp_legacy"])
