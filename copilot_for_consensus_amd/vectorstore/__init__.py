@@ -74,6 +74,8 @@ def _as_matrix(vectors, dim: int | None, device=None, dtype=torch.float32) -> to
         t = torch.as_tensor(np.asarray(vectors, dtype=np.float32))
     if t.dim() == 1:
         t = t[None]
+    if t.dim() != 2 or t.shape[1] == 0:
+        raise ValueError(f"expected non-empty vectors, got shape {tuple(t.shape)}")
     if dim is not None and t.shape[1] != dim:
         raise ValueError(f"vector dimension {t.shape[1]} != index dimension {dim}")
     return t.to(device=device, dtype=dtype) if device is not None else t.to(dtype)
@@ -83,6 +85,8 @@ class InMemoryVectorStore(VectorStore):
     """numpy cosine store (reference semantics, but upsert-correct)."""
 
     def __init__(self, dimension: int | None = None, **_):
+        if dimension is not None and int(dimension) <= 0:
+            raise ValueError(f"dimension must be positive, got {dimension}")
         self.dim = dimension
         self._ids: list[str] = []
         self._row: dict[str, int] = {}
@@ -147,6 +151,8 @@ class HipFlatIndex(VectorStore):
                  faiss_scores: bool = False, **_):
         if distance not in ("cosine", "dot", "l2", "euclid"):
             raise ValueError(f"unknown distance {distance!r}")
+        if int(dimension) <= 0:
+            raise ValueError(f"dimension must be positive, got {dimension}")
         self.dim = int(dimension)
         self.metric = "l2" if distance in ("l2", "euclid") else distance
         self.faiss_scores = faiss_scores
@@ -171,10 +177,12 @@ class HipFlatIndex(VectorStore):
         X = torch.zeros(cap, self.dim, dtype=torch.bfloat16, device=self.device)
         n2 = torch.zeros(cap, dtype=torch.float32, device=self.device)
         al = torch.zeros(cap, dtype=torch.bool, device=self.device)
-        if self._n:
-            X[:self._n] = self._X[:self._n]
-            n2[:self._n] = self._norm2[:self._n]
-            al[:self._n] = self._alive[:self._n]
+        # rows already written (add_embeddings counts new rows in _n before it reserves them)
+        k = min(self._n, self._cap)
+        if k:
+            X[:k] = self._X[:k]
+            n2[:k] = self._norm2[:k]
+            al[:k] = self._alive[:k]
         self._X, self._norm2, self._alive, self._cap = X, n2, al, cap
 
     def _prepare(self, vecs: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
@@ -425,6 +433,8 @@ def create_vector_store(cfg=None, **overrides) -> VectorStore:
     name = getattr(cfg, "driver_name", cfg) or "hip"
     kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
     kw.update(overrides)
+    if kw.get("index_type", "flat") not in ("flat", "ivf"):
+        raise ValueError(f"unknown index_type {kw['index_type']!r} (flat or ivf)")
     if name == "hip":
         if kw.get("index_type", "flat") == "ivf":
             return HipIVFIndex(**kw)
