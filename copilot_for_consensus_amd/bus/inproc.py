@@ -19,6 +19,7 @@ from typing import Any
 
 from ..contracts.events import EXCHANGE, ROUTING_KEYS
 from .base import Callback, EventPublisher, EventSubscriber, topic_matches
+from .validating import EventValidationError
 
 
 class _Queue:
@@ -140,9 +141,11 @@ class InProcSubscriber(EventSubscriber):
         try:
             cb(copy.deepcopy(event))
             self.processed += 1
-        except Exception:
+        except Exception as e:
             self.failed += 1
-            if redeliveries + 1 >= self.broker.max_redeliveries:
+            # a schema-invalid event fails the same way on every delivery: dead-letter it at once
+            poison = isinstance(e, EventValidationError)
+            if poison or redeliveries + 1 >= self.broker.max_redeliveries:
                 self.broker.dead_letters[self.queue_name].append(event)
             else:
                 with self.queue.cv:  # nack + requeue at the tail

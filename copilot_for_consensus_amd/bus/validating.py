@@ -3,10 +3,13 @@ validating_subscriber.py:30): every published / received event is checked agains
 JSON Schema of its type; invalid events raise (publish) or are rejected before the callback."""
 from __future__ import annotations
 
+import logging
 from typing import Any
 
 from ..contracts.registry import SchemaProvider, default_provider
 from .base import Callback, EventPublisher, EventSubscriber
+
+log = logging.getLogger(__name__)
 
 
 class EventValidationError(ValueError):
@@ -49,9 +52,14 @@ class ValidatingEventSubscriber(EventSubscriber):
                   exchange: str | None = None) -> None:
         def wrapper(event: dict[str, Any]) -> None:
             errs = self._schemas.validate_event(event)
-            if errs and self.strict:
+            if errs:
+                # strict: raise (the transport dead-letters it); non-strict: log and skip the
+                # callback (reference validating_subscriber.py wrapper)
                 self.rejected.append((event, errs))
-                raise EventValidationError(event_type, errs)
+                if self.strict:
+                    raise EventValidationError(event_type, errs)
+                log.warning("skipping invalid %s event: %s", event_type, "; ".join(errs[:3]))
+                return
             callback(event)
 
         self._inner.subscribe(event_type, wrapper, routing_key=routing_key, exchange=exchange)
