@@ -262,6 +262,9 @@ class SourceConfig:
             raise ValueError(f"source_type must be one of {SOURCE_TYPES}, got {self.source_type!r}")
         if not self.name or not self.url:
             raise ValueError("source name and url are required")
+        # the name becomes a directory under the archive store's base path: no path components
+        if any(c in str(self.name) for c in "/\\\0") or str(self.name).strip() in (".", ".."):
+            raise ValueError(f"invalid source name {self.name!r}: no path separators, '.' or '..'")
 
     @classmethod
     def from_mapping(cls, m: Mapping[str, Any]) -> "SourceConfig":

@@ -141,8 +141,15 @@ def create_app(service: BaseService, extra_routes: Callable | None = None, confi
     def health():
         # a bus-driven service whose consumer thread died is unhealthy (reference reporting/main.py:79-103)
         alive = service.consumer_alive()
-        return {"status": "unhealthy" if alive is False else "healthy", "service": service.name,
-                "events_processed": service.stats["events_processed"], "subscriber_thread_alive": alive}
+        out = {"status": "unhealthy" if alive is False else "healthy", "service": service.name,
+               "events_processed": service.stats["events_processed"], "subscriber_thread_alive": alive}
+        sched = getattr(service, "scheduler", None)
+        if service.name == "ingestion":   # reference ingestion/main.py health(): scheduler + source counts
+            srcs = service.list_sources()
+            out.update(scheduler_running=bool(sched and sched.is_running), sources_configured=len(srcs),
+                       sources_enabled=sum(1 for x in srcs if x.get("enabled", True)),
+                       total_files_ingested=service.stats.get("files_ingested", 0))
+        return out
 
     @app.get("/readyz")
     def readyz():

@@ -57,6 +57,7 @@ class IngestionService(BaseService):
                 path = None
         self.storage_path = path or Path(tempfile.mkdtemp(prefix="cfc-ingest-"))
         self.max_retries = max_retries
+        self.scheduler: "IngestionScheduler | None" = None   # set by the node when it runs threaded
         self.stats.update(files_ingested=0, files_skipped=0, files_failed=0)
 
     # ------------------------------------------------------------------ sources
@@ -195,8 +196,19 @@ class IngestionService(BaseService):
         """Drop the source's ``archives`` records (not the stored bytes); returns how many."""
         return self.store.delete_many("archives", {"source": name})
 
-    def ingest_all_enabled_sources(self) -> dict[str, list[str]]:
-        return {s["name"]: self.ingest_archive(s) for s in self.list_sources(enabled_only=True)}
+    def ingest_all_enabled_sources(self) -> dict[str, list[str] | Exception]:
+        """Ingest every enabled source; one source's failure (bad stored config, store error) is
+        returned in its slot and does not stop the others (reference service.py:1044)."""
+        out: dict[str, list[str] | Exception] = {}
+        for s in self.list_sources(enabled_only=True):
+            try:
+                out[s["name"]] = self.ingest_archive(s)
+            except Exception as e:  # noqa: BLE001 - isolated per source, reported
+                self.stats["files_failed"] += 1
+                self.log.error("source ingestion failed", source=s.get("name"), error=repr(e))
+                self.errors.report(e, context={"source": s.get("name")})
+                out[s["name"]] = e
+        return out
 
     def upload(self, filename: str, content: bytes) -> dict:
         name = sanitize_filename(filename)
@@ -231,20 +243,37 @@ class IngestionScheduler:
         self.service, self.interval = service, interval_seconds
         self._stop = threading.Event()
         self._thread: threading.Thread | None = None
+        self.runs = 0
 
-    def start(self):
+    @property
+    def is_running(self) -> bool:
+        return self._thread is not None and self._thread.is_alive()
+
+    def start(self) -> bool:
+        """Start the loop; False (and nothing started) if it is already running."""
+        if self.is_running:
+            return False
+        self._stop.clear()
+
         def loop():
             while not self._stop.is_set():
                 try:
                     self.service.ingest_all_enabled_sources()
                 except Exception as e:
                     self.service.log.error("scheduled ingestion failed", error=repr(e))
+                self.runs += 1
                 self._stop.wait(self.interval)
         self._thread = threading.Thread(target=loop, name="ingestion-scheduler", daemon=True)
         self._thread.start()
+        return True
 
-    def stop(self):
+    def stop(self, timeout: float | None = 5.0) -> bool:
+        """Stop the loop and wait for it; False if it was not running."""
+        if not self.is_running:
+            return False
         self._stop.set()
+        self._thread.join(timeout)
+        return True
 
 
 def ingestion_routes(app, service: IngestionService, auth=None):

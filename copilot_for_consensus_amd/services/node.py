@@ -126,6 +126,15 @@ class Node:
         self.connect()
         for s in self.services.values():
             s.start()
+        if threaded and "ingestion" in self.services:
+            # periodic ingestion of every enabled source (reference ingestion/main.py:374-385);
+            # INGESTION_SCHEDULE_INTERVAL_SECONDS <= 0 turns it off
+            from .ingestion import IngestionScheduler
+            interval = self.cfgs["ingestion"].schedule_interval_seconds
+            ing = self.services["ingestion"]
+            if interval and interval > 0 and getattr(ing, "scheduler", None) is None:
+                ing.scheduler = IngestionScheduler(ing, interval_seconds=interval)
+                ing.scheduler.start()
         if threaded:
             for name, s in self.services.items():
                 if s.subscriber is not None:
@@ -135,6 +144,9 @@ class Node:
                     self._threads.append(t)
 
     def stop(self) -> None:
+        ing = self.services.get("ingestion")
+        if ing is not None and getattr(ing, "scheduler", None) is not None:
+            ing.scheduler.stop()
         for s in self.services.values():
             if s.subscriber is not None:
                 s.subscriber.stop_consuming()
