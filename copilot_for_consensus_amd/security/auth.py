@@ -16,6 +16,7 @@ import time
 import urllib.parse
 import urllib.request
 from abc import ABC, abstractmethod
+from datetime import datetime, timezone
 from typing import Any
 
 from .jwt import JWTError, JWTManager, decode
@@ -142,29 +143,54 @@ class MockIdentityProvider(IdentityProvider):
 
 
 class RoleStore:
-    """user -> roles with pending approvals (auth/app/role_store.py:28), persisted in a collection."""
+    """user -> roles with pending approvals (auth/app/role_store.py:28), persisted in a collection.
+
+    Semantics of the reference: a new user is auto-promoted to admin + reader only when that is
+    enabled AND no admin exists yet; otherwise the configured auto-approve roles, otherwise
+    ``pending``.  Admin operations validate role names against ``VALID_ROLES``; assigning to an
+    unknown user creates the record; deny applies to pending requests only."""
+
+    VALID_ROLES = frozenset({"admin", "contributor", "reviewer", "reader"})
+    SEARCH_FIELDS = ("user_id", "email", "name")
 
     def __init__(self, document_store, collection: str = "user_roles", auto_approve_roles: list[str] | None = None,
                  first_user_auto_promotion: bool = False):
         self.store, self.coll = document_store, collection
-        self.auto_roles = auto_approve_roles or []
+        self.auto_roles = [r for r in (auto_approve_roles or []) if r]
         self.first_user_admin = first_user_auto_promotion
         self._lock = threading.Lock()
 
+    @staticmethod
+    def _now() -> str:
+        return datetime.now(timezone.utc).isoformat()
+
+    def _check_roles(self, roles) -> list[str]:
+        if not isinstance(roles, (list, tuple)) or not all(isinstance(r, str) for r in roles):
+            raise ValueError("roles must be a list of role names")
+        bad = [r for r in roles if r not in self.VALID_ROLES]
+        if bad:
+            raise ValueError(f"Invalid roles: {', '.join(bad)}. Valid roles are: {', '.join(sorted(self.VALID_ROLES))}")
+        return list(roles)
+
     def get(self, user_id: str) -> dict | None:
         return self.store.get_document(self.coll, user_id)
+
+    def find_by_role(self, role: str) -> list[dict]:
+        return self.store.query_documents(self.coll, {"roles": role, "status": {"$ne": "denied"}}, limit=1 << 30)
 
     def ensure_user(self, user: dict) -> dict:
         with self._lock:
             doc = self.get(user["sub"])
             if doc is None:
-                first = self.store.count_documents(self.coll) == 0
-                roles = list(self.auto_roles)
-                if first and self.first_user_admin:
-                    roles = sorted(set(roles) | {"admin"})
+                roles, status = [], "pending"
+                if self.first_user_admin and not self.find_by_role("admin"):
+                    roles, status = ["admin", "reader"], "approved"
+                elif self.auto_roles:
+                    roles, status = sorted(set(self.auto_roles)), "approved"
+                now = self._now()
                 doc = {"_id": user["sub"], "user_id": user["sub"], "email": user.get("email"), "name": user.get("name"),
-                       "provider": user.get("provider"), "roles": roles, "status": "approved" if roles else "pending",
-                       "created_at": time.time()}
+                       "provider": user.get("provider"), "roles": roles, "status": status, "created_at": now,
+                       "requested_at": now, "updated_at": now}
                 self.store.insert_document(self.coll, doc)
             return doc
 
@@ -172,32 +198,67 @@ class RoleStore:
         d = self.get(user_id)
         return list(d.get("roles", [])) if d and d.get("status") != "denied" else []
 
-    def assign(self, user_id: str, roles: list[str]) -> dict:
-        d = self.get(user_id)
-        if d is None:
-            raise KeyError(user_id)
-        new = sorted(set(d.get("roles", [])) | set(roles))
-        self.store.update_document(self.coll, user_id, {"roles": new, "status": "approved"})
-        return self.get(user_id)
+    def assign(self, user_id: str, roles: list[str], admin_user_id: str | None = None) -> dict:
+        roles = self._check_roles(roles)
+        now = self._now()
+        with self._lock:
+            d = self.get(user_id)
+            patch = {"status": "approved", "updated_at": now, "approved_by": admin_user_id, "approved_at": now}
+            if d is None:   # assigning to a user who never logged in creates the record
+                self.store.insert_document(self.coll, {"_id": user_id, "user_id": user_id, "roles": sorted(set(roles)),
+                                                       "created_at": now, **patch})
+            else:
+                self.store.update_document(self.coll, user_id,
+                                           {"roles": sorted(set(d.get("roles", [])) | set(roles)), **patch})
+            return self.get(user_id)
 
-    def revoke(self, user_id: str, roles: list[str]) -> dict:
-        d = self.get(user_id)
-        if d is None:
-            raise KeyError(user_id)
-        self.store.update_document(self.coll, user_id, {"roles": sorted(set(d.get("roles", [])) - set(roles))})
-        return self.get(user_id)
+    def revoke(self, user_id: str, roles: list[str], admin_user_id: str | None = None) -> dict:
+        roles = self._check_roles(roles)
+        with self._lock:
+            d = self.get(user_id)
+            if d is None:
+                raise KeyError(f"User record not found: {user_id}")
+            keep = [r for r in d.get("roles", []) if r not in roles]
+            self.store.update_document(self.coll, user_id, {"roles": keep, "updated_at": self._now(),
+                                                            "last_modified_by": admin_user_id})
+            return self.get(user_id)
 
-    def deny(self, user_id: str) -> dict:
-        self.store.update_document(self.coll, user_id, {"status": "denied", "roles": []})
-        return self.get(user_id)
+    def deny(self, user_id: str, admin_user_id: str | None = None) -> dict:
+        """Deny a PENDING request: KeyError if unknown, ValueError if not pending."""
+        with self._lock:
+            d = self.get(user_id)
+            if d is None:
+                raise KeyError(f"User record not found: {user_id}")
+            if d.get("status", "pending") != "pending":
+                raise ValueError(f"Cannot deny: user status is '{d.get('status')}', expected 'pending'")
+            now = self._now()
+            self.store.update_document(self.coll, user_id, {"status": "denied", "roles": [], "denied_by": admin_user_id,
+                                                            "denied_at": now, "updated_at": now})
+            return self.get(user_id)
 
-    def pending(self) -> list[dict]:
-        return self.store.query_documents(self.coll, {"status": "pending"}, limit=1000)
+    def pending(self, user_id: str | None = None, role: str | None = None, limit: int = 50, skip: int = 0,
+                sort_by: str = "requested_at", sort_order: int = -1) -> tuple[list[dict], int]:
+        """Pending requests filtered by user / role, sorted and paged -> (page, total)."""
+        q: dict = {"status": "pending"}
+        if user_id:
+            q["user_id"] = user_id
+        if role:
+            q["roles"] = role
+        total = self.store.count_documents(self.coll, q)
+        page = self.store.query_documents(self.coll, q, limit=limit, skip=skip, sort_by=sort_by,
+                                          sort_order="desc" if sort_order == -1 else "asc")
+        return page, total
 
-    def search(self, q: str) -> list[dict]:
-        ql = q.lower()
-        return [u for u in self.store.query_documents(self.coll, {}, limit=100000)
-                if ql in (u.get("email") or "").lower() or ql in (u.get("name") or "").lower()]
+    def search(self, term: str, by: str = "email") -> list[dict]:
+        """user_id: exact match; email / name: case-insensitive substring (records missing the
+        field never match)."""
+        if by not in self.SEARCH_FIELDS:
+            raise ValueError(f"Invalid search_by field: {by}. Must be one of {', '.join(self.SEARCH_FIELDS)}")
+        if by == "user_id":
+            return self.store.query_documents(self.coll, {"user_id": term}, limit=1 << 30)
+        t = term.lower()
+        return [u for u in self.store.query_documents(self.coll, {}, limit=1 << 30)
+                if isinstance(u.get(by), str) and t in u[by].lower()]
 
 
 class JWTMiddleware:
@@ -235,9 +296,14 @@ class JWTMiddleware:
         return claims
 
     def dependency(self):
-        from fastapi import Header, HTTPException
+        from fastapi import Cookie, Header, HTTPException
 
-        def dep(authorization: str | None = Header(default=None)) -> dict:
+        def dep(authorization: str | None = Header(default=None),
+                auth_token: str | None = Cookie(default=None)) -> dict:
+            # Authorization header first, then the httpOnly ``auth_token`` cookie the UI carries
+            # (reference middleware.py:480-511)
+            if not (authorization and authorization.lower().startswith("bearer ")) and auth_token:
+                authorization = f"Bearer {auth_token}"
             try:
                 return self.verify(authorization)
             except PermissionError as e:
@@ -292,9 +358,18 @@ class AuthService:
         return self.jwt.validate_token(token, audience)
 
     def refresh(self, token: str) -> dict:
-        claims = self.jwt.validate_token(token)
-        new = self.jwt.mint_token(claims["sub"], {k: claims.get(k) for k in ("email", "name", "provider")} |
-                                  {"roles": self.roles.roles(claims["sub"])})
+        """Signature and expiry are checked against the audience the token was minted for, and
+        the new token keeps that audience (reference main.py refresh: audience preserved)."""
+        from .jwt import decode_unverified
+        _, unverified = decode_unverified(token)
+        aud = unverified.get("aud")
+        aud = aud[0] if isinstance(aud, list) and aud else aud
+        claims = self.jwt.validate_token(token, audience=aud if isinstance(aud, str) else None)
+        sub = claims.get("sub")
+        if not isinstance(sub, str) or not sub:
+            raise PermissionError("Missing or invalid 'sub' claim in token")
+        new = self.jwt.mint_token(sub, {k: claims.get(k) for k in ("email", "name", "provider")} |
+                                  {"roles": self.roles.roles(sub)}, audience=aud if isinstance(aud, str) else None)
         return {"access_token": new, "token_type": "Bearer", "expires_in": self.jwt.default_expiry}
 
     def get_jwks(self) -> dict:

@@ -180,7 +180,9 @@ def test_auth_login_userinfo_admin(auth_client):
     admin = _login(c, "alice")                     # first user: auto-promoted admin
     user = _login(c, "bob")                        # pending, no roles
     h = lambda t: {"Authorization": f"Bearer {t}"}  # noqa: E731
-    assert c.get("/userinfo", headers=h(admin)).json()["roles"] == ["admin"]
+    assert c.get("/userinfo", headers=h(admin)).json()["roles"] == ["admin", "reader"]
+    assert c.get("/userinfo").json()["sub"] == "mock:bob"        # the callback's auth_token cookie
+    c.cookies.clear()
     assert c.get("/userinfo").status_code == 401
     assert c.get("/admin/role-assignments/pending", headers=h(user)).status_code == 403
     pend = c.get("/admin/role-assignments/pending", headers=h(admin)).json()["pending"]
@@ -191,7 +193,9 @@ def test_auth_login_userinfo_admin(auth_client):
     assert c.get("/admin/users/search", params={"q": "bob"}, headers=h(admin)).json()["users"][0]["_id"] == "mock:bob"
     r = c.request("DELETE", "/admin/users/mock:bob/roles", json={"roles": ["reader"]}, headers=h(admin))
     assert r.json()["roles"] == []
-    assert c.post("/admin/users/mock:bob/deny", headers=h(admin)).json()["status"] == "denied"
+    assert c.post("/admin/users/mock:bob/deny", headers=h(admin)).status_code == 409   # approved, not pending
+    _login(c, "carol")
+    assert c.post("/admin/users/mock:carol/deny", headers=h(admin)).json()["status"] == "denied"
     refreshed = c.get("/refresh", headers=h(admin)).json()["access_token"]
     assert c.get("/userinfo", headers=h(refreshed)).status_code == 200
     assert c.post("/logout").status_code == 200

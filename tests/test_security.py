@@ -135,17 +135,21 @@ def _auth(first_admin=True):
 def test_role_store_lifecycle():
     _, roles, _ = _auth()
     admin = roles.ensure_user({"sub": "u1", "email": "a@x", "name": "Ann"})
-    assert admin["roles"] == ["admin"] and admin["status"] == "approved"
+    assert admin["roles"] == ["admin", "reader"] and admin["status"] == "approved"
     second = roles.ensure_user({"sub": "u2", "email": "b@x", "name": "Bob"})
-    assert second["status"] == "pending" and [u["_id"] for u in roles.pending()] == ["u2"]
-    assert roles.assign("u2", ["reader", "processor"])["roles"] == ["processor", "reader"]
-    assert roles.revoke("u2", ["processor"])["roles"] == ["reader"]
-    assert [u["_id"] for u in roles.search("BOB")] == ["u2"]
-    roles.deny("u2")
-    assert roles.roles("u2") == []
+    assert second["status"] == "pending" and [u["_id"] for u in roles.pending()[0]] == ["u2"]
+    assert roles.assign("u2", ["reader", "contributor"])["roles"] == ["contributor", "reader"]
+    assert roles.revoke("u2", ["contributor"])["roles"] == ["reader"]
+    assert [u["_id"] for u in roles.search("BOB", "name")] == ["u2"]
+    with pytest.raises(ValueError):
+        roles.deny("u2")                              # approved: only pending requests can be denied
+    roles.ensure_user({"sub": "u3", "name": "Cy"})
+    roles.deny("u3")
+    assert roles.roles("u3") == [] and roles.get("u3")["status"] == "denied"
     with pytest.raises(KeyError):
-        roles.assign("ghost", ["reader"])
-    assert roles.ensure_user({"sub": "u1"})["roles"] == ["admin"]  # idempotent
+        roles.revoke("ghost", ["reader"])
+    assert roles.assign("ghost", ["reader"])["status"] == "approved"   # assigning creates the record
+    assert roles.ensure_user({"sub": "u1"})["roles"] == ["admin", "reader"]  # idempotent
 
 
 def test_pkce_pair_is_s256():
@@ -160,7 +164,7 @@ def test_login_flow_and_refresh():
     assert "state=" in start["authorization_url"]
     res = svc.handle_callback("mock-user", start["state"])
     claims = svc.validate_token(res["access_token"])
-    assert claims["sub"] == "mock:mock-user" and claims["roles"] == ["admin"]
+    assert claims["sub"] == "mock:mock-user" and claims["roles"] == ["admin", "reader"]
     with pytest.raises(PermissionError):
         svc.handle_callback("mock-user", start["state"])  # state is single-use
     with pytest.raises(PermissionError):
