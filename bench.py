@@ -45,6 +45,8 @@ def parse_args(argv=None):
     ap.add_argument("--llm-only", action="store_true", help="skip the CPU/encoder/kNN stages (diagnostic)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--index-prefill", type=int, default=1_000_000,
+                    help="background vectors resident in the HBM kNN index besides the run's own chunks")
     ap.add_argument("--no-overlap", action="store_true", help="run pipeline stages strictly sequentially")
     return ap.parse_args(argv)
 
@@ -69,14 +71,16 @@ def main(argv=None):
                          max_new_tokens=args.max_new, tp=args.tp, prefill_tokens=args.prefill_tokens, kv_dtype=args.kv_dtype,
                          weight_dtype=args.weights,
                          llm_only=args.llm_only, use_graph=not args.no_graph,
-                         seed=args.seed + 7919 * groups.dp_rank, groups=groups if args.tp > 1 else None)
+                         seed=args.seed + 7919 * groups.dp_rank, groups=groups if args.tp > 1 else None,
+                         index_prefill=args.index_prefill)
 
     pipe.prepare_sources(list(range(args.warmup + args.steps)))
 
     def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize(dev)
+        if dev.type == "cuda":   # CPU rehearsal (tests/test_bench_contract_cpu.py) has no device to sync
+            torch.cuda.synchronize(dev)
 
     t = time.perf_counter()
     for i, r in enumerate(pipe.run_steps(list(range(args.warmup)), overlap=not args.no_overlap)):

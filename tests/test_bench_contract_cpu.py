@@ -1,0 +1,54 @@
+"""The driver's bench.py contract, rehearsed on the CPU: one rank and two ranks under
+``torch.distributed.run`` (gloo, 127.0.0.1), tiny random-init models.  Checks the single JSON line
+rank 0 prints (keys, whole-job aggregate value, n_gpus, weak-scaling batch, parallelism tag) so the
+multi-GPU path the driver runs at N = 2..8 is exercised by construction here."""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--model", "tiny", "--encoder", "tiny", "--threads-per-gpu", "2", "--max-new", "3", "--steps", "2",
+        "--warmup", "1", "--index-prefill", "0", "--prefill-tokens", "4096"]
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(cmd):
+    env = {**os.environ, "CFC_DIST_BACKEND": "gloo", "OMP_NUM_THREADS": "2", "MASTER_ADDR": "127.0.0.1"}
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout           # exactly one JSON line, from rank 0 only
+    return json.loads(lines[0])
+
+
+def _check(d, n):
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == n and d["steps"] == 2 and d["warmup"] == 1
+    assert d["scaling"] == "weak" and d["higher_is_better"] is True and d["dtype"] == "bf16"
+    assert d["config"]["global_batch"] == 2 * n and d["config"]["parallelism"] == f"dp{n}"
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    # value is the whole-job aggregate: threads of every rank over the max elapsed time
+    assert d["value"] == pytest.approx(2 * n * 2 / (d["ms_per_step"] * 2 / 1000), rel=0.02)
+
+
+def test_bench_single_process_contract():
+    _check(_run([sys.executable, "bench.py", "--gpus", "1", *ARGS]), 1)
+
+
+def test_bench_two_ranks_under_torchrun():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", *ARGS]
+    _check(_run(cmd), 2)
