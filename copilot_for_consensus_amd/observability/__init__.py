@@ -19,6 +19,7 @@ import contextlib
 import json
 import logging
 import os
+import re
 import sys
 import threading
 import time
@@ -55,6 +56,8 @@ class StdoutLogger(Logger):
         self._lock = threading.Lock()
 
     def log(self, level, message, **kw):
+        level = str(level).upper()
+        level = "WARNING" if level == "WARN" else level
         if _LEVELS.get(level, 20) < self.level:
             return
         rec = {"timestamp": datetime.now(timezone.utc).isoformat().replace("+00:00", "Z"), "level": level,
@@ -83,7 +86,10 @@ def create_logger(cfg=None, **overrides) -> Logger:
     name = getattr(cfg, "driver_name", cfg) or "stdout"
     kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
     kw.update(overrides)
-    return {"stdout": StdoutLogger, "silent": SilentLogger}[name](**kw)
+    cls = {"stdout": StdoutLogger, "silent": SilentLogger}.get(name)
+    if cls is None:
+        raise ValueError(f"unknown logger driver {name!r} (stdout or silent)")
+    return cls(**kw)
 
 
 def set_default_logger(lg: Logger) -> None:
@@ -108,7 +114,21 @@ def uvicorn_log_config(level: str = "INFO") -> dict:
 # ------------------------------------------------------------------------------------- metrics
 
 def _key(name, tags):
-    return (name, tuple(sorted((tags or {}).items())))
+    return (name, tuple(sorted((str(k), str(v)) for k, v in (tags or {}).items())))
+
+
+_NAME_OK = re.compile(r"[^a-zA-Z0-9_:]")
+
+
+def _metric_name(name: str) -> str:
+    """Prometheus metric / label names: [a-zA-Z_:][a-zA-Z0-9_:]* (other characters become '_')."""
+    n = _NAME_OK.sub("_", str(name))
+    return n if n and not n[0].isdigit() else "_" + n
+
+
+def _label_value(v) -> str:
+    """Exposition-format escaping of a label value: backslash, double quote, newline."""
+    return str(v).replace("\\", "\\\\").replace('"', '\\"').replace("\n", "\\n")
 
 
 DEFAULT_BUCKETS = (0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1, 2.5, 5, 10, 30, 60, 120, 300)
@@ -153,6 +173,7 @@ class PrometheusMetricsCollector(MetricsCollector):
         self.hist: dict = {}
 
     def _n(self, name):
+        name = _metric_name(name)
         return f"{self.namespace}_{name}" if self.namespace and not name.startswith(self.namespace + "_") else name
 
     def increment(self, name, value=1.0, tags=None):
@@ -181,23 +202,45 @@ class PrometheusMetricsCollector(MetricsCollector):
     @staticmethod
     def _labels(tags, extra=None):
         items = list(tags) + (extra or [])
-        return "{" + ",".join(f'{k}="{v}"' for k, v in items) + "}" if items else ""
+        return "{" + ",".join(f'{_metric_name(k)}="{_label_value(v)}"' for k, v in items) + "}" if items else ""
 
     def render(self) -> str:
-        """Prometheus text exposition format 0.0.4."""
+        """Prometheus text exposition format 0.0.4: one ``# TYPE`` line per metric family, then
+        its samples (label values escaped)."""
         out = []
+        typed = set()
+
+        def family(n, kind):
+            if n not in typed:
+                typed.add(n)
+                out.append(f"# TYPE {n} {kind}")
+
         with self._lock:
             for (n, t), v in sorted(self.counters.items()):
+                family(n, "counter")
                 out.append(f"{n}{self._labels(t)} {v}")
             for (n, t), v in sorted(self.gauges.items()):
+                family(n, "gauge")
                 out.append(f"{n}{self._labels(t)} {v}")
             for (n, t), (counts, s, c) in sorted(self.hist.items()):
+                family(n, "histogram")
                 for b, cnt in zip(self.buckets, counts):
                     out.append(f"{n}_bucket{self._labels(t, [('le', b)])} {cnt}")
                 out.append(f"{n}_bucket{self._labels(t, [('le', '+Inf')])} {c}")
                 out.append(f"{n}_sum{self._labels(t)} {s}")
                 out.append(f"{n}_count{self._labels(t)} {c}")
         return "\n".join(out) + "\n"
+
+
+def _push_segment(key, value) -> tuple[str, str]:
+    """Pushgateway grouping-key path segment: URL-escaped, or ``key@base64/<urlsafe b64>`` when
+    the value contains '/' or is empty (the Pushgateway's own encoding for such values)."""
+    import base64
+    import urllib.parse
+    v = str(value)
+    if "/" in v or v == "":
+        return f"{key}@base64", base64.urlsafe_b64encode(v.encode()).decode() or "="
+    return str(key), urllib.parse.quote(v, safe="")
 
 
 class PushGatewayMetricsCollector(PrometheusMetricsCollector):
@@ -218,7 +261,8 @@ class PushGatewayMetricsCollector(PrometheusMetricsCollector):
         url = self.gateway.rstrip("/")
         if not url.startswith("http"):
             url = "http://" + url
-        url += f"/metrics/job/{self.job}" + "".join(f"/{k}/{v}" for k, v in self.grouping_key.items())
+        url += f"/metrics/job/{_push_segment('job', self.job)[1]}" + "".join(
+            "/{}/{}".format(*_push_segment(k, v)) for k, v in self.grouping_key.items())
         req = urllib.request.Request(url, data=self.render().encode(), method="PUT",
                                      headers={"Content-Type": "text/plain; version=0.0.4"})
         try:

@@ -1,0 +1,217 @@
+"""Logging, metrics and error reporting adapters (reference adapters/copilot_logging/tests,
+copilot_metrics/tests, copilot_error_reporting/tests): JSON-lines logger fields, level filtering
+and aliases, non-JSON values, exception tracebacks, factories; Prometheus counters / gauges /
+histograms (cumulative buckets, sum, count, one TYPE line per family, label-value escaping, name
+sanitising, namespacing, thread safety); Pushgateway grouping-key encoding; error reporters."""
+from __future__ import annotations
+
+import io
+import json
+import threading
+
+import pytest
+
+from copilot_for_consensus_amd.observability import (ConsoleErrorReporter, NoOpMetricsCollector,
+                                                     PrometheusMetricsCollector, PushGatewayMetricsCollector,
+                                                     SilentErrorReporter, SilentLogger, StdoutLogger, _push_segment,
+                                                     create_error_reporter, create_logger, create_metrics_collector,
+                                                     get_logger, set_default_logger, span, uvicorn_log_config)
+
+
+def _lines(buf):
+    return [json.loads(x) for x in buf.getvalue().splitlines()]
+
+
+# ------------------------------------------------------------------ logging
+def test_stdout_logger_fields_and_kv():
+    buf = io.StringIO()
+    lg = StdoutLogger(level="DEBUG", name="parsing", stream=buf)
+    lg.info("parsed archive", archive_id="abc", count=3, ok=True, ids=["a"], meta={"k": 1}, obj=object())
+    rec = _lines(buf)[0]
+    assert rec["level"] == "INFO" and rec["logger"] == "parsing" and rec["message"] == "parsed archive"
+    assert rec["archive_id"] == "abc" and rec["count"] == 3 and rec["ok"] is True and rec["ids"] == ["a"]
+    assert rec["meta"] == {"k": 1} and rec["obj"].startswith("<object")        # non-JSON values: repr
+    assert rec["timestamp"].endswith("Z") and "T" in rec["timestamp"]
+
+
+@pytest.mark.parametrize("level,emitted", [("DEBUG", 4), ("INFO", 3), ("WARNING", 2), ("warning", 2), ("ERROR", 1),
+                                           ("CRITICAL", 0), ("bogus", 3)])
+def test_level_filtering(level, emitted):
+    buf = io.StringIO()
+    lg = StdoutLogger(level=level, stream=buf)
+    lg.debug("d")
+    lg.info("i")
+    lg.warning("w")
+    lg.error("e")
+    assert len(_lines(buf)) == emitted
+
+
+def test_level_aliases_and_exception_traceback():
+    buf = io.StringIO()
+    lg = StdoutLogger(stream=buf)
+    lg.log("warn", "old alias")
+    try:
+        raise KeyError("boom")
+    except KeyError:
+        lg.exception("failed", stage="chunking")
+    recs = _lines(buf)
+    assert recs[0]["level"] == "WARNING"
+    assert recs[1]["level"] == "ERROR" and "KeyError" in recs[1]["traceback"] and recs[1]["stage"] == "chunking"
+
+
+def test_logger_is_thread_safe_line_by_line():
+    buf = io.StringIO()
+    lg = StdoutLogger(stream=buf)
+    ts = [threading.Thread(target=lambda k=k: [lg.info("m", k=k, i=i) for i in range(200)]) for k in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert len(_lines(buf)) == 1600          # every line parses: no interleaving
+
+
+def test_silent_logger_and_factories():
+    s = SilentLogger()
+    s.info("x", a=1)
+    assert s.records == [("INFO", "x", {"a": 1})]
+    assert isinstance(create_logger("silent"), SilentLogger)
+    assert isinstance(create_logger(None), StdoutLogger)
+
+    class Cfg:
+        driver_name = "stdout"
+        driver_config = {"level": "ERROR", "name": "svc"}
+    lg = create_logger(Cfg())
+    assert lg.level == 40 and lg.name == "svc"
+    with pytest.raises(ValueError):
+        create_logger("syslog")
+    set_default_logger(s)
+    try:
+        assert get_logger() is s
+    finally:
+        set_default_logger(None)
+    assert isinstance(get_logger("x"), StdoutLogger)
+
+
+def test_uvicorn_log_config_is_json():
+    cfg = uvicorn_log_config("WARNING")
+    assert cfg["loggers"]["uvicorn.access"]["level"] == "WARNING"
+    assert cfg["formatters"]["json"]["format"].startswith("{")
+
+
+# ------------------------------------------------------------------ metrics
+def test_noop_collector_accepts_everything():
+    m = NoOpMetricsCollector()
+    m.increment("x", tags={"a": 1})
+    m.observe("y", 1.0)
+    m.gauge("z", 2)
+    m.safe_push()
+
+
+def test_counters_gauges_histograms():
+    m = PrometheusMetricsCollector(namespace="copilot", buckets=(0.1, 1.0, 10.0))
+    m.increment("events_total", tags={"type": "a"})
+    m.increment("events_total", 2, tags={"type": "a"})
+    m.increment("events_total", tags={"type": "b"})
+    m.gauge("queue_depth", 5)
+    m.gauge("queue_depth", 3)                      # gauges overwrite
+    for v in (0.05, 0.5, 0.5, 5.0, 50.0):
+        m.observe("latency_seconds", v)
+    txt = m.render()
+    assert 'copilot_events_total{type="a"} 3.0' in txt and 'copilot_events_total{type="b"} 1.0' in txt
+    assert "copilot_queue_depth 3.0" in txt and "copilot_queue_depth 5.0" not in txt
+    for le, n in (("0.1", 1), ("1.0", 3), ("10.0", 4), ("+Inf", 5)):     # cumulative buckets
+        assert f'copilot_latency_seconds_bucket{{le="{le}"}} {n}' in txt
+    assert "copilot_latency_seconds_sum 56.05" in txt and "copilot_latency_seconds_count 5" in txt
+    assert txt.count("# TYPE copilot_events_total counter") == 1
+    assert "# TYPE copilot_queue_depth gauge" in txt and "# TYPE copilot_latency_seconds histogram" in txt
+    assert m.get_counter("events_total", {"type": "a"}) == 3
+
+
+def test_tag_order_and_types_do_not_split_series():
+    m = PrometheusMetricsCollector()
+    m.increment("x_total", tags={"a": 1, "b": "2"})
+    m.increment("x_total", tags={"b": 2, "a": "1"})
+    assert m.get_counter("x_total", {"a": "1", "b": "2"}) == 2
+
+
+def test_exposition_escaping_and_names():
+    m = PrometheusMetricsCollector(namespace="")
+    m.increment("bad-name.total", tags={"source": 'list "quic"\\main\nx', "bad-label": "v"})
+    txt = m.render()
+    assert 'bad_name_total{bad_label="v",source="list \\"quic\\"\\\\main\\nx"} 1.0' in txt
+    assert len(txt.strip().splitlines()) == 2          # the newline inside the value was escaped
+    m.increment("9lives")
+    assert "_9lives 1.0" in m.render()
+
+
+def test_namespace_not_doubled():
+    m = PrometheusMetricsCollector(namespace="copilot")
+    m.increment("copilot_x_total")
+    m.increment("x_total")
+    assert m.get_counter("x_total") == 2 and "copilot_copilot" not in m.render()
+
+
+def test_concurrent_increments():
+    m = PrometheusMetricsCollector()
+    ts = [threading.Thread(target=lambda: [m.increment("n_total") for _ in range(1000)]) for _ in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert m.get_counter("n_total") == 8000
+
+
+@pytest.mark.parametrize("k,v,seg", [("instance", "gpu0", ("instance", "gpu0")),
+                                     ("path", "a/b", ("path@base64", "YS9i")),
+                                     ("empty", "", ("empty@base64", "=")),
+                                     ("q", "a b&c", ("q", "a%20b%26c"))])
+def test_pushgateway_grouping_key_encoding(k, v, seg):
+    assert _push_segment(k, v) == seg
+
+
+def test_pushgateway_config_forms():
+    m = PushGatewayMetricsCollector(gateway="pgw:9091", grouping_key='{"instance": "n1"}')
+    assert m.grouping_key == {"instance": "n1"}
+    m = PushGatewayMetricsCollector(gateway="pgw:9091", grouping_key="a=1,b=2")
+    assert m.grouping_key == {"a": "1", "b": "2"}
+    PushGatewayMetricsCollector().push()          # no gateway configured: nothing to do
+
+
+def test_metrics_factory():
+    assert isinstance(create_metrics_collector(None), NoOpMetricsCollector)
+    assert isinstance(create_metrics_collector("prometheus"), PrometheusMetricsCollector)
+    with pytest.raises(ValueError):
+        create_metrics_collector("statsd")
+
+
+def test_span_observes_duration_even_on_error():
+    m = PrometheusMetricsCollector()
+    with pytest.raises(RuntimeError):
+        with span("stage", metrics=m):
+            raise RuntimeError("x")
+    assert "copilot_stage_duration_seconds_count 1" in m.render()
+
+
+# ------------------------------------------------------------------ error reporting
+def test_console_reporter_logs_and_records():
+    buf = io.StringIO()
+    rep = ConsoleErrorReporter(logger=StdoutLogger(stream=buf))
+    rep.report(ValueError("bad input"), context={"event_id": "e1"})
+    rep.capture_message("heads up", context={"k": 1})
+    recs = _lines(buf)
+    assert recs[0]["message"] == "ValueError: bad input" and recs[0]["context"] == {"event_id": "e1"}
+    assert "heads up" in recs[1]["message"]
+    assert [type(e).__name__ for e, _ in rep.reported] == ["ValueError", "RuntimeError"]
+
+
+def test_silent_reporter_and_factory():
+    rep = create_error_reporter("silent")
+    assert isinstance(rep, SilentErrorReporter)
+    ctx = {"a": 1}
+    rep.report(KeyError("k"), context=ctx)
+    ctx["a"] = 2                                  # context is snapshotted
+    assert rep.reported[0][1] == {"a": 1}
+    with pytest.raises(ImportError, match="sentry"):
+        create_error_reporter("sentry", dsn="https://x@example.invalid/1")
+    with pytest.raises(ValueError):
+        create_error_reporter("bugsnag")
