@@ -385,6 +385,7 @@ class ValidatingDocumentStore(DocumentStore):
         self._schemas = schema_provider or default_provider()
         self.strict = strict
         self.validation_errors: list[tuple[str, list[str]]] = []
+        self.skipped = 0
 
     def _check(self, collection, doc):
         errs = self._schemas.validate_document(collection, doc)
@@ -398,9 +399,20 @@ class ValidatingDocumentStore(DocumentStore):
         return self._inner.insert_document(collection, doc)
 
     def insert_many(self, collection, docs, ignore_duplicates=True):
+        """Batch insert.  In strict mode an invalid document is skipped (and recorded in
+        ``validation_errors`` / counted in ``skipped``) while the rest of the batch is stored --
+        the reference's per-message loop that logs a validation error and continues
+        (parsing/app/service.py _store_messages); one malformed message must not fail the archive."""
+        ok = []
         for d in docs:
-            self._check(collection, d)
-        return self._inner.insert_many(collection, docs, ignore_duplicates)
+            errs = self._schemas.validate_document(collection, d)
+            if errs:
+                self.validation_errors.append((collection, errs))
+                if self.strict:
+                    self.skipped += 1
+                    continue
+            ok.append(d)
+        return self._inner.insert_many(collection, ok, ignore_duplicates)
 
     def get_document(self, collection, doc_id):
         return self._inner.get_document(collection, doc_id)
@@ -409,6 +421,16 @@ class ValidatingDocumentStore(DocumentStore):
         return self._inner.query_documents(collection, filter_dict or {}, limit, sort_by, sort_order, skip)
 
     def update_document(self, collection, doc_id, patch):
+        """Strict mode validates the document as it WILL be after the update (store metadata
+        fields such as Cosmos' ``_etag`` / ``_ts`` ignored), reference validating_document_store.py."""
+        if self.strict:
+            cur = self._inner.get_document(collection, doc_id)
+            if cur is None:
+                raise DocumentNotFoundError(f"Document {doc_id} not found in collection {collection}")
+            after = sanitize_document(copy.deepcopy(cur))
+            apply_update(after, copy.deepcopy(patch))
+            after["_id"] = doc_id
+            self._check(collection, after)
         return self._inner.update_document(collection, doc_id, patch)
 
     def update_many(self, collection, filter_dict, patch):

@@ -231,3 +231,30 @@ def test_indexed_lookup_equals_full_scan(docs, flt):
     want = sorted(d["_id"] for d in plain.collections["c"].values() if query.matches(d, flt))
     assert ids(plain.query_documents("c", flt, limit=None)) == want
     assert ids(indexed.query_documents("c", flt, limit=None)) == want
+
+
+def test_validating_store_batch_skips_invalid_and_keeps_the_rest():
+    """One malformed message must not fail a whole archive (reference parsing service: log the
+    validation error, skip, continue)."""
+    inner = InMemoryDocumentStore()
+    vs = ValidatingDocumentStore(inner)
+    good = {"_id": "0123456789abcdef", "file_hash": "a" * 64, "file_size_bytes": 1, "source": "s",
+            "ingestion_date": "2025-01-01T00:00:00Z", "status": "pending"}
+    bad = {"_id": "fedcba9876543210", "status": "weird-status"}
+    ids = vs.insert_many("archives", [good, bad])
+    assert ids == ["0123456789abcdef"] and vs.skipped == 1 and len(vs.validation_errors) == 1
+    assert inner.get_document("archives", "fedcba9876543210") is None
+    lenient = ValidatingDocumentStore(InMemoryDocumentStore(), strict=False)
+    assert len(lenient.insert_many("archives", [good, bad])) == 2      # lenient: recorded, stored
+
+
+def test_validating_store_checks_updates_against_the_result():
+    vs = ValidatingDocumentStore(InMemoryDocumentStore())
+    vs.insert_document("archives", {"_id": "0123456789abcdef", "file_hash": "a" * 64, "file_size_bytes": 1,
+                                    "source": "s", "ingestion_date": "2025-01-01T00:00:00Z", "status": "pending"})
+    vs.update_document("archives", "0123456789abcdef", {"$set": {"status": "completed"}})
+    with pytest.raises(DocumentStoreError):
+        vs.update_document("archives", "0123456789abcdef", {"$set": {"status": "exploded"}})
+    assert vs.get_document("archives", "0123456789abcdef")["status"] == "completed"
+    with pytest.raises(DocumentNotFoundError):
+        vs.update_document("archives", "ffffffffffffffff", {"status": "completed"})
