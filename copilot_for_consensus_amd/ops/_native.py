@@ -29,7 +29,8 @@ _KERNEL_SIGS = {
     "cfc_paged_decode_attention": [P, P, P, P, P, I, I, I, I, I, I, I, F, I, P, P, P, P],
     "cfc_prefill_attention": [P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P, P],
     "cfc_prefill_rows": [I, I],
-    "cfc_encoder_attention": [P, P, P, P, I, I, I, I, F, P, P],
+    "cfc_encoder_rows": [],
+    "cfc_encoder_attention": [P, P, P, P, I, I, I, I, I, F, P, P],
     "cfc_rope_kv_write": [P, P, P, P, P, P, P, I, I, I, I, I, P],
     "cfc_v_cache_write_runs": [P, P, I, P, I, I, I, P],
     "cfc_decode_advance_cb": [P, P, I, P, P, P, P, P, P, P, I, P, P, I, I, P],

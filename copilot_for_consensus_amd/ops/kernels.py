@@ -198,7 +198,7 @@ def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, o
 
 
 PREFILL_TILE_ROWS = 128   # query rows per workgroup of the legacy single-head prefill kernels
-ENCODER_TILE_ROWS = 64    # query rows per workgroup of the encoder attention kernel
+ENCODER_TILE_ROWS = 256   # query rows per workgroup of the encoder attention kernel (attention.hip ENC_ROWS)
 
 
 def prefill_rows(Hq: int, Hkv: int) -> int:
@@ -269,8 +269,9 @@ def encoder_attention(qkv, cu_seqlens, H, D, scale, max_seqlen, tiles=None, out=
                  torch.tensor(q0, dtype=torch.int32, device=qkv.device))
     out = torch.empty(T, H, D, dtype=qkv.dtype, device=qkv.device) if out is None else out
     check(kernels().cfc_encoder_attention(qkv.data_ptr(), cu_seqlens.data_ptr(), tiles[0].data_ptr(),
-                                          tiles[1].data_ptr(), tiles[0].numel(), H, D, int(max_seqlen),
-                                          float(scale), out.data_ptr(), _stream(qkv)), "cfc_encoder_attention")
+                                          tiles[1].data_ptr(), tiles[0].numel(), ENCODER_TILE_ROWS, H, D,
+                                          int(max_seqlen), float(scale), out.data_ptr(), _stream(qkv)),
+          "cfc_encoder_attention")
     return out
 
 

@@ -932,10 +932,18 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
 // ------------------------------------------------------------------------------------------
 // Varlen bidirectional encoder attention (BERT family), D in {32, 64}, S <= 512.
 // Input qkv is the fused projection output [T, 3*H*D] (q | k | v, head-major inside each).
-// grid = (n_tiles, H); block = 256 = 4 waves x 16 query rows.  The WHOLE key/value range of
-// the sequence is staged once in LDS (K row-major, V transposed with the per-32-key slot
-// permutation), then each wave runs the swapped-product online softmax over it.
+// 1-D grid over (query tile, head), XCD-remapped; block = 256 = 4 waves, tile = ENC_ROWS = 256
+// query rows (wave w: rows 64w .. 64w+63 as ENC_R = 4 groups of 16).  The WHOLE key/value range
+// of the sequence is staged once in LDS per block (K row-major, V transposed with the per-32-key
+// slot permutation) -- with 256-row tiles a MiniLM sequence (S <= 256) stages its K/V once per
+// head instead of once per 64 rows -- then every wave runs the swapped-product online softmax:
+// each 32-key K / V fragment is read from LDS once and reused by the wave's 4 row groups.
+// Softmax: Q is pre-scaled by scale*log2(e) at load, the key mask runs only on the sequence's
+// last (partial) 32-key tile, exponentials are v_exp_f32 (inputs <= 0).
 // ------------------------------------------------------------------------------------------
+constexpr int ENC_R = 4;               // 16-row query groups per wave
+constexpr int ENC_ROWS = 64 * ENC_R;   // query rows per workgroup
+
 template <int D>
 __global__ void __launch_bounds__(256) encoder_attn_kernel(const uint16_t* __restrict__ qkv,
                                                            const int32_t* __restrict__ cu_seqlens,
@@ -944,8 +952,13 @@ __global__ void __launch_bounds__(256) encoder_attn_kernel(const uint16_t* __res
                                                            int H, uint16_t* __restrict__ out) {
   constexpr int NC = D / 8;         // 16-byte chunks per K row
   constexpr int KSTEPS = D / 32;    // MFMA k-steps over head_dim
+  constexpr int DT = D / 16;        // 16-wide output column tiles
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int t = blockIdx.x, h = blockIdx.y;
+  // logical block = tile * H + head, XCD-remapped: every (query tile, head) block of a sequence
+  // lands on ONE XCD, so the sequence's fused qkv rows (all heads share each 128-B line) are
+  // fetched from HBM once into that XCD's L2 instead of once per XCD.
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int t = lb / H, h = lb - t * H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
   const int col = lane & 15, g = lane >> 4;
   const int s = tile_seq[t], qs = tile_q0[t];
@@ -983,76 +996,110 @@ __global__ void __launch_bounds__(256) encoder_attn_kernel(const uint16_t* __res
     }
   }
 
-  const int my_row = qs + 16 * w + col;
-  bf16x8_t qf[KSTEPS];
-  {
-    const int r = min(my_row, S - 1);
+  // this wave's row groups that hold at least one row of the sequence (wave-uniform)
+  const int wrow0 = qs + 64 * w;
+  const int ng = min(ENC_R, max(0, (S - wrow0 + 15) >> 4));
+  bf16x8_t qf[ENC_R][KSTEPS];
+#pragma unroll
+  for (int rg = 0; rg < ENC_R; ++rg) {
+    const int r = min(wrow0 + 16 * rg + col, S - 1);
     const uint16_t* qr = qkv + (size_t)(beg + r) * row_stride + h * D;
 #pragma unroll
-    for (int c = 0; c < KSTEPS; ++c) qf[c] = as_bf16x8(*reinterpret_cast<const uint4*>(qr + 32 * c + 8 * g));
+    for (int c = 0; c < KSTEPS; ++c) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(qr + 32 * c + 8 * g), f);
+      uint4 u;
+      u.x = pack2bf(f[0] * scale_log2, f[1] * scale_log2);
+      u.y = pack2bf(f[2] * scale_log2, f[3] * scale_log2);
+      u.z = pack2bf(f[4] * scale_log2, f[5] * scale_log2);
+      u.w = pack2bf(f[6] * scale_log2, f[7] * scale_log2);
+      qf[rg][c] = as_bf16x8(u);
+    }
   }
   __syncthreads();
+  if (ng == 0) return;   // no barrier follows
 
-  constexpr int DT = D / 16;
-  f32x4_t o[DT];
+  f32x4_t o[ENC_R][DT];
+  float m[ENC_R], l[ENC_R];
 #pragma unroll
-  for (int i = 0; i < DT; ++i) o[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
+  for (int rg = 0; rg < ENC_R; ++rg) {
+    m[rg] = -INFINITY;
+    l[rg] = 0.f;
+#pragma unroll
+    for (int i = 0; i < DT; ++i) o[rg][i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
 
   for (int k0 = 0; k0 < S; k0 += 32) {
-    f32x4_t sc[2];
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      sc[st] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      const int r = k0 + 16 * st + col;
-#pragma unroll
-      for (int c = 0; c < KSTEPS; ++c) {
-        const uint4 kv = *reinterpret_cast<const uint4*>(klds + koff(r, 4 * c + g));
-        sc[st] = mfma16(as_bf16x8(kv), qf[c], sc[st]);
-      }
-    }
-    float tmax = -INFINITY;
+    bf16x8_t kf[2][KSTEPS];
 #pragma unroll
     for (int st = 0; st < 2; ++st)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = k0 + 16 * st + 4 * g + i;
-        float v = sc[st][i] * scale_log2;
-        v = key < S ? v : -INFINITY;
-        sc[st][i] = v;
-        tmax = fmaxf(tmax, v);
+      for (int c = 0; c < KSTEPS; ++c)
+        kf[st][c] = as_bf16x8(*reinterpret_cast<const uint4*>(klds + koff(k0 + 16 * st + col, 4 * c + g)));
+    bf16x8_t vf[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+      vf[dt] = as_bf16x8(*reinterpret_cast<const uint4*>(vlds + voff_chunk(16 * dt + col, (k0 >> 3) + g)));
+    const bool tail = k0 + 32 > S;
+
+#pragma unroll
+    for (int rg = 0; rg < ENC_R; ++rg) {
+      if (rg >= ng) break;
+      f32x4_t sc[2];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        sc[st] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < KSTEPS; ++c) sc[st] = mfma16(kf[st][c], qf[rg][c], sc[st]);
       }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mn = fmaxf(m, tmax);
-    const float alpha = exp2f(m - mn);
-    float rs = 0.f;
+      if (tail) {
 #pragma unroll
-    for (int st = 0; st < 2; ++st)
+        for (int st = 0; st < 2; ++st)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { const float e = exp2f(sc[st][i] - mn); sc[st][i] = e; rs += e; }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = mn;
-    const bf16x8_t pf = pack_p(sc[0], sc[1]);
+          for (int i = 0; i < 4; ++i)
+            if (k0 + 16 * st + 4 * g + i >= S) sc[st][i] = -INFINITY;
+      }
+      float tmax = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
+                         fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mn = fmaxf(m[rg], tmax);
+      const float alpha = __builtin_amdgcn_exp2f(m[rg] - mn);
+      float rs = 0.f;
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      o[dt] *= alpha;
-      const uint4 vv = *reinterpret_cast<const uint4*>(vlds + voff_chunk(16 * dt + col, (k0 >> 3) + g));
-      o[dt] = mfma16(as_bf16x8(vv), pf, o[dt]);
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float e = __builtin_amdgcn_exp2f(sc[st][i] - mn);
+          sc[st][i] = e;
+          rs += e;
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      l[rg] = l[rg] * alpha + rs;
+      m[rg] = mn;
+      const bf16x8_t pf = pack_p(sc[0], sc[1]);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        o[rg][dt] *= alpha;
+        o[rg][dt] = mfma16(vf[dt], pf, o[rg][dt]);
+      }
     }
   }
 
-  if (my_row < S) {
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-    uint16_t* orow = out + ((size_t)(beg + my_row) * H + h) * D;
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      uint2 pk;
-      pk.x = pack2bf(o[dt][0] * inv, o[dt][1] * inv);
-      pk.y = pack2bf(o[dt][2] * inv, o[dt][3] * inv);
-      *reinterpret_cast<uint2*>(orow + 16 * dt + 4 * g) = pk;
+  for (int rg = 0; rg < ENC_R; ++rg) {
+    const int my_row = wrow0 + 16 * rg + col;
+    if (rg < ng && my_row < S) {
+      const float inv = l[rg] > 0.f ? 1.f / l[rg] : 0.f;
+      uint16_t* orow = out + ((size_t)(beg + my_row) * H + h) * D;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        uint2 pk;
+        pk.x = pack2bf(o[rg][dt][0] * inv, o[rg][dt][1] * inv);
+        pk.y = pack2bf(o[rg][dt][2] * inv, o[rg][dt][3] * inv);
+        *reinterpret_cast<uint2*>(orow + 16 * dt + 4 * g) = pk;
+      }
     }
   }
 }
@@ -1188,18 +1235,21 @@ CFC_API int cfc_prefill_attention_fp8(const void* q, const void* k_cache, const 
   return CFC_CHECK_LAUNCH();
 }
 
+CFC_API int cfc_encoder_rows() { return ENC_ROWS; }
+
 CFC_API int cfc_encoder_attention(const void* qkv, const int32_t* cu_seqlens, const int32_t* tile_seq,
-                                  const int32_t* tile_q0, int n_tiles, int H, int head_dim, int max_seqlen, float scale,
-                                  void* out, hipStream_t stream) {
+                                  const int32_t* tile_q0, int n_tiles, int tile_rows, int H, int head_dim,
+                                  int max_seqlen, float scale, void* out, hipStream_t stream) {
+  if (tile_rows != ENC_ROWS) return -3;          // tiles cut for another kernel revision
   if (n_tiles <= 0) return 0;
   if (max_seqlen > 512) return -2;
   const int spad = (max_seqlen + 127) & ~127;
   const size_t lds = (size_t)spad * head_dim * 2 * 2;
   if (head_dim == 32) {
-    encoder_attn_kernel<32><<<dim3(n_tiles, H), 256, lds, stream>>>((const uint16_t*)qkv, cu_seqlens, tile_seq, tile_q0,
+    encoder_attn_kernel<32><<<dim3(n_tiles * H), 256, lds, stream>>>((const uint16_t*)qkv, cu_seqlens, tile_seq, tile_q0,
                                                                     scale * LOG2E, H, (uint16_t*)out);
   } else if (head_dim == 64) {
-    encoder_attn_kernel<64><<<dim3(n_tiles, H), 256, lds, stream>>>((const uint16_t*)qkv, cu_seqlens, tile_seq, tile_q0,
+    encoder_attn_kernel<64><<<dim3(n_tiles * H), 256, lds, stream>>>((const uint16_t*)qkv, cu_seqlens, tile_seq, tile_q0,
                                                                     scale * LOG2E, H, (uint16_t*)out);
   } else {
     return -1;
