@@ -60,8 +60,15 @@ class TokenWindowChunker(ThreadChunker):
     def __init__(self, chunk_size: int = 384, overlap: int = 50, min_chunk_size: int = 100, max_chunk_size: int = 512):
         if chunk_size <= 0:
             raise ValueError("chunk_size must be positive")
+        # a negative overlap would skip the words between two windows
+        if overlap < 0:
+            raise ValueError(f"overlap must be >= 0, got {overlap}")
         self.chunk_size, self.overlap = int(chunk_size), int(overlap)
-        self.min_chunk_size, self.max_chunk_size = int(min_chunk_size), int(max_chunk_size)
+        # A full window always meets the minimum: with CHUNK_SIZE_TOKENS set below the default
+        # minimum (100) the reference discards every full window and keeps only the tail
+        # (chunkers.py:184), silently losing the text -- the minimum is clamped to the window.
+        self.min_chunk_size = min(int(min_chunk_size), self.chunk_size)
+        self.max_chunk_size = int(max_chunk_size)
 
     def chunk(self, thread: Thread) -> list[Chunk]:
         _require(thread)
@@ -129,6 +136,8 @@ class SemanticChunker(ThreadChunker):
     _SENT = re.compile(r"(?<=[.!?])\s+")
 
     def __init__(self, target_chunk_size: int = 400, split_on_speaker: bool = False):
+        if target_chunk_size <= 0:
+            raise ValueError("target_chunk_size must be positive")
         self.target_chunk_size = int(target_chunk_size)
         self.split_on_speaker = bool(split_on_speaker)
 
@@ -181,7 +190,7 @@ class SemanticChunker(ThreadChunker):
 
 
 def create_chunker(cfg=None, **overrides) -> ThreadChunker:
-    name = getattr(cfg, "driver_name", cfg) or "token_window"
+    name = str(getattr(cfg, "driver_name", cfg) or "token_window").strip().lower()
     kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
     kw.update(overrides)
     if name == "token_window":

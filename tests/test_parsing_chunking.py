@@ -253,7 +253,7 @@ def test_create_chunker_from_config():
         driver_name = "token_window"
         driver_config = {"chunk_size": 10, "overlap": 2, "min_chunk_size": None}
     c = create_chunker(Cfg)
-    assert isinstance(c, TokenWindowChunker) and c.chunk_size == 10 and c.min_chunk_size == 100
+    assert isinstance(c, TokenWindowChunker) and c.chunk_size == 10 and c.min_chunk_size == 10   # clamped
     assert isinstance(create_chunker("semantic", split_on_speaker=True), SemanticChunker)
     assert isinstance(create_chunker("fixed_size"), FixedSizeChunker)
     with pytest.raises(ValueError):
@@ -390,3 +390,33 @@ def test_mbox_separator_blank_line_is_not_body():
     assert one.endswith(b"body one\n") and two.endswith(b"body two\n")
     crlf = split_mbox(mb.replace(b"\n", b"\r\n"))
     assert crlf[0].endswith(b"body one\r\n\r\n")
+
+
+@pytest.mark.parametrize("kw", [{"chunk_size": 0}, {"chunk_size": 10, "overlap": -1}])
+def test_token_window_rejects_word_dropping_parameters(kw):
+    with pytest.raises(ValueError):
+        TokenWindowChunker(**kw)
+
+
+def test_chunker_validation_and_case_insensitive_factory():
+    with pytest.raises(ValueError):
+        SemanticChunker(target_chunk_size=0)
+    with pytest.raises(ValueError):
+        FixedSizeChunker(messages_per_chunk=0)
+    assert isinstance(create_chunker("Token_Window"), TokenWindowChunker)
+    assert isinstance(create_chunker(" SEMANTIC "), SemanticChunker)
+    with pytest.raises(ValueError):
+        create_chunker("paragraph")
+    t = Thread(thread_id="t", text="   \n  ", metadata={}, message_doc_id="m")
+    for ch in (TokenWindowChunker(), SemanticChunker()):
+        with pytest.raises(ValueError):
+            ch.chunk(t)
+    with pytest.raises(ValueError):
+        TokenWindowChunker().chunk(Thread(thread_id="t", text="words here", metadata={}, message_doc_id=None))
+
+
+def test_small_window_below_default_minimum_keeps_every_word():
+    words = [f"w{i}" for i in range(95)]
+    ch = TokenWindowChunker(chunk_size=20, overlap=5)          # default min_chunk_size 100 > 20
+    out = ch.chunk(Thread(thread_id="t", text=" ".join(words), metadata={}, message_doc_id="m"))
+    assert len(out) > 1 and {w for c in out for w in c.text.split()} == set(words)
