@@ -729,6 +729,16 @@ __device__ __forceinline__ float pair_sum(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
+// reductions over the 4 lanes l, l^16, l^32, l^48 (one MFMA 16x16 output column): two VALU
+// permlane swaps instead of two ds_bpermute round trips
+__device__ __forceinline__ float quad_max(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return pair_max(fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1])));
+}
+__device__ __forceinline__ float quad_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return pair_sum(__uint_as_float(r[0]) + __uint_as_float(r[1]));
+}
 __device__ __forceinline__ int v5_off(int d, int c) { return d * 128 + ((c ^ ((d >> 1) & 7) ^ ((d & 1) << 2)) << 4); }
 
 template <int G, bool F8 = false>
@@ -976,29 +986,9 @@ __global__ void __launch_bounds__(256) encoder_attn_kernel(const uint16_t* __res
   // V^T element (d, slot): row d has Spad*2 bytes; 16-byte chunk c = slot>>3 swizzled by d&15.
   auto voff_chunk = [&](int d, int c) -> int { return d * Spad * 2 + ((c ^ (d & 15)) << 4); };
 
-  for (int id = tid; id < Spad * NC; id += 256) {
-    const int r = id / NC, ch = id % NC;
-    uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-    if (r < S) {
-      const uint16_t* base = qkv + (size_t)(beg + r) * row_stride;
-      kv = *reinterpret_cast<const uint4*>(base + H * D + h * D + ch * 8);
-      vv = *reinterpret_cast<const uint4*>(base + 2 * H * D + h * D + ch * 8);
-    }
-    *reinterpret_cast<uint4*>(klds + koff(r, ch)) = kv;
-    // scatter V row r (d = ch*8 .. +7) into V^T at the permuted slot of key r
-    const int kin = r & 31, hi = kin >> 4, gg = (kin >> 2) & 3, jj = (kin & 3) + 4 * hi;
-    const int slot = (r & ~31) + 8 * gg + jj;
-    const uint16_t* ve = reinterpret_cast<const uint16_t*>(&vv);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int d = ch * 8 + e;
-      *reinterpret_cast<uint16_t*>(vlds + voff_chunk(d, slot >> 3) + (slot & 7) * 2) = ve[e];
-    }
-  }
-
-  // this wave's row groups that hold at least one row of the sequence (wave-uniform)
+  // Q fragments first (pre-scaled), so their loads overlap the K/V staging below
   const int wrow0 = qs + 64 * w;
-  const int ng = min(ENC_R, max(0, (S - wrow0 + 15) >> 4));
+  const int ng = min(ENC_R, max(0, (S - wrow0 + 15) >> 4));   // row groups with >= 1 row (wave-uniform)
   bf16x8_t qf[ENC_R][KSTEPS];
 #pragma unroll
   for (int rg = 0; rg < ENC_R; ++rg) {
@@ -1014,6 +1004,40 @@ __global__ void __launch_bounds__(256) encoder_attn_kernel(const uint16_t* __res
       u.z = pack2bf(f[4] * scale_log2, f[5] * scale_log2);
       u.w = pack2bf(f[6] * scale_log2, f[7] * scale_log2);
       qf[rg][c] = as_bf16x8(u);
+    }
+  }
+
+  // K / V staging: every thread issues SB chunk loads of K and of V before any LDS write, so one
+  // memory round trip covers SB chunks (a load -> write -> load loop pays the latency per chunk)
+  constexpr int SB = 4;
+  const int nchunks = Spad * NC;
+  for (int id0 = tid; id0 < nchunks; id0 += 256 * SB) {
+    uint4 kv[SB], vv[SB];
+#pragma unroll
+    for (int b = 0; b < SB; ++b) {
+      const int id = id0 + 256 * b, r = id / NC, ch = id % NC;
+      kv[b] = make_uint4(0, 0, 0, 0);
+      vv[b] = make_uint4(0, 0, 0, 0);
+      if (id < nchunks && r < S) {
+        const uint16_t* base = qkv + (size_t)(beg + r) * row_stride;
+        kv[b] = *reinterpret_cast<const uint4*>(base + H * D + h * D + ch * 8);
+        vv[b] = *reinterpret_cast<const uint4*>(base + 2 * H * D + h * D + ch * 8);
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < SB; ++b) {
+      const int id = id0 + 256 * b, r = id / NC, ch = id % NC;
+      if (id >= nchunks) break;
+      *reinterpret_cast<uint4*>(klds + koff(r, ch)) = kv[b];
+      // scatter V row r (d = ch*8 .. +7) into V^T at the permuted slot of key r
+      const int kin = r & 31, hi = kin >> 4, gg = (kin >> 2) & 3, jj = (kin & 3) + 4 * hi;
+      const int slot = (r & ~31) + 8 * gg + jj;
+      const uint16_t* ve = reinterpret_cast<const uint16_t*>(&vv[b]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int d = ch * 8 + e;
+        *reinterpret_cast<uint16_t*>(vlds + voff_chunk(d, slot >> 3) + (slot & 7) * 2) = ve[e];
+      }
     }
   }
   __syncthreads();
@@ -1061,8 +1085,7 @@ __global__ void __launch_bounds__(256) encoder_attn_kernel(const uint16_t* __res
       }
       float tmax = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
                          fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax = quad_max(tmax);
       const float mn = fmaxf(m[rg], tmax);
       const float alpha = __builtin_amdgcn_exp2f(m[rg] - mn);
       float rs = 0.f;
@@ -1074,8 +1097,7 @@ __global__ void __launch_bounds__(256) encoder_attn_kernel(const uint16_t* __res
           sc[st][i] = e;
           rs += e;
         }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
+      rs = quad_sum(rs);
       l[rg] = l[rg] * alpha + rs;
       m[rg] = mn;
       const bf16x8_t pf = pack_p(sc[0], sc[1]);
