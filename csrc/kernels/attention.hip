@@ -746,14 +746,22 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ kc, const void* __restrict__ vc,
     const int32_t* __restrict__ block_tables, const int32_t* __restrict__ cu_q, const int32_t* __restrict__ ctx_lens,
     const int32_t* __restrict__ tile_seq, const int32_t* __restrict__ tile_q0, float scale_log2, int Hq, int Hkv,
-    int max_blocks, int window, float v_scale, uint16_t* __restrict__ out) {
+    int max_blocks, int window, float v_scale, int xcd_local, uint16_t* __restrict__ out) {
   // F8: e4m3 caches (K / k_scale folded into scale_log2 by the host, V / v_scale rescaled at the
   // output); tiles are widened to bf16 at the LDS write, so the MFMA loop is the bf16 one
   constexpr int D = 128;
   constexpr int QR = 256 / G;      // query rows per tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // LDS: [K buf0 16K][K buf1 16K][V buf0 16K][V buf1 16K]
-  const int t = blockIdx.x, hk = blockIdx.y;
+  // xcd_local: the (tile, kv-head) grid is XCD-remapped so each XCD takes a contiguous run of the
+  // kv-head-major order -- with Hkv a multiple of 8 one XCD serves whole kv-heads and its L2 holds
+  // only their K/V, instead of every XCD touching every head's K/V
+  int t = blockIdx.x, hk = blockIdx.y;
+  if (xcd_local) {
+    const int lin = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+    hk = lin / gridDim.x;
+    t = lin - hk * gridDim.x;
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
   const int l32 = lane & 31, hi = lane >> 5;
   const int hq = hk * G + (w % G);
@@ -1186,6 +1194,10 @@ static int prefill_variant() {
   static const int v = [] { const char* e = getenv("CFC_PREFILL_VARIANT"); return e ? atoi(e) : 5; }();
   return v;
 }
+static int prefill_xcd_local() {
+  static const int v = [] { const char* e = getenv("CFC_PREFILL_XCD"); return e ? atoi(e) : 1; }();
+  return v;
+}
 
 // Query rows per tile the default prefill kernel expects for Hq / Hkv heads (the host tiler's
 // granularity): 256 / G on the GQA-packed kernel, else PF_ROWS.
@@ -1208,7 +1220,7 @@ CFC_API int cfc_prefill_attention(const void* q, const void* k_cache, const void
 #define PF_ARGS (const uint16_t*)q, (const uint16_t*)k_cache, (const uint16_t*)v_cache, block_tables, cu_q, ctx_lens, \
     tile_seq, tile_q0, scale * LOG2E, Hq, Hkv, max_blocks, (uint16_t*)out
 #define PF5_ARGS (const uint16_t*)q, k_cache, v_cache, block_tables, cu_q, ctx_lens, \
-    tile_seq, tile_q0, scale * LOG2E, Hq, Hkv, max_blocks, window, 1.f, (uint16_t*)out
+    tile_seq, tile_q0, scale * LOG2E, Hq, Hkv, max_blocks, window, 1.f, prefill_xcd_local(), (uint16_t*)out
   if (tile_rows != PF_ROWS || (G * tile_rows == 256 && prefill_variant() == 5)) {
     // 5: GQA-packed 8-wave kernel (default)
     const dim3 grid(n_tiles, Hkv);
@@ -1246,7 +1258,7 @@ CFC_API int cfc_prefill_attention_fp8(const void* q, const void* k_cache, const 
   if (n_tiles <= 0) return 0;
   const dim3 grid(n_tiles, Hkv);
 #define PF8_ARGS (const uint16_t*)q, k_cache, v_cache, block_tables, cu_q, ctx_lens, tile_seq, tile_q0, \
-    scale * k_scale * LOG2E, Hq, Hkv, max_blocks, window, v_scale, (uint16_t*)out
+    scale * k_scale * LOG2E, Hq, Hkv, max_blocks, window, v_scale, prefill_xcd_local(), (uint16_t*)out
   switch (G) {
     case 1: prefill_gqa_kernel<1, true><<<grid, 512, 65536, stream>>>(PF8_ARGS); break;
     case 2: prefill_gqa_kernel<2, true><<<grid, 512, 65536, stream>>>(PF8_ARGS); break;
