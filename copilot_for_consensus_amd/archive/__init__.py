@@ -225,7 +225,7 @@ class DocumentStoreArchiveStore(ArchiveStore):
 
 
 def create_archive_store(cfg=None) -> ArchiveStore:
-    name = getattr(cfg, "driver_name", cfg) or "local"
+    name = str(getattr(cfg, "driver_name", cfg) or "local").strip().lower()
     kw = dict(getattr(cfg, "driver_config", {}) or {})
     if name == "local":
         return LocalVolumeArchiveStore(**{k: v for k, v in kw.items() if v is not None})

@@ -20,8 +20,8 @@ def _driver(cfg):
     if cfg is None:
         return "inproc", {}
     if isinstance(cfg, str):
-        return cfg, {}
-    return cfg.driver_name, dict(cfg.driver_config)
+        return cfg.strip().lower(), {}
+    return str(cfg.driver_name).strip().lower(), dict(cfg.driver_config)
 
 
 def create_publisher(cfg=None, enable_validation: bool = True, broker: InProcBroker | None = None,

@@ -111,6 +111,8 @@ def load_adapter_config(adapter: str, env: Mapping[str, str] | None = None, driv
     field, disc_env, default_driver, drivers = specs.ADAPTERS[adapter]
     if driver is None:
         driver = env.get(disc_env, default_driver) if disc_env else default_driver
+    if isinstance(driver, str):
+        driver = driver.strip().lower()      # VECTOR_STORE_TYPE=Qdrant selects the qdrant driver
     if driver is not None and driver not in drivers:
         raise ConfigError(f"{adapter}: unknown driver {driver!r} ({disc_env}); choose one of {sorted(drivers)}")
     cfg: dict[str, Any] = {}

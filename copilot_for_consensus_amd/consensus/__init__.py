@@ -270,7 +270,7 @@ class MLConsensusDetector(ConsensusDetector, _Ladder):
 
 
 def create_consensus_detector(cfg=None, **overrides) -> ConsensusDetector:
-    name = getattr(cfg, "driver_name", cfg) or "heuristic"
+    name = str(getattr(cfg, "driver_name", cfg) or "heuristic").strip().lower()
     kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
     kw.update(overrides)
     if name == "heuristic":

@@ -159,7 +159,7 @@ class MockDiffProvider(DraftDiffProvider):
 
 
 def create_draft_diff_provider(cfg=None, **overrides) -> DraftDiffProvider:
-    name = getattr(cfg, "driver_name", cfg) or "mock"
+    name = str(getattr(cfg, "driver_name", cfg) or "mock").strip().lower()
     kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
     kw.update(overrides)
     if name == "datatracker":

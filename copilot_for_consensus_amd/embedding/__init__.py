@@ -237,7 +237,7 @@ class OpenAIEmbeddingProvider(EmbeddingProvider):
 
 
 def create_embedding_provider(cfg=None, **overrides) -> EmbeddingProvider:
-    name = getattr(cfg, "driver_name", cfg) or "hip"
+    name = str(getattr(cfg, "driver_name", cfg) or "hip").strip().lower()
     kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
     kw.update(overrides)
     if name == "hip":

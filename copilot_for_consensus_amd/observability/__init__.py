@@ -83,7 +83,7 @@ _default_logger: Logger | None = None
 
 
 def create_logger(cfg=None, **overrides) -> Logger:
-    name = getattr(cfg, "driver_name", cfg) or "stdout"
+    name = str(getattr(cfg, "driver_name", cfg) or "stdout").strip().lower()
     kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
     kw.update(overrides)
     cls = {"stdout": StdoutLogger, "silent": SilentLogger}.get(name)
@@ -273,7 +273,7 @@ class PushGatewayMetricsCollector(PrometheusMetricsCollector):
 
 
 def create_metrics_collector(cfg=None, **overrides) -> MetricsCollector:
-    name = getattr(cfg, "driver_name", cfg) or "noop"
+    name = str(getattr(cfg, "driver_name", cfg) or "noop").strip().lower()
     kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
     kw.update(overrides)
     if name == "noop":
@@ -339,7 +339,7 @@ class SentryErrorReporter(ErrorReporter):
 
 
 def create_error_reporter(cfg=None, **overrides) -> ErrorReporter:
-    name = getattr(cfg, "driver_name", cfg) or "console"
+    name = str(getattr(cfg, "driver_name", cfg) or "console").strip().lower()
     kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
     kw.update(overrides)
     if name == "console":

@@ -114,6 +114,7 @@ class TopKCohesiveSelector(TopKRelevanceSelector):
 
 
 def create_context_selector(strategy: str = "top_k_relevance"):
+    strategy = str(strategy).strip().lower()
     if strategy in ("top_k_relevance", "topk", "relevance"):
         return TopKRelevanceSelector()
     if strategy in ("top_k_cohesive", "cohesive"):

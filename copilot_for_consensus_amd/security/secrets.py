@@ -78,7 +78,7 @@ class EnvSecretProvider(SecretProvider):
 
 
 def create_secret_provider(cfg=None, **overrides) -> SecretProvider:
-    name = getattr(cfg, "driver_name", cfg) or "local"
+    name = str(getattr(cfg, "driver_name", cfg) or "local").strip().lower()
     kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
     kw.update(overrides)
     if name == "local":

@@ -643,7 +643,7 @@ class MongoDocumentStore(DocumentStore):
 
 
 def create_document_store(cfg=None, enable_validation: bool = False, strict: bool = True) -> DocumentStore:
-    name = getattr(cfg, "driver_name", cfg) or "inmemory"
+    name = str(getattr(cfg, "driver_name", cfg) or "inmemory").strip().lower()
     kw = dict(getattr(cfg, "driver_config", {}) or {})
     if name == "inmemory":
         store: DocumentStore = InMemoryDocumentStore()

@@ -251,7 +251,7 @@ class OpenAISummarizer(Summarizer):
 
 
 def create_llm_backend(cfg=None, **overrides) -> Summarizer:
-    name = getattr(cfg, "driver_name", cfg) or "hip"
+    name = str(getattr(cfg, "driver_name", cfg) or "hip").strip().lower()
     kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
     kw.update(overrides)
     if name == "hip":

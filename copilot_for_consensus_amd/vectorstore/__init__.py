@@ -430,7 +430,7 @@ class HipIVFIndex(HipFlatIndex):
 
 
 def create_vector_store(cfg=None, **overrides) -> VectorStore:
-    name = getattr(cfg, "driver_name", cfg) or "hip"
+    name = str(getattr(cfg, "driver_name", cfg) or "hip").strip().lower()
     kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
     kw.update(overrides)
     if kw.get("index_type", "flat") not in ("flat", "ivf"):

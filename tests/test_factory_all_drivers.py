@@ -82,3 +82,29 @@ def test_factory_builds_every_driver(adapter, driver, tmp_path, monkeypatch):
 
 def test_every_adapter_has_a_factory():
     assert {a for a in specs.ADAPTERS if a not in ("event_retry", "oidc_providers")} <= set(_factories())
+
+
+@pytest.mark.parametrize("factory,name,cls", [
+    ("copilot_for_consensus_amd.consensus:create_consensus_detector", "Heuristic", "HeuristicConsensusDetector"),
+    ("copilot_for_consensus_amd.draft_diff:create_draft_diff_provider", "MOCK", "MockDiffProvider"),
+    ("copilot_for_consensus_amd.observability:create_metrics_collector", "Prometheus", "PrometheusMetricsCollector"),
+    ("copilot_for_consensus_amd.observability:create_logger", "Silent", "SilentLogger"),
+    ("copilot_for_consensus_amd.observability:create_error_reporter", " Console ", "ConsoleErrorReporter"),
+    ("copilot_for_consensus_amd.storage.document_store:create_document_store", "InMemory", "InMemoryDocumentStore"),
+    ("copilot_for_consensus_amd.vectorstore:create_vector_store", "InMemory", "InMemoryVectorStore"),
+    ("copilot_for_consensus_amd.chunking:create_chunker", "Semantic", "SemanticChunker"),
+    ("copilot_for_consensus_amd.summarization:create_llm_backend", "Mock", "MockSummarizer"),
+    ("copilot_for_consensus_amd.orchestration:create_context_selector", "Top_K_Cohesive", "TopKCohesiveSelector"),
+    ("copilot_for_consensus_amd.bus:create_publisher", "NOOP", "ValidatingEventPublisher"),
+])
+def test_factories_accept_any_case(factory, name, cls):
+    """The reference's factories lower-case the driver name (test_create_*_case_insensitive)."""
+    import importlib
+    mod, fn = factory.split(":")
+    obj = getattr(importlib.import_module(mod), fn)(name)
+    assert type(obj).__name__ == cls
+
+
+def test_config_discriminant_is_case_insensitive():
+    from copilot_for_consensus_amd.config.loader import load_adapter_config
+    assert load_adapter_config("vector_store", env={"VECTOR_STORE_TYPE": "Qdrant"}).driver_name == "qdrant"
