@@ -178,11 +178,29 @@ class HipLLMSummarizer(Summarizer):
 
 
 class _HTTPSummarizer(Summarizer):
+    """Shared HTTP behaviour of the Ollama / llama.cpp drivers (reference local_llm_summarizer.py,
+    llamacpp_summarizer.py): timeouts, connection and HTTP errors raise (infrastructure failures
+    the service retries); an empty completion degrades to a fallback text with 0 completion tokens."""
+
+    @staticmethod
+    def _check_timeout(timeout):
+        if timeout is None or float(timeout) <= 0:
+            raise ValueError(f"timeout must be a positive number of seconds, got {timeout!r}")
+        return float(timeout)
+
     def _post(self, url, payload, timeout):
         import requests
-        r = requests.post(url, json=payload, timeout=timeout)
+        r = requests.post(url, json=payload, timeout=timeout, headers={"Content-Type": "application/json"})
         r.raise_for_status()
         return r.json()
+
+    def _summary(self, thread, text, t0):
+        if not text:
+            return Summary(thread.thread_id, f"Unable to generate summary for thread {thread.thread_id}", [],
+                           self.backend, self.model, len(thread.prompt.split()), 0,
+                           int(1000 * (time.perf_counter() - t0)))
+        return Summary(thread.thread_id, text, [], self.backend, self.model, len(thread.prompt.split()),
+                       len(text.split()), int(1000 * (time.perf_counter() - t0)))
 
 
 class LocalLLMSummarizer(_HTTPSummarizer):
@@ -191,15 +209,16 @@ class LocalLLMSummarizer(_HTTPSummarizer):
 
     def __init__(self, local_llm_model="mistral", local_llm_endpoint="http://ollama:11434",
                  local_llm_timeout_seconds=300, **_):
-        self.model, self.endpoint, self.timeout = local_llm_model, local_llm_endpoint, local_llm_timeout_seconds
+        if not local_llm_model or not local_llm_endpoint:
+            raise ValueError("local LLM driver needs local_llm_model and local_llm_endpoint")
+        self.model, self.endpoint = local_llm_model, str(local_llm_endpoint).rstrip("/")
+        self.timeout = self._check_timeout(local_llm_timeout_seconds)
 
     def summarize(self, thread):
         t0 = time.perf_counter()
         d = self._post(f"{self.endpoint}/api/generate", {"model": self.model, "prompt": thread.prompt,
                                                           "stream": False}, self.timeout)
-        text = d.get("response", "")
-        return Summary(thread.thread_id, text, [], self.backend, self.model, len(thread.prompt.split()),
-                       len(text.split()), int(1000 * (time.perf_counter() - t0)))
+        return self._summary(thread, d.get("response", ""), t0)
 
 
 class LlamaCppSummarizer(_HTTPSummarizer):
@@ -208,15 +227,16 @@ class LlamaCppSummarizer(_HTTPSummarizer):
 
     def __init__(self, llamacpp_model="mistral", llamacpp_endpoint="http://llama-cpp:8081",
                  llamacpp_timeout_seconds=300, **_):
-        self.model, self.endpoint, self.timeout = llamacpp_model, llamacpp_endpoint, llamacpp_timeout_seconds
+        if not llamacpp_model or not llamacpp_endpoint:
+            raise ValueError("llama.cpp driver needs llamacpp_model and llamacpp_endpoint")
+        self.model, self.endpoint = llamacpp_model, str(llamacpp_endpoint).rstrip("/")
+        self.timeout = self._check_timeout(llamacpp_timeout_seconds)
 
     def summarize(self, thread):
         t0 = time.perf_counter()
         d = self._post(f"{self.endpoint}/completion", {"prompt": thread.prompt, "n_predict": 512, "temperature": 0.7,
                                                         "stop": ["</s>", "\n\n\n"]}, self.timeout)
-        text = d.get("content", "")
-        return Summary(thread.thread_id, text, [], self.backend, self.model, len(thread.prompt.split()),
-                       len(text.split()), int(1000 * (time.perf_counter() - t0)))
+        return self._summary(thread, d.get("content", ""), t0)
 
 
 class OpenAISummarizer(Summarizer):
