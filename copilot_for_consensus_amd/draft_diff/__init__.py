@@ -158,10 +158,26 @@ class MockDiffProvider(DraftDiffProvider):
                          f"mock://{draft_name}/{version_a}..{version_b}", {"mock": True, "generated": True})
 
 
+_CUSTOM_PROVIDERS: dict[str, type] = {}
+
+
+def register_draft_diff_provider(name: str, provider_class: type) -> None:
+    """Plug in a provider under a driver name (reference factory.py register_provider): the class
+    must subclass :class:`DraftDiffProvider`; it is built with the driver config as keyword args."""
+    if not (isinstance(provider_class, type) and issubclass(provider_class, DraftDiffProvider)):
+        raise TypeError(f"{provider_class!r} is not a DraftDiffProvider subclass")
+    key = str(name).strip().lower()
+    if not key:
+        raise ValueError("provider name must be non-empty")
+    _CUSTOM_PROVIDERS[key] = provider_class
+
+
 def create_draft_diff_provider(cfg=None, **overrides) -> DraftDiffProvider:
     name = str(getattr(cfg, "driver_name", cfg) or "mock").strip().lower()
     kw = {k: v for k, v in dict(getattr(cfg, "driver_config", {}) or {}).items() if v is not None}
     kw.update(overrides)
+    if name in _CUSTOM_PROVIDERS:
+        return _CUSTOM_PROVIDERS[name](**kw)
     if name == "datatracker":
         return DatatrackerDiffProvider(**{k: kw[k] for k in ("base_url", "diff_format", "fetch", "timeout") if k in kw})
     if name == "mock":

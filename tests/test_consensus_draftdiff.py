@@ -114,3 +114,23 @@ def test_local_diff_provider(tmp_path):
     (tmp_path / "draft-a-b-01.txt").write_text("y\n")
     d = create_draft_diff_provider("local", root=str(tmp_path)).getdiff("draft-a-b", "00", "01")
     assert d.source == "local" and "-x" in d.content and "+y" in d.content
+
+
+def test_register_custom_draft_diff_provider():
+    from copilot_for_consensus_amd.draft_diff import (DraftDiff, DraftDiffProvider, create_draft_diff_provider,
+                                                      register_draft_diff_provider)
+
+    class Echo(DraftDiffProvider):
+        def __init__(self, prefix="x"):
+            self.prefix = prefix
+
+        def getdiff(self, draft_name, version_a, version_b):
+            return DraftDiff(draft_name, version_a, version_b, "text", f"{self.prefix}:{draft_name}", "echo")
+
+    register_draft_diff_provider("Echo", Echo)
+    p = create_draft_diff_provider("echo", prefix="p")
+    assert isinstance(p, Echo) and p.getdiff("draft-a", "00", "01").content == "p:draft-a"
+    with pytest.raises(TypeError):
+        register_draft_diff_provider("bad", dict)
+    with pytest.raises(ValueError):
+        register_draft_diff_provider(" ", Echo)
