@@ -82,19 +82,22 @@ def main(argv=None):
         if dev.type == "cuda":   # CPU rehearsal (tests/test_bench_contract_cpu.py) has no device to sync
             torch.cuda.synchronize(dev)
 
-    t = time.perf_counter()
-    for i, r in enumerate(pipe.run_steps(list(range(args.warmup)), overlap=not args.no_overlap)):
-        if rank == 0:
-            print(f"[bench] warmup {i}: {r.summary()}", file=sys.stderr, flush=True)
+    def progress(kind):
+        # one stderr line per finished step on rank 0 (a long timed loop stays visibly alive);
+        # stdout carries only the final JSON line
+        def report(i, r):
+            if rank == 0:
+                print(f"[bench] {kind} {i}: {r.summary()}", file=sys.stderr, flush=True)
+        return report
+
+    pipe.run_steps(list(range(args.warmup)), overlap=not args.no_overlap, on_step=progress("warmup"))
 
     barrier()
     t0 = time.perf_counter()
-    results = pipe.run_steps(list(range(args.warmup, args.warmup + args.steps)), overlap=not args.no_overlap)
+    results = pipe.run_steps(list(range(args.warmup, args.warmup + args.steps)), overlap=not args.no_overlap,
+                             on_step=progress("step"))
     barrier()
     elapsed = time.perf_counter() - t0
-    if rank == 0:
-        for i, r in enumerate(results):
-            print(f"[bench] step {i}: {r.summary()}", file=sys.stderr, flush=True)
 
     # one report per DP replica: TP followers ran the same threads as their leader
     lead = groups.tp_rank == 0

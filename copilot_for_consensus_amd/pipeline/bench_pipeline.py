@@ -131,7 +131,7 @@ class BenchPipeline:
             ctx = self.rag.prepare(self.threads_per_step, step)
         return t0, ctx, ctx.prompts, dict(ctx.stage_s)
 
-    def run_steps(self, steps: list[int], overlap: bool = True) -> list[StepResult]:
+    def run_steps(self, steps: list[int], overlap: bool = True, on_step=None) -> list[StepResult]:
         """Run batches back to back.  With ``overlap`` the CPU + encoder stages of batch i+1 run on
         a worker thread (and a side HIP stream) while batch i is in the LLM; batch 0 is prepared
         inline so exactly the listed batches' work happens inside the caller's timing window."""
@@ -166,6 +166,8 @@ class BenchPipeline:
                 n_thr = 0 if self.follower else len(prompts)  # a TP group counts its threads once
                 results.append(StepResult(n_thr, [t3 - t0] * n_thr, sum(len(t) for t in res.tokens),
                                           sum(res.prompt_lens), stages))
+                if on_step is not None:   # progress report (host-side print, no device sync)
+                    on_step(n, results[-1])
                 if fut is not None:
                     pending = fut.result()
                 elif n + 1 < len(steps):
