@@ -308,3 +308,29 @@ def test_health_reports_scheduler_and_sources(env):
         assert c.get("/health").json()["scheduler_running"] is True
     finally:
         svc.scheduler.stop()
+
+
+from hypothesis import given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.text(max_size=400))
+def test_sanitize_filename_properties(raw):
+    """Upload names (reference fuzzing/corpus/filenames): whatever arrives, the stored name has no
+    path component, no leading dot, only [A-Za-z0-9._-], at most 255 characters, never empty."""
+    import re
+    name = sanitize_filename(raw)
+    assert name and len(name) <= 255
+    assert "/" not in name and "\\\\" not in name and not name.startswith(".")
+    assert re.fullmatch(r"[A-Za-z0-9._-]+", name)
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.text(max_size=60))
+def test_source_names_never_escape_the_archive_directory(name):
+    try:
+        cfg = SourceConfig.from_mapping({"name": name, "source_type": "local", "url": "/x"})
+    except (ValueError, TypeError):
+        return
+    assert "/" not in cfg.name and "\\\\" not in cfg.name and cfg.name.strip() not in (".", "..")
