@@ -7,7 +7,6 @@ from __future__ import annotations
 
 import os
 import shutil
-import threading
 import time
 
 import pytest
@@ -241,7 +240,7 @@ def test_scheduler_lifecycle(env):
         time.sleep(0.01)
     assert sch.runs == 1 and len(pub.get_events("ArchiveIngested")) == 1   # first run is immediate
     assert sch.stop() is True and not sch.is_running
-    assert [t for t in threading.enumerate() if t.name == "ingestion-scheduler"] == []
+    assert not sch._thread.is_alive()
 
 
 def test_scheduler_survives_errors_and_repeats(env):
