@@ -50,7 +50,11 @@ class Logger(ABC):
 
 class StdoutLogger(Logger):
     def __init__(self, level: str = "INFO", name: str | None = None, stream=None, **_):
-        self.level = _LEVELS.get(str(level).upper(), 20)
+        lv = str(level).upper()
+        lv = "WARNING" if lv == "WARN" else lv
+        if lv not in _LEVELS:
+            raise ValueError(f"Invalid log level {level!r}; choose one of {', '.join(_LEVELS)}")
+        self.level = _LEVELS[lv]
         self.name = name or "copilot"
         self.stream = stream or sys.stdout
         self._lock = threading.Lock()
@@ -71,12 +75,23 @@ class StdoutLogger(Logger):
 
 
 class SilentLogger(Logger):
+    """Records instead of printing (tests inspect what a service logged)."""
+
     def __init__(self, **_):
         self.records: list[tuple[str, str, dict]] = []
 
     def log(self, level, message, **kw):
         if len(self.records) < 10000:
-            self.records.append((level, message, kw))
+            self.records.append((str(level).upper(), message, kw))
+
+    def get_logs(self, level: str | None = None) -> list[tuple[str, str, dict]]:
+        return [r for r in self.records if level is None or r[0] == level.upper()]
+
+    def has_log(self, message: str, level: str | None = None) -> bool:
+        return any(message in r[1] for r in self.get_logs(level))
+
+    def clear(self) -> None:
+        self.records.clear()
 
 
 _default_logger: Logger | None = None
@@ -97,8 +112,18 @@ def set_default_logger(lg: Logger) -> None:
     _default_logger = lg
 
 
+_fallback_loggers: dict[str | None, Logger] = {}
+
+
 def get_logger(name: str | None = None) -> Logger:
-    return _default_logger or StdoutLogger(name=name)
+    """The process default (``set_default_logger``) if one is set, else a stdout logger cached by
+    name, so modules calling ``get_logger(__name__)`` repeatedly share one instance."""
+    if _default_logger is not None:
+        return _default_logger
+    lg = _fallback_loggers.get(name)
+    if lg is None:
+        lg = _fallback_loggers[name] = StdoutLogger(name=name)
+    return lg
 
 
 def uvicorn_log_config(level: str = "INFO") -> dict:
@@ -107,8 +132,10 @@ def uvicorn_log_config(level: str = "INFO") -> dict:
     return {"version": 1, "disable_existing_loggers": False,
             "formatters": {"json": {"format": fmt}},
             "handlers": {"default": {"class": "logging.StreamHandler", "formatter": "json", "stream": "ext://sys.stdout"}},
+            # access logs at WARNING: health probes and normal requests stay out of the log stream
             "loggers": {"uvicorn": {"handlers": ["default"], "level": level},
-                        "uvicorn.access": {"handlers": ["default"], "level": level, "propagate": False}}}
+                        "uvicorn.error": {"handlers": ["default"], "level": level, "propagate": False},
+                        "uvicorn.access": {"handlers": ["default"], "level": "WARNING", "propagate": False}}}
 
 
 # ------------------------------------------------------------------------------------- metrics

@@ -35,7 +35,7 @@ def test_stdout_logger_fields_and_kv():
 
 
 @pytest.mark.parametrize("level,emitted", [("DEBUG", 4), ("INFO", 3), ("WARNING", 2), ("warning", 2), ("ERROR", 1),
-                                           ("CRITICAL", 0), ("bogus", 3)])
+                                           ("CRITICAL", 0), ("warn", 2)])
 def test_level_filtering(level, emitted):
     buf = io.StringIO()
     lg = StdoutLogger(level=level, stream=buf)
@@ -92,10 +92,28 @@ def test_silent_logger_and_factories():
     assert isinstance(get_logger("x"), StdoutLogger)
 
 
-def test_uvicorn_log_config_is_json():
-    cfg = uvicorn_log_config("WARNING")
-    assert cfg["loggers"]["uvicorn.access"]["level"] == "WARNING"
+def test_invalid_level_raises():
+    with pytest.raises(ValueError, match="Invalid log level"):
+        StdoutLogger(level="LOUD")
+
+
+@pytest.mark.parametrize("level", ["DEBUG", "INFO", "WARNING", "ERROR"])
+def test_uvicorn_log_config(level):
+    cfg = uvicorn_log_config(level)
+    assert cfg["loggers"]["uvicorn.access"]["level"] == "WARNING"      # access noise always suppressed
+    assert cfg["loggers"]["uvicorn"]["level"] == level and cfg["loggers"]["uvicorn.error"]["level"] == level
     assert cfg["formatters"]["json"]["format"].startswith("{")
+
+
+def test_silent_logger_inspection_and_get_logger_cache():
+    s = SilentLogger()
+    s.info("parsed 3 messages")
+    s.error("store down")
+    assert [r[1] for r in s.get_logs("error")] == ["store down"]
+    assert s.has_log("parsed") and not s.has_log("parsed", level="ERROR")
+    s.clear()
+    assert s.get_logs() == []
+    assert get_logger("mod.a") is get_logger("mod.a") and get_logger("mod.a") is not get_logger("mod.b")
 
 
 # ------------------------------------------------------------------ metrics
