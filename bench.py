@@ -45,6 +45,8 @@ def parse_args(argv=None):
     ap.add_argument("--llm-only", action="store_true", help="skip the CPU/encoder/kNN stages (diagnostic)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--kv-max-prompt", type=int, default=4096,
+                    help="prompt tokens per thread the paged KV pool is sized for (x threads x 1.1)")
     ap.add_argument("--index-prefill", type=int, default=1_000_000,
                     help="background vectors resident in the HBM kNN index besides the run's own chunks")
     ap.add_argument("--no-overlap", action="store_true", help="run pipeline stages strictly sequentially")
@@ -72,7 +74,7 @@ def main(argv=None):
                          weight_dtype=args.weights,
                          llm_only=args.llm_only, use_graph=not args.no_graph,
                          seed=args.seed + 7919 * groups.dp_rank, groups=groups if args.tp > 1 else None,
-                         index_prefill=args.index_prefill)
+                         index_prefill=args.index_prefill, kv_max_prompt=args.kv_max_prompt)
 
     pipe.prepare_sources(list(range(args.warmup + args.steps)))
 

@@ -32,7 +32,7 @@ class StepResult:
 class BenchPipeline:
     def __init__(self, model="mistral-7b", encoder="minilm-l6", device="cuda", threads_per_step=128,
                  max_new_tokens=512, tp=1, prefill_tokens=16384, llm_only=False, use_graph=True, seed=0,
-                 index_prefill=1_000_000, groups=None, kv_dtype="bf16", weight_dtype="bf16"):
+                 index_prefill=1_000_000, groups=None, kv_dtype="bf16", weight_dtype="bf16", kv_max_prompt=4096):
         from ..models.decoder import DecoderModel, DecoderWeights, get_config
         from ..runtime.engine import LLMEngine
         from ..runtime.kv_cache import PagedKVCache, blocks_needed
@@ -60,8 +60,9 @@ class BenchPipeline:
             from ..parallel.custom_ar import maybe_create
             custom_ar = maybe_create(groups.tp_group, self.device, exchange_group=groups.tp_cpu_group)
         self.model = DecoderModel(w, tp_group=groups.tp_group if tp > 1 else None, custom_ar=custom_ar)
-        # KV budget: every thread of a step at the longest prompt we generate (3k) + max_new, x1.1
-        max_prompt = 4096
+        # KV budget: every thread of a step at ``kv_max_prompt`` prompt tokens + max_new, x1.1 (the
+        # prompts this pipeline builds stay near 2.6k; a 70B model on one GPU needs the tighter bound)
+        max_prompt = int(kv_max_prompt)
         nblk = int(1.1 * threads_per_step * blocks_needed(max_prompt + max_new_tokens)) + 64
         kvd = {"bf16": torch.bfloat16, "fp8": torch.float8_e4m3fn}[kv_dtype]
         self.kv = PagedKVCache(self.cfg.layers, nblk, w.kv_heads, self.cfg.head_dim, self.device, dtype=kvd)
