@@ -6,9 +6,11 @@ adapters/copilot_summarization/copilot_summarization/local_llm_summarizer.py:107
 docker-compose.infra.yml:296-298).  Inference only.
 
 MI355X layout choices:
-  * fused weights: one QKV projection [(Hq+2Hkv)*D, H], one gate|up projection [2F, H], so a
-    layer is 4 GEMMs (hipBLASLt) + 4 hand-written HIP kernels (fused residual+RMSNorm x2,
-    RoPE+paged-KV write, attention, SwiGLU);
+  * fused weights: one QKV projection [(Hq+2Hkv)*D, H], one gate|up projection [2F, H] (gate and
+    up rows interleaved in 8-row groups), so a layer is 4 GEMMs + RoPE/paged-KV write + attention
+    + 2 fused split-K-reduce/residual/RMSNorm kernels;
+  * decode (B > 4) projections on the hand-written weight-streaming MFMA GEMM (csrc/kernels/
+    dgemm.hip) with SwiGLU in the gate/up epilogue; B <= 4 on the GEMV; prefill on hipBLASLt;
   * tensor parallel (Megatron column/row split) with one all-reduce after o_proj and one after
     down_proj, vocab-parallel lm_head + all-gather of logits -- see :mod:`..parallel.tp`;
   * weights random-initialised directly on the device (no network: BASELINE "random-init
@@ -117,7 +119,7 @@ class DecoderWeights:
         self.ffn = cfg.ffn // tp_size
         self.vocab_shard = cfg.vocab_size // tp_size
         self.layers: list[dict[str, torch.Tensor]] = []
-        # gate_up rows: [gate; up] (False) or 32-row interleaved groups (True, see interleave_gate_up)
+        # gate_up rows: [gate; up] (False) or 8-row interleaved groups (True, see interleave_gate_up)
         self.gate_up_interleaved = False
         self.embed: torch.Tensor | None = None
         self.final_norm: torch.Tensor | None = None
@@ -273,9 +275,9 @@ class DecoderWeights:
         return w.finalize()
 
     def finalize(self) -> "DecoderWeights":
-        """Put gate/up rows in the 32-row interleaved order the fused decode SwiGLU GEMM reads (the
+        """Put gate/up rows in the 8-row interleaved order the fused decode SwiGLU GEMM reads (the
         prefill path's silu_mul reads the same layout, so one copy of the weights serves both)."""
-        if not self.gate_up_interleaved and self.ffn % 32 == 0:
+        if not self.gate_up_interleaved and self.ffn % 8 == 0:
             for layer in self.layers:
                 layer["gate_up"] = interleave_gate_up(layer["gate_up"])
             self.gate_up_interleaved = True
@@ -336,6 +338,9 @@ def load_config_json(path) -> DecoderConfig:
         sliding_window=int(window) if window else None)
 
 
+DGEMM_MAX_ROWS = 256   # decode batches above this run the library GEMM (one 256-row tile per W pass)
+
+
 class DecoderModel:
     """Stateless forward functions over :class:`DecoderWeights` + a paged KV cache."""
 
@@ -347,15 +352,18 @@ class DecoderModel:
         self.custom_ar = custom_ar
         self.scale = 1.0 / math.sqrt(self.cfg.head_dim)
         self.window = int(self.cfg.sliding_window or 0)
-        # decode projections on the split-K skinny MFMA GEMM with fused epilogues (TP=1; with TP>1
-        # the all-reduce sits between the projection and the residual/norm)
-        # decode GEMM mode (TP=1): "splitk" = library GEMMs, with o/down as batched split-K whose
-        # reduce carries residual+RMSNorm (default); "skinny" = the hand-written split-K kernel
-        # with fused SwiGLU too; "lib" = plain library GEMMs + separate norm kernels
-        mode = os.environ.get("CFC_DECODE_GEMM", "skinny" if os.environ.get("CFC_FUSED_DECODE") == "1" else "splitk")
+        # decode GEMM mode (B > 4): "dgemm" = the hand-written weight-streaming MFMA GEMM with
+        # SwiGLU fused into gate/up and split-K slabs reduced with residual + RMSNorm (default);
+        # "splitk" = library GEMMs with o/down as batched split-K into the same reduce; "lib" =
+        # plain library GEMMs + separate norm kernels
+        mode = os.environ.get("CFC_DECODE_GEMM", "dgemm")
         if fused_decode is not None:
-            mode = "skinny" if fused_decode else "lib"
-        if weights.tp_size != 1 or (mode == "skinny" and not weights.gate_up_interleaved):
+            mode = "dgemm" if fused_decode else "lib"
+        if mode not in ("dgemm", "splitk", "lib"):
+            raise ValueError(f"CFC_DECODE_GEMM={mode!r}: expected dgemm, splitk or lib")
+        if mode == "dgemm" and not (weights.gate_up_interleaved and self._dgemm_shapes()):
+            mode = "splitk"
+        if weights.tp_size != 1 and mode == "splitk":
             mode = "lib"
         self.fp8 = weights.fp8_layers is not None
         if self.fp8:
@@ -363,13 +371,21 @@ class DecoderModel:
         self.decode_gemm = mode
         # B <= 4 decode steps on the GEMV kernel (needs the interleaved gate/up layout for SwiGLU)
         gemv_shapes = (self.cfg.hidden % 8 == 0 and (weights.heads * self.cfg.head_dim) % 8 == 0
-                       and weights.ffn % 32 == 0 and self.cfg.head_dim % 2 == 0)
+                       and weights.ffn % 8 == 0 and self.cfg.head_dim % 2 == 0)
         self.decode_gemv = (os.environ.get("CFC_DECODE_GEMV", "1") != "0" and weights.gate_up_interleaved
-                            and mode == "splitk" and gemv_shapes and not self.fp8)
-        self.fused_decode = mode == "skinny"
+                            and mode in ("splitk", "dgemm") and weights.tp_size == 1 and gemv_shapes
+                            and not self.fp8)
+        self.fused_decode = mode == "dgemm"
         # B <= 4 decode on the ggml-quantized weights (GGUF checkpoints; csrc/kernels/quant.hip)
         self.decode_qgemv = (weights.qlayers is not None and os.environ.get("CFC_DECODE_QGEMV", "1") != "0"
                              and weights.tp_size == 1 and weights.gate_up_interleaved and not self.fp8)
+
+    def _dgemm_shapes(self) -> bool:
+        """Every decode projection of this rank fits the decode GEMM (N % 64, K % 64)."""
+        w, D = self.w, self.cfg.head_dim
+        qkv_n, q_k = (w.heads + 2 * w.kv_heads) * D, w.heads * D
+        return all(n % 64 == 0 for n in (qkv_n, self.cfg.hidden, 2 * w.ffn)) and all(
+            k % 64 == 0 for k in (self.cfg.hidden, q_k, w.ffn))
 
     def _lin(self, i: int, name: str, x: torch.Tensor) -> torch.Tensor:
         """Projection ``name`` of layer ``i``: bf16 library GEMM, or W8A8 FP8 in fp8 mode."""
@@ -436,10 +452,11 @@ class DecoderModel:
         cfg, w = self.cfg, self.w
         x = K.embedding(w.embed, ids)
         B = ids.shape[0]
-        if self.fused_decode and x.is_cuda and B <= K.SKINNY_MAX_M:
+        if (self.fused_decode and x.is_cuda and B <= DGEMM_MAX_ROWS
+                and not (B <= K.GEMV_MAX_M and (self.decode_gemv or self.decode_qgemv))):
             return self._forward_decode_fused(x, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
                                               part_blocks)
-        if self.decode_gemm == "splitk" and x.is_cuda:
+        if self.decode_gemm in ("splitk", "dgemm") and x.is_cuda and self.w.tp_size == 1:
             return self._forward_decode_splitk(x, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
                                                part_blocks)
         residual = None
@@ -457,26 +474,37 @@ class DecoderModel:
         return K.rmsnorm(x, w.final_norm, cfg.rms_eps, residual=residual)
 
     def _forward_decode_fused(self, x, positions, slots, ctx_lens, block_tables, kv, attn_workspace, part_blocks):
-        """Decode layer as 4 skinny GEMMs whose epilogues carry the elementwise work:
+        """Decode layer on the hand-written decode GEMM (dgemm.hip), elementwise work in epilogues:
         qkv -> RoPE/KV write -> attention -> [o + residual + mlp RMSNorm] -> [gate_up + SwiGLU] ->
-        [down + residual + next layer's RMSNorm].  Same rounding points as the unfused path."""
+        [down + residual + next layer's RMSNorm].  Same rounding points as the library path.
+        With TP the row-parallel o/down outputs are all-reduced (one-shot IPC all-reduce inside the
+        decode graph when available) before the residual + RMSNorm."""
         cfg, w = self.cfg, self.w
         B = x.shape[0]
         eps = cfg.rms_eps
         residual = x.clone()
         h = K.rmsnorm(x, w.layers[0]["attn_norm"], eps)
+        tp = w.tp_size > 1
         for i in range(cfg.layers):
             lw = w.layers[i]
-            qkv = K.skinny_linear(h, lw["qkv"])
+            qkv = K.dgemm_linear(h, lw["qkv"])
             q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
                                 cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
             attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
                                             part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
                                             k_scale=kv.k_scale, v_scale=kv.v_scale)
-            h = K.skinny_linear_residual_rmsnorm(attn.view(B, -1), lw["o"], residual, lw["mlp_norm"], eps)
-            a = K.skinny_swiglu(h, lw["gate_up"])
+            if tp:
+                o = self._all_reduce(K.dgemm_linear(attn.view(B, -1), lw["o"]))
+                h = K.rmsnorm(o, lw["mlp_norm"], eps, residual=residual)
+            else:
+                h = K.dgemm_residual_rmsnorm(attn.view(B, -1), lw["o"], residual, lw["mlp_norm"], eps)
+            a = K.dgemm_swiglu(h, lw["gate_up"])
             nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm
-            h = K.skinny_linear_residual_rmsnorm(a, lw["down"], residual, nxt, eps)
+            if tp:
+                d = self._all_reduce(K.dgemm_linear(a, lw["down"]))
+                h = K.rmsnorm(d, nxt, eps, residual=residual)
+            else:
+                h = K.dgemm_residual_rmsnorm(a, lw["down"], residual, nxt, eps)
         return h
 
     def _forward_decode_splitk(self, x, positions, slots, ctx_lens, block_tables, kv, attn_workspace, part_blocks):
@@ -584,6 +612,9 @@ class DecoderModel:
             # (the GEMV takes row pairs and 16-byte K slices: odd vocabularies, e.g. 32001-token
             # fine-tunes, stay on the library GEMM)
             local = K.gemv(hidden, self.w.lm_head)   # 262 MB weight stream: 4.6 -> ~6 TB/s at B=1
+        elif (self.fused_decode and hidden.is_cuda and hidden.shape[0] > K.GEMV_MAX_M
+                and hidden.shape[0] <= DGEMM_MAX_ROWS and K.dgemm_ok(hidden, head)):
+            local = K.dgemm_linear(hidden, head)   # the 262 MB (Mistral) / 1 GB (Llama-3) vocab stream
         else:
             local = F.linear(hidden, self.w.lm_head)
         if self.w.tp_size == 1:

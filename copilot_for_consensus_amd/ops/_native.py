@@ -52,8 +52,10 @@ _KERNEL_SIGS = {
     "cfc_topk_chunk_size": [],
     "cfc_l2_normalize": [P, P, P, I, I, P],
     "cfc_pool": [P, P, P, P, I, I, I, I, P],
-    "cfc_skinny_gemm": [P, P, I, I, I, I, I, P, P, I, P],
     "cfc_splitk_reduce": [P, I, I, I, I, P, I, P],
+    "cfc_dgemm": [P, P, I, I, I, I, I, I, P, P, I, P],
+    "cfc_dgemm_bm": [I],
+    "cfc_dgemm_ablate": [P, P, I, I, I, I, I, I, P, P],
     "cfc_gemv": [P, P, I, I, I, I, P, P, I, P],
     "cfc_qgemv": [P, I, I, I, I, P, P, c_int64, c_int64, c_int64, I, P, P, I, P],
     "cfc_dequant_bf16": [P, I, c_int64, P, P],

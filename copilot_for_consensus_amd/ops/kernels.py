@@ -275,9 +275,8 @@ def encoder_attention(qkv, cu_seqlens, H, D, scale, max_seqlen, tiles=None, out=
     return out
 
 
-# ----------------------------------------------------------------------------- skinny GEMM (decode)
+# ----------------------------------------------------------------------------- decode GEMM helpers
 
-SKINNY_MAX_M = 256          # above this the library GEMMs win (prefill shapes)
 _workspaces: dict = {}
 # Superseded workspaces are never freed: a hipGraph captured while one of them was current keeps
 # its raw pointer and writes fp32 partials through it on every replay.  Growth at least doubles,
@@ -299,81 +298,12 @@ def _workspace(device, numel: int) -> torch.Tensor:
     return ws
 
 
-def skinny_split(M: int, N: int, K: int, target_blocks: int = 512) -> int:
-    """Split-K factor: enough blocks to cover the 256 CUs twice, K slices of whole 64-deep stages."""
-    tiles = (N // 64) * ((M + 127) // 128)
-    stages = K // 64
-    best = 1
-    for s in (1, 2, 4, 7, 8, 14, 16):
-        if stages % s == 0 and tiles * s <= target_blocks * 1.25:
-            best = s
-    return best
-
-
-def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    return (x.is_cuda and x.dim() == 2 and x.shape[0] <= SKINNY_MAX_M and w.shape[0] % 64 == 0
-            and x.shape[1] % 64 == 0 and x.dtype == torch.bfloat16 and x.is_contiguous() and w.is_contiguous())
-
-
-def skinny_linear(x: torch.Tensor, w: torch.Tensor, split: int | None = None, out: torch.Tensor | None = None):
-    """x [M, K] @ w[N, K]^T -> bf16 [M, N] with the decode GEMM (split-K + reduce)."""
-    if not x.is_cuda:
-        return torch.nn.functional.linear(x, w)
-    M, K = x.shape
-    N = w.shape[0]
-    split = split or skinny_split(M, N, K)
-    out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device) if out is None else out
-    st = _stream(x)
-    if split == 1:
-        check(kernels().cfc_skinny_gemm(x.data_ptr(), w.data_ptr(), M, N, K, 1, 1, None, out.data_ptr(), N, st),
-              "cfc_skinny_gemm")
-        return out
-    ws = _workspace(x.device, split * M * N)
-    check(kernels().cfc_skinny_gemm(x.data_ptr(), w.data_ptr(), M, N, K, split, 0, ws.data_ptr(), None, 0, st),
-          "cfc_skinny_gemm")
-    check(kernels().cfc_splitk_reduce(ws.data_ptr(), split, M, N, 0, out.data_ptr(), N, st), "cfc_splitk_reduce")
-    return out
-
-
-def skinny_swiglu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, split: int | None = None):
-    """silu(x @ gate^T) * (x @ up^T) for gate/up weights interleaved in 32-row groups."""
-    if not x.is_cuda:
-        return ref.silu_mul_interleaved(torch.nn.functional.linear(x, w_gu_interleaved))
-    M, K = x.shape
-    N = w_gu_interleaved.shape[0]
-    split = split or skinny_split(M, N, K)
-    out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=x.device)
-    st = _stream(x)
-    if split == 1:
-        check(kernels().cfc_skinny_gemm(x.data_ptr(), w_gu_interleaved.data_ptr(), M, N, K, 1, 2, None,
-                                        out.data_ptr(), N // 2, st), "cfc_skinny_gemm")
-        return out
-    ws = _workspace(x.device, split * M * N)
-    check(kernels().cfc_skinny_gemm(x.data_ptr(), w_gu_interleaved.data_ptr(), M, N, K, split, 0, ws.data_ptr(),
-                                    None, 0, st), "cfc_skinny_gemm")
-    check(kernels().cfc_splitk_reduce(ws.data_ptr(), split, M, N, 1, out.data_ptr(), N // 2, st), "cfc_splitk_reduce")
-    return out
-
-
-def skinny_linear_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor,
-                                   eps: float, split: int | None = None) -> torch.Tensor:
-    """residual += x @ w^T (bf16-rounded projection); returns RMSNorm(residual) * norm_w."""
-    if not x.is_cuda:
-        y = torch.nn.functional.linear(x, w)
-        o, r = ref.rmsnorm(y, norm_w, eps, residual)
-        residual.copy_(r)
-        return o
-    M, K = x.shape
-    N = w.shape[0]
-    split = split or skinny_split(M, N, K)
-    ws = _workspace(x.device, split * M * N)
-    out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-    st = _stream(x)
-    check(kernels().cfc_skinny_gemm(x.data_ptr(), w.data_ptr(), M, N, K, split, 0, ws.data_ptr(), None, 0, st),
-          "cfc_skinny_gemm")
-    check(kernels().cfc_splitk_residual_rmsnorm(ws.data_ptr(), split, M, N, residual.data_ptr(), norm_w.data_ptr(),
-                                                float(eps), out.data_ptr(), st), "cfc_splitk_residual_rmsnorm")
-    return out
+def _linear_residual_rmsnorm_ref(x, w, residual, norm_w, eps):
+    """CPU path: residual += bf16(x @ w^T); returns RMSNorm(residual) * norm_w."""
+    y = torch.nn.functional.linear(x, w)
+    o, r = ref.rmsnorm(y, norm_w, eps, residual)
+    residual.copy_(r)
+    return o
 
 
 def lib_splitk_linear_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, split: int, residual: torch.Tensor,
@@ -383,7 +313,7 @@ def lib_splitk_linear_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, split: 
     one kernel that sums the partials, adds the residual and applies the next RMSNorm:
     residual += bf16(x @ w^T); returns RMSNorm(residual) * norm_w."""
     if not x.is_cuda:
-        return skinny_linear_residual_rmsnorm(x, w, residual, norm_w, eps)
+        return _linear_residual_rmsnorm_ref(x, w, residual, norm_w, eps)
     M, Kd = x.shape
     N = w.shape[0]
     if Kd % split:
@@ -398,12 +328,116 @@ def lib_splitk_linear_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, split: 
     return out
 
 
+# ----------------------------------------------------------------------------- decode GEMM (dgemm.hip)
+
+DGEMM_BNS = (128, 112, 96, 64)   # W rows per workgroup the kernel is built for
+DGEMM_CUS = 256                  # one workgroup per CU
+DGEMM_CU_RATE = 25e9             # W bytes/s one workgroup streams (6.4 TB/s over 256 CUs)
+DGEMM_PART_RATE = 6e12           # fp32 partial slab traffic, bytes/s
+
+
+def dgemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Shapes the decode GEMM takes: bf16, contiguous, N % 64 == 0, K % 64 == 0."""
+    return (x.is_cuda and x.dim() == 2 and w.dim() == 2 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and x.is_contiguous() and w.is_contiguous() and w.shape[1] == x.shape[1]
+            and w.shape[0] % 64 == 0 and x.shape[1] % 64 == 0 and x.shape[0] >= 1)
+
+
+def dgemm_config(M: int, N: int, K: int, swiglu: bool = False) -> tuple[int, int]:
+    """(W rows per workgroup, split-K) for one decode projection, from a two-term cost model:
+    each workgroup streams its W slice at a per-CU rate, in ceil(blocks / CUs) rounds (a partial
+    second round doubles the stream time of the CUs that run it), plus the fp32 partial slabs
+    written and read back once.  A fused SwiGLU epilogue needs split 1."""
+    bm = 64 if M <= 64 else (128 if M <= 128 else 256)
+    mt = (M + bm - 1) // bm
+    best = None
+    for bn in DGEMM_BNS:
+        if N % bn:
+            continue
+        tiles = (N // bn) * mt
+        for split in ([1] if swiglu else range(1, K // 64 + 1)):
+            blocks = tiles * split
+            rounds = -(-blocks // DGEMM_CUS)
+            t = rounds * (N * K * 2 / (N // bn * split)) / DGEMM_CU_RATE
+            if split > 1:
+                t += 2 * split * M * N * 4 / DGEMM_PART_RATE
+            if best is None or t < best[0] - 1e-12:
+                best = (t, bn, split)
+    return best[1], best[2]
+
+
+def dgemm(x: torch.Tensor, w: torch.Tensor, epi: str = "bf16", split: int = 1, bn: int | None = None,
+          out: torch.Tensor | None = None, part: torch.Tensor | None = None) -> torch.Tensor:
+    """One launch of the decode GEMM.  ``epi``: "bf16" -> out [M, N]; "swiglu" -> out [M, N/2]
+    (8-row interleaved gate/up weights); "part" -> fp32 split-K slabs part [split, M, N]."""
+    M, Kd = x.shape
+    N = w.shape[0]
+    if not dgemm_ok(x, w):
+        raise ValueError(f"dgemm: x {tuple(x.shape)} {x.dtype} w {tuple(w.shape)} {w.dtype}")
+    mode = {"part": 0, "bf16": 1, "swiglu": 2}[epi]
+    bn = bn or dgemm_config(M, N, Kd, swiglu=mode == 2)[0]
+    st = _stream(x)
+    if mode == 0:
+        part = _workspace(x.device, split * M * N)[:split * M * N].view(split, M, N) if part is None else part
+        check(kernels().cfc_dgemm(x.data_ptr(), w.data_ptr(), M, N, Kd, split, 0, bn, part.data_ptr(), None, 0, st),
+              "cfc_dgemm")
+        return part
+    if out is None:
+        out = torch.empty(M, N // 2 if mode == 2 else N, dtype=torch.bfloat16, device=x.device)
+    check(kernels().cfc_dgemm(x.data_ptr(), w.data_ptr(), M, N, Kd, 1, mode, bn, None, out.data_ptr(), out.stride(0),
+                              st), "cfc_dgemm")
+    return out
+
+
+def dgemm_linear(x: torch.Tensor, w: torch.Tensor, split: int | None = None, bn: int | None = None) -> torch.Tensor:
+    """bf16 x [M, K] @ w[N, K]^T on the decode GEMM (split-K slabs + reduce when N is small)."""
+    if not x.is_cuda:
+        return torch.nn.functional.linear(x, w)
+    M, Kd = x.shape
+    cbn, csplit = dgemm_config(M, w.shape[0], Kd)
+    bn, split = bn or cbn, split or csplit
+    if split == 1:
+        return dgemm(x, w, "bf16", bn=bn)
+    return splitk_reduce(dgemm(x, w, "part", split, bn=bn))
+
+
+def dgemm_swiglu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, split: int | None = None,
+                 bn: int | None = None) -> torch.Tensor:
+    """silu(x @ gate^T) * (x @ up^T) for 8-row interleaved gate/up weights (SwiGLU in the GEMM's
+    epilogue; split-K slabs + the SwiGLU reduce when asked for a split, e.g. TP-sharded N)."""
+    if not x.is_cuda:
+        return ref.silu_mul_interleaved(torch.nn.functional.linear(x, w_gu_interleaved))
+    M, Kd = x.shape
+    N = w_gu_interleaved.shape[0]
+    if split is None:
+        fbn, _ = dgemm_config(M, N, Kd, swiglu=True)
+        pbn, psplit = dgemm_config(M, N, Kd)
+        # split-K + reduce only when the fused grid would leave most CUs idle
+        use_split = (N // fbn) * ((M + 255) // 256) < DGEMM_CUS // 2 and psplit > 1
+        bn, split = (bn or pbn, psplit) if use_split else (bn or fbn, 1)
+    if split == 1:
+        return dgemm(x, w_gu_interleaved, "swiglu", bn=bn)
+    return splitk_reduce(dgemm(x, w_gu_interleaved, "part", split, bn=bn), swiglu=True)
+
+
+def dgemm_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor,
+                           eps: float, split: int | None = None, bn: int | None = None) -> torch.Tensor:
+    """residual += bf16(x @ w^T); returns RMSNorm(residual) * norm_w.  The split-K slabs go straight
+    into the residual + RMSNorm reduce (same rounding points as the library split-K path)."""
+    if not x.is_cuda:
+        return _linear_residual_rmsnorm_ref(x, w, residual, norm_w, eps)
+    M, Kd = x.shape
+    cbn, csplit = dgemm_config(M, w.shape[0], Kd)
+    bn, split = bn or cbn, split or csplit
+    return splitk_residual_rmsnorm(dgemm(x, w, "part", split, bn=bn), residual, norm_w, eps)
+
+
 GEMV_MAX_M = 4   # decode batches up to this size take the weight-streaming GEMV (gemm.hip: gemv_kernel)
 
 
 def gemv(x: torch.Tensor, w: torch.Tensor, epi: str = "bf16", out: torch.Tensor | None = None) -> torch.Tensor:
     """x [M <= 4, K] @ w[N, K]^T on the GEMV kernel.  ``epi``: "bf16" -> bf16 [M, N]; "f32" -> fp32
-    [M, N]; "swiglu" -> bf16 [M, N/2] = silu(gate) * up for 32-row interleaved gate/up weights."""
+    [M, N]; "swiglu" -> bf16 [M, N/2] = silu(gate) * up for 8-row interleaved gate/up weights."""
     if not x.is_cuda:
         y = torch.nn.functional.linear(x.float(), w.float())
         if epi == "swiglu":
@@ -430,7 +464,7 @@ def gemv_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tens
     """residual += bf16(x @ w^T) via the GEMV (fp32 out) and the split = 1 residual + RMSNorm reduce;
     returns RMSNorm(residual) * norm_w (same rounding points as lib_splitk_linear_residual_rmsnorm)."""
     if not x.is_cuda:
-        return skinny_linear_residual_rmsnorm(x, w, residual, norm_w, eps)
+        return _linear_residual_rmsnorm_ref(x, w, residual, norm_w, eps)
     M, N = x.shape[0], w.shape[0]
     part = _workspace(x.device, M * N)[:M * N].view(M, N)
     gemv(x, w, "f32", out=part)
@@ -667,7 +701,7 @@ def lib_split_for(K: int, N: int) -> int:
 
 
 def silu_mul(gu, out=None, interleaved: bool = False):
-    """silu(gate) * up; ``interleaved``: gate/up in 32-column groups (see ref.interleave_gate_up)."""
+    """silu(gate) * up; ``interleaved``: gate/up in 8-column groups (see ref.interleave_gate_up)."""
     if not gu.is_cuda:
         return ref.silu_mul_interleaved(gu) if interleaved else ref.silu_mul(gu)
     _req(gu, torch.bfloat16, "gu")

@@ -179,22 +179,28 @@ def silu_mul(gu):
     return (torch.nn.functional.silu(g) * u).to(gu.dtype)
 
 
+# gate/up rows of the fused MLP projection are stored interleaved in groups of GU_GROUP rows, so a
+# 16-row MFMA n-tile of the decode GEMM holds 8 gate rows and the 8 matching up rows
+# (csrc/kernels/dgemm.hip SwiGLU epilogue; the prefill silu_mul and the GEMV read the same layout)
+GU_GROUP = 8
+
+
 def interleave_gate_up(gu_w: torch.Tensor) -> torch.Tensor:
-    """[gate; up] rows (2F, H) -> 32-row groups [gate 32t..32t+31; up 32t..32t+31] (F % 32 == 0)."""
-    F = gu_w.shape[0] // 2
-    g, u = gu_w[:F].reshape(F // 32, 32, -1), gu_w[F:].reshape(F // 32, 32, -1)
+    """[gate; up] rows (2F, H) -> 8-row groups [gate 8t..8t+7; up 8t..8t+7] (F % 8 == 0)."""
+    F, G = gu_w.shape[0] // 2, GU_GROUP
+    g, u = gu_w[:F].reshape(F // G, G, -1), gu_w[F:].reshape(F // G, G, -1)
     return torch.stack([g, u], 1).reshape(2 * F, -1).contiguous()
 
 
 def deinterleave_gate_up(w: torch.Tensor) -> torch.Tensor:
-    F = w.shape[0] // 2
-    v = w.reshape(F // 32, 2, 32, -1)
+    F, G = w.shape[0] // 2, GU_GROUP
+    v = w.reshape(F // G, 2, G, -1)
     return torch.cat([v[:, 0].reshape(F, -1), v[:, 1].reshape(F, -1)]).contiguous()
 
 
 def silu_mul_interleaved(gu):
-    F = gu.shape[-1] // 2
-    v = gu.reshape(*gu.shape[:-1], F // 32, 2, 32).float()
+    F, G = gu.shape[-1] // 2, GU_GROUP
+    v = gu.reshape(*gu.shape[:-1], F // G, 2, G).float()
     return (torch.nn.functional.silu(v[..., 0, :]) * v[..., 1, :]).reshape(*gu.shape[:-1], F).to(gu.dtype)
 
 

@@ -1,0 +1,319 @@
+// Decode GEMM for gfx950 at batch sizes 5..256:  Y[M, N] = X[M, K] . W[N, K]^T  (bf16 in, fp32 acc).
+//
+// At decode a projection is a weight stream: W (14-235 MB per projection, the whole layer per
+// token step) is read exactly once while X (M x K, <= 7 MB) stays in L2.  At M = 128 every weight
+// byte carries 128 flops, so each CU must keep ~12 B/clk of W arriving AND run its MFMAs at ~40 %
+// of peak.  What the measurements on this chip said (scripts/bench_dgemm.py --ablate):
+//   * with the MFMAs removed an LDS-ring kernel was exactly as fast -- the limit is how the W bytes
+//     are fetched, not the math;
+//   * an LDS-DMA W ring (4-6 stages in flight per CU) stayed at ~4.1-4.5 TB/s however deep.
+// So here W never touches LDS:
+//
+//   * workgroup = BN/16 compute waves + 2 X-loader waves, tile = ALL M rows (BM = 64/128/256) x BN
+//     W rows (BN = 64..128, chosen per shape so ~256 workgroups run: one per CU);
+//   * compute wave w owns 16 W rows and loads its B fragments straight from HBM into a D-stage
+//     register ring (D = 8 x 64-deep K stages = 16 KB per wave in flight, the GEMV's depth).  Its
+//     only vector-memory instructions are those loads, so hipcc's own counted vmcnt waits are
+//     exact and never drain the ring; every load is unconditional (the tail re-reads the last
+//     stage) so no branch joins force a vmcnt(0) (round-2 finding);
+//   * X (an L2 hit, shared by all compute waves) is staged by the 2 loader waves with LDS-DMA
+//     (`global_load_lds_dwordx4`, written in asm so hipcc orders nothing behind it) into an
+//     NSX-slot LDS ring; only the loaders wait on vmcnt for it (counted, in one asm statement with
+//     the s_barrier), so the X and W streams never serialise each other through the in-order
+//     vmcnt counter;
+//   * the X image is lane-linear per DMA piece and XOR-swizzled through the SOURCE address: chunk
+//     c of row r at r*128 + ((c ^ (r & 7)) << 4), so the 16-row ds_read_b128 A-fragment reads are
+//     bank-conflict free (guide rule 21 / T2);
+//   * split-K over the grid for the small-N projections; blocks are remapped XCD-locally so the
+//     blocks of one XCD share a K slice and therefore the same X slice in that XCD's L2 (guide T1);
+//   * epilogues: fp32 split-K partials (reduced by the residual + RMSNorm / SwiGLU reduce), bf16,
+//     or SwiGLU over gate/up weights interleaved in 8-row groups (each 16-row n-tile = 8 gate +
+//     8 up rows, so silu(g) * u is one lane swap away; same bf16 rounding points as
+//     GEMM -> silu_mul).
+//
+// MFMA maps (guide §3): A = X rows (m on lane & 15, k = 8 * (lane >> 4) + j), B = W rows (n on
+// lane & 15, same k); C/D: n = lane & 15, m = 4 * (lane >> 4) + i.
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) void dg_lds_t;
+typedef unsigned int dg_u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int DG_LOADERS = 2;    // X-loader waves per workgroup
+enum { DG_PART = 0, DG_BF16 = 1, DG_SILU = 2 };
+
+template <int BM>
+struct DgShape {
+  static constexpr int MT = BM / 16;                  // m-tiles per compute wave
+  static constexpr int D = BM == 256 ? 4 : 8;         // W register ring depth (stages)
+  static constexpr int XSTAGE = BM * 128;             // X bytes per 64-deep stage
+  static constexpr int NSX = BM == 256 ? 4 : (BM == 128 ? 6 : 8);   // X ring slots (64-128 KB)
+  static constexpr int XP = BM / 8 / DG_LOADERS;      // 1-KB DMA pieces per loader wave per stage
+};
+
+__device__ __forceinline__ f32x4_t dg_mfma(uint4 a, uint4 b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                 c, 0, 0, 0);
+}
+
+// One 1-KB LDS-DMA piece: lane l's 16 source bytes land at lds_addr + 16 l.  Inline asm, so hipcc
+// sees no LDS write to order the compute waves' ds_reads behind; M0 (compiler-reserved) is saved
+// and restored inside the statement (guide §5.7).
+__device__ __forceinline__ void dg_glds16(const void* gsrc, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_addr)
+               : "memory");
+}
+
+// loader waves: s_waitcnt vmcnt(n) + s_barrier as ONE statement (n = DMA pieces still allowed in flight)
+template <int N>
+__device__ __forceinline__ void dg_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(N) : "memory");
+}
+
+template <int P, int MAXA>
+__device__ __forceinline__ void dg_wait_ahead(int ahead) {
+  if constexpr (MAXA == 0) {
+    dg_wait_barrier<0>();
+  } else {
+    if (ahead >= MAXA) dg_wait_barrier<MAXA * P>();
+    else dg_wait_ahead<P, MAXA - 1>(ahead);
+  }
+}
+
+// compute waves: their W loads stay in flight across the barrier; their LDS reads of the previous
+// stage are retired first (hipcc may sink the MFMA that waits for them below an asm statement),
+// so the loaders' next DMA into that slot cannot overtake them
+__device__ __forceinline__ void dg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <bool NT>
+__device__ __forceinline__ uint4 dg_ldw(const uint16_t* p) {
+  if constexpr (NT) {
+    const dg_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const dg_u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *reinterpret_cast<const uint4*>(p);
+  }
+}
+
+// ABL: ablation builds for the timing probes only (scripts/bench_dgemm.py --ablate); 0 in production.
+//   1 = no X DMA, 2 = no ds_read / MFMA (W loads kept live).
+template <int BM, int BN, int EPI, bool NTW, int ABL = 0>
+__global__ void __launch_bounds__(64 * (BN / 16 + DG_LOADERS), 1)
+    dgemm_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W, int M, int N, int K, int ntiles,
+                 int split, float* __restrict__ part, uint16_t* __restrict__ out, int ldo) {
+  using S = DgShape<BM>;
+  constexpr int NW = BN / 16;                         // compute waves
+  constexpr int D = S::D;
+  __shared__ __attribute__((aligned(16))) char smem[S::NSX * S::XSTAGE];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  // logical block: the blocks of one XCD take consecutive ids, i.e. (mostly) one K slice
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ks = lid / ntiles, tile = lid % ntiles;
+  const int n0 = tile * BN, m0 = blockIdx.y * BM;
+  const int nks = K >> 6;
+  const int kb = (int)((long)ks * nks / split), ke = (int)((long)(ks + 1) * nks / split);
+  const int nst = ke - kb;
+  const int kq = lane >> 4;         // 8-element k group within a 32-deep MFMA step
+
+  if (w >= NW) {
+    // ---------------- X loader wave: rows 8 XP l .. 8 XP (l+1) - 1 of the X stage image
+    const int l = w - NW;
+    const int prow = lane >> 3, pch = (lane & 7) ^ prow;   // row & 7 == prow for every piece
+    const uint16_t* xsrc[S::XP];
+#pragma unroll
+    for (int i = 0; i < S::XP; ++i) {
+      const int m = min(m0 + 8 * S::XP * l + 8 * i + prow, M - 1);   // rows past M: results dropped
+      xsrc[i] = X + (size_t)m * K + (size_t)kb * 64 + 8 * pch;
+    }
+    const uint32_t lds0 =
+        __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(dg_lds_t*)smem + 8 * S::XP * l * 128);
+    auto issue = [&](int st, int slot) {
+      if constexpr ((ABL & 1) != 0) return;
+#pragma unroll
+      for (int i = 0; i < S::XP; ++i) dg_glds16(xsrc[i] + st * 64, lds0 + slot * S::XSTAGE + i * 1024);
+    };
+#pragma unroll
+    for (int p = 0; p < S::NSX - 1; ++p)
+      if (p < nst) issue(p, p);
+    int slot = 0;
+    for (int st = 0; st < nst; ++st) {
+      if constexpr ((ABL & 1) != 0) dg_wait_barrier<0>();
+      else dg_wait_ahead<S::XP, S::NSX - 2>(nst - 1 - st);
+      // the slot read in iteration st-1 is free once every wave passed this barrier
+      if (st + S::NSX - 1 < nst) issue(st + S::NSX - 1, slot == 0 ? S::NSX - 1 : slot - 1);
+      slot = slot + 1 == S::NSX ? 0 : slot + 1;
+    }
+    return;
+  }
+
+  // ---------------- compute wave w: W rows n0 + 16 w + (lane & 15)
+  const uint16_t* wp = W + (size_t)(n0 + 16 * w + (lane & 15)) * K + (size_t)kb * 64 + 8 * kq;
+  uint4 ring[D][2];
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+    const int s = min(p, nst - 1);
+    ring[p][0] = dg_ldw<NTW>(wp + s * 64);
+    ring[p][1] = dg_ldw<NTW>(wp + s * 64 + 32);
+  }
+  f32x4_t acc[S::MT];
+#pragma unroll
+  for (int i = 0; i < S::MT; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int xoff = (lane & 15) * 128;
+  const int sw = lane & 7;
+  int xslot = 0;
+  auto compute = [&](const uint4 (&b)[2]) {
+    if constexpr ((ABL & 2) != 0) {
+      asm volatile("" ::"v"(__builtin_bit_cast(dg_u32x4, b[0])), "v"(__builtin_bit_cast(dg_u32x4, b[1])));
+    } else {
+      const char* ximg = smem + xslot * S::XSTAGE + xoff;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int chunk = ((4 * kk + kq) ^ sw) << 4;
+#pragma unroll
+        for (int i = 0; i < S::MT; ++i) {
+          const uint4 a = *reinterpret_cast<const uint4*>(ximg + i * 16 * 128 + chunk);
+          acc[i] = dg_mfma(a, b[kk], acc[i]);
+        }
+      }
+    }
+    xslot = xslot + 1 == S::NSX ? 0 : xslot + 1;
+  };
+
+  int st = 0;
+  for (; st + D <= nst; st += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      dg_barrier();                 // X stage st+u is in LDS
+      compute(ring[u]);
+      const int s = min(st + u + D, nst - 1);   // unconditional: the tail re-reads the last stage
+      ring[u][0] = dg_ldw<NTW>(wp + s * 64);
+      ring[u][1] = dg_ldw<NTW>(wp + s * 64 + 32);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < D; ++u) {
+    if (st + u < nst) {
+      dg_barrier();
+      compute(ring[u]);
+    }
+  }
+
+  // ---- epilogue: lane holds rows m0 + 16 i + 4 (lane >> 4) + r of W row (output column) n
+  const int n = n0 + 16 * w + (lane & 15);
+  const int mb = m0 + 4 * kq;
+  if constexpr (EPI == DG_SILU) {
+    // 8-row interleave: lanes 0-7 of each 16 hold gate rows, lanes 8-15 the matching up rows
+    const bool gate = (lane & 8) == 0;
+    const int oc = (n0 >> 1) + 8 * w + (lane & 7);
+#pragma unroll
+    for (int i = 0; i < S::MT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float up = __shfl_xor(acc[i][r], 8, 64);
+        const int m = mb + 16 * i + r;
+        if (gate && m < M) {
+          const float gt = bf2f(f2bf(acc[i][r])), u = bf2f(f2bf(up));
+          out[(size_t)m * ldo + oc] = f2bf(gt / (1.f + __expf(-gt)) * u);
+        }
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < S::MT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = mb + 16 * i + r;
+        if (m < M) {
+          if constexpr (EPI == DG_PART) part[((size_t)ks * M + m) * N + n] = acc[i][r];
+          else out[(size_t)m * ldo + n] = f2bf(acc[i][r]);
+        }
+      }
+  }
+}
+
+constexpr bool DG_NT = false;   // weight-stream cache policy (nontemporal: measured in bench_dgemm)
+
+template <int BM, int BN, bool NTW, int ABL>
+int dgemm_launch_bn(const void* x, const void* w, int M, int N, int K, int split, int epi, float* part, void* out,
+                    int ldo, hipStream_t stream) {
+  const int ntiles = N / BN;
+  const dim3 grid(ntiles * split, (M + BM - 1) / BM);
+  const int threads = 64 * (BN / 16 + DG_LOADERS);
+#define DG_ARGS (const uint16_t*)x, (const uint16_t*)w, M, N, K, ntiles, split, part, (uint16_t*)out, ldo
+  switch (epi) {
+    case DG_PART: dgemm_kernel<BM, BN, DG_PART, NTW, ABL><<<grid, threads, 0, stream>>>(DG_ARGS); break;
+    case DG_BF16: dgemm_kernel<BM, BN, DG_BF16, NTW, ABL><<<grid, threads, 0, stream>>>(DG_ARGS); break;
+    case DG_SILU: dgemm_kernel<BM, BN, DG_SILU, NTW, ABL><<<grid, threads, 0, stream>>>(DG_ARGS); break;
+    default: return -3;
+  }
+#undef DG_ARGS
+  return 0;
+}
+
+template <int BM, bool NTW = DG_NT, int ABL = 0>
+int dgemm_launch(const void* x, const void* w, int M, int N, int K, int split, int epi, int bn, float* part,
+                 void* out, int ldo, hipStream_t stream) {
+  switch (bn) {
+    case 64: return dgemm_launch_bn<BM, 64, NTW, ABL>(x, w, M, N, K, split, epi, part, out, ldo, stream);
+    case 96: return dgemm_launch_bn<BM, 96, NTW, ABL>(x, w, M, N, K, split, epi, part, out, ldo, stream);
+    case 112: return dgemm_launch_bn<BM, 112, NTW, ABL>(x, w, M, N, K, split, epi, part, out, ldo, stream);
+    case 128: return dgemm_launch_bn<BM, 128, NTW, ABL>(x, w, M, N, K, split, epi, part, out, ldo, stream);
+    default: return -5;
+  }
+}
+
+int dgemm_check(int M, int N, int K, int split, int epi, int bn, const float* part, const void* out) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % 64 || split < 1 || split > K / 64) return -1;
+  if (bn != 64 && bn != 96 && bn != 112 && bn != 128) return -5;
+  if (N % bn) return -1;
+  if (epi != DG_PART && split != 1) return -2;
+  if ((epi == DG_PART && !part) || (epi != DG_PART && !out)) return -2;
+  return 0;
+}
+
+}  // namespace
+
+// Which row tile (64 / 128 / 256) a batch of M rows runs with (M > 256 loops 256-row tiles over grid.y).
+CFC_API int cfc_dgemm_bm(int M) { return M <= 64 ? 64 : (M <= 128 ? 128 : 256); }
+
+// epi 0: fp32 split-K partials into part[split][M][N]; 1: bf16 into out (row stride ldo, split 1);
+// 2: SwiGLU over 8-row interleaved gate/up W -> bf16 [M, N/2] into out (split 1).
+// bn (W rows per workgroup) in {64, 96, 112, 128}, N % bn == 0, K % 64 == 0, 1 <= split <= K / 64.
+CFC_API int cfc_dgemm(const void* x, const void* w, int M, int N, int K, int split, int epi, int bn, float* part,
+                      void* out, int ldo, hipStream_t stream) {
+  if (const int e = dgemm_check(M, N, K, split, epi, bn, part, out)) return e;
+  int rc;
+  switch (cfc_dgemm_bm(M)) {
+    case 64: rc = dgemm_launch<64>(x, w, M, N, K, split, epi, bn, part, out, ldo, stream); break;
+    case 128: rc = dgemm_launch<128>(x, w, M, N, K, split, epi, bn, part, out, ldo, stream); break;
+    default: rc = dgemm_launch<256>(x, w, M, N, K, split, epi, bn, part, out, ldo, stream); break;
+  }
+  return rc ? rc : CFC_CHECK_LAUNCH();
+}
+
+// Timing probe only (scripts/bench_dgemm.py --ablate): split-K partial GEMM at BM = 128 with
+// ablation bits `abl` (1 no X DMA, 2 no MFMA) and +8 = nontemporal W loads.
+CFC_API int cfc_dgemm_ablate(const void* x, const void* w, int M, int N, int K, int split, int bn, int abl,
+                             float* part, hipStream_t stream) {
+  if (M > 128 || (abl & ~11)) return -1;
+  if (const int e = dgemm_check(M, N, K, split, DG_PART, bn, part, nullptr)) return e;
+  int rc;
+  switch (abl) {
+    case 0: rc = dgemm_launch<128, false, 0>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
+    case 1: rc = dgemm_launch<128, false, 1>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
+    case 2: rc = dgemm_launch<128, false, 2>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
+    case 3: rc = dgemm_launch<128, false, 3>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
+    case 8: rc = dgemm_launch<128, true, 0>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
+    case 9: rc = dgemm_launch<128, true, 1>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
+    case 10: rc = dgemm_launch<128, true, 2>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
+    case 11: rc = dgemm_launch<128, true, 3>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
+    default: return -3;
+  }
+  return rc ? rc : CFC_CHECK_LAUNCH();
+}

@@ -156,14 +156,14 @@ __global__ void __launch_bounds__(256) v_cache_runs_kernel(const uint16_t* __res
 }
 
 // out[t, f] = silu(gate[t, f]) * up[t, f].  Layout of gu[t]: [gate | up] halves, or (interleave)
-// 32-column groups [gate 32t..32t+31 | up 32t..32t+31] -- the layout the decode GEMM's fused
+// 8-column groups [gate 8t..8t+7 | up 8t..8t+7] -- the layout the decode GEMM's fused
 // SwiGLU epilogue needs, so prefill and decode share one weight copy.  grid = (cols/8/256, T).
 __global__ void silu_mul_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ gu, int F, int interleave) {
   const int t = blockIdx.y;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;   // 8-column group of the output
   if (c >= (F >> 3)) return;
-  const int gc = interleave ? ((c >> 2) << 3) + (c & 3) : c;
-  const int uc = interleave ? gc + 4 : c + (F >> 3);
+  const int gc = interleave ? 2 * c : c;          // 8-row gate/up groups: chunk 2c gate, 2c+1 up
+  const int uc = interleave ? 2 * c + 1 : c + (F >> 3);
   const uint4* row = reinterpret_cast<const uint4*>(gu + (size_t)t * 2 * F);
   float a[8], b[8], r[8];
   unpack8(row[gc], a);
@@ -189,8 +189,8 @@ __global__ void __launch_bounds__(1024) silu_mul_fp8_kernel(uint8_t* __restrict_
   for (int i = 0; i < SQ_MAX_VEC; ++i) {
     const int c = threadIdx.x + i * 1024;
     if (c < (F >> 3)) {
-      const int gc = interleave ? ((c >> 2) << 3) + (c & 3) : c;
-      const int uc = interleave ? gc + 4 : c + (F >> 3);
+      const int gc = interleave ? 2 * c : c;
+      const int uc = interleave ? 2 * c + 1 : c + (F >> 3);
       float a[8], b[8];
       unpack8(row[gc], a);
       unpack8(row[uc], b);
@@ -644,7 +644,7 @@ CFC_API int cfc_quant_fp8_rows(void* out, float* scale, const void* x, int M, in
 }
 
 CFC_API int cfc_silu_mul(void* out, const void* gu, int T, int F, int interleave, hipStream_t stream) {
-  if (F % 8 != 0 || (interleave && F % 32 != 0) || T > 65535) return -1;
+  if (F % 8 != 0 || T > 65535) return -1;
   if (T == 0) return 0;
   silu_mul_kernel<<<dim3((F / 8 + 255) / 256, T), 256, 0, stream>>>((uint16_t*)out, (const uint16_t*)gu, F, interleave);
   return CFC_CHECK_LAUNCH();
@@ -652,7 +652,7 @@ CFC_API int cfc_silu_mul(void* out, const void* gu, int T, int F, int interleave
 
 CFC_API int cfc_silu_mul_fp8(void* out, float* scale, const void* gu, int T, int F, int interleave,
                              hipStream_t stream) {
-  if (F % 8 != 0 || (interleave && F % 32 != 0) || F > 1024 * 8 * SQ_MAX_VEC || T < 0) return -1;
+  if (F % 8 != 0 || F > 1024 * 8 * SQ_MAX_VEC || T < 0) return -1;
   if (T == 0) return 0;
   silu_mul_fp8_kernel<<<T, 1024, 0, stream>>>((uint8_t*)out, scale, (const uint16_t*)gu, F, interleave);
   return CFC_CHECK_LAUNCH();

@@ -1,167 +1,11 @@
-// Skinny (decode-shaped) GEMM for gfx950:  Y[M, N] = X[M, K] . W[N, K]^T,  M <= 128 per row block.
-//
-// At decode the projections are weight-streaming problems: W (the whole layer, 14-235 MB) is read
-// once per step while X is a few MB and L2-resident.  The library kernels reach only 2-2.4 TB/s on
-// the small-N shapes (qkv, o, down: measured, profiles/), so this kernel is built around the
-// weight stream:
-//   * block = 4 waves, tile = all 128 rows x 64 columns; wave w owns columns [16w, 16w+16) and
-//     streams ITS W fragments straight from HBM into VGPRs (each W byte is read exactly once on the
-//     chip) through a PD-deep register ring -- no LDS round trip for the streamed operand
-//     (guide: "GEMV / decode weights: load straight to VGPRs, deep unroll, late vmcnt");
-//   * the X tile (shared by the 4 waves) is staged through LDS in full 128-B lines, XOR-swizzled
-//     so the 16-row ds_read_b128 fragment reads are bank-conflict free; double-buffered, one
-//     barrier per 64-deep K stage;
-//   * split-K over gridDim.y so the small-N shapes still launch >= 256 blocks; fp32 partial slabs
-//     go to a workspace and a second kernel reduces them with the layer's next elementwise op
-//     fused in (bf16 store, SwiGLU, or residual-add + RMSNorm), replacing the separate
-//     silu_mul / rmsnorm launches of the unfused layer;
-//   * EPI_SILU with split == 1: the gate/up weight rows are stored interleaved in 32-row groups
-//     (tile t = gate rows 32t..32t+31 then up rows 32t..32t+31), so the block holds matching gate
-//     and up columns and writes silu(g) * u directly (waves 2-3 pass their accumulators through LDS).
-// MFMA: v_mfma_f32_16x16x32_bf16 with A = X rows (m on lane&15), B = W rows (n on lane&15);
-// C/D: col (n) = lane & 15, row (m) = 4 * (lane >> 4) + i.
+// Split-K reduce kernels for the decode GEMM (dgemm.hip) and the library split-K path, and the
+// GEMV for single-stream / small-batch decode (M <= 4).
 #include "common.h"
 
 namespace {
 
-constexpr int SG_BN = 64;     // columns per block
-constexpr int SG_BM = 128;    // rows per block (8 MFMA m-tiles)
-constexpr int SG_BK = 64;     // K per pipeline stage
-constexpr int SG_PD = 4;      // W register-ring depth (stages in flight per wave)
-
-enum { EPI_PARTIAL = 0, EPI_BF16 = 1, EPI_SILU = 2 };
-
-__device__ __forceinline__ f32x4_t mfma16(bf16x8_t a, bf16x8_t b, f32x4_t c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ bf16x8_t as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8_t, v); }
-
-// X stage image: 128 rows x 128 B; chunk c (16 B) of row r at r*128 + ((c ^ (r & 7)) << 4).
-__device__ __forceinline__ int x_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
-
-template <int EPI>
-__global__ void __launch_bounds__(256, 2) skinny_gemm_kernel(const uint16_t* __restrict__ X,
-                                                             const uint16_t* __restrict__ W, int M, int N, int K,
-                                                             int Ks, float* __restrict__ part,
-                                                             uint16_t* __restrict__ out, int ldo) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * SG_BM * 128];   // 32 KB
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
-  const int col = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * SG_BN;
-  const int split = blockIdx.y;
-  const int m0 = blockIdx.z * SG_BM;
-  const int mrows = min(SG_BM, M - m0);
-  const int kbeg = split * Ks;
-  const int nst = Ks / SG_BK;
-
-  // W fragment pointer of this lane: row n0 + 16w + col, k offset 8g (+32 for the 2nd k-step)
-  const uint16_t* wp = W + (size_t)(n0 + 16 * w + col) * K + kbeg + 8 * g;
-  // X staging: thread loads rows (tid >> 3) + 32 i, 16-B chunk tid & 7 of each 64-k stage
-  const int xr = tid >> 3, xc = tid & 7;
-  const uint16_t* xp = X + (size_t)(m0 + xr) * K + kbeg + 8 * xc;
-
-  // Register rings PD stages deep for BOTH operands.  Stage s+PD-1 is issued (W then X) while
-  // stage s is multiplied; the ds_write of X(s+1) at the end of the iteration then only waits for
-  // loads issued PD-2 iterations ago, so the in-order vmcnt never drains the younger stages.
-  // (Issuing X one stage ahead and W PD ahead would NOT work: waiting for the X loads would also
-  // retire every older W load -- the counter is in order.)
-  uint4 wr[SG_PD][2];
-  uint4 xs[SG_PD][4];
-  auto load_w = [&](int st, uint4 (&dst)[2]) {
-    if (st < nst) {
-      dst[0] = *reinterpret_cast<const uint4*>(wp + st * SG_BK);
-      dst[1] = *reinterpret_cast<const uint4*>(wp + st * SG_BK + 32);
-    }
-  };
-  auto load_x = [&](int st, uint4 (&dst)[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (st < nst) dst[i] = xr + 32 * i < mrows ? *reinterpret_cast<const uint4*>(xp + (size_t)32 * i * K + st * SG_BK)
-                                                 : make_uint4(0, 0, 0, 0);
-  };
-  auto store_x = [&](int buf, const uint4 (&src)[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(smem + buf * SG_BM * 128 + x_off(xr + 32 * i, xc)) = src[i];
-  };
-
-  f32x4_t acc[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int p = 0; p < SG_PD - 1; ++p) {
-    load_w(p, wr[p]);
-    load_x(p, xs[p]);
-  }
-  store_x(0, xs[0]);
-  __syncthreads();
-
-  for (int s0 = 0; s0 < nst; s0 += SG_PD) {
-#pragma unroll
-    for (int u = 0; u < SG_PD; ++u) {
-      const int s = s0 + u;
-      if (s < nst) {
-        load_w(s + SG_PD - 1, wr[(u + SG_PD - 1) % SG_PD]);
-        load_x(s + SG_PD - 1, xs[(u + SG_PD - 1) % SG_PD]);
-        const char* xb = smem + (s & 1) * SG_BM * 128;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const bf16x8_t b = as_bf16x8(wr[u][ks]);
-#pragma unroll
-          for (int mt = 0; mt < 8; ++mt) {
-            const uint4 a = *reinterpret_cast<const uint4*>(xb + x_off(16 * mt + col, 4 * ks + g));
-            acc[mt] = mfma16(as_bf16x8(a), b, acc[mt]);
-          }
-        }
-        if (s + 1 < nst) store_x((s + 1) & 1, xs[(u + 1) % SG_PD]);
-        __syncthreads();
-      }
-    }
-  }
-
-  if constexpr (EPI == EPI_PARTIAL) {
-    float* pp = part + ((size_t)split * M + m0) * N + n0 + 16 * w + col;
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = 16 * mt + 4 * g + i;
-        if (r < mrows) pp[(size_t)r * N] = acc[mt][i];
-      }
-  } else if constexpr (EPI == EPI_BF16) {
-    uint16_t* op = out + (size_t)m0 * ldo + n0 + 16 * w + col;
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = 16 * mt + 4 * g + i;
-        if (r < mrows) op[(size_t)r * ldo] = f2bf(acc[mt][i]);
-      }
-  } else {  // EPI_SILU: waves 0,1 hold gate columns, waves 2,3 the matching up columns
-    float* ub = reinterpret_cast<float*>(smem);   // [128][32] fp32 = 16 KB (X buffers are drained)
-    if (w >= 2) {
-#pragma unroll
-      for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ub[(16 * mt + 4 * g + i) * 32 + 16 * (w - 2) + col] = acc[mt][i];
-    }
-    __syncthreads();
-    if (w < 2) {
-      uint16_t* op = out + (size_t)m0 * ldo + (n0 >> 1) + 16 * w + col;
-#pragma unroll
-      for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = 16 * mt + 4 * g + i;
-          const float gt = acc[mt][i], up = ub[r * 32 + 16 * w + col];
-          if (r < mrows) op[(size_t)r * ldo] = f2bf(gt / (1.f + __expf(-gt)) * up);
-        }
-    }
-  }
-}
-
 // Reduce the split-K partials [split][M][N] -> bf16 Y (mode 0) or silu(gate) * up for the
-// 32-interleaved gate/up layout (mode 1, output width N/2).  One thread per 4 output columns.
+// 8-row interleaved gate/up layout (mode 1, output width N/2).  One thread per 4 output columns.
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ part, int split, int M, int N,
                                                             int mode, uint16_t* __restrict__ out, int ldo) {
   const int m = blockIdx.y;
@@ -180,8 +24,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   } else {
     const int F = N >> 1;
     if (c4 >= F) return;
-    const int t = c4 >> 5, c = c4 & 31;
-    const int gcol = 64 * t + c, ucol = gcol + 32;
+    const int gcol = 16 * (c4 >> 3) + (c4 & 7), ucol = gcol + 8;
     float4 gs = make_float4(0.f, 0.f, 0.f, 0.f), us = gs;
     for (int p = 0; p < split; ++p) {
       const float* row = part + ((size_t)p * M + m) * N;
@@ -190,10 +33,12 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
       gs.x += a.x; gs.y += a.y; gs.z += a.z; gs.w += a.w;
       us.x += b.x; us.y += b.y; us.z += b.z; us.w += b.w;
     }
-    auto sl = [](float x) { return x / (1.f + __expf(-x)); };
+    // bf16-round the projection outputs first: the rounding points of GEMM -> silu_mul
+    auto sl = [](float x) { x = bf2f(f2bf(x)); return x / (1.f + __expf(-x)); };
+    auto rb = [](float x) { return bf2f(f2bf(x)); };
     uint2 o;
-    o.x = pack2bf(sl(gs.x) * us.x, sl(gs.y) * us.y);
-    o.y = pack2bf(sl(gs.z) * us.z, sl(gs.w) * us.w);
+    o.x = pack2bf(sl(gs.x) * rb(us.x), sl(gs.y) * rb(us.y));
+    o.y = pack2bf(sl(gs.z) * rb(us.z), sl(gs.w) * rb(us.w));
     *reinterpret_cast<uint2*>(out + (size_t)m * ldo + c4) = o;
   }
 }
@@ -273,7 +118,7 @@ __global__ void __launch_bounds__(1024) splitk_residual_rmsnorm_kernel(const flo
 // keeps its whole K=4096 slice in flight at once, and nontemporal loads keep the once-read weights
 // out of L2.  X rows are read from global (L2-resident, re-read once per wave = M/2 of W's bytes).
 // The 64 lane partials are summed with a butterfly.  Epilogues: fp32 store (feeds the residual +
-// RMSNorm reduce kernel with split = 1), bf16 store, or SwiGLU over the 32-row interleaved gate/up
+// RMSNorm reduce kernel with split = 1), bf16 store, or SwiGLU over the 8-row interleaved gate/up
 // weights (the wave's two rows are gate row j and up row j of output column j).
 // Grid: one 4-wave block per 8 W rows (4 output columns for SwiGLU) -> 512-3584 blocks for the
 // 7B shapes, i.e. >= 2 blocks per CU.
@@ -307,8 +152,8 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
   if (col >= ncols) return;
   int rows[GV_RW];
   if constexpr (EPI == GV_SWIGLU) {
-    rows[0] = 64 * (col >> 5) + (col & 31);   // gate row of output column `col`
-    rows[1] = rows[0] + 32;                   // matching up row
+    rows[0] = 16 * (col >> 3) + (col & 7);    // gate row of output column `col` (8-row groups)
+    rows[1] = rows[0] + 8;                    // matching up row
   } else {
     rows[0] = GV_RW * col;
     rows[1] = GV_RW * col + 1;
@@ -361,29 +206,10 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
 }
 }  // namespace
 
-// epi: 0 = fp32 partials into `part` ([split][M][N]), 1 = bf16 into out (split must be 1),
-//      2 = SwiGLU into out (interleaved gate/up W, split must be 1, out width N/2).
-CFC_API int cfc_skinny_gemm(const void* x, const void* w, int M, int N, int K, int split, int epi, float* part,
-                            void* out, int ldo, hipStream_t stream) {
-  if (M <= 0 || N % SG_BN || split <= 0 || K % (SG_BK * split)) return -1;
-  if (epi != EPI_PARTIAL && split != 1) return -2;
-  dim3 grid(N / SG_BN, split, (M + SG_BM - 1) / SG_BM);
-  const int Ks = K / split;
-#define SG_ARGS (const uint16_t*)x, (const uint16_t*)w, M, N, K, Ks, part, (uint16_t*)out, ldo
-  switch (epi) {
-    case EPI_PARTIAL: skinny_gemm_kernel<EPI_PARTIAL><<<grid, 256, 0, stream>>>(SG_ARGS); break;
-    case EPI_BF16: skinny_gemm_kernel<EPI_BF16><<<grid, 256, 0, stream>>>(SG_ARGS); break;
-    case EPI_SILU: skinny_gemm_kernel<EPI_SILU><<<grid, 256, 0, stream>>>(SG_ARGS); break;
-    default: return -3;
-  }
-#undef SG_ARGS
-  return CFC_CHECK_LAUNCH();
-}
-
 // mode 0: out[M, N] bf16 = sum of partials; mode 1: out[M, N/2] = silu(gate) * up (interleaved).
 CFC_API int cfc_splitk_reduce(const float* part, int split, int M, int N, int mode, void* out, int ldo,
                               hipStream_t stream) {
-  if (N % 4 || M <= 0 || (mode == 1 && N % 64)) return -1;
+  if (N % 4 || M <= 0 || (mode == 1 && N % 16)) return -1;
   const int cols = mode == 0 ? N : N / 2;
   dim3 grid((cols / 4 + 255) / 256, M);
   splitk_reduce_kernel<<<grid, 256, 0, stream>>>(part, split, M, N, mode, (uint16_t*)out, ldo);
@@ -407,11 +233,11 @@ CFC_API int cfc_splitk_residual_rmsnorm(const float* part, int split, int M, int
 }
 
 // M <= 4 GEMV. epi 0: fp32 [M, N] into yf; 1: bf16 into yb (row stride ldo); 2: SwiGLU over the
-// interleaved gate/up W -> bf16 [M, N/2] into yb.  N even (epi 2: N % 64 == 0), K % 8 == 0.
+// interleaved gate/up W -> bf16 [M, N/2] into yb.  N even (epi 2: N % 16 == 0), K % 8 == 0.
 CFC_API int cfc_gemv(const void* x, const void* w, int M, int N, int K, int epi, float* yf, void* yb, int ldo,
                      hipStream_t stream) {
   if (M < 1 || M > 4 || N <= 0 || N % 2 || K <= 0 || K % 8) return -1;
-  if (epi == GV_SWIGLU && N % 64) return -1;
+  if (epi == GV_SWIGLU && N % 16) return -1;
   if ((epi == GV_F32 && !yf) || (epi != GV_F32 && !yb)) return -2;
   const int ncols = epi == GV_SWIGLU ? N / 2 : N / GV_RW;
   const dim3 grid((ncols + 3) / 4);

@@ -1,0 +1,162 @@
+#!/usr/bin/env python3
+"""Decode GEMM (csrc/kernels/dgemm.hip) vs the library path, Mistral-7B / Llama-3-70B decode shapes.
+
+1. numerics: every epilogue (bf16, SwiGLU, split-K slabs -> residual + RMSNorm) against an fp32
+   PyTorch reference of the same op;
+2. timing: hipGraph of back-to-back calls whose weights rotate over >= 1 GB of copies, so no call
+   is served from the 256 MB Infinity Cache (in a real decode step the layer's 436 MB of weights
+   and the KV stream pass between two reads of the same projection).
+
+Usage: bench_dgemm.py [--m 128 256] [--split-sweep] [--shapes qkv o gate_up down]
+Writes one JSON line per (shape, M) to gpurun_out/dgemm.jsonl.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+import torch.nn.functional as F
+
+from copilot_for_consensus_amd.ops import kernels as K
+from copilot_for_consensus_amd.ops import reference as R
+from copilot_for_consensus_amd.runtime.gemm_tuning import enable_tuned_gemms
+
+SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
+          "qkv70": (10240, 8192), "gate_up70": (57344, 8192), "down70": (8192, 28672),
+          "qkv_tp8": (768, 4096), "gate_up_tp8": (3584, 4096), "down_tp8": (4096, 1792)}
+
+
+def rotated(w: torch.Tensor, min_bytes: int = 1 << 30) -> list:
+    n = max(2, -(-min_bytes // (w.numel() * 2)))
+    return [w] + [w.clone() for _ in range(n - 1)]
+
+
+def timed(fn_list, reps: int = 3) -> float:
+    """us per call: graph of one pass over fn_list, replayed `reps` times, median."""
+    for f in fn_list[:2]:
+        f()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for f in fn_list:
+            f()
+    g.replay()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        g.replay()
+        torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t) / len(fn_list) * 1e6)
+    return sorted(ts)[len(ts) // 2]
+
+
+def rel_err(a: torch.Tensor, ref: torch.Tensor) -> float:
+    return float((a.float() - ref.float()).abs().max() / ref.float().abs().max().clamp_min(1e-6))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", type=int, nargs="*", default=[128])
+    ap.add_argument("--shapes", nargs="*", default=["qkv", "o", "gate_up", "down"])
+    ap.add_argument("--split-sweep", action="store_true")
+    ap.add_argument("--ablate", action="store_true", help="time the ablation builds (1 no-X, 2 no-MFMA, 4 packed W, 8 nt)")
+    ap.add_argument("--calls", type=int, default=64)
+    ap.add_argument("--out", default="gpurun_out/dgemm.jsonl")
+    args = ap.parse_args()
+    enable_tuned_gemms()
+    os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
+    fh = open(args.out, "a")
+    torch.manual_seed(0)
+    for M in args.m:
+        for name in args.shapes:
+            N, Kd = SHAPES[name]
+            x = torch.randn(M, Kd, device="cuda").bfloat16()
+            w = (torch.randn(N, Kd, device="cuda") * 0.02).bfloat16()
+            ref = x.float() @ w.float().t()
+            row = {"shape": name, "M": M, "N": N, "K": Kd, "w_MB": round(N * Kd * 2 / 1e6, 1)}
+            # numerics (default config + a forced split)
+            bn_d, s_def = K.dgemm_config(M, N, Kd)
+            row["config"] = [bn_d, s_def]
+            for bn in K.DGEMM_BNS:
+                if N % bn == 0:
+                    row[f"err_bf16_bn{bn}"] = rel_err(K.dgemm(x, w, "bf16", bn=bn), ref)
+            for s in sorted({2, s_def}):
+                part = K.dgemm(x, w, "part", s, bn=bn_d).clone()
+                row[f"err_part_s{s}"] = rel_err(part.sum(0), ref)
+            if name.startswith("gate_up"):
+                refs = R.silu_mul_interleaved(ref.bfloat16()).float()
+                row["err_swiglu"] = rel_err(K.dgemm_swiglu(x, w), refs)
+                row["err_swiglu_split"] = rel_err(K.dgemm_swiglu(x, w, split=2, bn=64), refs)
+            if name.startswith(("o", "down")):
+                res0 = torch.randn(M, N, device="cuda").bfloat16()
+                nw = (1 + 0.1 * torch.randn(N, device="cuda")).bfloat16()
+                r1 = res0.clone()
+                y = K.dgemm_residual_rmsnorm(x, w, r1, nw, 1e-5)
+                yr, rr = R.rmsnorm(ref.bfloat16(), nw, 1e-5, res0.clone())
+                row["err_res_norm"] = rel_err(y, yr)
+                row["err_residual"] = rel_err(r1, rr)
+            torch.cuda.synchronize()
+            # timing over rotated weights
+            ws = rotated(w)
+            calls = [ws[i % len(ws)] for i in range(max(args.calls, len(ws)))]
+            wb = N * Kd * 2
+            t_lib = timed([lambda ww=ww: F.linear(x, ww) for ww in calls])
+            row["lib_us"] = round(t_lib, 1)
+            row["lib_TBs"] = round(wb / t_lib / 1e6, 2)
+            cfgs = {(bn_d, s_def)}
+            if args.split_sweep:
+                for bn in K.DGEMM_BNS:
+                    if N % bn:
+                        continue
+                    tiles = N // bn * ((M + 127) // 128 if M <= 128 else (M + 255) // 256)
+                    for s in range(1, Kd // 64 + 1):
+                        if tiles * s > 2 * K.DGEMM_CUS:
+                            break
+                        if tiles * s >= K.DGEMM_CUS // 3:
+                            cfgs.add((bn, s))
+            for bn, s in sorted(cfgs):
+                part = torch.empty(s, M, N, device="cuda", dtype=torch.float32)
+                if s == 1:
+                    fns = [lambda ww=ww, bn=bn: K.dgemm(x, ww, "bf16", bn=bn) for ww in calls]
+                else:
+                    fns = [lambda ww=ww, bn=bn, s=s, part=part: K.dgemm(x, ww, "part", s, bn=bn, part=part)
+                           for ww in calls]
+                row[f"dg_bn{bn}_s{s}_us"] = round(timed(fns), 1)
+            if args.ablate and M <= 128:
+                part = torch.empty(s_def, M, N, device="cuda", dtype=torch.float32)
+                for abl in (1, 2, 3, 8, 9, 10, 11):
+                    fns = [lambda ww=ww, a=abl: K.check(K.kernels().cfc_dgemm_ablate(
+                        x.data_ptr(), ww.data_ptr(), M, N, Kd, s_def, bn_d, a, part.data_ptr(), K._stream(x)),
+                        "ablate") for ww in calls]
+                    row[f"abl{abl}_us"] = round(timed(fns), 1)
+            if name.startswith("gate_up"):
+                row["lib_silu_us"] = round(timed([lambda ww=ww: K.silu_mul(F.linear(x, ww), interleaved=True)
+                                                  for ww in calls]), 1)
+                row["dg_swiglu_us"] = round(timed([lambda ww=ww: K.dgemm_swiglu(x, ww) for ww in calls]), 1)
+            if name.startswith(("o", "down")):
+                res = torch.randn(M, N, device="cuda").bfloat16()
+                nw = torch.ones(N, device="cuda").bfloat16()
+                sl = K.lib_split_for(Kd, N)
+                row["lib_split"] = sl
+                row["lib_res_norm_us"] = round(timed([lambda ww=ww: K.lib_splitk_linear_residual_rmsnorm(
+                    x, ww, sl, res, nw, 1e-5) for ww in calls]), 1)
+                row["dg_res_norm_us"] = round(timed([lambda ww=ww: K.dgemm_residual_rmsnorm(
+                    x, ww, res, nw, 1e-5) for ww in calls]), 1)
+            if name.startswith("qkv"):
+                row["dg_linear_us"] = round(timed([lambda ww=ww: K.dgemm_linear(x, ww) for ww in calls]), 1)
+            best = min(v for k, v in row.items() if k.startswith("dg_bn"))
+            row["dg_best_TBs"] = round(wb / best / 1e6, 2)
+            print(json.dumps(row), flush=True)
+            fh.write(json.dumps(row) + "\n")
+            fh.flush()
+            del ws, calls
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

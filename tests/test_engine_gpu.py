@@ -63,7 +63,10 @@ def test_graph_and_eager_decode_agree():
     assert res[0] == res[1]
 
 
-@pytest.mark.parametrize("mode", ["splitk", "skinny"])
+PROMPTS8 = [[1, 2, 3] * 30, [4, 5] * 70, [1, 7], [9] * 17, [3, 1, 4, 1, 5] * 9, [2, 6] * 33, [8] * 5, [7, 7, 1] * 21]
+
+
+@pytest.mark.parametrize("mode", ["splitk", "dgemm"])
 def test_decode_gemm_modes_match_library(mode, monkeypatch):
     cfg = get_config("tiny")
     w = DecoderWeights.random(cfg, "cuda", seed=11)
@@ -73,11 +76,12 @@ def test_decode_gemm_modes_match_library(mode, monkeypatch):
         model = DecoderModel(w)
         assert model.decode_gemm == m
         kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, "cuda")
-        res.append(LLMEngine(model, kv).generate([[1, 2, 3] * 30, [4, 5] * 70, [1, 7]], 24, ignore_eos=True).tokens)
+        # 8 sequences: decode batches above the GEMV's 4 rows take the mode's GEMMs
+        res.append(LLMEngine(model, kv).generate(PROMPTS8, 24, ignore_eos=True).tokens)
     agree = sum(a == b for x, y in zip(*res) for a, b in zip(x, y))
     # different fp32 summation orders: a bf16 near-tie can flip one greedy token, after which that
     # sequence continues differently; first tokens must agree exactly, the bulk must agree
-    assert [t[0] for t in res[0]] == [t[0] for t in res[1]] and agree >= 0.75 * 72, res
+    assert [t[0] for t in res[0]] == [t[0] for t in res[1]] and agree >= 0.75 * 8 * 24, res
 
 
 def test_fused_decode_matches_unfused():
@@ -88,9 +92,9 @@ def test_fused_decode_matches_unfused():
         m = DecoderModel(w, fused_decode=fused)
         assert m.fused_decode == fused
         kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, "cuda")
-        res.append(LLMEngine(m, kv).generate([[1, 2, 3] * 30, [4, 5] * 70, [1, 7]], 24, ignore_eos=True).tokens)
+        res.append(LLMEngine(m, kv).generate(PROMPTS8, 24, ignore_eos=True).tokens)
     agree = sum(a == b for x, y in zip(*res) for a, b in zip(x, y))
-    assert [t[0] for t in res[0]] == [t[0] for t in res[1]] and agree >= 0.9 * 72, res
+    assert [t[0] for t in res[0]] == [t[0] for t in res[1]] and agree >= 0.9 * 8 * 24, res
 
 
 def test_encoder_gpu_vs_cpu():

@@ -275,37 +275,67 @@ def _ref_linear(x, w):
     return (x.float() @ w.float().T).cpu()
 
 
-@pytest.mark.parametrize("M,N,Kd,split", [(1, 6144, 4096, None), (8, 4096, 4096, 8), (77, 1024, 512, 2),
-                                         (128, 4096, 14336, None), (128, 6144, 4096, 4), (200, 512, 1024, 1),
-                                         (128, 32000, 4096, 1)])
-def test_skinny_linear(M, N, Kd, split):
+@pytest.mark.parametrize("M,N,Kd,split,bn", [(5, 6144, 4096, None, None), (8, 4096, 4096, 8, 64),
+                                            (77, 1024, 512, 2, 128), (128, 4096, 14336, None, None),
+                                            (128, 6144, 4096, 4, 96), (128, 28672, 512, 1, 112),
+                                            (200, 512, 1024, 1, 128), (256, 768, 1024, 3, 96),
+                                            (128, 32000, 4096, 1, 128), (300, 640, 256, 1, 64), (64, 448, 320, 5, 112)])
+def test_dgemm_linear(M, N, Kd, split, bn):
+    """Hand-written decode GEMM vs fp32 x @ w^T: every row tile (64 / 128 / 256, M > 256 over
+    grid.y), every W tile width, split-K slabs + reduce, uneven K slices."""
     x = torch.randn(M, Kd, device=DEV).bfloat16()
     w = (torch.randn(N, Kd, device=DEV) * 0.02).bfloat16()
-    y = K.skinny_linear(x, w, split=split)
+    y = K.dgemm_linear(x, w, split=split, bn=bn)
     _close(y, _ref_linear(x, w), 3e-2)
 
 
-@pytest.mark.parametrize("M,split", [(128, 1), (5, 1), (128, 2), (130, 4)])
-def test_skinny_swiglu(M, split):
+def test_dgemm_asymmetric_exact():
+    """Small-integer operands (exact in bf16 and fp32): the output must match bit for bit, which
+    catches any row/column or k-order mix-up an all-random check could hide."""
+    M, N, Kd = 128, 256, 512
+    x = torch.randint(-3, 4, (M, Kd), device=DEV).bfloat16()
+    w = torch.randint(-2, 3, (N, Kd), device=DEV).bfloat16()
+    w[:, :7] += torch.arange(N, device=DEV).bfloat16().unsqueeze(1) % 5   # asymmetric in n
+    ref = (x.float() @ w.float().T)
+    for bn in K.DGEMM_BNS:
+        if N % bn == 0:
+            part = K.dgemm(x, w, "part", 2, bn=bn)
+            assert torch.equal(part.sum(0), ref), bn
+
+
+@pytest.mark.parametrize("M,split", [(128, None), (5, None), (64, None), (128, 2), (130, 4), (256, None)])
+def test_dgemm_swiglu(M, split):
     F, Kd = 1024, 512
     x = torch.randn(M, Kd, device=DEV).bfloat16()
     gu = (torch.randn(2 * F, Kd, device=DEV) * 0.05).bfloat16()
     wi = R.interleave_gate_up(gu)
     ref = R.silu_mul(_ref_linear(x, gu).bfloat16())
-    _close(K.skinny_swiglu(x, wi, split=split), ref, 3e-2)
+    _close(K.dgemm_swiglu(x, wi, split=split), ref, 3e-2)
 
 
-@pytest.mark.parametrize("M,N,Kd,split", [(128, 4096, 4096, 8), (3, 256, 512, 1), (128, 4096, 14336, 8)])
-def test_skinny_linear_residual_rmsnorm(M, N, Kd, split):
+@pytest.mark.parametrize("M,N,Kd,split", [(128, 4096, 4096, None), (5, 256, 512, 1), (128, 4096, 14336, 8),
+                                         (256, 1024, 1024, None)])
+def test_dgemm_residual_rmsnorm(M, N, Kd, split):
     x = torch.randn(M, Kd, device=DEV).bfloat16()
     w = (torch.randn(N, Kd, device=DEV) * 0.02).bfloat16()
     r = torch.randn(M, N, device=DEV).bfloat16()
     nw = (1 + 0.1 * torch.randn(N, device=DEV)).bfloat16()
     ref_o, ref_r = R.rmsnorm(_ref_linear(x, w).bfloat16(), nw.cpu(), 1e-5, r.cpu())
     rr = r.clone()
-    o = K.skinny_linear_residual_rmsnorm(x, w, rr, nw, 1e-5, split=split)
+    o = K.dgemm_residual_rmsnorm(x, w, rr, nw, 1e-5, split=split)
     _close(rr, ref_r, 3e-2)
     _close(o, ref_o, 5e-2)
+
+
+def test_dgemm_rejects_bad_shapes():
+    x = torch.randn(8, 100, device=DEV).bfloat16()
+    w = torch.randn(128, 100, device=DEV).bfloat16()
+    with pytest.raises(ValueError):
+        K.dgemm(x, w)
+    x = torch.randn(8, 128, device=DEV).bfloat16()
+    w = torch.randn(96, 128, device=DEV).bfloat16()
+    with pytest.raises(RuntimeError):
+        K.dgemm(x, w, bn=128)      # 96 rows do not tile by 128: the launcher refuses
 
 
 @pytest.mark.parametrize("M,N,Kd,split", [(128, 4096, 14336, 8), (5, 256, 512, 2)])
