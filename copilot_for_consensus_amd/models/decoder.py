@@ -567,7 +567,10 @@ class DecoderModel:
         qs, ks = w.heads * cfg.head_dim, w.kv_heads * cfg.head_dim
         for i in range(cfg.layers):
             lw, ql = w.layers[i], w.qlayers[i]
-            if ql["q"] is not None and ql["k"] is not None and ql["v"] is not None:
+            # a projection takes its quantized copy only when B rows of its input fit the qgemv's
+            # LDS stage (K.qgemv_fits); otherwise the bf16 GEMV of the same layer
+            fit_h, fit_o, fit_d = K.qgemv_fits(B, cfg.hidden), K.qgemv_fits(B, qs), K.qgemv_fits(B, w.ffn)
+            if ql["q"] is not None and ql["k"] is not None and ql["v"] is not None and fit_h:
                 qkv = torch.empty(B, qs + 2 * ks, dtype=torch.bfloat16, device=h.device)
                 ld = qkv.shape[1]   # q, k, v write their column slices (types may differ: Q4_K_M's v is often Q6_K)
                 K.qgemv(h, ql["q"], out=qkv, ldo=ld)
@@ -581,19 +584,19 @@ class DecoderModel:
                                             part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
                                             k_scale=kv.k_scale, v_scale=kv.v_scale)
             a2 = attn.view(B, -1)
-            if ql["o"] is not None:
+            if ql["o"] is not None and fit_o:
                 part = K._workspace(h.device, B * cfg.hidden)[:B * cfg.hidden].view(1, B, cfg.hidden)
                 K.qgemv(a2, ql["o"], "f32", out=part[0])
                 h = K.splitk_residual_rmsnorm(part, residual, lw["mlp_norm"], eps)
             else:
                 h = K.gemv_residual_rmsnorm(a2, lw["o"], residual, lw["mlp_norm"], eps)
             g, u = ql["gate"], ql["up"]
-            if g is not None and u is not None and g.qtype == u.qtype:
+            if g is not None and u is not None and g.qtype == u.qtype and fit_h:
                 a = K.qgemv(h, g, "swiglu", qw2=u)
             else:
                 a = K.gemv(h, lw["gate_up"], "swiglu")
             nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm
-            if ql["down"] is not None:
+            if ql["down"] is not None and fit_d:
                 part = K._workspace(h.device, B * cfg.hidden)[:B * cfg.hidden].view(1, B, cfg.hidden)
                 K.qgemv(a, ql["down"], "f32", out=part[0])
                 h = K.splitk_residual_rmsnorm(part, residual, nxt, eps)
@@ -605,7 +608,8 @@ class DecoderModel:
         """[B, V] logits (all-gathered over the vocab-parallel shards)."""
         head = self.w.lm_head
         if (self.decode_qgemv and self.w.q_lm_head is not None and hidden.is_cuda
-                and hidden.shape[0] <= K.GEMV_MAX_M and hidden.is_contiguous() and self.w.q_lm_head.N % 4 == 0):
+                and hidden.shape[0] <= K.GEMV_MAX_M and hidden.is_contiguous() and self.w.q_lm_head.N % 4 == 0
+                and K.qgemv_fits(hidden.shape[0], hidden.shape[1])):
             local = K.qgemv(hidden, self.w.q_lm_head)
         elif (self.decode_gemv and hidden.is_cuda and hidden.shape[0] <= K.GEMV_MAX_M
                 and hidden.is_contiguous() and head.shape[0] % 2 == 0 and head.shape[1] % 8 == 0):

@@ -648,6 +648,15 @@ def attach_random_quant(weights, recipe: str = "q4_k_m", seed: int = 0):
     return weights
 
 
+QGEMV_LDS_BYTES = 160 * 1024   # the quantized GEMV stages all of X in LDS (quant.hip: qgemv_launch_rk)
+
+
+def qgemv_fits(M: int, K: int) -> bool:
+    """Whether an M-row X of K columns fits the quantized GEMV's LDS stage (M*K*2 + 16 bytes):
+    a 70B-class ffn_down (K = 28672) fits 2 rows, not 3 -- those batches take the bf16 GEMV."""
+    return M * K * 2 + 16 <= QGEMV_LDS_BYTES
+
+
 def qgemv(x: torch.Tensor, qw: QWeight, epi: str = "bf16", qw2: QWeight | None = None,
           out: torch.Tensor | None = None, ldo: int | None = None) -> torch.Tensor:
     """x [M <= 4, K] bf16 @ dequant(qw)^T on the quantized GEMV (quant.hip).  ``epi``: "bf16" ->

@@ -91,7 +91,13 @@ def main(argv=None) -> int:
     if args.service == "reporting":
         from ..ui import ui_routes
         ui_routes(app, bases={"reporting": ""})       # its own API at the root; ingestion / auth via the gateway
-    run_service(svc, app, cfg.http_host, args.port or cfg.http_port)
+    if args.service == "ingestion":
+        node.start_scheduler()    # a standalone ingestion process schedules its own fetches (ingestion/main.py)
+    try:
+        run_service(svc, app, cfg.http_host, args.port or cfg.http_port)
+    finally:
+        if getattr(svc, "scheduler", None) is not None:
+            svc.scheduler.stop()
     return 0
 
 

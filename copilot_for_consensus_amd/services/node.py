@@ -126,15 +126,8 @@ class Node:
         self.connect()
         for s in self.services.values():
             s.start()
-        if threaded and "ingestion" in self.services:
-            # periodic ingestion of every enabled source (reference ingestion/main.py:374-385);
-            # INGESTION_SCHEDULE_INTERVAL_SECONDS <= 0 turns it off
-            from .ingestion import IngestionScheduler
-            interval = self.cfgs["ingestion"].schedule_interval_seconds
-            ing = self.services["ingestion"]
-            if interval and interval > 0 and getattr(ing, "scheduler", None) is None:
-                ing.scheduler = IngestionScheduler(ing, interval_seconds=interval)
-                ing.scheduler.start()
+        if threaded:
+            self.start_scheduler()
         if threaded:
             for name, s in self.services.items():
                 if s.subscriber is not None:
@@ -142,6 +135,20 @@ class Node:
                     s.consumer_thread = t
                     t.start()
                     self._threads.append(t)
+
+    def start_scheduler(self) -> bool:
+        """Periodic ingestion of every enabled source (reference ingestion/main.py:374-385), in the
+        node and in a standalone ``main ingestion`` process alike; INGESTION_SCHEDULE_INTERVAL_SECONDS
+        <= 0 turns it off.  Returns whether a scheduler is running."""
+        ing = self.services.get("ingestion")
+        if ing is None:
+            return False
+        from .ingestion import IngestionScheduler
+        interval = self.cfgs["ingestion"].schedule_interval_seconds
+        if interval and interval > 0 and getattr(ing, "scheduler", None) is None:
+            ing.scheduler = IngestionScheduler(ing, interval_seconds=interval)
+            ing.scheduler.start()
+        return getattr(ing, "scheduler", None) is not None and ing.scheduler.is_running
 
     def stop(self) -> None:
         ing = self.services.get("ingestion")

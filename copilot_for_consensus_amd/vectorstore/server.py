@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import re
 import threading
 import time
 from pathlib import Path
@@ -35,6 +36,11 @@ from fastapi import Body, FastAPI
 from fastapi.responses import JSONResponse
 
 _DIST = {"cosine": "cosine", "euclid": "l2", "dot": "dot"}
+
+
+# Qdrant's own rule for collection names; anything else (e.g. "..", "a/b", "%2E%2E") would name a
+# directory outside the persist root once it reaches save() / rmtree()
+_VALID_NAME = re.compile(r"^[A-Za-z0-9_-]{1,255}$")
 
 
 def _ok(result: Any, t0: float) -> dict:
@@ -86,6 +92,8 @@ def create_vector_app(device: str = "cuda", capacity: int = 1 << 20, index_type:
         from . import HipFlatIndex
         for d in sorted(p for p in persist.iterdir() if (p / "collection.json").exists()):
             meta = json.loads((d / "collection.json").read_text())
+            if not _VALID_NAME.match(str(meta.get("name", ""))) or meta["name"] != d.name:
+                continue   # a hand-edited or foreign directory: never let it name a path
             c = _Collection(meta["name"], meta["size"], meta["distance"], device, 1024, "flat", 0, 8)
             if (d / "index.json").exists():
                 c.index = HipFlatIndex.load(d, device=device)
@@ -95,12 +103,26 @@ def create_vector_app(device: str = "cuda", capacity: int = 1 << 20, index_type:
         if not persist:
             return
         import json
-        d = persist / c.name
+        d = coll_dir(c.name)
         c.index.save(d)
         (d / "collection.json").write_text(json.dumps({"name": c.name, "size": c.size, "distance": c.distance}))
 
     load_persisted()
     app.state.save_all = lambda: [save(c) for c in list(cols.values())]
+
+    def coll_dir(name: str) -> Path:
+        """persist/<name>, refused unless it resolves to a direct child of the persist root."""
+        d = (persist / name).resolve()
+        if not _VALID_NAME.match(name) or d.parent != persist.resolve():
+            raise ValueError(f"invalid collection name {name!r}")
+        return d
+
+    @app.middleware("http")
+    async def reject_bad_names(request, call_next):
+        parts = request.url.path.split("/")
+        if len(parts) >= 3 and parts[1] == "collections" and parts[2] and not _VALID_NAME.match(parts[2]):
+            return _err(400, f"invalid collection name {parts[2]!r}: expected [A-Za-z0-9_-]{{1,255}}")
+        return await call_next(request)
 
     def get(name: str) -> _Collection | None:
         with lock:
@@ -159,6 +181,8 @@ def create_vector_app(device: str = "cuda", capacity: int = 1 << 20, index_type:
         size, dist = vec.get("size"), str(vec.get("distance", "Cosine"))
         if not isinstance(size, int) or size <= 0 or dist.lower() not in _DIST:
             return _err(400, "vectors.size must be a positive int and distance one of Cosine, Euclid, Dot")
+        if not _VALID_NAME.match(name):
+            return _err(400, f"invalid collection name {name!r}: expected [A-Za-z0-9_-]{{1,255}}")
         with lock:
             if name in cols:
                 return _err(409, f"Collection `{name}` already exists!")
@@ -170,9 +194,9 @@ def create_vector_app(device: str = "cuda", capacity: int = 1 << 20, index_type:
         t0 = time.perf_counter()
         with lock:
             found = cols.pop(name, None) is not None
-        if found and persist and (persist / name).exists():
+        if found and persist and coll_dir(name).exists():
             import shutil
-            shutil.rmtree(persist / name, ignore_errors=True)
+            shutil.rmtree(coll_dir(name), ignore_errors=True)
         return _ok(found, t0)
 
     @app.put("/collections/{name}/points")

@@ -100,7 +100,7 @@ __device__ __forceinline__ uint4 dg_ldw(const uint16_t* p) {
 }
 
 // ABL: ablation builds for the timing probes only (scripts/bench_dgemm.py --ablate); 0 in production.
-//   1 = no X DMA, 2 = no ds_read / MFMA (W loads kept live).
+//   1 = no X DMA, 2 = no ds_read / MFMA (W loads kept live), 4 = no K-order rotation.
 template <int BM, int BN, int EPI, bool NTW, int ABL = 0>
 __global__ void __launch_bounds__(64 * (BN / 16 + DG_LOADERS), 1)
     dgemm_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W, int M, int N, int K, int ntiles,
@@ -120,6 +120,11 @@ __global__ void __launch_bounds__(64 * (BN / 16 + DG_LOADERS), 1)
   const int kb = (int)((long)ks * nks / split), ke = (int)((long)(ks + 1) * nks / split);
   const int nst = ke - kb;
   const int kq = lane >> 4;         // 8-element k group within a 32-deep MFMA step
+  // K-order rotation: workgroup `lid` walks its K slice starting at stage `rot` and wraps around,
+  // so the ~256 concurrent workgroups read different K offsets of their rows at any moment instead
+  // of all hitting the same power-of-2-strided address set in lock step (the sum is order-free)
+  const int rot = (ABL & 4) ? 0 : (int)((unsigned)lid * 37u % (unsigned)nst);
+  auto phys = [&](int s) { s += rot; return s >= nst ? s - nst : s; };
 
   if (w >= NW) {
     // ---------------- X loader wave: rows 8 XP l .. 8 XP (l+1) - 1 of the X stage image
@@ -136,7 +141,7 @@ __global__ void __launch_bounds__(64 * (BN / 16 + DG_LOADERS), 1)
     auto issue = [&](int st, int slot) {
       if constexpr ((ABL & 1) != 0) return;
 #pragma unroll
-      for (int i = 0; i < S::XP; ++i) dg_glds16(xsrc[i] + st * 64, lds0 + slot * S::XSTAGE + i * 1024);
+      for (int i = 0; i < S::XP; ++i) dg_glds16(xsrc[i] + phys(st) * 64, lds0 + slot * S::XSTAGE + i * 1024);
     };
 #pragma unroll
     for (int p = 0; p < S::NSX - 1; ++p)
@@ -157,7 +162,7 @@ __global__ void __launch_bounds__(64 * (BN / 16 + DG_LOADERS), 1)
   uint4 ring[D][2];
 #pragma unroll
   for (int p = 0; p < D; ++p) {
-    const int s = min(p, nst - 1);
+    const int s = phys(min(p, nst - 1));
     ring[p][0] = dg_ldw<NTW>(wp + s * 64);
     ring[p][1] = dg_ldw<NTW>(wp + s * 64 + 32);
   }
@@ -192,7 +197,7 @@ __global__ void __launch_bounds__(64 * (BN / 16 + DG_LOADERS), 1)
     for (int u = 0; u < D; ++u) {
       dg_barrier();                 // X stage st+u is in LDS
       compute(ring[u]);
-      const int s = min(st + u + D, nst - 1);   // unconditional: the tail re-reads the last stage
+      const int s = phys(min(st + u + D, nst - 1));   // unconditional: the tail re-reads the last stage
       ring[u][0] = dg_ldw<NTW>(wp + s * 64);
       ring[u][1] = dg_ldw<NTW>(wp + s * 64 + 32);
     }
@@ -298,10 +303,10 @@ CFC_API int cfc_dgemm(const void* x, const void* w, int M, int N, int K, int spl
 }
 
 // Timing probe only (scripts/bench_dgemm.py --ablate): split-K partial GEMM at BM = 128 with
-// ablation bits `abl` (1 no X DMA, 2 no MFMA) and +8 = nontemporal W loads.
+// ablation bits `abl` (1 no X DMA, 2 no MFMA, 4 no K rotation) and +8 = nontemporal W loads.
 CFC_API int cfc_dgemm_ablate(const void* x, const void* w, int M, int N, int K, int split, int bn, int abl,
                              float* part, hipStream_t stream) {
-  if (M > 128 || (abl & ~11)) return -1;
+  if (M > 128 || (abl & ~15)) return -1;
   if (const int e = dgemm_check(M, N, K, split, DG_PART, bn, part, nullptr)) return e;
   int rc;
   switch (abl) {
@@ -313,6 +318,8 @@ CFC_API int cfc_dgemm_ablate(const void* x, const void* w, int M, int N, int K, 
     case 9: rc = dgemm_launch<128, true, 1>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
     case 10: rc = dgemm_launch<128, true, 2>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
     case 11: rc = dgemm_launch<128, true, 3>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
+    case 4: rc = dgemm_launch<128, false, 4>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
+    case 7: rc = dgemm_launch<128, false, 7>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
     default: return -3;
   }
   return rc ? rc : CFC_CHECK_LAUNCH();

@@ -129,7 +129,7 @@ def main():
                 row[f"dg_bn{bn}_s{s}_us"] = round(timed(fns), 1)
             if args.ablate and M <= 128:
                 part = torch.empty(s_def, M, N, device="cuda", dtype=torch.float32)
-                for abl in (1, 2, 3, 8, 9, 10, 11):
+                for abl in (1, 2, 3, 4, 7, 9, 11):
                     fns = [lambda ww=ww, a=abl: K.check(K.kernels().cfc_dgemm_ablate(
                         x.data_ptr(), ww.data_ptr(), M, N, Kd, s_def, bn_d, a, part.data_ptr(), K._stream(x)),
                         "ablate") for ww in calls]

@@ -311,3 +311,20 @@ def test_jwt_auth_across_processes(deployment, tmp_path):
     assert _http("GET", d.url("reporting", "/api/reports"), headers={"Authorization": f"Bearer {bob2}"})[0] == 200
     assert _http("POST", d.url("ingestion", "/api/sources"), {**body, "name": "x"},
                  {"Authorization": f"Bearer {bob2}"})[0] == 403
+
+
+@pytest.mark.timeout(180)
+def test_standalone_ingestion_process_runs_its_scheduler(tmp_path):
+    """`main ingestion` on its own (the compose topology's ingestion container) starts
+    the periodic IngestionScheduler, as the reference's ingestion/main.py does; /health says so."""
+    d = Deployment(tmp_path, {"MESSAGE_BUS_TYPE": "noop", "DOCUMENT_STORE_TYPE": "inmemory",
+                              "VECTOR_STORE_TYPE": "inmemory", "INGESTION_SCHEDULE_INTERVAL_SECONDS": "3600"})
+    d.start("ingestion")
+    try:
+        d.wait_ready("ingestion")
+        code, health = _http("GET", d.url("ingestion", "/health"))
+        assert code == 200 and health["scheduler_running"] is True, health
+    finally:
+        p = d.procs["ingestion"]
+        os.killpg(p.pid, signal.SIGTERM)
+        p.wait(30)

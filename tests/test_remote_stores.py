@@ -173,3 +173,33 @@ def test_qdrant_rest_query_points_and_errors(qdrant_server):
     code, data = call("POST", "/collections/x/points/search/batch",
                       {"searches": [{"vector": [0, 0, 0], "limit": 1}, {"vector": [3, 4, 0], "limit": 1}]})
     assert [[p["id"] for p in r] for r in data["result"]] == [[1], [2]]
+
+
+def test_qdrant_rest_rejects_path_traversal_names(qdrant_server, tmp_path):
+    """a collection named '..' (or with a slash) must never reach save() / rmtree()."""
+    import json
+    import urllib.request
+    app, port = qdrant_server
+    base = f"http://127.0.0.1:{port}"
+    marker = tmp_path / "keep.txt"
+    marker.write_text("x")
+
+    def call(method, path, body=None):
+        req = urllib.request.Request(base + path, method=method, data=None if body is None else json.dumps(body).encode(),
+                                     headers={"Content-Type": "application/json"})
+        try:
+            with urllib.request.urlopen(req) as r:
+                return r.status
+        except urllib.error.HTTPError as e:
+            return e.code
+
+    for bad in ("%2E%2E", "a%2Fb", "..", "x%00y", "a.b"):
+        assert call("PUT", f"/collections/{bad}", {"vectors": {"size": 3}}) in (400, 404), bad
+        assert call("DELETE", f"/collections/{bad}") in (400, 404), bad
+        assert call("PUT", f"/collections/{bad}/points", {"points": []}) in (400, 404), bad
+    assert call("PUT", "/collections/ok_name-1", {"vectors": {"size": 3}}) == 200
+    app.state.save_all()
+    assert marker.exists() and (tmp_path / "vs" / "ok_name-1" / "collection.json").exists()
+    assert call("DELETE", "/collections/ok_name-1") == 200
+    assert marker.exists() and not (tmp_path / "vs" / "ok_name-1").exists()
+    assert sorted(app.state.collections) == []
