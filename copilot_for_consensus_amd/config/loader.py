@@ -3,7 +3,10 @@
 Mirrors the reference's runtime loader (adapters/copilot_config/copilot_config/runtime_loader.py:423
 ``get_config``; adapter_factory.py:26 ``create_adapter``): service settings come from env vars
 (with aliases) and defaults, each adapter's driver is chosen by its discriminant env var, driver
-fields are read from env / secrets and validated (type coercion, required fields).  Instead of
+fields are read from env / secrets, coerced to their types and validated against the driver's
+constraints (specs.CONSTRAINTS: required, minLength, pattern, enum, minimum / maximum, format: uri,
+conditional and one-of requirements -- the reference's schema_validation.py:279-372, applied at
+load time as runtime_loader.py:217 does).  Instead of
 code-generated dataclasses (scripts/generate_typed_configs.py) the typed objects are built from
 the spec tables at import time, and ``config_json_schema`` emits the JSON Schema served at
 ``/.well-known/configuration-schema``.
@@ -105,8 +108,70 @@ def env_is_set(name: str, env: Mapping[str, str] | None = None) -> bool:
     return bool((os.environ if env is None else env).get(name))
 
 
+def _missing(value: Any, rules: Mapping[str, Any]) -> bool:
+    if value is None:
+        return True
+    return isinstance(value, str) and int(rules.get("minLength", 0) or 0) >= 1 and len(value.strip()) < rules["minLength"]
+
+
+def _is_uri(value: str) -> bool:
+    from urllib.parse import urlparse
+    p = urlparse(value)
+    return bool(p.scheme and p.netloc)
+
+
+def validate_driver_config(adapter: str, driver: str, config: Mapping[str, Any]) -> None:
+    """Raise ConfigError when ``config`` breaks a rule of (adapter, driver) in specs.CONSTRAINTS.
+    Messages follow the reference: "<field> parameter is required" / "... is invalid"."""
+    import re
+
+    c = specs.CONSTRAINTS.get((adapter, driver))
+    if not c:
+        return
+    fields = c.get("fields", {})
+    where = f"{adapter}/{driver}"
+    for name in c.get("required", []):
+        if _missing(config.get(name), fields.get(name, {})):
+            raise ConfigError(f"{where}: {name} parameter is required")
+    for name, rules in fields.items():
+        v = config.get(name)
+        if v is None:
+            continue
+        if isinstance(v, str):
+            if _missing(v, rules):
+                raise ConfigError(f"{where}: {name} parameter is required")
+            if "pattern" in rules and re.match(rules["pattern"], v) is None:
+                raise ConfigError(f"{where}: {name} parameter is invalid ({v!r} !~ {rules['pattern']})")
+            if "enum" in rules:
+                vals = rules["enum"]
+                ok = (v.upper() in [str(e).upper() for e in vals]) if rules.get("case_insensitive") else v in vals
+                if not ok:
+                    raise ConfigError(f"{where}: {name} parameter is invalid ({v!r} not in {vals})")
+            if rules.get("format") == "uri" and not _is_uri(v):
+                raise ConfigError(f"{where}: {name} parameter is invalid (not a URI: {v!r})")
+        if isinstance(v, (int, float)) and not isinstance(v, bool):
+            if "minimum" in rules and v < rules["minimum"]:
+                raise ConfigError(f"{where}: {name} parameter is invalid ({v} < {rules['minimum']})")
+            if "maximum" in rules and v > rules["maximum"]:
+                raise ConfigError(f"{where}: {name} parameter is invalid ({v} > {rules['maximum']})")
+    for rule in c.get("conditional_required", []):
+        cond = rule["if"]
+        actual = config.get(cond["field"])
+        if isinstance(actual, str) and isinstance(cond["equals"], str):
+            hit = actual.upper() == cond["equals"].upper()
+        else:
+            hit = actual == cond["equals"]
+        for name in rule.get("then_required" if hit else "else_required", []):
+            if _missing(config.get(name), fields.get(name, {})):
+                raise ConfigError(f"{where}: {name} parameter is required when {cond['field']}={actual!r}")
+    for group in c.get("required_one_of", []):
+        if all(_missing(config.get(n), fields.get(n, {})) for n in group):
+            raise ConfigError(f"{where}: Either {' or '.join(group)} parameter is required")
+
+
 def load_adapter_config(adapter: str, env: Mapping[str, str] | None = None, driver: str | None = None,
-                        secrets=None, overrides: Mapping[str, Any] | None = None) -> AdapterConfig:
+                        secrets=None, overrides: Mapping[str, Any] | None = None,
+                        validate: bool = True) -> AdapterConfig:
     env = os.environ if env is None else env
     field, disc_env, default_driver, drivers = specs.ADAPTERS[adapter]
     if driver is None:
@@ -128,6 +193,8 @@ def load_adapter_config(adapter: str, env: Mapping[str, str] | None = None, driv
                     except Exception:  # secret backends are best effort at config time
                         val = None
             cfg[name] = val
+        if validate:
+            validate_driver_config(adapter, driver, cfg)
     return AdapterConfig(adapter, driver, cfg)
 
 
@@ -141,7 +208,9 @@ def get_config(service: str, env: Mapping[str, str] | None = None, secrets=None,
     if secrets is None and "secret_provider" in sspec["adapters"]:
         try:
             from ..security.secrets import create_secret_provider
-            secrets = create_secret_provider(load_adapter_config("secret_provider", env))
+            sp = load_adapter_config("secret_provider", env)
+            # the env driver reads the same mapping the rest of the config comes from
+            secrets = create_secret_provider(sp, **({"env": env} if sp.driver_name == "env" else {}))
         except Exception:
             secrets = None
     adapters = {}

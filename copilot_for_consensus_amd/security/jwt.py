@@ -298,6 +298,182 @@ class ECKey:
                            "y": b64u(_int_to_b(self.y, 32)), "d": b64u(_int_to_b(self.d, 32))})
 
 
+# ------------------------------------------------------------------------------------ PEM / DER
+# Just enough ASN.1 DER for the key files the reference's auth/generate_keys.py writes (PKCS#8
+# PrivateKeyInfo + SubjectPublicKeyInfo, via `cryptography`) and for OpenSSL's PKCS#1 / SEC1
+# forms, so a deployment's existing /run/secrets/jwt_private_key works unchanged.
+
+_OID_RSA = bytes.fromhex("2a864886f70d010101")          # 1.2.840.113549.1.1.1 rsaEncryption
+_OID_EC = bytes.fromhex("2a8648ce3d0201")                # 1.2.840.10045.2.1 id-ecPublicKey
+_OID_P256 = bytes.fromhex("2a8648ce3d030107")            # 1.2.840.10045.3.1.7 prime256v1
+
+
+def _der_read(buf: bytes, pos: int = 0) -> tuple[int, bytes, int]:
+    """One TLV at ``pos``: (tag, value, position after it)."""
+    if pos + 2 > len(buf):
+        raise JWTError("truncated DER")
+    tag, ln = buf[pos], buf[pos + 1]
+    pos += 2
+    if ln & 0x80:
+        n = ln & 0x7F
+        if n == 0 or n > 4 or pos + n > len(buf):
+            raise JWTError("bad DER length")
+        ln = int.from_bytes(buf[pos:pos + n], "big")
+        pos += n
+    if pos + ln > len(buf):
+        raise JWTError("truncated DER")
+    return tag, buf[pos:pos + ln], pos + ln
+
+
+def _der_items(seq: bytes) -> list[tuple[int, bytes]]:
+    out, pos = [], 0
+    while pos < len(seq):
+        tag, val, pos = _der_read(seq, pos)
+        out.append((tag, val))
+    return out
+
+
+def _der(tag: int, val: bytes) -> bytes:
+    n = len(val)
+    if n < 0x80:
+        return bytes([tag, n]) + val
+    lb = _int_to_b(n)
+    return bytes([tag, 0x80 | len(lb)]) + lb + val
+
+
+def _der_int(v: int) -> bytes:
+    b = _int_to_b(v) if v else b"\x00"
+    return _der(0x02, (b"\x00" + b) if b[0] & 0x80 else b)
+
+
+def _pem_decode(text: str) -> tuple[str, bytes]:
+    lines = [ln.strip() for ln in text.strip().splitlines() if ln.strip()]
+    if len(lines) < 2 or not lines[0].startswith("-----BEGIN ") or not lines[-1].startswith("-----END "):
+        raise JWTError("not a PEM block")
+    return lines[0][11:].rstrip("-").strip(), base64.b64decode("".join(lines[1:-1]))
+
+
+def _pem_encode(label: str, der: bytes) -> str:
+    body = base64.b64encode(der).decode()
+    return f"-----BEGIN {label}-----\n" + "\n".join(body[i:i + 64] for i in range(0, len(body), 64)) + \
+        f"\n-----END {label}-----\n"
+
+
+def _ints(seq: bytes) -> list[int]:
+    return [int.from_bytes(v, "big") for t, v in _der_items(seq) if t == 0x02]
+
+
+def load_pem_key(text: str) -> "RSAKey | ECKey":
+    """A PEM private or public key: PKCS#8 / PKCS#1 / SEC1 private keys, SPKI / PKCS#1 public keys
+    (RSA, or EC on P-256)."""
+    label, der = _pem_decode(text)
+    tag, body, _ = _der_read(der)
+    if tag != 0x30:
+        raise JWTError("PEM body is not a DER SEQUENCE")
+    items = _der_items(body)
+    if label == "RSA PRIVATE KEY":
+        v = _ints(body)
+        return RSAKey(v[1], v[2], v[3], v[4], v[5])
+    if label == "RSA PUBLIC KEY":
+        n, e = _ints(body)[:2]
+        return RSAKey(n, e)
+    if label == "EC PRIVATE KEY":
+        return _ec_from_sec1(body)
+    if label == "PRIVATE KEY":          # PKCS#8 PrivateKeyInfo {version, algorithm, privateKey}
+        alg = _der_items(items[1][1])
+        inner = _der_read(items[2][1])[1]
+        if alg[0][1] == _OID_RSA:
+            v = _ints(inner)
+            return RSAKey(v[1], v[2], v[3], v[4], v[5])
+        if alg[0][1] == _OID_EC and len(alg) > 1 and alg[1][1] == _OID_P256:
+            return _ec_from_sec1(inner)
+        raise JWTError("unsupported PKCS#8 key algorithm (RSA and EC P-256 only)")
+    if label == "PUBLIC KEY":           # SubjectPublicKeyInfo {algorithm, BIT STRING}
+        alg = _der_items(items[0][1])
+        bits = items[1][1][1:]          # skip the unused-bits byte
+        if alg[0][1] == _OID_RSA:
+            n, e = _ints(_der_read(bits)[1])[:2]
+            return RSAKey(n, e)
+        if alg[0][1] == _OID_EC and bits[:1] == b"\x04" and len(bits) == 65:
+            return ECKey(int.from_bytes(bits[1:33], "big"), int.from_bytes(bits[33:], "big"))
+        raise JWTError("unsupported public key algorithm (RSA and EC P-256 only)")
+    raise JWTError(f"unsupported PEM block {label!r}")
+
+
+def _ec_from_sec1(seq: bytes) -> "ECKey":
+    """ECPrivateKey {version, privateKey OCTET STRING, [0] params, [1] publicKey}."""
+    items = _der_items(seq)
+    d = int.from_bytes(items[1][1], "big")
+    x, y = _jmul(d, _G)
+    return ECKey(x, y, d)
+
+
+def rsa_private_pem(k: "RSAKey") -> str:
+    """PKCS#8 PEM (the format of the reference's generate_keys.py)."""
+    dp, dq, qi = k.d % (k.p - 1), k.d % (k.q - 1), pow(k.q, -1, k.p)
+    rsa = _der(0x30, b"".join(_der_int(v) for v in (0, k.n, k.e, k.d, k.p, k.q, dp, dq, qi)))
+    alg = _der(0x30, _der(0x06, _OID_RSA) + _der(0x05, b""))
+    return _pem_encode("PRIVATE KEY", _der(0x30, _der_int(0) + alg + _der(0x04, rsa)))
+
+
+def rsa_public_pem(k: "RSAKey") -> str:
+    alg = _der(0x30, _der(0x06, _OID_RSA) + _der(0x05, b""))
+    pub = _der(0x30, _der_int(k.n) + _der_int(k.e))
+    return _pem_encode("PUBLIC KEY", _der(0x30, alg + _der(0x03, b"\x00" + pub)))
+
+
+def ec_private_pem(k: "ECKey") -> str:
+    sec1 = _der(0x30, _der_int(1) + _der(0x04, _int_to_b(k.d, 32)) +
+                _der(0xA1, _der(0x03, b"\x00\x04" + _int_to_b(k.x, 32) + _int_to_b(k.y, 32))))
+    alg = _der(0x30, _der(0x06, _OID_EC) + _der(0x06, _OID_P256))
+    return _pem_encode("PRIVATE KEY", _der(0x30, _der_int(0) + alg + _der(0x04, sec1)))
+
+
+def _load_private(text: str, kind: type):
+    """A private key given as PEM (any form load_pem_key reads) or as this module's JSON."""
+    if text.lstrip().startswith("-----BEGIN"):
+        key = load_pem_key(text)
+    else:
+        key = RSAKey.from_private_json(text) if kind is RSAKey else ECKey.from_jwk(json.loads(text))
+    if not isinstance(key, kind) or key.d is None:
+        raise JWTError(f"expected a {kind.__name__[:2]} private key")
+    return key
+
+
+def _check_public(key, public_key: str | None) -> None:
+    """The configured public key must be the private key's own (a mismatched pair would mint
+    tokens that no verifier holding the published key accepts)."""
+    if not public_key:
+        return
+    pub = load_pem_key(public_key) if public_key.lstrip().startswith("-----BEGIN") else None
+    if pub is None:
+        return
+    same = (pub.n, pub.e) == (key.n, key.e) if isinstance(key, RSAKey) else (pub.x, pub.y) == (key.x, key.y)
+    if not same:
+        raise JWTError("public_key does not match private_key")
+
+
+def generate_keys(output_dir, algorithm: str = "RS256", bits: int = 2048) -> tuple:
+    """Write ``jwt_private_key`` / ``jwt_public_key`` (PEM) into a secrets directory -- the local
+    secret provider's layout (reference auth/generate_keys.py writes the same PKCS#8 / SPKI PEM).
+    Existing files are kept.  Returns the two paths."""
+    from pathlib import Path
+    out = Path(output_dir)
+    out.mkdir(parents=True, exist_ok=True)
+    priv, pub = out / "jwt_private_key", out / "jwt_public_key"
+    if not (priv.exists() and pub.exists()):
+        if algorithm.upper().startswith("ES"):
+            k = ECKey.generate()
+            priv.write_text(ec_private_pem(k))
+            pub.write_text(k.public_pem())
+        else:
+            k = RSAKey.generate(bits)
+            priv.write_text(rsa_private_pem(k))
+            pub.write_text(rsa_public_pem(k))
+        priv.chmod(0o600)
+    return priv, pub
+
+
 # ------------------------------------------------------------------------------------ signers
 
 class JWTSigner(ABC):
@@ -336,13 +512,15 @@ class HMACSigner(JWTSigner):
 class RSASigner(JWTSigner):
     algorithm = "RS256"
 
-    def __init__(self, private_key: str | RSAKey | None = None, key_id: str = "default", bits: int = 2048, **_):
+    def __init__(self, private_key: str | RSAKey | None = None, key_id: str = "default", bits: int = 2048,
+                 public_key: str | None = None, **_):
         if isinstance(private_key, RSAKey):
             self.key = private_key
         elif private_key:
-            self.key = RSAKey.from_private_json(private_key)
+            self.key = _load_private(private_key, RSAKey)
         else:
-            self.key = RSAKey.generate(bits)
+            self.key = RSAKey.generate(bits)   # tests / explicit ephemeral use; config requires a key
+        _check_public(self.key, public_key)
         self.key_id = key_id
 
     def sign(self, message):
@@ -358,13 +536,15 @@ class RSASigner(JWTSigner):
 class ECSigner(JWTSigner):
     algorithm = "ES256"
 
-    def __init__(self, private_key: str | ECKey | None = None, key_id: str = "default", **_):
+    def __init__(self, private_key: str | ECKey | None = None, key_id: str = "default", public_key: str | None = None,
+                 **_):
         if isinstance(private_key, ECKey):
             self.key = private_key
         elif private_key:
-            self.key = ECKey.from_jwk(json.loads(private_key))
+            self.key = _load_private(private_key, ECKey)
         else:
             self.key = ECKey.generate()
+        _check_public(self.key, public_key)
         self.key_id = key_id
 
     def sign(self, message):

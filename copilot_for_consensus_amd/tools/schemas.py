@@ -17,9 +17,47 @@ import sys
 from pathlib import Path
 
 
+def driver_json_schema(adapter: str, driver: str) -> dict:
+    """One driver's schema in the reference's layout (docs/schemas/configs/adapters/drivers/
+    <adapter>/<driver>.json): properties with source/env_var/default plus the validation keywords
+    and x-* extensions of config/specs.py CONSTRAINTS."""
+    from ..config.loader import _field_schema
+    from ..config.specs import ADAPTERS, CONSTRAINTS, SECRET_FIELDS
+    fields = ADAPTERS[adapter][3][driver]
+    c = CONSTRAINTS.get((adapter, driver), {})
+    props = {}
+    for name, spec in fields.items():
+        p = _field_schema(spec)
+        secret = SECRET_FIELDS.get((adapter, driver, name))
+        if secret:
+            p.update(source="secret", secret_name=secret)
+        p.update({k: v for k, v in c.get("fields", {}).get(name, {}).items() if k != "case_insensitive"})
+        props[name] = p
+    out = {"$schema": "https://json-schema.org/draft/2020-12/schema", "title": f"{adapter} driver {driver}",
+           "type": "object", "properties": props}
+    if c.get("required"):
+        out["required"] = list(c["required"])
+    if c.get("conditional_required"):
+        out["x-conditional_required"] = [dict(r) for r in c["conditional_required"]]
+    if c.get("required_one_of"):
+        out["x-required_one_of"] = [list(g) for g in c["required_one_of"]]
+    return out
+
+
+def adapter_json_schema(adapter: str) -> dict:
+    """The adapter schema (reference docs/schemas/configs/adapters/<adapter>.json): discriminant
+    env var and the driver schema references."""
+    from ..config.specs import ADAPTERS
+    field, env, default, drivers = ADAPTERS[adapter]
+    return {"$schema": "https://json-schema.org/draft/2020-12/schema", "title": f"{adapter} adapter",
+            "type": "object",
+            "discriminant": {"field": field, "env_var": env, "enum": sorted(drivers), "default": default},
+            "drivers": {d: {"$ref": f"drivers/{adapter}/{d}.json"} for d in drivers}}
+
+
 def export_all(root: str | Path) -> list[Path]:
     from ..config.loader import config_json_schema
-    from ..config.specs import SERVICES
+    from ..config.specs import ADAPTERS, SERVICES
     from ..contracts.registry import default_provider
     root = Path(root)
     out = default_provider().export(root)
@@ -29,6 +67,16 @@ def export_all(root: str | Path) -> list[Path]:
         p = cd / f"{svc}.json"
         p.write_text(json.dumps(config_json_schema(svc), indent=2) + "\n", encoding="utf-8")
         out.append(p)
+    ad = root / "configs" / "adapters"
+    for adapter, (_f, _e, _d, drivers) in ADAPTERS.items():
+        (ad / "drivers" / adapter).mkdir(parents=True, exist_ok=True)
+        p = ad / f"{adapter}.json"
+        p.write_text(json.dumps(adapter_json_schema(adapter), indent=2) + "\n", encoding="utf-8")
+        out.append(p)
+        for d in drivers:
+            p = ad / "drivers" / adapter / f"{d}.json"
+            p.write_text(json.dumps(driver_json_schema(adapter, d), indent=2) + "\n", encoding="utf-8")
+            out.append(p)
     return out
 
 

@@ -26,9 +26,9 @@ def main():
         calls = [ws[i % n] for i in range(max(48, n))]
         for rpi, d, rot in [(1, 2, 0), (1, 2, 1), (2, 2, 1), (2, 4, 1), (4, 4, 1), (4, 8, 1), (8, 8, 1), (8, 16, 1),
                             (16, 16, 0), (16, 16, 1), (16, 32, 1), (16, 8, 1)]:
-            st = torch.cuda.current_stream().cuda_stream
             def run(ww):
-                rc = lib.stream_probe(ww.data_ptr(), N, K, rpi, d, rot, out.data_ptr(), st)
+                rc = lib.stream_probe(ww.data_ptr(), N, K, rpi, d, rot, out.data_ptr(),
+                                      torch.cuda.current_stream().cuda_stream)
                 assert rc == 0, rc
             run(calls[0])
             torch.cuda.synchronize()

@@ -66,8 +66,13 @@ def test_overrides_beat_env():
 
 
 def test_every_service_loads_and_exports_schema():
+    from copilot_for_consensus_amd.security.jwt import RSAKey, rsa_private_pem, rsa_public_pem
+    k = RSAKey.generate(1024)
+    # the auth service's default local RS256 signer needs its key pair (reference
+    # drivers/jwt_signer/local.json x-conditional_required), here as env secrets
+    keys = {"JWT_PRIVATE_KEY": rsa_private_pem(k), "JWT_PUBLIC_KEY": rsa_public_pem(k), "SECRET_PROVIDER_TYPE": "env"}
     for svc in specs.SERVICES:
-        cfg = get_config(svc, env={})
+        cfg = get_config(svc, env=keys if svc == "auth" else {})
         sch = config_json_schema(svc)
         assert sch["service_name"] == svc
         for a in specs.SERVICES[svc]["adapters"]:

@@ -267,8 +267,11 @@ def test_jwt_auth_across_processes(deployment, tmp_path):
     """Auth as its own process (RS256 keys, mock OIDC provider, roles in the shared document store);
     ingestion and reporting in theirs verify bearer tokens against its JWKS (reference
     copilot_auth/middleware.py:122-270, role checks :424; ingestion requires admin, reporting reader)."""
+    from copilot_for_consensus_amd.security.jwt import generate_keys
+    priv, pub = generate_keys(tmp_path / "secrets")      # what tools.generate_keys writes
     d = deployment({"JWT_AUTH_ENABLED": "true", "AUTH_ENABLE_MOCK_PROVIDER": "true",
-                    "AUTH_FIRST_USER_AUTO_PROMOTION_ENABLED": "true", "AUTH_JWT_ALGORITHM": "RS256"})
+                    "AUTH_FIRST_USER_AUTO_PROMOTION_ENABLED": "true", "AUTH_JWT_ALGORITHM": "RS256",
+                    "JWT_PRIVATE_KEY": priv.read_text(), "JWT_PUBLIC_KEY": pub.read_text()})
     auth_url = f"http://127.0.0.1:{d.ports['auth']}"
     d.env.update({"INGESTION_AUTH_SERVICE_URL": auth_url, "REPORTING_AUTH_SERVICE_URL": auth_url,
                   "AUTH_PORT": str(d.ports["auth"])})

@@ -188,7 +188,9 @@ def test_services_pipeline_over_rabbitmq_driver(broker, tmp_path):
     env = {"DOCUMENT_STORE_TYPE": "inmemory", "MESSAGE_BUS_TYPE": "rabbitmq", "RABBITMQ_HOST": "127.0.0.1",
            "METRICS_TYPE": "noop", "LOG_TYPE": "silent", "ERROR_REPORTER_TYPE": "silent",
            "EMBEDDING_BACKEND_TYPE": "mock", "VECTOR_STORE_TYPE": "inmemory", "LLM_BACKEND_TYPE": "mock",
-           "ARCHIVE_STORE_TYPE": "inmemory", "SECRET_PROVIDER_TYPE": "env"}
+           "ARCHIVE_STORE_TYPE": "inmemory", "SECRET_PROVIDER_TYPE": "env",
+           # required by the rabbitmq driver schema (secrets rabbitmq_username / rabbitmq_password)
+           "RABBITMQ_USERNAME": "guest", "RABBITMQ_PASSWORD": "guest"}
     emb = HipEncoderProvider(model_name="tiny", device="cpu")
     node = Node(env=env, embedding_provider=emb, vector_store=HipFlatIndex(emb.dimension, device="cpu"),
                 summarizer=MockSummarizer(mock_latency_ms=0))
