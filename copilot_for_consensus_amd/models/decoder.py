@@ -129,6 +129,10 @@ class DecoderWeights:
         self.q_lm_head = None
         # opt-in W8A8 FP8 projections (e4m3fn + per-output-channel scales): to_fp8()
         self.fp8_layers: list[dict] | None = None
+        # second copies of the decode projections in the decode GEMM's fragment-packed layout
+        # (K.PackedWeight): pack_decode()
+        self.packed: list[dict] | None = None
+        self.packed_lm_head = None
         self.cos_sin = rope_cos_sin(cfg.max_positions, cfg.head_dim, cfg.rope_theta, device=self.device,
                                     llama3_scaling=cfg.rope_llama3)
 
@@ -303,8 +307,33 @@ class DecoderWeights:
             torch.cuda.empty_cache()
         return self
 
+    DECODE_PACKED = ("qkv", "o", "gate_up", "down")
+
+    def packed_bytes(self) -> int:
+        """HBM a pack_decode() adds (the projections + the lm_head, bf16)."""
+        n = sum(layer[k].numel() * 2 for layer in self.layers for k in self.DECODE_PACKED if layer.get(k) is not None)
+        return n + (self.lm_head.numel() * 2 if self.lm_head is not None else 0)
+
+    def pack_decode(self, m: int = 128) -> "DecoderWeights":
+        """Copy every decode projection (and the lm_head) into the decode GEMM's fragment-packed
+        layout, tiled for an m-row batch (K.pack_dgemm_weight: each 16-row x 32-k MFMA fragment 1 KB
+        contiguous, each workgroup's slice one contiguous span -- the flat stream runs at ~5.8 TB/s
+        where row-major fragments read at 4-5).  The row-major copies stay for prefill (hipBLASLt)
+        and the B <= 4 GEMV, so this costs packed_bytes() more HBM (14.5 GB for Mistral-7B):
+        DecoderModel takes it only where that fits."""
+        if self.packed is not None:
+            return self
+        self.packed = [{k: K.pack_dgemm_weight(layer[k], swiglu=k == "gate_up", m=m) for k in self.DECODE_PACKED}
+                       for layer in self.layers]
+        head = self.lm_head
+        if head is not None and head.shape[0] % 64 == 0 and head.shape[1] % 64 == 0:
+            self.packed_lm_head = K.pack_dgemm_weight(head, m=m)
+        return self
+
     def nbytes(self) -> int:
         n = sum(t.numel() * t.element_size() for layer in self.layers for t in layer.values() if t is not None)
+        n += sum(p.nbytes() for layer in self.packed or [] for p in layer.values())
+        n += self.packed_lm_head.nbytes() if self.packed_lm_head is not None else 0
         for q in self.fp8_layers or []:
             n += sum(a.numel() * a.element_size() + b.numel() * b.element_size() for a, b in q.values())
         return n + sum(t.numel() * t.element_size() for t in (self.embed, self.final_norm, self.lm_head))
@@ -379,6 +408,22 @@ class DecoderModel:
         # B <= 4 decode on the ggml-quantized weights (GGUF checkpoints; csrc/kernels/quant.hip)
         self.decode_qgemv = (weights.qlayers is not None and os.environ.get("CFC_DECODE_QGEMV", "1") != "0"
                              and weights.tp_size == 1 and weights.gate_up_interleaved and not self.fp8)
+        # packed decode weights (CFC_DECODE_PACKED: auto = when HBM allows, 1 = always, 0 = never)
+        if self.fused_decode and weights.device.type == "cuda" and self._want_packed():
+            weights.pack_decode()
+
+    PACKED_FREE_FRACTION = 0.3   # HBM left free after packing (KV pool, activations, workspaces)
+
+    def _want_packed(self) -> bool:
+        pk = os.environ.get("CFC_DECODE_PACKED", "auto")
+        if pk not in ("auto", "0", "1"):
+            raise ValueError(f"CFC_DECODE_PACKED={pk!r}: expected auto, 0 or 1")
+        if pk == "0" or not self.w.layers or self.w.layers[0].get("qkv") is None:
+            return False
+        if pk == "1":
+            return True
+        free, total = torch.cuda.mem_get_info(self.w.device)
+        return free - self.w.packed_bytes() > self.PACKED_FREE_FRACTION * total
 
     def _dgemm_shapes(self) -> bool:
         """Every decode projection of this rank fits the decode GEMM (N % 64, K % 64)."""
@@ -487,24 +532,25 @@ class DecoderModel:
         tp = w.tp_size > 1
         for i in range(cfg.layers):
             lw = w.layers[i]
-            qkv = K.dgemm_linear(h, lw["qkv"])
+            pw = w.packed[i] if w.packed is not None else lw    # fragment-packed copies when present
+            qkv = K.dgemm_linear(h, pw["qkv"])
             q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
                                 cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
             attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
                                             part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
                                             k_scale=kv.k_scale, v_scale=kv.v_scale)
             if tp:
-                o = self._all_reduce(K.dgemm_linear(attn.view(B, -1), lw["o"]))
+                o = self._all_reduce(K.dgemm_linear(attn.view(B, -1), pw["o"]))
                 h = K.rmsnorm(o, lw["mlp_norm"], eps, residual=residual)
             else:
-                h = K.dgemm_residual_rmsnorm(attn.view(B, -1), lw["o"], residual, lw["mlp_norm"], eps)
-            a = K.dgemm_swiglu(h, lw["gate_up"])
+                h = K.dgemm_residual_rmsnorm(attn.view(B, -1), pw["o"], residual, lw["mlp_norm"], eps)
+            a = K.dgemm_swiglu(h, pw["gate_up"])
             nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm
             if tp:
-                d = self._all_reduce(K.dgemm_linear(a, lw["down"]))
+                d = self._all_reduce(K.dgemm_linear(a, pw["down"]))
                 h = K.rmsnorm(d, nxt, eps, residual=residual)
             else:
-                h = K.dgemm_residual_rmsnorm(a, lw["down"], residual, nxt, eps)
+                h = K.dgemm_residual_rmsnorm(a, pw["down"], residual, nxt, eps)
         return h
 
     def _forward_decode_splitk(self, x, positions, slots, ctx_lens, block_tables, kv, attn_workspace, part_blocks):
@@ -618,7 +664,9 @@ class DecoderModel:
             local = K.gemv(hidden, self.w.lm_head)   # 262 MB weight stream: 4.6 -> ~6 TB/s at B=1
         elif (self.fused_decode and hidden.is_cuda and hidden.shape[0] > K.GEMV_MAX_M
                 and hidden.shape[0] <= DGEMM_MAX_ROWS and K.dgemm_ok(hidden, head)):
-            local = K.dgemm_linear(hidden, head)   # the 262 MB (Mistral) / 1 GB (Llama-3) vocab stream
+            # the 262 MB (Mistral) / 1 GB (Llama-3) vocab stream
+            ph = self.w.packed_lm_head
+            local = K.dgemm_linear(hidden, ph if ph is not None else head)
         else:
             local = F.linear(hidden, self.w.lm_head)
         if self.w.tp_size == 1:

@@ -53,8 +53,9 @@ _KERNEL_SIGS = {
     "cfc_l2_normalize": [P, P, P, I, I, P],
     "cfc_pool": [P, P, P, P, I, I, I, I, P],
     "cfc_splitk_reduce": [P, I, I, I, I, P, I, P],
-    "cfc_dgemm": [P, P, I, I, I, I, I, I, P, P, I, P],
+    "cfc_dgemm": [P, P, I, I, I, I, I, I, I, P, P, I, P],
     "cfc_dgemm_bm": [I],
+    "cfc_dgemm_pack": [P, P, I, I, I, P],
     "cfc_dgemm_ablate": [P, P, I, I, I, I, I, I, P, P],
     "cfc_gemv": [P, P, I, I, I, I, P, P, I, P],
     "cfc_qgemv": [P, I, I, I, I, P, P, c_int64, c_int64, c_int64, I, P, P, I, P],

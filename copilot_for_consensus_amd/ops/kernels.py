@@ -334,67 +334,119 @@ DGEMM_BNS = (128, 112, 96, 64)   # W rows per workgroup the kernel is built for
 DGEMM_CUS = 256                  # one workgroup per CU
 DGEMM_CU_RATE = 25e9             # W bytes/s one workgroup streams (6.4 TB/s over 256 CUs)
 DGEMM_PART_RATE = 6e12           # fp32 partial slab traffic, bytes/s
+DGEMM_X_RATE = 90e9              # per-CU L2 -> LDS rate of the X re-reads (ablation: X costs ~12 us of gate/up)
+
+
+class PackedWeight:
+    """A projection weight in the decode GEMM's fragment-packed layout for bn-row workgroups
+    (cfc_dgemm_pack): [N/bn][K/32][bn/16][64 lanes][8] bf16 -- every 16-row x 32-k MFMA B fragment
+    1 KB contiguous in lane order, each workgroup's W slice one contiguous span.  The row-major
+    copy stays for prefill (hipBLASLt) and the B <= 4 GEMV."""
+
+    __slots__ = ("data", "N", "K", "bn")
+
+    def __init__(self, data: torch.Tensor, N: int, K: int, bn: int):
+        self.data, self.N, self.K, self.bn = data, N, K, bn
+
+    @property
+    def shape(self):
+        return (self.N, self.K)
+
+    def nbytes(self) -> int:
+        return self.data.numel() * self.data.element_size()
+
+
+def pack_dgemm_weight(w: torch.Tensor, bn: int | None = None, swiglu: bool = False, m: int = 128) -> PackedWeight:
+    """Row-major bf16 W[N, K] -> PackedWeight for bn-row workgroups (default: the tile width the
+    decode GEMM picks for an m-row batch of this shape)."""
+    N, Kd = w.shape
+    bn = bn or dgemm_config(m, N, Kd, swiglu=swiglu)[0]
+    if w.is_cuda:
+        _req(w, torch.bfloat16, "w")
+        out = torch.empty(N * Kd, dtype=torch.bfloat16, device=w.device)
+        check(kernels().cfc_dgemm_pack(w.data_ptr(), out.data_ptr(), N, Kd, bn, _stream(w)), "cfc_dgemm_pack")
+    else:
+        out = ref.pack_dgemm_weight(w, bn).reshape(-1)
+    return PackedWeight(out, N, Kd, bn)
+
+
+def _rowmajor(w):
+    if isinstance(w, PackedWeight):
+        return ref.unpack_dgemm_weight(w.data.view(w.N // w.bn, w.K // 32, w.bn // 16, 64, 8))
+    return w
 
 
 def dgemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
     """Shapes the decode GEMM takes: bf16, contiguous, N % 64 == 0, K % 64 == 0."""
+    if isinstance(w, PackedWeight):
+        return (x.is_cuda and x.dim() == 2 and x.dtype == torch.bfloat16 and x.is_contiguous()
+                and w.K == x.shape[1] and w.N % 64 == 0 and w.K % 64 == 0 and x.shape[0] >= 1)
     return (x.is_cuda and x.dim() == 2 and w.dim() == 2 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
             and x.is_contiguous() and w.is_contiguous() and w.shape[1] == x.shape[1]
             and w.shape[0] % 64 == 0 and x.shape[1] % 64 == 0 and x.shape[0] >= 1)
 
 
-def dgemm_config(M: int, N: int, K: int, swiglu: bool = False) -> tuple[int, int]:
-    """(W rows per workgroup, split-K) for one decode projection, from a two-term cost model:
-    each workgroup streams its W slice at a per-CU rate, in ceil(blocks / CUs) rounds (a partial
-    second round doubles the stream time of the CUs that run it), plus the fp32 partial slabs
-    written and read back once.  A fused SwiGLU epilogue needs split 1."""
+def dgemm_config(M: int, N: int, K: int, swiglu: bool = False, bn: int | None = None) -> tuple[int, int]:
+    """(W rows per workgroup, split-K) for one decode projection, from a three-term cost model:
+    each workgroup streams its W slice from HBM at a per-CU rate and re-reads its X slice (every
+    workgroup reads all BM rows of its K range: X traffic / W traffic = BM / BN) from L2 at a
+    per-CU rate, in ceil(blocks / CUs) rounds (a partial second round doubles the time of the CUs
+    that run it), plus the fp32 partial slabs written and read back once.  A fused SwiGLU epilogue
+    needs split 1.  Rates fitted to bench_dgemm.py sweeps on one MI355X (profiles/dgemm_*.txt)."""
     bm = 64 if M <= 64 else (128 if M <= 128 else 256)
     mt = (M + bm - 1) // bm
     best = None
-    for bn in DGEMM_BNS:
-        if N % bn:
+    for cand in (bn,) if bn else DGEMM_BNS:
+        if N % cand:
             continue
-        tiles = (N // bn) * mt
+        tiles = (N // cand) * mt
         for split in ([1] if swiglu else range(1, K // 64 + 1)):
             blocks = tiles * split
             rounds = -(-blocks // DGEMM_CUS)
-            t = rounds * (N * K * 2 / (N // bn * split)) / DGEMM_CU_RATE
+            t = rounds * (cand * K * 2 / split / DGEMM_CU_RATE + bm * K * 2 / split / DGEMM_X_RATE)
             if split > 1:
                 t += 2 * split * M * N * 4 / DGEMM_PART_RATE
             if best is None or t < best[0] - 1e-12:
-                best = (t, bn, split)
+                best = (t, cand, split)
     return best[1], best[2]
 
 
 def dgemm(x: torch.Tensor, w: torch.Tensor, epi: str = "bf16", split: int = 1, bn: int | None = None,
           out: torch.Tensor | None = None, part: torch.Tensor | None = None) -> torch.Tensor:
     """One launch of the decode GEMM.  ``epi``: "bf16" -> out [M, N]; "swiglu" -> out [M, N/2]
-    (8-row interleaved gate/up weights); "part" -> fp32 split-K slabs part [split, M, N]."""
+    (8-row interleaved gate/up weights); "part" -> fp32 split-K slabs part [split, M, N].
+    ``w``: row-major bf16 [N, K] or a PackedWeight (the fast, contiguous-stream layout)."""
     M, Kd = x.shape
     N = w.shape[0]
     if not dgemm_ok(x, w):
-        raise ValueError(f"dgemm: x {tuple(x.shape)} {x.dtype} w {tuple(w.shape)} {w.dtype}")
+        raise ValueError(f"dgemm: x {tuple(x.shape)} {x.dtype} w {tuple(w.shape)} {getattr(w, 'dtype', 'packed')}")
+    packed = isinstance(w, PackedWeight)
+    wptr = w.data.data_ptr() if packed else w.data_ptr()
     mode = {"part": 0, "bf16": 1, "swiglu": 2}[epi]
+    if packed:
+        if bn not in (None, w.bn):
+            raise ValueError(f"dgemm: weight packed for bn={w.bn}, asked for bn={bn}")
+        bn = w.bn
     bn = bn or dgemm_config(M, N, Kd, swiglu=mode == 2)[0]
     st = _stream(x)
     if mode == 0:
         part = _workspace(x.device, split * M * N)[:split * M * N].view(split, M, N) if part is None else part
-        check(kernels().cfc_dgemm(x.data_ptr(), w.data_ptr(), M, N, Kd, split, 0, bn, part.data_ptr(), None, 0, st),
-              "cfc_dgemm")
+        check(kernels().cfc_dgemm(x.data_ptr(), wptr, M, N, Kd, split, 0, bn, int(packed), part.data_ptr(), None, 0,
+                                  st), "cfc_dgemm")
         return part
     if out is None:
         out = torch.empty(M, N // 2 if mode == 2 else N, dtype=torch.bfloat16, device=x.device)
-    check(kernels().cfc_dgemm(x.data_ptr(), w.data_ptr(), M, N, Kd, 1, mode, bn, None, out.data_ptr(), out.stride(0),
-                              st), "cfc_dgemm")
+    check(kernels().cfc_dgemm(x.data_ptr(), wptr, M, N, Kd, 1, mode, bn, int(packed), None, out.data_ptr(),
+                              out.stride(0), st), "cfc_dgemm")
     return out
 
 
 def dgemm_linear(x: torch.Tensor, w: torch.Tensor, split: int | None = None, bn: int | None = None) -> torch.Tensor:
     """bf16 x [M, K] @ w[N, K]^T on the decode GEMM (split-K slabs + reduce when N is small)."""
     if not x.is_cuda:
-        return torch.nn.functional.linear(x, w)
+        return torch.nn.functional.linear(x, _rowmajor(w))
     M, Kd = x.shape
-    cbn, csplit = dgemm_config(M, w.shape[0], Kd)
+    cbn, csplit = dgemm_config(M, w.shape[0], Kd, bn=getattr(w, "bn", None) or bn)
     bn, split = bn or cbn, split or csplit
     if split == 1:
         return dgemm(x, w, "bf16", bn=bn)
@@ -406,12 +458,13 @@ def dgemm_swiglu(x: torch.Tensor, w_gu_interleaved: torch.Tensor, split: int | N
     """silu(x @ gate^T) * (x @ up^T) for 8-row interleaved gate/up weights (SwiGLU in the GEMM's
     epilogue; split-K slabs + the SwiGLU reduce when asked for a split, e.g. TP-sharded N)."""
     if not x.is_cuda:
-        return ref.silu_mul_interleaved(torch.nn.functional.linear(x, w_gu_interleaved))
+        return ref.silu_mul_interleaved(torch.nn.functional.linear(x, _rowmajor(w_gu_interleaved)))
     M, Kd = x.shape
     N = w_gu_interleaved.shape[0]
+    wbn = getattr(w_gu_interleaved, "bn", None) or bn
     if split is None:
-        fbn, _ = dgemm_config(M, N, Kd, swiglu=True)
-        pbn, psplit = dgemm_config(M, N, Kd)
+        fbn, _ = dgemm_config(M, N, Kd, swiglu=True, bn=wbn)
+        pbn, psplit = dgemm_config(M, N, Kd, bn=wbn)
         # split-K + reduce only when the fused grid would leave most CUs idle
         use_split = (N // fbn) * ((M + 255) // 256) < DGEMM_CUS // 2 and psplit > 1
         bn, split = (bn or pbn, psplit) if use_split else (bn or fbn, 1)
@@ -425,9 +478,9 @@ def dgemm_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, residual: torch.Ten
     """residual += bf16(x @ w^T); returns RMSNorm(residual) * norm_w.  The split-K slabs go straight
     into the residual + RMSNorm reduce (same rounding points as the library split-K path)."""
     if not x.is_cuda:
-        return _linear_residual_rmsnorm_ref(x, w, residual, norm_w, eps)
+        return _linear_residual_rmsnorm_ref(x, _rowmajor(w), residual, norm_w, eps)
     M, Kd = x.shape
-    cbn, csplit = dgemm_config(M, w.shape[0], Kd)
+    cbn, csplit = dgemm_config(M, w.shape[0], Kd, bn=getattr(w, "bn", None) or bn)
     bn, split = bn or cbn, split or csplit
     return splitk_residual_rmsnorm(dgemm(x, w, "part", split, bn=bn), residual, norm_w, eps)
 

@@ -198,6 +198,21 @@ def deinterleave_gate_up(w: torch.Tensor) -> torch.Tensor:
     return torch.cat([v[:, 0].reshape(F, -1), v[:, 1].reshape(F, -1)]).contiguous()
 
 
+def pack_dgemm_weight(w: torch.Tensor, bn: int) -> torch.Tensor:
+    """Row-major W[N, K] -> the decode GEMM's fragment-packed layout for bn-row workgroups,
+    [N/bn, K/32, bn/16, 64, 8]: packed[t, kg, w, 16 q + r, j] = W[bn t + 16 w + r, 32 kg + 8 q + j]
+    (lane 16q + r of a 16x16x32 MFMA holds B[k = 8q + j][n = r]; one workgroup's slice is contiguous)."""
+    N, K = w.shape
+    v = w.reshape(N // bn, bn // 16, 16, K // 32, 4, 8)          # t, w, r, kg, q, j
+    return v.permute(0, 3, 1, 4, 2, 5).reshape(N // bn, K // 32, bn // 16, 64, 8).contiguous()
+
+
+def unpack_dgemm_weight(p: torch.Tensor) -> torch.Tensor:
+    T, G, NW = p.shape[0], p.shape[1], p.shape[2]
+    v = p.reshape(T, G, NW, 4, 16, 8)                              # t, kg, w, q, r, j
+    return v.permute(0, 2, 4, 1, 3, 5).reshape(T * NW * 16, G * 32).contiguous()
+
+
 def silu_mul_interleaved(gu):
     F, G = gu.shape[-1] // 2, GU_GROUP
     v = gu.reshape(*gu.shape[:-1], F // G, 2, G).float()

@@ -33,7 +33,7 @@ from ..contracts.events import EXCHANGE, Event, utc_now_iso
 from ..orchestration import (TopKRelevanceSelector, build_context, format_citations, prompt_template,
                              substitute_prompt)
 from ..parsing import MessageParser, ThreadBuilder
-from ..storage.document_store import InMemoryDocumentStore
+from ..storage.document_store import DocumentAlreadyExistsError, InMemoryDocumentStore
 from ..utils.synthetic import SyntheticArchive
 
 
@@ -105,8 +105,8 @@ class RagPipeline:
         try:
             self.docs.insert_document("archives", {"_id": aid, "file_hash": sha, "file_size_bytes": len(raw),
                                                    "source": "bench", "ingestion_date": started, "status": "pending"})
-        except Exception:
-            pass
+        except DocumentAlreadyExistsError:
+            pass    # the same synthetic archive again (content-addressed id): nothing new to record
         self._publish("ArchiveIngested", archive_id=aid, source_name="bench", source_type="local",
                       source_url=f"file:///bench/step{step}.mbox", file_size_bytes=len(raw), file_hash_sha256=sha,
                       ingestion_started_at=started, ingestion_completed_at=utc_now_iso())
@@ -237,8 +237,8 @@ class RagPipeline:
                    "metadata": {"summary_id": sid, "tokens_prompt": len(p), "tokens_completion": len(toks)}}
             try:
                 self.docs.insert_document("summaries", doc)
-            except Exception:
-                pass
+            except DocumentAlreadyExistsError:
+                self.docs.update_document("summaries", rid, doc)    # regenerated: the newest summary wins
             self.docs.update_document("threads", th["_id"], {"summary_id": rid})
             self._publish("ReportPublished", thread_id=th["_id"], report_id=rid, format="markdown", notified=False,
                           delivery_channels=["api"], summary_url=f"/api/reports/{rid}")

@@ -19,7 +19,7 @@ from abc import ABC, abstractmethod
 from datetime import datetime, timezone
 from typing import Any
 
-from .jwt import JWTError, JWTManager, decode
+from .jwt import ECKey, JWTError, JWTManager, RSAKey, decode, decode_unverified
 
 
 def pkce_pair() -> tuple[str, str]:
@@ -40,14 +40,112 @@ class IdentityProvider(ABC):
 
 
 class OIDCProvider(IdentityProvider):
-    def __init__(self, name: str, client_id: str, client_secret: str, redirect_uri: str, authorize_endpoint: str,
-                 token_endpoint: str, userinfo_endpoint: str, scope: str = "openid email profile"):
+    """OAuth2 / OpenID Connect code flow with PKCE.  With a ``discovery_url`` (or an ``issuer``,
+    whose ``/.well-known/openid-configuration`` is used) the endpoints, issuer and JWKS URI come
+    from discovery (reference oidc_provider.py:72-96) and every id_token is verified: RS256 / ES256
+    signature against the provider's JWKS (re-fetched once on an unknown ``kid``: key rotation),
+    ``iss``, ``aud`` = client_id, ``exp`` / ``nbf`` with leeway and ``nonce``
+    (oidc_provider.py:312-355).  Plain OAuth providers (GitHub) have no id_token."""
+
+    JWKS_TTL = 3600.0
+
+    def __init__(self, name: str, client_id: str, client_secret: str, redirect_uri: str,
+                 authorize_endpoint: str | None = None, token_endpoint: str | None = None,
+                 userinfo_endpoint: str | None = None, scope: str = "openid email profile",
+                 discovery_url: str | None = None, issuer: str | None = None, jwks_uri: str | None = None,
+                 leeway: int = 60):
         self.name = name
         self.client_id, self.client_secret, self.redirect_uri = client_id, client_secret, redirect_uri
         self.authorize_endpoint, self.token_endpoint = authorize_endpoint, token_endpoint
         self.userinfo_endpoint, self.scope = userinfo_endpoint, scope
+        if discovery_url is None and issuer:
+            discovery_url = issuer.rstrip("/") + "/.well-known/openid-configuration"
+        self.discovery_url, self.issuer, self.jwks_uri, self.leeway = discovery_url, issuer, jwks_uri, leeway
+        self._discovered = False
+        self._jwks: dict | None = None
+        self._jwks_at = 0.0
+        self._lock = threading.Lock()
+
+    def _fetch_json(self, url: str) -> dict:
+        req = urllib.request.Request(url, headers={"Accept": "application/json"})
+        return json.loads(urllib.request.urlopen(req, timeout=10).read())
+
+    def discover(self) -> None:
+        """Endpoints, issuer and jwks_uri from the discovery document (explicit arguments win)."""
+        if self._discovered or not self.discovery_url:
+            return
+        try:
+            doc = self._fetch_json(self.discovery_url)
+        except (OSError, ValueError) as e:
+            raise PermissionError(f"{self.name}: OIDC discovery failed: {e}") from e
+        self.authorize_endpoint = self.authorize_endpoint or doc.get("authorization_endpoint")
+        self.token_endpoint = self.token_endpoint or doc.get("token_endpoint")
+        self.userinfo_endpoint = self.userinfo_endpoint or doc.get("userinfo_endpoint")
+        self.jwks_uri = self.jwks_uri or doc.get("jwks_uri")
+        self.issuer = self.issuer or doc.get("issuer")
+        if not (self.authorize_endpoint and self.token_endpoint):
+            raise PermissionError(f"{self.name}: discovery document lacks authorization/token endpoints")
+        self._discovered = True
+
+    def _signing_key(self, header: dict):
+        """The JWKS key for this token's kid (one refresh on a miss or after JWKS_TTL)."""
+        for attempt in (0, 1):
+            with self._lock:
+                stale = self._jwks is None or time.time() - self._jwks_at > self.JWKS_TTL or attempt == 1
+                if stale:
+                    try:
+                        self._jwks, self._jwks_at = self._fetch_json(self.jwks_uri), time.time()
+                    except (OSError, ValueError) as e:
+                        raise PermissionError(f"{self.name}: JWKS fetch failed: {e}") from e
+                keys = [k for k in self._jwks.get("keys", []) if k.get("use", "sig") == "sig"]
+            kid = header.get("kid")
+            match = [k for k in keys if k.get("kid") == kid] if kid else (keys if len(keys) == 1 else [])
+            if match:
+                jwk = match[0]
+                return ECKey.from_jwk(jwk) if jwk.get("kty") == "EC" else RSAKey.from_jwk(jwk)
+            if stale:
+                break
+        raise PermissionError(f"{self.name}: id_token key {header.get('kid')!r} not in the provider JWKS")
+
+    def _expected_issuer(self, claims: dict) -> str | None:
+        iss = self.issuer
+        if iss and "{tenantid}" in iss:   # Microsoft multi-tenant discovery documents template the tenant
+            iss = iss.replace("{tenantid}", str(claims.get("tid", "")))
+        return iss
+
+    def verify_id_token(self, id_token: str, nonce: str) -> dict:
+        """Verified id_token claims (signature, iss, aud, exp/nbf, nonce); raises PermissionError."""
+        self.discover()
+        try:
+            header, claims = decode_unverified(id_token)
+        except JWTError as e:
+            raise PermissionError("malformed id_token") from e
+        if header.get("alg") not in ("RS256", "ES256"):
+            raise PermissionError(f"id_token algorithm {header.get('alg')!r} not accepted")
+        if self.jwks_uri:
+            try:
+                claims = decode(id_token, self._signing_key(header), audience=self.client_id,
+                                issuer=self._expected_issuer(claims), leeway=self.leeway)
+            except JWTError as e:
+                raise PermissionError(f"id_token rejected: {e}") from e
+        else:
+            # no JWKS published: the token came straight from the token endpoint over TLS (OIDC Core
+            # 3.1.3.7); the registered claims are still checked
+            now = time.time()
+            if "exp" in claims and now > claims["exp"] + self.leeway:
+                raise PermissionError("id_token expired")
+            aud = claims.get("aud")
+            if self.client_id not in (aud if isinstance(aud, list) else [aud]):
+                raise PermissionError("id_token audience mismatch")
+            want = self._expected_issuer(claims)
+            if want and claims.get("iss") != want:
+                raise PermissionError("id_token issuer mismatch")
+        if claims.get("nonce") != nonce:
+            raise PermissionError("id_token nonce mismatch")
+        return claims
 
     def authorization_url(self, state, nonce, code_challenge):
+        self.discover()
         q = {"response_type": "code", "client_id": self.client_id, "redirect_uri": self.redirect_uri,
              "scope": self.scope, "state": state, "nonce": nonce, "code_challenge": code_challenge,
              "code_challenge_method": "S256"}
@@ -64,17 +162,8 @@ class OIDCProvider(IdentityProvider):
 
     require_nonce = True
 
-    @staticmethod
-    def id_token_claims(id_token: str) -> dict:
-        """Payload of an ID token received straight from the token endpoint over TLS (OIDC Core
-        3.1.3.7 lets the code-flow client rely on the TLS server check instead of the signature)."""
-        try:
-            body = id_token.split(".")[1]
-            return json.loads(base64.urlsafe_b64decode(body + "=" * (-len(body) % 4)))
-        except (IndexError, ValueError) as e:
-            raise PermissionError("malformed id_token") from e
-
     def exchange_code(self, code, code_verifier, nonce):
+        self.discover()
         tok = self._post(self.token_endpoint, {"grant_type": "authorization_code", "code": code,
                                                "redirect_uri": self.redirect_uri, "client_id": self.client_id,
                                                "client_secret": self.client_secret, "code_verifier": code_verifier})
@@ -82,12 +171,7 @@ class OIDCProvider(IdentityProvider):
             raise PermissionError(f"token endpoint refused the code: {tok.get('error', 'no access_token')}")
         id_token = tok.get("id_token")
         if id_token:
-            claims = self.id_token_claims(id_token)
-            if claims.get("nonce") != nonce:
-                raise PermissionError("id_token nonce mismatch")
-            aud = claims.get("aud")
-            if aud is not None and self.client_id not in (aud if isinstance(aud, list) else [aud]):
-                raise PermissionError("id_token audience mismatch")
+            self.verify_id_token(id_token, nonce)
         elif self.require_nonce and "openid" in self.scope.split():
             # an OpenID provider must return an id_token carrying our nonce (plain OAuth providers
             # such as GitHub do not request the openid scope and have no nonce to check)
@@ -109,25 +193,23 @@ def github_provider(github_client_id, github_client_secret, github_redirect_uri=
 
 def google_provider(google_client_id, google_client_secret, google_redirect_uri=None, **_):
     return OIDCProvider("google", google_client_id, google_client_secret, google_redirect_uri or "",
-                        "https://accounts.google.com/o/oauth2/v2/auth", "https://oauth2.googleapis.com/token",
-                        "https://openidconnect.googleapis.com/v1/userinfo")
+                        issuer="https://accounts.google.com")
 
 
 def microsoft_provider(microsoft_client_id, microsoft_client_secret, microsoft_redirect_uri=None,
                        microsoft_tenant="common", **_):
-    base = f"https://login.microsoftonline.com/{microsoft_tenant}/oauth2/v2.0"
     return OIDCProvider("microsoft", microsoft_client_id, microsoft_client_secret, microsoft_redirect_uri or "",
-                        f"{base}/authorize", f"{base}/token", "https://graph.microsoft.com/oidc/userinfo")
+                        discovery_url=f"https://login.microsoftonline.com/{microsoft_tenant}/v2.0/"
+                                      ".well-known/openid-configuration")
 
 
 def datatracker_provider(datatracker_client_id, datatracker_client_secret, datatracker_redirect_uri=None,
                          datatracker_issuer="https://auth.ietf.org/api/openid", **_):
     """IETF Datatracker login through its OpenID Connect provider (the reference ships only a
     scaffold that raises NotImplementedError, datatracker_provider.py:14)."""
-    base = datatracker_issuer.rstrip("/")
     return OIDCProvider("datatracker", datatracker_client_id, datatracker_client_secret,
-                        datatracker_redirect_uri or "", f"{base}/authorize", f"{base}/token", f"{base}/userinfo",
-                        scope="openid profile email roles")
+                        datatracker_redirect_uri or "", scope="openid profile email roles",
+                        issuer=datatracker_issuer.rstrip("/"))
 
 
 class MockIdentityProvider(IdentityProvider):

@@ -24,7 +24,7 @@ from ..contracts.events import utc_now_iso
 from ..orchestration import (TopKRelevanceSelector, build_context, create_context_selector, format_citations,
                              prompt_template, substitute_prompt)
 from ..parsing import MessageParser, ThreadBuilder
-from ..retry import DocumentNotFoundError, retry_with_backoff
+from ..retry import DocumentNotFoundError, RetryExhaustedError, retry_with_backoff
 from ..storage.document_store import DocumentAlreadyExistsError
 from ..summarization import Summarizer
 from ..summarization import Thread as SumThread
@@ -61,6 +61,18 @@ class ParsingService(_CleanupMixin, BaseService):
         self.archives = archive_store
         self.parser = parser or MessageParser()
         self.threads = ThreadBuilder()
+        self._parsed: dict[str, int] = {}    # archive_id -> messages parsed by the current attempt
+
+    def _set_archive_status(self, archive_id: str, fields: dict) -> None:
+        """Archive status is bookkeeping: a store outage must not fail the parse, but is logged and
+        counted (a lost update leaves the archive 'processing' until requeue_incomplete)."""
+        try:
+            self.store.update_document("archives", archive_id, fields)
+        except Exception as e:  # noqa: BLE001 -- logged + counted, the parse result stands
+            self.log.warning("archive status update failed", archive_id=archive_id, status=fields.get("status"),
+                             error=repr(e))
+            self.metrics.increment("parsing_archive_status_update_failures_total",
+                                   tags={"status": str(fields.get("status"))})
 
     def subscriptions(self):
         return {"ArchiveIngested": self._on_archive, "SourceDeletionRequested": self._handle_source_deletion}
@@ -73,19 +85,15 @@ class ParsingService(_CleanupMixin, BaseService):
         if raw is None:
             raise DocumentNotFoundError(f"archive {archive_id} not in archive store yet")
         t = time.perf_counter()
-        try:
-            self.store.update_document("archives", archive_id, {"status": "processing", "lastAttemptTime": _now()})
-        except Exception:
-            pass
+        self._set_archive_status(archive_id, {"status": "processing", "lastAttemptTime": _now()})
         msgs, errs = self.parser.parse_mbox_bytes(raw, archive_id)
+        self._parsed[archive_id] = len(msgs)
         threads = self.threads.build_threads(msgs)
         self.store.insert_many("messages", msgs)
         self.store.insert_many("threads", threads)
-        try:
-            self.store.update_document("archives", archive_id, {"status": "completed", "message_count": len(msgs),
-                                                                "lastUpdated": _now()})
-        except Exception:
-            pass
+        self._set_archive_status(archive_id, {"status": "completed", "message_count": len(msgs),
+                                              "lastUpdated": _now()})
+        self._parsed.pop(archive_id, None)
         self.metrics.increment("parsing_messages_parsed_total", len(msgs))
         self.metrics.observe("parsing_duration_seconds", time.perf_counter() - t)
         # one JSONParsed per message (reference parsing/app/service.py:681-740): downstream
@@ -99,12 +107,13 @@ class ParsingService(_CleanupMixin, BaseService):
     def on_failure(self, event_type, event, error):
         if event_type == "ArchiveIngested":
             aid = event["data"]["archive_id"]
-            try:
-                self.store.update_document("archives", aid, {"status": "failed"})
-            except Exception:
-                pass
-            self.publish("ParsingFailed", archive_id=aid, error_message=str(error) or type(error).__name__,
-                         error_type=type(error).__name__, messages_parsed_before_failure=0, retry_count=0,
+            self._set_archive_status(aid, {"status": "failed", "lastUpdated": _now()})
+            ctx = getattr(error, "context", None)       # RetryExhaustedError carries the retry context
+            retries = max(0, int(getattr(ctx, "attempt_number", 1)) - 1) if ctx is not None else 0
+            cause = error.__cause__ if isinstance(error, RetryExhaustedError) and error.__cause__ else error
+            self.publish("ParsingFailed", archive_id=aid, error_message=str(cause) or type(cause).__name__,
+                         error_type=type(cause).__name__,
+                         messages_parsed_before_failure=self._parsed.pop(aid, 0), retry_count=retries,
                          failed_at=utc_now_iso())
 
     def requeue_incomplete(self):
@@ -346,13 +355,16 @@ class OrchestratorService(BaseService):
         if event_type == "EmbeddingsGenerated":
             try:
                 tids = self._resolve_threads(event["data"]["chunk_ids"])
-            except Exception:
+            except Exception as e:  # noqa: BLE001 -- the store failing too: logged below, nothing to name
+                self.log.warning("could not resolve the failed event's threads", error=repr(e))
                 tids = []
             if not tids:  # chunks never became visible: nothing to name (the event needs >= 1 thread)
                 self.log.error("orchestration failed before threads resolved", error=repr(error))
                 return
+            ctx = getattr(error, "context", None)
             self.publish("OrchestrationFailed", thread_ids=tids, error_type=type(error).__name__,
-                         error_message=str(error) or type(error).__name__, retry_count=0)
+                         error_message=str(error) or type(error).__name__,
+                         retry_count=max(0, int(getattr(ctx, "attempt_number", 1)) - 1) if ctx is not None else 0)
 
     def requeue_incomplete(self):
         n = 0

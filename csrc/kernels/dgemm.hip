@@ -40,16 +40,26 @@ namespace {
 typedef __attribute__((address_space(3))) void dg_lds_t;
 typedef unsigned int dg_u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int DG_LOADERS = 2;    // X-loader waves per workgroup
+// X-loader waves per workgroup: fill the workgroup up to 8 waves (2 per SIMD, 256 VGPRs each), at
+// least one
+template <int BN>
+constexpr int dg_loaders() { return BN / 16 >= 7 ? 1 : 8 - BN / 16 > 2 ? 2 : 8 - BN / 16; }
 enum { DG_PART = 0, DG_BF16 = 1, DG_SILU = 2 };
 
-template <int BM>
+template <int BM, int BN>
 struct DgShape {
+  static constexpr int NW = BN / 16;                  // compute waves
+  static constexpr int LOADERS = dg_loaders<BN>();
+  static constexpr int WAVES = NW + LOADERS;
   static constexpr int MT = BM / 16;                  // m-tiles per compute wave
-  static constexpr int D = BM == 256 ? 4 : 8;         // W register ring depth (stages)
+  // W register ring depth (64-deep stages); 9 waves (BN = 128) leave 168 VGPRs per lane
+  static constexpr int D = BM == 256 ? 4 : (WAVES > 8 ? 6 : 8);
   static constexpr int XSTAGE = BM * 128;             // X bytes per 64-deep stage
-  static constexpr int NSX = BM == 256 ? 4 : (BM == 128 ? 6 : 8);   // X ring slots (64-128 KB)
-  static constexpr int XP = BM / 8 / DG_LOADERS;      // 1-KB DMA pieces per loader wave per stage
+  static constexpr int XP = BM / 8 / LOADERS;         // 1-KB DMA pieces per loader wave per stage
+  // X ring slots (64-128 KB); a loader keeps NSX - 2 stages in flight at its wait, and vmcnt
+  // counts at most 63 of its pieces
+  static constexpr int NSX_BASE = BM == 256 ? 4 : (BM == 128 ? 6 : 8);
+  static constexpr int NSX = (NSX_BASE - 2 <= 63 / XP ? NSX_BASE : 2 + 63 / XP);
 };
 
 __device__ __forceinline__ f32x4_t dg_mfma(uint4 a, uint4 b, f32x4_t c) {
@@ -89,6 +99,14 @@ __device__ __forceinline__ void dg_wait_ahead(int ahead) {
 // so the loaders' next DMA into that slot cannot overtake them
 __device__ __forceinline__ void dg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// per-lane part of the offset in voff (one VGPR for the whole ring), the wave-uniform stage part in
+// soff (an SGPR)
+template <bool NT>
+__device__ __forceinline__ uint4 dg_ldw_buf(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  const dg_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, NT ? 2 : 0);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 template <bool NT>
 __device__ __forceinline__ uint4 dg_ldw(const uint16_t* p) {
   if constexpr (NT) {
@@ -101,12 +119,21 @@ __device__ __forceinline__ uint4 dg_ldw(const uint16_t* p) {
 
 // ABL: ablation builds for the timing probes only (scripts/bench_dgemm.py --ablate); 0 in production.
 //   1 = no X DMA, 2 = no ds_read / MFMA (W loads kept live), 4 = no K-order rotation.
-template <int BM, int BN, int EPI, bool NTW, int ABL = 0>
-__global__ void __launch_bounds__(64 * (BN / 16 + DG_LOADERS), 1)
+// PACKED: W in the fragment-packed layout of cfc_dgemm_pack for this BN: tile-major, then 32-deep
+// k group, then wave: Wp[N/BN][K/32][BN/16][64][8], so the 16 rows x 32 k of one MFMA B fragment
+// are 1 KB contiguous in lane order and a workgroup's whole W slice (BN rows x its K range) is ONE
+// contiguous span that its waves read front to back, 2 KB each per stage.  Measured
+// (scripts/probes_stream.py, probes_flat.py): row-major fragments (16 rows x 64 B per instruction,
+// 8 KB row stride) stream at 3.8-4.2 TB/s however deep the ring; contiguous 1-KB pieces at
+// 6.0 TB/s from the same 224-256 workgroups.  Packed loads are buffer loads (32-bit offsets into
+// the workgroup's span) so the cache policy can be set: NTW = nontemporal for these once-read
+// bytes (guide "nt-weights").
+template <int BM, int BN, int EPI, bool NTW, int ABL = 0, bool PACKED = true>
+__global__ void __launch_bounds__((64 * DgShape<BM, BN>::WAVES), 1)
     dgemm_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W, int M, int N, int K, int ntiles,
                  int split, float* __restrict__ part, uint16_t* __restrict__ out, int ldo) {
-  using S = DgShape<BM>;
-  constexpr int NW = BN / 16;                         // compute waves
+  using S = DgShape<BM, BN>;
+  constexpr int NW = S::NW;
   constexpr int D = S::D;
   __shared__ __attribute__((aligned(16))) char smem[S::NSX * S::XSTAGE];
   const int lane = threadIdx.x & 63;
@@ -127,7 +154,7 @@ __global__ void __launch_bounds__(64 * (BN / 16 + DG_LOADERS), 1)
   auto phys = [&](int s) { s += rot; return s >= nst ? s - nst : s; };
 
   if (w >= NW) {
-    // ---------------- X loader wave: rows 8 XP l .. 8 XP (l+1) - 1 of the X stage image
+    // ---------------- X loader wave, LDS-DMA: rows 8 XP l .. 8 XP (l+1) - 1 of the X stage image
     const int l = w - NW;
     const int prow = lane >> 3, pch = (lane & 7) ^ prow;   // row & 7 == prow for every piece
     const uint16_t* xsrc[S::XP];
@@ -158,14 +185,31 @@ __global__ void __launch_bounds__(64 * (BN / 16 + DG_LOADERS), 1)
   }
 
   // ---------------- compute wave w: W rows n0 + 16 w + (lane & 15)
-  const uint16_t* wp = W + (size_t)(n0 + 16 * w + (lane & 15)) * K + (size_t)kb * 64 + 8 * kq;
   uint4 ring[D][2];
+  // packed: the workgroup's span, tile n0 / BN over all of K (split slices are sub-ranges of it),
+  // as a buffer descriptor built from wave-uniform values (guide T20: no waterfall loops)
+  const uint16_t* span = W + (size_t)(n0 / BN) * ((size_t)BN * K);
+  const uint32_t span_lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)span);
+  const uint32_t span_hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)span >> 32));
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uintptr_t)span_hi << 32) | span_lo), (short)0, PACKED ? BN * K * 2 : 0, 0x00020000);
+  const int wvoff = lane * 16;                                                   // per-lane byte offset
+  const int wsoff = __builtin_amdgcn_readfirstlane(((kb * 2) * NW + w) * 1024);  // k group 2 kb, wave w
+  // row-major: this lane's row and k offset
+  const uint16_t* wp = W + (size_t)(n0 + 16 * w + (lane & 15)) * K + (size_t)kb * 64 + 8 * kq;
+  // stage s of this lane: the kk = 0 and kk = 1 halves of its B fragments
+  auto load_stage = [&](int s, uint4 (&dst)[2]) {
+    if constexpr (PACKED) {
+      const int so = __builtin_amdgcn_readfirstlane(wsoff + s * 2 * NW * 1024);
+      dst[0] = dg_ldw_buf<NTW>(wrs, wvoff, so);
+      dst[1] = dg_ldw_buf<NTW>(wrs, wvoff, so + NW * 1024);
+    } else {
+      dst[0] = dg_ldw<NTW>(wp + s * 64);
+      dst[1] = dg_ldw<NTW>(wp + s * 64 + 32);
+    }
+  };
 #pragma unroll
-  for (int p = 0; p < D; ++p) {
-    const int s = phys(min(p, nst - 1));
-    ring[p][0] = dg_ldw<NTW>(wp + s * 64);
-    ring[p][1] = dg_ldw<NTW>(wp + s * 64 + 32);
-  }
+  for (int p = 0; p < D; ++p) load_stage(phys(min(p, nst - 1)), ring[p]);
   f32x4_t acc[S::MT];
 #pragma unroll
   for (int i = 0; i < S::MT; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -197,9 +241,7 @@ __global__ void __launch_bounds__(64 * (BN / 16 + DG_LOADERS), 1)
     for (int u = 0; u < D; ++u) {
       dg_barrier();                 // X stage st+u is in LDS
       compute(ring[u]);
-      const int s = phys(min(st + u + D, nst - 1));   // unconditional: the tail re-reads the last stage
-      ring[u][0] = dg_ldw<NTW>(wp + s * 64);
-      ring[u][1] = dg_ldw<NTW>(wp + s * 64 + 32);
+      load_stage(phys(min(st + u + D, nst - 1)), ring[u]);   // unconditional: the tail re-reads the last stage
     }
   }
 #pragma unroll
@@ -242,35 +284,60 @@ __global__ void __launch_bounds__(64 * (BN / 16 + DG_LOADERS), 1)
   }
 }
 
-constexpr bool DG_NT = false;   // weight-stream cache policy (nontemporal: measured in bench_dgemm)
+constexpr bool DG_NT = true;    // nontemporal packed weight stream (bench_dgemm --ablate: ~10 % faster)
 
-template <int BM, int BN, bool NTW, int ABL>
+template <int BM, int BN, bool NTW, int ABL, bool PK>
 int dgemm_launch_bn(const void* x, const void* w, int M, int N, int K, int split, int epi, float* part, void* out,
                     int ldo, hipStream_t stream) {
   const int ntiles = N / BN;
   const dim3 grid(ntiles * split, (M + BM - 1) / BM);
-  const int threads = 64 * (BN / 16 + DG_LOADERS);
+  const int threads = 64 * DgShape<BM, BN>::WAVES;
 #define DG_ARGS (const uint16_t*)x, (const uint16_t*)w, M, N, K, ntiles, split, part, (uint16_t*)out, ldo
   switch (epi) {
-    case DG_PART: dgemm_kernel<BM, BN, DG_PART, NTW, ABL><<<grid, threads, 0, stream>>>(DG_ARGS); break;
-    case DG_BF16: dgemm_kernel<BM, BN, DG_BF16, NTW, ABL><<<grid, threads, 0, stream>>>(DG_ARGS); break;
-    case DG_SILU: dgemm_kernel<BM, BN, DG_SILU, NTW, ABL><<<grid, threads, 0, stream>>>(DG_ARGS); break;
+    case DG_PART: dgemm_kernel<BM, BN, DG_PART, NTW, ABL, PK><<<grid, threads, 0, stream>>>(DG_ARGS); break;
+    case DG_BF16: dgemm_kernel<BM, BN, DG_BF16, NTW, ABL, PK><<<grid, threads, 0, stream>>>(DG_ARGS); break;
+    case DG_SILU: dgemm_kernel<BM, BN, DG_SILU, NTW, ABL, PK><<<grid, threads, 0, stream>>>(DG_ARGS); break;
     default: return -3;
   }
 #undef DG_ARGS
   return 0;
 }
 
-template <int BM, bool NTW = DG_NT, int ABL = 0>
-int dgemm_launch(const void* x, const void* w, int M, int N, int K, int split, int epi, int bn, float* part,
-                 void* out, int ldo, hipStream_t stream) {
+template <int BM, bool NTW, int ABL, bool PK>
+int dgemm_launch_pk(const void* x, const void* w, int M, int N, int K, int split, int epi, int bn, float* part,
+                    void* out, int ldo, hipStream_t stream) {
   switch (bn) {
-    case 64: return dgemm_launch_bn<BM, 64, NTW, ABL>(x, w, M, N, K, split, epi, part, out, ldo, stream);
-    case 96: return dgemm_launch_bn<BM, 96, NTW, ABL>(x, w, M, N, K, split, epi, part, out, ldo, stream);
-    case 112: return dgemm_launch_bn<BM, 112, NTW, ABL>(x, w, M, N, K, split, epi, part, out, ldo, stream);
-    case 128: return dgemm_launch_bn<BM, 128, NTW, ABL>(x, w, M, N, K, split, epi, part, out, ldo, stream);
+    case 64: return dgemm_launch_bn<BM, 64, NTW, ABL, PK>(x, w, M, N, K, split, epi, part, out, ldo, stream);
+    case 96: return dgemm_launch_bn<BM, 96, NTW, ABL, PK>(x, w, M, N, K, split, epi, part, out, ldo, stream);
+    case 112: return dgemm_launch_bn<BM, 112, NTW, ABL, PK>(x, w, M, N, K, split, epi, part, out, ldo, stream);
+    case 128: return dgemm_launch_bn<BM, 128, NTW, ABL, PK>(x, w, M, N, K, split, epi, part, out, ldo, stream);
     default: return -5;
   }
+}
+
+// packed weights stream nontemporal (NTW); row-major ones keep the default policy
+template <int BM, int ABL = 0>
+int dgemm_launch(const void* x, const void* w, int M, int N, int K, int split, int epi, int bn, int packed,
+                 float* part, void* out, int ldo, hipStream_t stream) {
+  return packed ? dgemm_launch_pk<BM, DG_NT, ABL, true>(x, w, M, N, K, split, epi, bn, part, out, ldo, stream)
+                : dgemm_launch_pk<BM, false, ABL, false>(x, w, M, N, K, split, epi, bn, part, out, ldo, stream);
+}
+
+// Fragment-pack a row-major W[N][K] for workgroups of nw = BN/16 waves:
+// Wp[t][kg][w][l][j] = W[BN t + 16 w + (l & 15)][32 kg + 8 (l >> 4) + j].  One thread per 16-B piece.
+__global__ void dgemm_pack_kernel(const uint16_t* __restrict__ W, uint16_t* __restrict__ Wp, int N, int K, int nw) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t total = (size_t)N * K / 8;
+  if (i >= total) return;
+  const int l = (int)(i & 63);
+  const size_t frag = i >> 6;
+  const int kgs = K / 32;
+  const int w = (int)(frag % nw);
+  const size_t t2 = frag / nw;
+  const int kg = (int)(t2 % kgs), t = (int)(t2 / kgs);
+  const int row = 16 * (t * nw + w) + (l & 15);
+  const uint4 v = *reinterpret_cast<const uint4*>(W + (size_t)row * K + 32 * kg + 8 * (l >> 4));
+  reinterpret_cast<uint4*>(Wp)[i] = v;
 }
 
 int dgemm_check(int M, int N, int K, int split, int epi, int bn, const float* part, const void* out) {
@@ -290,36 +357,48 @@ CFC_API int cfc_dgemm_bm(int M) { return M <= 64 ? 64 : (M <= 128 ? 128 : 256); 
 // epi 0: fp32 split-K partials into part[split][M][N]; 1: bf16 into out (row stride ldo, split 1);
 // 2: SwiGLU over 8-row interleaved gate/up W -> bf16 [M, N/2] into out (split 1).
 // bn (W rows per workgroup) in {64, 96, 112, 128}, N % bn == 0, K % 64 == 0, 1 <= split <= K / 64.
-CFC_API int cfc_dgemm(const void* x, const void* w, int M, int N, int K, int split, int epi, int bn, float* part,
-                      void* out, int ldo, hipStream_t stream) {
+// packed: w is in the fragment-packed layout cfc_dgemm_pack wrote for this same bn (else row-major [N][K]).
+CFC_API int cfc_dgemm(const void* x, const void* w, int M, int N, int K, int split, int epi, int bn, int packed,
+                      float* part, void* out, int ldo, hipStream_t stream) {
   if (const int e = dgemm_check(M, N, K, split, epi, bn, part, out)) return e;
   int rc;
   switch (cfc_dgemm_bm(M)) {
-    case 64: rc = dgemm_launch<64>(x, w, M, N, K, split, epi, bn, part, out, ldo, stream); break;
-    case 128: rc = dgemm_launch<128>(x, w, M, N, K, split, epi, bn, part, out, ldo, stream); break;
-    default: rc = dgemm_launch<256>(x, w, M, N, K, split, epi, bn, part, out, ldo, stream); break;
+    case 64: rc = dgemm_launch<64>(x, w, M, N, K, split, epi, bn, packed, part, out, ldo, stream); break;
+    case 128: rc = dgemm_launch<128>(x, w, M, N, K, split, epi, bn, packed, part, out, ldo, stream); break;
+    default: rc = dgemm_launch<256>(x, w, M, N, K, split, epi, bn, packed, part, out, ldo, stream); break;
   }
   return rc ? rc : CFC_CHECK_LAUNCH();
 }
 
-// Timing probe only (scripts/bench_dgemm.py --ablate): split-K partial GEMM at BM = 128 with
-// ablation bits `abl` (1 no X DMA, 2 no MFMA, 4 no K rotation) and +8 = nontemporal W loads.
+// Row-major W[N][K] bf16 -> the fragment-packed layout for bn-row workgroups (same size; the
+// packed weight is only valid with that bn).  N % bn == 0, bn % 16 == 0, K % 64 == 0.
+CFC_API int cfc_dgemm_pack(const void* w, void* wp, int N, int K, int bn, hipStream_t stream) {
+  if (N <= 0 || K <= 0 || bn <= 0 || bn % 16 || N % bn || K % 64 || w == wp) return -1;
+  const size_t pieces = (size_t)N * K / 8;
+  dgemm_pack_kernel<<<(unsigned)((pieces + 255) / 256), 256, 0, stream>>>((const uint16_t*)w, (uint16_t*)wp, N, K,
+                                                                           bn / 16);
+  return CFC_CHECK_LAUNCH();
+}
+
+// Timing probe only (scripts/bench_dgemm.py --ablate): split-K partial GEMM at BM = 128 on a
+// packed weight, ablation bits `abl` (1 no X DMA, 2 no MFMA, 4 no K rotation); +8 = default
+// (not nontemporal) cache policy on the weight stream.
 CFC_API int cfc_dgemm_ablate(const void* x, const void* w, int M, int N, int K, int split, int bn, int abl,
                              float* part, hipStream_t stream) {
   if (M > 128 || (abl & ~15)) return -1;
   if (const int e = dgemm_check(M, N, K, split, DG_PART, bn, part, nullptr)) return e;
   int rc;
   switch (abl) {
-    case 0: rc = dgemm_launch<128, false, 0>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
-    case 1: rc = dgemm_launch<128, false, 1>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
-    case 2: rc = dgemm_launch<128, false, 2>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
-    case 3: rc = dgemm_launch<128, false, 3>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
-    case 8: rc = dgemm_launch<128, true, 0>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
-    case 9: rc = dgemm_launch<128, true, 1>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
-    case 10: rc = dgemm_launch<128, true, 2>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
-    case 11: rc = dgemm_launch<128, true, 3>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
-    case 4: rc = dgemm_launch<128, false, 4>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
-    case 7: rc = dgemm_launch<128, false, 7>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
+#define DG_ABL(A, NT) rc = dgemm_launch_pk<128, NT, A, true>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
+    case 0: DG_ABL(0, true)
+    case 1: DG_ABL(1, true)
+    case 2: DG_ABL(2, true)
+    case 3: DG_ABL(3, true)
+    case 4: DG_ABL(4, true)
+    case 7: DG_ABL(7, true)
+    case 8: DG_ABL(0, false)
+    case 11: DG_ABL(3, false)
+#undef DG_ABL
     default: return -3;
   }
   return rc ? rc : CFC_CHECK_LAUNCH();

@@ -53,3 +53,37 @@ extern "C" int stream_probe(const void* w, int N, int K, int rpi, int d, int rot
   SP_CASE(8, 8, 1) SP_CASE(8, 16, 1) SP_CASE(16, 16, 0) SP_CASE(16, 16, 1) SP_CASE(16, 32, 1) SP_CASE(16, 8, 1)
   return -2;
 }
+
+// Flat stream: the matrix read as one contiguous byte array.  Workgroup b of G owns a contiguous
+// span; its NWV waves interleave 1-KB pieces (wave w takes pieces w, w+NWV, ...) with F pieces in
+// flight per wave.  Upper bound for any weight-stream layout at a given grid and concurrency.
+template <int F>
+__global__ void __launch_bounds__(512) flat_kernel(const uint4* __restrict__ W, size_t n16, int nwv, float* out) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (w >= nwv) return;
+  const size_t pieces = n16 / 64;
+  const size_t per = (pieces + gridDim.x - 1) / gridDim.x;
+  const size_t p0 = blockIdx.x * per, p1 = min(pieces, p0 + per);
+  unsigned acc = 0;
+  size_t p = p0 + w;
+  uint4 r[F];
+  for (; p + (size_t)(F - 1) * nwv < p1; p += (size_t)F * nwv) {
+#pragma unroll
+    for (int i = 0; i < F; ++i) r[i] = W[(p + (size_t)i * nwv) * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < F; ++i) acc ^= r[i].x + r[i].y + r[i].z + r[i].w;
+  }
+  for (; p < p1; p += nwv) acc ^= W[p * 64 + lane].x;
+  if (acc == 0x12345678u) out[0] = 1.f;
+}
+
+extern "C" int flat_probe(const void* w, size_t bytes, int grid, int nwv, int f, float* out, hipStream_t st) {
+  const size_t n16 = bytes / 16;
+  switch (f) {
+    case 4: flat_kernel<4><<<grid, 64 * nwv, 0, st>>>((const uint4*)w, n16, nwv, out); break;
+    case 8: flat_kernel<8><<<grid, 64 * nwv, 0, st>>>((const uint4*)w, n16, nwv, out); break;
+    case 16: flat_kernel<16><<<grid, 64 * nwv, 0, st>>>((const uint4*)w, n16, nwv, out); break;
+    default: return -2;
+  }
+  return (int)hipGetLastError();
+}

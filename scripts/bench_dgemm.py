@@ -88,8 +88,12 @@ def main():
             for s in sorted({2, s_def}):
                 part = K.dgemm(x, w, "part", s, bn=bn_d).clone()
                 row[f"err_part_s{s}"] = rel_err(part.sum(0), ref)
+            wpk = K.pack_dgemm_weight(w, bn_d)
+            row["err_packed_bf16"] = rel_err(K.dgemm(x, wpk, "bf16"), ref)
+            row["err_packed_part"] = rel_err(K.dgemm(x, wpk, "part", max(2, s_def)).sum(0), ref)
             if name.startswith("gate_up"):
                 refs = R.silu_mul_interleaved(ref.bfloat16()).float()
+                row["err_packed_swiglu"] = rel_err(K.dgemm_swiglu(x, K.pack_dgemm_weight(w, swiglu=True)), refs)
                 row["err_swiglu"] = rel_err(K.dgemm_swiglu(x, w), refs)
                 row["err_swiglu_split"] = rel_err(K.dgemm_swiglu(x, w, split=2, bn=64), refs)
             if name.startswith(("o", "down")):
@@ -119,25 +123,38 @@ def main():
                             break
                         if tiles * s >= K.DGEMM_CUS // 3:
                             cfgs.add((bn, s))
+            packs = {}
+
+            def pcalls_for(bn):
+                if bn not in packs:
+                    packs.clear()
+                    torch.cuda.empty_cache()
+                    pk = [K.pack_dgemm_weight(ww, bn) for ww in ws]
+                    packs[bn] = [pk[i % len(pk)] for i in range(len(calls))]
+                return packs[bn]
             for bn, s in sorted(cfgs):
                 part = torch.empty(s, M, N, device="cuda", dtype=torch.float32)
-                if s == 1:
-                    fns = [lambda ww=ww, bn=bn: K.dgemm(x, ww, "bf16", bn=bn) for ww in calls]
-                else:
-                    fns = [lambda ww=ww, bn=bn, s=s, part=part: K.dgemm(x, ww, "part", s, bn=bn, part=part)
-                           for ww in calls]
-                row[f"dg_bn{bn}_s{s}_us"] = round(timed(fns), 1)
+                for tag, cl in (("dg", calls), ("pk", pcalls_for(bn))):
+                    if s == 1:
+                        fns = [lambda ww=ww, bn=bn: K.dgemm(x, ww, "bf16", bn=bn) for ww in cl]
+                    else:
+                        fns = [lambda ww=ww, bn=bn, s=s, part=part: K.dgemm(x, ww, "part", s, bn=bn, part=part)
+                               for ww in cl]
+                    row[f"{tag}_bn{bn}_s{s}_us"] = round(timed(fns), 1)
             if args.ablate and M <= 128:
                 part = torch.empty(s_def, M, N, device="cuda", dtype=torch.float32)
-                for abl in (1, 2, 3, 4, 7, 9, 11):
+                pcalls = pcalls_for(bn_d)
+                for abl in (1, 2, 3, 4, 7, 8, 11):
                     fns = [lambda ww=ww, a=abl: K.check(K.kernels().cfc_dgemm_ablate(
-                        x.data_ptr(), ww.data_ptr(), M, N, Kd, s_def, bn_d, a, part.data_ptr(), K._stream(x)),
-                        "ablate") for ww in calls]
-                    row[f"abl{abl}_us"] = round(timed(fns), 1)
+                        x.data_ptr(), ww.data.data_ptr(), M, N, Kd, s_def, bn_d, a, part.data_ptr(), K._stream(x)),
+                        "ablate") for ww in pcalls]
+                    row[f"pk_abl{abl}_us"] = round(timed(fns), 1)
             if name.startswith("gate_up"):
                 row["lib_silu_us"] = round(timed([lambda ww=ww: K.silu_mul(F.linear(x, ww), interleaved=True)
                                                   for ww in calls]), 1)
                 row["dg_swiglu_us"] = round(timed([lambda ww=ww: K.dgemm_swiglu(x, ww) for ww in calls]), 1)
+                fbn = K.dgemm_config(M, N, Kd, swiglu=True)[0]
+                row["pk_swiglu_us"] = round(timed([lambda ww=ww: K.dgemm_swiglu(x, ww) for ww in pcalls_for(fbn)]), 1)
             if name.startswith(("o", "down")):
                 res = torch.randn(M, N, device="cuda").bfloat16()
                 nw = torch.ones(N, device="cuda").bfloat16()
@@ -147,14 +164,18 @@ def main():
                     x, ww, sl, res, nw, 1e-5) for ww in calls]), 1)
                 row["dg_res_norm_us"] = round(timed([lambda ww=ww: K.dgemm_residual_rmsnorm(
                     x, ww, res, nw, 1e-5) for ww in calls]), 1)
+                row["pk_res_norm_us"] = round(timed([lambda ww=ww: K.dgemm_residual_rmsnorm(
+                    x, ww, res, nw, 1e-5) for ww in pcalls_for(bn_d)]), 1)
             if name.startswith("qkv"):
                 row["dg_linear_us"] = round(timed([lambda ww=ww: K.dgemm_linear(x, ww) for ww in calls]), 1)
-            best = min(v for k, v in row.items() if k.startswith("dg_bn"))
-            row["dg_best_TBs"] = round(wb / best / 1e6, 2)
+                row["pk_linear_us"] = round(timed([lambda ww=ww: K.dgemm_linear(x, ww) for ww in pcalls_for(bn_d)]), 1)
+            for tag in ("dg", "pk"):
+                best = min(v for k, v in row.items() if k.startswith(f"{tag}_bn"))
+                row[f"{tag}_best_TBs"] = round(wb / best / 1e6, 2)
             print(json.dumps(row), flush=True)
             fh.write(json.dumps(row) + "\n")
             fh.flush()
-            del ws, calls
+            del ws, calls, packs
             torch.cuda.empty_cache()
 
 

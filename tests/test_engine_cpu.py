@@ -189,3 +189,30 @@ def test_mha_incremental_decode_matches_full_recompute():
     gen = eng.generate([p], 4, ignore_eos=True).tokens[0]
     for t in range(1, 4):
         assert eng.generate([p + gen[:t]], 1, ignore_eos=True).tokens[0][0] == gen[t]
+
+
+def test_packed_decode_weights_round_trip():
+    """DecoderWeights.pack_decode: every projection's packed copy unpacks to the row-major weight
+    (CPU reference packer), tiled with the decode GEMM's choice for a 128-row batch."""
+    from copilot_for_consensus_amd.ops import kernels as K
+    cfg = get_config("tiny")
+    w = DecoderWeights.random(cfg, "cpu").pack_decode()
+    for layer, packed in zip(w.layers, w.packed):
+        for name, p in packed.items():
+            assert isinstance(p, K.PackedWeight) and p.shape == tuple(layer[name].shape)
+            assert torch.equal(K._rowmajor(p), layer[name]), name
+    assert w.packed_bytes() == sum(p.nbytes() for layer in w.packed for p in layer.values()) + \
+        w.packed_lm_head.nbytes()
+    x = torch.randn(3, cfg.hidden).bfloat16()
+    assert torch.equal(K.dgemm_linear(x, w.packed[0]["qkv"]), torch.nn.functional.linear(x, w.layers[0]["qkv"]))
+
+
+def test_pack_layout_fragment_order():
+    """Packed element [nb, kb, t, lane, j] = W[nb*bn + 16t + lane%16, 32kb + 8(lane//16) + j]."""
+    bn, N, Kd = 64, 128, 96
+    w = torch.arange(N * Kd, dtype=torch.float32).view(N, Kd)
+    p = R.pack_dgemm_weight(w, bn)
+    assert p.shape == (N // bn, Kd // 32, bn // 16, 64, 8)
+    for nb, kb, t, lane, j in [(0, 0, 0, 0, 0), (1, 2, 3, 63, 7), (0, 1, 2, 17, 5), (1, 0, 1, 40, 3)]:
+        assert p[nb, kb, t, lane, j] == w[nb * bn + 16 * t + lane % 16, 32 * kb + 8 * (lane // 16) + j]
+    assert torch.equal(R.unpack_dgemm_weight(p), w)

@@ -327,6 +327,60 @@ def test_dgemm_residual_rmsnorm(M, N, Kd, split):
     _close(o, ref_o, 5e-2)
 
 
+@pytest.mark.parametrize("bn", [64, 96, 112, 128])
+def test_dgemm_pack_matches_reference_layout(bn):
+    """The GPU pack kernel writes exactly the layout reference.pack_dgemm_weight describes."""
+    N, Kd = (1280 if bn == 128 else 1344), 320
+    w = torch.randn(N, Kd, device=DEV).bfloat16()
+    pw = K.pack_dgemm_weight(w, bn)
+    assert torch.equal(pw.data.cpu(), R.pack_dgemm_weight(w.cpu(), bn).reshape(-1))
+    assert torch.equal(K._rowmajor(pw).cpu(), w.cpu())
+
+
+@pytest.mark.parametrize("M,N,Kd,split,bn", [(128, 6144, 4096, None, 128), (5, 4096, 4096, 4, 64),
+                                            (77, 1024, 512, 2, 128), (200, 512, 1024, 1, 128),
+                                            (256, 768, 1024, 3, 96), (128, 28672, 512, 1, 112),
+                                            (300, 640, 256, 1, 64), (64, 448, 320, 5, 112)])
+def test_dgemm_packed_linear(M, N, Kd, split, bn):
+    """Fragment-packed weights (buffer-load stream) vs fp32 x @ w^T, every row tile and W width."""
+    x = torch.randn(M, Kd, device=DEV).bfloat16()
+    w = (torch.randn(N, Kd, device=DEV) * 0.02).bfloat16()
+    y = K.dgemm_linear(x, K.pack_dgemm_weight(w, bn), split=split)
+    _close(y, _ref_linear(x, w), 3e-2)
+
+
+def test_dgemm_packed_exact():
+    M, N, Kd = 128, 448, 512
+    x = torch.randint(-3, 4, (M, Kd), device=DEV).bfloat16()
+    w = torch.randint(-2, 3, (N, Kd), device=DEV).bfloat16()
+    w[:, :7] += torch.arange(N, device=DEV).bfloat16().unsqueeze(1) % 5
+    ref = (x.float() @ w.float().T)
+    for bn in K.DGEMM_BNS:
+        if N % bn == 0:
+            for split in (1, 3):
+                part = K.dgemm(x, K.pack_dgemm_weight(w, bn), "part", split)
+                assert torch.equal(part.sum(0), ref), (bn, split)
+
+
+@pytest.mark.parametrize("M,split", [(128, None), (5, None), (128, 2), (256, None)])
+def test_dgemm_packed_swiglu_and_norm(M, split):
+    F, Kd = 1024, 512
+    x = torch.randn(M, Kd, device=DEV).bfloat16()
+    gu = (torch.randn(2 * F, Kd, device=DEV) * 0.05).bfloat16()
+    ref = R.silu_mul(_ref_linear(x, gu).bfloat16())
+    pw = K.pack_dgemm_weight(R.interleave_gate_up(gu), swiglu=True, m=M)
+    _close(K.dgemm_swiglu(x, pw, split=split), ref, 3e-2)
+    w = (torch.randn(Kd, F, device=DEV) * 0.02).bfloat16()
+    a = torch.randn(M, F, device=DEV).bfloat16()
+    r = torch.randn(M, Kd, device=DEV).bfloat16()
+    nw = (1 + 0.1 * torch.randn(Kd, device=DEV)).bfloat16()
+    ref_o, ref_r = R.rmsnorm(_ref_linear(a, w).bfloat16(), nw.cpu(), 1e-5, r.cpu())
+    rr = r.clone()
+    o = K.dgemm_residual_rmsnorm(a, K.pack_dgemm_weight(w, m=M), rr, nw, 1e-5, split=split)
+    _close(rr, ref_r, 3e-2)
+    _close(o, ref_o, 5e-2)
+
+
 def test_dgemm_rejects_bad_shapes():
     x = torch.randn(8, 100, device=DEV).bfloat16()
     w = torch.randn(128, 100, device=DEV).bfloat16()

@@ -1,5 +1,6 @@
 """The MongoDB document-store driver (storage/document_store.py: MongoDocumentStore) against a
-stand-in pymongo (tests/fake_pymongo.py): pymongo is not in this image.
+stand-in pymongo client (tests/fake_pymongo.py): the image has the pymongo package but no MongoDB
+server, so the client API is faked in-process (wire-level parity with a live mongod stays unpinned).
 
 Checks the reference driver's contract (mongo_document_store.py:103-452): ping on connect, admin
 authSource by default, typed connection errors; ObjectId ids round-trip as strings (nested ids in
@@ -139,3 +140,18 @@ def test_services_pipeline_on_mongodb(server, tmp_path):
     assert len(db["summaries"].docs) == 2 and len(db["threads"].docs) == 2
     assert all(d.get("summary_id") for d in db["threads"].docs.values())
     assert create_document_store("mongodb").__class__ is MongoDocumentStore
+
+
+def test_real_bson_object_ids_round_trip():
+    """With the real pymongo package present, ids use bson.ObjectId: a 24-hex id is queried as an
+    ObjectId, anything else (the framework's 16-hex content ids) as the raw string, and nested
+    ObjectIds in results come back as strings."""
+    bson = pytest.importorskip("bson")
+    oid = bson.ObjectId()
+    s = MongoDocumentStore(host="127.0.0.1", port=27017, database="copilot")
+    q = s._oid_query(str(oid))
+    assert isinstance(q["_id"], bson.ObjectId) and q["_id"] == oid
+    assert s._oid_query("0123456789abcdef") == {"_id": "0123456789abcdef"}
+    doc = {"_id": oid, "thread": {"ids": [bson.ObjectId(), "x"]}}
+    out = MongoDocumentStore._stringify_ids(doc)
+    assert out["_id"] == str(oid) and isinstance(out["thread"]["ids"][0], str) and out["thread"]["ids"][1] == "x"

@@ -252,6 +252,64 @@ def test_oidc_exchange_checks_nonce_audience_and_subject():
         _FakeOIDC.make({"access_token": "at"}, {"email": "x@y"}, scope="read:user").exchange_code("c", "v", "n")
 
 
+def test_oidc_discovery_and_jwks_verified_id_token():
+    """Discovery fills the endpoints; the id_token is verified against the provider JWKS: signature,
+    iss, aud, exp and nonce; an unknown kid triggers one JWKS refresh (key rotation)."""
+    import time as _t
+
+    from copilot_for_consensus_amd.security.auth import OIDCProvider
+    k_old, k_new = J.RSAKey.generate(1024), J.RSAKey.generate(1024)
+    jwks = {"keys": [k_old.public_jwk("old")]}
+    fetched = []
+
+    def fetch(url):
+        fetched.append(url)
+        if url.endswith("/.well-known/openid-configuration"):
+            return {"issuer": "https://idp.example", "authorization_endpoint": "https://idp.example/auth",
+                    "token_endpoint": "https://idp.example/token", "userinfo_endpoint": "https://idp.example/me",
+                    "jwks_uri": "https://idp.example/jwks"}
+        return {"keys": list(jwks["keys"])}
+
+    def signed(key, kid, **claims):
+        base = {"iss": "https://idp.example", "aud": "client-1", "sub": "u", "nonce": "n1",
+                "exp": int(_t.time()) + 300}
+        base.update(claims)
+        return J.encode(base, J.RSASigner(key, key_id=kid))
+
+    token = {"access_token": "at"}
+    p = OIDCProvider("acme", "client-1", "secret", "https://app/cb", issuer="https://idp.example")
+    p._fetch_json = fetch
+    p._post = lambda url, data: dict(token)
+    p._get = lambda url, tok: {"sub": "u"}
+    assert p.authorization_url("s", "n1", "c").startswith("https://idp.example/auth?")
+    token["id_token"] = signed(k_old, "old")
+    assert p.exchange_code("c", "v", "n1")["sub"] == "acme:u"
+    for bad, why in ((signed(k_old, "old", iss="https://evil"), "issuer"),
+                     (signed(k_old, "old", aud="other"), "audience"),
+                     (signed(k_old, "old", exp=int(_t.time()) - 3600), "expired"),
+                     (signed(k_old, "old", nonce="n2"), "nonce")):
+        token["id_token"] = bad
+        with pytest.raises(PermissionError, match=why):
+            p.exchange_code("c", "v", "n1")
+    h, b, _ = signed(k_old, "old").split(".")
+    token["id_token"] = f"{h}.{b}.{J.b64u(k_new.sign(f'{h}.{b}'.encode()))}"   # signed by a key not in JWKS
+    with pytest.raises(PermissionError, match="signature"):
+        p.exchange_code("c", "v", "n1")
+    # rotation: the provider starts signing with "new"; the first miss refetches the JWKS
+    jwks["keys"].append(k_new.public_jwk("new"))
+    n_before = len(fetched)
+    token["id_token"] = signed(k_new, "new")
+    assert p.exchange_code("c", "v", "n1")["sub"] == "acme:u"
+    assert len(fetched) == n_before + 1
+    token["id_token"] = signed(k_new, "gone")
+    with pytest.raises(PermissionError, match="not in the provider JWKS"):
+        p.exchange_code("c", "v", "n1")
+    # HS256 (a symmetric alg an attacker could forge with a public key) is refused outright
+    token["id_token"] = J.encode({"iss": "https://idp.example", "aud": "client-1", "nonce": "n1"}, J.HMACSigner("x"))
+    with pytest.raises(PermissionError, match="algorithm"):
+        p.exchange_code("c", "v", "n1")
+
+
 def test_auth_service_require_nonce_flag_reaches_providers():
     p = _FakeOIDC.make({"access_token": "at"}, {"sub": "u"})
     store = InMemoryDocumentStore()

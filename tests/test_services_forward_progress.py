@@ -82,9 +82,40 @@ def test_parsing_missing_archive_retries_then_fails():
     store.insert_document("archives", {"_id": "0123456789abcdef", "status": "pending", "source": "wg"})
     sub.inject_event(_archive_event("0123456789abcdef"))
     failed = rec.get_events("ParsingFailed")
-    assert len(failed) == 1 and failed[0]["data"]["error_type"] == "RetryExhaustedError"
+    # the event names the root cause and how many retries ran (not the wrapper / zero)
+    assert len(failed) == 1 and failed[0]["data"]["error_type"] == "DocumentNotFoundError"
+    assert failed[0]["data"]["retry_count"] == FAST.max_attempts - 1
+    assert failed[0]["data"]["messages_parsed_before_failure"] == 0
     assert store.get_document("archives", "0123456789abcdef")["status"] == "failed"
     assert svc.get_stats()["events_failed"] == 1
+
+
+def test_parsing_failure_after_parse_reports_progress_and_logs_status_errors():
+    """A store that fails inserting messages: ParsingFailed carries the messages parsed before the
+    failure; a failing archive-status update is logged and counted, not silently dropped."""
+    from copilot_for_consensus_amd.observability import PrometheusMetricsCollector
+
+    class FlakyStore(InMemoryDocumentStore):
+        def insert_many(self, coll, docs):
+            raise ConnectionError("store down")
+
+        def update_document(self, coll, doc_id, fields):
+            if coll == "archives":
+                raise ConnectionError("store down")
+            return super().update_document(coll, doc_id, fields)
+
+    store, archives = FlakyStore(), InMemoryArchiveStore()
+    aid = _archive(store, archives)
+    pub, rec = _pub()
+    metrics = PrometheusMetricsCollector()
+    svc = ParsingService(pub, None, store, archives, retry_config=FAST, metrics=metrics)
+    sub = _wire(svc)
+    with pytest.raises(ConnectionError):      # not a transient error class: fails at once, re-raised
+        sub.inject_event(_archive_event(aid))
+    failed = rec.get_events("ParsingFailed")
+    assert len(failed) == 1 and failed[0]["data"]["error_type"] == "ConnectionError"
+    assert failed[0]["data"]["messages_parsed_before_failure"] > 0
+    assert metrics.get_counter("parsing_archive_status_update_failures_total", {"status": "processing"}) >= 1
 
 
 def test_parsing_startup_requeue_of_pending_archives():
