@@ -33,7 +33,7 @@ _KERNEL_SIGS = {
     "cfc_encoder_attention": [P, P, P, P, I, I, I, I, I, F, P, P],
     "cfc_rope_kv_write": [P, P, P, P, P, P, P, I, I, I, I, I, P],
     "cfc_v_cache_write_runs": [P, P, I, P, I, I, I, P],
-    "cfc_decode_advance_cb": [P, P, I, P, P, P, P, P, P, P, I, P, P, I, I, P],
+    "cfc_decode_advance_cb": [P, P, I, P, P, P, P, P, P, P, I, P, P, I, I] + [P] * 6 + [I] * 4 + [P] * 4,
     "cfc_rope_kv_write_fp8": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, P],
     "cfc_v_cache_write_runs_fp8": [P, P, I, P, I, I, I, F, P],
     "cfc_paged_decode_attention_fp8": [P, P, P, P, P, I, I, I, I, I, I, I, F, I, F, F, P, P, P, P],
@@ -46,7 +46,7 @@ _KERNEL_SIGS = {
     "cfc_embedding": [P, P, P, I, I, P],
     "cfc_sample": [P, I, I, F, c_uint32, P, P, P],
     "cfc_sample_truncated": [P, I, I, F, I, F, F, c_uint32, P, P, P],
-    "cfc_decode_advance": [P, P, I, P, P, P, P, P, P, I, P, P, I, I, P],
+    "cfc_decode_advance": [P, P, I, P, P, P, P, P, P, I, P, P, I, I] + [P] * 6 + [I] * 4 + [P] * 4,
     "cfc_knn_scores": [P, P, I, I, I, P, P, P, P],
     "cfc_topk_pass": [P, P, I, I, I, I, P, P, P],
     "cfc_topk_chunk_size": [],
@@ -54,6 +54,7 @@ _KERNEL_SIGS = {
     "cfc_pool": [P, P, P, P, I, I, I, I, P],
     "cfc_splitk_reduce": [P, I, I, I, I, P, I, P],
     "cfc_dgemm": [P, P, I, I, I, I, I, I, I, P, P, I, P],
+    "cfc_pgemm": [P, P, P, P, I, I, I, I, I, P],
     "cfc_dgemm_bm": [I],
     "cfc_dgemm_pack": [P, P, I, I, I, P],
     "cfc_dgemm_ablate": [P, P, I, I, I, I, I, I, P, P],

@@ -485,6 +485,49 @@ def dgemm_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, residual: torch.Ten
     return splitk_residual_rmsnorm(dgemm(x, w, "part", split, bn=bn), residual, norm_w, eps)
 
 
+# ------------------------------------------------------------------ prefill / encoder GEMM
+PGEMM_EPI = {"bf16": 0, "bias": 1, "bias_gelu": 2, "swiglu": 3}
+
+
+def pgemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Shapes the prefill GEMM (pgemm.hip) takes: bf16 contiguous, K % 64 == 0, N % 64 == 0, byte
+    spans < 4 GiB (32-bit DMA offsets)."""
+    return (x.is_cuda and x.dim() == 2 and w.dim() == 2 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and x.is_contiguous() and w.is_contiguous() and x.shape[1] == w.shape[1] and x.shape[1] % 64 == 0
+            and w.shape[0] % 64 == 0 and x.shape[0] >= 1 and x.numel() * 2 < 2 ** 32 and w.numel() * 2 < 2 ** 32)
+
+
+def pgemm(x: torch.Tensor, w: torch.Tensor, epi: str = "bf16", bias: torch.Tensor | None = None,
+          out: torch.Tensor | None = None) -> torch.Tensor:
+    """Hand-written MFMA GEMM for prefill / encoder shapes: x [M, K] @ w[N, K]^T with the following
+    elementwise op fused into the epilogue.  ``epi``: "bf16"; "bias" (+ bias[N]); "bias_gelu"
+    (gelu_erf(y + bias)); "swiglu" (8-row interleaved gate/up weights -> [M, N/2] =
+    silu(gate) * up with the unfused path's bf16 rounding of gate and up)."""
+    mode = PGEMM_EPI[epi]
+    if not x.is_cuda:
+        y = torch.nn.functional.linear(x.float(), w.float())
+        if mode in (1, 2):
+            y = y + bias.float()
+        if mode == 2:
+            y = torch.nn.functional.gelu(y)
+        if mode == 3:
+            return ref.silu_mul_interleaved(y.to(x.dtype))
+        return y.to(x.dtype)
+    if not pgemm_ok(x, w):
+        raise ValueError(f"pgemm: x {tuple(x.shape)} {x.dtype} w {tuple(w.shape)} {w.dtype}")
+    M, Kd = x.shape
+    N = w.shape[0]
+    if mode in (1, 2):
+        _req(bias, torch.bfloat16, "bias")
+        if bias.numel() != N:
+            raise ValueError(f"pgemm: bias of {bias.numel()} for N = {N}")
+    if out is None:
+        out = torch.empty(M, N // 2 if mode == 3 else N, dtype=torch.bfloat16, device=x.device)
+    check(kernels().cfc_pgemm(x.data_ptr(), w.data_ptr(), bias.data_ptr() if bias is not None else None,
+                              out.data_ptr(), M, N, Kd, mode, out.stride(0), _stream(x)), "cfc_pgemm")
+    return out
+
+
 GEMV_MAX_M = 4   # decode batches up to this size take the weight-streaming GEMV (gemm.hip: gemv_kernel)
 
 
@@ -905,10 +948,21 @@ def sample(logits, out_ids, temperature=0.0, seed=0, step=None):
     return out_ids
 
 
+def _stop_args(stop_state):
+    """ctypes tail of the decode-advance calls: the stop-string tables (runtime/stops.py) or nulls."""
+    if stop_state is None:
+        return [None] * 6 + [0, 0, 0, 0] + [None] * 3
+    a = stop_state.kernel_args()
+    return [a["head"].data_ptr(), a["tail"].data_ptr(), a["tlen"].data_ptr(), a["contains"].data_ptr(),
+            a["stops"].data_ptr(), a["stop_lens"].data_ptr(), a["n_str"], a["L"], a["H"], a["strip"],
+            a["win"].data_ptr(), a["wlen"].data_ptr(), a["keep"].data_ptr()]
+
+
 def decode_advance_cb(next_ids, tokens, gen, limit, input_ids, positions, ctx_lens, slots, block_tables, done,
-                      stop_ids):
+                      stop_ids, stop_state=None):
     """Continuous-batching bookkeeping after a decode step: per-slot token count / limit; finished
-    and empty slots (done = 1) are frozen (graph-capturable, no host sync)."""
+    and empty slots (done = 1) are frozen (graph-capturable, no host sync).  ``stop_state``
+    (runtime.stops.StopState): slots also finish when their text reaches a stop string."""
     B = next_ids.numel()
     cap = tokens.shape[1]
     if not next_ids.is_cuda:
@@ -923,6 +977,11 @@ def decode_advance_cb(next_ids, tokens, gen, limit, input_ids, positions, ctx_le
         fin = gen[idx] >= limit[idx]
         if stop_ids.numel():
             fin |= torch.isin(next_ids[idx], stop_ids)
+        if stop_state is not None:
+            for k, b in enumerate(idx.tolist()):
+                if stop_state.host_feed(b, int(next_ids[b])):
+                    fin[k] = True
+                    stop_state.keep[b] = int(gen[b])
         done[idx] = fin.to(done.dtype)
         go = idx[~fin]
         input_ids[go] = next_ids[go]
@@ -936,15 +995,23 @@ def decode_advance_cb(next_ids, tokens, gen, limit, input_ids, positions, ctx_le
                                           ctx_lens.data_ptr(), slots.data_ptr(), block_tables.data_ptr(),
                                           block_tables.shape[1], done.data_ptr(),
                                           _p(stop_ids) if stop_ids.numel() else None, stop_ids.numel(), B,
-                                          _stream(next_ids)), "cfc_decode_advance_cb")
+                                          *_stop_args(stop_state), _stream(next_ids)), "cfc_decode_advance_cb")
 
 
-def decode_advance(next_ids, tokens, step, input_ids, positions, ctx_lens, slots, block_tables, done, stop_ids):
-    """Device-side bookkeeping after each decode step (graph-capturable, no host sync)."""
+def decode_advance(next_ids, tokens, step, input_ids, positions, ctx_lens, slots, block_tables, done, stop_ids,
+                   stop_state=None):
+    """Device-side bookkeeping after each decode step (graph-capturable, no host sync).
+    ``stop_state``: a slot whose text reaches a stop string is marked done and keeps
+    ``stop_state.keep[b]`` tokens."""
     B = next_ids.numel()
     max_new = tokens.shape[1]
     if not next_ids.is_cuda:
         st = int(step[0])
+        if stop_state is not None:
+            for b in range(B):
+                if not int(done[b]) and stop_state.host_feed(b, int(next_ids[b])):
+                    done[b] = 1
+                    stop_state.keep[b] = st + 1
         if st < max_new:
             tokens[:, st] = next_ids
         input_ids.copy_(next_ids)
@@ -960,7 +1027,8 @@ def decode_advance(next_ids, tokens, step, input_ids, positions, ctx_lens, slots
                                        input_ids.data_ptr(), positions.data_ptr(), ctx_lens.data_ptr(),
                                        slots.data_ptr(), block_tables.data_ptr(), block_tables.shape[1],
                                        done.data_ptr(), _p(stop_ids) if stop_ids.numel() else None,
-                                       stop_ids.numel(), B, _stream(next_ids)), "cfc_decode_advance")
+                                       stop_ids.numel(), B, *_stop_args(stop_state), _stream(next_ids)),
+          "cfc_decode_advance")
 
 
 # ----------------------------------------------------------------------------- vector search

@@ -53,7 +53,8 @@ class Request:
 class ContinuousEngine:
     def __init__(self, engine, max_slots: int = 128, max_new_cap: int = 512, max_prompt: int = 4096,
                  steps_per_sync: int = 16, stop_ids: tuple[int, ...] = (), temperature: float = 0.0, seed: int = 0,
-                 max_admit_tokens: int | None = None, min_admit: int = 1, max_wait_s: float = 0.5):
+                 max_admit_tokens: int | None = None, min_admit: int = 1, max_wait_s: float = 0.5,
+                 stop_strings=None):
         self.engine = engine
         self.model = engine.model
         self.kv = engine.kv
@@ -86,6 +87,10 @@ class ContinuousEngine:
         self.next_ids = torch.zeros(B, **i32)
         self.step_t = torch.zeros(1, **i32)     # sampler RNG salt
         self.stop_t = torch.tensor(self.stop_ids, **i32)
+        # stop strings matched on the device (runtime/stops.py): a slot finishes at the token that
+        # completes one, so the slot is freed and refilled instead of decoding to its limit
+        self.stop_strings = stop_strings
+        self.stop_state = stop_strings.new_state(B, dev) if stop_strings is not None else None
         self.part_blocks = engine._part_blocks(B, self.max_blocks)
         P = -self.part_blocks
         ws = B * self.model.w.heads * P * (self.model.cfg.head_dim + 2) if P > 1 else 1
@@ -226,11 +231,16 @@ class ContinuousEngine:
         slots = [self.free.pop() for _ in take]
         bt = np.full((len(take), self.max_blocks), self.scratch, np.int32)
         rows = np.zeros((len(take), 6), np.int32)       # ids, positions, ctx, slot, limit, done
+        sstates = []
         for i, (r, s, tbl, f) in enumerate(zip(take, slots, tables, first)):
             bt[i, :len(tbl)] = tbl
             n = len(r.prompt)
+            hit = False
+            if self.stop_strings is not None:    # the prefill's token is every request's first
+                st0, hit = self.stop_strings.feed(self.stop_strings.initial(), int(f))
+                sstates.append(st0)
             rows[i] = (f, n, n + 1, tbl[n // KV_BLOCK] * KV_BLOCK + n % KV_BLOCK, r.max_new,
-                       int(r.max_new <= 1 or f in self.stop_ids))
+                       int(r.max_new <= 1 or f in self.stop_ids or hit))
             r.first_token_s = now
             self.slot_req[s] = r
             r.slot = s
@@ -241,6 +251,8 @@ class ContinuousEngine:
         for j, dst in enumerate((self.ids, self.positions, self.ctx_lens, self.slots, self.limit, self.done)):
             dst.index_copy_(0, idx, rows_t[:, j].contiguous())
         self.gen.index_fill_(0, idx, 1)
+        if self.stop_state is not None:
+            self.stop_state.set_slots(slots, sstates)
         self.tokens.index_copy_(0, idx, torch.nn.functional.pad(rows_t[:, :1], (0, self.cap - 1)))
         self.stats["admitted"] += len(take)
 
@@ -250,12 +262,13 @@ class ContinuousEngine:
         logits = self.model.logits(hidden)
         K.sample(logits, self.next_ids, self.sampling, self.seed, self.step_t)
         K.decode_advance_cb(self.next_ids, self.tokens, self.gen, self.limit, self.ids, self.positions,
-                            self.ctx_lens, self.slots, self.block_tables, self.done, self.stop_t)
+                            self.ctx_lens, self.slots, self.block_tables, self.done, self.stop_t, self.stop_state)
         self.step_t.add_(1)
 
     def _state(self):
+        extra = [self.stop_state.win, self.stop_state.wlen, self.stop_state.keep] if self.stop_state else []
         return [self.ids, self.positions, self.ctx_lens, self.slots, self.tokens, self.gen, self.done,
-                self.next_ids, self.step_t]
+                self.next_ids, self.step_t] + extra
 
     def _burst(self, n: int) -> None:
         if self.use_graph and self.graph is None:

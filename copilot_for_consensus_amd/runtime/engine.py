@@ -59,12 +59,14 @@ class _DecodeState:
         self.done = torch.zeros(B, **i32)
         self.next_ids = torch.zeros(B, **i32)
         self.stop_ids = torch.zeros(0, **i32)
+        self.stop_state = None     # runtime.stops.StopState when the request has stop strings
         self.workspace = torch.empty(max(1, n_part_ws), dtype=torch.float32, device=device)
         self.graph = None
 
     def tensors(self):
+        extra = [self.stop_state.win, self.stop_state.wlen, self.stop_state.keep] if self.stop_state else []
         return [self.ids, self.positions, self.ctx_lens, self.slots, self.block_tables, self.step, self.tokens,
-                self.done, self.next_ids]
+                self.done, self.next_ids] + extra
 
 
 class LLMEngine:
@@ -183,17 +185,20 @@ class LLMEngine:
         logits = self.model.logits(hidden)
         K.sample(logits, st.next_ids, temperature, seed, st.step)
         K.decode_advance(st.next_ids, st.tokens, st.step, st.ids, st.positions, st.ctx_lens, st.slots,
-                         st.block_tables, st.done, st.stop_ids)
+                         st.block_tables, st.done, st.stop_ids, st.stop_state)
 
-    def _state(self, B, max_blocks, max_new, part_blocks, stop_ids):
-        key = (B, max_blocks, max_new, tuple(stop_ids))
+    def _state(self, B, max_blocks, max_new, part_blocks, stop_ids, stop_strings=None):
+        key = (B, max_blocks, max_new, tuple(stop_ids), id(stop_strings) if stop_strings is not None else None)
         st = self._states.get(key)
         if st is None:
             P = -part_blocks if part_blocks < 0 else math.ceil(max_blocks / part_blocks)
             ws = B * self.model.w.heads * P * (self.cfg.head_dim + 2) if P > 1 else 1
             st = _DecodeState(B, max_blocks, max_new, self.device, ws)
-            # persistent: a captured graph holds this pointer
+            # persistent: a captured graph holds these pointers
             st.stop_ids = torch.tensor(list(stop_ids), dtype=torch.int32, device=self.device)
+            if stop_strings is not None:
+                st.stop_state = stop_strings.new_state(B, self.device)
+                st.stop_matcher = stop_strings      # keeps id(stop_strings) in the key valid
             self._states[key] = st
         return st
 
@@ -218,9 +223,12 @@ class LLMEngine:
     @torch.inference_mode()
     def generate(self, prompts: list[list[int]], max_new_tokens: int, temperature: float = 0.0, seed: int = 0,
                  stop_ids: tuple[int, ...] = (), ignore_eos: bool = False, top_k: int = 0, top_p: float = 1.0,
-                 min_p: float = 0.0) -> GenerationResult:
+                 min_p: float = 0.0, stop_strings=None) -> GenerationResult:
         """``temperature`` (or a :class:`ops.kernels.SamplingParams`) with optional top-k / top-p /
-        min-p truncation -- all applied on device inside the captured decode step."""
+        min-p truncation -- all applied on device inside the captured decode step.
+        ``stop_strings`` (runtime.stops.StopStringMatcher): a sequence finishes, on the device, at
+        the token whose text completes a stop string; its tokens end with that token (the caller
+        cuts the text at the stop, as llama.cpp's server does)."""
         if top_k or top_p < 1.0 or min_p > 0.0:
             temperature = K.SamplingParams(float(temperature), int(top_k), float(top_p), float(min_p))
         else:
@@ -268,7 +276,7 @@ class LLMEngine:
             t1 = time.perf_counter()
 
             part_blocks = self._part_blocks(B, max_blocks)
-            st = self._state(B, max_blocks, max_new_tokens, part_blocks, stop_ids)
+            st = self._state(B, max_blocks, max_new_tokens, part_blocks, stop_ids, stop_strings)
             st.block_tables.zero_()
             bt = torch.zeros(B, max_blocks, dtype=torch.int32)
             for b, t in enumerate(tables):
@@ -284,7 +292,18 @@ class LLMEngine:
             st.tokens.zero_()
             st.tokens[:, 0].copy_(f)
             st.step.fill_(1)
-            st.done.copy_(torch.isin(f, st.stop_ids.cpu()).to(torch.int32) if stop_ids else torch.zeros(B, dtype=torch.int32))
+            done0 = torch.isin(f, st.stop_ids.cpu()).to(torch.int32) if stop_ids else torch.zeros(B, dtype=torch.int32)
+            if stop_strings is not None:
+                # the prefill's token is the first of every sequence: fed on the host
+                states, keep = [], []
+                for b in range(B):
+                    s0, hit = stop_strings.feed(stop_strings.initial(), int(first[b]))
+                    states.append(s0)
+                    keep.append(1 if hit else st.stop_state.cap)
+                    if hit:
+                        done0[b] = 1
+                st.stop_state.set_slots(range(B), states, keep)
+            st.done.copy_(done0)
 
             steps = 0
             rng = span("llm.decode")
@@ -297,9 +316,11 @@ class LLMEngine:
                 else:
                     self._decode_step(st, part_blocks, temperature, seed)
                 steps += 1
-                if stop_ids and (i % self.stop_check_interval == 0) and bool(st.done.all()):
+                if (stop_ids or stop_strings is not None) and (i % self.stop_check_interval == 0) \
+                        and bool(st.done.all()):
                     break
             tokens = st.tokens.cpu()
+            keep = st.stop_state.keep.cpu().tolist() if stop_strings is not None else [steps + 1] * B
             if sync:
                 torch.cuda.synchronize(self.device)
             rng.__exit__(None, None, None)
@@ -310,7 +331,7 @@ class LLMEngine:
         out = []
         stop = set(stop_ids)
         for b in range(B):
-            row = tokens[b, :steps + 1].tolist()
+            row = tokens[b, :min(steps + 1, keep[b])].tolist()
             for j, t in enumerate(row):
                 if t in stop:
                     row = row[:j]

@@ -116,6 +116,19 @@ class BPETokenizer:
                 out.append(([self.bos_id] + ids) if add_bos else ids)
         return out
 
+    # decode() drops a leading space of the whole text (SentencePiece "▁" prefix)
+    strips_leading_space = True
+
+    def token_bytes(self, i: int) -> bytes:
+        """Bytes token ``i`` contributes to decode() output (byte tokens <0xNN>, "▁" -> space;
+        BOS / EOS contribute nothing) -- the stop-string matcher's view of the text."""
+        if i in (self.bos_id, self.eos_id) or not 0 <= i < len(self.vocab):
+            return b""
+        t = self.vocab[i]
+        if len(t) == 6 and t.startswith("<0x") and t.endswith(">"):
+            return bytes([int(t[3:5], 16)])
+        return t.replace("\u2581", " ").encode("utf-8")
+
     def decode(self, ids: list[int]) -> str:
         arr = np.asarray([i for i in ids if i not in (self.bos_id, self.eos_id)], dtype=np.int32)
         cap = max(64, 16 * len(arr))
@@ -300,6 +313,19 @@ class ByteLevelBPETokenizer:
 
     def encode_batch(self, texts: list[str], add_bos: bool = True, cap: int = 16384) -> list[list[int]]:
         return [self.encode(t, add_bos) for t in texts]
+
+    strips_leading_space = False
+
+    def token_bytes(self, i: int) -> bytes:
+        """Bytes token ``i`` contributes to decode() output (specials verbatim, BOS / EOS nothing)."""
+        if i in (self.bos_id, self.eos_id) or not 0 <= i < len(self.vocab):
+            return b""
+        inv = getattr(self, "_inv_special", None)
+        if inv is None:
+            inv = self._inv_special = {v: k for k, v in self.special.items()}
+        if i in inv:
+            return inv[i].encode("utf-8")
+        return bytes(self._u2b[c] for c in self.vocab[i] if c in self._u2b)
 
     def decode(self, ids: list[int]) -> str:
         skip = {i for i in (self.bos_id, self.eos_id) if i is not None}

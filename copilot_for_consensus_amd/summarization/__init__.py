@@ -127,6 +127,10 @@ class HipLLMSummarizer(Summarizer):
         if isinstance(stop_sequences, str):
             stop_sequences = json.loads(stop_sequences)
         self.stop_sequences = tuple(s for s in (stop_sequences or ()) if s)
+        # the stops are matched on the device as tokens arrive (runtime/stops.py): a thread stops
+        # decoding at "\n\n\n" even when it spans several tokens, not after max_new_tokens
+        from ..runtime.stops import StopStringMatcher
+        self.stop_matcher = StopStringMatcher.for_tokenizer(self.tokenizer, self.stop_sequences)
         self.max_batch = int(max_batch)
         self.ignore_eos = ignore_eos
         self.context_limit = cfg.max_positions - self.max_new_tokens
@@ -160,7 +164,8 @@ class HipLLMSummarizer(Summarizer):
             ids = token_ids[s:s + self.max_batch] if token_ids is not None else [self._tokens(t.prompt) for t in part]
             t0 = time.perf_counter()
             res = self.engine.generate(ids, self.max_new_tokens, temperature=self.sampling,
-                                       ignore_eos=self.ignore_eos)
+                                       ignore_eos=self.ignore_eos,
+                                       stop_strings=None if self.ignore_eos else self.stop_matcher)
             ms = int(1000 * (time.perf_counter() - t0))
             self.last_stats = self.gpu_stats(res)
             for t, p, g in zip(part, ids, res.tokens):

@@ -521,12 +521,66 @@ __global__ void __launch_bounds__(256) sample_topk_kernel(const uint16_t* __rest
 //   tokens[b][step] = next[b]; input_ids[b] = next[b]; positions[b]++; ctx_lens[b]++;
 //   slots[b] = block_tables[b][pos/32]*32 + pos%32; done[b] |= next[b] in stop_ids.
 // Thread 0 of block 0 also bumps the device step counter.
+// Stop strings on the device (runtime/stops.py builds the tables): per token id the first L bytes
+// it adds to the decoded text, its last H = L - 1 bytes, its byte length and whether a stop lies
+// entirely inside it; per slot the last H bytes generated so far (wlen -1 = nothing yet, so a
+// SentencePiece leading space is dropped as decode() does) and `keep` = tokens through the
+// stop-completing one.  n_str == 0: no stop strings (the pointers are null).
+struct StopTab {
+  const uint8_t* head;
+  const uint8_t* tail;
+  const int32_t* tlen;
+  const uint8_t* contains;
+  const uint8_t* stops;
+  const int32_t* stop_lens;
+  int n_str, L, H, strip;
+  uint8_t* win;
+  int32_t* wlen;
+  int32_t* keep;
+};
+
+// Feed token `tok` to slot b's window; true when a stop string now ends inside the token's bytes
+// (a stop within the token, or one straddling the window and the token's first bytes).
+__device__ bool stop_feed(const StopTab& t, int b, int tok) {
+  uint8_t* w = t.win + (size_t)b * t.H;
+  int wl = t.wlen[b];
+  const bool fresh = wl < 0;
+  if (fresh) wl = 0;
+  const uint8_t* hd = t.head + (size_t)tok * t.L;
+  int n = t.tlen[tok], off = 0;
+  if (fresh && t.strip && n > 0 && hd[0] == ' ') { off = 1; n -= 1; }
+  bool hit = t.contains[tok] != 0;
+  for (int s = 0; s < t.n_str && !hit; ++s) {
+    const uint8_t* sp = t.stops + (size_t)s * t.L;
+    const int ls = t.stop_lens[s];
+    for (int j = 1; j < ls && !hit; ++j) {   // j bytes from the window's end, ls - j from the token
+      if (j > wl || ls - j > n) continue;
+      bool ok = true;
+      for (int q = 0; q < j && ok; ++q) ok = w[wl - j + q] == sp[q];
+      for (int q = 0; q < ls - j && ok; ++q) ok = hd[off + q] == sp[j + q];
+      hit = ok;
+    }
+  }
+  if (n >= t.H) {
+    const uint8_t* tl = t.tail + (size_t)tok * t.H;
+    for (int q = 0; q < t.H; ++q) w[q] = tl[q];
+    wl = t.H;
+  } else if (n > 0) {
+    const int kb = min(wl, t.H - n);
+    for (int q = 0; q < kb; ++q) w[q] = w[wl - kb + q];
+    for (int q = 0; q < n; ++q) w[kb + q] = hd[off + q];
+    wl = kb + n;
+  }
+  t.wlen[b] = (fresh && n == 0) ? -1 : wl;
+  return hit;
+}
+
 __global__ void decode_advance_kernel(const int32_t* __restrict__ next, int32_t* __restrict__ tokens, int max_new,
                                       int32_t* __restrict__ step_ptr, int32_t* __restrict__ input_ids,
                                       int32_t* __restrict__ positions, int32_t* __restrict__ ctx_lens,
                                       int32_t* __restrict__ slots, const int32_t* __restrict__ block_tables,
                                       int max_blocks, int32_t* __restrict__ done, const int32_t* __restrict__ stop_ids,
-                                      int n_stop, int B) {
+                                      int n_stop, int B, StopTab st) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   const int step = *step_ptr;
   __syncthreads();
@@ -539,6 +593,10 @@ __global__ void decode_advance_kernel(const int32_t* __restrict__ next, int32_t*
     ctx_lens[b] = pos + 1;
     slots[b] = block_tables[(size_t)b * max_blocks + pos / KV_BS] * KV_BS + pos % KV_BS;
     int d = done[b];
+    if (st.n_str > 0 && !d && stop_feed(st, b, tok)) {
+      d = 1;
+      st.keep[b] = step + 1;   // tokens 0..step kept; the text is cut at the stop by the caller
+    }
     for (int i = 0; i < n_stop; ++i) d |= (tok == stop_ids[i]);
     done[b] = d;
   }
@@ -556,7 +614,7 @@ __global__ void decode_advance_cb_kernel(const int32_t* __restrict__ next, int32
                                          int32_t* __restrict__ ctx_lens, int32_t* __restrict__ slots,
                                          const int32_t* __restrict__ block_tables, int max_blocks,
                                          int32_t* __restrict__ done, const int32_t* __restrict__ stop_ids, int n_stop,
-                                         int B) {
+                                         int B, StopTab st) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B || done[b]) return;
   const int tok = next[b];
@@ -565,6 +623,10 @@ __global__ void decode_advance_cb_kernel(const int32_t* __restrict__ next, int32
   gen[b] = g + 1;
   int d = g + 1 >= limit[b];
   for (int i = 0; i < n_stop; ++i) d |= (tok == stop_ids[i]);
+  if (st.n_str > 0 && stop_feed(st, b, tok)) {
+    d = 1;
+    st.keep[b] = g + 1;
+  }
   done[b] = d;
   if (d) return;
   input_ids[b] = tok;
@@ -628,11 +690,18 @@ CFC_API int cfc_v_cache_write_runs_fp8(const void* qkv, const int32_t* runs, int
 CFC_API int cfc_decode_advance_cb(const int32_t* next, int32_t* tokens, int cap, int32_t* gen, const int32_t* limit,
                                   int32_t* input_ids, int32_t* positions, int32_t* ctx_lens, int32_t* slots,
                                   const int32_t* block_tables, int max_blocks, int32_t* done, const int32_t* stop_ids,
-                                  int n_stop, int B, hipStream_t stream) {
+                                  int n_stop, int B, const uint8_t* head, const uint8_t* tail, const int32_t* tlen,
+                                  const uint8_t* contains, const uint8_t* stops, const int32_t* stop_lens, int n_str,
+                                  int L, int H, int strip, uint8_t* win, int32_t* wlen, int32_t* keep,
+                                  hipStream_t stream) {
   if (B <= 0) return 0;
+  if (n_str > 0 && (L < 1 || H < 1 || L > 32 || !head || !tail || !tlen || !contains || !stops || !stop_lens ||
+                    !win || !wlen || !keep))
+    return -1;
+  const StopTab st{head, tail, tlen, contains, stops, stop_lens, n_str, L, H, strip, win, wlen, keep};
   decode_advance_cb_kernel<<<(B + 255) / 256, 256, 0, stream>>>(next, tokens, cap, gen, limit, input_ids, positions,
                                                                  ctx_lens, slots, block_tables, max_blocks, done,
-                                                                 stop_ids, n_stop, B);
+                                                                 stop_ids, n_stop, B, st);
   return CFC_CHECK_LAUNCH();
 }
 
@@ -694,11 +763,17 @@ CFC_API int cfc_sample(const void* logits, int B, int V, float temperature, uint
 CFC_API int cfc_decode_advance(const int32_t* next, int32_t* tokens, int max_new, int32_t* step_ptr, int32_t* input_ids,
                                int32_t* positions, int32_t* ctx_lens, int32_t* slots, const int32_t* block_tables,
                                int max_blocks, int32_t* done, const int32_t* stop_ids, int n_stop, int B,
-                               hipStream_t stream) {
+                               const uint8_t* head, const uint8_t* tail, const int32_t* tlen, const uint8_t* contains,
+                               const uint8_t* stops, const int32_t* stop_lens, int n_str, int L, int H, int strip,
+                               uint8_t* win, int32_t* wlen, int32_t* keep, hipStream_t stream) {
   if (B <= 0) return 0;
   if (B > 1024) return -1;  // single workgroup: the step counter bump must not race other blocks
+  if (n_str > 0 && (L < 1 || H < 1 || L > 32 || !head || !tail || !tlen || !contains || !stops || !stop_lens ||
+                    !win || !wlen || !keep))
+    return -1;
+  const StopTab st{head, tail, tlen, contains, stops, stop_lens, n_str, L, H, strip, win, wlen, keep};
   decode_advance_kernel<<<1, ((B + 63) / 64) * 64, 0, stream>>>(next, tokens, max_new, step_ptr, input_ids, positions,
                                                                ctx_lens, slots, block_tables, max_blocks, done,
-                                                               stop_ids, n_stop, B);
+                                                               stop_ids, n_stop, B, st);
   return CFC_CHECK_LAUNCH();
 }

@@ -1,0 +1,202 @@
+// Prefill / encoder GEMM for gfx950:  Y[M, N] = X[M, K] . W[N, K]^T  (bf16 in, fp32 accumulate),
+// with the elementwise op that follows each projection fused into the epilogue.
+//
+// Shapes: the decoder's prefill projections (M = prompt tokens of a batch, thousands to tens of
+// thousands; N, K = 4096 .. 28672) and the sentence encoders' (M = tokens of an embedding batch,
+// N, K = 384 .. 3072).  Compute bound: 256 x 256 output tile per workgroup, 128 FLOP per staged
+// byte, so each CU must keep ~55 GB/s of X and W arriving through L2 while its MFMAs run.
+//
+//   * workgroup = 8 waves (2 along M x 4 along N), 512 threads, one workgroup per CU (launch
+//     bound 1), each wave a 128 x 64 output block: 8 x 4 accumulator tiles of 16 x 16
+//     (v_mfma_f32_16x16x32_bf16, 128 accumulator VGPRs);
+//   * K in 64-deep tiles, both operands staged global -> LDS by LDS-DMA (`global_load_lds_dwordx4`,
+//     written in asm: hipcc orders nothing behind it and never drains it before an ordinary load),
+//     two LDS stages of 64 KB: the DMA of tile t+1 runs under the MFMAs of tile t, one barrier per
+//     tile (its counted wait retires tile t's DMA and the previous tile's ds_reads together);
+//   * each LDS image is 256 rows x 128 B, XOR-swizzled through the SOURCE address (chunk c of row r
+//     at r * 128 + ((c ^ (r & 7)) << 4)), so the 16-row ds_read_b128 fragment reads are
+//     bank-conflict free (guide rule 21 / T2) -- the same image as the decode GEMM's X stage;
+//   * operands swapped in the MFMA (W fragment as A, X fragment as B) so each lane's accumulator
+//     holds 4 CONSECUTIVE output columns of one row: the epilogue stores 8 bytes per lane straight
+//     from registers, and SwiGLU's gate/up pairs are one lane swap (__shfl_xor 32) away;
+//   * blockIdx -> tile: bijective XCD remap (guide T1), then groups of 8 M-tiles sweep the N-tiles,
+//     so the ~32 workgroups resident on one XCD share X rows and W rows in that XCD's L2.
+//
+// Epilogues: bf16; + bias (encoder qkv); + bias -> GELU(erf) (encoder FFN up); SwiGLU over 8-row
+// interleaved gate/up weights (decoder gate_up, reference.interleave_gate_up) -> [M, N/2].
+//
+// Bounds: K % 64 == 0, N % 64 == 0, ldo % 4 == 0; M and N need not be tile multiples (rows past
+// the edge read the last valid row, their results are never stored).  X, W byte spans < 4 GiB
+// (32-bit DMA offsets).
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) void pg_lds_t;
+
+enum { PG_BF16 = 0, PG_BIAS = 1, PG_BIAS_GELU = 2, PG_SWIGLU = 3 };
+
+constexpr int PG_BM = 256, PG_BN = 256, PG_BK = 64;
+constexpr int PG_STAGE = (PG_BM + PG_BN) * PG_BK * 2;   // 64 KB: A image then B image
+constexpr int PG_GROUP_M = 8;
+
+// One 1-KB LDS-DMA piece from sbase + voff (per lane): lane l's 16 bytes land at lds_addr + 16 l.
+// SGPR base + 32-bit VGPR offset (one VGPR per piece instead of a 64-bit pointer).  M0 is saved and
+// restored inside the statement (guide §5.7).
+__device__ __forceinline__ void pg_glds16(uint32_t voff, const void* sbase, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds_addr)
+      : "memory");
+}
+
+__device__ __forceinline__ float pg_gelu(float v) { return 0.5f * v * (1.f + erff(v * 0.70710678118654752f)); }
+
+__device__ __forceinline__ float pg_bfr(float v) { return bf2f(f2bf(v)); }
+
+template <int EPI>
+__global__ void __launch_bounds__(512, 1)
+    pgemm_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W, const uint16_t* __restrict__ bias,
+                 uint16_t* __restrict__ out, int M, int N, int K, int ldo, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * PG_STAGE];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 2, wc = w & 3;
+
+  // ---- tile of this workgroup: XCD-local id, then GROUP_M-row groups sweeping the N tiles
+  const int nwg = tiles_m * tiles_n;
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int per_group = PG_GROUP_M * tiles_n;
+  const int first_m = (id / per_group) * PG_GROUP_M;
+  const int gsz = min(tiles_m - first_m, PG_GROUP_M);
+  const int in_group = id % per_group;
+  const int m0 = (first_m + in_group % gsz) * PG_BM;
+  const int n0 = (in_group / gsz) * PG_BN;
+
+  // ---- DMA sources: piece p = 8 i + w (i = 0..3) covers image rows 8p .. 8p+7 of A and of B
+  const int prow = lane >> 3, pch = (lane & 7) ^ prow;   // image row & 7 == prow for every piece
+  uint32_t va[4], vb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 8 * (8 * i + w) + prow;
+    va[i] = ((uint32_t)min(m0 + r, M - 1) * (uint32_t)K + 8u * pch) * 2u;
+    vb[i] = ((uint32_t)min(n0 + r, N - 1) * (uint32_t)K + 8u * pch) * 2u;
+  }
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(pg_lds_t*)smem + w * 1024);
+  auto issue = [&](int t, int s) {
+    const uint16_t* xa = X + (size_t)t * PG_BK;
+    const uint16_t* wb = W + (size_t)t * PG_BK;
+    const uint32_t la = lds0 + s * PG_STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pg_glds16(va[i], xa, la + i * 8192);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pg_glds16(vb[i], wb, la + PG_BM * 128 + i * 8192);
+  };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // fragment reads: row (lane & 15) of a 16-row tile, 16-byte chunk 4 kk + (lane >> 4) of the
+  // 32-deep half kk, through the image swizzle (row & 7 == lane & 7)
+  const int frow = (lane & 15) * 128;
+  const int nk = K / PG_BK;
+  issue(0, 0);
+  for (int t = 0; t < nk; ++t) {
+    // tile t's DMA (the only one in flight) retired and the previous tile's ds_reads done, in
+    // every wave: after this barrier stage t & 1 is readable and stage (t + 1) & 1 writable
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (t + 1 < nk) issue(t + 1, (t + 1) & 1);
+    const char* sa = smem + (t & 1) * PG_STAGE + wr * 128 * 128 + frow;
+    const char* sb = smem + (t & 1) * PG_STAGE + PG_BM * 128 + wc * 64 * 128 + frow;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = ((4 * kk + (lane >> 4)) ^ (lane & 7)) << 4;
+      bf16x8_t af[8], bw[4];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(sa + i * 16 * 128 + ch);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bw[j] = *reinterpret_cast<const bf16x8_t*>(sb + j * 16 * 128 + ch);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: lane holds rows m = .. + (lane & 15), columns n = .. + 4 (lane >> 4) + 0..3
+  const int g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wr * 128 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int nb = n0 + wc * 64 + j * 16;   // n-tile base
+      const int n = nb + 4 * g;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if constexpr (EPI == PG_SWIGLU) {
+        // 16-row n-tile = 8 gate rows then 8 up rows: groups 0,1 hold gate cols 0..7, groups 2,3
+        // the matching up cols; bf16 rounding of g and u as the unfused GEMM -> silu_mul path
+        float u[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) u[e] = __shfl_xor(v[e], 32, 64);
+        if (g < 2 && m < M && nb < N) {
+          float y[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float gg = pg_bfr(v[e]);
+            y[e] = gg / (1.f + __expf(-gg)) * pg_bfr(u[e]);
+          }
+          *reinterpret_cast<uint2*>(out + (size_t)m * ldo + nb / 2 + 4 * g) =
+              make_uint2(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]));
+        }
+      } else {
+        if (m < M && n < N) {
+          if constexpr (EPI == PG_BIAS || EPI == PG_BIAS_GELU) {
+            const uint2 bb = *reinterpret_cast<const uint2*>(bias + n);
+            v[0] += __uint_as_float(bb.x << 16);
+            v[1] += __uint_as_float(bb.x & 0xffff0000u);
+            v[2] += __uint_as_float(bb.y << 16);
+            v[3] += __uint_as_float(bb.y & 0xffff0000u);
+          }
+          if constexpr (EPI == PG_BIAS_GELU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = pg_gelu(v[e]);
+          }
+          *reinterpret_cast<uint2*>(out + (size_t)m * ldo + n) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+        }
+      }
+    }
+  }
+}
+
+template <int EPI>
+int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int M, int N, int K, int ldo,
+                 hipStream_t stream) {
+  const int tm = (M + PG_BM - 1) / PG_BM, tn = (N + PG_BN - 1) / PG_BN;
+  pgemm_kernel<EPI><<<tm * tn, 512, 0, stream>>>((const uint16_t*)x, (const uint16_t*)w, (const uint16_t*)bias,
+                                                 (uint16_t*)out, M, N, K, ldo, tm, tn);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// epi: 0 bf16, 1 + bias, 2 + bias -> GELU, 3 SwiGLU (out [M, N/2]); ldo = output row stride.
+CFC_API int cfc_pgemm(const void* x, const void* w, const void* bias, void* out, int M, int N, int K, int epi,
+                      int ldo, hipStream_t stream) {
+  if (M < 1 || N < 64 || K < 64 || K % 64 || N % 64 || ldo % 4 || (epi != 3 && ldo < N) ||
+      (epi == 3 && ldo < N / 2) || (uint64_t)M * K * 2 >= (1ull << 32) || (uint64_t)N * K * 2 >= (1ull << 32) ||
+      ((epi == 1 || epi == 2) && bias == nullptr))
+    return (int)hipErrorInvalidValue;
+  switch (epi) {
+    case 0: return pgemm_launch<PG_BF16>(x, w, bias, out, M, N, K, ldo, stream);
+    case 1: return pgemm_launch<PG_BIAS>(x, w, bias, out, M, N, K, ldo, stream);
+    case 2: return pgemm_launch<PG_BIAS_GELU>(x, w, bias, out, M, N, K, ldo, stream);
+    case 3: return pgemm_launch<PG_SWIGLU>(x, w, bias, out, M, N, K, ldo, stream);
+    default: return (int)hipErrorInvalidValue;
+  }
+}

@@ -381,6 +381,41 @@ def test_dgemm_packed_swiglu_and_norm(M, split):
     _close(o, ref_o, 5e-2)
 
 
+@pytest.mark.parametrize("M,N,Kd,epi", [(512, 512, 256, "bf16"), (300, 1152, 384, "bias"), (257, 1536, 384, "bias_gelu"),
+                                       (1000, 768, 1536, "bf16"), (129, 2048, 512, "swiglu"), (64, 320, 128, "bf16"),
+                                       (2048, 4096, 1024, "bf16")])
+def test_pgemm(M, N, Kd, epi):
+    """Prefill / encoder GEMM with its fused epilogue vs the fp32 reference of the same op: edge
+    tiles in M and N (rows/cols past the edge never stored), bias, bias+GELU, SwiGLU."""
+    x = (torch.rand(M, Kd, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(N, Kd, device=DEV) * 2 - 1) / Kd ** 0.5).bfloat16()
+    b = (torch.rand(N, device=DEV) * 0.2 - 0.1).bfloat16()
+    ref = _ref_linear(x, w)
+    if epi in ("bias", "bias_gelu"):
+        ref = ref + b.float().cpu()
+    if epi == "bias_gelu":
+        ref = torch.nn.functional.gelu(ref)
+    if epi == "swiglu":
+        gu = R.deinterleave_gate_up(w.cpu())      # the same weights in [gate; up] order
+        ref = R.silu_mul(_ref_linear(x, gu.to(DEV)).bfloat16()).float()
+    out = torch.full((M, N // 2 if epi == "swiglu" else N), float("nan"), device=DEV).bfloat16()
+    y = K.pgemm(x, w, epi, bias=b, out=out)
+    _close(y, ref, 3e-2)
+
+
+def test_pgemm_exact_and_strided_out():
+    """Small-integer operands: bit-exact; output written into a wider buffer (ldo > N) leaves the
+    other columns untouched."""
+    M, N, Kd = 300, 320, 192
+    x = torch.randint(-3, 4, (M, Kd), device=DEV).bfloat16()
+    w = torch.randint(-2, 3, (N, Kd), device=DEV).bfloat16()
+    w[:, :5] += torch.arange(N, device=DEV).bfloat16().unsqueeze(1) % 7
+    buf = torch.zeros(M, N + 64, device=DEV).bfloat16()
+    K.pgemm(x, w, out=buf[:, :N])
+    assert torch.equal(buf[:, :N].float(), x.float() @ w.float().T)
+    assert torch.equal(buf[:, N:], torch.zeros_like(buf[:, N:]))
+
+
 def test_dgemm_rejects_bad_shapes():
     x = torch.randn(8, 100, device=DEV).bfloat16()
     w = torch.randn(128, 100, device=DEV).bfloat16()
