@@ -370,6 +370,18 @@ def load_config_json(path) -> DecoderConfig:
 DGEMM_MAX_ROWS = 256   # decode batches above this run the library GEMM (one 256-row tile per W pass)
 
 
+def argmax_keys(local: torch.Tensor, offset: int) -> torch.Tensor:
+    """Per row of a vocab shard's logits, (max logit, argmax) packed into ONE int64 whose signed
+    order is (logit, -global index): the high word an order-preserving image of the fp32 maximum,
+    the low word 0xffffffff - (offset + argmax).  The MAX over shards is then the global greedy
+    token (smallest index on exact ties), so TP greedy decode reduces B int64 instead of
+    all-gathering B x V logits."""
+    v, i = local.float().max(dim=1)
+    b = v.view(torch.int32).to(torch.int64)
+    ku = torch.where(b >= 0, b + 2 ** 31, 2 ** 31 - 1 - (b & 0x7FFFFFFF))
+    return ((ku - 2 ** 31) << 32) | (0xFFFFFFFF - (i.to(torch.int64) + offset))
+
+
 class DecoderModel:
     """Stateless forward functions over :class:`DecoderWeights` + a paged KV cache."""
 
@@ -650,8 +662,43 @@ class DecoderModel:
                 h = K.gemv_residual_rmsnorm(a, lw["down"], residual, nxt, eps)
         return h
 
+    def greedy_ids(self, hidden: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """Greedy next tokens into ``out`` [B] int32 without gathering the logits: each vocab
+        shard's argmax_keys, MAX-reduced over the TP group -- on the one-shot IPC kernel when it is
+        up (then a TP decode step holds no RCCL call and is captured whole), else one RCCL / gloo
+        all-reduce of B int64."""
+        local = self._local_logits(hidden)
+        if self.w.tp_size == 1:
+            return K.sample(local, out, 0.0)
+        keys = argmax_keys(local, self.w.tp_rank * self.w.vocab_shard)
+        ar = self.custom_ar
+        if ar is not None and ar.supports_keys(keys.numel()):
+            return ar.keymax(keys, out)
+        torch.distributed.all_reduce(keys, op=torch.distributed.ReduceOp.MAX, group=self.tp_group)
+        out.copy_((0xFFFFFFFF - (keys & 0xFFFFFFFF)).to(torch.int32))
+        return out
+
+    def graph_collectives_ok(self, B: int) -> bool:
+        """Every collective of a greedy decode step at batch B runs on the one-shot IPC kernels (so
+        the step can be captured even when the process group's backend cannot be, e.g. gloo)."""
+        ar = self.custom_ar
+        if self.w.tp_size == 1:
+            return True
+        n = B * self.cfg.hidden       # the o / down all-reduces: B x hidden bf16
+        return (ar is not None and ar.enabled and ar.supports_keys(B) and n % 8 == 0
+                and n * 2 <= ar.staging_bytes)
+
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """[B, V] logits (all-gathered over the vocab-parallel shards)."""
+        local = self._local_logits(hidden)
+        if self.w.tp_size == 1:
+            return local
+        parts = [torch.empty_like(local) for _ in range(self.w.tp_size)]
+        torch.distributed.all_gather(parts, local, group=self.tp_group)
+        return torch.cat(parts, -1)
+
+    def _local_logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        """This rank's vocab shard of the logits [B, V / tp]."""
         head = self.w.lm_head
         if (self.decode_qgemv and self.w.q_lm_head is not None and hidden.is_cuda
                 and hidden.shape[0] <= K.GEMV_MAX_M and hidden.is_contiguous() and self.w.q_lm_head.N % 4 == 0
@@ -669,8 +716,4 @@ class DecoderModel:
             local = K.dgemm_linear(hidden, ph if ph is not None else head)
         else:
             local = F.linear(hidden, self.w.lm_head)
-        if self.w.tp_size == 1:
-            return local
-        parts = [torch.empty_like(local) for _ in range(self.w.tp_size)]
-        torch.distributed.all_gather(parts, local, group=self.tp_group)
-        return torch.cat(parts, -1)
+        return local

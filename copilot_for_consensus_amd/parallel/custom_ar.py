@@ -49,7 +49,8 @@ class OneShotAllReduce:
             raise ValueError("one-shot all-reduce supports up to 8 ranks (one xGMI hop)")
         self.device = torch.device(device or "cuda")
         self.staging_bytes = int(staging_bytes)
-        self.blocks = min(int(blocks), lib.cfc_ar_max_blocks())
+        self.blocks = min(int(blocks), lib.cfc_ar_max_blocks() - 1)   # the last signal block: keymax
+        self.key_rows = lib.cfc_ar_key_rows()
         region = ctypes.c_int64()
         _check(lib.cfc_ar_region_bytes(self.staging_bytes, ctypes.byref(region)), "cfc_ar_region_bytes")
         self.region_bytes = region.value
@@ -104,6 +105,20 @@ class OneShotAllReduce:
                                           self.err.data_ptr(), torch.cuda.current_stream(x.device).cuda_stream)
         _check(rc, "cfc_oneshot_allreduce")
         return out
+
+    def supports_keys(self, n: int) -> bool:
+        return self.enabled and 0 < n <= self.key_rows
+
+    def keymax(self, keys: torch.Tensor, out_ids: torch.Tensor) -> torch.Tensor:
+        """out_ids[i] = 0xffffffff - low word of max over ranks of keys[i] (int64 keys, int32 out):
+        the TP greedy lm_head's (max logit, argmax) reduce (see models.decoder.argmax_keys)."""
+        if keys.dtype != torch.int64 or out_ids.dtype != torch.int32 or not keys.is_contiguous():
+            raise ValueError("keymax: int64 contiguous keys -> int32 ids")
+        rc = _lib().cfc_oneshot_keymax(keys.data_ptr(), out_ids.data_ptr(), keys.numel(), self._bases, self.world,
+                                       self.rank, self.staging_bytes, self.epochs.data_ptr(), self.err.data_ptr(),
+                                       torch.cuda.current_stream(keys.device).cuda_stream)
+        _check(rc, "cfc_oneshot_keymax")
+        return out_ids
 
     def errors(self) -> int:
         return int(self.err.item())

@@ -95,7 +95,7 @@ class ContinuousEngine:
         P = -self.part_blocks
         ws = B * self.model.w.heads * P * (self.model.cfg.head_dim + 2) if P > 1 else 1
         self.workspace = torch.empty(max(1, ws), dtype=torch.float32, device=dev)
-        self.use_graph = engine.use_graph
+        self.use_graph = engine._graph_for(B, self.sampling)
         self.graph = None
         self.queue: collections.deque[Request] = collections.deque()
         self.slot_req: list[Request | None] = [None] * B
@@ -259,8 +259,7 @@ class ContinuousEngine:
     def _decode_step(self) -> None:
         hidden = self.model.forward_decode(self.ids, self.positions, self.slots, self.ctx_lens, self.block_tables,
                                            self.kv, attn_workspace=self.workspace, part_blocks=self.part_blocks)
-        logits = self.model.logits(hidden)
-        K.sample(logits, self.next_ids, self.sampling, self.seed, self.step_t)
+        self.engine._next_tokens(hidden, self.next_ids, self.sampling, self.seed, self.step_t)
         K.decode_advance_cb(self.next_ids, self.tokens, self.gen, self.limit, self.ids, self.positions,
                             self.ctx_lens, self.slots, self.block_tables, self.done, self.stop_t, self.stop_state)
         self.step_t.add_(1)

@@ -79,11 +79,14 @@ class LLMEngine:
         self.max_prefill_tokens = max_prefill_tokens
         self.use_graph = use_graph and kv.device.type == "cuda"
         tp_group = getattr(model, "tp_group", None)
-        if self.use_graph and tp_group is not None:
+        # gloo collectives cannot be captured in a hipGraph (RCCL's can): with a gloo TP group a
+        # step is captured only when every collective in it runs on the one-shot IPC kernels
+        # (greedy decode: o/down all-reduces + the argmax key reduce; see _graph_for)
+        self._gloo_tp = False
+        if tp_group is not None and getattr(model.w, "tp_size", 1) > 1:
             import torch.distributed as dist
-            # gloo collectives cannot be captured in a hipGraph (RCCL's can): eager decode steps
-            if dist.get_backend(tp_group) == "gloo":
-                self.use_graph = False
+            self._gloo_tp = dist.get_backend(tp_group) == "gloo"
+        self.last_used_graph = False
         # query rows per prefill attention tile (the GQA-packed kernel takes 256 / G)
         self._prefill_rows = (K.prefill_rows(model.w.heads, model.w.kv_heads) if kv.device.type == "cuda"
                               else K.PREFILL_TILE_ROWS)
@@ -165,9 +168,8 @@ class LLMEngine:
                 d_ids, d_pos, d_slots, d_cu, d_ctx, d_bt.view(len(rows), maxb), self.kv, tiles=(d_tseq, d_tq0),
                 last_idx=d_last.long() if last_rows else None, v_runs=d_runs.view(-1, 4))
             if finishing:
-                logits = self.model.logits(hidden)
                 out = torch.empty(len(finishing), dtype=torch.int32, device=self.device)
-                K.sample(logits, out, temperature, seed, torch.zeros(1, dtype=torch.int32, device=self.device))
+                self._next_tokens(hidden, out, temperature, seed, torch.zeros(1, dtype=torch.int32, device=self.device))
                 first_dev.index_copy_(0, d_fin.long(), out)
         return first_dev.tolist()      # the one host sync of the prefill
 
@@ -179,11 +181,27 @@ class LLMEngine:
 
         return first
 
+    def _tp_greedy(self, temperature) -> bool:
+        return getattr(self.model.w, "tp_size", 1) > 1 and K.SamplingParams.of(temperature).temperature <= 0
+
+    def _graph_for(self, B, temperature) -> bool:
+        if not self.use_graph:
+            return False
+        if self._gloo_tp:
+            return self._tp_greedy(temperature) and self.model.graph_collectives_ok(B)
+        return True
+
+    def _next_tokens(self, hidden, out, temperature, seed, step):
+        """Sample the next token of every row; TP greedy reduces (max, argmax) keys instead of
+        all-gathering the logits (DecoderModel.greedy_ids)."""
+        if self._tp_greedy(temperature):
+            return self.model.greedy_ids(hidden, out)
+        return K.sample(self.model.logits(hidden), out, temperature, seed, step)
+
     def _decode_step(self, st: _DecodeState, part_blocks, temperature, seed):
         hidden = self.model.forward_decode(st.ids, st.positions, st.slots, st.ctx_lens, st.block_tables, self.kv,
                                            attn_workspace=st.workspace, part_blocks=part_blocks)
-        logits = self.model.logits(hidden)
-        K.sample(logits, st.next_ids, temperature, seed, st.step)
+        self._next_tokens(hidden, st.next_ids, temperature, seed, st.step)
         K.decode_advance(st.next_ids, st.tokens, st.step, st.ids, st.positions, st.ctx_lens, st.slots,
                          st.block_tables, st.done, st.stop_ids, st.stop_state)
 
@@ -308,10 +326,12 @@ class LLMEngine:
             steps = 0
             rng = span("llm.decode")
             rng.__enter__()
-            if self.use_graph and (st.graph is None or st.graph[1:] != (part_blocks, temperature, seed)):
+            use_graph = self._graph_for(B, temperature)
+            self.last_used_graph = use_graph
+            if use_graph and (st.graph is None or st.graph[1:] != (part_blocks, temperature, seed)):
                 self._capture(st, part_blocks, temperature, seed)
             for i in range(1, max_new_tokens):
-                if self.use_graph:
+                if use_graph:
                     st.graph[0].replay()
                 else:
                     self._decode_step(st, part_blocks, temperature, seed)

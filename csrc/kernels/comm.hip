@@ -5,6 +5,7 @@
 // remote loads are never served from a stale L2 line) and exported with hipIpcGetMemHandle:
 //
 //   [ signals: CFC_AR_MAX_BLOCKS x CFC_AR_MAX_RANKS int32 ][ staging parity 0 ][ staging parity 1 ]
+//   [ key area parity 0 ][ key area parity 1 ]
 //
 // Call k, block b (each block owns one contiguous slice of the tensor):
 //   1. copy its slice of the input into this rank's staging[k & 1];
@@ -15,7 +16,12 @@
 // Double-buffering by parity makes one barrier per call sufficient: a peer that reached call k+1
 // has finished kernel k (same stream), so nobody still reads staging[(k+2) & 1]'s previous use.
 // Epochs live in a per-rank device array (one counter per block), so the launch has fixed
-// arguments and is captured into the decode hipGraph like any other kernel.  Every spin is bounded:
+// arguments and is captured into the decode hipGraph like any other kernel.
+//
+// The same protocol also reduces per-row int64 keys with MAX (the TP greedy lm_head: each vocab
+// shard's (max logit, argmax) packed into one order-preserving key, so the decode graph needs no
+// logits all-gather): it owns the last signal block and its own double-buffered key area, so its
+// epochs never interleave with the sum's slices.  Every spin is bounded:
 // on timeout the block records an error and exits, so a missing peer fails the call instead of
 // hanging the GPU.
 #include "common.h"
@@ -24,6 +30,9 @@
 #define CFC_AR_MAX_BLOCKS 64
 #define CFC_AR_SIGNAL_BYTES (CFC_AR_MAX_BLOCKS * CFC_AR_MAX_RANKS * 4)
 #define CFC_AR_SPIN_LIMIT (1u << 22)   // ~1 us per uncached poll: a few seconds, then fail
+#define CFC_AR_SUM_BLOCKS (CFC_AR_MAX_BLOCKS - 1)   // the last signal block belongs to the key-max
+#define CFC_AR_KEY_ROWS 1024
+#define CFC_AR_KEY_BYTES (CFC_AR_KEY_ROWS * 8)
 
 struct ArPeers {
   char* base[CFC_AR_MAX_RANKS];  // each rank's shared region, mapped into this process
@@ -112,14 +121,72 @@ __global__ void __launch_bounds__(256) oneshot_allreduce_kernel(const uint16_t* 
   if (threadIdx.x == 0) epochs[b] = epoch;
 }
 
+// Max of int64 keys[n] over the ranks -> out_ids[i] = 0xffffffff - (low 32 bits of the max key).
+// One block of 256 threads; signal block CFC_AR_SUM_BLOCKS; key area after the two staging buffers.
+template <int NR>
+__global__ void __launch_bounds__(256) oneshot_keymax_kernel(const int64_t* __restrict__ keys,
+                                                             int32_t* __restrict__ out_ids, int n, ArPeers peers,
+                                                             int rank, int64_t staging_bytes,
+                                                             int* __restrict__ epochs, int* __restrict__ err) {
+  constexpr int b = CFC_AR_SUM_BLOCKS;
+  __shared__ int s_epoch, s_ok;
+  if (threadIdx.x == 0) {
+    s_epoch = epochs[b] + 1;
+    s_ok = 1;
+  }
+  __syncthreads();
+  const int epoch = s_epoch;
+  const int64_t area = CFC_AR_SIGNAL_BYTES + 2 * staging_bytes + (int64_t)(epoch & 1) * CFC_AR_KEY_BYTES;
+  int64_t* mine = reinterpret_cast<int64_t*>(peers.base[rank] + area);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) mine[i] = keys[i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x < NR) {
+    int* sig = reinterpret_cast<int*>(peers.base[threadIdx.x]) + b * CFC_AR_MAX_RANKS + rank;
+    store_signal(sig, epoch);
+  }
+  if (threadIdx.x < NR) {
+    const int* sig = reinterpret_cast<const int*>(peers.base[rank]) + b * CFC_AR_MAX_RANKS + threadIdx.x;
+    unsigned spins = 0;
+    while (load_signal(sig) < epoch) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > CFC_AR_SPIN_LIMIT) {
+        s_ok = 0;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __threadfence_system();
+  if (!s_ok) {
+    if (threadIdx.x == 0) {
+      atomicAdd(err, 1);
+      epochs[b] = epoch;
+    }
+    return;
+  }
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    int64_t best = reinterpret_cast<const int64_t*>(peers.base[0] + area)[i];
+#pragma unroll
+    for (int r = 1; r < NR; ++r) {
+      const int64_t k = reinterpret_cast<const int64_t*>(peers.base[r] + area)[i];
+      best = k > best ? k : best;
+    }
+    out_ids[i] = (int32_t)(0xffffffffu - (uint32_t)(best & 0xffffffff));
+  }
+  if (threadIdx.x == 0) epochs[b] = epoch;
+}
+
 }  // namespace
 
-// Shared region: signals + two staging buffers of `staging_bytes`, uncached, zeroed.
+// Shared region: signals + two staging buffers of `staging_bytes` + two key areas, uncached, zeroed.
 CFC_API int cfc_ar_region_bytes(int64_t staging_bytes, int64_t* out) {
   if (staging_bytes <= 0 || staging_bytes % 16) return -1;
-  *out = CFC_AR_SIGNAL_BYTES + 2 * staging_bytes;
+  *out = CFC_AR_SIGNAL_BYTES + 2 * staging_bytes + 2 * CFC_AR_KEY_BYTES;
   return 0;
 }
+
+CFC_API int cfc_ar_key_rows() { return CFC_AR_KEY_ROWS; }
 
 CFC_API int cfc_ar_alloc(int64_t bytes, void** ptr) {
   hipError_t e = hipExtMallocWithFlags(ptr, (size_t)bytes, hipDeviceMallocUncached);
@@ -143,6 +210,7 @@ CFC_API int cfc_ar_ipc_open(const void* handle, void** ptr) {
 
 CFC_API int cfc_ar_ipc_close(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
 
+// epochs arrays are CFC_AR_MAX_BLOCKS long; the sum uses at most CFC_AR_SUM_BLOCKS blocks
 CFC_API int cfc_ar_max_blocks() { return CFC_AR_MAX_BLOCKS; }
 
 // in/out: n bf16 (n % 8 == 0, 16-byte aligned, n * 2 <= staging_bytes); bases: `world` device
@@ -152,7 +220,7 @@ CFC_API int cfc_oneshot_allreduce(const void* in, void* out, int64_t n, const vo
                                   int rank, int64_t staging_bytes, int blocks, int* epochs, int* err,
                                   hipStream_t stream) {
   if (world < 1 || world > CFC_AR_MAX_RANKS || rank < 0 || rank >= world) return -1;
-  if (n <= 0 || n % 8 || n * 2 > staging_bytes || blocks < 1 || blocks > CFC_AR_MAX_BLOCKS) return -2;
+  if (n <= 0 || n % 8 || n * 2 > staging_bytes || blocks < 1 || blocks > CFC_AR_SUM_BLOCKS) return -2;
   if (((uintptr_t)in | (uintptr_t)out) & 15) return -3;
   ArPeers peers{};
   for (int r = 0; r < world; ++r) peers.base[r] = (char*)bases[r];
@@ -169,5 +237,25 @@ CFC_API int cfc_oneshot_allreduce(const void* in, void* out, int64_t n, const vo
     default: return -1;
   }
 #undef AR_CASE
+  return CFC_CHECK_LAUNCH();
+}
+
+// keys: n int64 (n <= CFC_AR_KEY_ROWS) per rank; out_ids: n int32 = 0xffffffff - low word of the
+// max key over the ranks.  Same region / epochs / err as cfc_oneshot_allreduce.
+CFC_API int cfc_oneshot_keymax(const int64_t* keys, int32_t* out_ids, int n, const void* const* bases, int world,
+                               int rank, int64_t staging_bytes, int* epochs, int* err, hipStream_t stream) {
+  if (world < 1 || world > CFC_AR_MAX_RANKS || rank < 0 || rank >= world) return -1;
+  if (n <= 0 || n > CFC_AR_KEY_ROWS) return -2;
+  ArPeers peers{};
+  for (int r = 0; r < world; ++r) peers.base[r] = (char*)bases[r];
+#define KM_CASE(NR) \
+  case NR: \
+    oneshot_keymax_kernel<NR><<<1, 256, 0, stream>>>(keys, out_ids, n, peers, rank, staging_bytes, epochs, err); \
+    break;
+  switch (world) {
+    KM_CASE(1) KM_CASE(2) KM_CASE(3) KM_CASE(4) KM_CASE(5) KM_CASE(6) KM_CASE(7) KM_CASE(8)
+    default: return -1;
+  }
+#undef KM_CASE
   return CFC_CHECK_LAUNCH();
 }

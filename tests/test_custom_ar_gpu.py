@@ -126,8 +126,13 @@ def _tp_worker(rank, world, port, q, prompts, n_new):
         ar = maybe_create(g.tp_group, env.device)
         m = DecoderModel(w, tp_group=g.tp_group, custom_ar=ar)
         kv = PagedKVCache(cfg.layers, 64, w.kv_heads, cfg.head_dim, env.device)
-        toks = LLMEngine(m, kv, use_graph=False).generate(prompts, n_new, ignore_eos=True).tokens
-        q.put((rank, {"tokens": toks, "custom_ar": ar is not None and ar.enabled,
+        eng = LLMEngine(m, kv, use_graph=True)
+        # greedy: every decode collective (o / down all-reduce, argmax key reduce) on the IPC
+        # kernels, so the step is captured whole although the group is gloo
+        toks = eng.generate(prompts, n_new, ignore_eos=True).tokens
+        graphed = eng.last_used_graph
+        eager = LLMEngine(m, kv, use_graph=False).generate(prompts, n_new, ignore_eos=True).tokens
+        q.put((rank, {"tokens": toks, "eager": eager, "graphed": graphed, "custom_ar": ar is not None and ar.enabled,
                       "errors": ar.errors() if ar is not None else -1}))
         import torch.distributed as dist
         dist.barrier()
@@ -140,8 +145,9 @@ def _tp_worker(rank, world, port, q, prompts, n_new):
 
 
 def test_tp2_decoder_with_oneshot_allreduce_matches_tp1():
-    """TP=2 (two processes sharing the GPU, decode all-reduces on the one-shot IPC kernel) generates
-    the same greedy tokens as the unsharded model."""
+    """TP=2 (two processes sharing the GPU, decode all-reduces and the greedy argmax key reduce on
+    the one-shot IPC kernels) runs its decode as a captured hipGraph and generates the same greedy
+    tokens as its eager steps and as the unsharded model."""
     import torch.multiprocessing as mp
     from copilot_for_consensus_amd.models.decoder import DecoderModel, DecoderWeights, get_config
     from copilot_for_consensus_amd.runtime.engine import LLMEngine
@@ -170,6 +176,8 @@ def test_tp2_decoder_with_oneshot_allreduce_matches_tp1():
     for r in range(2):
         assert "exception" not in res[r], res[r]
         assert res[r]["custom_ar"] and res[r]["errors"] == 0, res[r]
+        assert res[r]["graphed"], "TP=2 greedy decode should run as a captured graph"
+        assert res[r]["tokens"] == res[r]["eager"], (res[r]["tokens"], res[r]["eager"])
     assert res[0]["tokens"] == res[1]["tokens"]
     agree = sum(a == b for x, y in zip(res[0]["tokens"], ref) for a, b in zip(x, y))
     assert agree >= 0.9 * sum(len(x) for x in ref), (res[0]["tokens"], ref)

@@ -230,3 +230,20 @@ def test_heartbeat_thread_and_timeouts():
     hb.stop()
     env = configure_collective_timeouts(120)
     assert os.environ["TORCH_NCCL_ASYNC_ERROR_HANDLING"] == "1" and env["collective_timeout_s"] == 120
+
+
+def test_argmax_keys_reduce_equals_global_argmax():
+    """TP greedy: MAX over the shards' packed (logit, -index) keys is the unsharded argmax,
+    negative logits and exact ties (smallest index wins) included."""
+    from copilot_for_consensus_amd.models.decoder import argmax_keys
+    g = torch.Generator().manual_seed(0)
+    for V, tp in ((512, 2), (1000, 4), (96, 8)):
+        x = torch.randn(9, V, generator=g) * 5 - 3
+        x[0] = -7.5                       # all equal, all negative: index 0
+        x[1, V // 2] = x[1, V - 1] = 50.0  # tie across shards: the first one
+        x = x.bfloat16()
+        Vs = V // tp
+        keys = torch.stack([argmax_keys(x[:, r * Vs:(r + 1) * Vs], r * Vs) for r in range(tp)]).max(0).values
+        ids = (0xFFFFFFFF - (keys & 0xFFFFFFFF)).to(torch.int32)
+        want = torch.tensor([int(torch.nonzero(row == row.max())[0]) for row in x.float()], dtype=torch.int32)
+        assert torch.equal(ids, want), (ids, want)
