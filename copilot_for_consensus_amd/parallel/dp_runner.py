@@ -36,15 +36,22 @@ from .resilience import Heartbeat, Watchdog, WorkLedger, _get
 class ResilientDPRunner:
     def __init__(self, store, rank: int, world: int, process_batch: Callable[[list[str]], dict[str, Any]],
                  batch_size: int = 128, heartbeat_interval: float = 2.0, timeout: float = 30.0,
-                 stall_timeout: float | None = None, poll: float = 0.2, job: str = "job"):
+                 stall_timeout: float | None = None, poll: float = 0.2, job: str = "job",
+                 heartbeat: Heartbeat | None = None, liveness_prefix: str | None = None):
+        """``heartbeat`` / ``liveness_prefix``: a long-lived worker (the DP summarization service,
+        parallel/dp_service.py) beats under one namespace across all its jobs, so a worker that died
+        between jobs is already known dead when the next job starts (no per-job rendezvous wait on
+        it); by default liveness is per job."""
         self.store, self.rank, self.world = store, rank, world
         self.process_batch = process_batch
         self.batch_size = max(1, int(batch_size))
         self.poll = poll
         self.job = job
         self.ledger = WorkLedger(_Prefixed(store, f"{job}/"))
-        self.hb = Heartbeat(_Prefixed(store, f"{job}/"), rank, interval=heartbeat_interval)
-        self.watchdog = Watchdog(_Prefixed(store, f"{job}/"), world, timeout=timeout, stall_timeout=stall_timeout)
+        live_ns = _Prefixed(store, liveness_prefix if liveness_prefix is not None else f"{job}/")
+        self.hb = heartbeat or Heartbeat(live_ns, rank, interval=heartbeat_interval)
+        self._own_hb = heartbeat is None
+        self.watchdog = Watchdog(live_ns, world, timeout=timeout, stall_timeout=stall_timeout)
         self.stats = {"batches": 0, "items": 0, "reclaimed": {}}
 
     # ---------------------------------------------------------------- setup
@@ -54,7 +61,10 @@ class ResilientDPRunner:
         # early finisher; wait (bounded) for every rank's first heartbeat before the loop starts
         self.store.add(f"{self.job}/arrived", 1)
         deadline = time.monotonic() + wait_s
-        while int(self.store.add(f"{self.job}/arrived", 0)) < self.world and time.monotonic() < deadline:
+        while time.monotonic() < deadline:
+            arrived = int(self.store.add(f"{self.job}/arrived", 0))
+            if arrived >= self.world or (not self._own_hb and arrived >= self.world - len(self.watchdog.dead_ranks())):
+                break
             time.sleep(self.poll)
         if int(self.store.add(f"{self.job}/init_ticket", 1)) == 1:
             ids = list(items)
@@ -93,7 +103,8 @@ class ResilientDPRunner:
     # ---------------------------------------------------------------- loop
     def run(self, items: dict[str, float], wait_s: float = 120.0, max_seconds: float | None = None) -> dict[str, Any]:
         """``items``: id -> cost (e.g. prompt tokens).  Returns this rank's results (id -> value)."""
-        self.hb.start()
+        if self._own_hb:
+            self.hb.start()
         results: dict[str, Any] = {}
         t0 = time.monotonic()
         try:
@@ -115,7 +126,8 @@ class ResilientDPRunner:
                 self._maybe_reclaim()
                 time.sleep(self.poll)
         finally:
-            self.hb.stop()
+            if self._own_hb:
+                self.hb.stop()
 
 
 class _Prefixed:

@@ -10,6 +10,15 @@ infrastructure a one-process-per-service deployment needs.
     python -m copilot_for_consensus_amd.services.main embedserver  # HIP encoder behind OpenAI / Ollama / TEI embeddings
 
 Reference entry points: <service>/main.py (e.g. ingestion/main.py:179, parsing/main.py:101-124).
+
+Multi-GPU: launched by torchrun (WORLD_SIZE > 1), ``node`` and ``summarization`` run one process
+per GPU -- CFC_TP consecutive ranks form one tensor-parallel model, the TP-group leaders are data-
+parallel summarization workers (ORCHESTRATOR_DP / CFC_DP, if set, must equal WORLD_SIZE / CFC_TP).
+Global rank 0 runs the service(s) and shards every summarization batch over the workers through
+the job's TCPStore (parallel/dp_service.py: LPT assignment, heartbeats, takeover of a dead
+worker's threads); the other ranks only run models:
+
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m copilot_for_consensus_amd.services.main node
 """
 from __future__ import annotations
 
@@ -67,9 +76,14 @@ def main(argv=None) -> int:
 
     from .base import create_app, run_service
     from .node import Node
+    dist_ctx = None
+    if args.service in ("node", "summarization"):
+        dist_ctx = _distributed()
+        if dist_ctx is not None and not dist_ctx["serve"]:
+            return _model_rank(dist_ctx)
     try:
         only = None if args.service == "node" else [args.service]
-        node = Node(services=only)
+        node = Node(services=only, summarizer=dist_ctx["summarizer"] if dist_ctx else None)
         node.connect(only)
     except Exception as e:  # noqa: BLE001 -- fail fast: a service that cannot reach its bus/store exits 1
         print(f"[{args.service}] start-up failed: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
@@ -77,8 +91,11 @@ def main(argv=None) -> int:
     if args.service == "node":
         import uvicorn
         node.start(threaded=True)
-        uvicorn.run(node.http_app(), host="0.0.0.0", port=args.port or 8080)
-        node.stop()
+        try:
+            uvicorn.run(node.http_app(), host="0.0.0.0", port=args.port or 8080)
+        finally:
+            node.stop()
+            _close_distributed(dist_ctx)
         return 0
     svc = node.services[args.service]
     cfg = node.cfgs[args.service]
@@ -98,7 +115,64 @@ def main(argv=None) -> int:
     finally:
         if getattr(svc, "scheduler", None) is not None:
             svc.scheduler.stop()
+        _close_distributed(dist_ctx)
     return 0
+
+
+def _distributed() -> dict | None:
+    """torchrun env -> process groups, this rank's model and its role (see the module doc)."""
+    import os
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return None
+    import torch.distributed as dist
+
+    from ..parallel import init_distributed, make_groups
+    from ..parallel.dp_service import DPSummarizer, TPBroadcast
+    from ..summarization import create_llm_backend
+    env = init_distributed()
+    scfg = get_config("summarization")
+    llm = scfg.llm_backend
+    tp = int((llm.driver_config or {}).get("tensor_parallel") or 1) if llm.driver_name == "hip" else 1
+    groups = make_groups(env, tp)
+    want_dp = int(get_config("orchestrator").data_parallel or 1)
+    if want_dp > 1 and want_dp != groups.dp_size:
+        raise SystemExit(f"ORCHESTRATOR_DP={want_dp} but WORLD_SIZE / CFC_TP = {groups.dp_size}")
+    over = dict(tensor_parallel=tp, tp_group=groups.tp_group, tp_rank=groups.tp_rank,
+                device=str(env.device)) if llm.driver_name == "hip" else {}
+    local = create_llm_backend(llm, **over)
+    tp_bcast = None
+    if tp > 1 and groups.tp_rank == 0:
+        tp_bcast = local.tp_hook = TPBroadcast(groups)
+    store = dist.distributed_c10d._get_default_store()
+    serve = env.rank == 0
+    summarizer = DPSummarizer(store, groups.dp_size, local) if serve and groups.dp_size > 1 else local
+    return {"env": env, "groups": groups, "store": store, "local": local, "summarizer": summarizer,
+            "serve": serve, "tp_bcast": tp_bcast}
+
+
+def _model_rank(ctx: dict) -> int:
+    """A rank that only runs models: TP follower, or DP worker (TP-group leader) until shutdown."""
+    from ..parallel.dp_service import dp_worker_loop, tp_follow
+    g = ctx["groups"]
+    if g.tp_rank != 0:
+        n = tp_follow(ctx["local"], g)
+        print(f"[rank {ctx['env'].rank}] TP follower done after {n} batches", flush=True)
+        return 0
+    jobs = dp_worker_loop(ctx["store"], g.dp_rank, g.dp_size, ctx["local"])
+    if ctx["tp_bcast"] is not None:
+        ctx["tp_bcast"].stop()
+    print(f"[rank {ctx['env'].rank}] DP worker done after {jobs} jobs", flush=True)
+    return 0
+
+
+def _close_distributed(ctx: dict | None) -> None:
+    if not ctx:
+        return
+    close = getattr(ctx["summarizer"], "close", None)
+    if callable(close) and ctx["summarizer"] is not ctx["local"]:
+        close()               # DP workers exit their loops
+    if ctx["tp_bcast"] is not None:
+        ctx["tp_bcast"].stop()
 
 
 def _infra(args) -> int:

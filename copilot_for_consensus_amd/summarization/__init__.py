@@ -163,15 +163,23 @@ class HipLLMSummarizer(Summarizer):
             part = threads[s:s + self.max_batch]
             ids = token_ids[s:s + self.max_batch] if token_ids is not None else [self._tokens(t.prompt) for t in part]
             t0 = time.perf_counter()
-            res = self.engine.generate(ids, self.max_new_tokens, temperature=self.sampling,
-                                       ignore_eos=self.ignore_eos,
-                                       stop_strings=None if self.ignore_eos else self.stop_matcher)
+            res = self.generate_ids(ids)
             ms = int(1000 * (time.perf_counter() - t0))
             self.last_stats = self.gpu_stats(res)
             for t, p, g in zip(part, ids, res.tokens):
                 text = self.apply_stops(self.tokenizer.decode(g)).strip() or "(empty summary)"
                 out.append(Summary(t.thread_id, text, [], self.backend, self.model, len(p), len(g), ms))
         return out
+
+    # TP leader: called with each batch's token ids before generating, so the followers
+    # (parallel/dp_service.tp_follow) step the same engine call in lockstep
+    tp_hook = None
+
+    def generate_ids(self, ids: list[list[int]]):
+        if self.tp_hook is not None:
+            self.tp_hook(ids)
+        return self.engine.generate(ids, self.max_new_tokens, temperature=self.sampling, ignore_eos=self.ignore_eos,
+                                    stop_strings=None if self.ignore_eos else self.stop_matcher)
 
     def apply_stops(self, text: str) -> str:
         """Cut at the first stop sequence (string-level stops, as the llama.cpp server applies them)."""

@@ -1,0 +1,159 @@
+"""Data-parallel summarization in the services (parallel/dp_service.py, services/main.py under
+torchrun): rank 0's DPSummarizer shards every batch over the DP workers through the job store;
+every thread gets exactly one summary, also when a worker is killed mid-batch; the torchrun entry
+point assigns the roles (2 gloo ranks on the CPU, mock LLM)."""
+from __future__ import annotations
+
+import os
+import signal
+import socket
+import time
+
+import pytest
+import torch.multiprocessing as mp
+from torch.distributed import TCPStore
+
+from copilot_for_consensus_amd.summarization import Summarizer, Summary, Thread
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class RankSummarizer(Summarizer):
+    """Tags each summary with the rank that produced it; rank ``slow`` blocks on its first batch
+    (so the test can kill it while it holds unfinished threads)."""
+    backend, model = "mock", "rank-mock"
+
+    def __init__(self, rank, store=None, slow=None):
+        self.rank, self.store, self.slow, self.calls = rank, store, slow, 0
+
+    def summarize(self, thread):
+        return self.summarize_batch([thread])[0]
+
+    def summarize_batch(self, threads):
+        self.calls += 1
+        if self.rank == self.slow and self.store is not None:
+            self.store.set(f"started/{self.rank}", "1")
+            time.sleep(3600)
+        time.sleep(0.01 * len(threads))
+        return [Summary(t.thread_id, f"rank{self.rank}:{t.thread_id}", [], self.backend, self.model, 1, 1, 0)
+                for t in threads]
+
+
+def _worker(port, rank, world, slow, q):
+    from copilot_for_consensus_amd.parallel.dp_service import dp_worker_loop
+    store = TCPStore("127.0.0.1", port, is_master=False, timeout=__import__("datetime").timedelta(seconds=60))
+    jobs = dp_worker_loop(store, rank, world, RankSummarizer(rank, store, slow), batch_size=4, timeout=3.0,
+                          heartbeat_interval=0.3, max_idle_s=60)
+    q.put((rank, jobs))
+
+
+def _threads(n, tag="t"):
+    return [Thread(f"{tag}{i:03d}", [f"message {i}"], prompt=f"prompt {i} " * (1 + i % 7)) for i in range(n)]
+
+
+def _start(world, slow=None):
+    import datetime
+
+    from copilot_for_consensus_amd.parallel.dp_service import DPSummarizer
+    port = _free_port()
+    store = TCPStore("127.0.0.1", port, is_master=True, wait_for_workers=False,
+                     timeout=datetime.timedelta(seconds=60))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = {r: ctx.Process(target=_worker, args=(port, r, world, slow, q), daemon=True) for r in range(1, world)}
+    for p in procs.values():
+        p.start()
+    dps = DPSummarizer(store, world, RankSummarizer(0), batch_size=4, timeout=3.0, heartbeat_interval=0.3)
+    assert dps.wait_workers(120) == world
+    return store, dps, procs, q
+
+
+def test_dp_summarizer_covers_every_thread_once():
+    store, dps, procs, q = _start(3)
+    try:
+        for batch in (_threads(30, "a"), _threads(7, "b"), _threads(1, "c")):
+            out = dps.summarize_batch(batch)
+            assert [s.thread_id for s in out] == [t.thread_id for t in batch]
+            assert all(s.summary_markdown.endswith(":" + s.thread_id) for s in out)
+        ranks = {s.summary_markdown.split(":")[0] for s in dps.summarize_batch(_threads(40, "d"))}
+        assert len(ranks) >= 2, ranks           # the work really spread over the workers
+        dps.close()
+        done = dict(q.get(timeout=60) for _ in procs)
+        assert set(done) == {1, 2} and all(1 <= v <= 4 for v in done.values()), done
+    finally:
+        for p in procs.values():
+            p.join(timeout=10)
+            if p.is_alive():
+                p.kill()
+
+
+def test_killed_worker_threads_are_taken_over():
+    store, dps, procs, q = _start(3, slow=2)
+    try:
+        import threading
+        box = {}
+        th = threading.Thread(target=lambda: box.setdefault("out", dps.summarize_batch(_threads(24, "k"))))
+        th.start()
+        deadline = time.time() + 60
+        while not store.check(["started/2"]):
+            assert time.time() < deadline, "worker 2 never started its batch"
+            time.sleep(0.05)
+        os.kill(procs[2].pid, signal.SIGKILL)        # dies holding unfinished threads
+        th.join(timeout=90)
+        assert not th.is_alive(), "the job never completed after the worker died"
+        out = box["out"]
+        assert [s.thread_id for s in out] == [f"k{i:03d}" for i in range(24)]
+        assert {s.summary_markdown.split(":")[0] for s in out} <= {"rank0", "rank1"}
+        dps.close()
+        assert q.get(timeout=60)[0] == 1
+    finally:
+        for p in procs.values():
+            p.join(timeout=10)
+            if p.is_alive():
+                p.kill()
+
+
+def _main_rank(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), CFC_DIST_BACKEND="gloo", LLM_BACKEND_TYPE="mock",
+                      LLM_MOCK_LATENCY_MS="0", CUDA_VISIBLE_DEVICES="")
+    try:
+        from copilot_for_consensus_amd.services import main as M
+        ctx = M._distributed()
+        if not ctx["serve"]:
+            q.put((rank, "worker", M._model_rank(ctx)))
+            return
+        out = ctx["summarizer"].summarize_batch(_threads(12, "m"))
+        q.put((rank, "leader", [s.thread_id for s in out], type(ctx["summarizer"]).__name__))
+        M._close_distributed(ctx)
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_services_main_torchrun_roles():
+    """services.main under a 2-rank (gloo) torchrun env: rank 0 serves with a DPSummarizer, rank 1
+    becomes a DP worker and exits when rank 0 closes."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_main_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        got = {}
+        for _ in procs:
+            item = q.get(timeout=120)
+            got[item[0]] = item
+        assert got[0][1] == "leader" and got[0][3] == "DPSummarizer", got
+        assert got[0][2] == [f"m{i:03d}" for i in range(12)]
+        assert got[1][1] == "worker" and got[1][2] == 0, got
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
