@@ -164,23 +164,17 @@ class RagPipeline:
                       vector_store_updated=True, avg_generation_time_ms=1000 * dt / max(1, len(order)))
         st["embed"] = dt
 
-        # orchestrate: thread centroid query -> fused HIP kNN scan of the whole index -> top-k selection
+        # orchestrate: the service's relevance (OrchestratorService.candidates): every chunk scored by
+        # cosine to its thread's centroid, a search restricted to the thread's own rows of the HBM
+        # index -- here all threads of the batch in one segment pass over their (consecutive) rows
         t = time.perf_counter()
         tids = list(by_thread)
         spans, r = [], row0
         for tid in tids:
             spans.append((r, r + len(by_thread[tid])))
             r += len(by_thread[tid])
-        cent = torch.stack([vecs[a - row0:b - row0].mean(0) for a, b in spans])
-        k = 64
-        cand_scores: dict[str, float] = {}
-        for s in range(0, len(tids), 16):
-            v, i = self.index.search(cent[s:s + 16], k)
-            for vv, ii in zip(v.cpu().tolist(), i.cpu().tolist()):
-                for score, row in zip(vv, ii):
-                    cid = self.index._ids[row]
-                    if cid is not None:
-                        cand_scores[cid] = score
+        sc = self.index.span_centroid_scores(self.index._X, spans).cpu().tolist()
+        cand_scores = {c["_id"]: s for c, s in zip(order, sc)}
         prepared_threads, prompts, texts, sels, ctxs = [], [], [], [], []
         msg_by_id = {m["_id"]: m for m in msgs}
         thread_docs = {x["_id"]: x for x in threads}
@@ -188,8 +182,8 @@ class RagPipeline:
             cands = []
             for c in by_thread[tid]:
                 cc = dict(c)
-                cc["similarity_score"] = cand_scores.get(c["_id"], 0.5)
-                cc["source_type"] = "vector_store" if c["_id"] in cand_scores else "thread_chunks"
+                cc["similarity_score"] = cand_scores[c["_id"]]
+                cc["source_type"] = "vector_store"
                 cands.append(cc)
             sel = self.selector.select(tid, cands, self.top_k, self.budget)
             chosen = {s_.chunk_id for s_ in sel.selected_chunks}

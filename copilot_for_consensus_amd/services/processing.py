@@ -292,22 +292,25 @@ class OrchestratorService(BaseService):
         return sorted({c["thread_id"] for c in chunks})
 
     def candidates(self, thread_id: str) -> list[dict]:
+        """The thread's chunks scored by cosine to the thread's centroid, in ONE search restricted to
+        the thread's own rows (HipFlatIndex: a device gather + GEMV; reference context_sources.py
+        queries the whole collection, keeps the global top-k and filters it to the thread, which
+        can drop the thread's own chunks).  Every chunk is on one scale: without a vector store
+        (or none of the thread's vectors stored) all get the reference's neutral 0.5; a chunk whose
+        vector is missing while others have one ranks last (0.0)."""
         chunks = self.store.query_documents("chunks", {"thread_id": thread_id}, limit=1 << 20)
         scores: dict[str, float] = {}
-        if self.vectors is not None and hasattr(self.vectors, "search") and chunks:
-            import torch
+        if self.vectors is not None and chunks:
             try:
-                vecs = torch.stack([torch.tensor(self.vectors.get(c["_id"]).vector) for c in chunks
-                                    if c.get("embedding_generated")])
-                q = vecs.mean(0, keepdim=True)
-                for r in self.vectors.query_batch(q, min(len(chunks) * 4, 1024))[0]:
-                    scores[r.id] = r.score
-            except (KeyError, RuntimeError):
+                scores = self.vectors.centroid_scores([c["_id"] for c in chunks if c.get("embedding_generated")])
+            except (RuntimeError, ValueError, OSError) as e:
+                self.log.warning("vector scoring failed; neutral scores", thread_id=thread_id, error=repr(e))
                 scores = {}
+        missing = 0.0 if scores else 0.5        # neutral score (context_sources.py:21) only when none scored
         out = []
         for c in chunks:
             cc = dict(c)
-            cc["similarity_score"] = scores.get(c["_id"], 0.5)  # neutral score (context_sources.py:21)
+            cc["similarity_score"] = scores.get(c["_id"], missing)
             cc["source_type"] = "vector_store" if c["_id"] in scores else "thread_chunks"
             out.append(cc)
         return out

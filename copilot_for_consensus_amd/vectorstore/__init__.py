@@ -66,6 +66,26 @@ class VectorStore(ABC):
     def query_batch(self, query_vectors, top_k: int = 10) -> list[list[SearchResult]]:
         return [self.query(q, top_k) for q in query_vectors]
 
+    def centroid_scores(self, ids: Sequence[str]) -> dict[str, float]:
+        """Cosine similarity of each stored vector of ``ids`` to their normalised mean -- the
+        orchestrator's relevance of a thread's chunks to the thread (a search restricted to the
+        thread's own rows: every chunk scored on one scale, none dropped by a global top-k).
+        Ids not in the store are left out.  Generic path: one get() per id."""
+        have, vecs = [], []
+        for i in ids:
+            try:
+                vecs.append(np.asarray(self.get(i).vector, dtype=np.float32))
+            except KeyError:
+                continue
+            have.append(i)
+        if not vecs:
+            return {}
+        X = np.stack(vecs)
+        X = X / np.maximum(np.linalg.norm(X, axis=1, keepdims=True), 1e-12)
+        c = X.mean(0)
+        c = c / max(float(np.linalg.norm(c)), 1e-12)
+        return dict(zip(have, (X @ c).astype(float).tolist()))
+
 
 def _as_matrix(vectors, dim: int | None, device=None, dtype=torch.float32) -> torch.Tensor:
     if isinstance(vectors, torch.Tensor):
@@ -259,6 +279,29 @@ class HipFlatIndex(VectorStore):
         return SearchResult(id, 1.0, self._X[r].float().cpu().tolist(), dict(self._meta[r]))
 
     # ------------------------------------------------------------------ search
+    def centroid_scores(self, ids):
+        """Device path of VectorStore.centroid_scores: one gather of the rows, one GEMV, one copy out."""
+        with self._lock:
+            have = [i for i in ids if i in self._row]
+            if not have:
+                return {}
+            idx = torch.tensor([self._row[i] for i in have], dtype=torch.long, device=self.device)
+            s = self.span_centroid_scores(self._X.index_select(0, idx), [(0, len(have))])
+            return dict(zip(have, s.cpu().tolist()))
+
+    @staticmethod
+    def span_centroid_scores(X: torch.Tensor, spans) -> torch.Tensor:
+        """Rows of X grouped in consecutive spans (one per thread): cosine of every row to its own
+        span's normalised mean, fp32 [rows] on X's device (segment sums, no per-span launches)."""
+        Xf = torch.nn.functional.normalize(X.float(), dim=1)
+        lens = torch.tensor([b - a for a, b in spans], device=X.device)
+        seg = torch.repeat_interleave(torch.arange(len(spans), device=X.device), lens)
+        base = spans[0][0]
+        rows = Xf[base:base + int(lens.sum())]
+        cent = torch.zeros(len(spans), X.shape[1], device=X.device).index_add_(0, seg, rows)
+        cent = torch.nn.functional.normalize(cent, dim=1)
+        return (rows * cent[seg]).sum(1)
+
     def search(self, Q: torch.Tensor, k: int, rows: tuple[int, int] | None = None) -> tuple[torch.Tensor, torch.Tensor]:
         """Device-side exact search: (scores [nq, k], row indices [nq, k]) for queries Q."""
         from ..ops import kernels as K

@@ -223,7 +223,13 @@ def _run(d, tmp_path, extra_infra=(), late_archive=True):
     code, body = _http("POST", d.url("ingestion", "/api/sources/wg/trigger"))
     assert code == 200 and len(body["archive_ids"]) == 1, body
     reports = _wait_reports(d, 2)
-    code, threads = _http("GET", d.url("reporting", "/api/threads"))
+    # a thread's summary_id is written right after its report: poll briefly (busy CI hosts)
+    deadline = time.time() + 60
+    while True:
+        code, threads = _http("GET", d.url("reporting", "/api/threads"))
+        if all(t["summary_id"] for t in threads["threads"]) or time.time() > deadline:
+            break
+        time.sleep(0.2)
     assert all(t["summary_id"] for t in threads["threads"])
     code, rep = _http("GET", d.url("reporting", f"/api/reports/{reports[0]['_id']}"))
     assert code == 200 and rep["content_markdown"]
