@@ -18,6 +18,8 @@ import urllib.request
 import uuid
 from typing import Any, Callable
 
+import numpy as np
+
 from . import SearchResult, VectorStore, _as_matrix
 
 _NS = uuid.UUID("6ba7b810-9dad-11d1-80b4-00c04fd430c8")
@@ -123,6 +125,23 @@ class QdrantVectorStore(VectorStore):
         if code == 404 or not data or not data.get("result"):
             raise KeyError(id)
         return self._result(data["result"], 1.0)
+
+    def centroid_scores(self, ids):
+        """One retrieve call for the thread's points (Qdrant POST /points), scored locally."""
+        ids = list(ids)
+        if not ids:
+            return {}
+        _, data = self.http("POST", f"/collections/{self.collection}/points",
+                            {"ids": [string_to_uuid(i) for i in ids], "with_vector": True, "with_payload": True})
+        got = {r.id: r.vector for r in (self._result(p, 1.0) for p in data.get("result") or [])}
+        have = [i for i in ids if i in got and got[i]]
+        if not have:
+            return {}
+        X = np.asarray([got[i] for i in have], dtype=np.float32)
+        X = X / np.maximum(np.linalg.norm(X, axis=1, keepdims=True), 1e-12)
+        c = X.mean(0)
+        c = c / max(float(np.linalg.norm(c)), 1e-12)
+        return dict(zip(have, (X @ c).astype(float).tolist()))
 
 
 class AzureAISearchVectorStore(VectorStore):

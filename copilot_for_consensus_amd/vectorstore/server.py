@@ -16,6 +16,7 @@ this server runs its searches on the MI355X:
   POST /collections/{name}/points/delete        {"points": [ids]}
   POST /collections/{name}/points/count         -> {"count"}
   GET  /collections/{name}/points/{id}
+  POST /collections/{name}/points               retrieve {"ids", "with_vector", "with_payload"} (missing ids skipped)
   GET  /collections, /healthz, /readyz
 
 Scores follow Qdrant: cosine similarity / dot product (descending), Euclid = distance (ascending).
@@ -215,6 +216,21 @@ def create_vector_app(device: str = "cuda", capacity: int = 1 << 20, index_type:
         metas = [{**(p.get("payload") or {}), "_qdrant_id": p["id"]} for p in pts]
         c.index.add_embeddings(ids, [p["vector"] for p in pts], metas)
         return _ok({"operation_id": 0, "status": "completed"}, t0)
+
+    @app.post("/collections/{name}/points")
+    def retrieve_points(name: str, body: dict = Body(...)):
+        t0 = time.perf_counter()
+        c = get(name)
+        if c is None:
+            return _err(404, f"Collection `{name}` doesn't exist!")
+        out = []
+        for pid in body.get("ids") or []:
+            try:
+                r = c.index.get(str(pid))
+            except KeyError:
+                continue
+            out.append(point(c, r, bool(body.get("with_payload", True)), bool(body.get("with_vector", False))))
+        return _ok(out, t0)
 
     @app.post("/collections/{name}/points/search")
     def search_points(name: str, body: dict = Body(...)):

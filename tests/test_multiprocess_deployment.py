@@ -230,7 +230,8 @@ def _run(d, tmp_path, extra_infra=(), late_archive=True):
         if all(t["summary_id"] for t in threads["threads"]) or time.time() > deadline:
             break
         time.sleep(0.2)
-    assert all(t["summary_id"] for t in threads["threads"])
+    assert all(t["summary_id"] for t in threads["threads"]), (
+        threads, [r["_id"] for r in _reports(d)], d.log("orchestrator"), d.log("summarization"))
     code, rep = _http("GET", d.url("reporting", f"/api/reports/{reports[0]['_id']}"))
     assert code == 200 and rep["content_markdown"]
     # semantic topic search: reporting embeds the topic, the vector store answers over REST
@@ -263,8 +264,13 @@ def _run(d, tmp_path, extra_infra=(), late_archive=True):
     d.start("chunking")
     reports = _wait_reports(d, 5)
     assert len(reports) == 5
-    st = admin.stats()["queues"]
-    assert all(st[q]["ready"] == 0 and st[q]["unacked"] == 0 for q in SERVICES if q in st)
+    deadline = time.time() + 60        # the last events (reporting, cleanup) may still be in flight
+    while True:
+        st = admin.stats()["queues"]
+        if all(st[q]["ready"] == 0 and st[q]["unacked"] == 0 for q in SERVICES if q in st) or time.time() > deadline:
+            break
+        time.sleep(0.2)
+    assert all(st[q]["ready"] == 0 and st[q]["unacked"] == 0 for q in SERVICES if q in st), st
     assert not any(q.endswith(".dlq") and v["ready"] for q, v in st.items())
 
 
