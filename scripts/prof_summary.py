@@ -13,7 +13,10 @@ def main(root, out=None, top=30):
     if not stats and dbs:   # rocprofv3's default rocpd SQLite output (ROCm 7.x)
         import sqlite3
         con = sqlite3.connect(dbs[0])
-        rows = con.execute("select name, total_calls, total_duration, average from top_kernels").fetchall()
+        # the rocpd top_kernels view reports durations in MICROseconds (a round-2 summary printed
+        # them as ns and came out 1000x small): scale to ns so the arithmetic below is uniform
+        rows = [(n, c, t * 1e3, a * 1e3) for n, c, t, a in
+                con.execute("select name, total_calls, total_duration, average from top_kernels").fetchall()]
         tot = sum(r[2] for r in rows) or 1
         lines.append(f"# {dbs[0]}\n# total kernel time {tot/1e6:.1f} ms over {sum(r[1] for r in rows)} dispatches")
         lines.append(f"{'pct':>6} {'total_ms':>10} {'calls':>7} {'avg_us':>9}  kernel")
@@ -23,6 +26,11 @@ def main(root, out=None, top=30):
         rows = list(csv.DictReader(open(stats[0])))
         tot = sum(float(r["TotalDurationNs"]) for r in rows)
         lines.append(f"# {stats[0]}\n# total kernel time {tot/1e6:.1f} ms over {sum(int(r['Calls']) for r in rows)} dispatches")
+        if dbs:   # the same run in rocpd form: its top_kernels total, read as microseconds
+            import sqlite3
+            t_db = sum(r[0] for r in sqlite3.connect(dbs[0]).execute("select total_duration from top_kernels"))
+            lines.append(f"# rocpd top_kernels total of the same run: {t_db / 1e3:.1f} ms if read as us "
+                         f"({t_db / 1e6:.3f} ms if read as ns)")
         lines.append(f"{'pct':>6} {'total_ms':>10} {'calls':>7} {'avg_us':>9}  kernel")
         for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:top]:
             lines.append(f"{100*float(r['TotalDurationNs'])/tot:6.2f} {float(r['TotalDurationNs'])/1e6:10.2f} "

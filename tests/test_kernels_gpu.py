@@ -422,9 +422,9 @@ def test_dgemm_rejects_bad_shapes():
     with pytest.raises(ValueError):
         K.dgemm(x, w)
     x = torch.randn(8, 128, device=DEV).bfloat16()
-    w = torch.randn(96, 128, device=DEV).bfloat16()
+    w = torch.randn(192, 128, device=DEV).bfloat16()
     with pytest.raises(RuntimeError):
-        K.dgemm(x, w, bn=128)      # 96 rows do not tile by 128: the launcher refuses
+        K.dgemm(x, w, bn=128)      # 192 rows do not tile by 128: the launcher refuses
 
 
 @pytest.mark.parametrize("M,N,Kd,split", [(128, 4096, 14336, 8), (5, 256, 512, 2)])
