@@ -49,6 +49,9 @@ _KERNEL_SIGS = {
     "cfc_decode_advance": [P, P, I, P, P, P, P, P, P, I, P, P, I, I] + [P] * 6 + [I] * 4 + [P] * 4,
     "cfc_knn_scores": [P, P, I, I, I, P, P, P, P],
     "cfc_topk_pass": [P, P, I, I, I, I, P, P, P],
+    "cfc_knn_topk": [P, P, I, I, I, I, P, P, P, I, P, P, P],
+    "cfc_knn_topk_rows": [],
+    "cfc_ivf_topk": [P, P, I, I, I, P, P, P, P, I, P, I, I, P, P, P],
     "cfc_topk_chunk_size": [],
     "cfc_l2_normalize": [P, P, P, I, I, P],
     "cfc_pool": [P, P, P, P, I, I, I, I, P],

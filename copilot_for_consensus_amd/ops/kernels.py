@@ -1070,6 +1070,45 @@ def topk(scores: torch.Tensor, k: int, ids: torch.Tensor | None = None):
     return torch.gather(cur_v, 1, order), torch.gather(cur_i, 1, order)
 
 
+def _merge_candidates(cv: torch.Tensor, ci: torch.Tensor, k: int):
+    """Exact top-k of per-chunk candidates [nq, m] (values, row ids) -> sorted [nq, k]."""
+    return topk(cv, k, ci)
+
+
+def knn_topk(X, Q, k: int, xnorm2=None, qnorm2=None, alive=None, row_lo: int = 0, N: int | None = None):
+    """Fused flat scan + top-k (knn.hip knn_topk_kernel) over rows [row_lo, N) of X for <= 16
+    queries: (scores [nq, k] descending, row indices [nq, k]); the [nq, N] scores never reach HBM."""
+    N = X.shape[0] if N is None else N
+    nq = Q.shape[0]
+    if not X.is_cuda:
+        sc = ref.knn_scores(X[row_lo:N], Q, None if xnorm2 is None else xnorm2[row_lo:N], qnorm2)
+        if alive is not None:
+            sc = sc.masked_fill(~alive[row_lo:N].bool()[None], float("-inf"))
+        v, i = torch.topk(sc.float(), min(k, N - row_lo), dim=1)
+        return v, i + row_lo
+    R = kernels().cfc_knn_topk_rows()
+    nch = -(-(N - row_lo) // R)
+    cv = torch.empty(nq, nch * k, dtype=torch.float32, device=X.device)
+    ci = torch.empty(nq, nch * k, dtype=torch.int64, device=X.device)
+    check(kernels().cfc_knn_topk(X.data_ptr(), Q.data_ptr(), N, row_lo, nq, X.shape[1], _p(xnorm2), _p(qnorm2),
+                                 _p(alive), k, cv.data_ptr(), ci.data_ptr(), _stream(X)), "cfc_knn_topk")
+    return _merge_candidates(cv, ci, min(k, N - row_lo))
+
+
+def ivf_topk(X, Q, probe: torch.Tensor, list_off: torch.Tensor, maxc: int, k: int, xnorm2=None, qnorm2=None,
+             alive=None):
+    """IVF scan of the probed lists, one launch for every (query, probe, chunk): candidates
+    [nq, nprobe * maxc * k] (values, row indices; -inf / -1 padding).  ``probe`` int32 [nq, nprobe]
+    list ids, ``list_off`` int64 [nlist + 1] row offsets on the device."""
+    nq, nprobe = probe.shape
+    cv = torch.empty(nq, nprobe * maxc * k, dtype=torch.float32, device=X.device)
+    ci = torch.empty(nq, nprobe * maxc * k, dtype=torch.int64, device=X.device)
+    check(kernels().cfc_ivf_topk(X.data_ptr(), Q.data_ptr(), X.shape[0], nq, X.shape[1], _p(xnorm2), _p(qnorm2),
+                                 _p(alive), probe.data_ptr(), nprobe, list_off.data_ptr(), maxc, k, cv.data_ptr(),
+                                 ci.data_ptr(), _stream(X)), "cfc_ivf_topk")
+    return cv, ci
+
+
 def l2_normalize(x, out=None, norms2=None):
     if not x.is_cuda:
         o, n2 = ref.l2_normalize(x)

@@ -90,6 +90,8 @@ class VectorStore(ABC):
 def _as_matrix(vectors, dim: int | None, device=None, dtype=torch.float32) -> torch.Tensor:
     if isinstance(vectors, torch.Tensor):
         t = vectors
+    elif isinstance(vectors, (list, tuple)) and vectors and all(isinstance(v, torch.Tensor) for v in vectors):
+        t = torch.stack([v.reshape(-1) for v in vectors])
     else:
         t = torch.as_tensor(np.asarray(vectors, dtype=np.float32))
     if t.dim() == 1:
@@ -317,6 +319,10 @@ class HipFlatIndex(VectorStore):
         else:
             Qn = Q.contiguous()
             qn2 = Qn.float().pow(2).sum(1)
+        if Q.is_cuda and nq <= 16 and k <= 256:
+            # fused scan + top-k: only k candidates per 1024-row chunk leave the CUs
+            return K.knn_topk(self._X, Qn, k, self._norm2 if self.metric == "l2" else None, qn2,
+                              self._alive if self._dead else None, row_lo=lo, N=hi)
         xn2 = self._norm2[lo:hi] if self.metric == "l2" else None
         if Q.is_cuda and nq <= 16:
             scores = K.knn_scores(X, Qn, xn2, qn2)
@@ -391,31 +397,47 @@ class HipFlatIndex(VectorStore):
 
 
 class HipIVFIndex(HipFlatIndex):
-    """IVF-flat: rows grouped by nearest centroid; ``nprobe`` lists scanned per query."""
+    """IVF-flat (FAISS IndexIVFFlat semantics, faiss_store.py:105-111): rows regrouped so every
+    inverted list is one contiguous row range of the HBM index; a search probes the ``nprobe``
+    nearest centroids and scans all (query, list, 1024-row chunk) work items in ONE fused
+    scan + top-k launch (knn.hip cfc_ivf_topk, list-offset table on the device), then merges
+    the candidates on the device -- no per-list launches, no host syncs before the results.
+    Rows added after training form an unsorted tail scanned by the fused flat kernel until the
+    next regroup.  k-means runs on a bf16 row sample (fp32 only for the sample and centroids:
+    a 100M x 384 index never gets an fp32 copy); assignment of all rows is chunked bf16 GEMMs."""
+
+    SAMPLE_PER_LIST = 256
+    ASSIGN_CHUNK = 1 << 20
 
     def __init__(self, dimension=384, distance="cosine", nlist: int = 0, nprobe: int = 8, **kw):
         super().__init__(dimension, distance, **kw)
         self.nlist, self.nprobe = int(nlist), int(nprobe)
         self.centroids: torch.Tensor | None = None
         self._list_off: list[int] = []
+        self._list_off_t: torch.Tensor | None = None
+        self._maxc = 1
         self._trained_n = 0
 
     def train(self, sample: torch.Tensor | None = None, iters: int = 10, seed: int = 0) -> None:
-        """k-means on the GPU (GEMM assignment + index_add centroid update), then regroup rows."""
+        """k-means on the GPU over a sample of <= SAMPLE_PER_LIST rows per list, then regroup."""
         with self._lock:
             self.compact()
             n = self._n
             if n == 0:
                 return
             nlist = self.nlist or max(1, int(math.sqrt(n)))
-            X = (sample if sample is not None else self._X[:n]).to(self.device).float()
             g = torch.Generator(device="cpu").manual_seed(seed)
+            if sample is None:
+                m = min(n, max(nlist, self.SAMPLE_PER_LIST * nlist))
+                idx = torch.randperm(n, generator=g)[:m].to(self.device)
+                sample = self._X.index_select(0, idx)         # bf16 rows, no full-index copy
+            X = sample.to(self.device).float()
             C = X[torch.randperm(X.shape[0], generator=g)[:nlist].to(self.device)].clone()
             for _ in range(iters):
                 a = torch.argmax(X @ C.T, 1) if self.metric != "l2" else torch.argmin(torch.cdist(X, C), 1)
                 sums = torch.zeros_like(C).index_add_(0, a, X)
-                cnt = torch.bincount(a, minlength=C.shape[0]).clamp_min(1).float()[:, None]
-                C = sums / cnt
+                cnt = torch.bincount(a, minlength=C.shape[0])
+                C = torch.where(cnt[:, None] > 0, sums / cnt.clamp_min(1).float()[:, None], C)   # keep empty lists' seeds
                 if self.metric == "cosine":
                     C = torch.nn.functional.normalize(C, dim=1)
             self.centroids = C.to(torch.bfloat16)
@@ -423,8 +445,16 @@ class HipIVFIndex(HipFlatIndex):
             self._regroup()
 
     def _assign(self, X: torch.Tensor) -> torch.Tensor:
-        C = self.centroids.float()
-        return torch.argmax(X.float() @ C.T, 1) if self.metric != "l2" else torch.argmin(torch.cdist(X.float(), C), 1)
+        C = self.centroids
+        out = []
+        for s in range(0, X.shape[0], self.ASSIGN_CHUNK):
+            xc = X[s:s + self.ASSIGN_CHUNK]
+            if self.metric != "l2":
+                out.append(torch.argmax((xc @ C.T).float(), 1))
+            else:   # argmin ||x - c||^2 = argmax (2 x.c - ||c||^2)
+                cn = C.float().pow(2).sum(1)
+                out.append(torch.argmax(2 * (xc @ C.T).float() - cn[None, :], 1))
+        return torch.cat(out)
 
     def _regroup(self):
         n = self._n
@@ -432,14 +462,18 @@ class HipIVFIndex(HipFlatIndex):
         order = torch.argsort(a, stable=True)
         self._X[:n] = self._X[:n].index_select(0, order)
         self._norm2[:n] = self._norm2[:n].index_select(0, order)
+        self._alive[:n] = self._alive[:n].index_select(0, order)
         o = order.cpu().tolist()
         self._ids = [self._ids[r] for r in o]
         self._meta = [self._meta[r] for r in o]
-        self._row = {i: r for r, i in enumerate(self._ids)}
-        counts = torch.bincount(a, minlength=self.nlist).cpu().tolist()
-        self._list_off = [0]
-        for c in counts:
-            self._list_off.append(self._list_off[-1] + c)
+        self._row = {i: r for r, i in enumerate(self._ids) if i is not None}
+        counts = torch.bincount(a, minlength=self.nlist)
+        off = torch.zeros(self.nlist + 1, dtype=torch.int64, device=self.device)
+        off[1:] = torch.cumsum(counts, 0)
+        self._list_off_t = off
+        self._list_off = off.cpu().tolist()
+        R = 1024
+        self._maxc = max(1, -(-int(counts.max()) // R)) if n else 1
         self._trained_n = n
 
     def add_embeddings(self, ids, vectors, metadatas=None):
@@ -448,28 +482,60 @@ class HipIVFIndex(HipFlatIndex):
         if self.centroids is not None and self._n > 2 * max(self._trained_n, 1):
             self._regroup()
 
+    def probe_lists(self, Q: torch.Tensor) -> torch.Tensor:
+        """[nq, nprobe] int32 ids of each query's nearest lists (on the device)."""
+        sc = Q.float() @ self.centroids.float().T
+        if self.metric == "l2":
+            sc = 2 * sc - self.centroids.float().pow(2).sum(1)[None, :]
+        return torch.topk(sc, min(self.nprobe, self.nlist), dim=1).indices.to(torch.int32).contiguous()
+
     def search(self, Q, k, rows=None):
         if self.centroids is None or rows is not None:
             return super().search(Q, k, rows)
+        from ..ops import kernels as K
         Q = _as_matrix(Q, self.dim, device=self.device, dtype=torch.bfloat16)
-        probe = torch.topk((Q.float() @ self.centroids.float().T), min(self.nprobe, self.nlist), dim=1).indices.cpu()
+        if self.metric == "cosine":
+            Qn, qn2 = K.l2_normalize(Q.contiguous()), None
+        else:
+            Qn = Q.contiguous()
+            qn2 = Qn.float().pow(2).sum(1)
+        probe = self.probe_lists(Qn)
+        xn2 = self._norm2 if self.metric == "l2" else None
+        alive = self._alive if self._dead else None
+        if not Q.is_cuda or k > 256:
+            return self._search_ref(Qn, qn2, probe, k)
+        cv, ci = K.ivf_topk(self._X, Qn, probe, self._list_off_t, self._maxc, k, xn2, qn2, alive)
+        if self._n > self._trained_n:       # the unsorted tail, for every query
+            tv, ti = [], []
+            for s in range(0, Qn.shape[0], 16):
+                v, i = K.knn_topk(self._X, Qn[s:s + 16], k, xn2, None if qn2 is None else qn2[s:s + 16], alive,
+                                  row_lo=self._trained_n, N=self._n)
+                tv.append(v)
+                ti.append(i)
+            cv, ci = torch.cat([cv, torch.cat(tv)], 1), torch.cat([ci, torch.cat(ti)], 1)
+        return K.topk(cv, min(k, self.count()), ci)
+
+    def _search_ref(self, Qn, qn2, probe, k):
+        """CPU / large-k path: the probed lists' rows, exact scores, top-k (same results)."""
+        rows = []
+        for qi in range(Qn.shape[0]):
+            rr = [torch.arange(self._list_off[c], self._list_off[c + 1]) for c in probe[qi].tolist()]
+            rr.append(torch.arange(self._trained_n, self._n))
+            rows.append(torch.cat(rr))
         vs, is_ = [], []
-        for qi in range(Q.shape[0]):
-            cand_v, cand_i = [], []
-            spans = [(self._list_off[c], self._list_off[c + 1]) for c in probe[qi].tolist()]
-            spans.append((self._trained_n, self._n))  # un-grouped tail
-            for lo, hi in spans:
-                if hi > lo:
-                    v, i = super().search(Q[qi:qi + 1], min(k, hi - lo), rows=(lo, hi))
-                    cand_v.append(v)
-                    cand_i.append(i)
-            v = torch.cat(cand_v, 1)
-            i = torch.cat(cand_i, 1)
-            top = torch.topk(v, min(k, v.shape[1]), dim=1)
-            vs.append(top.values)
-            is_.append(torch.gather(i, 1, top.indices))
-        kk = min(x.shape[1] for x in vs)
-        return torch.cat([x[:, :kk] for x in vs]), torch.cat([x[:, :kk] for x in is_])
+        for qi, r in enumerate(rows):
+            r = r.to(self.device)
+            X = self._X.index_select(0, r).float()
+            sc = X @ Qn[qi].float()
+            if self.metric == "l2":
+                sc = -(self._norm2.index_select(0, r) + qn2[qi] - 2 * sc)
+            sc = sc.masked_fill(~self._alive.index_select(0, r), float("-inf"))
+            kk = min(k, sc.numel())
+            v, i = torch.topk(sc, kk)
+            pad = k - kk
+            vs.append(torch.cat([v, v.new_full((pad,), float("-inf"))]))
+            is_.append(torch.cat([r[i], r.new_full((pad,), -1)]))
+        return torch.stack(vs), torch.stack(is_)
 
 
 def create_vector_store(cfg=None, **overrides) -> VectorStore:

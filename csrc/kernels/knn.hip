@@ -10,6 +10,11 @@
 //     straight from HBM into the A operand: the GEMV regime of guide §5 table, last row).
 //   * cfc_topk: exact per-query top-k by 4-pass 8-bit radix select in LDS per chunk; applied
 //     recursively on the candidates until one chunk remains.
+//   * cfc_knn_topk / cfc_ivf_topk: the scan and the top-k FUSED: each workgroup scores its
+//     1024-row chunk against its queries into LDS and radix-selects every query's k best there,
+//     so only k candidates per (query, chunk) reach HBM (never the [nq, N] score matrix); the
+//     IVF form takes (query, probed list, chunk) work items from a device list-offset table in
+//     one launch.  The candidates are merged by cfc_topk_pass.
 //   * cfc_l2_normalize: rows -> unit length (+ fp32 norms), used on insert for cosine.
 //   * cfc_pool: masked mean / CLS pooling over varlen sequences (+ optional L2 normalise):
 //     the SentenceTransformer Pooling+Normalize modules.
@@ -140,6 +145,155 @@ __global__ void __launch_bounds__(256) topk_chunk_kernel(const float* __restrict
   for (int s = kk + tid; s < k; s += 256) { ov[s] = -INFINITY; oi[s] = -1; }
 }
 
+// ------------------------------------------------------------------ fused scan + top-k
+constexpr int KT_ROWS = 1024;   // rows per workgroup chunk (scores [nqb][KT_ROWS] fp32 in LDS)
+
+// Wave-level exact top-k of sc[0..len) (LDS) by 4 passes of 8-bit radix select over the
+// order-preserving keys; writes exactly k slots (ov/oi; -inf / -1 padding when len < k).
+// hist: this wave's 256-entry LDS histogram.
+__device__ void wave_topk(const float* sc, int len, int k, int64_t row0, const int64_t* ids, float* ov, int64_t* oi,
+                          uint32_t* hist) {
+  const int lane = threadIdx.x & 63;
+  const int kk = min(k, len);
+  uint32_t prefix = 0, mask = 0, need = (uint32_t)kk;
+  for (int shift = 24; shift >= 0 && kk > 0; shift -= 8) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) hist[4 * lane + j] = 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int i = lane; i < len; i += 64) {
+      const uint32_t key = f2key(sc[i]);
+      if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // lane l owns digits 255-4l .. 252-4l (descending); inclusive prefix over lanes finds the digit
+    uint32_t c[4], tot = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { c[j] = hist[255 - 4 * lane - j]; tot += c[j]; }
+    uint32_t inc = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += v;
+    }
+    const uint32_t exc = inc - tot;
+    const uint64_t hit = __ballot(exc < need && inc >= need);
+    const int owner = __ffsll((unsigned long long)hit) - 1;
+    uint32_t d = 0, acc_before = 0;
+    if (lane == owner) {
+      uint32_t a = exc;
+      int j = 0;
+      for (; j < 3; ++j) {
+        if (a + c[j] >= need) break;
+        a += c[j];
+      }
+      d = 255 - 4 * lane - j;
+      acc_before = a;
+    }
+    d = __shfl(d, owner, 64);
+    acc_before = __shfl(acc_before, owner, 64);
+    need -= acc_before;
+    prefix |= d << shift;
+    mask |= 255u << shift;
+  }
+  const uint32_t thr = prefix;
+  const uint32_t n_gt = (uint32_t)kk - need;
+  uint32_t base_gt = 0, base_eq = 0;
+  for (int i0 = 0; i0 < len && kk > 0; i0 += 64) {
+    const int i = i0 + lane;
+    const uint32_t key = i < len ? f2key(sc[i]) : 0u;
+    const bool gt = i < len && key > thr, eq = i < len && key == thr;
+    const uint64_t bg = __ballot(gt), be = __ballot(eq);
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int slot = -1;
+    if (gt) slot = (int)(base_gt + __popcll(bg & below));
+    else if (eq) {
+      const uint32_t e = base_eq + __popcll(be & below);
+      if (e < need) slot = (int)(n_gt + e);
+    }
+    if (slot >= 0) {
+      ov[slot] = key2f(key);
+      oi[slot] = ids ? ids[row0 + i] : row0 + i;
+    }
+    base_gt += __popcll(bg);
+    base_eq += __popcll(be);
+  }
+  for (int s2 = kk + lane; s2 < k; s2 += 64) { ov[s2] = -INFINITY; oi[s2] = -1; }
+}
+
+// Work item = a chunk of <= KT_ROWS consecutive rows and a set of queries (qsel < 0: all nq, else
+// query qsel only).  Flat: blockIdx.x = chunk, queries all.  IVF (probe != null): blockIdx.x =
+// (q * nprobe + j) * maxc + c -> list probe[q][j], its chunk c.  out_v/out_i: [nq][nslots][k].
+template <int KC>
+__global__ void __launch_bounds__(256) knn_topk_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Q,
+                                                       int N, int nq, const float* __restrict__ xnorm2,
+                                                       const float* __restrict__ qnorm2,
+                                                       const uint8_t* __restrict__ alive, int k, int row_lo,
+                                                       const int32_t* __restrict__ probe, int nprobe, int maxc,
+                                                       const int64_t* __restrict__ list_off, int nslots,
+                                                       float* __restrict__ out_v, int64_t* __restrict__ out_i) {
+  constexpr int D = KC * 32;
+  extern __shared__ __attribute__((aligned(16))) float kt_smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int lo, hi, q0, nqb, slot;
+  if (probe == nullptr) {
+    lo = row_lo + blockIdx.x * KT_ROWS;
+    hi = min(N, lo + KT_ROWS);
+    q0 = 0;
+    nqb = nq;
+    slot = blockIdx.x;
+  } else {
+    const int c = blockIdx.x % maxc, qj = blockIdx.x / maxc;
+    q0 = qj / nprobe;
+    nqb = 1;
+    slot = (qj % nprobe) * maxc + c;
+    const int l = probe[qj];
+    lo = (int)list_off[l] + c * KT_ROWS;
+    hi = min((int)list_off[l + 1], lo + KT_ROWS);
+  }
+  const int len = max(0, hi - lo);
+  float* sc = kt_smem;                                        // [nqb][KT_ROWS]
+  uint32_t* hist = reinterpret_cast<uint32_t*>(kt_smem + nqb * KT_ROWS) + 256 * w;
+  if (len > 0) {
+    const int col = lane & 15, g = lane >> 4;
+    const bool qv = col < nqb;
+    bf16x8_t qf[KC];
+    const uint16_t* qr = Q + (size_t)(q0 + (qv ? col : 0)) * D;
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+      qf[c] = as_bf16x8(qv ? *reinterpret_cast<const uint4*>(qr + 32 * c + 8 * g) : make_uint4(0, 0, 0, 0));
+    const float qn = (qnorm2 && qv) ? qnorm2[q0 + col] : 0.f;
+    const int ngroups = (len + 15) / 16;
+    for (int grp = w; grp < ngroups; grp += 4) {
+      const int r0 = lo + grp * 16;
+      const int r = min(r0 + col, hi - 1);
+      const uint16_t* xr = X + (size_t)r * D;
+      uint4 a[KC];
+#pragma unroll
+      for (int c = 0; c < KC; ++c) a[c] = *reinterpret_cast<const uint4*>(xr + 32 * c + 8 * g);
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < KC; ++c) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[c]), qf[c], acc, 0, 0, 0);
+      if (qv) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = r0 + 4 * g + i;
+          if (row < hi) {
+            float v = acc[i];
+            if (xnorm2) v = -(xnorm2[row] + qn - 2.f * v);
+            if (alive && !alive[row]) v = -INFINITY;
+            sc[col * KT_ROWS + (row - lo)] = v;
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int qi = w; qi < nqb; qi += 4) {
+    const size_t o = ((size_t)(q0 + qi) * nslots + slot) * k;
+    wave_topk(sc + qi * KT_ROWS, len, k, lo, nullptr, out_v + o, out_i + o, hist);
+  }
+}
+
 __global__ void __launch_bounds__(256) l2_normalize_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ in,
                                                            float* __restrict__ norms2, int dim) {
   __shared__ float red[16];
@@ -242,4 +396,62 @@ CFC_API int cfc_pool(float* out_f32, void* out_bf16, const void* hidden, const i
   pool_kernel<<<nseq, 256, dim * sizeof(float), stream>>>(out_f32, (uint16_t*)out_bf16, (const uint16_t*)hidden,
                                                           cu_seqlens, dim, mode, normalize);
   return CFC_CHECK_LAUNCH();
+}
+
+namespace {
+template <int KC>
+int knn_topk_launch(const void* X, const void* Q, int N, int nq, const float* xnorm2, const float* qnorm2,
+                    const uint8_t* alive, int k, int row_lo, const int32_t* probe, int nprobe, int maxc,
+                    const int64_t* list_off, int nslots, float* out_v, int64_t* out_i, int blocks, int nqb,
+                    hipStream_t stream) {
+  const size_t lds = (size_t)nqb * KT_ROWS * 4 + 4 * 256 * 4;
+  knn_topk_kernel<KC><<<blocks, 256, lds, stream>>>((const uint16_t*)X, (const uint16_t*)Q, N, nq, xnorm2, qnorm2,
+                                                    alive, k, row_lo, probe, nprobe, maxc, list_off, nslots, out_v,
+                                                    out_i);
+  return CFC_CHECK_LAUNCH();
+}
+
+int knn_topk_dispatch(int dim, const void* X, const void* Q, int N, int nq, const float* xnorm2, const float* qnorm2,
+                      const uint8_t* alive, int k, int row_lo, const int32_t* probe, int nprobe, int maxc,
+                      const int64_t* list_off, int nslots, float* out_v, int64_t* out_i, int blocks, int nqb,
+                      hipStream_t stream) {
+#define KT(KC) return knn_topk_launch<KC>(X, Q, N, nq, xnorm2, qnorm2, alive, k, row_lo, probe, nprobe, maxc, \
+                                          list_off, nslots, out_v, out_i, blocks, nqb, stream)
+  switch (dim / 32) {
+    case 4: KT(4);
+    case 8: KT(8);
+    case 12: KT(12);
+    case 16: KT(16);
+    case 24: KT(24);
+    case 32: KT(32);
+    default: return -2;
+  }
+#undef KT
+}
+}  // namespace
+
+// Flat index, rows [row_lo, N): candidates out [nq][ceil((N - row_lo) / 1024)][k] (unsorted
+// within a chunk; merge with cfc_topk_pass).  nq <= 16, k <= 256; alive: optional uint8 row mask.
+CFC_API int cfc_knn_topk(const void* X, const void* Q, int N, int row_lo, int nq, int dim, const float* xnorm2,
+                         const float* qnorm2, const uint8_t* alive, int k, float* out_v, int64_t* out_i,
+                         hipStream_t stream) {
+  if (nq < 1 || nq > 16 || dim % 32 != 0 || N <= row_lo || row_lo < 0 || k < 1 || k > 256) return -1;
+  const int nch = (N - row_lo + KT_ROWS - 1) / KT_ROWS;
+  return knn_topk_dispatch(dim, X, Q, N, nq, xnorm2, qnorm2, alive, k, row_lo, nullptr, 1, 1, nullptr, nch, out_v,
+                           out_i, nch, nq, stream);
+}
+
+CFC_API int cfc_knn_topk_rows() { return KT_ROWS; }
+
+// IVF: probe [nq][nprobe] list ids, list_off [nlist + 1] row offsets (rows grouped by list), maxc =
+// max chunks of any list.  One launch of nq * nprobe * maxc workgroups; candidates out
+// [nq][nprobe * maxc][k].
+CFC_API int cfc_ivf_topk(const void* X, const void* Q, int N, int nq, int dim, const float* xnorm2,
+                         const float* qnorm2, const uint8_t* alive, const int32_t* probe, int nprobe,
+                         const int64_t* list_off, int maxc, int k, float* out_v, int64_t* out_i, hipStream_t stream) {
+  if (nq < 1 || nprobe < 1 || maxc < 1 || dim % 32 != 0 || k < 1 || k > 256) return -1;
+  const long blocks = (long)nq * nprobe * maxc;
+  if (blocks > (1L << 30)) return -1;
+  return knn_topk_dispatch(dim, X, Q, N, nq, xnorm2, qnorm2, alive, k, 0, probe, nprobe, maxc, list_off,
+                           nprobe * maxc, out_v, out_i, (int)blocks, 1, stream);
 }
