@@ -188,6 +188,8 @@ def run_service(service: BaseService, app, host: str = "0.0.0.0", port: int = 80
 
     def consume():
         service.start()
+        if hasattr(service, "start_async"):
+            service.start_async()
         if service.subscriber is not None:
             service.subscriber.start_consuming()
 
@@ -201,3 +203,5 @@ def run_service(service: BaseService, app, host: str = "0.0.0.0", port: int = 80
         if service.subscriber is not None:
             service.subscriber.stop_consuming()
         t.join(timeout=10)
+        if hasattr(service, "stop_async"):
+            service.stop_async()

@@ -97,7 +97,8 @@ class Node:
                 citation_count=cfgs["summarization"].citation_count,
                 context_window_tokens=cfgs["summarization"].context_window_tokens,
                 max_batch_threads=cfgs["summarization"].max_batch_threads,
-                batch_wait_ms=cfgs["summarization"].batch_wait_ms, retry_delay_seconds=0.1, **common),
+                batch_wait_ms=cfgs["summarization"].batch_wait_ms, retry_delay_seconds=0.1,
+                continuous=cfgs["summarization"].continuous_batching, **common),
             "reporting": lambda: ReportingService(
                 pub("reporting"), sub("reporting"), self.store, self.vectors, self.embedder,
                 notify_enabled=cfgs["reporting"].notify_enabled,
@@ -126,6 +127,8 @@ class Node:
         self.connect()
         for s in self.services.values():
             s.start()
+            if threaded and hasattr(s, "start_async"):
+                s.start_async()        # the summarizer's continuous engine / micro-batcher
         if threaded:
             self.start_scheduler()
         if threaded:
@@ -159,6 +162,9 @@ class Node:
                 s.subscriber.stop_consuming()
         for t in self._threads:
             t.join(timeout=5)
+        for s in self.services.values():
+            if hasattr(s, "stop_async"):
+                s.stop_async()
 
     def http_app(self, auth_base: str = "/auth"):
         """The all-in-one HTTP front in the gateway's layout (deploy/gateway/nginx.conf):

@@ -382,9 +382,13 @@ class SummarizationService(BaseService):
 
     def __init__(self, publisher, subscriber, document_store, summarizer: Summarizer, citation_count: int = 12,
                  context_window_tokens: int = 4096, max_batch_threads: int = 128, batch_wait_ms: int = 50,
-                 max_retries: int = 3, retry_delay_seconds: float = 5.0, **kw):
+                 max_retries: int = 3, retry_delay_seconds: float = 5.0, continuous: bool = True, **kw):
         super().__init__(publisher, subscriber, document_store, **kw)
         self.summarizer = summarizer
+        # continuous batching (a summarizer with start_continuous, e.g. the HIP engine): requests go
+        # straight into the running decode batch; otherwise micro-batches of <= max_batch_threads
+        self.continuous = continuous
+        self._streaming = False
         self.citation_count, self.ctx_tokens = citation_count, context_window_tokens
         self.max_batch, self.batch_wait = max_batch_threads, batch_wait_ms / 1000.0
         self.max_retries, self.retry_delay = max_retries, retry_delay_seconds
@@ -434,20 +438,36 @@ class SummarizationService(BaseService):
         self.metrics.observe("summarization_latency_seconds", time.perf_counter() - t0)
         for k, v in (getattr(self.summarizer, "last_stats", None) or {}).items():
             self.metrics.gauge(f"summarization_gpu_{k}", float(v))
-        out = []
-        for (tid, ctx, _), s in zip(prepared, summaries):
-            cites = format_citations(ctx["chunks"], self.citation_count)
-            sid = cids.summary_id(tid, [c["chunk_id"] for c in cites])
-            self.metrics.increment("summarization_tokens_total", s.tokens_prompt, tags={"type": "prompt"})
-            self.metrics.increment("summarization_tokens_total", s.tokens_completion, tags={"type": "completion"})
-            out.append(self.publish("SummaryComplete", summary_id=sid, thread_id=tid,
-                                    summary_markdown=s.summary_markdown or "(empty summary)", citations=cites,
-                                    llm_backend=s.llm_backend, llm_model=s.llm_model, tokens_prompt=s.tokens_prompt,
-                                    tokens_completion=s.tokens_completion, latency_ms=int(s.latency_ms)))
-        return out
+        return [self._publish_summary(tid, ctx, s) for (tid, ctx, _), s in zip(prepared, summaries)]
 
-    # micro-batching: requests accumulate for up to batch_wait_ms (or max_batch) before one engine call
+    def _publish_summary(self, tid: str, ctx: dict, s) -> dict:
+        cites = format_citations(ctx["chunks"], self.citation_count)
+        sid = cids.summary_id(tid, [c["chunk_id"] for c in cites])
+        self.metrics.increment("summarization_tokens_total", s.tokens_prompt, tags={"type": "prompt"})
+        self.metrics.increment("summarization_tokens_total", s.tokens_completion, tags={"type": "completion"})
+        return self.publish("SummaryComplete", summary_id=sid, thread_id=tid,
+                            summary_markdown=s.summary_markdown or "(empty summary)", citations=cites,
+                            llm_backend=s.llm_backend, llm_model=s.llm_model, tokens_prompt=s.tokens_prompt,
+                            tokens_completion=s.tokens_completion, latency_ms=int(s.latency_ms))
+
+    # continuous batching (start_async with a streaming summarizer): each request is prepared and
+    # submitted at once; the engine thread publishes its summary when its sequence finishes.
+    # micro-batching otherwise: requests accumulate for up to batch_wait_ms (or max_batch) before
+    # one engine call
     def _on_request(self, event):
+        if self._streaming:
+            tid, ctx, prompt = self.prepare(event)     # store not ready -> raises -> the retry policy
+            t0 = time.perf_counter()
+
+            def done(s, err, tid=tid, ctx=ctx, event=event):
+                if err is not None:
+                    self.log.error("summarization failed", thread_id=tid, error=repr(err))
+                    self.on_failure("SummarizationRequested", event, err)
+                    return
+                self.metrics.observe("summarization_latency_seconds", time.perf_counter() - t0)
+                self._publish_summary(tid, ctx, s)
+            self.summarizer.submit(SumThread(tid, ctx["messages"], len(ctx["chunks"]), self.ctx_tokens, prompt), done)
+            return
         if self._worker is None:
             self.summarize_events([event])
             return
@@ -477,6 +497,22 @@ class SummarizationService(BaseService):
 
     def stop_batching(self) -> None:
         self._stop = True
+
+    def start_async(self) -> None:
+        """Background engine for a consuming service: continuous batching when the summarizer
+        streams, else the micro-batcher (when batches are allowed)."""
+        start = getattr(self.summarizer, "start_continuous", None)
+        if self.continuous and callable(start):
+            start()
+            self._streaming = True
+        elif self.max_batch > 1:
+            self.start_batching()
+
+    def stop_async(self) -> None:
+        if self._streaming:
+            self.summarizer.stop_continuous()
+            self._streaming = False
+        self.stop_batching()
 
     def on_failure(self, event_type, event, error):
         if event_type == "SummarizationRequested":

@@ -189,6 +189,96 @@ class HipLLMSummarizer(Summarizer):
     def summarize(self, thread: Thread) -> Summary:
         return self.summarize_batch([thread])[0]
 
+    # ------------------------------------------------------------ continuous (service) mode
+    def start_continuous(self, steps_per_sync: int = 16, min_admit: int = 1, max_wait_s: float = 0.05) -> None:
+        """Serve :meth:`submit` ted threads through a ContinuousEngine on a background thread: a
+        thread joins the running decode batch at the next burst boundary and leaves it at its stop
+        (EOS, a stop string on the device, or max_new_tokens), its slot refilled from the queue --
+        no batch-of-N latency for a bursty bus load."""
+        import collections
+        import threading
+
+        from ..runtime.continuous import ContinuousEngine
+        if getattr(self, "_ce", None) is not None:
+            return
+        eos = () if self.ignore_eos else (self.cfg.eos_id,)
+        self._ce = ContinuousEngine(self.engine, max_slots=self.max_batch, max_new_cap=self.max_new_tokens,
+                                    max_prompt=self.context_limit, steps_per_sync=steps_per_sync, stop_ids=eos,
+                                    temperature=self.sampling, min_admit=min_admit, max_wait_s=max_wait_s,
+                                    stop_strings=None if self.ignore_eos else self.stop_matcher)
+        self._inbox: collections.deque = collections.deque()
+        self._cv = threading.Condition()
+        self._live: dict = {}
+        self._ce_stop = False
+        self._ce_thread = threading.Thread(target=self._serve, name="llm-continuous", daemon=True)
+        self._ce_thread.start()
+
+    def submit(self, thread: Thread, done) -> None:
+        """Queue one thread; ``done(summary, error)`` is called from the engine thread."""
+        ids = self._tokens(thread.prompt)
+        with self._cv:
+            self._inbox.append((thread, ids, time.perf_counter(), done))
+            self._cv.notify()
+
+    def _finish(self, thread, ids, t0, done, toks) -> None:
+        text = self.apply_stops(self.tokenizer.decode(toks)).strip() or "(empty summary)"
+        done(Summary(thread.thread_id, text, [], self.backend, self.model, len(ids), len(toks),
+                     int(1000 * (time.perf_counter() - t0))), None)
+
+    def _serve(self) -> None:
+        ce = self._ce
+        while True:
+            with self._cv:
+                while not self._ce_stop and not self._inbox and not ce.pending():
+                    self._cv.wait(0.5)
+                if self._ce_stop:
+                    break
+                new = list(self._inbox)
+                self._inbox.clear()
+            for item in new:
+                thread, ids, t0, done = item
+                try:
+                    r = ce.submit(ids, self.max_new_tokens)
+                except ValueError as e:
+                    done(None, e)
+                    continue
+                self._live[r.rid] = item
+            try:
+                finished = ce.step()
+            except Exception as e:  # noqa: BLE001 -- engine failure: every queued / running thread fails
+                for item in list(self._live.values()):
+                    item[3](None, e)
+                self._live.clear()
+                self._ce = ce = self._reset_continuous(ce)
+                continue
+            for r in finished:
+                item = self._live.pop(r.rid, None)
+                if item is not None:
+                    try:
+                        self._finish(*item, r.tokens or [])
+                    except Exception as e:  # noqa: BLE001 -- a callback failing must not stop the engine
+                        item[3](None, e)
+
+    def _reset_continuous(self, ce):
+        from ..runtime.continuous import ContinuousEngine
+        try:
+            ce.close()
+        except Exception:  # noqa: BLE001 -- best effort: the old slots' blocks may be gone with the error
+            pass
+        return ContinuousEngine(self.engine, max_slots=ce.B, max_new_cap=ce.cap, max_prompt=ce.max_prompt,
+                                steps_per_sync=ce.steps_per_sync, stop_ids=ce.stop_ids, temperature=ce.sampling,
+                                min_admit=ce.min_admit, max_wait_s=ce.max_wait_s, stop_strings=ce.stop_strings)
+
+    def stop_continuous(self) -> None:
+        if getattr(self, "_ce", None) is None:
+            return
+        with self._cv:
+            self._ce_stop = True
+            self._cv.notify()
+        self._ce_thread.join(timeout=30)
+        self._ce.close()
+        self._ce = None
+
 
 class _HTTPSummarizer(Summarizer):
     """Shared HTTP behaviour of the Ollama / llama.cpp drivers (reference local_llm_summarizer.py,

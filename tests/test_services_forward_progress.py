@@ -343,3 +343,39 @@ def test_reporting_waits_for_thread():
                                    "tokens_completion": 1, "latency_ms": 1}).to_dict()
     sub.inject_event(ev)  # thread never appears: retries exhausted, no report
     assert svc.get_stats()["events_failed"] == 1 and rec.get_events("ReportPublished") == []
+
+
+def test_summarization_continuous_engine_publishes_each_thread():
+    """start_async with the HIP summarizer (tiny decoder, CPU path): requests are submitted into a
+    ContinuousEngine as they arrive and every thread's SummaryComplete is published from the
+    engine thread; the texts equal the batch path's (greedy)."""
+    import time
+
+    from copilot_for_consensus_amd.summarization import HipLLMSummarizer, Thread
+    store = InMemoryDocumentStore()
+    _, threads, vs = _embedded(store)
+    opub, _ = _pub()
+    orch = OrchestratorService(opub, None, store, vs)
+    reqs = [orch.orchestrate_thread(t["_id"]) for t in threads]
+    llm = HipLLMSummarizer(model="tiny", device="cpu", max_new_tokens=12, kv_cache_tokens=16384, max_batch=4,
+                           temperature=0.0)
+    pub, rec = _pub()
+    svc = SummarizationService(pub, None, store, llm, max_retries=1, retry_delay_seconds=0)
+    svc.start_async()
+    assert svc._streaming
+    try:
+        for r in reqs:
+            svc._on_request(r)
+        deadline = time.time() + 120
+        while time.time() < deadline and len(rec.get_events("SummaryComplete")) < len(reqs):
+            time.sleep(0.05)
+    finally:
+        svc.stop_async()
+    done = rec.get_events("SummaryComplete")
+    assert sorted(e["data"]["thread_id"] for e in done) == sorted(t["_id"] for t in threads)
+    # same text as the one-shot batch path for the same prompts
+    batch = SummarizationService(pub, None, store, llm)
+    prepared = [batch.prepare(r) for r in reqs]
+    want = llm.summarize_batch([Thread(tid, ctx["messages"], len(ctx["chunks"]), 4096, p) for tid, ctx, p in prepared])
+    got = {e["data"]["thread_id"]: e["data"]["summary_markdown"] for e in done}
+    assert [got[s.thread_id] for s in want] == [s.summary_markdown for s in want]
