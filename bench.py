@@ -50,6 +50,9 @@ def parse_args(argv=None):
     ap.add_argument("--index-prefill", type=int, default=1_000_000,
                     help="background vectors resident in the HBM kNN index besides the run's own chunks")
     ap.add_argument("--no-overlap", action="store_true", help="run pipeline stages strictly sequentially")
+    ap.add_argument("--pipeline", choices=["bench", "node"], default="bench",
+                    help="bench: the stage code with a static LLM batch (headline); node: the real services "
+                         "(Node, in-proc bus, continuous summarization engine), pipeline/node_bench.py")
     return ap.parse_args(argv)
 
 
@@ -69,6 +72,8 @@ def main(argv=None):
     dev = env.device
     # TP groups of args.tp consecutive ranks (one engine per group), DP across groups
     groups = make_groups(env, args.tp)
+    if args.pipeline == "node":
+        return _main_node(args, env, groups)
     pipe = BenchPipeline(model=args.model, encoder=args.encoder, device=dev, threads_per_step=args.threads_per_gpu,
                          max_new_tokens=args.max_new, tp=args.tp, prefill_tokens=args.prefill_tokens, kv_dtype=args.kv_dtype,
                          weight_dtype=args.weights,
@@ -152,6 +157,71 @@ def main(argv=None):
             "baseline_threads_per_s": round(BASELINE_THREADS_PER_S, 4),
         }
         print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _main_node(args, env, groups):
+    """--pipeline node: the same metric through the deployment's services (one node per rank)."""
+    import torch
+    import torch.distributed as dist
+
+    from copilot_for_consensus_amd.pipeline.node_bench import NodeBench
+    if args.tp > 1:
+        raise SystemExit("--pipeline node runs one model per rank (use torchrun ranks for DP)")
+    world, rank, dev = env.world, env.rank, env.device
+    nb = NodeBench(model=args.model, encoder=args.encoder, device=dev, threads_per_step=args.threads_per_gpu,
+                   max_new_tokens=args.max_new, seed=args.seed + 7919 * groups.dp_rank, index_prefill=args.index_prefill)
+    nb.prepare_sources(list(range(args.warmup + args.steps)))
+
+    def report(kind):
+        def f(i, r):
+            if rank == 0:
+                print(f"[bench-node] {kind} {i}: {r.summary()}", file=sys.stderr, flush=True)
+        return f
+    if args.warmup:
+        nb.run_steps(list(range(args.warmup)), on_step=report("warmup"))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+    barrier()
+    t0 = time.perf_counter()
+    results = nb.run_steps(list(range(args.warmup, args.warmup + args.steps)), on_step=report("step"))
+    barrier()
+    elapsed = time.perf_counter() - t0
+    threads = sum(r.threads for r in results)
+    gen = sum(r.generated_tokens for r in results)
+    prompt = sum(r.prompt_tokens for r in results)
+    lats = [x for r in results for x in r.latencies_s]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([threads, gen, prompt], dtype=torch.float64, device=dev)
+        dist.all_reduce(c)
+        threads, gen, prompt = (float(x) for x in c.tolist())
+        parts = [None] * world
+        dist.all_gather_object(parts, lats)
+        lats = [x for p in parts for x in p]
+    nb.close()
+    if rank == 0:
+        value = threads / elapsed
+        print(json.dumps({
+            "metric": "end-to-end threads summarized/sec + p50 summary latency, Mistral-7B TP=1/8",
+            "value": round(value, 4), "unit": "threads/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": round(value / BASELINE_THREADS_PER_S, 2), "dtype": "bf16",
+            "data": "synthetic .mbox threads, random-init weights",
+            "config": {"model": args.model, "encoder": args.encoder, "global_batch": args.threads_per_gpu * world,
+                       "seq_len": round(prompt / max(threads, 1)), "max_new_tokens": args.max_new, "kv_cache": "bf16",
+                       "parallelism": f"dp{world}",
+                       "pipeline": "node: ingestion+parse+chunk+embed+index+select+continuous prefill/decode+report"},
+            "p50_summary_latency_s": round(statistics.median(lats), 3) if lats else None,
+            "generated_tokens_per_s": round(gen / elapsed, 1), "prompt_tokens_per_s": round(prompt / elapsed, 1),
+            "baseline_threads_per_s": round(BASELINE_THREADS_PER_S, 4)}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

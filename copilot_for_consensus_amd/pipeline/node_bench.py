@@ -1,0 +1,135 @@
+"""``bench.py --pipeline node``: the headline workload through the REAL services.
+
+The default bench pipeline (pipeline/bench_pipeline.py) calls the stage code directly with a
+static 128-thread LLM batch.  This one runs the deployment itself: a :class:`~..services.node.Node`
+(ingestion, parsing, chunking, embedding, orchestrator, summarization, reporting on the in-process
+bus, document store in memory, HIP encoder + HBM vector index + HIP decoder on the GPU) with the
+summarization service on its continuous engine.  Each step's synthetic mailing-list archive enters
+through the ingestion service (a local source: fetch -> archive store -> ``ArchiveIngested``) and
+the step is done when every one of its threads has a report in the store.  The archives of all
+timed steps are queued at once (a backlog, as a mailing-list backfill produces), so stages
+overlap the way the event-driven services overlap them.
+
+Same model, encoder, threads per step, generated tokens (``LLM_IGNORE_EOS`` as the bench
+pipeline's ``ignore_eos``: random-init weights would otherwise stop at arbitrary points) and
+selection settings (top-5 chunks, 2048-token context) as the bench pipeline.
+"""
+from __future__ import annotations
+
+import dataclasses
+import statistics
+import tempfile
+import time
+from datetime import datetime
+from pathlib import Path
+
+import torch
+
+
+@dataclasses.dataclass
+class NodeStepResult:
+    threads: int
+    generated_tokens: int
+    prompt_tokens: int
+    latencies_s: list
+    wall_s: float
+
+    def summary(self) -> str:
+        p50 = statistics.median(self.latencies_s) if self.latencies_s else float("nan")
+        return (f"threads={self.threads} prompt_tok={self.prompt_tokens} gen_tok={self.generated_tokens} "
+                f"p50={p50:.2f}s wall={self.wall_s:.2f}s")
+
+
+class NodeBench:
+    def __init__(self, model: str = "mistral-7b", encoder: str = "minilm-l6", device="cuda",
+                 threads_per_step: int = 128, max_new_tokens: int = 512, seed: int = 0,
+                 index_prefill: int = 1_000_000, continuous: bool = True):
+        from ..services.node import Node
+        from ..utils.synthetic import SyntheticArchive
+        dev = str(device)
+        self.tmp = Path(tempfile.mkdtemp(prefix="cfc-node-bench-"))
+        enc_name = {"minilm-l6": "all-MiniLM-L6-v2"}.get(encoder, encoder)
+        self.env = {
+            "EMBEDDING_BACKEND_TYPE": "hip", "EMBEDDING_MODEL_NAME": enc_name, "EMBEDDING_DEVICE": dev,
+            "EMBEDDING_RANDOM_SEED": str(seed),
+            "VECTOR_STORE_TYPE": "hip", "VECTOR_STORE_DEVICE": dev,
+            "VECTOR_STORE_CAPACITY": str(index_prefill + (1 << 20)),
+            "LLM_BACKEND_TYPE": "hip", "LLM_MODEL_PRESET": model, "LLM_DEVICE": dev,
+            "LLM_MAX_NEW_TOKENS": str(max_new_tokens), "LLM_MAX_BATCH": str(threads_per_step),
+            "LLM_TEMPERATURE": "0", "LLM_IGNORE_EOS": "true", "LLM_RANDOM_SEED": "1234",
+            "LLM_KV_CACHE_TOKENS": str(max(65536, threads_per_step * (4096 + max_new_tokens))),
+            "SUMMARIZATION_CONTINUOUS_BATCHING": "true" if continuous else "false",
+            "SUMMARIZATION_MAX_BATCH_THREADS": str(threads_per_step), "SUMMARIZATION_MIN_ADMIT": str(threads_per_step),
+            "SUMMARIZATION_ADMIT_WAIT_MS": "500",
+            "ORCHESTRATOR_TOP_K": "5", "ORCHESTRATOR_CONTEXT_WINDOW_TOKENS": "2048",
+            "INGESTION_STORAGE_PATH": str(self.tmp / "ingest"), "INGESTION_SCHEDULE_INTERVAL_SECONDS": "0",
+            "ARCHIVE_STORE_TYPE": "local", "ARCHIVE_BASE_PATH": str(self.tmp / "archives"),
+            "DOCUMENT_STORE_TYPE": "inmemory", "MESSAGE_BUS_TYPE": "inproc",
+        }
+        self.node = Node(env=self.env)
+        if index_prefill and hasattr(self.node.vectors, "add_embeddings"):
+            # the same 1M-vector resident index the bench pipeline searches next to (rows of other lists)
+            g = torch.Generator(device=dev).manual_seed(seed + 99)
+            dim = int(self.node.embedder.dimension)
+            for s in range(0, index_prefill, 1 << 18):
+                n = min(1 << 18, index_prefill - s)
+                v = torch.randn(n, dim, device=dev, generator=g)
+                self.node.vectors.add_embeddings([f"prefill-{s + i}" for i in range(n)], v, [{} for _ in range(n)])
+        self.node.start(threaded=True)
+        self.ingestion = self.node.services["ingestion"]
+        self.store = self.node.store
+        self.generator = SyntheticArchive(seed=seed)
+        self.threads_per_step = threads_per_step
+        self.sources: dict[int, Path] = {}
+
+    def prepare_sources(self, steps) -> None:
+        """The steps' archives as local mailing-list sources (outside the timed region)."""
+        for s in steps:
+            d = self.tmp / f"src{s}"
+            d.mkdir(parents=True, exist_ok=True)
+            (d / f"step{s}.mbox").write_bytes(self.generator.mbox(self.threads_per_step))
+            self.sources[s] = d
+
+    def _submit(self, step: int) -> tuple[list[str], float]:
+        t0 = time.time()
+        ids = self.ingestion.ingest_archive({"name": f"bench-{step}", "source_type": "local",
+                                            "url": str(self.sources[step]), "enabled": True})
+        return ids, t0
+
+    def _thread_ids(self, archive_ids: list[str]) -> list[str]:
+        return [t["_id"] for t in self.store.query_documents("threads", {"archive_id": {"$in": archive_ids}},
+                                                             limit=1 << 20)]
+
+    def run_steps(self, steps, on_step=None, timeout_s: float = 3600.0) -> list[NodeStepResult]:
+        """Queue every step's archive, then wait until each step's threads all have reports."""
+        subs = {s: self._submit(s) for s in steps}
+        out: list[NodeStepResult] = []
+        deadline = time.time() + timeout_s
+        pending = list(steps)
+        while pending:
+            if time.time() > deadline:
+                raise TimeoutError(f"node bench: steps {pending} unfinished after {timeout_s}s")
+            s = pending[0]
+            aids, t0 = subs[s]
+            tids = self._thread_ids(aids)
+            reports = self.store.query_documents("summaries", {"thread_id": {"$in": tids}}, limit=1 << 20) \
+                if tids else []
+            if len(tids) < self.threads_per_step or len({r["thread_id"] for r in reports}) < len(tids):
+                time.sleep(0.05)
+                continue
+            lat = [max(0.0, datetime.fromisoformat(r["generated_at"].replace("Z", "+00:00")).timestamp() - t0)
+                   for r in reports]
+            meta = [r.get("metadata") or {} for r in reports]
+            res = NodeStepResult(len(tids), sum(int(m.get("tokens_completion", 0)) for m in meta),
+                                 sum(int(m.get("tokens_prompt", 0)) for m in meta), lat, time.time() - t0)
+            out.append(res)
+            if on_step is not None:
+                on_step(s, res)
+            pending.pop(0)
+        return out
+
+    def close(self) -> None:
+        self.node.stop()
+        import shutil
+        shutil.rmtree(self.tmp, ignore_errors=True)
+

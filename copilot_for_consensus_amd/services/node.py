@@ -98,7 +98,9 @@ class Node:
                 context_window_tokens=cfgs["summarization"].context_window_tokens,
                 max_batch_threads=cfgs["summarization"].max_batch_threads,
                 batch_wait_ms=cfgs["summarization"].batch_wait_ms, retry_delay_seconds=0.1,
-                continuous=cfgs["summarization"].continuous_batching, **common),
+                continuous=cfgs["summarization"].continuous_batching,
+                min_admit=cfgs["summarization"].min_admit, admit_wait_ms=cfgs["summarization"].admit_wait_ms,
+                **common),
             "reporting": lambda: ReportingService(
                 pub("reporting"), sub("reporting"), self.store, self.vectors, self.embedder,
                 notify_enabled=cfgs["reporting"].notify_enabled,

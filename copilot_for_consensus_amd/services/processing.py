@@ -382,12 +382,14 @@ class SummarizationService(BaseService):
 
     def __init__(self, publisher, subscriber, document_store, summarizer: Summarizer, citation_count: int = 12,
                  context_window_tokens: int = 4096, max_batch_threads: int = 128, batch_wait_ms: int = 50,
-                 max_retries: int = 3, retry_delay_seconds: float = 5.0, continuous: bool = True, **kw):
+                 max_retries: int = 3, retry_delay_seconds: float = 5.0, continuous: bool = True,
+                 min_admit: int = 1, admit_wait_ms: int = 50, **kw):
         super().__init__(publisher, subscriber, document_store, **kw)
         self.summarizer = summarizer
         # continuous batching (a summarizer with start_continuous, e.g. the HIP engine): requests go
         # straight into the running decode batch; otherwise micro-batches of <= max_batch_threads
         self.continuous = continuous
+        self.min_admit, self.admit_wait = int(min_admit), admit_wait_ms / 1000.0
         self._streaming = False
         self.citation_count, self.ctx_tokens = citation_count, context_window_tokens
         self.max_batch, self.batch_wait = max_batch_threads, batch_wait_ms / 1000.0
@@ -503,7 +505,7 @@ class SummarizationService(BaseService):
         streams, else the micro-batcher (when batches are allowed)."""
         start = getattr(self.summarizer, "start_continuous", None)
         if self.continuous and callable(start):
-            start()
+            start(min_admit=self.min_admit, max_wait_s=self.admit_wait)
             self._streaming = True
         elif self.max_batch > 1:
             self.start_batching()

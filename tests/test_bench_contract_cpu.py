@@ -52,3 +52,11 @@ def test_bench_two_ranks_under_torchrun():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", *ARGS]
     _check(_run(cmd), 2)
+
+
+def test_bench_node_pipeline_contract():
+    """--pipeline node: the same JSON contract measured through the real services (Node on the
+    in-proc bus, continuous summarization engine), every thread of every step reported."""
+    d = _run([sys.executable, "bench.py", "--gpus", "1", "--pipeline", "node", *ARGS])
+    _check(d, 1)
+    assert d["config"]["pipeline"].startswith("node:")
