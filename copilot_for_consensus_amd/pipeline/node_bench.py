@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import dataclasses
 import statistics
+import sys
 import tempfile
 import time
 from datetime import datetime
@@ -66,7 +67,9 @@ class NodeBench:
             "ARCHIVE_STORE_TYPE": "local", "ARCHIVE_BASE_PATH": str(self.tmp / "archives"),
             "DOCUMENT_STORE_TYPE": "inmemory", "MESSAGE_BUS_TYPE": "inproc",
         }
+        t0 = time.time()
         self.node = Node(env=self.env)
+        print(f"[bench-node] services and models built in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
         if index_prefill and hasattr(self.node.vectors, "add_embeddings"):
             # the same 1M-vector resident index the bench pipeline searches next to (rows of other lists)
             g = torch.Generator(device=dev).manual_seed(seed + 99)
@@ -76,6 +79,7 @@ class NodeBench:
                 v = torch.randn(n, dim, device=dev, generator=g)
                 self.node.vectors.add_embeddings([f"prefill-{s + i}" for i in range(n)], v, [{} for _ in range(n)])
         self.node.start(threaded=True)
+        print(f"[bench-node] node running ({time.time() - t0:.1f}s)", file=sys.stderr, flush=True)
         self.ingestion = self.node.services["ingestion"]
         self.store = self.node.store
         self.generator = SyntheticArchive(seed=seed)
@@ -106,7 +110,13 @@ class NodeBench:
         out: list[NodeStepResult] = []
         deadline = time.time() + timeout_s
         pending = list(steps)
+        last_note = time.time()
         while pending:
+            if time.time() - last_note > 15:      # a visible heartbeat of the pipeline's progress
+                last_note = time.time()
+                c = {k: self.store.count_documents(k, {}) for k in ("messages", "threads", "chunks", "summaries")}
+                c["embedded"] = self.store.count_documents("chunks", {"embedding_generated": True})
+                print(f"[bench-node] waiting on step {pending[0]}: {c}", file=sys.stderr, flush=True)
             if time.time() > deadline:
                 raise TimeoutError(f"node bench: steps {pending} unfinished after {timeout_s}s")
             s = pending[0]

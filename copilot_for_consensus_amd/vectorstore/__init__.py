@@ -255,6 +255,8 @@ class HipFlatIndex(VectorStore):
 
     def compact(self) -> None:
         with self._lock:
+            if self._dead == 0:
+                return
             keep = [r for r in range(self._n) if self._ids[r] is not None]
             idx = torch.tensor(keep, dtype=torch.long, device=self.device)
             n = len(keep)

@@ -148,70 +148,57 @@ __global__ void __launch_bounds__(256) topk_chunk_kernel(const float* __restrict
 // ------------------------------------------------------------------ fused scan + top-k
 constexpr int KT_ROWS = 1024;   // rows per workgroup chunk (scores [nqb][KT_ROWS] fp32 in LDS)
 
-// Wave-level exact top-k of sc[0..len) (LDS) by 4 passes of 8-bit radix select over the
-// order-preserving keys; writes exactly k slots (ov/oi; -inf / -1 padding when len < k).
-// hist: this wave's 256-entry LDS histogram.
-__device__ void wave_topk(const float* sc, int len, int k, int64_t row0, const int64_t* ids, float* ov, int64_t* oi,
-                          uint32_t* hist) {
+// Wave-level exact top-k of sc[0..len) (LDS, len <= KT_ROWS): every lane holds 16 keys in
+// registers (row lane + 64 j); the k-th largest key is found bit by bit, MSB first, from wave-wide
+// counts of keys >= the candidate (32 rounds of 16 compares + a butterfly sum) -- no LDS atomics:
+// a radix histogram serialises here because the scores of one chunk share their top key bytes.
+// Writes exactly k slots (ov/oi; -inf / -1 padding when len < k).
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ void wave_topk(const float* sc, int len, int k, int64_t row0, const int64_t* ids, float* ov, int64_t* oi,
+                          uint32_t* /*unused*/) {
   const int lane = threadIdx.x & 63;
   const int kk = min(k, len);
-  uint32_t prefix = 0, mask = 0, need = (uint32_t)kk;
-  for (int shift = 24; shift >= 0 && kk > 0; shift -= 8) {
+  uint32_t key[KT_ROWS / 64];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) hist[4 * lane + j] = 0;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    for (int i = lane; i < len; i += 64) {
-      const uint32_t key = f2key(sc[i]);
-      if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // lane l owns digits 255-4l .. 252-4l (descending); inclusive prefix over lanes finds the digit
-    uint32_t c[4], tot = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { c[j] = hist[255 - 4 * lane - j]; tot += c[j]; }
-    uint32_t inc = tot;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t v = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += v;
-    }
-    const uint32_t exc = inc - tot;
-    const uint64_t hit = __ballot(exc < need && inc >= need);
-    const int owner = __ffsll((unsigned long long)hit) - 1;
-    uint32_t d = 0, acc_before = 0;
-    if (lane == owner) {
-      uint32_t a = exc;
-      int j = 0;
-      for (; j < 3; ++j) {
-        if (a + c[j] >= need) break;
-        a += c[j];
-      }
-      d = 255 - 4 * lane - j;
-      acc_before = a;
-    }
-    d = __shfl(d, owner, 64);
-    acc_before = __shfl(acc_before, owner, 64);
-    need -= acc_before;
-    prefix |= d << shift;
-    mask |= 255u << shift;
+  for (int j = 0; j < KT_ROWS / 64; ++j) {
+    const int i = lane + 64 * j;
+    key[j] = i < len ? f2key(sc[i]) : 0u;
   }
-  const uint32_t thr = prefix;
-  const uint32_t n_gt = (uint32_t)kk - need;
+  uint32_t thr = 0;
+  if (kk > 0) {
+    for (int b = 31; b >= 0; --b) {
+      const uint32_t cand = thr | (1u << b);
+      int c = 0;
+#pragma unroll
+      for (int j = 0; j < KT_ROWS / 64; ++j) c += key[j] >= cand;
+      if (wave_sum_i(c) >= kk) thr = cand;     // wave-uniform decision
+    }
+  }
+  int gt = 0;
+#pragma unroll
+  for (int j = 0; j < KT_ROWS / 64; ++j) gt += key[j] > thr;
+  const uint32_t n_gt = (uint32_t)wave_sum_i(gt);
+  const uint32_t need = (uint32_t)kk - n_gt;   // keys == thr to take (>= 1 when kk > 0)
   uint32_t base_gt = 0, base_eq = 0;
-  for (int i0 = 0; i0 < len && kk > 0; i0 += 64) {
-    const int i = i0 + lane;
-    const uint32_t key = i < len ? f2key(sc[i]) : 0u;
-    const bool gt = i < len && key > thr, eq = i < len && key == thr;
-    const uint64_t bg = __ballot(gt), be = __ballot(eq);
-    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+  for (int j = 0; j < KT_ROWS / 64; ++j) {
+    const int i = lane + 64 * j;
+    const bool g = kk > 0 && i < len && key[j] > thr, e = kk > 0 && i < len && key[j] == thr;
+    const uint64_t bg = __ballot(g), be = __ballot(e);
     int slot = -1;
-    if (gt) slot = (int)(base_gt + __popcll(bg & below));
-    else if (eq) {
-      const uint32_t e = base_eq + __popcll(be & below);
-      if (e < need) slot = (int)(n_gt + e);
+    if (g) slot = (int)(base_gt + __popcll(bg & below));
+    else if (e) {
+      const uint32_t q = base_eq + __popcll(be & below);
+      if (q < need) slot = (int)(n_gt + q);
     }
     if (slot >= 0) {
-      ov[slot] = key2f(key);
+      ov[slot] = key2f(key[j]);
       oi[slot] = ids ? ids[row0 + i] : row0 + i;
     }
     base_gt += __popcll(bg);
