@@ -545,9 +545,15 @@ class DecoderModel:
         for i in range(cfg.layers):
             lw = w.layers[i]
             pw = w.packed[i] if w.packed is not None else lw    # fragment-packed copies when present
-            qkv = K.dgemm_linear(h, pw["qkv"])
-            q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
-                                cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
+            wq = pw["qkv"]
+            qbn, qsplit = K.dgemm_config(B, wq.shape[0], h.shape[1], bn=getattr(wq, "bn", None))
+            if qsplit > 1:   # split-K slabs straight into RoPE / KV write (the reduce folded in)
+                q = K.rope_kv_write_part(K.dgemm(h, wq, "part", qsplit, bn=qbn), positions, slots, w.cos_sin,
+                                         kv.k[i], kv.v[i], w.heads, w.kv_heads, cfg.head_dim, k_scale=kv.k_scale,
+                                         v_scale=kv.v_scale)
+            else:
+                q = K.rope_kv_write(K.dgemm_linear(h, wq), positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads,
+                                    w.kv_heads, cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
             attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
                                             part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
                                             k_scale=kv.k_scale, v_scale=kv.v_scale)

@@ -111,6 +111,26 @@ def _fp8(cache) -> bool:
     return cache.dtype == torch.float8_e4m3fn
 
 
+def rope_kv_write_part(part, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D, k_scale=1.0, v_scale=1.0):
+    """Decode RoPE + K/V write reading the qkv projection's fp32 split-K slabs ``part``
+    [split, T, (Hq + 2 Hkv) D] directly (the split-K reduce folded in; same bf16 values)."""
+    split, T, N = part.shape
+    if not part.is_cuda:
+        qkv = part.sum(0).to(torch.bfloat16)
+        return rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D, k_scale=k_scale,
+                             v_scale=v_scale)
+    if N != (Hq + 2 * Hkv) * D or part.dtype != torch.float32 or not part.is_contiguous():
+        raise ValueError(f"rope_kv_write_part: part {tuple(part.shape)} {part.dtype}")
+    _req(positions, torch.int32, "positions")
+    _req(slots, torch.int32, "slots")
+    q_out = torch.empty(T, Hq, D, dtype=torch.bfloat16, device=part.device)
+    check(kernels().cfc_rope_kv_write_part(part.data_ptr(), split, positions.data_ptr(), slots.data_ptr(),
+                                           cos_sin.data_ptr(), q_out.data_ptr(), k_cache.data_ptr(),
+                                           v_cache.data_ptr(), T, Hq, Hkv, D, int(_fp8(k_cache)), 1.0 / k_scale,
+                                           1.0 / v_scale, _stream(part)), "cfc_rope_kv_write_part")
+    return q_out
+
+
 def rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D, q_out=None, runs=None,
                   k_scale=1.0, v_scale=1.0):
     """RoPE on q/k + paged K/V cache write.  ``runs`` (device int32 [R, 4] from :func:`v_runs`):

@@ -20,12 +20,33 @@ __device__ __forceinline__ int v_slot(int key_in_block) {
 
 // qkv: [T, (Hq + 2*Hkv) * D] (q heads | k heads | v heads), positions [T], slots [T] (-1 = skip
 // cache write), cos_sin [max_pos][D/2][2] fp32 (cos, sin interleaved).
+// 8 consecutive qkv values of token row `row_off` (element offset): from the bf16 qkv, or summed
+// from `split` fp32 split-K slabs of the decode GEMM (slab stride `slab` elements) and rounded to
+// bf16 -- the same values splitk_reduce would have written, without the round trip
+__device__ __forceinline__ void qkv_load8(const uint16_t* qkv, const float* part, int split, size_t slab, size_t off,
+                                          float* f) {
+  if (part == nullptr) {
+    unpack8(*reinterpret_cast<const uint4*>(qkv + off), f);
+    return;
+  }
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  for (int p = 0; p < split; ++p) {
+    const float4 x = *reinterpret_cast<const float4*>(part + p * slab + off);
+    const float4 y = *reinterpret_cast<const float4*>(part + p * slab + off + 4);
+    a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+    b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
+  }
+  f[0] = bf2f(f2bf(a.x)); f[1] = bf2f(f2bf(a.y)); f[2] = bf2f(f2bf(a.z)); f[3] = bf2f(f2bf(a.w));
+  f[4] = bf2f(f2bf(b.x)); f[5] = bf2f(f2bf(b.y)); f[6] = bf2f(f2bf(b.z)); f[7] = bf2f(f2bf(b.w));
+}
+
 template <bool F8>
 __global__ void __launch_bounds__(64) rope_kv_kernel(const uint16_t* __restrict__ qkv, const int32_t* __restrict__ positions,
                                                      const int32_t* __restrict__ slots, const float* __restrict__ cos_sin,
                                                      uint16_t* __restrict__ q_out, void* __restrict__ k_cache,
                                                      void* __restrict__ v_cache, int Hq, int Hkv, int D,
-                                                     int write_v, float inv_k, float inv_v) {
+                                                     int write_v, float inv_k, float inv_v,
+                                                     const float* __restrict__ part = nullptr, int split = 0) {
   // grid = (T, ceil(items / 64)): one 8-element item per thread -- (Hq + Hkv) * D/16 rotation
   // items then Hkv * D/8 V items -- so a decode batch of 128 tokens is ~900 blocks, not 128.
   // write_v = 0: V goes through v_cache_runs_kernel instead (prefill: whole blocks, 16-B stores).
@@ -37,7 +58,7 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const uint16_t* __restrict_
   const int it = blockIdx.y * 64 + threadIdx.x;
   if (it >= n_rot + n_v) return;
   const int stride = (Hq + 2 * Hkv) * D;
-  const uint16_t* row = qkv + (size_t)tok * stride;
+  const size_t row0 = (size_t)tok * stride, slab = (size_t)gridDim.x * stride;
   const int slot = slots[tok];
   if (it < n_rot) {
     const int head = it / nv, c = it - head * nv;  // head < Hq: query, else key (head - Hq)
@@ -48,10 +69,9 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const uint16_t* __restrict_
       const float4 t = cs[j];
       csv[4 * j] = t.x; csv[4 * j + 1] = t.y; csv[4 * j + 2] = t.z; csv[4 * j + 3] = t.w;
     }
-    const uint16_t* src = row + head * D;
     float a[8], b[8], ra[8], rb[8];
-    unpack8(*reinterpret_cast<const uint4*>(src + c * 8), a);
-    unpack8(*reinterpret_cast<const uint4*>(src + half + c * 8), b);
+    qkv_load8(qkv, part, split, slab, row0 + head * D + c * 8, a);
+    qkv_load8(qkv, part, split, slab, row0 + head * D + half + c * 8, b);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float cv = csv[2 * j], sv = csv[2 * j + 1];
@@ -85,7 +105,9 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const uint16_t* __restrict_
   } else if (slot >= 0) {
     const int v = it - n_rot;
     const int kh = v / (D / 8), c = v % (D / 8);
-    const uint4 val = *reinterpret_cast<const uint4*>(row + (Hq + Hkv + kh) * D + c * 8);
+    float vf[8];
+    qkv_load8(qkv, part, split, slab, row0 + (Hq + Hkv + kh) * D + c * 8, vf);
+    const uint4 val = pack8(vf);
     const int blk = slot / KV_BS, off = slot % KV_BS;
     const int sl = v_slot(off);
     const size_t e0 = (((size_t)blk * Hkv + kh) * D + c * 8) * KV_BS + sl;
@@ -775,5 +797,24 @@ CFC_API int cfc_decode_advance(const int32_t* next, int32_t* tokens, int max_new
   decode_advance_kernel<<<1, ((B + 63) / 64) * 64, 0, stream>>>(next, tokens, max_new, step_ptr, input_ids, positions,
                                                                ctx_lens, slots, block_tables, max_blocks, done,
                                                                stop_ids, n_stop, B, st);
+  return CFC_CHECK_LAUNCH();
+}
+
+// Decode: RoPE + K/V cache write straight from the qkv projection's fp32 split-K slabs
+// part [split][T][(Hq + 2 Hkv) D] (dgemm "part" epilogue) -- the reduce kernel folded in.
+CFC_API int cfc_rope_kv_write_part(const float* part, int split, const int32_t* positions, const int32_t* slots,
+                                   const float* cos_sin, void* q_out, void* k_cache, void* v_cache, int T, int Hq,
+                                   int Hkv, int head_dim, int fp8, float inv_k, float inv_v, hipStream_t stream) {
+  if (head_dim % 16 != 0 || T < 0 || split < 1 || part == nullptr) return -1;
+  if (T == 0) return 0;
+  const int items = (Hq + Hkv) * (head_dim / 16) + Hkv * (head_dim / 8);
+  if (fp8)
+    rope_kv_kernel<true><<<dim3(T, (items + 63) / 64), 64, 0, stream>>>(
+        nullptr, positions, slots, cos_sin, (uint16_t*)q_out, k_cache, v_cache, Hq, Hkv, head_dim, 1, inv_k, inv_v,
+        part, split);
+  else
+    rope_kv_kernel<false><<<dim3(T, (items + 63) / 64), 64, 0, stream>>>(
+        nullptr, positions, slots, cos_sin, (uint16_t*)q_out, k_cache, v_cache, Hq, Hkv, head_dim, 1, 1.f, 1.f,
+        part, split);
   return CFC_CHECK_LAUNCH();
 }

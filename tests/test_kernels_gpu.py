@@ -465,6 +465,25 @@ def test_pgemm_exact_and_strided_out():
     assert torch.equal(buf[:, N:], torch.zeros_like(buf[:, N:]))
 
 
+@pytest.mark.parametrize("split", [1, 3, 4])
+def test_rope_kv_write_from_splitk_slabs_matches_reduce_then_rope(split):
+    """rope_kv_write_part == splitk_reduce -> rope_kv_write, bit for bit (q, K cache, V cache)."""
+    Hq, Hkv, D, T, nblk = 8, 2, 128, 5, 4
+    N = (Hq + 2 * Hkv) * D
+    part = torch.randn(split, T, N, device=DEV)
+    cs = R.rope_cos_sin(256, D, 1e4, device=DEV)
+    pos = torch.tensor([0, 3, 17, 100, 255], dtype=torch.int32, device=DEV)
+    slots = torch.tensor([0, 5, 40, 63, 90], dtype=torch.int32, device=DEV)
+
+    def caches():
+        return (torch.zeros(nblk, Hkv, 32, D, device=DEV).bfloat16(), torch.zeros(nblk, Hkv, D, 32, device=DEV).bfloat16())
+    k1, v1 = caches()
+    q1 = K.rope_kv_write(K.splitk_reduce(part), pos, slots, cs, k1, v1, Hq, Hkv, D)
+    k2, v2 = caches()
+    q2 = K.rope_kv_write_part(part, pos, slots, cs, k2, v2, Hq, Hkv, D)
+    assert torch.equal(q1, q2) and torch.equal(k1, k2) and torch.equal(v1, v2)
+
+
 def test_dgemm_rejects_bad_shapes():
     x = torch.randn(8, 100, device=DEV).bfloat16()
     w = torch.randn(128, 100, device=DEV).bfloat16()
