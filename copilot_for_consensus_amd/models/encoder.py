@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 from pathlib import Path
 
 import torch
@@ -150,15 +151,31 @@ class EncoderModel:
         c = self.cfg
         x = K.embed_layernorm(ids, positions, self.p["word"], self.p["pos"], self.p["type"], self.p["emb_g"],
                               self.p["emb_b"], c.ln_eps)
+        lin = self._linear
         for lw in self.layers:
-            qkv = F.linear(x, lw["qkv"], lw["qkv_b"])
+            qkv = lin(x, lw["qkv"], "bias", lw["qkv_b"])
             a = K.encoder_attention(qkv, cu_seqlens, c.heads, c.head_dim, self.scale, max_seqlen, tiles=tiles)
-            o = F.linear(a.view(a.shape[0], -1), lw["o"])
+            o = lin(a.view(a.shape[0], -1), lw["o"])
             x = K.layernorm(o, lw["ln1_g"], lw["ln1_b"], c.ln_eps, bias=lw["o_b"], residual=x)
-            h = K.bias_gelu(F.linear(x, lw["up"]), lw["up_b"])
-            o2 = F.linear(h, lw["down"])
+            h = lin(x, lw["up"], "bias_gelu", lw["up_b"])
+            o2 = lin(h, lw["down"])
             x = K.layernorm(o2, lw["ln2_g"], lw["ln2_b"], c.ln_eps, bias=lw["down_b"], residual=x)
         return x
+
+    # projection GEMMs: the hand-written pgemm (csrc/kernels/pgemm.hip, bias / bias+GELU fused in
+    # its epilogue) where it measured at or above hipBLASLt -- the small-K (K <= 512) shapes of the
+    # MiniLM-class encoders (qkv 1.10x, o 1.06x, up+GELU 0.98x vs library GEMM + bias_gelu:
+    # profiles/r03_pgemm_v1_vs_hipblaslt.log); the library GEMM for K >= 768 (BGE-base).
+    # CFC_ENCODER_GEMM = auto | hip | lib.
+    PGEMM_MAX_K = 512
+
+    def _linear(self, x, w, epi: str = "bf16", bias=None):
+        mode = os.environ.get("CFC_ENCODER_GEMM", "auto")
+        use = x.is_cuda and K.pgemm_ok(x, w) and (mode == "hip" or (mode == "auto" and w.shape[1] <= self.PGEMM_MAX_K))
+        if use:
+            return K.pgemm(x, w, epi, bias=bias)
+        y = F.linear(x, w, bias if epi == "bias" else None)
+        return K.bias_gelu(y, bias) if epi == "bias_gelu" else y
 
     @torch.inference_mode()
     def encode_ids(self, batch: list[list[int]], pooling: str | None = None, normalize: bool | None = None,
