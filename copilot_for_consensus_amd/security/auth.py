@@ -399,8 +399,12 @@ class AuthService:
     """Login flow state machine + token minting + role administration."""
 
     def __init__(self, jwt_manager: JWTManager, role_store: RoleStore, providers: dict[str, IdentityProvider],
-                 require_pkce: bool = True, require_nonce: bool = True, state_ttl: int = 600):
+                 require_pkce: bool = True, require_nonce: bool = True, state_ttl: int = 600,
+                 max_session_seconds: int = 86400):
         self.jwt, self.roles, self.providers = jwt_manager, role_store, providers
+        # a refresh keeps the login's auth_time; past this lifetime the user must log in again at the
+        # provider (so a stolen token cannot be renewed forever and a revocation there takes effect)
+        self.max_session_seconds = int(max_session_seconds)
         self.require_pkce, self.require_nonce = require_pkce, require_nonce
         for p in providers.values():   # the nonce is checked inside OIDCProvider.exchange_code
             if isinstance(p, OIDCProvider):
@@ -431,7 +435,7 @@ class AuthService:
         doc = self.roles.ensure_user(user)
         token = self.jwt.mint_token(user["sub"], {"email": user.get("email"), "name": user.get("name"),
                                                   "roles": self.roles.roles(user["sub"]),
-                                                  "provider": user.get("provider")},
+                                                  "provider": user.get("provider"), "auth_time": int(time.time())},
                                     audience=st.get("audience"))
         return {"access_token": token, "token_type": "Bearer", "expires_in": self.jwt.default_expiry,
                 "user": {k: doc.get(k) for k in ("user_id", "email", "name", "roles", "status")}}
@@ -450,8 +454,14 @@ class AuthService:
         sub = claims.get("sub")
         if not isinstance(sub, str) or not sub:
             raise PermissionError("Missing or invalid 'sub' claim in token")
+        auth_time = claims.get("auth_time", claims.get("iat"))
+        if not isinstance(auth_time, (int, float)) or time.time() - auth_time > self.max_session_seconds:
+            raise PermissionError("session older than the maximum lifetime: log in again")
+        if self.roles.get(sub) is not None and self.roles.get(sub).get("status") == "denied":
+            raise PermissionError("user access has been denied")
         new = self.jwt.mint_token(sub, {k: claims.get(k) for k in ("email", "name", "provider")} |
-                                  {"roles": self.roles.roles(sub)}, audience=aud if isinstance(aud, str) else None)
+                                  {"roles": self.roles.roles(sub), "auth_time": int(auth_time)},
+                                  audience=aud if isinstance(aud, str) else None)
         return {"access_token": new, "token_type": "Bearer", "expires_in": self.jwt.default_expiry}
 
     def get_jwks(self) -> dict:

@@ -70,7 +70,8 @@ def main(argv=None) -> int:
                           RoleStore(store, cfg.role_store_collection,
                                     (cfg.auto_approve_roles or "").split(",") if cfg.auto_approve_enabled else [],
                                     cfg.first_user_auto_promotion_enabled), provs,
-                          require_pkce=cfg.require_pkce, require_nonce=cfg.require_nonce)
+                          require_pkce=cfg.require_pkce, require_nonce=cfg.require_nonce,
+                          max_session_seconds=cfg.max_session_seconds)
         uvicorn.run(create_auth_app(svc, cfg.cookie_secure), host=cfg.host, port=args.port or cfg.port)
         return 0
 

@@ -195,6 +195,20 @@ class DocumentStoreServer:
             self._wal = None
 
 
+_NON_IDEMPOTENT_OPERATORS = ("$inc", "$push", "$addToSet", "$pop", "$pull", "$mul")
+
+
+def _idempotent(op: str, args) -> bool:
+    """A write that is safe to re-send after a lost reply: clear_collection, and updates whose
+    patch only sets fields (plain values or $set / $unset) -- never $inc / $push & co."""
+    if op == "clear_collection":
+        return True
+    if op not in ("update_document", "update_many"):
+        return False
+    patch = args[-1] if args else None
+    return isinstance(patch, dict) and not any(k in _NON_IDEMPOTENT_OPERATORS for k in patch)
+
+
 class RemoteDocumentStore(DocumentStore):
     """Client of :class:`DocumentStoreServer` (``DOCUMENT_STORE_TYPE=cfcstore``)."""
 
@@ -238,9 +252,9 @@ class RemoteDocumentStore(DocumentStore):
                     if self._sock is not None:
                         self._sock.close()
                     self._sock = None
-                    if attempt or op in WRITE_OPS - {"update_document", "update_many", "clear_collection"}:
-                        # an insert / delete may have been applied before the connection broke:
-                        # surface the failure instead of guessing
+                    if attempt or (op in WRITE_OPS and not _idempotent(op, args)):
+                        # an insert / delete / counter update may have been applied before the
+                        # connection broke: surface the failure instead of applying it twice
                         raise DocumentStoreConnectionError(f"{op}: {e}") from e
         if not rep.get("ok"):
             raise _ERRORS.get(rep.get("error"), DocumentStoreError)(rep.get("message", "document store error"))

@@ -203,3 +203,15 @@ def test_qdrant_rest_rejects_path_traversal_names(qdrant_server, tmp_path):
     assert call("DELETE", "/collections/ok_name-1") == 200
     assert marker.exists() and not (tmp_path / "vs" / "ok_name-1").exists()
     assert sorted(app.state.collections) == []
+
+
+def test_docstore_client_retries_only_idempotent_writes():
+    """After a lost reply a plain field update is re-sent, a counter / array operator update is
+    not (it may already have been applied)."""
+    from copilot_for_consensus_amd.storage.server import _idempotent
+    assert _idempotent("update_document", ("c", "id", {"status": "done"}))
+    assert _idempotent("update_many", ("c", {"a": 1}, {"$set": {"b": 2}}))
+    assert _idempotent("clear_collection", ("c",))
+    assert not _idempotent("update_document", ("c", "id", {"$inc": {"attemptCount": 1}}))
+    assert not _idempotent("update_many", ("c", {}, {"$push": {"log": "x"}}))
+    assert not _idempotent("insert_document", ("c", {"_id": "x"}))

@@ -343,3 +343,22 @@ def test_rsa_crt_fault_is_caught():
     key.dp ^= 1 << 5          # simulate a faulty half-exponentiation
     with pytest.raises(J.JWTError, match="self-check"):
         key.sign(b"payload")
+
+
+def test_refresh_refuses_sessions_past_max_lifetime_and_denied_users():
+    import time as _t
+    store = InMemoryDocumentStore()
+    mgr = J.JWTManager(J.HMACSigner("k"))
+    svc = AuthService(mgr, RoleStore(store), {"mock": __import__(
+        "copilot_for_consensus_amd.security.auth", fromlist=["MockIdentityProvider"]).MockIdentityProvider()},
+        max_session_seconds=100)
+    st = svc.initiate_login("mock")["state"]
+    tok = svc.handle_callback("alice", st)["access_token"]
+    new = svc.refresh(tok)["access_token"]
+    assert J.decode_unverified(new)[1]["auth_time"] == J.decode_unverified(tok)[1]["auth_time"]   # kept, not reset
+    old = mgr.mint_token("mock:alice", {"auth_time": int(_t.time()) - 1000})
+    with pytest.raises(PermissionError, match="lifetime"):
+        svc.refresh(old)
+    svc.roles.deny("mock:alice")
+    with pytest.raises(PermissionError, match="denied"):
+        svc.refresh(tok)
