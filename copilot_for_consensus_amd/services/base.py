@@ -114,6 +114,18 @@ class BaseService:
             return dict(self.stats)
 
 
+def own_gpu_stream() -> None:
+    """Give the calling thread its own HIP stream (PyTorch's current stream is per thread): the
+    services of one node share the GPU, and on the default stream every service's kernels (an
+    embedding batch, the orchestrator's scoring) would queue behind the LLM's decode bursts."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.set_stream(torch.cuda.Stream())
+    except (ImportError, RuntimeError):
+        pass
+
+
 def create_app(service: BaseService, extra_routes: Callable | None = None, config_schema: dict | None = None,
                auth_dependency=None):
     """FastAPI app with the health/readiness/stats/config-schema routes every service exposes."""

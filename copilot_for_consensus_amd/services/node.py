@@ -23,6 +23,7 @@ from ..retry import RetryConfig
 from ..storage.document_store import create_document_store
 from ..summarization import create_llm_backend
 from ..vectorstore import create_vector_store
+from .base import own_gpu_stream
 from .ingestion import IngestionService
 from .processing import ChunkingService, EmbeddingService, OrchestratorService, ParsingService, SummarizationService
 from .reporting import ReportingService
@@ -136,7 +137,10 @@ class Node:
         if threaded:
             for name, s in self.services.items():
                 if s.subscriber is not None:
-                    t = threading.Thread(target=s.subscriber.start_consuming, name=f"{name}-consumer", daemon=True)
+                    def consume(sub=s.subscriber):
+                        own_gpu_stream()
+                        sub.start_consuming()
+                    t = threading.Thread(target=consume, name=f"{name}-consumer", daemon=True)
                     s.consumer_thread = t
                     t.start()
                     self._threads.append(t)

@@ -193,16 +193,65 @@ class EmbeddingService(BaseService):
     name = "embedding"
 
     def __init__(self, publisher, subscriber, document_store, embedding_provider, vector_store,
-                 max_retries: int = 3, retry_backoff_seconds: float = 5.0, **kw):
+                 max_retries: int = 3, retry_backoff_seconds: float = 5.0, max_batch_chunks: int = 4096,
+                 batch_wait_ms: int = 20, **kw):
         super().__init__(publisher, subscriber, document_store, **kw)
         self.embedder, self.vectors = embedding_provider, vector_store
         self.max_retries, self.backoff = max_retries, retry_backoff_seconds
+        # micro-batching (start_async): ChunksPrepared events of many messages -> one encoder batch
+        self.max_batch_chunks, self.batch_wait = int(max_batch_chunks), batch_wait_ms / 1000.0
+        self._queue: list[dict] = []
+        self._qlock = threading.Condition()
+        self._worker: threading.Thread | None = None
+        self._stop = False
 
     def subscriptions(self):
         return {"ChunksPrepared": self._on_chunks, "SourceDeletionRequested": self._on_delete}
 
     def _on_chunks(self, event):
+        if self._worker is not None:
+            with self._qlock:
+                self._queue.append(event)
+                self._qlock.notify()
+            return
         self.process_chunks(event["data"]["chunk_ids"])
+
+    def start_async(self) -> None:
+        """Batch ChunksPrepared events (<= max_batch_chunks chunks or batch_wait_ms) into one
+        encoder call on this service's own GPU stream; a failing batch is retried event by event
+        so one bad message fails alone."""
+        from .base import own_gpu_stream
+
+        def loop():
+            own_gpu_stream()
+            while not self._stop:
+                with self._qlock:
+                    if not self._queue:
+                        self._qlock.wait(0.1)
+                        continue
+                    deadline = time.time() + self.batch_wait
+                    while (sum(len(e["data"]["chunk_ids"]) for e in self._queue) < self.max_batch_chunks
+                           and time.time() < deadline):
+                        self._qlock.wait(max(0.0, deadline - time.time()))
+                    batch, n = [], 0
+                    while self._queue and (not batch or n + len(self._queue[0]["data"]["chunk_ids"])
+                                           <= self.max_batch_chunks):
+                        ev = self._queue.pop(0)
+                        batch.append(ev)
+                        n += len(ev["data"]["chunk_ids"])
+                try:
+                    self.process_chunks([c for ev in batch for c in ev["data"]["chunk_ids"]])
+                except Exception:  # noqa: BLE001 -- isolate: each event on its own, with the retry policy
+                    for ev in batch:
+                        try:
+                            self._wrap("ChunksPrepared", lambda e: self.process_chunks(e["data"]["chunk_ids"]))(ev)
+                        except Exception as e:  # noqa: BLE001 -- already reported by the wrapper
+                            self.log.error("embedding event failed", error=repr(e))
+        self._worker = threading.Thread(target=loop, name="embedding-batcher", daemon=True)
+        self._worker.start()
+
+    def stop_async(self) -> None:
+        self._stop = True
 
     def process_chunks(self, chunk_ids: list[str]) -> int:
         if not chunk_ids:
@@ -222,6 +271,11 @@ class EmbeddingService(BaseService):
                                     [{"thread_id": c["thread_id"], "message_id": c["message_id"],
                                       "message_doc_id": c["message_doc_id"], "chunk_index": c["chunk_index"]}
                                      for c in chunks])
+        if getattr(vecs, "is_cuda", False):
+            # the index rows are written on this thread's stream; readers (the orchestrator) use
+            # their own: the rows must be in HBM before the event that announces them
+            import torch
+            torch.cuda.current_stream(vecs.device).synchronize()
         self.store.update_many("chunks", {"_id": {"$in": [c["_id"] for c in chunks]}},
                                {"embedding_generated": True, "lastUpdated": _now()})
         self.metrics.increment("embedding_chunks_processed_total", len(chunks))

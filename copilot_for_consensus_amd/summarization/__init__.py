@@ -226,6 +226,8 @@ class HipLLMSummarizer(Summarizer):
                      int(1000 * (time.perf_counter() - t0))), None)
 
     def _serve(self) -> None:
+        from ..services.base import own_gpu_stream
+        own_gpu_stream()
         ce = self._ce
         while True:
             with self._cv:
