@@ -280,7 +280,9 @@ class ContinuousEngine:
             for t, v in zip(self._state(), saved):
                 t.copy_(v)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            # thread_local: other service threads keep launching / syncing their own streams while
+            # this step is captured (global mode would invalidate the capture)
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self._decode_step()
             for t, v in zip(self._state(), saved):
                 t.copy_(v)

@@ -231,7 +231,7 @@ class LLMEngine:
         for t, v in zip(st.tensors(), saved):
             t.copy_(v)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):   # other threads may use the GPU
             self._decode_step(st, part_blocks, temperature, seed)
         for t, v in zip(st.tensors(), saved):
             t.copy_(v)

@@ -150,15 +150,10 @@ constexpr int KT_ROWS = 1024;   // rows per workgroup chunk (scores [nqb][KT_ROW
 
 // Wave-level exact top-k of sc[0..len) (LDS, len <= KT_ROWS): every lane holds 16 keys in
 // registers (row lane + 64 j); the k-th largest key is found bit by bit, MSB first, from wave-wide
-// counts of keys >= the candidate (32 rounds of 16 compares + a butterfly sum) -- no LDS atomics:
-// a radix histogram serialises here because the scores of one chunk share their top key bytes.
+// counts of keys >= the candidate (32 rounds of 16 compare-ballot-popcounts, all in SGPRs/VALU) --
+// no LDS: a radix histogram's atomics serialise here because one chunk's scores share their top
+// key bytes, and a shuffle-tree sum pays an LDS round trip per level.
 // Writes exactly k slots (ov/oi; -inf / -1 padding when len < k).
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
 __device__ __forceinline__ void wave_topk(const float* sc, int len, int k, int64_t row0, const int64_t* ids, float* ov, int64_t* oi,
                           uint32_t* /*unused*/) {
   const int lane = threadIdx.x & 63;
@@ -175,14 +170,14 @@ __device__ __forceinline__ void wave_topk(const float* sc, int len, int k, int64
       const uint32_t cand = thr | (1u << b);
       int c = 0;
 #pragma unroll
-      for (int j = 0; j < KT_ROWS / 64; ++j) c += key[j] >= cand;
-      if (wave_sum_i(c) >= kk) thr = cand;     // wave-uniform decision
+      for (int j = 0; j < KT_ROWS / 64; ++j) c += __popcll(__ballot(key[j] >= cand));
+      if (c >= kk) thr = cand;                 // wave-uniform decision
     }
   }
   int gt = 0;
 #pragma unroll
-  for (int j = 0; j < KT_ROWS / 64; ++j) gt += key[j] > thr;
-  const uint32_t n_gt = (uint32_t)wave_sum_i(gt);
+  for (int j = 0; j < KT_ROWS / 64; ++j) gt += __popcll(__ballot(key[j] > thr));
+  const uint32_t n_gt = (uint32_t)gt;
   const uint32_t need = (uint32_t)kk - n_gt;   // keys == thr to take (>= 1 when kk > 0)
   uint32_t base_gt = 0, base_eq = 0;
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
