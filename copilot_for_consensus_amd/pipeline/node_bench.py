@@ -61,7 +61,7 @@ class NodeBench:
             "LLM_KV_CACHE_TOKENS": str(max(65536, threads_per_step * (4096 + max_new_tokens))),
             "SUMMARIZATION_CONTINUOUS_BATCHING": "true" if continuous else "false",
             "SUMMARIZATION_MAX_BATCH_THREADS": str(threads_per_step), "SUMMARIZATION_MIN_ADMIT": str(threads_per_step),
-            "SUMMARIZATION_ADMIT_WAIT_MS": "500",
+            "SUMMARIZATION_ADMIT_WAIT_MS": "3000",
             "ORCHESTRATOR_TOP_K": "5", "ORCHESTRATOR_CONTEXT_WINDOW_TOKENS": "2048",
             "INGESTION_STORAGE_PATH": str(self.tmp / "ingest"), "INGESTION_SCHEDULE_INTERVAL_SECONDS": "0",
             "ARCHIVE_STORE_TYPE": "local", "ARCHIVE_BASE_PATH": str(self.tmp / "archives"),

@@ -182,7 +182,9 @@ class ContinuousEngine:
             return
         idle = all(r is None for r in self.slot_req)
         waited = time.perf_counter() - self.queue[0].submitted_s
-        if not idle and len(self.queue) < min(self.min_admit, len(self.free)) and waited < self.max_wait_s:
+        # an idle engine waits too (up to max_wait_s for min_admit requests): admitting the first
+        # arrival alone would stagger every later admission into small prefills
+        if len(self.queue) < min(self.min_admit, len(self.free)) and waited < self.max_wait_s:
             return
         take: list[Request] = []
         budget = self.max_admit_tokens

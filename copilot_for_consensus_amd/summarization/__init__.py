@@ -253,6 +253,9 @@ class HipLLMSummarizer(Summarizer):
                 self._live.clear()
                 self._ce = ce = self._reset_continuous(ce)
                 continue
+            if not finished and all(x is None for x in ce.slot_req):
+                with self._cv:      # admission is waiting for more requests: do not spin on the GIL
+                    self._cv.wait(0.005)
             for r in finished:
                 item = self._live.pop(r.rid, None)
                 if item is not None:
