@@ -138,7 +138,14 @@ class NodeBench:
             pending.pop(0)
         return out
 
+    def engine_stats(self) -> dict:
+        """The summarizer's continuous-engine counters (admissions, decode steps, prefill / decode s)."""
+        llm = getattr(self.node.services.get("summarization"), "summarizer", None)
+        ce = getattr(llm, "_ce", None)
+        return dict(ce.stats) if ce is not None else {}
+
     def close(self) -> None:
+        print(f"[bench-node] continuous engine: {self.engine_stats()}", file=sys.stderr, flush=True)
         self.node.stop()
         import shutil
         shutil.rmtree(self.tmp, ignore_errors=True)

@@ -257,6 +257,7 @@ class ContinuousEngine:
             self.stop_state.set_slots(slots, sstates)
         self.tokens.index_copy_(0, idx, torch.nn.functional.pad(rows_t[:, :1], (0, self.cap - 1)))
         self.stats["admitted"] += len(take)
+        self.stats["admissions"] = self.stats.get("admissions", 0) + 1
 
     def _decode_step(self) -> None:
         hidden = self.model.forward_decode(self.ids, self.positions, self.slots, self.ctx_lens, self.block_tables,
