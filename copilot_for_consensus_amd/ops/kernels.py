@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 
 import torch
 
@@ -517,12 +518,18 @@ def pgemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
             and w.shape[0] % 64 == 0 and x.shape[0] >= 1 and x.numel() * 2 < 2 ** 32 and w.numel() * 2 < 2 ** 32)
 
 
+PGEMM_VARIANTS = {"ring5": 0, "stage2": 1, "ring4": 2}
+PGEMM_VARIANT = os.environ.get("CFC_PGEMM_VARIANT", "ring5")
+
+
 def pgemm(x: torch.Tensor, w: torch.Tensor, epi: str = "bf16", bias: torch.Tensor | None = None,
-          out: torch.Tensor | None = None) -> torch.Tensor:
+          out: torch.Tensor | None = None, variant: str | None = None) -> torch.Tensor:
     """Hand-written MFMA GEMM for prefill / encoder shapes: x [M, K] @ w[N, K]^T with the following
     elementwise op fused into the epilogue.  ``epi``: "bf16"; "bias" (+ bias[N]); "bias_gelu"
     (gelu_erf(y + bias)); "swiglu" (8-row interleaved gate/up weights -> [M, N/2] =
-    silu(gate) * up with the unfused path's bf16 rounding of gate and up)."""
+    silu(gate) * up with the unfused path's bf16 rounding of gate and up).  ``variant``: the K
+    loop ("ring5" default: BK=32 ring of 5 LDS slots; "ring4"; "stage2": the 2-stage BK=64
+    kernel), $CFC_PGEMM_VARIANT when None."""
     mode = PGEMM_EPI[epi]
     if not x.is_cuda:
         y = torch.nn.functional.linear(x.float(), w.float())
@@ -544,7 +551,8 @@ def pgemm(x: torch.Tensor, w: torch.Tensor, epi: str = "bf16", bias: torch.Tenso
     if out is None:
         out = torch.empty(M, N // 2 if mode == 3 else N, dtype=torch.bfloat16, device=x.device)
     check(kernels().cfc_pgemm(x.data_ptr(), w.data_ptr(), bias.data_ptr() if bias is not None else None,
-                              out.data_ptr(), M, N, Kd, mode, out.stride(0), _stream(x)), "cfc_pgemm")
+                              out.data_ptr(), M, N, Kd, mode | (PGEMM_VARIANTS[variant or PGEMM_VARIANT] << 4),
+                              out.stride(0), _stream(x)), "cfc_pgemm")
     return out
 
 

@@ -56,6 +56,57 @@ __device__ __forceinline__ float pg_gelu(float v) { return 0.5f * v * (1.f + erf
 
 __device__ __forceinline__ float pg_bfr(float v) { return bf2f(f2bf(v)); }
 
+// Epilogue of both kernels: lane holds rows m = mw + 16 i + (lane & 15), columns
+// n = nw + 16 j + 4 (lane >> 4) + 0..3 of the wave's 128 x 64 block.
+template <int EPI>
+__device__ __forceinline__ void pg_epilogue(const f32x4_t (&acc)[8][4], const uint16_t* __restrict__ bias,
+                                            uint16_t* __restrict__ out, int M, int N, int ldo, int mw, int nw) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = mw + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int nb = nw + j * 16;   // n-tile base
+      const int n = nb + 4 * g;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if constexpr (EPI == PG_SWIGLU) {
+        // 16-row n-tile = 8 gate rows then 8 up rows: groups 0,1 hold gate cols 0..7, groups 2,3
+        // the matching up cols; bf16 rounding of g and u as the unfused GEMM -> silu_mul path
+        float u[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) u[e] = __shfl_xor(v[e], 32, 64);
+        if (g < 2 && m < M && nb < N) {
+          float y[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float gg = pg_bfr(v[e]);
+            y[e] = gg / (1.f + __expf(-gg)) * pg_bfr(u[e]);
+          }
+          *reinterpret_cast<uint2*>(out + (size_t)m * ldo + nb / 2 + 4 * g) =
+              make_uint2(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]));
+        }
+      } else {
+        if (m < M && n < N) {
+          if constexpr (EPI == PG_BIAS || EPI == PG_BIAS_GELU) {
+            const uint2 bb = *reinterpret_cast<const uint2*>(bias + n);
+            v[0] += __uint_as_float(bb.x << 16);
+            v[1] += __uint_as_float(bb.x & 0xffff0000u);
+            v[2] += __uint_as_float(bb.y << 16);
+            v[3] += __uint_as_float(bb.y & 0xffff0000u);
+          }
+          if constexpr (EPI == PG_BIAS_GELU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = pg_gelu(v[e]);
+          }
+          *reinterpret_cast<uint2*>(out + (size_t)m * ldo + n) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+        }
+      }
+    }
+  }
+}
+
 template <int EPI>
 __global__ void __launch_bounds__(512, 1)
     pgemm_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W, const uint16_t* __restrict__ bias,
@@ -128,75 +179,181 @@ __global__ void __launch_bounds__(512, 1)
     }
   }
 
-  // ---- epilogue: lane holds rows m = .. + (lane & 15), columns n = .. + 4 (lane >> 4) + 0..3
-  const int g = lane >> 4;
+  pg_epilogue<EPI>(acc, bias, out, M, N, ldo, m0 + wr * 128, n0 + wc * 64);
+}
+
+
+// ---- v2: BK = 32 ring of R LDS slots ------------------------------------------------------------
+// Same tile, waves and epilogue as pgemm_kernel; the K loop is a ring instead of a 2-stage double
+// buffer.  A slot is one 32-deep K step of both operands: A image then B image, 256 rows x 64 B
+// each (32 KB).  Step t's MFMAs run on fragments read from LDS during step t - 1, so the LDS reads
+// of step t + 1 overlap them.  At the top of step t each wave waits (counted vmcnt) for ITS DMA of
+// step t + 1 with the later steps left in flight and retires its ds_reads of step t (lgkmcnt(0));
+// then one raw barrier: step t + 1 is readable everywhere and step t's slot (in registers in every
+// wave) is free, so the DMA of step t + R goes into it right away.  A slot's DMA thus has R - 1
+// steps of MFMA work (~1k cycles per step per SIMD pair) to land, against one 64-deep tile in the
+// 2-stage kernel: what that kernel waits for at its vmcnt(0) (guide "Pipelining across barriers").
+//
+// 64-B image rows: 4 rows share a 256-B bank row, so the 16-row fragment read (lane: row
+// lane & 15, chunk lane >> 4) is swizzled as chunk' = chunk ^ f((row >> 2) & 3), f = 0,3,2,1: every
+// ds_read_b128 lane group then covers the 16 bank slots of one bank row exactly once.  The DMA
+// writes lane-linear (16-row x 64-B piece per wave instruction), so the swizzle goes on its source
+// chunk (guide rule 21).
+constexpr int PR_BK = 32;
+constexpr int PR_SLOT = (PG_BM + PG_BN) * PR_BK * 2;   // 32 KB
+
+__device__ __forceinline__ int pr_f(int x) { return (4 - x) & 3; }
+
+template <int EPI, int R>
+__global__ void __launch_bounds__(512, 1)
+    pgemm_ring_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W,
+                      const uint16_t* __restrict__ bias, uint16_t* __restrict__ out, int M, int N, int K, int ldo,
+                      int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem[R * PR_SLOT];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 2, wc = w & 3;
+
+  const int nwg = tiles_m * tiles_n;
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int per_group = PG_GROUP_M * tiles_n;
+  const int first_m = (id / per_group) * PG_GROUP_M;
+  const int gsz = min(tiles_m - first_m, PG_GROUP_M);
+  const int in_group = id % per_group;
+  const int m0 = (first_m + in_group % gsz) * PG_BM;
+  const int n0 = (in_group / gsz) * PG_BN;
+
+  // ---- DMA: wave w moves pieces w and w + 8 of A (image rows 16 p .. 16 p + 15) and of B;
+  // lane l lands at row l >> 2, slot chunk l & 3 of its piece
+  const int prow = lane >> 2, pch = (lane & 3) ^ pr_f((prow >> 2) & 3);
+  uint32_t va[2], vb[2];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wr * 128 + i * 16 + (lane & 15);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int nb = n0 + wc * 64 + j * 16;   // n-tile base
-      const int n = nb + 4 * g;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if constexpr (EPI == PG_SWIGLU) {
-        // 16-row n-tile = 8 gate rows then 8 up rows: groups 0,1 hold gate cols 0..7, groups 2,3
-        // the matching up cols; bf16 rounding of g and u as the unfused GEMM -> silu_mul path
-        float u[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) u[e] = __shfl_xor(v[e], 32, 64);
-        if (g < 2 && m < M && nb < N) {
-          float y[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float gg = pg_bfr(v[e]);
-            y[e] = gg / (1.f + __expf(-gg)) * pg_bfr(u[e]);
-          }
-          *reinterpret_cast<uint2*>(out + (size_t)m * ldo + nb / 2 + 4 * g) =
-              make_uint2(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]));
-        }
-      } else {
-        if (m < M && n < N) {
-          if constexpr (EPI == PG_BIAS || EPI == PG_BIAS_GELU) {
-            const uint2 bb = *reinterpret_cast<const uint2*>(bias + n);
-            v[0] += __uint_as_float(bb.x << 16);
-            v[1] += __uint_as_float(bb.x & 0xffff0000u);
-            v[2] += __uint_as_float(bb.y << 16);
-            v[3] += __uint_as_float(bb.y & 0xffff0000u);
-          }
-          if constexpr (EPI == PG_BIAS_GELU) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = pg_gelu(v[e]);
-          }
-          *reinterpret_cast<uint2*>(out + (size_t)m * ldo + n) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
-        }
-      }
-    }
+  for (int i = 0; i < 2; ++i) {
+    const int r = 16 * (w + 8 * i) + prow;
+    va[i] = ((uint32_t)min(m0 + r, M - 1) * (uint32_t)K + 8u * pch) * 2u;
+    vb[i] = ((uint32_t)min(n0 + r, N - 1) * (uint32_t)K + 8u * pch) * 2u;
   }
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(pg_lds_t*)smem + w * 1024);
+  auto issue = [&](int t, int s) {
+    const uint16_t* xa = X + (size_t)t * PR_BK;
+    const uint16_t* wb = W + (size_t)t * PR_BK;
+    const uint32_t la = lds0 + s * PR_SLOT;
+    pg_glds16(va[0], xa, la);
+    pg_glds16(va[1], xa, la + 8192);
+    pg_glds16(vb[0], wb, la + PG_BM * 64);
+    pg_glds16(vb[1], wb, la + PG_BM * 64 + 8192);
+  };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int frow = (lane & 15) * 64;
+  const int ch = ((lane >> 4) ^ pr_f(((lane & 15) >> 2) & 3)) << 4;
+  const char* ra = smem + wr * 128 * 64 + frow + ch;
+  const char* rb = smem + PG_BM * 64 + wc * 64 * 64 + frow + ch;
+  const int nk = K / PR_BK;
+  // Fragments of step t are read from LDS during step t - 1's MFMAs.  B (4 fragments) is
+  // double-buffered and read first; A fragment i is re-read in place right after its last MFMA of
+  // the step (sched_barrier pins each read there: hoisted, the reads would double the live
+  // fragments and spill).  The reads of the last step's "next" fragments touch a slot nobody
+  // writes any more and are never used (branch-free MFMA stream).
+  bf16x8_t af[8], bq[2][4];
+  auto rd_a = [&](int s, int i) { return *reinterpret_cast<const bf16x8_t*>(ra + s * PR_SLOT + i * 16 * 64); };
+  auto rd_b = [&](int s, int j) { return *reinterpret_cast<const bf16x8_t*>(rb + s * PR_SLOT + j * 16 * 64); };
+  // Wait (own DMAs) for step t + 1 with the steps after it left in flight, retire this wave's
+  // ds_reads, then the barrier: step t + 1 readable everywhere, slot of step t free.
+  auto sync_next = [&](int t) {
+    const int ahead = min(nk - 2 - t, R - 2);
+    if (ahead >= 3)
+      asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (ahead == 2)
+      asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (ahead == 1)
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+#define PR_STEP(T, S, S1, BC, BN)                                                                         \
+  do {                                                                                                   \
+    if ((T) + 1 < nk) {                                                                                  \
+      sync_next(T);                                                                                      \
+      if ((T) + R < nk) issue((T) + R, S);                                                               \
+    }                                                                                                    \
+    _Pragma("unroll") for (int j = 0; j < 4; ++j) BN[j] = rd_b(S1, j);                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                                   \
+    __builtin_amdgcn_s_setprio(1);                                                                       \
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                                      \
+      _Pragma("unroll") for (int j = 0; j < 4; ++j) acc[i][j] =                                          \
+          __builtin_amdgcn_mfma_f32_16x16x32_bf16(BC[j], af[i], acc[i][j], 0, 0, 0);                     \
+      af[i] = rd_a(S1, i);                                                                               \
+      __builtin_amdgcn_sched_barrier(0);                                                                 \
+    }                                                                                                    \
+    __builtin_amdgcn_s_setprio(0);                                                                       \
+  } while (0)
+  for (int t = 0; t < R && t < nk; ++t) issue(t, t);
+  {
+    const int ahead = min(nk - 1, R - 1);   // step 0 landed, steps 1 .. ahead in flight
+    if (ahead >= 4)
+      asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+    else if (ahead == 3)
+      asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+    else if (ahead == 2)
+      asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+    else if (ahead == 1)
+      asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bq[0][j] = rd_b(0, j);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) af[i] = rd_a(0, i);
+  int s = 0;   // ring slot of step t
+  for (int t = 0; t < nk; t += 2) {
+    const int s1 = (s == R - 1) ? 0 : s + 1;
+    const int s2 = (s1 == R - 1) ? 0 : s1 + 1;
+    PR_STEP(t, s, s1, bq[0], bq[1]);
+    PR_STEP(t + 1, s1, s2, bq[1], bq[0]);   // nk is even (K % 64 == 0)
+    s = s2;
+  }
+#undef PR_STEP
+  pg_epilogue<EPI>(acc, bias, out, M, N, ldo, m0 + wr * 128, n0 + wc * 64);
 }
 
 template <int EPI>
 int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int M, int N, int K, int ldo,
-                 hipStream_t stream) {
+                 int variant, hipStream_t stream) {
   const int tm = (M + PG_BM - 1) / PG_BM, tn = (N + PG_BN - 1) / PG_BN;
-  pgemm_kernel<EPI><<<tm * tn, 512, 0, stream>>>((const uint16_t*)x, (const uint16_t*)w, (const uint16_t*)bias,
-                                                 (uint16_t*)out, M, N, K, ldo, tm, tn);
+  const uint16_t *xp = (const uint16_t*)x, *wp = (const uint16_t*)w, *bp = (const uint16_t*)bias;
+  uint16_t* op = (uint16_t*)out;
+  switch (variant) {
+    case 0: pgemm_ring_kernel<EPI, 5><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn); break;
+    case 1: pgemm_kernel<EPI><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn); break;
+    case 2: pgemm_ring_kernel<EPI, 4><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn); break;
+    default: return (int)hipErrorInvalidValue;
+  }
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
-// epi: 0 bf16, 1 + bias, 2 + bias -> GELU, 3 SwiGLU (out [M, N/2]); ldo = output row stride.
-CFC_API int cfc_pgemm(const void* x, const void* w, const void* bias, void* out, int M, int N, int K, int epi,
+// epi & 15: 0 bf16, 1 + bias, 2 + bias -> GELU, 3 SwiGLU (out [M, N/2]); epi >> 4: kernel variant
+// (0 ring of 5 slots -- the default, 1 the 2-stage kernel, 2 ring of 4 slots); ldo = output row stride.
+CFC_API int cfc_pgemm(const void* x, const void* w, const void* bias, void* out, int M, int N, int K, int epi_v,
                       int ldo, hipStream_t stream) {
+  const int epi = epi_v & 15, variant = epi_v >> 4;
   if (M < 1 || N < 64 || K < 64 || K % 64 || N % 64 || ldo % 4 || (epi != 3 && ldo < N) ||
       (epi == 3 && ldo < N / 2) || (uint64_t)M * K * 2 >= (1ull << 32) || (uint64_t)N * K * 2 >= (1ull << 32) ||
       ((epi == 1 || epi == 2) && bias == nullptr))
     return (int)hipErrorInvalidValue;
   switch (epi) {
-    case 0: return pgemm_launch<PG_BF16>(x, w, bias, out, M, N, K, ldo, stream);
-    case 1: return pgemm_launch<PG_BIAS>(x, w, bias, out, M, N, K, ldo, stream);
-    case 2: return pgemm_launch<PG_BIAS_GELU>(x, w, bias, out, M, N, K, ldo, stream);
-    case 3: return pgemm_launch<PG_SWIGLU>(x, w, bias, out, M, N, K, ldo, stream);
+    case 0: return pgemm_launch<PG_BF16>(x, w, bias, out, M, N, K, ldo, variant, stream);
+    case 1: return pgemm_launch<PG_BIAS>(x, w, bias, out, M, N, K, ldo, variant, stream);
+    case 2: return pgemm_launch<PG_BIAS_GELU>(x, w, bias, out, M, N, K, ldo, variant, stream);
+    case 3: return pgemm_launch<PG_SWIGLU>(x, w, bias, out, M, N, K, ldo, variant, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }

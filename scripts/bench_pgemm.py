@@ -2,7 +2,7 @@
 """Prefill / encoder GEMM (csrc/kernels/pgemm.hip) vs the library path on the headline's shapes.
 
 numerics against an fp32 reference, then hipGraph timing (median of 5 replays of 8 calls) of:
-  pg_*   the hand-written kernel with its fused epilogue;
+  <variant>_*   the hand-written kernel (each K-loop variant) with its fused epilogue;
   lib_*  F.linear (hipBLASLt, TunableOp table when present) + the separate elementwise kernel.
 Random [-1, 1)-scale operands (guide §5.4 rule 25: never zero-filled).
 Writes one JSON line per shape to gpurun_out/pgemm.jsonl.
@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--shapes", nargs="*", default=list(SHAPES))
     ap.add_argument("--m", type=int, default=None, help="override M")
     ap.add_argument("--out", default="gpurun_out/pgemm.jsonl")
+    ap.add_argument("--variants", nargs="*", default=["ring5", "ring4", "stage2"])
+    ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
     enable_tuned_gemms()
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
@@ -82,9 +84,8 @@ def main():
         w = ((torch.rand(N, Kd, device="cuda") * 2 - 1) / Kd ** 0.5).bfloat16()
         b = (torch.rand(N, device="cuda") * 0.2 - 0.1).bfloat16()
         row = {"shape": name, "M": M, "N": N, "K": Kd, "epi": epi}
-        # numerics on the first 512 rows (fp32 reference of the same op)
+        # numerics on the first 512 rows (fp32 reference of the same op), every variant
         xs = x[:512].contiguous()
-        y = K.pgemm(xs, w, epi, bias=b)
         ref = xs.float() @ w.float().t()
         if epi in ("bias", "bias_gelu"):
             ref = ref + b.float()
@@ -92,13 +93,28 @@ def main():
             ref = F.gelu(ref)
         if epi == "swiglu":
             ref = R.silu_mul_interleaved(ref.bfloat16()).float()
-        row["err"] = rel_err(y, ref)
         flops = 2.0 * M * N * Kd
-        t_pg = timed(lambda: K.pgemm(x, w, epi, bias=b))
-        t_lib = timed(lib_fn(x, w, b, epi))
-        row.update(pg_us=round(t_pg * 1e6, 1), lib_us=round(t_lib * 1e6, 1),
-                   pg_TFs=round(flops / t_pg / 1e12, 1), lib_TFs=round(flops / t_lib / 1e12, 1),
-                   speedup=round(t_lib / t_pg, 3))
+        fns = {"lib": lib_fn(x, w, b, epi)}
+        for v in args.variants:
+            row[f"err_{v}"] = rel_err(K.pgemm(xs, w, epi, bias=b, variant=v), ref)
+            fns[v] = (lambda v=v: K.pgemm(x, w, epi, bias=b, variant=v))
+        # whole-matrix agreement of each variant with the 2-stage kernel (same fp32 sums per tile)
+        y0 = K.pgemm(x, w, epi, bias=b, variant="stage2")
+        for v in args.variants:
+            if v != "stage2":
+                row[f"maxdiff_{v}_vs_stage2"] = float((K.pgemm(x, w, epi, bias=b, variant=v).float() - y0.float()).abs().max())
+        del y0
+        ts = {k: [] for k in fns}
+        for _ in range(args.rounds):          # interleaved rounds in one process (guide rule 24)
+            for k, fn in fns.items():
+                ts[k].append(timed(fn))
+        for k, v in ts.items():
+            t = sorted(v)[len(v) // 2]
+            row[f"{k}_us"] = round(t * 1e6, 1)
+            row[f"{k}_TFs"] = round(flops / t / 1e12, 1)
+        best = min(args.variants, key=lambda v: row[f"{v}_us"])
+        row["best"] = best
+        row["speedup_best_vs_lib"] = round(row["lib_us"] / row[f"{best}_us"], 3)
         print(json.dumps(row), flush=True)
         fh.write(json.dumps(row) + "\n")
         fh.flush()

@@ -432,8 +432,9 @@ def test_dgemm_packed_swiglu_and_norm(M, split):
 
 @pytest.mark.parametrize("M,N,Kd,epi", [(512, 512, 256, "bf16"), (300, 1152, 384, "bias"), (257, 1536, 384, "bias_gelu"),
                                        (1000, 768, 1536, "bf16"), (129, 2048, 512, "swiglu"), (64, 320, 128, "bf16"),
-                                       (2048, 4096, 1024, "bf16")])
-def test_pgemm(M, N, Kd, epi):
+                                       (2048, 4096, 1024, "bf16"), (513, 640, 4096, "swiglu")])
+@pytest.mark.parametrize("variant", ["ring5", "ring4", "stage2"])
+def test_pgemm(M, N, Kd, epi, variant):
     """Prefill / encoder GEMM with its fused epilogue vs the fp32 reference of the same op: edge
     tiles in M and N (rows/cols past the edge never stored), bias, bias+GELU, SwiGLU."""
     x = (torch.rand(M, Kd, device=DEV) * 2 - 1).bfloat16()
@@ -448,11 +449,12 @@ def test_pgemm(M, N, Kd, epi):
         gu = R.deinterleave_gate_up(w.cpu())      # the same weights in [gate; up] order
         ref = R.silu_mul(_ref_linear(x, gu.to(DEV)).bfloat16()).float()
     out = torch.full((M, N // 2 if epi == "swiglu" else N), float("nan"), device=DEV).bfloat16()
-    y = K.pgemm(x, w, epi, bias=b, out=out)
+    y = K.pgemm(x, w, epi, bias=b, out=out, variant=variant)
     _close(y, ref, 3e-2)
 
 
-def test_pgemm_exact_and_strided_out():
+@pytest.mark.parametrize("variant", ["ring5", "ring4", "stage2"])
+def test_pgemm_exact_and_strided_out(variant):
     """Small-integer operands: bit-exact; output written into a wider buffer (ldo > N) leaves the
     other columns untouched."""
     M, N, Kd = 300, 320, 192
@@ -460,7 +462,7 @@ def test_pgemm_exact_and_strided_out():
     w = torch.randint(-2, 3, (N, Kd), device=DEV).bfloat16()
     w[:, :5] += torch.arange(N, device=DEV).bfloat16().unsqueeze(1) % 7
     buf = torch.zeros(M, N + 64, device=DEV).bfloat16()
-    K.pgemm(x, w, out=buf[:, :N])
+    K.pgemm(x, w, out=buf[:, :N], variant=variant)
     assert torch.equal(buf[:, :N].float(), x.float() @ w.float().T)
     assert torch.equal(buf[:, N:], torch.zeros_like(buf[:, N:]))
 
