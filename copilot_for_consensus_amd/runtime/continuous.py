@@ -54,7 +54,7 @@ class ContinuousEngine:
     def __init__(self, engine, max_slots: int = 128, max_new_cap: int = 512, max_prompt: int = 4096,
                  steps_per_sync: int = 16, stop_ids: tuple[int, ...] = (), temperature: float = 0.0, seed: int = 0,
                  max_admit_tokens: int | None = None, min_admit: int = 1, max_wait_s: float = 0.5,
-                 stop_strings=None):
+                 stop_strings=None, bulk_admit_frac: float = 0.5):
         self.engine = engine
         self.model = engine.model
         self.kv = engine.kv
@@ -70,6 +70,12 @@ class ContinuousEngine:
         # admission batching: prefill waits for `min_admit` queued threads (or the oldest waiting
         # `max_wait_s`, or an idle engine) -- fewer, larger prefills interrupt the decode less
         self.min_admit, self.max_wait_s = max(1, int(min_admit)), float(max_wait_s)
+        # bulk admission: with at least this fraction of the slots free, the token budget is lifted
+        # and every free slot is filled in one (chunked) prefill.  Pausing a mostly empty decode
+        # batch costs little, while admitting a backlog ~24 prompts at a time with a 16-step burst
+        # between groups staggers the slots' finish times for good: every later refill is then a
+        # small group and the decode batch never runs full (the static batch's throughput).
+        self.bulk_free = max(1, math.ceil(float(bulk_admit_frac) * self.B)) if bulk_admit_frac > 0 else self.B + 1
         self.max_blocks = 8 * math.ceil(blocks_needed(self.max_prompt + self.cap) / 8)
         # empty slots read and write this block only
         self.scratch = self.kv.pool.alloc(1)[0]
@@ -187,7 +193,7 @@ class ContinuousEngine:
         if len(self.queue) < min(self.min_admit, len(self.free)) and waited < self.max_wait_s:
             return
         take: list[Request] = []
-        budget = self.max_admit_tokens
+        budget = self.max_admit_tokens if len(self.free) < self.bulk_free else float("inf")
         while self.queue and len(take) < len(self.free) and (not take or budget >= len(self.queue[0].prompt)):
             r = self.queue.popleft()
             take.append(r)

@@ -117,3 +117,23 @@ def test_admission_waits_for_kv_blocks_instead_of_failing():
     assert len(done) == 5 and all(len(r.tokens) == 8 for r in reqs)
     want = eng.generate([prompts[4]], 8, temperature=0.0, ignore_eos=True).tokens[0]
     assert reqs[4].tokens == want
+
+
+def test_bulk_admission_fills_a_mostly_empty_batch_in_one_prefill():
+    """A backlog larger than the admission token budget: with most slots free the budget is lifted
+    and every free slot is filled by one admission (no staggered groups); with bulk admission off
+    the budget splits it.  Outputs are the same either way."""
+    model, kv = _setup("cpu", blocks=160)
+    reqs = [([1] + [(7 * i + j) % 400 + 3 for j in range(90)], 6) for i in range(8)]
+    out = {}
+    for frac in (0.5, 0.0):
+        eng = LLMEngine(model, kv, max_prefill_tokens=64, use_graph=False, prefix_cache=False)
+        ce = ContinuousEngine(eng, max_slots=8, max_new_cap=8, max_prompt=128, steps_per_sync=2,
+                              max_admit_tokens=200, bulk_admit_frac=frac)
+        hs = [ce.submit(p, m) for p, m in reqs]
+        ce.run()
+        ce.close()
+        out[frac] = ([h.tokens for h in hs], ce.stats["admissions"])
+    assert out[0.5][1] == 1
+    assert out[0.0][1] == 4          # 91-token prompts, 200-token budget: 2 per admission
+    assert out[0.5][0] == out[0.0][0]
