@@ -27,9 +27,10 @@ const http = require("http");
 const BASE = process.env.UI_BASE;
 const store = {};
 global.localStorage = {getItem: (k) => store[k] || null, setItem: (k, v) => { store[k] = v; }, removeItem: (k) => { delete store[k]; }};
-const el = () => ({value: "", innerHTML: "", classList: {toggle() {}}, getAttribute: () => ""});
-const nodes = {"#token": el(), "#view": el(), "#msg": el()};
-global.document = {querySelector: (s) => nodes[s] || el(), querySelectorAll: () => [], getElementById: () => el()};
+const el = () => ({value: "", innerHTML: "", textContent: "", hidden: false, classList: {toggle() {}}, getAttribute: () => ""});
+const nodes = {"#token": el(), "#view": el(), "#msg": el(), "#nav-admin": el()};
+global.document = {querySelector: (s) => nodes[s] || el(), querySelectorAll: () => [], getElementById: () => el(), body: el()};
+global.matchMedia = () => ({matches: false});
 global.location = {hash: ""};
 global.window = global;
 global.addEventListener = () => {};
@@ -52,6 +53,7 @@ require("vm").runInThisContext(SCRIPT.replace(/\nroute\(\);\s*$/, "\n"));   // p
     location.hash = h;
     await route();
     out[h] = nodes["#view"].innerHTML;
+    if (h === "#/reports") out["nav_admin_hidden"] = nodes["#nav-admin"].hidden;
   }
   process.stdout.write(JSON.stringify(out));
 })().catch((e) => { console.error("UI error", e); process.exit(2); });
@@ -117,8 +119,11 @@ def test_views_render_live_data(live, tmp_path):
     hashes = ["#/reports", "#/reports?source=wg&sort_by=generated_at&sort_order=asc&limit=10",
               "#/reports?min_messages=99", f"#/report/{rep[0]['_id']}", "#/threads",
               "#/threads?sort_by=last_message_date&limit=10", f"#/thread/{thread['_id']}", f"#/message/{msg['_id']}",
-              "#/sources", "#/source/wg", "#/reports?topic=consensus"]
-    out = _render(base, hashes, tmp_path)
+              "#/sources", "#/source/wg", "#/reports?topic=consensus", f"#/summary/{rep[0]['thread_id']}"]
+    out = _render(base, hashes + ["#/admin"], tmp_path)
+    # AccessDenied: nobody is signed in, so the admin view is refused and its nav link hidden
+    assert "Access denied" in out["#/admin"] and out["nav_admin_hidden"] is True
+    assert rep[0]["thread_id"] in out[f"#/summary/{rep[0]['thread_id']}"]
     assert all('class="err"' not in out[h] for h in hashes), {h: out[h][:300] for h in hashes if 'class="err"' in out[h]}
     assert rep[0]["_id"] in out["#/reports"] and "thread start" in out["#/reports"]
     assert "No reports match" in out["#/reports?min_messages=99"]
