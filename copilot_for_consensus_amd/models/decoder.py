@@ -410,6 +410,12 @@ class DecoderModel:
         if self.fp8:
             mode = "lib"          # W8A8: every projection through linear_fp8 (bf16 fused paths need bf16 weights)
         self.decode_gemm = mode
+        # prefill GEMM (packed prompt rows): "hip" = the hand-written MFMA GEMM (csrc/kernels/pgemm.hip,
+        # SwiGLU fused into gate/up), "lib" = the library GEMM + silu_mul (CFC_PREFILL_GEMM)
+        pm = os.environ.get("CFC_PREFILL_GEMM", self.PREFILL_GEMM_DEFAULT)
+        if pm not in ("hip", "lib"):
+            raise ValueError(f"CFC_PREFILL_GEMM={pm!r}: expected hip or lib")
+        self.prefill_gemm = "lib" if self.fp8 else pm
         # B <= 4 decode steps on the GEMV kernel (needs the interleaved gate/up layout for SwiGLU)
         gemv_shapes = (self.cfg.hidden % 8 == 0 and (weights.heads * self.cfg.head_dim) % 8 == 0
                        and weights.ffn % 8 == 0 and self.cfg.head_dim % 2 == 0)
@@ -425,6 +431,8 @@ class DecoderModel:
             weights.pack_decode()
 
     PACKED_FREE_FRACTION = 0.3   # HBM left free after packing (KV pool, activations, workspaces)
+    PREFILL_GEMM_DEFAULT = "lib"
+    PGEMM_MIN_ROWS = 256         # fewer packed rows than one 256-row tile: the library GEMM
 
     def _want_packed(self) -> bool:
         pk = os.environ.get("CFC_DECODE_PACKED", "auto")
@@ -450,6 +458,16 @@ class DecoderModel:
             w8, s = self.w.fp8_layers[i][name]
             return K.linear_fp8(x, w8, s)
         return F.linear(x, self.w.layers[i][name])
+
+    def _plin(self, i: int, name: str, x: torch.Tensor, epi: str = "bf16") -> torch.Tensor:
+        """Prefill projection: the hand-written pgemm when selected and the shape fits (``epi``
+        "swiglu" returns silu(gate) * up of the interleaved gate/up weights), else the library."""
+        wt = self.w.layers[i][name]
+        if (self.prefill_gemm == "hip" and x.is_cuda and x.shape[0] >= self.PGEMM_MIN_ROWS and x.is_contiguous()
+                and K.pgemm_ok(x, wt) and (epi != "swiglu" or self.w.gate_up_interleaved)):
+            return K.pgemm(x, wt, epi)
+        y = self._lin(i, name, x)
+        return K.silu_mul(y, interleaved=self.w.gate_up_interleaved) if epi == "swiglu" else y
 
     def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.w.tp_size > 1:
@@ -477,9 +495,8 @@ class DecoderModel:
             a = K.silu_mul_fp8(self._lin(i, "gate_up", h), interleaved=self.w.gate_up_interleaved)
             return self._all_reduce(self._lin(i, "down", a))
         h = K.rmsnorm(attn_out, lw["mlp_norm"], self.cfg.rms_eps, residual=residual)
-        gu = self._lin(i, "gate_up", h)
-        a = K.silu_mul(gu, interleaved=self.w.gate_up_interleaved)
-        return self._all_reduce(self._lin(i, "down", a))
+        a = self._plin(i, "gate_up", h, "swiglu")
+        return self._all_reduce(self._plin(i, "down", a))
 
     def forward_prefill(self, ids, positions, slots, cu_q, ctx_lens, block_tables, kv, tiles=None,
                         last_idx=None, v_runs=None) -> torch.Tensor:
@@ -491,12 +508,12 @@ class DecoderModel:
         for i in range(cfg.layers):
             lw = w.layers[i]
             h, residual = self._layer_pre(i, x, residual)
-            qkv = self._lin(i, "qkv", h)
+            qkv = self._plin(i, "qkv", h)
             q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
                                 cfg.head_dim, runs=v_runs, k_scale=kv.k_scale, v_scale=kv.v_scale)
             attn = K.prefill_attention(q, kv.k[i], kv.v[i], block_tables, cu_q, ctx_lens, self.scale, tiles=tiles,
                                        window=self.window, k_scale=kv.k_scale, v_scale=kv.v_scale)
-            o = self._all_reduce(self._lin(i, "o", attn.view(attn.shape[0], -1)))
+            o = self._all_reduce(self._plin(i, "o", attn.view(attn.shape[0], -1)))
             x = self._mlp(i, o, residual)
         if last_idx is not None:
             x = x.index_select(0, last_idx)

@@ -197,3 +197,41 @@ def test_odd_vocab_lm_head_single_stream():
     assert all(0 <= t < cfg.vocab_size for t in outs[0][0])
     assert outs[0][0][0] == outs[1][0][0]
     assert sum(a == b for a, b in zip(outs[0][0], outs[1][0])) >= 6, outs
+
+
+@pytest.mark.parametrize("mode", ["hip", "lib"])
+def test_prefill_gemm_modes_match_reference_logits(mode):
+    """Prefill projections on the hand-written pgemm (SwiGLU fused into gate/up) or the library:
+    the last-token logits of each prompt against the fp32 CPU reference model."""
+    cfg = get_config("tiny")
+
+    def _prefill_logits(model, cfg, dev, prompts):
+        kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, dev)
+        eng = LLMEngine(model, kv, max_prefill_tokens=512, use_graph=False)
+        seen = []
+        orig_logits = model.logits
+        model.logits = lambda h: seen.append(orig_logits(h)) or seen[-1]
+        try:
+            eng.generate(prompts, max_new_tokens=1, ignore_eos=True)
+        finally:
+            model.logits = orig_logits
+        return seen[0].float().cpu()
+
+    w = DecoderWeights.random(cfg, "cuda", seed=11)
+    m = DecoderModel(w)
+    m.prefill_gemm, m.PGEMM_MIN_ROWS = mode, 64
+    prompts = [[1] + list(range(7, 7 + 150)), [1] + list(range(40, 40 + 130)), [1, 5, 9] * 20]
+    calls = []
+    if mode == "hip":
+        from copilot_for_consensus_amd.ops import kernels as K
+        orig = K.pgemm
+        K.pgemm = lambda *a, **k: calls.append(1) or orig(*a, **k)
+    try:
+        got = _prefill_logits(m, cfg, "cuda", prompts)
+    finally:
+        if mode == "hip":
+            K.pgemm = orig
+    want = _prefill_logits(DecoderModel(_to_cpu_fp32_model(w)), cfg, "cpu", prompts)
+    rel = float((got - want).abs().max() / want.abs().max())
+    assert rel < 5e-2 and torch.equal(got.argmax(-1), want.argmax(-1)), rel
+    assert (len(calls) > 0) == (mode == "hip")
