@@ -452,9 +452,34 @@ class SummarizationService(BaseService):
         self._qlock = threading.Condition()
         self._worker: threading.Thread | None = None
         self._stop = False
+        # requests in the engine, by (thread, selected chunks): the orchestrator can request one
+        # thread twice when its chunks arrive in two EmbeddingsGenerated events that both find every
+        # chunk embedded; the copy is dropped instead of decoded a second time
+        self._inflight: set = set()
+        self._flight_lock = threading.Lock()
 
     def subscriptions(self):
         return {"SummarizationRequested": self._on_request}
+
+    @staticmethod
+    def _request_key(event: dict) -> tuple:
+        d = event["data"]
+        return (d["thread_ids"][0], tuple(s.get("chunk_id") for s in d.get("selected_chunks") or []))
+
+    def _claim(self, event: dict) -> bool:
+        """True when this request is not already in flight (and marks it so)."""
+        key = self._request_key(event)
+        with self._flight_lock:
+            if key in self._inflight:
+                self.metrics.increment("summarization_duplicate_skipped_total")
+                self.log.info("duplicate summarization request skipped", thread_id=key[0])
+                return False
+            self._inflight.add(key)
+            return True
+
+    def _release(self, event: dict) -> None:
+        with self._flight_lock:
+            self._inflight.discard(self._request_key(event))
 
     def _context(self, thread_id: str, selected: list[dict]) -> dict:
         ids = [s["chunk_id"] for s in selected]
@@ -476,7 +501,15 @@ class SummarizationService(BaseService):
         return tid, ctx, substitute_prompt(d["prompt_template"], tid, ctx)
 
     def summarize_events(self, events: list[dict]) -> list[dict]:
-        """Batch path: one engine call for all requested threads."""
+        """Batch path: one engine call for all requested threads (in-flight duplicates dropped)."""
+        events = [ev for ev in events if self._claim(ev)]
+        try:
+            return self._summarize_claimed(events)
+        finally:
+            for ev in events:
+                self._release(ev)
+
+    def _summarize_claimed(self, events: list[dict]) -> list[dict]:
         prepared = []
         for ev in events:
             try:
@@ -512,17 +545,31 @@ class SummarizationService(BaseService):
     # one engine call
     def _on_request(self, event):
         if self._streaming:
-            tid, ctx, prompt = self.prepare(event)     # store not ready -> raises -> the retry policy
+            if not self._claim(event):
+                return
+            try:
+                tid, ctx, prompt = self.prepare(event)     # store not ready -> raises -> the retry policy
+            except BaseException:
+                self._release(event)
+                raise
             t0 = time.perf_counter()
 
             def done(s, err, tid=tid, ctx=ctx, event=event):
-                if err is not None:
-                    self.log.error("summarization failed", thread_id=tid, error=repr(err))
-                    self.on_failure("SummarizationRequested", event, err)
-                    return
-                self.metrics.observe("summarization_latency_seconds", time.perf_counter() - t0)
-                self._publish_summary(tid, ctx, s)
-            self.summarizer.submit(SumThread(tid, ctx["messages"], len(ctx["chunks"]), self.ctx_tokens, prompt), done)
+                try:
+                    if err is not None:
+                        self.log.error("summarization failed", thread_id=tid, error=repr(err))
+                        self.on_failure("SummarizationRequested", event, err)
+                        return
+                    self.metrics.observe("summarization_latency_seconds", time.perf_counter() - t0)
+                    self._publish_summary(tid, ctx, s)
+                finally:
+                    self._release(event)    # after the SummaryComplete is out
+            try:
+                self.summarizer.submit(SumThread(tid, ctx["messages"], len(ctx["chunks"]), self.ctx_tokens, prompt),
+                                       done)
+            except BaseException:
+                self._release(event)
+                raise
             return
         if self._worker is None:
             self.summarize_events([event])

@@ -379,3 +379,53 @@ def test_summarization_continuous_engine_publishes_each_thread():
     want = llm.summarize_batch([Thread(tid, ctx["messages"], len(ctx["chunks"]), 4096, p) for tid, ctx, p in prepared])
     got = {e["data"]["thread_id"]: e["data"]["summary_markdown"] for e in done}
     assert [got[s.thread_id] for s in want] == [s.summary_markdown for s in want]
+
+
+def test_duplicate_in_flight_summarization_request_is_dropped():
+    """The orchestrator can request one thread twice (its chunks embedded in two events that both
+    find every chunk done): while the first request is in the engine the copy is dropped; once it
+    has completed, the same request is served again (the orchestrator's own "report exists" check
+    is what stops re-requests after that)."""
+    import threading as th
+
+    store = InMemoryDocumentStore()
+    _, threads, vs = _embedded(store)
+    opub, _ = _pub()
+    req = OrchestratorService(opub, None, store, vs).orchestrate_thread(threads[0]["_id"])
+    gate = th.Event()
+    submitted = []
+
+    class Streaming(MockSummarizer):
+        def start_continuous(self, **kw):
+            pass
+
+        def stop_continuous(self):
+            pass
+
+        def submit(self, thread, done):
+            submitted.append(thread.thread_id)
+
+            def run():
+                gate.wait(10)
+                done(self.summarize(thread), None)
+            th.Thread(target=run, daemon=True).start()
+
+    pub, rec = _pub()
+    svc = SummarizationService(pub, None, store, Streaming(mock_latency_ms=0))
+    svc.start_async()
+    svc._on_request(req)
+    svc._on_request(req)                   # in flight: dropped
+    assert submitted == [threads[0]["_id"]]
+    gate.set()
+    import time
+    deadline = time.time() + 10
+    while time.time() < deadline and not rec.get_events("SummaryComplete"):
+        time.sleep(0.01)
+    while time.time() < deadline and svc._inflight:
+        time.sleep(0.01)
+    assert len(rec.get_events("SummaryComplete")) == 1
+    svc._on_request(req)                   # completed: a new request is served
+    assert len(submitted) == 2
+    # batch path: copies inside one batch are summarised once
+    batch = SummarizationService(pub, None, store, MockSummarizer(mock_latency_ms=0))
+    assert len(batch.summarize_events([req, req])) == 1
