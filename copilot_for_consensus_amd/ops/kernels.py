@@ -519,7 +519,8 @@ def pgemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 PGEMM_VARIANTS = {"ring5": 0, "stage2": 1, "ring4": 2}
-PGEMM_VARIANT = os.environ.get("CFC_PGEMM_VARIANT", "ring5")
+# stage2 measured fastest of the three on every headline shape (profiles/r03s2_pgemm_variants.jsonl)
+PGEMM_VARIANT = os.environ.get("CFC_PGEMM_VARIANT", "stage2")
 
 
 def pgemm(x: torch.Tensor, w: torch.Tensor, epi: str = "bf16", bias: torch.Tensor | None = None,
@@ -528,8 +529,8 @@ def pgemm(x: torch.Tensor, w: torch.Tensor, epi: str = "bf16", bias: torch.Tenso
     elementwise op fused into the epilogue.  ``epi``: "bf16"; "bias" (+ bias[N]); "bias_gelu"
     (gelu_erf(y + bias)); "swiglu" (8-row interleaved gate/up weights -> [M, N/2] =
     silu(gate) * up with the unfused path's bf16 rounding of gate and up).  ``variant``: the K
-    loop ("ring5" default: BK=32 ring of 5 LDS slots; "ring4"; "stage2": the 2-stage BK=64
-    kernel), $CFC_PGEMM_VARIANT when None."""
+    loop ("stage2" default: 2 LDS stages of BK=64; "ring5" / "ring4": BK=32 rings of 5 / 4 LDS
+    slots), $CFC_PGEMM_VARIANT when None."""
     mode = PGEMM_EPI[epi]
     if not x.is_cuda:
         y = torch.nn.functional.linear(x.float(), w.float())

@@ -323,6 +323,7 @@ __global__ void __launch_bounds__(512, 1)
   pg_epilogue<EPI>(acc, bias, out, M, N, ldo, m0 + wr * 128, n0 + wc * 64);
 }
 
+
 template <int EPI>
 int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int M, int N, int K, int ldo,
                  int variant, hipStream_t stream) {
@@ -340,8 +341,9 @@ int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int 
 
 }  // namespace
 
-// epi & 15: 0 bf16, 1 + bias, 2 + bias -> GELU, 3 SwiGLU (out [M, N/2]); epi >> 4: kernel variant
-// (0 ring of 5 slots -- the default, 1 the 2-stage kernel, 2 ring of 4 slots); ldo = output row stride.
+// epi & 15: 0 bf16, 1 + bias, 2 + bias -> GELU, 3 SwiGLU (out [M, N/2]); epi >> 4: K-loop variant
+// (0 BK = 32 ring of 5 slots, 1 the 2-stage BK = 64 kernel -- the Python default, measured fastest,
+// 2 ring of 4 slots); ldo = output row stride.
 CFC_API int cfc_pgemm(const void* x, const void* w, const void* bias, void* out, int M, int N, int K, int epi_v,
                       int ldo, hipStream_t stream) {
   const int epi = epi_v & 15, variant = epi_v >> 4;

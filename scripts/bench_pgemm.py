@@ -70,7 +70,7 @@ def main():
     ap.add_argument("--shapes", nargs="*", default=list(SHAPES))
     ap.add_argument("--m", type=int, default=None, help="override M")
     ap.add_argument("--out", default="gpurun_out/pgemm.jsonl")
-    ap.add_argument("--variants", nargs="*", default=["ring5", "ring4", "stage2"])
+    ap.add_argument("--variants", nargs="*", default=["stage2", "ring5", "ring4"])
     ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
     enable_tuned_gemms()
