@@ -79,7 +79,10 @@ def main(argv=None):
                          weight_dtype=args.weights,
                          llm_only=args.llm_only, use_graph=not args.no_graph,
                          seed=args.seed + 7919 * groups.dp_rank, groups=groups if args.tp > 1 else None,
-                         index_prefill=args.index_prefill, kv_max_prompt=args.kv_max_prompt)
+                         index_prefill=args.index_prefill, kv_max_prompt=args.kv_max_prompt,
+                         # DP: the TP leaders' RAG indexes form one sharded index (vectors of a thread on
+                         # the GPU that owns it; insert + relevance exchanged over RCCL each batch)
+                         index_group=groups.dp_group if groups.dp_size > 1 and not args.llm_only else None)
 
     pipe.prepare_sources(list(range(args.warmup + args.steps)))
 
@@ -150,6 +153,8 @@ def main(argv=None):
                 "kv_cache": "bf16" if args.kv_dtype == "bf16" else "fp8_e4m3fn (opt-in, reduced-precision KV)",
                 "parallelism": f"dp{groups.dp_size}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
                 "pipeline": "llm-only" if args.llm_only else "parse+chunk+embed+knn+select+prefill+decode",
+                "index": (f"sharded over {groups.dp_size} GPUs by thread (RCCL all_to_all insert + relevance)"
+                          if groups.dp_size > 1 and not args.llm_only else "one HBM index per GPU"),
             },
             "p50_summary_latency_s": round(p50, 3) if p50 is not None else None,
             "generated_tokens_per_s": round(gen_tokens / elapsed, 1),

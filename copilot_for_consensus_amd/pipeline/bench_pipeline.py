@@ -32,7 +32,8 @@ class StepResult:
 class BenchPipeline:
     def __init__(self, model="mistral-7b", encoder="minilm-l6", device="cuda", threads_per_step=128,
                  max_new_tokens=512, tp=1, prefill_tokens=16384, llm_only=False, use_graph=True, seed=0,
-                 index_prefill=1_000_000, groups=None, kv_dtype="bf16", weight_dtype="bf16", kv_max_prompt=4096):
+                 index_prefill=1_000_000, groups=None, kv_dtype="bf16", weight_dtype="bf16", kv_max_prompt=4096,
+                 index_group=None):
         from ..models.decoder import DecoderModel, DecoderWeights, get_config
         from ..runtime.engine import LLMEngine
         from ..runtime.kv_cache import PagedKVCache, blocks_needed
@@ -78,7 +79,7 @@ class BenchPipeline:
             self.rag = RagPipeline(encoder=encoder, device=self.device, decoder_vocab=self.cfg.vocab_size,
                                    bos_id=self.cfg.bos_id, seed=seed, publisher=self.events, llm_model=model,
                                    max_prompt_tokens=self.cfg.max_positions - max_new_tokens,
-                                   index_prefill=index_prefill)
+                                   index_prefill=index_prefill, index_group=index_group)
 
     def prepare_sources(self, steps: list[int]) -> None:
         """Generate the synthetic archives of the given steps up front (outside the timed region)."""

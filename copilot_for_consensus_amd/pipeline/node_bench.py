@@ -17,6 +17,7 @@ selection settings (top-5 chunks, 2048-token context) as the bench pipeline.
 from __future__ import annotations
 
 import dataclasses
+import os
 import statistics
 import sys
 import tempfile
@@ -60,8 +61,10 @@ class NodeBench:
             "LLM_TEMPERATURE": "0", "LLM_IGNORE_EOS": "true", "LLM_RANDOM_SEED": "1234",
             "LLM_KV_CACHE_TOKENS": str(max(65536, threads_per_step * (4096 + max_new_tokens))),
             "SUMMARIZATION_CONTINUOUS_BATCHING": "true" if continuous else "false",
-            "SUMMARIZATION_MAX_BATCH_THREADS": str(threads_per_step), "SUMMARIZATION_MIN_ADMIT": str(threads_per_step),
-            "SUMMARIZATION_ADMIT_WAIT_MS": "3000",
+            "SUMMARIZATION_MAX_BATCH_THREADS": str(threads_per_step),
+            # admission: wait for a full batch (or 3 s) -- overridable for A/B runs
+            "SUMMARIZATION_MIN_ADMIT": os.environ.get("CFC_NODE_MIN_ADMIT", str(threads_per_step)),
+            "SUMMARIZATION_ADMIT_WAIT_MS": os.environ.get("CFC_NODE_ADMIT_WAIT_MS", "3000"),
             "ORCHESTRATOR_TOP_K": "5", "ORCHESTRATOR_CONTEXT_WINDOW_TOKENS": "2048",
             "INGESTION_STORAGE_PATH": str(self.tmp / "ingest"), "INGESTION_SCHEDULE_INTERVAL_SECONDS": "0",
             "ARCHIVE_STORE_TYPE": "local", "ARCHIVE_BASE_PATH": str(self.tmp / "archives"),

@@ -52,7 +52,7 @@ class RagPipeline:
     def __init__(self, encoder: str = "minilm-l6", device="cuda", decoder_vocab: int = 32000, bos_id: int = 1,
                  seed: int = 0, top_k: int = 5, context_window_tokens: int = 2048, index_prefill: int = 1_000_000,
                  publisher=None, validate_events: bool = True, llm_model: str = "mistral-7b",
-                 max_prompt_tokens: int | None = None):
+                 max_prompt_tokens: int | None = None, index_group=None):
         from ..embedding import HipEncoderProvider
         from ..runtime.tokenizer import synthetic_bpe
         from ..vectorstore import HipFlatIndex
@@ -62,8 +62,16 @@ class RagPipeline:
         self.bos_id = bos_id
         self.docs = InMemoryDocumentStore()
         self.archives = InMemoryArchiveStore()
-        self.index = HipFlatIndex(dimension=self.embedder.dimension, distance="cosine",
-                                  capacity=index_prefill + (1 << 18), device=str(self.device))
+        self.local_index = HipFlatIndex(dimension=self.embedder.dimension, distance="cosine",
+                                        capacity=index_prefill + (1 << 18), device=str(self.device))
+        # DP ranks (index_group): one logical index sharded over the GPUs -- each rank's shard holds
+        # its 1M prefill rows and the chunk vectors of the threads it owns (parallel/knn.py
+        # add_thread_rows: vectors out and relevance scores back over RCCL every batch)
+        self.sharded = None
+        if index_group is not None:
+            from ..parallel.knn import ShardedVectorIndex
+            self.sharded = ShardedVectorIndex(self.local_index, group=index_group)
+        self.index = self.local_index
         if index_prefill:
             g = torch.Generator(device=self.device).manual_seed(seed + 99)
             noise = torch.randn(index_prefill, self.embedder.dimension, device=self.device, generator=g)
@@ -152,8 +160,14 @@ class RagPipeline:
         order = [c for tid in by_thread for c in by_thread[tid]]
         vecs = self.embedder.embed_tensor([c["text"] for c in order])
         row0 = self.index._n
-        self.index.add_embeddings([c["_id"] for c in order], vecs,
-                                  [{"thread_id": c["thread_id"], "message_id": c["message_id"]} for c in order])
+        sharded_scores = None
+        if self.sharded is not None:
+            # insert on the owning shards + the owners' thread-restricted relevance (collective)
+            sharded_scores = self.sharded.add_thread_rows([c["thread_id"] for c in order], [c["_id"] for c in order],
+                                                          vecs)
+        else:
+            self.index.add_embeddings([c["_id"] for c in order], vecs,
+                                      [{"thread_id": c["thread_id"], "message_id": c["message_id"]} for c in order])
         self.docs.update_many("chunks", {"_id": {"$in": [c["_id"] for c in order]}}, {"embedding_generated": True})
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
@@ -173,7 +187,8 @@ class RagPipeline:
         for tid in tids:
             spans.append((r, r + len(by_thread[tid])))
             r += len(by_thread[tid])
-        sc = self.index.span_centroid_scores(self.index._X, spans).cpu().tolist()
+        sc = (sharded_scores if sharded_scores is not None
+              else self.index.span_centroid_scores(self.index._X, spans)).cpu().tolist()
         cand_scores = {c["_id"]: s for c, s in zip(order, sc)}
         prepared_threads, prompts, texts, sels, ctxs = [], [], [], [], []
         msg_by_id = {m["_id"]: m for m in msgs}

@@ -51,7 +51,9 @@ def test_bench_single_process_contract():
 def test_bench_two_ranks_under_torchrun():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", *ARGS]
-    _check(_run(cmd), 2)
+    d = _run(cmd)
+    _check(d, 2)
+    assert d["config"]["index"].startswith("sharded over 2 GPUs")    # the DP data plane ran
 
 
 def test_bench_node_pipeline_contract():

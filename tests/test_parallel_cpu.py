@@ -3,6 +3,7 @@ sharded kNN == single index, DP sharding helpers."""
 import os
 import socket
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -139,6 +140,52 @@ def test_sharded_knn_matches_single_index():
     assert [[t[0] for t in q] for q in outs[0][0]] == ref
     assert outs[0][1] + outs[1][1] == 300 and 0 < outs[0][1] < 300
     assert outs[0][2] == 300 and outs[0][3] == "c7"
+
+
+def _thread_rows(env, batches):
+    """Each rank inserts ITS batch (rank-local threads) through add_thread_rows."""
+    from copilot_for_consensus_amd.parallel.knn import ShardedVectorIndex
+    from copilot_for_consensus_amd.vectorstore import HipFlatIndex
+    idx = ShardedVectorIndex(HipFlatIndex(32, device="cpu", capacity=512))
+    tids, ids, X = batches[env.rank]
+    sc = idx.add_thread_rows(tids, ids, X)
+    stored = {idx.local._ids[r]: idx.local._meta[r]["thread_id"] for r in range(idx.local._n)}
+    return sc.tolist(), stored
+
+
+def test_thread_owned_sharded_insert_and_relevance_matches_single_index():
+    """DP data plane of the bench / orchestrator: every rank's rows land on the shard that owns
+    their THREAD, and the relevance scores that come back equal the single-index computation
+    (cosine of each row to its own thread's centroid) for every rank's batch."""
+    from copilot_for_consensus_amd.parallel.dp import owner_of
+    from copilot_for_consensus_amd.vectorstore import HipFlatIndex
+    g = torch.Generator().manual_seed(3)
+    batches = []
+    for r in range(2):
+        tids, ids = [], []
+        for t in range(9):
+            for c in range(1 + (t * 7 + r) % 4):
+                tids.append(f"r{r}-thread-{t}")
+                ids.append(f"r{r}-t{t}-c{c}")
+        batches.append((tids, ids, torch.randn(len(ids), 32, generator=g)))
+    outs = _run(_thread_rows, 2, batches)
+    for r, (tids, ids, X) in enumerate(batches):
+        single = HipFlatIndex(32, device="cpu")
+        single.add_embeddings(ids, X)
+        spans, a = [], 0
+        for i in range(1, len(ids) + 1):
+            if i == len(ids) or tids[i] != tids[a]:
+                spans.append((a, i))
+                a = i
+        want = HipFlatIndex.span_centroid_scores(single._X, spans).tolist()
+        assert outs[r][0] == pytest.approx(want, abs=1e-5)
+    # every row is stored exactly once, on its thread's owner
+    seen = {}
+    for r, (_, stored) in enumerate(outs):
+        for cid, tid in stored.items():
+            assert owner_of(tid, 2) == r and cid not in seen
+            seen[cid] = tid
+    assert len(seen) == sum(len(b[1]) for b in batches)
 
 
 # ---------------------------------------------------------------- DP helpers
