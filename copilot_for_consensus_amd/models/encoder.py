@@ -155,11 +155,9 @@ class EncoderModel:
         for lw in self.layers:
             qkv = lin(x, lw["qkv"], "bias", lw["qkv_b"])
             a = K.encoder_attention(qkv, cu_seqlens, c.heads, c.head_dim, self.scale, max_seqlen, tiles=tiles)
-            o = lin(a.view(a.shape[0], -1), lw["o"])
-            x = K.layernorm(o, lw["ln1_g"], lw["ln1_b"], c.ln_eps, bias=lw["o_b"], residual=x)
+            x = self._linear_ln(a.view(a.shape[0], -1), lw["o"], lw["o_b"], x, lw["ln1_g"], lw["ln1_b"])
             h = lin(x, lw["up"], "bias_gelu", lw["up_b"])
-            o2 = lin(h, lw["down"])
-            x = K.layernorm(o2, lw["ln2_g"], lw["ln2_b"], c.ln_eps, bias=lw["down_b"], residual=x)
+            x = self._linear_ln(h, lw["down"], lw["down_b"], x, lw["ln2_g"], lw["ln2_b"])
         return x
 
     # projection GEMMs: the hand-written pgemm (csrc/kernels/pgemm.hip, bias / bias+GELU fused in
@@ -176,6 +174,17 @@ class EncoderModel:
             return K.pgemm(x, w, epi, bias=bias)
         y = F.linear(x, w, bias if epi == "bias" else None)
         return K.bias_gelu(y, bias) if epi == "bias_gelu" else y
+
+    def _linear_ln(self, x, w, bias, residual, gamma, beta):
+        """LayerNorm(x @ w^T + bias + residual): one fused kernel (pgemm_ln: the row statistics
+        reduced inside the workgroup that owns the whole row) for the hidden sizes it is built for
+        (384), else the projection then the residual + LayerNorm kernel.  CFC_ENCODER_LN_FUSED=0
+        forces the unfused path."""
+        eps = self.cfg.ln_eps
+        if (x.is_cuda and os.environ.get("CFC_ENCODER_LN_FUSED", "1") != "0"
+                and os.environ.get("CFC_ENCODER_GEMM", "auto") != "lib" and K.pgemm_ln_ok(x, w)):
+            return K.pgemm_ln(x, w, bias, residual, gamma, beta, eps)
+        return K.layernorm(self._linear(x, w), gamma, beta, eps, bias=bias, residual=residual)
 
     @torch.inference_mode()
     def encode_ids(self, batch: list[list[int]], pooling: str | None = None, normalize: bool | None = None,

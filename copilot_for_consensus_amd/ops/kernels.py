@@ -557,6 +557,38 @@ def pgemm(x: torch.Tensor, w: torch.Tensor, epi: str = "bf16", bias: torch.Tenso
     return out
 
 
+PGEMM_LN_N = (384,)     # output widths the fused GEMM + LayerNorm kernel is built for
+
+
+def pgemm_ln_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return pgemm_ok(x, w) and w.shape[0] in PGEMM_LN_N
+
+
+def pgemm_ln(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, residual: torch.Tensor, gamma: torch.Tensor,
+             beta: torch.Tensor, eps: float, out: torch.Tensor | None = None) -> torch.Tensor:
+    """LayerNorm(x @ w^T + bias + residual) * gamma + beta in one kernel (the post-LN encoder
+    sub-layer: attention o-proj and FFN down with their residual and LayerNorm).
+    Numerics as the unfused path: projection rounded to bf16, the rest in fp32."""
+    if not x.is_cuda:
+        y = torch.nn.functional.linear(x.float(), w.float()).to(x.dtype)
+        return ref.layernorm(y, gamma, beta, eps, bias, residual)
+    if not pgemm_ln_ok(x, w):
+        raise ValueError(f"pgemm_ln: x {tuple(x.shape)} w {tuple(w.shape)}")
+    M, Kd = x.shape
+    N = w.shape[0]
+    for t, name in ((bias, "bias"), (gamma, "gamma"), (beta, "beta")):
+        _req(t, torch.bfloat16, name)
+        if t.numel() != N:
+            raise ValueError(f"pgemm_ln: {name} of {t.numel()} for N = {N}")
+    _req(residual, torch.bfloat16, "residual")
+    if residual.shape != (M, N) or not residual.is_contiguous():
+        raise ValueError(f"pgemm_ln: residual {tuple(residual.shape)} for [{M}, {N}]")
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device) if out is None else out
+    check(kernels().cfc_pgemm_ln(x.data_ptr(), w.data_ptr(), bias.data_ptr(), residual.data_ptr(), gamma.data_ptr(),
+                                 beta.data_ptr(), out.data_ptr(), M, N, Kd, float(eps), _stream(x)), "cfc_pgemm_ln")
+    return out
+
+
 GEMV_MAX_M = 4   # decode batches up to this size take the weight-streaming GEMV (gemm.hip: gemv_kernel)
 
 

@@ -324,6 +324,150 @@ __global__ void __launch_bounds__(512, 1)
 }
 
 
+
+// ---- encoder sub-layer epilogue: Y = LayerNorm(X . W^T + bias + residual) --------------------------
+// The post-LN BERT projections whose output width is the hidden size (o-proj K = hidden, FFN down
+// K = 4 x hidden) for hidden NC16 x 16 (384: MiniLM / bge-small).  A workgroup owns WHOLE rows: a
+// 128-row x N tile, so the row statistics of the LayerNorm are reduced inside it (waves' partial
+// sums through LDS) and the normalised row is written once -- no bf16 round trip of the projection
+// output and no separate residual + LayerNorm pass.
+//   * 8 waves = 2 (M) x 4 (N), wave tile 64 rows x N/4 columns: acc[4][NC16/4] tiles of 16 x 16;
+//   * K in 64-deep tiles, A (128 rows) and B (N rows) images staged by LDS-DMA in 8-row x 128-B
+//     pieces, XOR-swizzled through the source address as the 2-stage kernel, two LDS stages;
+//   * epilogue numerics as the unfused path: projection rounded to bf16, then bias + residual and
+//     the LayerNorm in fp32 (mean and E[x^2] - mean^2 over the row), gamma / beta, bf16 store.
+template <int NC16>
+__global__ void __launch_bounds__(512, 1)
+    pgemm_ln_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W, const uint16_t* __restrict__ bias,
+                    const uint16_t* __restrict__ residual, const uint16_t* __restrict__ gamma,
+                    const uint16_t* __restrict__ beta, uint16_t* __restrict__ out, int M, int K, float eps) {
+  constexpr int N = NC16 * 16, BM = 128, JT = NC16 / 4;           // JT column tiles per wave
+  constexpr int STAGE = (BM + N) * PG_BK * 2;
+  constexpr int PA = BM / 8 / 8, PB = N / 8 / 8;                  // DMA pieces per wave per stage
+  static_assert(NC16 % 4 == 0 && N % 64 == 0, "N = 64 k, split over 4 waves in 16-column tiles");
+  static_assert(2 * STAGE <= 160 * 1024, "two stages must fit the LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const int m0 = blockIdx.x * BM;
+
+  const int prow = lane >> 3, pch = (lane & 7) ^ prow;
+  uint32_t va[PA], vb[PB];
+#pragma unroll
+  for (int i = 0; i < PA; ++i) va[i] = ((uint32_t)min(m0 + 8 * (8 * i + w) + prow, M - 1) * (uint32_t)K + 8u * pch) * 2u;
+#pragma unroll
+  for (int i = 0; i < PB; ++i) vb[i] = ((uint32_t)(8 * (8 * i + w) + prow) * (uint32_t)K + 8u * pch) * 2u;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(pg_lds_t*)smem + w * 1024);
+  auto issue = [&](int t, int s) {
+    const uint16_t* xa = X + (size_t)t * PG_BK;
+    const uint16_t* wb = W + (size_t)t * PG_BK;
+    const uint32_t la = lds0 + s * STAGE;
+#pragma unroll
+    for (int i = 0; i < PA; ++i) pg_glds16(va[i], xa, la + i * 8192);
+#pragma unroll
+    for (int i = 0; i < PB; ++i) pg_glds16(vb[i], wb, la + BM * 128 + i * 8192);
+  };
+
+  f32x4_t acc[4][JT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < JT; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int frow = (lane & 15) * 128;
+  const int nk = K / PG_BK;
+  issue(0, 0);
+  for (int t = 0; t < nk; ++t) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (t + 1 < nk) issue(t + 1, (t + 1) & 1);
+    const char* sa = smem + (t & 1) * STAGE + wr * 64 * 128 + frow;
+    const char* sb = smem + (t & 1) * STAGE + BM * 128 + wc * (N / 4) * 128 + frow;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = ((4 * kk + (lane >> 4)) ^ (lane & 7)) << 4;
+      bf16x8_t af[4], bw[JT];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(sa + i * 16 * 128 + ch);
+#pragma unroll
+      for (int j = 0; j < JT; ++j) bw[j] = *reinterpret_cast<const bf16x8_t*>(sb + j * 16 * 128 + ch);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < JT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: lane holds rows m0 + 64 wr + 16 i + (lane & 15), columns n0w + 16 j + 4 g + e
+  const int g = lane >> 4;
+  const int n0w = wc * (N / 4);
+  float s1[4], s2[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wr * 64 + i * 16 + (lane & 15);
+    s1[i] = s2[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < JT; ++j) {
+      const int n = n0w + j * 16 + 4 * g;
+      const uint2 bb = *reinterpret_cast<const uint2*>(bias + n);
+      uint2 rr = make_uint2(0u, 0u);
+      if (m < M) rr = *reinterpret_cast<const uint2*>(residual + (size_t)m * N + n);
+      float v[4];
+      v[0] = pg_bfr(acc[i][j][0]) + __uint_as_float(bb.x << 16) + __uint_as_float(rr.x << 16);
+      v[1] = pg_bfr(acc[i][j][1]) + __uint_as_float(bb.x & 0xffff0000u) + __uint_as_float(rr.x & 0xffff0000u);
+      v[2] = pg_bfr(acc[i][j][2]) + __uint_as_float(bb.y << 16) + __uint_as_float(rr.y << 16);
+      v[3] = pg_bfr(acc[i][j][3]) + __uint_as_float(bb.y & 0xffff0000u) + __uint_as_float(rr.y & 0xffff0000u);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[i][j][e] = v[e];
+        s1[i] += v[e];
+        s2[i] += v[e] * v[e];
+      }
+    }
+    // the row's 4 column groups of this wave (lanes l, l ^ 16, l ^ 32, l ^ 48)
+    s1[i] += __shfl_xor(s1[i], 16, 64);
+    s1[i] += __shfl_xor(s1[i], 32, 64);
+    s2[i] += __shfl_xor(s2[i], 16, 64);
+    s2[i] += __shfl_xor(s2[i], 32, 64);
+  }
+  // the 4 waves of a row band through LDS: red[wc][row][2] (the stages are free after the barrier)
+  float* red = reinterpret_cast<float*>(smem);
+  __syncthreads();
+  if (g == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = wr * 64 + i * 16 + (lane & 15);
+      red[(wc * BM + r) * 2] = s1[i];
+      red[(wc * BM + r) * 2 + 1] = s2[i];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = wr * 64 + i * 16 + (lane & 15);
+    const int m = m0 + r;
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      t1 += red[(q * BM + r) * 2];
+      t2 += red[(q * BM + r) * 2 + 1];
+    }
+    const float mean = t1 * (1.f / N);
+    const float rstd = rsqrtf(fmaxf(t2 * (1.f / N) - mean * mean, 0.f) + eps);
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < JT; ++j) {
+      const int n = n0w + j * 16 + 4 * g;
+      const uint2 gg = *reinterpret_cast<const uint2*>(gamma + n);
+      const uint2 be = *reinterpret_cast<const uint2*>(beta + n);
+      const float y0 = (acc[i][j][0] - mean) * rstd * __uint_as_float(gg.x << 16) + __uint_as_float(be.x << 16);
+      const float y1 = (acc[i][j][1] - mean) * rstd * __uint_as_float(gg.x & 0xffff0000u) + __uint_as_float(be.x & 0xffff0000u);
+      const float y2 = (acc[i][j][2] - mean) * rstd * __uint_as_float(gg.y << 16) + __uint_as_float(be.y << 16);
+      const float y3 = (acc[i][j][3] - mean) * rstd * __uint_as_float(gg.y & 0xffff0000u) + __uint_as_float(be.y & 0xffff0000u);
+      *reinterpret_cast<uint2*>(out + (size_t)m * N + n) = make_uint2(pack2bf(y0, y1), pack2bf(y2, y3));
+    }
+  }
+}
+
 template <int EPI>
 int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int M, int N, int K, int ldo,
                  int variant, hipStream_t stream) {
@@ -358,4 +502,17 @@ CFC_API int cfc_pgemm(const void* x, const void* w, const void* bias, void* out,
     case 3: return pgemm_launch<PG_SWIGLU>(x, w, bias, out, M, N, K, ldo, variant, stream);
     default: return (int)hipErrorInvalidValue;
   }
+}
+
+// Y[M, N] = LayerNorm(X[M, K] . W[N, K]^T + bias + residual) * gamma + beta, N = 384 (the encoder
+// hidden sizes this kernel is built for), K % 64 == 0; out may not alias residual or X.
+CFC_API int cfc_pgemm_ln(const void* x, const void* w, const void* bias, const void* residual, const void* gamma,
+                         const void* beta, void* out, int M, int N, int K, float eps, hipStream_t stream) {
+  if (M < 1 || K < 64 || K % 64 || N != 384 || (uint64_t)M * K * 2 >= (1ull << 32) || !bias || !residual || !gamma ||
+      !beta || out == residual || out == x)
+    return (int)hipErrorInvalidValue;
+  pgemm_ln_kernel<24><<<(M + 127) / 128, 512, 0, stream>>>(
+      (const uint16_t*)x, (const uint16_t*)w, (const uint16_t*)bias, (const uint16_t*)residual, (const uint16_t*)gamma,
+      (const uint16_t*)beta, (uint16_t*)out, M, K, eps);
+  return (int)hipGetLastError();
 }

@@ -634,3 +634,24 @@ def test_sample_all_nan_row_stays_in_vocab(V):
         K.sample(logits, out, temperature=t, seed=3)
         ids = out.cpu().tolist()
         assert all(0 <= i < V for i in ids), (t, ids)
+
+
+@pytest.mark.parametrize("M,Kd", [(300, 384), (1000, 1536), (64, 384), (129, 768)])
+def test_pgemm_ln(M, Kd):
+    """Fused projection + bias + residual + LayerNorm (post-LN encoder sub-layer) vs the fp32
+    reference of the unfused op (projection rounded to bf16 first, as the unfused path does);
+    edge rows past M are never written."""
+    N = 384
+    x = (torch.rand(M, Kd, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(N, Kd, device=DEV) * 2 - 1) / Kd ** 0.5).bfloat16()
+    b = (torch.rand(N, device=DEV) * 0.2 - 0.1).bfloat16()
+    res = torch.randn(M, N, device=DEV).bfloat16()
+    g = (1 + 0.1 * torch.randn(N, device=DEV)).bfloat16()
+    be = (0.1 * torch.randn(N, device=DEV)).bfloat16()
+    y = K.pgemm_ln(x, w, b, res, g, be, 1e-12)
+    proj = _ref_linear(x, w).bfloat16()
+    want = R.layernorm(proj, g.cpu(), be.cpu(), 1e-12, b.cpu(), res.cpu())
+    _close(y, want.float(), 3e-2)
+    # the same as the unfused kernels on the device
+    unf = K.layernorm(K.pgemm(x, w), g, be, 1e-12, bias=b, residual=res)
+    assert float((y.float() - unf.float()).abs().max()) <= 0.0625
