@@ -6,9 +6,10 @@ static 128-thread LLM batch.  This one runs the deployment itself: a :class:`~..
 bus, document store in memory, HIP encoder + HBM vector index + HIP decoder on the GPU) with the
 summarization service on its continuous engine.  Each step's synthetic mailing-list archive enters
 through the ingestion service (a local source: fetch -> archive store -> ``ArchiveIngested``) and
-the step is done when every one of its threads has a report in the store.  The archives of all
-timed steps are queued at once (a backlog, as a mailing-list backfill produces), so stages
-overlap the way the event-driven services overlap them.
+the step is done when every one of its threads has a report in the store.  Archives are submitted
+paced: at most two steps in flight (``CFC_NODE_MAX_INFLIGHT``; 0 queues every step at once, a
+backfill's backlog), so stages overlap the way the event-driven services overlap them and the
+reported latency is a step's own.
 
 Same model, encoder, threads per step, generated tokens (``LLM_IGNORE_EOS`` as the bench
 pipeline's ``ignore_eos``: random-init weights would otherwise stop at arbitrary points) and
@@ -107,10 +108,24 @@ class NodeBench:
         return [t["_id"] for t in self.store.query_documents("threads", {"archive_id": {"$in": archive_ids}},
                                                              limit=1 << 20)]
 
-    def run_steps(self, steps, on_step=None, timeout_s: float = 3600.0) -> list[NodeStepResult]:
-        """Queue every step's archive, then wait until each step's threads all have reports."""
-        subs = {s: self._submit(s) for s in steps}
+    def run_steps(self, steps, on_step=None, timeout_s: float = 3600.0, max_inflight: int | None = None
+                  ) -> list[NodeStepResult]:
+        """Submit the steps' archives through the ingestion service and wait until each step's
+        threads all have reports.  ``max_inflight`` (default $CFC_NODE_MAX_INFLIGHT, 0 = all at
+        once): at most that many steps submitted and unfinished -- a paced source, so a step's
+        latency is its own (queue + upstream + summarization), not the position in a whole backlog;
+        2 keeps the next batch's upstream work overlapped with the running decode."""
+        if max_inflight is None:
+            max_inflight = int(os.environ.get("CFC_NODE_MAX_INFLIGHT", "2"))
+        todo = list(steps)
+        subs = {}
+
+        def refill():
+            while todo and (max_inflight <= 0 or len(subs) - len(out) < max_inflight):
+                s = todo.pop(0)
+                subs[s] = self._submit(s)
         out: list[NodeStepResult] = []
+        refill()
         deadline = time.time() + timeout_s
         pending = list(steps)
         last_note = time.time()
@@ -139,6 +154,7 @@ class NodeBench:
             if on_step is not None:
                 on_step(s, res)
             pending.pop(0)
+            refill()
         return out
 
     def engine_stats(self) -> dict:
