@@ -1,0 +1,102 @@
+"""Thread-owned sharded HBM index (parallel/knn.py add_thread_rows) on a real GPU: two DP ranks as
+two processes on the box's one GPU (gloo between them, the vectors in HBM, the HIP flat index
+per rank).  Each rank inserts its own batch; the relevance scores that come back must equal the
+single-index computation on the device, every row must be stored once on its thread's owner, and
+an exact global search over the two shards must return the single index's top-k."""
+from __future__ import annotations
+
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _batches(dim=384):
+    g = torch.Generator().manual_seed(11)
+    out = []
+    for r in range(2):
+        tids, ids = [], []
+        for t in range(40):
+            for c in range(1 + (3 * t + r) % 6):
+                tids.append(f"r{r}-thread-{t}")
+                ids.append(f"r{r}-t{t}-c{c}")
+        out.append((tids, ids, torch.randn(len(ids), dim, generator=g)))
+    return out
+
+
+def _worker(rank, port, q, batches, Q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                          LOCAL_RANK=str(rank), CFC_DIST_BACKEND="gloo")
+        from copilot_for_consensus_amd.parallel import init_distributed
+        from copilot_for_consensus_amd.parallel.knn import ShardedVectorIndex
+        from copilot_for_consensus_amd.vectorstore import HipFlatIndex
+        env = init_distributed(backend="gloo")
+        idx = ShardedVectorIndex(HipFlatIndex(384, device=str(env.device), capacity=4096))
+        tids, ids, X = batches[rank]
+        sc = idx.add_thread_rows(tids, ids, X.to(env.device))
+        torch.cuda.synchronize()
+        stored = {idx.local._ids[r]: idx.local._meta[r]["thread_id"] for r in range(idx.local._n)}
+        res = idx.query_batch(Q.to(env.device), 10)
+        q.put((rank, {"scores": sc.cpu().tolist(), "stored": stored, "dev": str(sc.device),
+                      "top": [[r.id for r in qq] for qq in res]}))
+    except BaseException as e:  # noqa: BLE001 -- reported to the parent
+        import traceback
+        q.put((rank, {"exception": traceback.format_exc() + repr(e)}))
+
+
+def test_sharded_index_two_ranks_on_the_gpu():
+    import torch.multiprocessing as mp
+
+    from copilot_for_consensus_amd.parallel.dp import owner_of
+    from copilot_for_consensus_amd.vectorstore import HipFlatIndex
+    batches = _batches()
+    Q = torch.randn(4, 384, generator=torch.Generator().manual_seed(5))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q, batches, Q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = {}
+    try:
+        for _ in procs:
+            r, res = q.get(timeout=150)
+            results[r] = res
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(2):
+        assert "exception" not in results[r], results[r]
+        assert results[r]["dev"].startswith("cuda")
+    single = HipFlatIndex(384, device="cuda", capacity=4096)
+    for r, (tids, ids, X) in enumerate(batches):
+        row0 = single._n
+        single.add_embeddings(ids, X.cuda())
+        spans, a = [], 0
+        for i in range(1, len(ids) + 1):
+            if i == len(ids) or tids[i] != tids[a]:
+                spans.append((row0 + a, row0 + i))
+                a = i
+        want = HipFlatIndex.span_centroid_scores(single._X, spans).cpu()
+        got = torch.tensor(results[r]["scores"])
+        assert float((got - want).abs().max()) < 1e-4
+    seen = {}
+    for r in range(2):
+        for cid, tid in results[r]["stored"].items():
+            assert owner_of(tid, 2) == r and cid not in seen
+            seen[cid] = tid
+    assert len(seen) == sum(len(b[1]) for b in batches)
+    want_top = [[x.id for x in qq] for qq in single.query_batch(Q.cuda(), 10)]
+    assert results[0]["top"] == results[1]["top"] == want_top
