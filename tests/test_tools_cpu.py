@@ -158,7 +158,7 @@ def test_ui_served():
     r = c.get("/ui")
     assert r.status_code == 200 and "Copilot for Consensus" in r.text and "/api/reports/search" in r.text
     # reference ui/src/routes: Login, Callback, AdminDashboard / PendingAssignments / UserRolesList
-    for route in ("async login()", "async callback(q)", "async admin(q)", "/admin/role-assignments/pending",
+    for route in ("async login(q)", "async callback(q)", "async admin(q)", "async summary(_, id)", "/admin/role-assignments/pending",
                   "/admin/users/search"):
         assert route in r.text, route
     # ReportsList / DiscussionsList filters + paging, MessageDetail chunks, UserRolesList
