@@ -50,6 +50,8 @@ def parse_args(argv=None):
     ap.add_argument("--index-prefill", type=int, default=1_000_000,
                     help="background vectors resident in the HBM kNN index besides the run's own chunks")
     ap.add_argument("--no-overlap", action="store_true", help="run pipeline stages strictly sequentially")
+    ap.add_argument("--overlap-prefill", choices=["on", "off"], default=os.environ.get("CFC_OVERLAP_PREFILL", "off"),
+                    help="prefill batch i+1 on half the CUs beside batch i's decode (runtime/cu_partition.py)")
     ap.add_argument("--pipeline", choices=["bench", "node"], default="bench",
                     help="bench: the stage code with a static LLM batch (headline); node: the real services "
                          "(Node, in-proc bus, continuous summarization engine), pipeline/node_bench.py")
@@ -82,7 +84,8 @@ def main(argv=None):
                          index_prefill=args.index_prefill, kv_max_prompt=args.kv_max_prompt,
                          # DP: the TP leaders' RAG indexes form one sharded index (vectors of a thread on
                          # the GPU that owns it; insert + relevance exchanged over RCCL each batch)
-                         index_group=groups.dp_group if groups.dp_size > 1 and not args.llm_only else None)
+                         index_group=groups.dp_group if groups.dp_size > 1 and not args.llm_only else None,
+                         overlap_prefill=args.overlap_prefill == "on" and not args.no_overlap)
 
     pipe.prepare_sources(list(range(args.warmup + args.steps)))
 
@@ -100,12 +103,15 @@ def main(argv=None):
                 print(f"[bench] {kind} {i}: {r.summary()}", file=sys.stderr, flush=True)
         return report
 
-    pipe.run_steps(list(range(args.warmup)), overlap=not args.no_overlap, on_step=progress("warmup"))
+    def run(steps, kind):
+        if pipe.overlap_prefill:
+            return pipe.run_steps_overlapped(steps, on_step=progress(kind))
+        return pipe.run_steps(steps, overlap=not args.no_overlap, on_step=progress(kind))
+    run(list(range(args.warmup)), "warmup")
 
     barrier()
     t0 = time.perf_counter()
-    results = pipe.run_steps(list(range(args.warmup, args.warmup + args.steps)), overlap=not args.no_overlap,
-                             on_step=progress("step"))
+    results = run(list(range(args.warmup, args.warmup + args.steps)), "step")
     barrier()
     elapsed = time.perf_counter() - t0
 
@@ -155,6 +161,8 @@ def main(argv=None):
                 "pipeline": "llm-only" if args.llm_only else "parse+chunk+embed+knn+select+prefill+decode",
                 "index": (f"sharded over {groups.dp_size} GPUs by thread (RCCL all_to_all insert + relevance)"
                           if groups.dp_size > 1 and not args.llm_only else "one HBM index per GPU"),
+                "schedule": ("prefill of batch i+1 on half the CUs beside batch i's decode" if pipe.overlap_prefill
+                             else "prefill then decode per batch (next batch's preparation overlapped)"),
             },
             "p50_summary_latency_s": round(p50, 3) if p50 is not None else None,
             "generated_tokens_per_s": round(gen_tokens / elapsed, 1),

@@ -33,7 +33,7 @@ class BenchPipeline:
     def __init__(self, model="mistral-7b", encoder="minilm-l6", device="cuda", threads_per_step=128,
                  max_new_tokens=512, tp=1, prefill_tokens=16384, llm_only=False, use_graph=True, seed=0,
                  index_prefill=1_000_000, groups=None, kv_dtype="bf16", weight_dtype="bf16", kv_max_prompt=4096,
-                 index_group=None):
+                 index_group=None, overlap_prefill=False):
         from ..models.decoder import DecoderModel, DecoderWeights, get_config
         from ..runtime.engine import LLMEngine
         from ..runtime.kv_cache import PagedKVCache, blocks_needed
@@ -64,7 +64,11 @@ class BenchPipeline:
         # KV budget: every thread of a step at ``kv_max_prompt`` prompt tokens + max_new, x1.1 (the
         # prompts this pipeline builds stay near 2.6k; a 70B model on one GPU needs the tighter bound)
         max_prompt = int(kv_max_prompt)
+        # prefill of batch i+1 beside the decode of batch i (run_steps_overlapped): two batches' KV
+        self.overlap_prefill = bool(overlap_prefill) and tp == 1 and self.device.type == "cuda"
         nblk = int(1.1 * threads_per_step * blocks_needed(max_prompt + max_new_tokens)) + 64
+        if self.overlap_prefill:
+            nblk *= 2
         kvd = {"bf16": torch.bfloat16, "fp8": torch.float8_e4m3fn}[kv_dtype]
         self.kv = PagedKVCache(self.cfg.layers, nblk, w.kv_heads, self.cfg.head_dim, self.device, dtype=kvd)
         self.engine = LLMEngine(self.model, self.kv, max_prefill_tokens=prefill_tokens, use_graph=use_graph)
@@ -177,6 +181,62 @@ class BenchPipeline:
         finally:
             if pool:
                 pool.shutdown(wait=True)
+        return results
+
+    def run_steps_overlapped(self, steps: list[int], on_step=None) -> list[StepResult]:
+        """Batch i+1's preparation AND prefill run on a worker thread while batch i decodes: the
+        prefill on one half of the CUs, the decode on the other half until that prefill is done,
+        then on the whole GPU (runtime/cu_partition.py).  Batch 0 is prepared and prefilled inline
+        on the whole GPU, so exactly the listed batches' work happens inside the caller's window.
+        Two decode states (slots 0 / 1) and two batches of KV blocks are live at a time."""
+        import concurrent.futures as cf
+
+        from ..runtime.cu_partition import partition_streams
+        results = []
+        if not steps:
+            return results
+        full = torch.cuda.current_stream(self.device)
+        if getattr(self, "_partitions", None) is None:
+            self._partitions = partition_streams(self.device)
+        sp, sd = self._partitions
+
+        def prep_and_start(step, slot, stream):
+            t0, ctx, prompts, stages = self._prepare(step)
+            with torch.cuda.stream(stream):
+                job = self.engine.start(prompts, self.max_new, temperature=0.0, ignore_eos=True, slot=slot,
+                                        stream_sync=True)
+            return t0, ctx, prompts, stages, job
+
+        pool = cf.ThreadPoolExecutor(1)
+        pending = prep_and_start(steps[0], steps[0] % 2, full)
+        try:
+            for n, step in enumerate(steps):
+                t0, ctx, prompts, stages, job = pending
+                fut = None
+                if n + 1 < len(steps):
+                    fut = pool.submit(prep_and_start, steps[n + 1], steps[n + 1] % 2, sp)
+                with span(f"bench.llm.step{step}"):
+                    if fut is not None:
+                        with torch.cuda.stream(sd):
+                            res = self.engine.finish(job, switch=lambda f=fut: full if f.done() else None)
+                    else:
+                        res = self.engine.finish(job)
+                stages["prefill"] = res.prefill_s
+                stages["decode"] = res.decode_s
+                t2 = time.perf_counter()
+                if ctx is not None:
+                    self.rag.finish(ctx, res)
+                    stages["report"] = time.perf_counter() - t2
+                t3 = time.perf_counter()
+                stages["total"] = t3 - t0
+                results.append(StepResult(len(prompts), [t3 - t0] * len(prompts), sum(len(t) for t in res.tokens),
+                                          sum(res.prompt_lens), stages))
+                if on_step is not None:
+                    on_step(n, results[-1])
+                if fut is not None:
+                    pending = fut.result()
+        finally:
+            pool.shutdown(wait=True)
         return results
 
     def run_step(self, step: int) -> StepResult:

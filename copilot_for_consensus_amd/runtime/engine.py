@@ -17,6 +17,7 @@ from __future__ import annotations
 import dataclasses
 import math
 import os
+import threading
 import time
 
 import numpy as np
@@ -42,6 +43,25 @@ class GenerationResult:
     @property
     def total_s(self) -> float:
         return self.prefill_s + self.decode_s
+
+
+@dataclasses.dataclass
+class _Job:
+    """A prefilled batch waiting for (or in) its decode: LLMEngine.start -> LLMEngine.finish."""
+    st: object
+    tables: list
+    fresh: list
+    lens: list
+    start: list
+    B: int
+    max_new: int
+    stop_ids: tuple
+    stop_strings: object
+    part_blocks: int
+    temperature: object
+    seed: int
+    prefill_s: float
+    ready: object = None          # event recorded after the state setup (stream handoff)
 
 
 class _DecodeState:
@@ -92,6 +112,7 @@ class LLMEngine:
                               else K.PREFILL_TILE_ROWS)
         self.stop_check_interval = stop_check_interval
         self._states: dict[tuple, _DecodeState] = {}
+        self._alloc_lock = threading.RLock()     # KV / prefix-cache bookkeeping of start / finish
         # shared-prefix reuse of whole KV blocks (system prompt + template head of every thread)
         if prefix_cache is None:
             prefix_cache = os.environ.get("CFC_PREFIX_CACHE", "1") != "0"
@@ -205,8 +226,8 @@ class LLMEngine:
         K.decode_advance(st.next_ids, st.tokens, st.step, st.ids, st.positions, st.ctx_lens, st.slots,
                          st.block_tables, st.done, st.stop_ids, st.stop_state)
 
-    def _state(self, B, max_blocks, max_new, part_blocks, stop_ids, stop_strings=None):
-        key = (B, max_blocks, max_new, tuple(stop_ids), id(stop_strings) if stop_strings is not None else None)
+    def _state(self, B, max_blocks, max_new, part_blocks, stop_ids, stop_strings=None, slot=0):
+        key = (B, max_blocks, max_new, tuple(stop_ids), id(stop_strings) if stop_strings is not None else None, slot)
         st = self._states.get(key)
         if st is None:
             P = -part_blocks if part_blocks < 0 else math.ceil(max_blocks / part_blocks)
@@ -260,6 +281,26 @@ class LLMEngine:
             stop_ids = tuple(stop_ids) + (self.cfg.eos_id,)
         if ignore_eos:
             stop_ids = ()
+        job = self.start(prompts, max_new_tokens, temperature, seed, stop_ids, stop_strings=stop_strings,
+                         _resolved=True)
+        return self.finish(job)
+
+    @torch.inference_mode()
+    def start(self, prompts: list[list[int]], max_new_tokens: int, temperature=0.0, seed: int = 0,
+              stop_ids: tuple[int, ...] = (), ignore_eos: bool = False, stop_strings=None, slot: int = 0,
+              stream_sync: bool = False, _resolved: bool = False) -> _Job:
+        """First half of :meth:`generate`: KV allocation, the chunked prefill and the decode state
+        of the batch.  ``slot`` picks one of several decode states (and captured graphs) of the same
+        shape, so a batch can be prefilled while another one decodes; ``stream_sync`` waits on the
+        current stream only (not the device) -- the other batch's decode keeps running.  A
+        thread-safe pair with :meth:`finish` (allocation and release are serialised)."""
+        if not _resolved:
+            temperature = K.SamplingParams.of(temperature)
+            if not ignore_eos and self.cfg.eos_id not in stop_ids:
+                stop_ids = tuple(stop_ids) + (self.cfg.eos_id,)
+            if ignore_eos:
+                stop_ids = ()
+        B = len(prompts)
         lens = [len(p) for p in prompts]
         if max(lens) + max_new_tokens > self.cfg.max_positions:
             raise ValueError("prompt + max_new_tokens exceeds max_positions")
@@ -268,33 +309,38 @@ class LLMEngine:
         max_blocks = 8 * math.ceil(max(need) / 8)
         pc = self.prefix_cache
         tables, start, fresh = [], [], []
-        try:
-            for p, n in zip(prompts, need):
-                shared = pc.acquire(p) if pc is not None else []
-                tables.append(shared)       # registered before alloc so a failure releases it
-                new = pc.alloc(n - len(shared)) if pc is not None else self.kv.pool.alloc(n)
-                fresh.append(new)
-                tables[-1] = shared + new
-                start.append(len(shared) * KV_BLOCK)
-                if pc is not None:
-                    pc.insert(p, tables[-1])
-        except BaseException:
-            self._release(tables, fresh, failed=True)
-            raise
-        ok = False
-        try:
-            sync = self.device.type == "cuda"
+        with self._alloc_lock:
+            try:
+                for p, n in zip(prompts, need):
+                    shared = pc.acquire(p) if pc is not None else []
+                    tables.append(shared)       # registered before alloc so a failure releases it
+                    new = pc.alloc(n - len(shared)) if pc is not None else self.kv.pool.alloc(n)
+                    fresh.append(new)
+                    tables[-1] = shared + new
+                    start.append(len(shared) * KV_BLOCK)
+                    if pc is not None:
+                        pc.insert(p, tables[-1])
+            except BaseException:
+                self._release(tables, fresh, failed=True)
+                raise
+        sync = self.device.type == "cuda"
+
+        def barrier():
             if sync:
-                torch.cuda.synchronize(self.device)
+                if stream_sync:
+                    torch.cuda.current_stream(self.device).synchronize()
+                else:
+                    torch.cuda.synchronize(self.device)
+        try:
+            barrier()
             t0 = time.perf_counter()
             with span("llm.prefill"):
                 first = self._prefill(prompts, tables, temperature, seed, start)
-            if sync:
-                torch.cuda.synchronize(self.device)
+            barrier()
             t1 = time.perf_counter()
 
             part_blocks = self._part_blocks(B, max_blocks)
-            st = self._state(B, max_blocks, max_new_tokens, part_blocks, stop_ids, stop_strings)
+            st = self._state(B, max_blocks, max_new_tokens, part_blocks, stop_ids, stop_strings, slot)
             st.block_tables.zero_()
             bt = torch.zeros(B, max_blocks, dtype=torch.int32)
             for b, t in enumerate(tables):
@@ -322,7 +368,32 @@ class LLMEngine:
                         done0[b] = 1
                 st.stop_state.set_slots(range(B), states, keep)
             st.done.copy_(done0)
+            ready = None
+            if sync:
+                ready = torch.cuda.Event()
+                ready.record(torch.cuda.current_stream(self.device))
+        except BaseException:
+            with self._alloc_lock:
+                self._release(tables, fresh, failed=True)
+            raise
+        return _Job(st, tables, fresh, lens, start, B, max_new_tokens, tuple(stop_ids), stop_strings, part_blocks,
+                    temperature, seed, t1 - t0, ready)
 
+    @torch.inference_mode()
+    def finish(self, job: _Job, switch=None) -> GenerationResult:
+        """Second half of :meth:`generate`: the decode of a started batch, on the current stream.
+        ``switch``: called between decode steps; a stream it returns takes the remaining steps
+        (ordered behind the steps already issued) -- a decode that started on a partition of the
+        CUs beside another batch's prefill widens to the whole GPU once that prefill is done."""
+        st, B, max_new_tokens = job.st, job.B, job.max_new
+        stop_ids, stop_strings, part_blocks = job.stop_ids, job.stop_strings, job.part_blocks
+        temperature, seed = job.temperature, job.seed
+        sync = self.device.type == "cuda"
+        ok = False
+        try:
+            if job.ready is not None:
+                torch.cuda.current_stream(self.device).wait_event(job.ready)
+            t1 = time.perf_counter()
             steps = 0
             rng = span("llm.decode")
             rng.__enter__()
@@ -330,8 +401,20 @@ class LLMEngine:
             self.last_used_graph = use_graph
             if use_graph and (st.graph is None or st.graph[1:] != (part_blocks, temperature, seed)):
                 self._capture(st, part_blocks, temperature, seed)
+            cur = torch.cuda.current_stream(self.device) if sync else None
             for i in range(1, max_new_tokens):
-                if use_graph:
+                if switch is not None and cur is not None:
+                    nxt = switch()
+                    if nxt is not None and nxt != cur:
+                        nxt.wait_stream(cur)
+                        cur, switch = nxt, None
+                if cur is not None:
+                    with torch.cuda.stream(cur):
+                        if use_graph:
+                            st.graph[0].replay()
+                        else:
+                            self._decode_step(st, part_blocks, temperature, seed)
+                elif use_graph:
                     st.graph[0].replay()
                 else:
                     self._decode_step(st, part_blocks, temperature, seed)
@@ -339,15 +422,18 @@ class LLMEngine:
                 if (stop_ids or stop_strings is not None) and (i % self.stop_check_interval == 0) \
                         and bool(st.done.all()):
                     break
+            if cur is not None:
+                torch.cuda.current_stream(self.device).wait_stream(cur)
             tokens = st.tokens.cpu()
             keep = st.stop_state.keep.cpu().tolist() if stop_strings is not None else [steps + 1] * B
             if sync:
-                torch.cuda.synchronize(self.device)
+                torch.cuda.current_stream(self.device).synchronize()
             rng.__exit__(None, None, None)
             t2 = time.perf_counter()
             ok = True
         finally:
-            self._release(tables, fresh, failed=not ok)
+            with self._alloc_lock:
+                self._release(job.tables, job.fresh, failed=not ok)
         out = []
         stop = set(stop_ids)
         for b in range(B):
@@ -357,8 +443,8 @@ class LLMEngine:
                     row = row[:j]
                     break
             out.append(row)
-        return GenerationResult(out, lens, prefill_s=t1 - t0, decode_s=t2 - t1, ttft_s=t1 - t0, decode_steps=steps,
-                                cached_prompt_tokens=sum(start))
+        return GenerationResult(out, job.lens, prefill_s=job.prefill_s, decode_s=t2 - t1, ttft_s=job.prefill_s,
+                                decode_steps=steps, cached_prompt_tokens=sum(job.start))
 
     def _release(self, tables, fresh, failed: bool = False):
         if self.prefix_cache is None:

@@ -235,3 +235,35 @@ def test_prefill_gemm_modes_match_reference_logits(mode):
     rel = float((got - want).abs().max() / want.abs().max())
     assert rel < 5e-2 and torch.equal(got.argmax(-1), want.argmax(-1)), rel
     assert (len(calls) > 0) == (mode == "hip")
+
+
+def test_prefill_beside_decode_on_cu_partitions_matches_generate():
+    """Batch B prefilled on half the CUs (worker thread, its own decode state slot) while batch A
+    decodes on the other half and widens to the whole GPU when B's prefill is done: both batches'
+    tokens equal their plain generate() (greedy)."""
+    import concurrent.futures as cf
+
+    from copilot_for_consensus_amd.runtime.cu_partition import partition_streams
+    cfg = get_config("tiny")
+    w = DecoderWeights.random(cfg, "cuda", seed=7)
+    m = DecoderModel(w)
+    kv = PagedKVCache(cfg.layers, 160, cfg.kv_heads, cfg.head_dim, "cuda")
+    eng = LLMEngine(m, kv, max_prefill_tokens=128)
+    A = [[1] + list(range(3, 3 + 70)), [1, 4, 9] * 15, [1] + list(range(100, 160))]
+    Bp = [[1] + list(range(200, 290)), [1, 7] * 30, [1] + list(range(11, 51))]
+    want_a = eng.generate(A, 24, ignore_eos=True).tokens
+    want_b = eng.generate(Bp, 24, ignore_eos=True).tokens
+    sp, sd = partition_streams()
+    full = torch.cuda.current_stream()
+    ja = eng.start(A, 24, ignore_eos=True, slot=0)
+
+    def start_b():
+        with torch.cuda.stream(sp):
+            return eng.start(Bp, 24, ignore_eos=True, slot=1, stream_sync=True)
+    with cf.ThreadPoolExecutor(1) as pool:
+        fut = pool.submit(start_b)
+        with torch.cuda.stream(sd):
+            got_a = eng.finish(ja, switch=lambda: full if fut.done() else None).tokens
+        jb = fut.result()
+    got_b = eng.finish(jb).tokens
+    assert got_a == want_a and got_b == want_b
