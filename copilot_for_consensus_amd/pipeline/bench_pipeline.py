@@ -191,13 +191,17 @@ class BenchPipeline:
         Two decode states (slots 0 / 1) and two batches of KV blocks are live at a time."""
         import concurrent.futures as cf
 
-        from ..runtime.cu_partition import partition_streams
+        import os
+
+        from ..runtime.cu_partition import partition_streams, priority_streams
         results = []
         if not steps:
             return results
         full = torch.cuda.current_stream(self.device)
         if getattr(self, "_partitions", None) is None:
-            self._partitions = partition_streams(self.device)
+            # CFC_OVERLAP_MODE: cumask = disjoint CU halves; priority = whole chip, decode stream first
+            mode = os.environ.get("CFC_OVERLAP_MODE", "cumask")
+            self._partitions = priority_streams(self.device) if mode == "priority" else partition_streams(self.device)
         sp, sd = self._partitions
 
         def prep_and_start(step, slot, stream):

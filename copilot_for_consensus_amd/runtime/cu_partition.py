@@ -45,3 +45,11 @@ def partition_streams(device=None, block: int = 8):
     pre = [c for c in range(n_cu) if (c // block) % 2 == 0]
     dec = [c for c in range(n_cu) if (c // block) % 2 == 1]
     return masked_stream(pre, n_cu, device), masked_stream(dec, n_cu, device)
+
+
+def priority_streams(device=None):
+    """(prefill stream, decode stream) on the whole chip, the decode stream at the highest
+    priority: the dispatcher serves the decode kernels' workgroups first and the prefill GEMMs
+    fill what is left (the alternative to disjoint CU sets)."""
+    lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
+    return torch.cuda.Stream(device=device, priority=lo), torch.cuda.Stream(device=device, priority=hi)
