@@ -154,13 +154,14 @@ constexpr int KT_ROWS = 1024;   // rows per workgroup chunk (scores [nqb][KT_ROW
 // no LDS: a radix histogram's atomics serialise here because one chunk's scores share their top
 // key bytes, and a shuffle-tree sum pays an LDS round trip per level.
 // Writes exactly k slots (ov/oi; -inf / -1 padding when len < k).
+template <int ROWS>
 __device__ __forceinline__ void wave_topk(const float* sc, int len, int k, int64_t row0, const int64_t* ids, float* ov, int64_t* oi,
                           uint32_t* /*unused*/) {
   const int lane = threadIdx.x & 63;
   const int kk = min(k, len);
-  uint32_t key[KT_ROWS / 64];
+  uint32_t key[ROWS / 64];
 #pragma unroll
-  for (int j = 0; j < KT_ROWS / 64; ++j) {
+  for (int j = 0; j < ROWS / 64; ++j) {
     const int i = lane + 64 * j;
     key[j] = i < len ? f2key(sc[i]) : 0u;
   }
@@ -170,19 +171,19 @@ __device__ __forceinline__ void wave_topk(const float* sc, int len, int k, int64
       const uint32_t cand = thr | (1u << b);
       int c = 0;
 #pragma unroll
-      for (int j = 0; j < KT_ROWS / 64; ++j) c += __popcll(__ballot(key[j] >= cand));
+      for (int j = 0; j < ROWS / 64; ++j) c += __popcll(__ballot(key[j] >= cand));
       if (c >= kk) thr = cand;                 // wave-uniform decision
     }
   }
   int gt = 0;
 #pragma unroll
-  for (int j = 0; j < KT_ROWS / 64; ++j) gt += __popcll(__ballot(key[j] > thr));
+  for (int j = 0; j < ROWS / 64; ++j) gt += __popcll(__ballot(key[j] > thr));
   const uint32_t n_gt = (uint32_t)gt;
   const uint32_t need = (uint32_t)kk - n_gt;   // keys == thr to take (>= 1 when kk > 0)
   uint32_t base_gt = 0, base_eq = 0;
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
-  for (int j = 0; j < KT_ROWS / 64; ++j) {
+  for (int j = 0; j < ROWS / 64; ++j) {
     const int i = lane + 64 * j;
     const bool g = kk > 0 && i < len && key[j] > thr, e = kk > 0 && i < len && key[j] == thr;
     const uint64_t bg = __ballot(g), be = __ballot(e);
@@ -202,10 +203,13 @@ __device__ __forceinline__ void wave_topk(const float* sc, int len, int k, int64
   for (int s2 = kk + lane; s2 < k; s2 += 64) { ov[s2] = -INFINITY; oi[s2] = -1; }
 }
 
-// Work item = a chunk of <= KT_ROWS consecutive rows and a set of queries (qsel < 0: all nq, else
+// Work item = a chunk of <= ROWS consecutive rows and a set of queries (qsel < 0: all nq, else
 // query qsel only).  Flat: blockIdx.x = chunk, queries all.  IVF (probe != null): blockIdx.x =
 // (q * nprobe + j) * maxc + c -> list probe[q][j], its chunk c.  out_v/out_i: [nq][nslots][k].
-template <int KC>
+// ROWS per workgroup: the scores of all its queries sit in LDS between the scan and the select, so
+// with many queries the chunk is shorter (knn_flat_rows) -- more workgroups resident per CU, one
+// workgroup's select overlapping the others' scans.
+template <int KC, int ROWS>
 __global__ void __launch_bounds__(256) knn_topk_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Q,
                                                        int N, int nq, const float* __restrict__ xnorm2,
                                                        const float* __restrict__ qnorm2,
@@ -218,8 +222,8 @@ __global__ void __launch_bounds__(256) knn_topk_kernel(const uint16_t* __restric
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int lo, hi, q0, nqb, slot;
   if (probe == nullptr) {
-    lo = row_lo + blockIdx.x * KT_ROWS;
-    hi = min(N, lo + KT_ROWS);
+    lo = row_lo + blockIdx.x * ROWS;
+    hi = min(N, lo + ROWS);
     q0 = 0;
     nqb = nq;
     slot = blockIdx.x;
@@ -229,12 +233,12 @@ __global__ void __launch_bounds__(256) knn_topk_kernel(const uint16_t* __restric
     nqb = 1;
     slot = (qj % nprobe) * maxc + c;
     const int l = probe[qj];
-    lo = (int)list_off[l] + c * KT_ROWS;
-    hi = min((int)list_off[l + 1], lo + KT_ROWS);
+    lo = (int)list_off[l] + c * ROWS;
+    hi = min((int)list_off[l + 1], lo + ROWS);
   }
   const int len = max(0, hi - lo);
-  float* sc = kt_smem;                                        // [nqb][KT_ROWS]
-  uint32_t* hist = reinterpret_cast<uint32_t*>(kt_smem + nqb * KT_ROWS) + 256 * w;
+  float* sc = kt_smem;                                        // [nqb][ROWS]
+  uint32_t* hist = reinterpret_cast<uint32_t*>(kt_smem + nqb * ROWS) + 256 * w;
   if (len > 0) {
     const int col = lane & 15, g = lane >> 4;
     const bool qv = col < nqb;
@@ -263,7 +267,7 @@ __global__ void __launch_bounds__(256) knn_topk_kernel(const uint16_t* __restric
             float v = acc[i];
             if (xnorm2) v = -(xnorm2[row] + qn - 2.f * v);
             if (alive && !alive[row]) v = -INFINITY;
-            sc[col * KT_ROWS + (row - lo)] = v;
+            sc[col * ROWS + (row - lo)] = v;
           }
         }
       }
@@ -272,7 +276,7 @@ __global__ void __launch_bounds__(256) knn_topk_kernel(const uint16_t* __restric
   __syncthreads();
   for (int qi = w; qi < nqb; qi += 4) {
     const size_t o = ((size_t)(q0 + qi) * nslots + slot) * k;
-    wave_topk(sc + qi * KT_ROWS, len, k, lo, nullptr, out_v + o, out_i + o, hist);
+    wave_topk<ROWS>(sc + qi * ROWS, len, k, lo, nullptr, out_v + o, out_i + o, hist);
   }
 }
 
@@ -381,24 +385,33 @@ CFC_API int cfc_pool(float* out_f32, void* out_bf16, const void* hidden, const i
 }
 
 namespace {
+// rows per flat-scan workgroup for nq queries: [nq][ROWS] fp32 scores <= 16 KB of LDS from 4 queries on
+constexpr int knn_flat_rows(int nq) { return nq <= 4 ? KT_ROWS : (nq <= 8 ? 512 : 256); }
+
 template <int KC>
 int knn_topk_launch(const void* X, const void* Q, int N, int nq, const float* xnorm2, const float* qnorm2,
                     const uint8_t* alive, int k, int row_lo, const int32_t* probe, int nprobe, int maxc,
                     const int64_t* list_off, int nslots, float* out_v, int64_t* out_i, int blocks, int nqb,
-                    hipStream_t stream) {
-  const size_t lds = (size_t)nqb * KT_ROWS * 4 + 4 * 256 * 4;
-  knn_topk_kernel<KC><<<blocks, 256, lds, stream>>>((const uint16_t*)X, (const uint16_t*)Q, N, nq, xnorm2, qnorm2,
-                                                    alive, k, row_lo, probe, nprobe, maxc, list_off, nslots, out_v,
-                                                    out_i);
+                    int rows, hipStream_t stream) {
+  const size_t lds = (size_t)nqb * rows * 4 + 4 * 256 * 4;
+#define KTL(R) knn_topk_kernel<KC, R><<<blocks, 256, lds, stream>>>((const uint16_t*)X, (const uint16_t*)Q, N, nq, \
+      xnorm2, qnorm2, alive, k, row_lo, probe, nprobe, maxc, list_off, nslots, out_v, out_i)
+  switch (rows) {
+    case 1024: KTL(1024); break;
+    case 512: KTL(512); break;
+    case 256: KTL(256); break;
+    default: return -3;
+  }
+#undef KTL
   return CFC_CHECK_LAUNCH();
 }
 
 int knn_topk_dispatch(int dim, const void* X, const void* Q, int N, int nq, const float* xnorm2, const float* qnorm2,
                       const uint8_t* alive, int k, int row_lo, const int32_t* probe, int nprobe, int maxc,
                       const int64_t* list_off, int nslots, float* out_v, int64_t* out_i, int blocks, int nqb,
-                      hipStream_t stream) {
+                      int rows, hipStream_t stream) {
 #define KT(KC) return knn_topk_launch<KC>(X, Q, N, nq, xnorm2, qnorm2, alive, k, row_lo, probe, nprobe, maxc, \
-                                          list_off, nslots, out_v, out_i, blocks, nqb, stream)
+                                          list_off, nslots, out_v, out_i, blocks, nqb, rows, stream)
   switch (dim / 32) {
     case 4: KT(4);
     case 8: KT(8);
@@ -412,18 +425,22 @@ int knn_topk_dispatch(int dim, const void* X, const void* Q, int N, int nq, cons
 }
 }  // namespace
 
-// Flat index, rows [row_lo, N): candidates out [nq][ceil((N - row_lo) / 1024)][k] (unsorted
-// within a chunk; merge with cfc_topk_pass).  nq <= 16, k <= 256; alive: optional uint8 row mask.
+// Flat index, rows [row_lo, N): candidates out [nq][ceil((N - row_lo) / cfc_knn_flat_rows(nq))][k]
+// (unsorted within a chunk; merge with cfc_topk_pass).  nq <= 16, k <= 256; alive: optional uint8 row mask.
 CFC_API int cfc_knn_topk(const void* X, const void* Q, int N, int row_lo, int nq, int dim, const float* xnorm2,
                          const float* qnorm2, const uint8_t* alive, int k, float* out_v, int64_t* out_i,
                          hipStream_t stream) {
   if (nq < 1 || nq > 16 || dim % 32 != 0 || N <= row_lo || row_lo < 0 || k < 1 || k > 256) return -1;
-  const int nch = (N - row_lo + KT_ROWS - 1) / KT_ROWS;
+  const int rows = knn_flat_rows(nq);
+  const int nch = (N - row_lo + rows - 1) / rows;
   return knn_topk_dispatch(dim, X, Q, N, nq, xnorm2, qnorm2, alive, k, row_lo, nullptr, 1, 1, nullptr, nch, out_v,
-                           out_i, nch, nq, stream);
+                           out_i, nch, nq, rows, stream);
 }
 
+// rows per IVF list chunk (one workgroup each)
 CFC_API int cfc_knn_topk_rows() { return KT_ROWS; }
+// rows per flat-scan workgroup for nq queries (the candidate count of cfc_knn_topk)
+CFC_API int cfc_knn_flat_rows(int nq) { return knn_flat_rows(nq); }
 
 // IVF: probe [nq][nprobe] list ids, list_off [nlist + 1] row offsets (rows grouped by list), maxc =
 // max chunks of any list.  One launch of nq * nprobe * maxc workgroups; candidates out
@@ -435,5 +452,5 @@ CFC_API int cfc_ivf_topk(const void* X, const void* Q, int N, int nq, int dim, c
   const long blocks = (long)nq * nprobe * maxc;
   if (blocks > (1L << 30)) return -1;
   return knn_topk_dispatch(dim, X, Q, N, nq, xnorm2, qnorm2, alive, k, 0, probe, nprobe, maxc, list_off,
-                           nprobe * maxc, out_v, out_i, (int)blocks, 1, stream);
+                           nprobe * maxc, out_v, out_i, (int)blocks, 1, KT_ROWS, stream);
 }
