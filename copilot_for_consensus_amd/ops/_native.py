@@ -52,7 +52,7 @@ _KERNEL_SIGS = {
     "cfc_topk_pass": [P, P, I, I, I, I, P, P, P],
     "cfc_knn_topk": [P, P, I, I, I, I, P, P, P, I, P, P, P],
     "cfc_knn_topk_rows": [],
-    "cfc_knn_flat_rows": [I],
+    "cfc_knn_flat_rows": [I, I],
     "cfc_ivf_topk": [P, P, I, I, I, P, P, P, P, I, P, I, I, P, P, P],
     "cfc_topk_chunk_size": [],
     "cfc_l2_normalize": [P, P, P, I, I, P],

@@ -1147,7 +1147,7 @@ def knn_topk(X, Q, k: int, xnorm2=None, qnorm2=None, alive=None, row_lo: int = 0
             sc = sc.masked_fill(~alive[row_lo:N].bool()[None], float("-inf"))
         v, i = torch.topk(sc.float(), min(k, N - row_lo), dim=1)
         return v, i + row_lo
-    R = kernels().cfc_knn_flat_rows(nq)
+    R = kernels().cfc_knn_flat_rows(nq, k)
     nch = -(-(N - row_lo) // R)
     cv = torch.empty(nq, nch * k, dtype=torch.float32, device=X.device)
     ci = torch.empty(nq, nch * k, dtype=torch.int64, device=X.device)

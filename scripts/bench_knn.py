@@ -69,7 +69,7 @@ def main():
             return torch.nn.functional.normalize(torch.randn(nq, dim, device="cuda", generator=g), dim=1)
         c = centers[torch.randint(0, args.clusters, (nq,), device="cuda", generator=g)]
         return torch.nn.functional.normalize(c + 0.02 * torch.randn(nq, dim, device="cuda", generator=g), dim=1)
-    for nq, k in ((1, 10), (16, 10), (16, 150)):
+    for nq, k in ((1, 10), (1, 150), (16, 10), (16, 150)):
         Q = queries(nq)
         for _ in range(2):
             idx.search(Q, k)
