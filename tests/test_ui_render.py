@@ -119,7 +119,7 @@ def test_views_render_live_data(live, tmp_path):
     hashes = ["#/reports", "#/reports?source=wg&sort_by=generated_at&sort_order=asc&limit=10",
               "#/reports?min_messages=99", f"#/report/{rep[0]['_id']}", "#/threads",
               "#/threads?sort_by=last_message_date&limit=10", f"#/thread/{thread['_id']}", f"#/message/{msg['_id']}",
-              "#/sources", "#/source/wg", "#/reports?topic=consensus", f"#/summary/{rep[0]['thread_id']}"]
+              "#/sources", "#/source/wg", "#/source/", "#/reports?topic=consensus", f"#/summary/{rep[0]['thread_id']}"]
     out = _render(base, hashes + ["#/admin"], tmp_path)
     # AccessDenied: nobody is signed in, so the admin view is refused and its nav link hidden
     assert "Access denied" in out["#/admin"] and out["nav_admin_hidden"] is True
@@ -132,4 +132,30 @@ def test_views_render_live_data(live, tmp_path):
     assert thread["subject"][:20] in out["#/threads"] or thread["_id"] in out["#/threads"]
     assert "Chunks (" in out[f"#/message/{msg['_id']}"] and "embedded" in out[f"#/message/{msg['_id']}"]
     assert "wg" in out["#/sources"] and "Source wg" in out["#/source/wg"]
+    assert "New source" in out["#/source/"] and 'name="password"' in out["#/source/"]
     assert "<th>Score</th>" in out["#/reports?topic=consensus"]
+
+
+def test_source_form_validation_matches_reference_rules(tmp_path):
+    """sourceErrors() mirrors SourceForm.tsx validate(): name / type / url always, port (1..65535),
+    username and password when the type is imap."""
+    import pathlib
+    html = (pathlib.Path(__file__).parents[1] / "copilot_for_consensus_amd" / "ui" / "index.html").read_text()
+    js = "\n".join(re.findall(r"<script>(.*?)</script>", html, re.S))
+    m = re.search(r"function sourceErrors\(b\) \{.*?\n\}", js, re.S)
+    assert m, "sourceErrors not found in the page script"
+    cases = [{"name": "a", "source_type": "local", "url": "/x"},
+             {"name": "", "source_type": "local", "url": ""},
+             {"name": "a", "source_type": "imap", "url": "imap.example.org"},
+             {"name": "a", "source_type": "imap", "url": "h", "port": 70000, "username": "u", "password": "p"},
+             {"name": "a", "source_type": "imap", "url": "h", "port": 993, "username": "u", "password": "p"}]
+    prog = m.group(0) + f"\nprocess.stdout.write(JSON.stringify({json.dumps(cases)}.map(sourceErrors)));"
+    (tmp_path / "v.js").write_text(prog)
+    r = subprocess.run([NODE, str(tmp_path / "v.js")], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    assert out[0] == [] and out[4] == []
+    assert out[1] == ["Name is required", "URL is required"]
+    assert out[2] == ["Port is required for IMAP sources", "Username is required for IMAP sources",
+                      "Password is required for IMAP sources"]
+    assert out[3] == ["Port must be between 1 and 65535"]
