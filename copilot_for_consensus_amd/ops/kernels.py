@@ -510,30 +510,38 @@ def dgemm_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, residual: torch.Ten
 PGEMM_EPI = {"bf16": 0, "bias": 1, "bias_gelu": 2, "swiglu": 3}
 
 
-def pgemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+def pgemm_ok(x: torch.Tensor, w) -> bool:
     """Shapes the prefill GEMM (pgemm.hip) takes: bf16 contiguous, K % 64 == 0, N % 64 == 0, byte
-    spans < 4 GiB (32-bit DMA offsets)."""
+    spans < 4 GiB (32-bit DMA offsets); ``w`` row-major [N, K] or a PackedWeight."""
+    if isinstance(w, PackedWeight):
+        return (x.is_cuda and x.dim() == 2 and x.dtype == torch.bfloat16 and x.is_contiguous() and x.shape[1] == w.K
+                and w.K % 64 == 0 and w.N % 64 == 0 and x.shape[0] >= 1 and x.numel() * 2 < 2 ** 32
+                and w.N * w.K * 2 < 2 ** 32)
     return (x.is_cuda and x.dim() == 2 and w.dim() == 2 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
             and x.is_contiguous() and w.is_contiguous() and x.shape[1] == w.shape[1] and x.shape[1] % 64 == 0
             and w.shape[0] % 64 == 0 and x.shape[0] >= 1 and x.numel() * 2 < 2 ** 32 and w.numel() * 2 < 2 ** 32)
 
 
-PGEMM_VARIANTS = {"ring5": 0, "stage2": 1, "ring4": 2}
-# stage2 measured fastest of the three on every headline shape (profiles/r03s2_pgemm_variants.jsonl)
+PGEMM_VARIANTS = {"ring5": 0, "stage2": 1, "ring4": 2, "pp": 3, "w4": 4}
+# row-major W default K loop (a PackedWeight always runs the ping-pong kernel "pp")
 PGEMM_VARIANT = os.environ.get("CFC_PGEMM_VARIANT", "stage2")
 
 
-def pgemm(x: torch.Tensor, w: torch.Tensor, epi: str = "bf16", bias: torch.Tensor | None = None,
+def pgemm(x: torch.Tensor, w, epi: str = "bf16", bias: torch.Tensor | None = None,
           out: torch.Tensor | None = None, variant: str | None = None) -> torch.Tensor:
     """Hand-written MFMA GEMM for prefill / encoder shapes: x [M, K] @ w[N, K]^T with the following
     elementwise op fused into the epilogue.  ``epi``: "bf16"; "bias" (+ bias[N]); "bias_gelu"
     (gelu_erf(y + bias)); "swiglu" (8-row interleaved gate/up weights -> [M, N/2] =
-    silu(gate) * up with the unfused path's bf16 rounding of gate and up).  ``variant``: the K
-    loop ("stage2" default: 2 LDS stages of BK=64; "ring5" / "ring4": BK=32 rings of 5 / 4 LDS
-    slots), $CFC_PGEMM_VARIANT when None."""
+    silu(gate) * up with the unfused path's bf16 rounding of gate and up).  ``w``: row-major bf16
+    [N, K], or the decode GEMM's PackedWeight (one weight copy for prefill and decode: the "w4" or,
+    for any other variant, the "pp" kernel).  ``variant``: the K loop ("stage2": 2 LDS stages of
+    BK=64; "ring5" / "ring4": BK=32 rings of 5 / 4 LDS slots; "pp": two wave groups ping-ponging
+    over half-tile stages; "w4": four 128x128 waves software-pipelined over a 4-stage ring),
+    $CFC_PGEMM_VARIANT when None."""
     mode = PGEMM_EPI[epi]
+    packed = isinstance(w, PackedWeight)
     if not x.is_cuda:
-        y = torch.nn.functional.linear(x.float(), w.float())
+        y = torch.nn.functional.linear(x.float(), _rowmajor(w).float())
         if mode in (1, 2):
             y = y + bias.float()
         if mode == 2:
@@ -542,7 +550,7 @@ def pgemm(x: torch.Tensor, w: torch.Tensor, epi: str = "bf16", bias: torch.Tenso
             return ref.silu_mul_interleaved(y.to(x.dtype))
         return y.to(x.dtype)
     if not pgemm_ok(x, w):
-        raise ValueError(f"pgemm: x {tuple(x.shape)} {x.dtype} w {tuple(w.shape)} {w.dtype}")
+        raise ValueError(f"pgemm: x {tuple(x.shape)} {x.dtype} w {tuple(w.shape)} {getattr(w, 'dtype', 'packed')}")
     M, Kd = x.shape
     N = w.shape[0]
     if mode in (1, 2):
@@ -551,9 +559,10 @@ def pgemm(x: torch.Tensor, w: torch.Tensor, epi: str = "bf16", bias: torch.Tenso
             raise ValueError(f"pgemm: bias of {bias.numel()} for N = {N}")
     if out is None:
         out = torch.empty(M, N // 2 if mode == 3 else N, dtype=torch.bfloat16, device=x.device)
-    check(kernels().cfc_pgemm(x.data_ptr(), w.data_ptr(), bias.data_ptr() if bias is not None else None,
+    wptr = w.data.data_ptr() if packed else w.data_ptr()
+    check(kernels().cfc_pgemm(x.data_ptr(), wptr, bias.data_ptr() if bias is not None else None,
                               out.data_ptr(), M, N, Kd, mode | (PGEMM_VARIANTS[variant or PGEMM_VARIANT] << 4),
-                              out.stride(0), _stream(x)), "cfc_pgemm")
+                              out.stride(0), w.bn // 16 if packed else 0, _stream(x)), "cfc_pgemm")
     return out
 
 

@@ -151,21 +151,24 @@ def dp_worker_loop(store, rank: int, world: int, local: Summarizer, prefix: str 
 
 # ------------------------------------------------------------------ tensor parallel followers
 class TPBroadcast:
-    """Leader side: hands each generate call's token ids to the TP followers (HipLLMSummarizer.tp_hook)."""
+    """Leader side: hands every engine call's control message to the TP followers
+    (HipLLMSummarizer.tp_hook: ("gen", ids) for a static batch, the continuous engine's
+    ("cstart" | "cstep" | "creset" | "cstop", ...) messages)."""
 
     def __init__(self, groups):
         self.g = groups
 
-    def __call__(self, ids) -> None:
+    def __call__(self, msg) -> None:
         import torch.distributed as dist
-        dist.broadcast_object_list([ids], src=self.g.tp_src, group=self.g.tp_cpu_group)
+        dist.broadcast_object_list([msg], src=self.g.tp_src, group=self.g.tp_cpu_group)
 
     def stop(self) -> None:
         self(None)
 
 
 def tp_follow(summarizer, groups) -> int:
-    """TP follower: step the engine with the leader's token ids until it sends None."""
+    """TP follower: replay the leader's engine calls (HipLLMSummarizer.tp_serve) until it sends None.
+    Returns the number of messages served."""
     import torch.distributed as dist
     n = 0
     while True:
@@ -173,5 +176,5 @@ def tp_follow(summarizer, groups) -> int:
         dist.broadcast_object_list(box, src=groups.tp_src, group=groups.tp_cpu_group)
         if box[0] is None:
             return n
-        summarizer.generate_ids(box[0])
+        summarizer.tp_serve(box[0])
         n += 1

@@ -17,6 +17,14 @@ Here the decode batch is a fixed set of ``max_slots`` slots:
   and limit are written into the slot rows.
 
 Greedy outputs equal :meth:`LLMEngine.generate` on each request alone (tests/test_continuous.py).
+
+Tensor parallel: every rank of a TP group holds a ContinuousEngine over its weight shard, and all
+of them must make the same device calls in the same order (prefills, decode bursts: their
+all-reduces pair up).  The leader alone decides admissions (they depend on its clock and its
+queue) and hands each step's decision to the followers through ``sync`` -- a ("cstep", admitted
+requests, slots to cancel, burst length) message; a follower replays it with :meth:`follow`.  The
+rest is deterministic on every rank: the block allocator and the prefix cache see the same calls,
+greedy tokens are all-reduced, so slots finish and free together.
 """
 from __future__ import annotations
 
@@ -54,8 +62,10 @@ class ContinuousEngine:
     def __init__(self, engine, max_slots: int = 128, max_new_cap: int = 512, max_prompt: int = 4096,
                  steps_per_sync: int = 16, stop_ids: tuple[int, ...] = (), temperature: float = 0.0, seed: int = 0,
                  max_admit_tokens: int | None = None, min_admit: int = 1, max_wait_s: float = 0.5,
-                 stop_strings=None, bulk_admit_frac: float = 0.5):
+                 stop_strings=None, bulk_admit_frac: float = 0.5, sync=None):
         self.engine = engine
+        # TP leader: called with each step's decision before any device work (see the module doc)
+        self.sync = sync
         self.model = engine.model
         self.kv = engine.kv
         self.device = self.kv.device
@@ -108,6 +118,7 @@ class ContinuousEngine:
         self.slot_tables: list[tuple[list[int], list[int]] | None] = [None] * B
         self.free = list(range(B - 1, -1, -1))
         self._cancelled: list[Request] = []
+        self._cancel_slots: list[int] = []     # running requests to stop at the next step
         self._rid = 0
         self.stats = {"steps": 0, "admitted": 0, "finished": 0, "prefill_s": 0.0, "decode_s": 0.0}
 
@@ -127,7 +138,8 @@ class ContinuousEngine:
 
     def cancel(self, r: Request) -> None:
         """Stop a request early (client gone, stop string seen): a queued one is dropped, a running
-        one has its slot marked done on the device, so the next harvest returns its tokens so far."""
+        one has its slot marked done on the device at the next step, so that step's harvest returns
+        its tokens so far."""
         if r.finished_s is not None or r.cancelled:
             return
         r.cancelled = True
@@ -136,7 +148,7 @@ class ContinuousEngine:
             r.tokens, r.finished_s = [], time.perf_counter()
             self._cancelled.append(r)
         elif r.slot is not None and self.slot_req[r.slot] is r:
-            self.done[r.slot] = 1
+            self._cancel_slots.append(r.slot)
 
     def partial(self, reqs: list[Request]) -> dict[int, list[int]]:
         """Tokens generated so far by running requests (one device->host copy): rid -> tokens."""
@@ -160,13 +172,34 @@ class ContinuousEngine:
     @torch.inference_mode()
     def step(self) -> list[Request]:
         """Admit what fits, run one burst of decode steps, harvest; returns requests finished now."""
-        self._admit()
+        take = self._select()
+        cancels, self._cancel_slots = self._cancel_slots, []
+        if self.sync is not None:
+            self.sync(("cstep", [(r.rid, r.prompt, r.max_new) for r in take], cancels, self.steps_per_sync))
         early, self._cancelled = self._cancelled, []
+        return early + self._run_step(take, cancels, self.steps_per_sync)
+
+    @torch.inference_mode()
+    def follow(self, msg) -> int:
+        """TP follower: replay one leader step (the ``sync`` message) on this rank's shard.  Returns
+        how many requests finished (the leader reports them; followers only free their slots)."""
+        _, admitted, cancels, n = msg
+        now = time.perf_counter()
+        take = [Request(int(rid), list(p), int(mx), now) for rid, p, mx in admitted]
+        fin = self._run_step(take, list(cancels), int(n))
+        self.queue.clear()       # held back for lack of KV blocks: the leader sends them again
+        return len(fin)
+
+    def _run_step(self, take: list[Request], cancels: list[int], n: int) -> list[Request]:
+        for s in cancels:
+            if self.slot_req[s] is not None:
+                self.done[s] = 1
+        self._admit(take)
         if all(r is None for r in self.slot_req):
-            return early
+            return []
         t = time.perf_counter()
-        self._burst(self.steps_per_sync)
-        out = early + self._harvest()
+        self._burst(n)
+        out = self._harvest()
         self.stats["decode_s"] += time.perf_counter() - t
         return out
 
@@ -183,21 +216,28 @@ class ContinuousEngine:
         self.kv.pool.free([self.scratch])
 
     # ------------------------------------------------------------------ internals
-    def _admit(self) -> None:
+    def _select(self) -> list[Request]:
+        """The admission decision (leader side): queued requests to prefill into free slots now."""
         if not self.queue or not self.free:
-            return
-        idle = all(r is None for r in self.slot_req)
+            return []
         waited = time.perf_counter() - self.queue[0].submitted_s
         # an idle engine waits too (up to max_wait_s for min_admit requests): admitting the first
         # arrival alone would stagger every later admission into small prefills
         if len(self.queue) < min(self.min_admit, len(self.free)) and waited < self.max_wait_s:
-            return
+            return []
         take: list[Request] = []
         budget = self.max_admit_tokens if len(self.free) < self.bulk_free else float("inf")
         while self.queue and len(take) < len(self.free) and (not take or budget >= len(self.queue[0].prompt)):
             r = self.queue.popleft()
             take.append(r)
             budget -= len(r.prompt)
+        return take
+
+    def _admit(self, take: list[Request]) -> None:
+        """Prefill ``take`` into free slots; what the KV pool cannot hold goes back to the queue front."""
+        if not take:
+            return
+        idle = all(r is None for r in self.slot_req)
         pc = self.engine.prefix_cache
         tables, fresh, start = [], [], []
         try:

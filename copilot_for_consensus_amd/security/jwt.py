@@ -445,9 +445,27 @@ def _check_public(key, public_key: str | None) -> None:
     tokens that no verifier holding the published key accepts)."""
     if not public_key:
         return
-    pub = load_pem_key(public_key) if public_key.lstrip().startswith("-----BEGIN") else None
-    if pub is None:
-        return
+    text = public_key.strip()
+    if text.startswith("-----BEGIN"):
+        pub = load_pem_key(text)
+    else:
+        try:
+            jwk = json.loads(text)
+        except ValueError:
+            raise JWTError("public_key is neither PEM nor a JSON / JWK key") from None
+        if isinstance(jwk, dict) and "keys" in jwk and jwk["keys"]:   # a JWKS: its first key
+            jwk = jwk["keys"][0]
+        if not isinstance(jwk, dict):
+            raise JWTError("public_key JSON is not a JWK object")
+        kty = jwk.get("kty") or ("RSA" if "n" in jwk else "EC" if "x" in jwk else None)
+        if kty == "RSA":
+            pub = RSAKey.from_jwk(jwk)
+        elif kty == "EC":
+            pub = ECKey.from_jwk(jwk)
+        else:
+            raise JWTError(f"public_key JWK has an unsupported kty {kty!r}")
+    if type(pub) is not type(key):
+        raise JWTError("public_key does not match private_key (different key types)")
     same = (pub.n, pub.e) == (key.n, key.e) if isinstance(key, RSAKey) else (pub.x, pub.y) == (key.x, key.y)
     if not same:
         raise JWTError("public_key does not match private_key")

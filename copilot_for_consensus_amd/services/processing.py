@@ -224,12 +224,14 @@ class EmbeddingService(BaseService):
 
         def loop():
             own_gpu_stream()
-            while not self._stop:
+            while True:
                 with self._qlock:
                     if not self._queue:
+                        if self._stop:
+                            break          # stopped and drained: no acked ChunksPrepared is dropped
                         self._qlock.wait(0.1)
                         continue
-                    deadline = time.time() + self.batch_wait
+                    deadline = time.time() + (0.0 if self._stop else self.batch_wait)
                     while (sum(len(e["data"]["chunk_ids"]) for e in self._queue) < self.max_batch_chunks
                            and time.time() < deadline):
                         self._qlock.wait(max(0.0, deadline - time.time()))
@@ -250,8 +252,16 @@ class EmbeddingService(BaseService):
         self._worker = threading.Thread(target=loop, name="embedding-batcher", daemon=True)
         self._worker.start()
 
-    def stop_async(self) -> None:
-        self._stop = True
+    def stop_async(self, timeout: float = 120.0) -> None:
+        """Stop the batcher after it embedded every queued event (their bus messages were acked
+        when queued, so dropping them would lose the chunks until a restart's requeue)."""
+        with self._qlock:
+            self._stop = True
+            self._qlock.notify_all()
+        if self._worker is not None:
+            self._worker.join(timeout=timeout)
+            if not self._worker.is_alive():
+                self._worker = None
 
     def process_chunks(self, chunk_ids: list[str]) -> int:
         if not chunk_ids:

@@ -171,15 +171,35 @@ class HipLLMSummarizer(Summarizer):
                 out.append(Summary(t.thread_id, text, [], self.backend, self.model, len(p), len(g), ms))
         return out
 
-    # TP leader: called with each batch's token ids before generating, so the followers
-    # (parallel/dp_service.tp_follow) step the same engine call in lockstep
+    # TP leader: called with every engine call's control message before it runs, so the followers
+    # (parallel/dp_service.tp_follow -> tp_serve) make the same device calls in lockstep:
+    # ("gen", ids) for a static batch, ("cstart", params) / ("cstep", ...) / ("creset",) / ("cstop",)
+    # for the continuous engine
     tp_hook = None
 
     def generate_ids(self, ids: list[list[int]]):
         if self.tp_hook is not None:
-            self.tp_hook(ids)
+            self.tp_hook(("gen", ids))
         return self.engine.generate(ids, self.max_new_tokens, temperature=self.sampling, ignore_eos=self.ignore_eos,
                                     stop_strings=None if self.ignore_eos else self.stop_matcher)
+
+    def tp_serve(self, msg) -> None:
+        """TP follower side of one leader message (see ``tp_hook``)."""
+        kind = msg[0]
+        if kind == "gen":
+            self.generate_ids(msg[1])
+        elif kind == "cstart":
+            self._ce = self._new_continuous(**msg[1])
+        elif kind == "cstep":
+            self._ce.follow(msg)
+        elif kind == "creset":
+            self._ce = self._reset_continuous(self._ce)
+        elif kind == "cstop":
+            if getattr(self, "_ce", None) is not None:
+                self._ce.close()
+                self._ce = None
+        else:
+            raise ValueError(f"unknown TP control message {kind!r}")
 
     def apply_stops(self, text: str) -> str:
         """Cut at the first stop sequence (string-level stops, as the llama.cpp server applies them)."""
@@ -190,22 +210,29 @@ class HipLLMSummarizer(Summarizer):
         return self.summarize_batch([thread])[0]
 
     # ------------------------------------------------------------ continuous (service) mode
+    def _new_continuous(self, steps_per_sync: int, min_admit: int, max_wait_s: float):
+        from ..runtime.continuous import ContinuousEngine
+        eos = () if self.ignore_eos else (self.cfg.eos_id,)
+        return ContinuousEngine(self.engine, max_slots=self.max_batch, max_new_cap=self.max_new_tokens,
+                                max_prompt=self.context_limit, steps_per_sync=steps_per_sync, stop_ids=eos,
+                                temperature=self.sampling, min_admit=min_admit, max_wait_s=max_wait_s,
+                                stop_strings=None if self.ignore_eos else self.stop_matcher, sync=self.tp_hook)
+
     def start_continuous(self, steps_per_sync: int = 16, min_admit: int = 1, max_wait_s: float = 0.05) -> None:
         """Serve :meth:`submit` ted threads through a ContinuousEngine on a background thread: a
         thread joins the running decode batch at the next burst boundary and leaves it at its stop
         (EOS, a stop string on the device, or max_new_tokens), its slot refilled from the queue --
-        no batch-of-N latency for a bursty bus load."""
+        no batch-of-N latency for a bursty bus load.  Under tensor
+        parallelism the followers build the same engine and replay every step (``tp_hook``)."""
         import collections
         import threading
 
-        from ..runtime.continuous import ContinuousEngine
         if getattr(self, "_ce", None) is not None:
             return
-        eos = () if self.ignore_eos else (self.cfg.eos_id,)
-        self._ce = ContinuousEngine(self.engine, max_slots=self.max_batch, max_new_cap=self.max_new_tokens,
-                                    max_prompt=self.context_limit, steps_per_sync=steps_per_sync, stop_ids=eos,
-                                    temperature=self.sampling, min_admit=min_admit, max_wait_s=max_wait_s,
-                                    stop_strings=None if self.ignore_eos else self.stop_matcher)
+        params = dict(steps_per_sync=steps_per_sync, min_admit=min_admit, max_wait_s=max_wait_s)
+        if self.tp_hook is not None:
+            self.tp_hook(("cstart", params))
+        self._ce = self._new_continuous(**params)
         self._inbox: collections.deque = collections.deque()
         self._cv = threading.Condition()
         self._live: dict = {}
@@ -214,65 +241,91 @@ class HipLLMSummarizer(Summarizer):
         self._ce_thread.start()
 
     def submit(self, thread: Thread, done) -> None:
-        """Queue one thread; ``done(summary, error)`` is called from the engine thread."""
+        """Queue one thread; ``done(summary, error)`` is called exactly once, from the engine thread
+        (with an error when the engine fails or is stopped before the thread finished)."""
         ids = self._tokens(thread.prompt)
         with self._cv:
+            if self._ce_stop:
+                raise RuntimeError("summarizer is stopping")
             self._inbox.append((thread, ids, time.perf_counter(), done))
             self._cv.notify()
 
+    @staticmethod
+    def _deliver(done, summary, error) -> None:
+        """One call of a request's callback; a callback that raises is logged, never re-invoked
+        (it may already have published its SummaryComplete)."""
+        try:
+            done(summary, error)
+        except Exception as e:  # noqa: BLE001 -- the engine thread must keep serving
+            import sys
+            print(f"[summarizer] done callback failed: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
+
     def _finish(self, thread, ids, t0, done, toks) -> None:
-        text = self.apply_stops(self.tokenizer.decode(toks)).strip() or "(empty summary)"
-        done(Summary(thread.thread_id, text, [], self.backend, self.model, len(ids), len(toks),
-                     int(1000 * (time.perf_counter() - t0))), None)
+        try:
+            text = self.apply_stops(self.tokenizer.decode(toks)).strip() or "(empty summary)"
+            s = Summary(thread.thread_id, text, [], self.backend, self.model, len(ids), len(toks),
+                        int(1000 * (time.perf_counter() - t0)))
+        except Exception as e:  # noqa: BLE001 -- a decode failure fails this thread alone
+            self._deliver(done, None, e)
+            return
+        self._deliver(done, s, None)
 
     def _serve(self) -> None:
         from ..services.base import own_gpu_stream
         own_gpu_stream()
         ce = self._ce
-        while True:
-            with self._cv:
-                while not self._ce_stop and not self._inbox and not ce.pending():
-                    self._cv.wait(0.5)
-                if self._ce_stop:
-                    break
-                new = list(self._inbox)
-                self._inbox.clear()
-            for item in new:
-                thread, ids, t0, done = item
-                try:
-                    r = ce.submit(ids, self.max_new_tokens)
-                except ValueError as e:
-                    done(None, e)
-                    continue
-                self._live[r.rid] = item
-            try:
-                finished = ce.step()
-            except Exception as e:  # noqa: BLE001 -- engine failure: every queued / running thread fails
-                for item in list(self._live.values()):
-                    item[3](None, e)
-                self._live.clear()
-                self._ce = ce = self._reset_continuous(ce)
-                continue
-            if not finished and all(x is None for x in ce.slot_req):
-                with self._cv:      # admission is waiting for more requests: do not spin on the GIL
-                    self._cv.wait(0.005)
-            for r in finished:
-                item = self._live.pop(r.rid, None)
-                if item is not None:
+        try:
+            while True:
+                with self._cv:
+                    while not self._ce_stop and not self._inbox and not ce.pending():
+                        self._cv.wait(0.5)
+                    if self._ce_stop:
+                        break
+                    new = list(self._inbox)
+                    self._inbox.clear()
+                for item in new:
+                    thread, ids, t0, done = item
                     try:
+                        r = ce.submit(ids, self.max_new_tokens)
+                    except ValueError as e:
+                        self._deliver(done, None, e)
+                        continue
+                    self._live[r.rid] = item
+                try:
+                    finished = ce.step()
+                except Exception as e:  # noqa: BLE001 -- engine failure: every queued / running thread fails
+                    live, self._live = list(self._live.values()), {}
+                    for item in live:
+                        self._deliver(item[3], None, e)
+                    self._ce = ce = self._reset_continuous(ce, leader=True)
+                    continue
+                if not finished and all(x is None for x in ce.slot_req):
+                    with self._cv:      # admission is waiting for more requests: do not spin on the GIL
+                        self._cv.wait(0.005)
+                for r in finished:
+                    item = self._live.pop(r.rid, None)
+                    if item is not None:
                         self._finish(*item, r.tokens or [])
-                    except Exception as e:  # noqa: BLE001 -- a callback failing must not stop the engine
-                        item[3](None, e)
+        finally:
+            # stopped (or the thread died): every thread still queued or running gets its failure, so
+            # the service publishes SummarizationFailed and releases its in-flight key -- none is
+            # dropped silently (the bus message was acked when the request was queued)
+            with self._cv:
+                left = list(self._inbox) + list(self._live.values())
+                self._inbox.clear()
+                self._live = {}
+            err = RuntimeError("summarizer stopped before the thread finished")
+            for item in left:
+                self._deliver(item[3], None, err)
 
-    def _reset_continuous(self, ce):
-        from ..runtime.continuous import ContinuousEngine
+    def _reset_continuous(self, ce, leader: bool = False):
+        if leader and self.tp_hook is not None:
+            self.tp_hook(("creset",))
         try:
             ce.close()
         except Exception:  # noqa: BLE001 -- best effort: the old slots' blocks may be gone with the error
             pass
-        return ContinuousEngine(self.engine, max_slots=ce.B, max_new_cap=ce.cap, max_prompt=ce.max_prompt,
-                                steps_per_sync=ce.steps_per_sync, stop_ids=ce.stop_ids, temperature=ce.sampling,
-                                min_admit=ce.min_admit, max_wait_s=ce.max_wait_s, stop_strings=ce.stop_strings)
+        return self._new_continuous(ce.steps_per_sync, ce.min_admit, ce.max_wait_s)
 
     def stop_continuous(self) -> None:
         if getattr(self, "_ce", None) is None:
@@ -281,6 +334,10 @@ class HipLLMSummarizer(Summarizer):
             self._ce_stop = True
             self._cv.notify()
         self._ce_thread.join(timeout=30)
+        if self._ce_thread.is_alive():
+            return             # a step is still running on the device: leave the engine to it
+        if self.tp_hook is not None:
+            self.tp_hook(("cstop",))
         self._ce.close()
         self._ce = None
 

@@ -56,10 +56,10 @@ __device__ __forceinline__ float pg_gelu(float v) { return 0.5f * v * (1.f + erf
 
 __device__ __forceinline__ float pg_bfr(float v) { return bf2f(f2bf(v)); }
 
-// Epilogue of both kernels: lane holds rows m = mw + 16 i + (lane & 15), columns
-// n = nw + 16 j + 4 (lane >> 4) + 0..3 of the wave's 128 x 64 block.
-template <int EPI>
-__device__ __forceinline__ void pg_epilogue(const f32x4_t (&acc)[8][4], const uint16_t* __restrict__ bias,
+// Epilogue of every kernel here: lane holds rows m = mw + 16 i + (lane & 15), columns
+// n = nw + 16 j + 4 (lane >> 4) + 0..3 of the wave's 128 x 16 NJ block.
+template <int EPI, int NJ>
+__device__ __forceinline__ void pg_epilogue(const f32x4_t (&acc)[8][NJ], const uint16_t* __restrict__ bias,
                                             uint16_t* __restrict__ out, int M, int N, int ldo, int mw, int nw) {
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
@@ -67,7 +67,7 @@ __device__ __forceinline__ void pg_epilogue(const f32x4_t (&acc)[8][4], const ui
   for (int i = 0; i < 8; ++i) {
     const int m = mw + i * 16 + (lane & 15);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int nb = nw + j * 16;   // n-tile base
       const int n = nb + 4 * g;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
@@ -324,6 +324,214 @@ __global__ void __launch_bounds__(512, 1)
 }
 
 
+// ---- v3: ping-pong of two wave groups over half-tile LDS-DMA stages ------------------------------
+// The 2-stage kernel above waits 30-35 % of its cycles (profiles/r03s2_pmc_pgemm_vs_hipblaslt.txt):
+// every wave reaches the tile's vmcnt(0) + barrier at once, then all read LDS at once, and nothing
+// covers either.  Here the 8 waves are two groups of 4 (waves 0-3, 4-7: one of each on every SIMD),
+// run one barrier apart, so on each SIMD one wave's MFMA segment covers its partner's load segment
+// (LDS-DMA issue, fragment ds_reads, counted vmcnt) and the matrix pipe never waits for either
+// (guide §5 "The 256² 8-phase template", MI355X_MICROARCH "Two waves per SIMD").
+//
+//   * tile 256 x 256, BK = 64; wave (grp, wc) owns output rows 128 grp .. +128, cols 64 wc .. +64;
+//   * a K-tile is 4 half-tiles of 16 KB: X0 = X tile rows {0-63, 128-191}, X1 = {64-127, 192-255},
+//     W0 = W rows 0-127, W1 = W rows 128-255; two K-tile buffers = 128 KB of LDS;
+//   * K-tile kt runs in two segments of 32 MFMAs per wave: A (X0 and both W halves: the wave's first
+//     64 rows) and B (X1: its last 64 rows, W fragments kept in registers);
+//   * stream of half-tiles: segment A of tile kt issues tile kt+1's {W1, X1}, segment B issues tile
+//     kt+2's {X0, W0} -- each into a half whose last reader (either group) retired its ds_reads
+//     (lgkmcnt(0)) before the barrier that precedes the issue; counted vmcnt(8) / vmcnt(6) leave
+//     2-3 half-tiles of DMA in flight per wave (48-64 KB per CU) and retire exactly what the next
+//     segment reads, one barrier (two for the lagging group) ahead of the read;
+//   * X image: 128 rows x 128 B per half, chunk c of image row r at r*128 + ((c ^ (r & 7)) << 4)
+//     (swizzled through the DMA SOURCE address, guide rule 21), 8-row x 128-B pieces;
+//   * W: row-major as X, or fragment-packed (the decode GEMM's cfc_dgemm_pack layout, wnw = its
+//     bn / 16): every 16-row x 32-k MFMA fragment is 1 KB contiguous in lane order, so each DMA piece
+//     is one whole fragment and its ds_read_b128 at lane * 16 is conflict free -- one weight copy
+//     serves prefill and decode.
+constexpr int PP_HALF = 128 * 128;        // bytes of one half-tile (128 rows x 64 k bf16)
+constexpr int PP_BUF = 4 * PP_HALF;       // X0 X1 W0 W1
+
+__device__ __forceinline__ void pp_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+template <int N>
+__device__ __forceinline__ void pp_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
+}
+
+// PF: probe flags (scripts/bench_pgemm.py --probe; 0 in production): 1 = no s_setprio, 2 = static
+// priority 1 for group 1 instead of per-segment flips.  gm = M-tiles per N sweep of the tile order.
+template <int EPI, bool PACKED, int PF = 0>
+__global__ void __launch_bounds__(512, 1)
+    pgemm_pp_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W, const uint16_t* __restrict__ bias,
+                    uint16_t* __restrict__ out, int M, int N, int K, int ldo, int tiles_m, int tiles_n, int wnw,
+                    int gm = PG_GROUP_M) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * PP_BUF];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = w >> 2, wc = w & 3;
+
+  const int nwg = tiles_m * tiles_n;
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int per_group = gm * tiles_n;
+  const int first_m = (id / per_group) * gm;
+  const int gsz = min(tiles_m - first_m, gm);
+  const int in_group = id % per_group;
+  const int m0 = (first_m + in_group % gsz) * PG_BM;
+  const int n0 = (in_group / gsz) * PG_BN;
+  const int nk = K / PG_BK;
+
+  // ---- DMA sources.  X: pieces w and w + 8 of half h = image rows 8 p .. 8 p + 7 (lane: row
+  // lane >> 3, chunk lane & 7 through the swizzle; image row r is tile row (r >> 6) * 128 + 64 h + (r & 63))
+  uint32_t vx[2][2], vw[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = 8 * (w + 8 * i) + (lane >> 3);
+      const int trow = (r >> 6) * 128 + 64 * h + (r & 63);
+      const int c = (lane & 7) ^ (r & 7);
+      vx[h][i] = ((uint32_t)min(m0 + trow, M - 1) * (uint32_t)K + 8u * c) * 2u;
+    }
+  // W half h, pieces w and w + 8.  Packed: piece f = fragment (n-tile f >> 1 of the half, k group
+  // f & 1 of the K-tile); its 1 KB sits at ((g / wnw) * K/32 + kg) * wnw + g % wnw fragments
+  // (cfc_dgemm_pack).  Row-major: as X, image row r = W tile row 128 h + r.
+  const int kg_all = K / 32;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if constexpr (PACKED) {
+        const int f = w + 8 * i;
+        const int g = min(n0 / 16 + 8 * h + (f >> 1), N / 16 - 1);
+        vw[h][i] = (uint32_t)(((g / wnw) * kg_all + (f & 1)) * wnw + g % wnw) * 1024u + 16u * lane;
+      } else {
+        const int r = 8 * (w + 8 * i) + (lane >> 3);
+        const int c = (lane & 7) ^ (r & 7);
+        vw[h][i] = ((uint32_t)min(n0 + 128 * h + r, N - 1) * (uint32_t)K + 8u * c) * 2u;
+      }
+    }
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(pg_lds_t*)smem + w * 1024);
+  // per K-tile advance of the W source: 2 fragments of every 16-row group (packed) or 64 columns
+  const size_t wstep = PACKED ? (size_t)2 * wnw * 512 : (size_t)PG_BK;
+  auto issue_x = [&](int kt, int h) {
+    const uint16_t* src = X + (size_t)kt * PG_BK;
+    const uint32_t la = lds0 + (kt & 1) * PP_BUF + h * PP_HALF;
+    pg_glds16(vx[h][0], src, la);
+    pg_glds16(vx[h][1], src, la + 8192);
+  };
+  auto issue_w = [&](int kt, int h) {
+    const uint16_t* src = W + (size_t)kt * wstep;
+    const uint32_t la = lds0 + (kt & 1) * PP_BUF + (2 + h) * PP_HALF;
+    pg_glds16(vw[h][0], src, la);
+    pg_glds16(vw[h][1], src, la + 8192);
+  };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // fragment reads.  X: image row 64 grp + 16 i + (lane & 15) of the half, chunk 4 kk + (lane >> 4)
+  // through the swizzle (row & 7 == lane & 7).  W n-tile T = 4 wc + j lies in half T >> 3.
+  const int xrd = (64 * grp + (lane & 15)) * 128;
+  const int sw = lane & 7;
+  auto rd_x = [&](int buf, int h, int i, int kk) {
+    return *reinterpret_cast<const bf16x8_t*>(smem + buf + h * PP_HALF + xrd + i * 16 * 128 +
+                                              (((4 * kk + (lane >> 4)) ^ sw) << 4));
+  };
+  auto rd_w = [&](int buf, int j, int kk) {
+    const int T = 4 * wc + j;
+    const char* half = smem + buf + (2 + (T >> 3)) * PP_HALF;
+    if constexpr (PACKED) {
+      return *reinterpret_cast<const bf16x8_t*>(half + (2 * (T & 7) + kk) * 1024 + 16 * lane);
+    } else {
+      return *reinterpret_cast<const bf16x8_t*>(half + (16 * (T & 7) + (lane & 15)) * 128 +
+                                                (((4 * kk + (lane >> 4)) ^ sw) << 4));
+    }
+  };
+
+  // ---- prologue: tile 0 whole, tile 1's {X0, W0}; tile 0's X0 / W0 / W1 landed in every wave
+  issue_x(0, 0);
+  issue_w(0, 0);
+  issue_w(0, 1);
+  issue_x(0, 1);
+  if (nk > 1) {
+    issue_x(1, 0);
+    issue_w(1, 0);
+    pp_wait_barrier<6>();
+  } else {
+    pp_wait_barrier<2>();
+  }
+  if (grp == 1) pp_barrier();   // the stagger: group 1 runs one barrier behind group 0
+  if constexpr ((PF & 2) != 0) {
+    if (grp == 1) __builtin_amdgcn_s_setprio(1);
+  }
+  constexpr bool FLIP = (PF & 3) == 0;
+
+  bf16x8_t wf[4][2], xf[4][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = (kt & 1) * PP_BUF;
+    // ======== segment A: load part (tile kt+1's W1 / X1 into the other buffer; fragments)
+    if (kt + 1 < nk) {
+      issue_w(kt + 1, 1);
+      issue_x(kt + 1, 1);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) wf[j][kk] = rd_w(buf, j, kk);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) xf[i][kk] = rd_x(buf, 0, i, kk);
+    // retire tile kt's X1 (segment B reads it) and this wave's ds_reads
+    if (kt + 1 < nk) pp_wait_barrier<8>();
+    else pp_wait_barrier<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (FLIP) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][kk], xf[i][kk], acc[i][j], 0, 0, 0);
+    if constexpr (FLIP) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    pp_barrier();
+    // ======== segment B: load part (tile kt+2's X0 / W0 into this buffer's free halves)
+    if (kt + 2 < nk) {
+      issue_x(kt + 2, 0);
+      issue_w(kt + 2, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) xf[i][kk] = rd_x(buf, 1, i, kk);
+    // retire tile kt+1's X0 / W0 / W1 (next segment A reads them)
+    if (kt + 2 < nk) pp_wait_barrier<6>();
+    else if (kt + 1 < nk) pp_wait_barrier<2>();
+    else pp_wait_barrier<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (FLIP) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][kk], xf[i][kk], acc[4 + i][j], 0, 0, 0);
+    if constexpr (FLIP) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    pp_barrier();
+  }
+
+  // wave rows: segment A's m-tiles i = tile rows 128 grp + 16 i, segment B's = 128 grp + 64 + 16 i
+  pg_epilogue<EPI>(acc, bias, out, M, N, ldo, m0 + grp * 128, n0 + wc * 64);
+  if (grp == 0) pp_barrier();   // matches group 1's stagger barrier
+}
+
 
 // ---- encoder sub-layer epilogue: Y = LayerNorm(X . W^T + bias + residual) --------------------------
 // The post-LN BERT projections whose output width is the hidden size (o-proj K = hidden, FFN down
@@ -468,16 +676,161 @@ __global__ void __launch_bounds__(512, 1)
   }
 }
 
+// ---- v4: four waves of 128 x 128, one per SIMD, software-pipelined -----------------------------
+// The library's shape of the same tile (hipBLASLt MT256x256x64, 4 waves: profiles/
+// r03s2_pmc_pgemm_vs_hipblaslt.txt): a wave owns a 128 x 128 output block (64 accumulator tiles,
+// 256 registers -- the AGPR half of the file), so each MFMA costs half the LDS fragment bytes of the
+// 8-wave kernels' 128 x 64 blocks (16 ds_read_b128 per 64 MFMAs) -- less LDS traffic and less
+// energy per flop, which is what the clock under DVFS rewards (guide §5.4 rule 28).  With one wave
+// per SIMD nothing else covers its waits, so the wave pipelines itself:
+//   * K in 32-deep steps through a ring of 4 LDS stages (X image 256 rows x 64 B + W image 16
+//     fragments, 32 KB per stage); the DMA of step t + 4 is issued at the top of step t into the
+//     stage step t just vacated: three steps (~3k cycles of MFMA) to land;
+//   * fragments of step t + 1 are read from LDS into the second register set DURING step t's 64
+//     MFMAs (one ds_read_b128 per 3 MFMAs, all issued by MFMA 45 so they land before the step
+//     ends); the step's 8 DMA pieces are interleaved the same way;
+//   * one barrier per step, behind a counted vmcnt (step t + 1's DMA; t + 2, t + 3 stay in flight)
+//     and lgkmcnt(0) (step t + 1's fragments in registers, every read of stage t % 4 retired).
+// X image: 64-B rows (16-row x 64-B DMA pieces), chunk c of row r at r*64 + ((c ^ f((r >> 2) & 3)) << 4),
+// f = 0,3,2,1: conflict-free 16-row fragment reads (the ring kernel's image).  W: packed fragments
+// (1 KB each, lane order) or a row-major image like X.
+constexpr int W4_BK = 32;
+constexpr int W4_STAGE = (PG_BM + PG_BN) * W4_BK * 2;   // 32 KB
+constexpr int W4_NS = 4;
+
+template <int EPI, bool PACKED>
+__global__ void __launch_bounds__(256, 1)
+    pgemm_w4_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W, const uint16_t* __restrict__ bias,
+                    uint16_t* __restrict__ out, int M, int N, int K, int ldo, int tiles_m, int tiles_n, int wnw) {
+  __shared__ __attribute__((aligned(16))) char smem[W4_NS * W4_STAGE];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 1, wc = w & 1;
+
+  const int nwg = tiles_m * tiles_n;
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int per_group = PG_GROUP_M * tiles_n;
+  const int first_m = (id / per_group) * PG_GROUP_M;
+  const int gsz = min(tiles_m - first_m, PG_GROUP_M);
+  const int in_group = id % per_group;
+  const int m0 = (first_m + in_group % gsz) * PG_BM;
+  const int n0 = (in_group / gsz) * PG_BN;
+  const int ns = K / W4_BK;                       // even (K % 64 == 0)
+
+  // ---- DMA sources: pieces p = w + 4 i (i = 0..3) of each image.  X piece = image rows 16 p ..
+  // 16 p + 15 (lane: row lane >> 2, slot lane & 3 through the swizzle)
+  const int prow = lane >> 2, pch = (lane & 3) ^ pr_f((prow >> 2) & 3);
+  uint32_t vx[4], vw[4];
+  const int kg_all = K / 32;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p = w + 4 * i;
+    vx[i] = ((uint32_t)min(m0 + 16 * p + prow, M - 1) * (uint32_t)K + 8u * pch) * 2u;
+    if constexpr (PACKED) {
+      const int g = min(n0 / 16 + p, N / 16 - 1);
+      vw[i] = (uint32_t)((g / wnw) * kg_all * wnw + g % wnw) * 1024u + 16u * lane;
+    } else {
+      vw[i] = ((uint32_t)min(n0 + 16 * p + prow, N - 1) * (uint32_t)K + 8u * pch) * 2u;
+    }
+  }
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(pg_lds_t*)smem + w * 1024);
+  const size_t wstep = PACKED ? (size_t)wnw * 512 : (size_t)W4_BK;   // per step: one k group / 32 columns
+  auto issue_piece = [&](int t, int i) {        // piece i (0..3: X, 4..7: W) of step t
+    const uint32_t la = lds0 + (t & (W4_NS - 1)) * W4_STAGE;
+    if (i < 4) pg_glds16(vx[i], X + (size_t)t * W4_BK, la + i * 4096);
+    else pg_glds16(vw[i - 4], W + (size_t)t * wstep, la + PG_BM * 64 + (i - 4) * 4096);
+  };
+
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // fragment reads of step t: X m-tile i = image rows 16 (8 wr + i) + (lane & 15); W n-tile j
+  const int fr = lane & 15;
+  const int xch = ((lane >> 4) ^ pr_f((fr >> 2) & 3)) << 4;
+  const char* xrd = smem + (wr * 128 + fr) * 64 + xch;
+  const char* wrd = PACKED ? smem + PG_BM * 64 + wc * 8 * 1024 + 16 * lane : smem + PG_BM * 64 + (wc * 128 + fr) * 64 + xch;
+  auto rd_x = [&](int t, int i) {
+    return *reinterpret_cast<const bf16x8_t*>(xrd + (t & (W4_NS - 1)) * W4_STAGE + i * 16 * 64);
+  };
+  auto rd_w = [&](int t, int j) {
+    return *reinterpret_cast<const bf16x8_t*>(wrd + (t & (W4_NS - 1)) * W4_STAGE + j * (PACKED ? 1024 : 16 * 64));
+  };
+
+  // ---- prologue: steps 0..3 issued, step 0 landed everywhere, its fragments in set A
+#pragma unroll
+  for (int t = 0; t < W4_NS; ++t)
+    if (t < ns)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) issue_piece(t, i);
+  {
+    const int ahead = min(ns - 1, W4_NS - 1);     // steps issued after step 0
+    if (ahead >= 3) pp_wait_barrier<24>();
+    else if (ahead == 2) pp_wait_barrier<16>();
+    else pp_wait_barrier<8>();
+  }
+  bf16x8_t fa_x[8], fa_w[8], fb_x[8], fb_w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa_x[i] = rd_x(0, i);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fa_w[j] = rd_w(0, j);
+
+  // One step: wait for step t + 1's DMA and every wave's reads of stage t, barrier, DMA of step
+  // t + 4 into stage t, 64 MFMAs on (cx, cw) with step t + 1's fragments read into (nx, nw).
+#define W4_STEP(T, CX, CW, NX, NWF)                                                                     \
+  do {                                                                                                  \
+    const int t_ = (T);                                                                                 \
+    const int ahead_ = min(ns - 1, t_ + 3) - (t_ + 1);    /* steps issued after step t+1 */            \
+    if (ahead_ >= 2) pp_wait_barrier<16>();                                                             \
+    else if (ahead_ == 1) pp_wait_barrier<8>();                                                         \
+    else pp_wait_barrier<0>();                                                                          \
+    const bool more_ = t_ + 1 < ns, dma_ = t_ + W4_NS < ns;                                             \
+    __builtin_amdgcn_sched_barrier(0);                                                                  \
+    _Pragma("unroll") for (int q = 0; q < 16; ++q) {                                                    \
+      _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                                   \
+        const int mm = 4 * q + e, i = mm >> 3, j = mm & 7;                                              \
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(CW[j], CX[i], acc[i][j], 0, 0, 0);          \
+      }                                                                                                 \
+      if (q < 12) {                                                                                     \
+        if (more_) {                                                                                    \
+          if (q < 8) NX[q] = rd_x(t_ + 1, q);                                                           \
+          else NWF[q - 8] = rd_w(t_ + 1, q - 8);                                                        \
+          if (q >= 8) NWF[q - 4] = rd_w(t_ + 1, q - 4);                                                 \
+        }                                                                                               \
+        if (q < 8 && dma_) issue_piece(t_ + W4_NS, q);                                                  \
+      }                                                                                                 \
+      __builtin_amdgcn_sched_barrier(0);                                                                \
+    }                                                                                                   \
+  } while (0)
+
+  for (int t = 0; t < ns; t += 2) {
+    W4_STEP(t, fa_x, fa_w, fb_x, fb_w);
+    W4_STEP(t + 1, fb_x, fb_w, fa_x, fa_w);
+  }
+#undef W4_STEP
+
+  pg_epilogue<EPI>(acc, bias, out, M, N, ldo, m0 + wr * 128, n0 + wc * 128);
+}
+
 template <int EPI>
 int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int M, int N, int K, int ldo,
-                 int variant, hipStream_t stream) {
+                 int variant, int wnw, hipStream_t stream) {
   const int tm = (M + PG_BM - 1) / PG_BM, tn = (N + PG_BN - 1) / PG_BN;
   const uint16_t *xp = (const uint16_t*)x, *wp = (const uint16_t*)w, *bp = (const uint16_t*)bias;
   uint16_t* op = (uint16_t*)out;
+  if (wnw > 0) {   // fragment-packed W: the ping-pong (default) or the 4-wave kernel
+    if (variant == 4) pgemm_w4_kernel<EPI, true><<<tm * tn, 256, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, wnw);
+    else pgemm_pp_kernel<EPI, true><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, wnw);
+    return (int)hipGetLastError();
+  }
   switch (variant) {
     case 0: pgemm_ring_kernel<EPI, 5><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn); break;
     case 1: pgemm_kernel<EPI><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn); break;
     case 2: pgemm_ring_kernel<EPI, 4><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn); break;
+    case 3: pgemm_pp_kernel<EPI, false><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, 1); break;
+    case 4: pgemm_w4_kernel<EPI, false><<<tm * tn, 256, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, 1); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
@@ -486,22 +839,43 @@ int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int 
 }  // namespace
 
 // epi & 15: 0 bf16, 1 + bias, 2 + bias -> GELU, 3 SwiGLU (out [M, N/2]); epi >> 4: K-loop variant
-// (0 BK = 32 ring of 5 slots, 1 the 2-stage BK = 64 kernel -- the Python default, measured fastest,
-// 2 ring of 4 slots); ldo = output row stride.
+// for a row-major W (0 BK = 32 ring of 5 slots, 1 the 2-stage BK = 64 kernel, 2 ring of 4 slots,
+// 3 the ping-pong kernel); ldo = output row stride.  wnw > 0: W is in the decode GEMM's
+// fragment-packed layout for bn = 16 wnw (cfc_dgemm_pack; N % (16 wnw) == 0) and runs on the
+// ping-pong kernel whatever the variant.
 CFC_API int cfc_pgemm(const void* x, const void* w, const void* bias, void* out, int M, int N, int K, int epi_v,
-                      int ldo, hipStream_t stream) {
+                      int ldo, int wnw, hipStream_t stream) {
   const int epi = epi_v & 15, variant = epi_v >> 4;
   if (M < 1 || N < 64 || K < 64 || K % 64 || N % 64 || ldo % 4 || (epi != 3 && ldo < N) ||
       (epi == 3 && ldo < N / 2) || (uint64_t)M * K * 2 >= (1ull << 32) || (uint64_t)N * K * 2 >= (1ull << 32) ||
-      ((epi == 1 || epi == 2) && bias == nullptr))
+      ((epi == 1 || epi == 2) && bias == nullptr) || wnw < 0 || (wnw > 0 && N % (16 * wnw)))
     return (int)hipErrorInvalidValue;
   switch (epi) {
-    case 0: return pgemm_launch<PG_BF16>(x, w, bias, out, M, N, K, ldo, variant, stream);
-    case 1: return pgemm_launch<PG_BIAS>(x, w, bias, out, M, N, K, ldo, variant, stream);
-    case 2: return pgemm_launch<PG_BIAS_GELU>(x, w, bias, out, M, N, K, ldo, variant, stream);
-    case 3: return pgemm_launch<PG_SWIGLU>(x, w, bias, out, M, N, K, ldo, variant, stream);
+    case 0: return pgemm_launch<PG_BF16>(x, w, bias, out, M, N, K, ldo, variant, wnw, stream);
+    case 1: return pgemm_launch<PG_BIAS>(x, w, bias, out, M, N, K, ldo, variant, wnw, stream);
+    case 2: return pgemm_launch<PG_BIAS_GELU>(x, w, bias, out, M, N, K, ldo, variant, wnw, stream);
+    case 3: return pgemm_launch<PG_SWIGLU>(x, w, bias, out, M, N, K, ldo, variant, wnw, stream);
     default: return (int)hipErrorInvalidValue;
   }
+}
+
+// Timing probe only (scripts/bench_pgemm.py --probe): the ping-pong kernel, bf16 epilogue, packed W
+// (wnw > 0), probe flags pf (see pgemm_pp_kernel) and tile-order group gm.
+CFC_API int cfc_pgemm_probe(const void* x, const void* w, void* out, int M, int N, int K, int wnw, int pf, int gm,
+                            hipStream_t stream) {
+  if (M < 1 || K % 64 || N % 64 || wnw < 1 || N % (16 * wnw) || gm < 1) return (int)hipErrorInvalidValue;
+  const int tm = (M + PG_BM - 1) / PG_BM, tn = (N + PG_BN - 1) / PG_BN;
+  const uint16_t *xp = (const uint16_t*)x, *wp = (const uint16_t*)w;
+  uint16_t* op = (uint16_t*)out;
+#define PP_PROBE(F) pgemm_pp_kernel<PG_BF16, true, F><<<tm * tn, 512, 0, stream>>>(xp, wp, nullptr, op, M, N, K, N, tm, tn, wnw, gm); break;
+  switch (pf) {
+    case 0: PP_PROBE(0)
+    case 1: PP_PROBE(1)
+    case 2: PP_PROBE(2)
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef PP_PROBE
+  return (int)hipGetLastError();
 }
 
 // Y[M, N] = LayerNorm(X[M, K] . W[N, K]^T + bias + residual) * gamma + beta, N = 384 (the encoder

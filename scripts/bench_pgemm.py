@@ -70,7 +70,9 @@ def main():
     ap.add_argument("--shapes", nargs="*", default=list(SHAPES))
     ap.add_argument("--m", type=int, default=None, help="override M")
     ap.add_argument("--out", default="gpurun_out/pgemm.jsonl")
-    ap.add_argument("--variants", nargs="*", default=["stage2", "ring5", "ring4"])
+    ap.add_argument("--variants", nargs="*", default=["stage2", "pp", "packed"],
+                    help="row-major K loops (stage2 / ring5 / ring4 / pp / w4) and 'packed' / 'packed_w4' = "
+                         "the ping-pong / 4-wave kernel on the decode GEMM's fragment-packed weight")
     ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
     enable_tuned_gemms()
@@ -95,14 +97,21 @@ def main():
             ref = R.silu_mul_interleaved(ref.bfloat16()).float()
         flops = 2.0 * M * N * Kd
         fns = {"lib": lib_fn(x, w, b, epi)}
+        pw = (K.pack_dgemm_weight(w, swiglu=epi == "swiglu") if any(v.startswith("packed") for v in args.variants)
+              else None)
+
+        def run(v, xx):
+            if v.startswith("packed"):      # packed = ping-pong, packed_w4 = the 4-wave kernel
+                return K.pgemm(xx, pw, epi, bias=b, variant=v[7:] or "pp")
+            return K.pgemm(xx, w, epi, bias=b, variant=v)
         for v in args.variants:
-            row[f"err_{v}"] = rel_err(K.pgemm(xs, w, epi, bias=b, variant=v), ref)
-            fns[v] = (lambda v=v: K.pgemm(x, w, epi, bias=b, variant=v))
+            row[f"err_{v}"] = rel_err(run(v, xs), ref)
+            fns[v] = (lambda v=v: run(v, x))
         # whole-matrix agreement of each variant with the 2-stage kernel (same fp32 sums per tile)
         y0 = K.pgemm(x, w, epi, bias=b, variant="stage2")
         for v in args.variants:
             if v != "stage2":
-                row[f"maxdiff_{v}_vs_stage2"] = float((K.pgemm(x, w, epi, bias=b, variant=v).float() - y0.float()).abs().max())
+                row[f"maxdiff_{v}_vs_stage2"] = float((run(v, x).float() - y0.float()).abs().max())
         del y0
         ts = {k: [] for k in fns}
         for _ in range(args.rounds):          # interleaved rounds in one process (guide rule 24)
@@ -118,7 +127,7 @@ def main():
         print(json.dumps(row), flush=True)
         fh.write(json.dumps(row) + "\n")
         fh.flush()
-        del x, w
+        del x, w, pw
         torch.cuda.empty_cache()
 
 

@@ -137,3 +137,57 @@ def test_bulk_admission_fills_a_mostly_empty_batch_in_one_prefill():
     assert out[0.5][1] == 1
     assert out[0.0][1] == 4          # 91-token prompts, 200-token budget: 2 per admission
     assert out[0.5][0] == out[0.0][0]
+
+
+def _hip_summarizer(**kw):
+    from copilot_for_consensus_amd.summarization import HipLLMSummarizer
+    return HipLLMSummarizer(model="tiny", device="cpu", kv_cache_tokens=8192, ignore_eos=True, **kw)
+
+
+def test_stop_continuous_fails_every_unfinished_thread_exactly_once():
+    """Stopping the service engine with threads queued and running: every submitted thread gets
+    its callback exactly once -- a summary or an error -- so none is dropped silently."""
+    import collections
+    import time
+
+    from copilot_for_consensus_amd.summarization import Thread
+    s = _hip_summarizer(max_new_tokens=300, max_batch=2)
+    s.start_continuous(steps_per_sync=4, min_admit=1, max_wait_s=0.0)
+    calls, errs = collections.Counter(), {}
+
+    def cb(tid):
+        def done(summary, err):
+            calls[tid] += 1
+            errs[tid] = err
+        return done
+    for i in range(6):
+        s.submit(Thread(f"t{i}", ["m"], prompt="word " * 30), cb(f"t{i}"))
+    time.sleep(0.3)
+    s.stop_continuous()
+    assert sorted(calls) == [f"t{i}" for i in range(6)] and set(calls.values()) == {1}, calls
+    assert any(e is not None for e in errs.values())       # 2 slots x 300 tokens: not all could finish
+    with pytest.raises(RuntimeError):        # a stopped engine refuses new threads (the bus redelivers)
+        s.submit(Thread("late", ["m"]), cb("late"))
+
+
+def test_raising_done_callback_is_not_called_twice():
+    """A callback that raises (e.g. its publish failed after the summary was built) is logged, not
+    re-invoked with an error -- a second call would publish SummarizationFailed for a thread whose
+    SummaryComplete may already be out."""
+    import time
+
+    from copilot_for_consensus_amd.summarization import Thread
+    s = _hip_summarizer(max_new_tokens=4, max_batch=2)
+    s.start_continuous(steps_per_sync=2, min_admit=1, max_wait_s=0.0)
+    seen = []
+
+    def done(summary, err):
+        seen.append((summary is not None, err))
+        raise ConnectionError("bus down")
+    s.submit(Thread("x", ["m"], prompt="word " * 10), done)
+    deadline = time.time() + 60
+    while not seen and time.time() < deadline:
+        time.sleep(0.02)
+    time.sleep(0.2)
+    s.stop_continuous()
+    assert seen == [(True, None)], seen

@@ -157,3 +157,77 @@ def test_services_main_torchrun_roles():
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
+
+
+_TP_NODE_ENV = {"DOCUMENT_STORE_TYPE": "inmemory", "MESSAGE_BUS_TYPE": "inproc", "METRICS_TYPE": "noop",
+                "LOG_TYPE": "silent", "ERROR_REPORTER_TYPE": "silent", "EMBEDDING_BACKEND_TYPE": "mock",
+                "VECTOR_STORE_TYPE": "inmemory", "ARCHIVE_STORE_TYPE": "inmemory", "SECRET_PROVIDER_TYPE": "env",
+                "LLM_BACKEND_TYPE": "hip", "LLM_MODEL_PRESET": "tiny", "CFC_TP": "2", "LLM_DEVICE": "cpu",
+                "LLM_MAX_NEW_TOKENS": "8", "LLM_KV_CACHE_TOKENS": "8192", "LLM_MAX_BATCH": "8",
+                "SUMMARIZATION_CONTINUOUS_BATCHING": "true", "CFC_DIST_BACKEND": "gloo", "CUDA_VISIBLE_DEVICES": ""}
+
+
+def _tp_node_rank(rank, port, src_dir, q):
+    os.environ.update(_TP_NODE_ENV, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+                      LOCAL_RANK=str(rank))
+    import torch
+    torch.set_num_threads(2)
+    try:
+        from copilot_for_consensus_amd.services import main as M
+        ctx = M._distributed()
+        if not ctx["serve"]:
+            q.put((rank, "follower", M._model_rank(ctx)))
+            return
+        from copilot_for_consensus_amd.services.node import Node
+        node = Node(env=_TP_NODE_ENV, summarizer=ctx["summarizer"])
+        node.start(threaded=True)
+        try:
+            ing = node.services["ingestion"]
+            ing.create_source({"name": "tp", "source_type": "local", "url": src_dir})
+            ing.trigger_ingestion("tp")
+            deadline = time.time() + 240
+            while time.time() < deadline and node.store.count_documents("summaries") < 2:
+                time.sleep(0.1)
+            sums = node.store.query_documents("summaries", {}, limit=10)
+            engine = ctx["local"]._ce
+            q.put((rank, "leader", type(ctx["summarizer"]).__name__, len(sums), dict(engine.stats) if engine else None))
+        finally:
+            node.stop()
+            M._close_distributed(ctx)
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_services_main_tp2_continuous_node_summarizes_and_exits(tmp_path):
+    """services.main roles with CFC_TP=2 and continuous batching on (tiny decoder, 2 gloo ranks on
+    the CPU): rank 0 runs the whole node, its summarizer the TP leader's continuous engine; rank 1
+    replays every engine step (prefills, decode bursts: their all-reduces pair up).  The node
+    summarizes the fixture's threads through the bus and both ranks exit cleanly -- the round-3
+    deadlock (followers waiting on a broadcast the continuous engine never sent) is gone."""
+    import shutil
+    src = tmp_path / "src"
+    src.mkdir()
+    shutil.copy(os.path.join(os.path.dirname(__file__), "fixtures", "sample.mbox"), src / "a.mbox")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tp_node_rank, args=(r, port, str(src), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        got = {}
+        for _ in procs:
+            item = q.get(timeout=300)
+            got[item[0]] = item
+        assert got[0][1] == "leader", got
+        assert got[0][2] == "HipLLMSummarizer" and got[0][3] == 2, got
+        assert got[0][4]["admitted"] == 2 and got[0][4]["finished"] == 2, got
+        assert got[1][1] == "follower" and got[1][2] == 0, got      # _model_rank exit code
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0, [p.exitcode for p in procs]
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()

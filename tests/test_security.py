@@ -362,3 +362,25 @@ def test_refresh_refuses_sessions_past_max_lifetime_and_denied_users():
     svc.roles.deny("mock:alice")
     with pytest.raises(PermissionError, match="denied"):
         svc.refresh(tok)
+
+
+def test_public_key_check_reads_jwk_and_rejects_mismatch():
+    """A configured public key given as a JWK / JWKS is compared with the private key too (not only
+    PEM): the matching key passes, another key or an unreadable value is refused."""
+    import json
+
+    from copilot_for_consensus_amd.security.jwt import ECKey, ECSigner, JWTError, RSAKey, RSASigner
+    rk, other = RSAKey.generate(1024), RSAKey.generate(1024)
+    RSASigner(rk, public_key=json.dumps(rk.public_jwk("k")))
+    RSASigner(rk, public_key=json.dumps({"keys": [rk.public_jwk("k")]}))
+    RSASigner(rk, public_key=J.rsa_public_pem(rk))
+    with pytest.raises(JWTError):
+        RSASigner(rk, public_key=json.dumps(other.public_jwk("k")))
+    with pytest.raises(JWTError):
+        RSASigner(rk, public_key="not a key")
+    ek = ECKey.generate()
+    ECSigner(ek, public_key=json.dumps(ek.public_jwk("e")))
+    with pytest.raises(JWTError):
+        ECSigner(ek, public_key=json.dumps(ECKey.generate().public_jwk("e")))
+    with pytest.raises(JWTError):          # an RSA public key for an EC private key
+        ECSigner(ek, public_key=json.dumps(rk.public_jwk("k")))
