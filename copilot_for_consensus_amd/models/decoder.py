@@ -133,6 +133,7 @@ class DecoderWeights:
         # (K.PackedWeight): pack_decode()
         self.packed: list[dict] | None = None
         self.packed_lm_head = None
+        self.packed_only = False      # row-major projections dropped after packing
         self.cos_sin = rope_cos_sin(cfg.max_positions, cfg.head_dim, cfg.rope_theta, device=self.device,
                                     llama3_scaling=cfg.rope_llama3)
 
@@ -314,21 +315,39 @@ class DecoderWeights:
         n = sum(layer[k].numel() * 2 for layer in self.layers for k in self.DECODE_PACKED if layer.get(k) is not None)
         return n + (self.lm_head.numel() * 2 if self.lm_head is not None else 0)
 
-    def pack_decode(self, m: int = 128) -> "DecoderWeights":
-        """Copy every decode projection (and the lm_head) into the decode GEMM's fragment-packed
-        layout, tiled for an m-row batch (K.pack_dgemm_weight: each 16-row x 32-k MFMA fragment 1 KB
+    def pack_decode(self, m: int = 128, drop_rowmajor: bool = False) -> "DecoderWeights":
+        """Copy every projection (and the lm_head) into the decode GEMM's fragment-packed layout,
+        tiled for an m-row batch (K.pack_dgemm_weight: each 16-row x 32-k MFMA fragment 1 KB
         contiguous, each workgroup's slice one contiguous span -- the flat stream runs at ~5.8 TB/s
-        where row-major fragments read at 4-5).  The row-major copies stay for prefill (hipBLASLt)
-        and the B <= 4 GEMV, so this costs packed_bytes() more HBM (14.5 GB for Mistral-7B):
-        DecoderModel takes it only where that fits."""
+        where row-major fragments read at 4-5).  The prefill GEMM (pgemm.hip) reads the same packed
+        copy.  ``drop_rowmajor``: free each row-major projection as soon as its packed copy exists
+        (one weight copy; peak HBM = the weights + one layer), otherwise both stay (the row-major
+        one for the B <= 4 GEMV and the library paths; packed_bytes() more HBM)."""
         if self.packed is not None:
             return self
-        self.packed = [{k: K.pack_dgemm_weight(layer[k], swiglu=k == "gate_up", m=m) for k in self.DECODE_PACKED}
-                       for layer in self.layers]
+        self.packed = []
+        for layer in self.layers:
+            self.packed.append({k: K.pack_dgemm_weight(layer[k], swiglu=k == "gate_up", m=m)
+                                for k in self.DECODE_PACKED})
+            if drop_rowmajor:
+                for k in self.DECODE_PACKED:
+                    layer[k] = None
+        self.packed_only = bool(drop_rowmajor)
         head = self.lm_head
         if head is not None and head.shape[0] % 64 == 0 and head.shape[1] % 64 == 0:
             self.packed_lm_head = K.pack_dgemm_weight(head, m=m)
+        if drop_rowmajor and self.device.type == "cuda":
+            torch.cuda.empty_cache()
         return self
+
+    def rowmajor_layer(self, i: int) -> dict[str, torch.Tensor]:
+        """Layer i's tensors with every projection row-major (unpacked from the packed copy when the
+        row-major one was dropped) -- for reference models and checkpoint export."""
+        out = dict(self.layers[i])
+        for k in self.DECODE_PACKED:
+            if out.get(k) is None and self.packed is not None:
+                out[k] = K._rowmajor(self.packed[i][k])
+        return out
 
     def nbytes(self) -> int:
         n = sum(t.numel() * t.element_size() for layer in self.layers for t in layer.values() if t is not None)
@@ -411,11 +430,15 @@ class DecoderModel:
             mode = "lib"          # W8A8: every projection through linear_fp8 (bf16 fused paths need bf16 weights)
         self.decode_gemm = mode
         # prefill GEMM (packed prompt rows): "hip" = the hand-written MFMA GEMM (csrc/kernels/pgemm.hip,
-        # SwiGLU fused into gate/up), "lib" = the library GEMM + silu_mul (CFC_PREFILL_GEMM)
+        # SwiGLU fused into gate/up, reading the packed weights), "lib" = the library GEMM + silu_mul
+        # (CFC_PREFILL_GEMM); CFC_PGEMM_VARIANT picks pgemm's K loop
         pm = os.environ.get("CFC_PREFILL_GEMM", self.PREFILL_GEMM_DEFAULT)
         if pm not in ("hip", "lib"):
             raise ValueError(f"CFC_PREFILL_GEMM={pm!r}: expected hip or lib")
         self.prefill_gemm = "lib" if self.fp8 else pm
+        self.pgemm_variant = os.environ.get("CFC_PGEMM_VARIANT", self.PGEMM_VARIANT_DEFAULT)
+        if self.pgemm_variant not in K.PGEMM_VARIANTS:
+            raise ValueError(f"CFC_PGEMM_VARIANT={self.pgemm_variant!r}: expected one of {sorted(K.PGEMM_VARIANTS)}")
         # B <= 4 decode steps on the GEMV kernel (needs the interleaved gate/up layout for SwiGLU)
         gemv_shapes = (self.cfg.hidden % 8 == 0 and (weights.heads * self.cfg.head_dim) % 8 == 0
                        and weights.ffn % 8 == 0 and self.cfg.head_dim % 2 == 0)
@@ -426,24 +449,48 @@ class DecoderModel:
         # B <= 4 decode on the ggml-quantized weights (GGUF checkpoints; csrc/kernels/quant.hip)
         self.decode_qgemv = (weights.qlayers is not None and os.environ.get("CFC_DECODE_QGEMV", "1") != "0"
                              and weights.tp_size == 1 and weights.gate_up_interleaved and not self.fp8)
-        # packed decode weights (CFC_DECODE_PACKED: auto = when HBM allows, 1 = always, 0 = never)
-        if self.fused_decode and weights.device.type == "cuda" and self._want_packed():
-            weights.pack_decode()
+        # packed weights (CFC_DECODE_PACKED: auto / 1 = pack, 0 = never): one fragment-packed copy read by
+        # the decode GEMM and the prefill GEMM.  The row-major copies are dropped (CFC_WEIGHTS_PACKED_ONLY:
+        # auto = when the decode and prefill both run on the packed copy, 1 = always, 0 = keep both)
+        if (self.fused_decode or self.prefill_gemm == "hip") and weights.device.type == "cuda":
+            pk = self._packing()
+            if pk is not None:
+                weights.pack_decode(drop_rowmajor=pk == "only")
+        if weights.packed_only:
+            # nothing may read the row-major projections any more (the B <= 4 GEMV reads the packed ones)
+            self.decode_gemm = "dgemm"
+            self.fused_decode = True
+            self.prefill_gemm = "hip"
 
-    PACKED_FREE_FRACTION = 0.3   # HBM left free after packing (KV pool, activations, workspaces)
-    PREFILL_GEMM_DEFAULT = "lib"
-    PGEMM_MIN_ROWS = 256         # fewer packed rows than one 256-row tile: the library GEMM
+    PACKED_FREE_FRACTION = 0.3   # HBM left free after packing when both copies are kept
+    PREFILL_GEMM_DEFAULT = "hip"
+    PGEMM_VARIANT_DEFAULT = "pp"
+    PGEMM_MIN_ROWS = 256         # fewer prompt rows than one 256-row tile: the decode GEMM (packed) or the library
 
-    def _want_packed(self) -> bool:
+    def _packing(self) -> str | None:
+        """None (row-major only), "both" (packed + row-major) or "only" (packed only)."""
         pk = os.environ.get("CFC_DECODE_PACKED", "auto")
         if pk not in ("auto", "0", "1"):
             raise ValueError(f"CFC_DECODE_PACKED={pk!r}: expected auto, 0 or 1")
-        if pk == "0" or not self.w.layers or self.w.layers[0].get("qkv") is None:
-            return False
+        po = os.environ.get("CFC_WEIGHTS_PACKED_ONLY", "auto")
+        if po not in ("auto", "0", "1"):
+            raise ValueError(f"CFC_WEIGHTS_PACKED_ONLY={po!r}: expected auto, 0 or 1")
+        if pk == "0" or not self.w.layers or self.w.layers[0].get("qkv") is None or not self._dgemm_shapes():
+            return None
+        if not self.w.gate_up_interleaved:
+            return None
+        # packed-only needs every consumer of the projections on the packed copy: the fused decode
+        # GEMM (not fp8 / a small-batch GEMV with quantized weights) and the hand-written prefill
+        only_ok = self.decode_gemm == "dgemm" and self.prefill_gemm == "hip" and not self.fp8 \
+            and self.w.qlayers is None
+        if po == "1" or (po == "auto" and only_ok):
+            if not only_ok:
+                raise ValueError("CFC_WEIGHTS_PACKED_ONLY=1 needs CFC_DECODE_GEMM=dgemm and CFC_PREFILL_GEMM=hip")
+            return "only"
         if pk == "1":
-            return True
+            return "both"
         free, total = torch.cuda.mem_get_info(self.w.device)
-        return free - self.w.packed_bytes() > self.PACKED_FREE_FRACTION * total
+        return "both" if free - self.w.packed_bytes() > self.PACKED_FREE_FRACTION * total else None
 
     def _dgemm_shapes(self) -> bool:
         """Every decode projection of this rank fits the decode GEMM (N % 64, K % 64)."""
@@ -460,12 +507,17 @@ class DecoderModel:
         return F.linear(x, self.w.layers[i][name])
 
     def _plin(self, i: int, name: str, x: torch.Tensor, epi: str = "bf16") -> torch.Tensor:
-        """Prefill projection: the hand-written pgemm when selected and the shape fits (``epi``
-        "swiglu" returns silu(gate) * up of the interleaved gate/up weights), else the library."""
-        wt = self.w.layers[i][name]
-        if (self.prefill_gemm == "hip" and x.is_cuda and x.shape[0] >= self.PGEMM_MIN_ROWS and x.is_contiguous()
-                and K.pgemm_ok(x, wt) and (epi != "swiglu" or self.w.gate_up_interleaved)):
-            return K.pgemm(x, wt, epi)
+        """Prefill projection (``epi`` "swiglu" returns silu(gate) * up of the interleaved gate/up
+        weights): the hand-written pgemm on the packed weight when selected and the shape fits;
+        fewer rows than one pgemm tile on the decode GEMM (same packed weight); else the library."""
+        pw = self.w.packed[i][name] if self.w.packed is not None else None
+        wt = pw if pw is not None else self.w.layers[i][name]
+        if self.prefill_gemm == "hip" and x.is_cuda and x.is_contiguous() and (
+                epi != "swiglu" or self.w.gate_up_interleaved):
+            if x.shape[0] >= self.PGEMM_MIN_ROWS and K.pgemm_ok(x, wt):
+                return K.pgemm(x, wt, epi, variant=self.pgemm_variant)
+            if pw is not None and K.dgemm_ok(x, pw):
+                return K.dgemm_swiglu(x, pw) if epi == "swiglu" else K.dgemm_linear(x, pw)
         y = self._lin(i, name, x)
         return K.silu_mul(y, interleaved=self.w.gate_up_interleaved) if epi == "swiglu" else y
 
@@ -526,7 +578,7 @@ class DecoderModel:
         cfg, w = self.cfg, self.w
         x = K.embedding(w.embed, ids)
         B = ids.shape[0]
-        if (self.fused_decode and x.is_cuda and B <= DGEMM_MAX_ROWS
+        if (self.fused_decode and x.is_cuda and (B <= DGEMM_MAX_ROWS or self.w.packed_only)
                 and not (B <= K.GEMV_MAX_M and (self.decode_gemv or self.decode_qgemv))):
             return self._forward_decode_fused(x, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
                                               part_blocks)
@@ -625,7 +677,10 @@ class DecoderModel:
         cfg, w = self.cfg, self.w
         B, eps = h.shape[0], cfg.rms_eps
         for i in range(cfg.layers):
+            # packed-only weights: the packed-weight GEMV reads the packed copies
             lw = w.layers[i]
+            if w.packed_only:
+                lw = dict(lw, **w.packed[i])
             qkv = K.gemv(h, lw["qkv"])
             q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
                                 cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)

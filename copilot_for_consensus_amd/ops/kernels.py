@@ -601,27 +601,34 @@ def pgemm_ln(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, residual: tor
 GEMV_MAX_M = 4   # decode batches up to this size take the weight-streaming GEMV (gemm.hip: gemv_kernel)
 
 
-def gemv(x: torch.Tensor, w: torch.Tensor, epi: str = "bf16", out: torch.Tensor | None = None) -> torch.Tensor:
+def gemv(x: torch.Tensor, w, epi: str = "bf16", out: torch.Tensor | None = None) -> torch.Tensor:
     """x [M <= 4, K] @ w[N, K]^T on the GEMV kernel.  ``epi``: "bf16" -> bf16 [M, N]; "f32" -> fp32
-    [M, N]; "swiglu" -> bf16 [M, N/2] = silu(gate) * up for 8-row interleaved gate/up weights."""
+    [M, N]; "swiglu" -> bf16 [M, N/2] = silu(gate) * up for 8-row interleaved gate/up weights.
+    ``w``: row-major bf16 or a PackedWeight (the packed-weight GEMV: one weight copy)."""
+    packed = isinstance(w, PackedWeight)
     if not x.is_cuda:
-        y = torch.nn.functional.linear(x.float(), w.float())
+        y = torch.nn.functional.linear(x.float(), _rowmajor(w).float())
         if epi == "swiglu":
             return ref.silu_mul_interleaved(y.to(x.dtype))
         return y if epi == "f32" else y.to(x.dtype)
     _req(x, torch.bfloat16, "x")
-    _req(w, torch.bfloat16, "w")
+    if not packed:
+        _req(w, torch.bfloat16, "w")
     M, Kd = x.shape
     N = w.shape[0]
-    if w.shape[1] != Kd or not (1 <= M <= GEMV_MAX_M) or not x.is_contiguous() or not w.is_contiguous():
+    if w.shape[1] != Kd or not (1 <= M <= GEMV_MAX_M) or not x.is_contiguous() or not (packed or w.is_contiguous()):
         raise ValueError(f"gemv: x {tuple(x.shape)} w {tuple(w.shape)} (M <= {GEMV_MAX_M}, contiguous)")
     mode = {"f32": 0, "bf16": 1, "swiglu": 2}[epi]
     if out is None:
         shape = (M, N // 2) if epi == "swiglu" else (M, N)
         out = torch.empty(shape, dtype=torch.float32 if epi == "f32" else torch.bfloat16, device=x.device)
     yf, yb = (out.data_ptr(), None) if epi == "f32" else (None, out.data_ptr())
-    check(kernels().cfc_gemv(x.data_ptr(), w.data_ptr(), M, N, Kd, mode, yf, yb, out.shape[1], _stream(x)),
-          "cfc_gemv")
+    if packed:
+        check(kernels().cfc_gemv_packed(x.data_ptr(), w.data.data_ptr(), M, N, Kd, w.bn // 16, mode, yf, yb,
+                                        out.shape[1], _stream(x)), "cfc_gemv_packed")
+    else:
+        check(kernels().cfc_gemv(x.data_ptr(), w.data_ptr(), M, N, Kd, mode, yf, yb, out.shape[1], _stream(x)),
+              "cfc_gemv")
     return out
 
 
@@ -630,7 +637,7 @@ def gemv_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tens
     """residual += bf16(x @ w^T) via the GEMV (fp32 out) and the split = 1 residual + RMSNorm reduce;
     returns RMSNorm(residual) * norm_w (same rounding points as lib_splitk_linear_residual_rmsnorm)."""
     if not x.is_cuda:
-        return _linear_residual_rmsnorm_ref(x, w, residual, norm_w, eps)
+        return _linear_residual_rmsnorm_ref(x, _rowmajor(w), residual, norm_w, eps)
     M, N = x.shape[0], w.shape[0]
     part = _workspace(x.device, M * N)[:M * N].view(M, N)
     gemv(x, w, "f32", out=part)

@@ -12,11 +12,12 @@ infrastructure a one-process-per-service deployment needs.
 Reference entry points: <service>/main.py (e.g. ingestion/main.py:179, parsing/main.py:101-124).
 
 Multi-GPU: launched by torchrun (WORLD_SIZE > 1), ``node`` and ``summarization`` run one process
-per GPU -- CFC_TP consecutive ranks form one tensor-parallel model, the TP-group leaders are data-
-parallel summarization workers (ORCHESTRATOR_DP / CFC_DP, if set, must equal WORLD_SIZE / CFC_TP).
-Global rank 0 runs the service(s) and shards every summarization batch over the workers through
-the job's TCPStore (parallel/dp_service.py: LPT assignment, heartbeats, takeover of a dead
-worker's threads); the other ranks only run models:
+per GPU -- CFC_TP consecutive ranks form one tensor-parallel model, the TP-group leaders are the
+data-parallel ranks (ORCHESTRATOR_DP / CFC_DP, if set, must equal WORLD_SIZE / CFC_TP).  Global
+rank 0 runs the service(s); every DP rank embeds, indexes (its own HBM shard) and summarizes the
+threads it owns, rank 0's services reaching them through the job's TCPStore (parallel/dp_node.py:
+owner routing, streaming summaries, heartbeats, takeover of a dead rank's threads); TP followers
+replay their leader's engine steps:
 
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m copilot_for_consensus_amd.services.main node
 """
@@ -84,7 +85,9 @@ def main(argv=None) -> int:
             return _model_rank(dist_ctx)
     try:
         only = None if args.service == "node" else [args.service]
-        node = Node(services=only, summarizer=dist_ctx["summarizer"] if dist_ctx else None)
+        node = Node(services=only, summarizer=dist_ctx["summarizer"] if dist_ctx else None,
+                    vector_store=dist_ctx["vector_store"] if dist_ctx else None,
+                    embedding_provider=dist_ctx["embedder"] if dist_ctx else None)
         node.connect(only)
     except Exception as e:  # noqa: BLE001 -- fail fast: a service that cannot reach its bus/store exits 1
         print(f"[{args.service}] start-up failed: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
@@ -121,15 +124,18 @@ def main(argv=None) -> int:
 
 
 def _distributed() -> dict | None:
-    """torchrun env -> process groups, this rank's model and its role (see the module doc)."""
+    """torchrun env -> process groups, this rank's models and its role (see the module doc)."""
     import os
     if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
         return None
     import torch.distributed as dist
 
+    from ..embedding import create_embedding_provider
     from ..parallel import init_distributed, make_groups
-    from ..parallel.dp_service import DPSummarizer, TPBroadcast
+    from ..parallel.dp_node import DPNodeWorker, build_rank0
+    from ..parallel.dp_service import TPBroadcast
     from ..summarization import create_llm_backend
+    from ..vectorstore import create_vector_store
     env = init_distributed()
     scfg = get_config("summarization")
     llm = scfg.llm_backend
@@ -146,32 +152,45 @@ def _distributed() -> dict | None:
         tp_bcast = local.tp_hook = TPBroadcast(groups)
     store = dist.distributed_c10d._get_default_store()
     serve = env.rank == 0
-    summarizer = DPSummarizer(store, groups.dp_size, local) if serve and groups.dp_size > 1 else local
-    return {"env": env, "groups": groups, "store": store, "local": local, "summarizer": summarizer,
-            "serve": serve, "tp_bcast": tp_bcast}
+    ctx = {"env": env, "groups": groups, "store": store, "local": local, "summarizer": local, "serve": serve,
+           "tp_bcast": tp_bcast, "worker": None, "vector_store": None, "embedder": None}
+    if groups.dp_size > 1 and groups.tp_rank == 0:
+        # every DP rank embeds, indexes and summarizes the threads it owns (parallel/dp_node.py)
+        ecfg = get_config("embedding")
+        embedder = create_embedding_provider(ecfg.embedding_backend)
+        index = create_vector_store(ecfg.vector_store, dimension=int(embedder.dimension))
+        worker = DPNodeWorker(store, groups.dp_rank, groups.dp_size, embedder, index, local)
+        ctx.update(worker=worker, embedder=embedder)
+        if serve:
+            vs, summ = build_rank0(store, groups.dp_size, worker)
+            ctx.update(vector_store=vs, summarizer=summ)
+            worker.start(serve=False)
+    return ctx
 
 
 def _model_rank(ctx: dict) -> int:
     """A rank that only runs models: TP follower, or DP worker (TP-group leader) until shutdown."""
-    from ..parallel.dp_service import dp_worker_loop, tp_follow
+    from ..parallel.dp_service import tp_follow
     g = ctx["groups"]
     if g.tp_rank != 0:
         n = tp_follow(ctx["local"], g)
-        print(f"[rank {ctx['env'].rank}] TP follower done after {n} batches", flush=True)
+        print(f"[rank {ctx['env'].rank}] TP follower done after {n} messages", flush=True)
         return 0
-    jobs = dp_worker_loop(ctx["store"], g.dp_rank, g.dp_size, ctx["local"])
+    stats = ctx["worker"].run_until_shutdown()
     if ctx["tp_bcast"] is not None:
         ctx["tp_bcast"].stop()
-    print(f"[rank {ctx['env'].rank}] DP worker done after {jobs} jobs", flush=True)
+    ctx["worker_stats"] = stats
+    print(f"[rank {ctx['env'].rank}] DP worker done: {stats}", flush=True)
     return 0
 
 
 def _close_distributed(ctx: dict | None) -> None:
     if not ctx:
         return
-    close = getattr(ctx["summarizer"], "close", None)
-    if callable(close) and ctx["summarizer"] is not ctx["local"]:
-        close()               # DP workers exit their loops
+    if ctx.get("worker") is not None and ctx["serve"]:
+        from ..parallel.dp_node import shutdown_workers
+        shutdown_workers(ctx["store"])      # DP workers leave their serve loops
+        ctx["worker"].stop()
     if ctx["tp_bcast"] is not None:
         ctx["tp_bcast"].stop()
 

@@ -274,25 +274,34 @@ class EmbeddingService(BaseService):
                 raise DocumentNotFoundError("chunks not visible yet")
             return 0  # already embedded (idempotent replay)
         t = time.perf_counter()
-        vecs = retry_with_backoff(lambda: self.embedder.embed_tensor([c["text"] for c in chunks]),
-                                  self.max_retries, self.backoff)
-        dt = time.perf_counter() - t
-        self.vectors.add_embeddings([c["_id"] for c in chunks], vecs,
-                                    [{"thread_id": c["thread_id"], "message_id": c["message_id"],
-                                      "message_doc_id": c["message_doc_id"], "chunk_index": c["chunk_index"]}
-                                     for c in chunks])
-        if getattr(vecs, "is_cuda", False):
-            # the index rows are written on this thread's stream; readers (the orchestrator) use
-            # their own: the rows must be in HBM before the event that announces them
-            import torch
-            torch.cuda.current_stream(vecs.device).synchronize()
+        metas = [{"thread_id": c["thread_id"], "message_id": c["message_id"], "message_doc_id": c["message_doc_id"],
+                  "chunk_index": c["chunk_index"]} for c in chunks]
+        model, backend, dim = self.embedder.model_name, self.embedder.backend, int(self.embedder.dimension)
+        if hasattr(self.vectors, "embed_and_store"):
+            # data-parallel node (parallel/dp_node.py): each thread's chunks are embedded on, and
+            # stay in the HBM index shard of, the GPU that owns the thread
+            info = retry_with_backoff(lambda: self.vectors.embed_and_store(
+                [{"id": c["_id"], "thread_id": c["thread_id"], "text": c["text"], "meta": m}
+                 for c, m in zip(chunks, metas)]), self.max_retries, self.backoff)
+            model, backend, dim = info["model"], info["backend"], int(info["dimension"])
+            dt = time.perf_counter() - t
+        else:
+            vecs = retry_with_backoff(lambda: self.embedder.embed_tensor([c["text"] for c in chunks]),
+                                      self.max_retries, self.backoff)
+            dt = time.perf_counter() - t
+            self.vectors.add_embeddings([c["_id"] for c in chunks], vecs, metas)
+            if getattr(vecs, "is_cuda", False):
+                # the index rows are written on this thread's stream; readers (the orchestrator) use
+                # their own: the rows must be in HBM before the event that announces them
+                import torch
+                torch.cuda.current_stream(vecs.device).synchronize()
         self.store.update_many("chunks", {"_id": {"$in": [c["_id"] for c in chunks]}},
                                {"embedding_generated": True, "lastUpdated": _now()})
         self.metrics.increment("embedding_chunks_processed_total", len(chunks))
         self.metrics.observe("embedding_generation_duration_seconds", dt)
         self.publish("EmbeddingsGenerated", chunk_ids=[c["_id"] for c in chunks], embedding_count=len(chunks),
-                     embedding_model=self.embedder.model_name, embedding_backend=self.embedder.backend,
-                     embedding_dimension=int(self.embedder.dimension), vector_store_collection="embeddings",
+                     embedding_model=model, embedding_backend=backend,
+                     embedding_dimension=dim, vector_store_collection="embeddings",
                      vector_store_updated=True, avg_generation_time_ms=1000 * dt / len(chunks))
         return len(chunks)
 
@@ -366,7 +375,10 @@ class OrchestratorService(BaseService):
         scores: dict[str, float] = {}
         if self.vectors is not None and chunks:
             try:
-                scores = self.vectors.centroid_scores([c["_id"] for c in chunks if c.get("embedding_generated")])
+                ids = [c["_id"] for c in chunks if c.get("embedding_generated")]
+                # a thread-sharded (DP) store answers from the shard that owns the thread
+                scores = (self.vectors.centroid_scores(ids, thread_id=thread_id)
+                          if getattr(self.vectors, "thread_sharded", False) else self.vectors.centroid_scores(ids))
             except (RuntimeError, ValueError, OSError) as e:
                 self.log.warning("vector scoring failed; neutral scores", thread_id=thread_id, error=repr(e))
                 scores = {}

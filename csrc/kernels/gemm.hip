@@ -204,6 +204,92 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
     }
   }
 }
+
+// GEMV over the decode GEMM's fragment-packed weight (cfc_dgemm_pack, bn = 16 nw): the B <= 4
+// decode path when only the packed copy of a projection exists (one weight copy for prefill,
+// batched and single-stream decode).  A packed fragment = 16 W rows x 32 k, lane l holding row
+// l & 15, k = 8 (l >> 4) .. +8 -- one 16-byte load per lane, 1 KB per wave instruction, the
+// contiguous pieces the stream reads fastest.
+//   * one workgroup per 16-row group g, its 4 waves split the K/32 fragments of the group (wave w
+//     streams fragments [w KG / 4, (w + 1) KG / 4) at stride nw KB: kg-major inside the span of the
+//     group's bn-row tile), GVP_U fragments in flight per wave, nontemporal buffer loads;
+//   * each lane dots its 8 weights with x[m][32 kg + 8 (l >> 4) ..] (16-byte loads of the L1/L2-
+//     resident activation rows, one address per 16 lanes);
+//   * lanes of one row are summed with two xor-shuffles, the 4 waves through LDS; epilogues as the
+//     row-major GEMV (fp32 / bf16 / SwiGLU over the 8-row interleaved gate/up groups: lanes r and
+//     r + 8 of a group hold gate and up row r of output column 8 g + r).
+constexpr int GVP_U = 8;
+
+template <int MT, int EPI>
+__global__ void __launch_bounds__(256) gemv_packed_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
+                                                          int N, int K, int nw, float* __restrict__ yf,
+                                                          uint16_t* __restrict__ yb, int ldo) {
+  __shared__ float red[4][MT][16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = blockIdx.x;                        // 16-row group
+  const int KG = K / 32;
+  const int kb = w * KG / 4, ke = (w + 1) * KG / 4;
+  const int q = lane >> 4;
+  // byte offset of fragment (g, kg): (((g / nw) * KG + kg) * nw + g % nw) KB; + 16 per lane
+  const uint16_t* span = Wp + (size_t)(g / nw) * KG * nw * 512 + (size_t)(g % nw) * 512;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)span);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)span >> 32));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uintptr_t)hi << 32) | lo), (short)0, (int)((size_t)KG * nw * 1024 - (size_t)(g % nw) * 1024), 0x00020000);
+  const int voff = 16 * lane;
+  float acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = 0.f;
+  for (int k0 = kb; k0 < ke; k0 += GVP_U) {
+    uint4 wv[GVP_U], xv[GVP_U][MT];
+#pragma unroll
+    for (int u = 0; u < GVP_U; ++u) {
+      const int kg = min(k0 + u, ke - 1);          // tail: re-read the last fragment, weight 0 below
+      const gv_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, kg * nw * 1024, 2);
+      wv[u] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+#pragma unroll
+    for (int u = 0; u < GVP_U; ++u) {
+      const int kg = min(k0 + u, ke - 1);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) xv[u][m] = *reinterpret_cast<const uint4*>(X + (size_t)m * K + 32 * kg + 8 * q);
+    }
+#pragma unroll
+    for (int u = 0; u < GVP_U; ++u) {
+      if (k0 + u < ke) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m] += dot8(wv[u], xv[u][m]);
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    acc[m] += __shfl_xor(acc[m], 16, 64);
+    acc[m] += __shfl_xor(acc[m], 32, 64);
+  }
+  if (q == 0) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) red[w][m][lane] = acc[m];
+  }
+  __syncthreads();
+  if (w != 0 || q != 0) return;
+  const int r = lane;                              // row 16 g + r
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const float v = red[0][m][r] + red[1][m][r] + red[2][m][r] + red[3][m][r];
+    if constexpr (EPI == GV_SWIGLU) {
+      const float up = __shfl_xor(v, 8, 64);
+      if (r < 8) {
+        const float gg = bf2f(f2bf(v)), uu = bf2f(f2bf(up));
+        yb[(size_t)m * ldo + 8 * g + r] = f2bf(gg / (1.f + __expf(-gg)) * uu);
+      }
+    } else if constexpr (EPI == GV_BF16) {
+      yb[(size_t)m * ldo + 16 * g + r] = f2bf(v);
+    } else {
+      yf[(size_t)m * N + 16 * g + r] = v;
+    }
+  }
+}
 }  // namespace
 
 // mode 0: out[M, N] bf16 = sum of partials; mode 1: out[M, N/2] = silu(gate) * up (interleaved).
@@ -252,5 +338,26 @@ CFC_API int cfc_gemv(const void* x, const void* w, int M, int N, int K, int epi,
   switch (M) { GV_CASE(1) GV_CASE(2) GV_CASE(3) GV_CASE(4) }
 #undef GV_CASE
 #undef GV_ARGS
+  return CFC_CHECK_LAUNCH();
+}
+
+// M <= 4 GEMV over a fragment-packed W (cfc_dgemm_pack layout for bn = 16 nw): epilogues as
+// cfc_gemv.  N % (16 nw) == 0, K % 64 == 0.
+CFC_API int cfc_gemv_packed(const void* x, const void* wp, int M, int N, int K, int nw, int epi, float* yf, void* yb,
+                            int ldo, hipStream_t stream) {
+  if (M < 1 || M > 4 || N <= 0 || nw <= 0 || N % (16 * nw) || K <= 0 || K % 64) return -1;
+  if ((epi == GV_F32 && !yf) || (epi != GV_F32 && !yb)) return -2;
+  const dim3 grid(N / 16);
+#define GVP_ARGS (const uint16_t*)x, (const uint16_t*)wp, N, K, nw, yf, (uint16_t*)yb, ldo
+#define GVP_CASE(MT)                                                                                 \
+  case MT:                                                                                           \
+    if (epi == GV_F32) gemv_packed_kernel<MT, GV_F32><<<grid, 256, 0, stream>>>(GVP_ARGS);           \
+    else if (epi == GV_BF16) gemv_packed_kernel<MT, GV_BF16><<<grid, 256, 0, stream>>>(GVP_ARGS);    \
+    else if (epi == GV_SWIGLU) gemv_packed_kernel<MT, GV_SWIGLU><<<grid, 256, 0, stream>>>(GVP_ARGS); \
+    else return -3;                                                                                  \
+    break;
+  switch (M) { GVP_CASE(1) GVP_CASE(2) GVP_CASE(3) GVP_CASE(4) }
+#undef GVP_CASE
+#undef GVP_ARGS
   return CFC_CHECK_LAUNCH();
 }

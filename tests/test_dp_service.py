@@ -117,46 +117,122 @@ def test_killed_worker_threads_are_taken_over():
                 p.kill()
 
 
-def _main_rank(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), CFC_DIST_BACKEND="gloo", LLM_BACKEND_TYPE="mock",
-                      LLM_MOCK_LATENCY_MS="0", CUDA_VISIBLE_DEVICES="")
+_DP_NODE_ENV = {"DOCUMENT_STORE_TYPE": "inmemory", "MESSAGE_BUS_TYPE": "inproc", "METRICS_TYPE": "noop",
+                "LOG_TYPE": "silent", "ERROR_REPORTER_TYPE": "silent", "EMBEDDING_BACKEND_TYPE": "mock",
+                "VECTOR_STORE_TYPE": "inmemory", "ARCHIVE_STORE_TYPE": "inmemory", "SECRET_PROVIDER_TYPE": "env",
+                "LLM_BACKEND_TYPE": "mock", "MOCK_LATENCY_MS": "20", "CFC_DIST_BACKEND": "gloo",
+                "CUDA_VISIBLE_DEVICES": "", "SUMMARIZATION_CONTINUOUS_BATCHING": "true"}
+
+
+def _write_mbox(path, n_threads, seed=1):
+    from copilot_for_consensus_amd.utils.synthetic import SyntheticArchive
+    path.mkdir(parents=True, exist_ok=True)
+    (path / "list.mbox").write_bytes(SyntheticArchive(seed=seed).mbox(n_threads, messages_per_thread=(2, 3)))
+
+
+def _dp_node_rank(rank, world, port, src_dir, n_threads, q, kill_rank=None):
+    os.environ.update(_DP_NODE_ENV, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    if kill_rank is not None and rank == kill_rank:
+        os.environ["MOCK_LATENCY_MS"] = "600000"            # never finishes a thread: killed holding work
     try:
         from copilot_for_consensus_amd.services import main as M
         ctx = M._distributed()
         if not ctx["serve"]:
-            q.put((rank, "worker", M._model_rank(ctx)))
+            M._model_rank(ctx)
+            q.put((rank, "worker", ctx.get("worker_stats")))
             return
-        out = ctx["summarizer"].summarize_batch(_threads(12, "m"))
-        q.put((rank, "leader", [s.thread_id for s in out], type(ctx["summarizer"]).__name__))
-        M._close_distributed(ctx)
+        from copilot_for_consensus_amd.services.node import Node
+        node = Node(env=_DP_NODE_ENV, summarizer=ctx["summarizer"], vector_store=ctx["vector_store"],
+                    embedding_provider=ctx["embedder"])
+        node.start(threaded=True)
+        try:
+            ing = node.services["ingestion"]
+            ing.create_source({"name": "dp", "source_type": "local", "url": src_dir})
+            ing.trigger_ingestion("dp")
+            if kill_rank is not None:
+                deadline = time.time() + 120
+                summ = ctx["summarizer"]
+                while time.time() < deadline and not any(r == kill_rank for *_, r in list(summ._inflight.values())):
+                    time.sleep(0.05)
+                time.sleep(0.5)
+                q.put((rank, "kill", kill_rank))             # it holds threads: the test kills it now
+            deadline = time.time() + 240
+            while time.time() < deadline and node.store.count_documents("summaries") < n_threads:
+                time.sleep(0.1)
+            n_sum = node.store.count_documents("summaries")
+            n_thr = node.store.count_documents("threads")
+            hits = node.services["reporting"].search_reports_by_topic("the working group discussion", limit=5,
+                                                                       min_score=-1.0)
+            q.put((rank, "leader", type(ctx["summarizer"]).__name__, n_thr, n_sum, dict(ctx["summarizer"].stats),
+                   dict(ctx["worker"].stats), ctx["vector_store"].count(), len(hits)))
+        finally:
+            node.stop()
+            M._close_distributed(ctx)
     except Exception:  # noqa: BLE001
         import traceback
         q.put((rank, "error", traceback.format_exc()))
 
 
-def test_services_main_torchrun_roles():
-    """services.main under a 2-rank (gloo) torchrun env: rank 0 serves with a DPSummarizer, rank 1
-    becomes a DP worker and exits when rank 0 closes."""
+def _run_dp_node(tmp_path, world, n_threads, kill_rank=None):
+    src = tmp_path / "src"
+    _write_mbox(src, n_threads)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_main_rank, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_dp_node_rank, args=(r, world, port, str(src), n_threads, q, kill_rank))
+             for r in range(world)]
     for p in procs:
         p.start()
+    got = {}
     try:
-        got = {}
-        for _ in procs:
-            item = q.get(timeout=120)
+        while len(got) < world:
+            item = q.get(timeout=300)
+            if item[1] == "kill":
+                os.kill(procs[item[2]].pid, signal.SIGKILL)
+                got[item[2]] = (item[2], "killed")
+                continue
             got[item[0]] = item
-        assert got[0][1] == "leader" and got[0][3] == "DPSummarizer", got
-        assert got[0][2] == [f"m{i:03d}" for i in range(12)]
-        assert got[1][1] == "worker" and got[1][2] == 0, got
+        for p in procs:
+            p.join(timeout=60)
     finally:
         for p in procs:
-            p.join(timeout=30)
             if p.is_alive():
                 p.kill()
+    return got, procs
+
+
+def test_services_main_torchrun_roles(tmp_path):
+    """services.main under a 2-rank (gloo) torchrun env, the whole node on rank 0 with DP routing
+    (parallel/dp_node.py): BOTH ranks embed chunks into their own index shards and summarize the
+    threads they own; every thread gets exactly one summary; topic search fans out over the shards;
+    rank 1 exits when rank 0 closes."""
+    n = 12
+    got, procs = _run_dp_node(tmp_path, 2, n)
+    assert got[0][1] == "leader" and got[0][2] == "DPNodeSummarizer", got
+    _, _, _, n_thr, n_sum, sstats, w0, n_vec, n_hits = got[0]
+    assert n_thr == n and n_sum == n, got[0]
+    assert sstats["completed"] == n and sstats["duplicates"] == 0, sstats
+    assert all(c > 0 for c in sstats["per_rank"]), sstats          # both ranks summarized
+    assert got[1][1] == "worker", got
+    w1 = got[1][2]
+    assert w0["embedded"] > 0 and w1["embedded"] > 0, (w0, w1)      # both ranks embedded their threads' chunks
+    assert w0["embedded"] + w1["embedded"] == n_vec and w1["summaries"] == sstats["per_rank"][1]
+    assert w1["queries"] >= 1 and n_hits >= 1                        # the topic search reached rank 1's shard
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def test_dp_node_killed_rank_threads_taken_over(tmp_path):
+    """3 DP ranks; rank 2 is killed while it holds threads: its heartbeat goes stale, rank 0
+    resubmits them to the live ranks and every thread still gets exactly one summary."""
+    n = 12
+    got, procs = _run_dp_node(tmp_path, 3, n, kill_rank=2)
+    assert got[0][1] == "leader", got
+    _, _, _, n_thr, n_sum, sstats, *_ = got[0]
+    assert n_sum == n_thr == n, got[0]
+    assert sstats["resubmitted"] >= 1 and sstats["per_rank"][2] == 0, sstats
+    assert sstats["completed"] == n, sstats
+    assert got[1][1] == "worker" and got[2][1] == "killed", got
 
 
 _TP_NODE_ENV = {"DOCUMENT_STORE_TYPE": "inmemory", "MESSAGE_BUS_TYPE": "inproc", "METRICS_TYPE": "noop",

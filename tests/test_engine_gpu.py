@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 
 def _to_cpu_fp32_model(w: DecoderWeights):
     c = DecoderWeights(w.cfg, "cpu")
-    c.layers = [{k: v.cpu() for k, v in layer.items()} for layer in w.layers]
+    c.layers = [{k: v.cpu() for k, v in w.rowmajor_layer(i).items()} for i in range(w.cfg.layers)]
     c.embed, c.final_norm, c.lm_head = w.embed.cpu(), w.final_norm.cpu(), w.lm_head.cpu()
     c.gate_up_interleaved = w.gate_up_interleaved
     return c
@@ -69,11 +69,11 @@ PROMPTS8 = [[1, 2, 3] * 30, [4, 5] * 70, [1, 7], [9] * 17, [3, 1, 4, 1, 5] * 9, 
 @pytest.mark.parametrize("mode", ["splitk", "dgemm"])
 def test_decode_gemm_modes_match_library(mode, monkeypatch):
     cfg = get_config("tiny")
-    w = DecoderWeights.random(cfg, "cuda", seed=11)
     res = []
     for m in (mode, "lib"):
         monkeypatch.setenv("CFC_DECODE_GEMM", m)
-        model = DecoderModel(w)
+        # fresh weights per model: the dgemm model keeps only the packed copy of the projections
+        model = DecoderModel(DecoderWeights.random(cfg, "cuda", seed=11))
         assert model.decode_gemm == m
         kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, "cuda")
         # 8 sequences: decode batches above the GEMV's 4 rows take the mode's GEMMs
@@ -86,10 +86,9 @@ def test_decode_gemm_modes_match_library(mode, monkeypatch):
 
 def test_fused_decode_matches_unfused():
     cfg = get_config("tiny")
-    w = DecoderWeights.random(cfg, "cuda", seed=7)
     res = []
     for fused in (True, False):
-        m = DecoderModel(w, fused_decode=fused)
+        m = DecoderModel(DecoderWeights.random(cfg, "cuda", seed=7), fused_decode=fused)
         assert m.fused_decode == fused
         kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, "cuda")
         res.append(LLMEngine(m, kv).generate(PROMPTS8, 24, ignore_eos=True).tokens)
@@ -143,7 +142,7 @@ def test_mha_generation_matches_reference():
 
 
 def test_gemv_decode_matches_splitk_decode(monkeypatch):
-    """B <= 4 decode on the GEMV kernel vs the library split-K decode path, same weights."""
+    """B <= 4 decode on the GEMV kernel (over the packed-only weights) vs the decode GEMM, same weights."""
     cfg = get_config("small")
     w = DecoderWeights.random(cfg, "cuda", seed=13)
     res = []
@@ -200,7 +199,7 @@ def test_odd_vocab_lm_head_single_stream():
 
 
 @pytest.mark.parametrize("mode", ["hip", "lib"])
-def test_prefill_gemm_modes_match_reference_logits(mode):
+def test_prefill_gemm_modes_match_reference_logits(mode, monkeypatch):
     """Prefill projections on the hand-written pgemm (SwiGLU fused into gate/up) or the library:
     the last-token logits of each prompt against the fp32 CPU reference model."""
     cfg = get_config("tiny")
@@ -218,8 +217,10 @@ def test_prefill_gemm_modes_match_reference_logits(mode):
         return seen[0].float().cpu()
 
     w = DecoderWeights.random(cfg, "cuda", seed=11)
+    monkeypatch.setenv("CFC_PREFILL_GEMM", mode)
     m = DecoderModel(w)
-    m.prefill_gemm, m.PGEMM_MIN_ROWS = mode, 64
+    m.PGEMM_MIN_ROWS = 64
+    assert m.prefill_gemm == mode
     prompts = [[1] + list(range(7, 7 + 150)), [1] + list(range(40, 40 + 130)), [1, 5, 9] * 20]
     calls = []
     if mode == "hip":
@@ -235,6 +236,7 @@ def test_prefill_gemm_modes_match_reference_logits(mode):
     rel = float((got - want).abs().max() / want.abs().max())
     assert rel < 5e-2 and torch.equal(got.argmax(-1), want.argmax(-1)), rel
     assert (len(calls) > 0) == (mode == "hip")
+    assert m.w.packed_only == (mode == "hip")       # the hip prefill + dgemm decode keep one weight copy
 
 
 def test_prefill_beside_decode_on_cu_partitions_matches_generate():

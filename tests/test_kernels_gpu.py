@@ -502,6 +502,23 @@ def test_pgemm_packed_exact(variant):
     assert torch.equal(y.float(), x.float() @ w.float().T)
 
 
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,Kd,bn", [(6144, 4096, 96), (1024, 1536, 64), (2240, 512, 112), (768, 448 + 64, 128)])
+def test_gemv_packed_weight(M, N, Kd, bn):
+    """The B <= 4 GEMV over the fragment-packed weight (packed-only decode) vs the fp32 reference and
+    vs the row-major GEMV: fp32, bf16 and SwiGLU epilogues."""
+    x = (torch.rand(M, Kd, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(N, Kd, device=DEV) * 2 - 1) / Kd ** 0.5).bfloat16()
+    pw = K.pack_dgemm_weight(w, bn=bn)
+    ref = _ref_linear(x, w)
+    _close(K.gemv(x, pw, "f32"), ref, 1e-3)
+    _close(K.gemv(x, pw, "bf16"), ref, 1e-2)
+    torch.testing.assert_close(K.gemv(x, pw, "f32"), K.gemv(x, w, "f32"), rtol=1e-4, atol=1e-4)
+    if N % 16 == 0:
+        want = R.silu_mul(_ref_linear(x, R.deinterleave_gate_up(w.cpu()).to(DEV)).bfloat16()).float()
+        _close(K.gemv(x, pw, "swiglu"), want, 3e-2)
+
+
 @pytest.mark.parametrize("split", [1, 3, 4])
 def test_rope_kv_write_from_splitk_slabs_matches_reduce_then_rope(split):
     """rope_kv_write_part == splitk_reduce -> rope_kv_write, bit for bit (q, K cache, V cache)."""
