@@ -52,6 +52,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-overlap", action="store_true", help="run pipeline stages strictly sequentially")
     ap.add_argument("--overlap-prefill", choices=["on", "off"], default=os.environ.get("CFC_OVERLAP_PREFILL", "off"),
                     help="prefill batch i+1 on half the CUs beside batch i's decode (runtime/cu_partition.py)")
+    ap.add_argument("--latency-rate", type=float, default=8.0,
+                    help="latency half of the metric: Poisson arrivals per second per GPU served by the continuous "
+                         "engine after the timed throughput steps (0 = skip)")
+    ap.add_argument("--latency-steps", type=int, default=2, help="batches of threads the latency probe replays")
     ap.add_argument("--pipeline", choices=["bench", "node"], default="bench",
                     help="bench: the stage code with a static LLM batch (headline); node: the real services "
                          "(Node, in-proc bus, continuous summarization engine), pipeline/node_bench.py")
@@ -87,7 +91,9 @@ def main(argv=None):
                          index_group=groups.dp_group if groups.dp_size > 1 and not args.llm_only else None,
                          overlap_prefill=args.overlap_prefill == "on" and not args.no_overlap)
 
-    pipe.prepare_sources(list(range(args.warmup + args.steps)))
+    probe_steps = list(range(args.warmup + args.steps, args.warmup + args.steps + args.latency_steps)) \
+        if args.latency_rate > 0 and args.tp == 1 and not args.llm_only else []
+    pipe.prepare_sources(list(range(args.warmup + args.steps)) + probe_steps)
 
     def barrier():
         if world > 1:
@@ -136,6 +142,22 @@ def main(argv=None):
 
     value = threads / elapsed
     p50 = statistics.median(lat_all) if lat_all else None
+    latency = None
+    if probe_steps:
+        # after the timed window: the same GPUs at a load below saturation (Poisson arrivals)
+        barrier()
+        probe = pipe.latency_probe(probe_steps, args.latency_rate, seed=args.seed + 104729 * groups.dp_rank)
+        if world > 1:
+            parts = [None] * world
+            dist.all_gather_object(parts, probe)
+            probe = parts
+        else:
+            probe = [probe]
+        latency = dict(probe[0])
+        latency.update(threads=sum(p["threads"] for p in probe),
+                       p50_s=round(statistics.median([p["p50_s"] for p in probe]), 3),
+                       p95_s=round(max(p["p95_s"] for p in probe), 3),
+                       throughput_threads_per_s=round(sum(p["throughput_threads_per_s"] for p in probe), 3))
     if rank == 0:
         out = {
             "metric": "end-to-end threads summarized/sec + p50 summary latency, Mistral-7B TP=1/8",
@@ -165,6 +187,8 @@ def main(argv=None):
                              else "prefill then decode per batch (next batch's preparation overlapped)"),
             },
             "p50_summary_latency_s": round(p50, 3) if p50 is not None else None,
+            # latency half of the metric at a stated arrival rate below saturation (continuous engine)
+            "latency_mode": latency,
             "generated_tokens_per_s": round(gen_tokens / elapsed, 1),
             "prompt_tokens_per_s": round(prompt_tokens / elapsed, 1),
             "baseline_threads_per_s": round(BASELINE_THREADS_PER_S, 4),

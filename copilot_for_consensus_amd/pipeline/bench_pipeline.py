@@ -245,3 +245,51 @@ class BenchPipeline:
 
     def run_step(self, step: int) -> StepResult:
         return self.run_steps([step], overlap=False)[0]
+
+    def latency_probe(self, steps: list[int], rate_per_s: float, seed: int = 0, steps_per_sync: int = 16) -> dict:
+        """The latency half of the metric under load below saturation: the threads of ``steps``
+        (prepared by the same RAG path as the throughput steps) arrive as a Poisson process of
+        ``rate_per_s`` and are served by the continuous engine (runtime/continuous.py -- the
+        summarization service's engine): a thread joins the running decode batch at the next burst
+        boundary and leaves it after its 512 tokens.  Latency = the thread's share of the pipeline
+        preparation (its batch's parse / chunk / embed / select time / threads) + arrival ->
+        last token.  Not in the timed throughput window."""
+        import numpy as np
+
+        from ..runtime.continuous import ContinuousEngine
+        prompts, prep_s = [], 0.0
+        for st in steps:
+            _, ctx, p, stages = self._prepare(st)
+            prep_s += sum(stages.values())
+            prompts.extend(p)
+        if not prompts:
+            return {}
+        per_thread_prep = prep_s / len(prompts)
+        ce = ContinuousEngine(self.engine, max_slots=self.threads_per_step, max_new_cap=self.max_new,
+                              max_prompt=max(len(x) for x in prompts), steps_per_sync=steps_per_sync, stop_ids=(),
+                              min_admit=1, max_wait_s=0.05)
+        rng = np.random.default_rng(seed)
+        arrive = np.cumsum(rng.exponential(1.0 / float(rate_per_s), len(prompts)))
+        t0 = time.perf_counter()
+        nxt, lat, arrival_of = 0, [], {}
+        try:
+            while nxt < len(prompts) or ce.pending():
+                now = time.perf_counter() - t0
+                while nxt < len(prompts) and arrive[nxt] <= now:
+                    r = ce.submit(prompts[nxt], self.max_new)
+                    arrival_of[r.rid] = t0 + float(arrive[nxt])
+                    nxt += 1
+                if ce.pending():
+                    for r in ce.step():
+                        lat.append(r.finished_s - arrival_of.pop(r.rid))
+                elif nxt < len(prompts):
+                    time.sleep(max(0.0, float(arrive[nxt]) - (time.perf_counter() - t0)))
+        finally:
+            ce.close()
+        wall = time.perf_counter() - t0
+        lat = np.asarray(lat) + per_thread_prep
+        return {"arrival_rate_per_gpu": float(rate_per_s), "threads": int(len(lat)),
+                "p50_s": round(float(np.percentile(lat, 50)), 3), "p95_s": round(float(np.percentile(lat, 95)), 3),
+                "throughput_threads_per_s": round(len(lat) / wall, 3),
+                "prep_per_thread_s": round(per_thread_prep, 4),
+                "engine": f"continuous ({self.threads_per_step} slots, {steps_per_sync} decode steps per admission)"}

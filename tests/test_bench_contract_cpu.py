@@ -34,7 +34,7 @@ def _run(cmd):
     return json.loads(lines[0])
 
 
-def _check(d, n):
+def _check(d, n, latency=True):
     assert KEYS <= set(d)
     assert d["n_gpus"] == n and d["steps"] == 2 and d["warmup"] == 1
     assert d["scaling"] == "weak" and d["higher_is_better"] is True and d["dtype"] == "bf16"
@@ -42,6 +42,12 @@ def _check(d, n):
     assert d["value"] > 0 and d["ms_per_step"] > 0
     # value is the whole-job aggregate: threads of every rank over the max elapsed time
     assert d["value"] == pytest.approx(2 * n * 2 / (d["ms_per_step"] * 2 / 1000), rel=0.02)
+    if not latency:
+        return
+    # the latency half: Poisson arrivals on the continuous engine after the timed window
+    lm = d["latency_mode"]
+    assert lm["threads"] == 2 * 2 * n and lm["arrival_rate_per_gpu"] == 8.0
+    assert 0 < lm["p50_s"] <= lm["p95_s"]
 
 
 def test_bench_single_process_contract():
@@ -60,5 +66,5 @@ def test_bench_node_pipeline_contract():
     """--pipeline node: the same JSON contract measured through the real services (Node on the
     in-proc bus, continuous summarization engine), every thread of every step reported."""
     d = _run([sys.executable, "bench.py", "--gpus", "1", "--pipeline", "node", *ARGS])
-    _check(d, 1)
+    _check(d, 1, latency=False)
     assert d["config"]["pipeline"].startswith("node:")
