@@ -50,7 +50,7 @@ class ShardedVectorIndex(VectorStore):
         self.local.add_embeddings(ids, vectors, metadatas)
 
     def delete(self, id):
-        if id in self.local._row:
+        if self.local.has(id):
             self.local.delete(id)
 
     def clear(self):
@@ -65,7 +65,7 @@ class ShardedVectorIndex(VectorStore):
 
     def get(self, id):
         """Collective: the owner returns the vector, every rank receives it."""
-        res = self.local.get(id) if id in self.local._row else None
+        res = self.local.get(id) if self.local.has(id) else None
         if self.world == 1:
             if res is None:
                 raise KeyError(id)
@@ -196,9 +196,9 @@ class ShardedVectorIndex(VectorStore):
         # resolve winners owned here, then share the resolved records
         local: dict[int, tuple] = {}
         for r in row[owner == self.rank].tolist():
-            if r >= 0 and r not in local and self.local._ids[r] is not None:
+            if r >= 0 and r not in local and self.local._tab.id_at(r) is not None:
                 vec = self.local._X[r].float().cpu().tolist() if with_vectors else []
-                local[r] = (self.local._ids[r], vec, dict(self.local._meta[r] or {}))
+                local[r] = (self.local._tab.id_at(r), vec, self.local._tab.meta_at(r))
         tables = [local]
         if self.world > 1:
             tables = [None] * self.world

@@ -29,6 +29,8 @@ from typing import Any, Sequence
 import numpy as np
 import torch
 
+from .rowtable import RowTable
+
 
 @dataclasses.dataclass
 class SearchResult:
@@ -184,9 +186,8 @@ class HipFlatIndex(VectorStore):
         self._X = torch.empty(0, self.dim, dtype=torch.bfloat16, device=self.device)
         self._norm2 = torch.empty(0, dtype=torch.float32, device=self.device)
         self._alive = torch.empty(0, dtype=torch.bool, device=self.device)
-        self._ids: list[str | None] = []
-        self._row: dict[str, int] = {}
-        self._meta: list[dict | None] = []
+        # ids + metadata: numpy columns and byte heaps, no Python object per row (rowtable.py)
+        self._tab = RowTable(max(1024, int(capacity)))
         self._dead = 0
         self._lock = threading.RLock()
         self._reserve(capacity)
@@ -225,30 +226,42 @@ class HipFlatIndex(VectorStore):
         metadatas = list(metadatas) if metadatas is not None else [{} for _ in ids]
         v, n2 = self._prepare(vecs)
         with self._lock:
-            rows = []
-            for i in ids:
-                r = self._row.get(i)
-                if r is None:
-                    r = self._n
-                    self._n += 1
-                    self._row[i] = r
-                    self._ids.append(i)
-                    self._meta.append(None)
-                rows.append(r)
+            rows = self._tab.upsert(ids, metadatas)
+            self._n = self._tab.n
             self._reserve(self._n)
-            idx = torch.tensor(rows, dtype=torch.long, device=self.device)
+            idx = torch.from_numpy(rows).to(self.device)
             self._X.index_copy_(0, idx, v)
             self._norm2.index_copy_(0, idx, n2)
             self._alive[idx] = True
-            for r, m in zip(rows, metadatas):
-                self._meta[r] = dict(m or {})
+
+    def add_bulk(self, ids, vectors, metadatas=None) -> None:
+        """Bulk build of NEW ids (no upsert check): vectors straight into HBM, ids / metadata into
+        the row table in one vectorised append -- the path for 10M-100M-row indexes."""
+        vecs = _as_matrix(vectors, self.dim, device=self.device, dtype=torch.bfloat16) \
+            if not isinstance(vectors, torch.Tensor) else vectors
+        if len(ids) != vecs.shape[0]:
+            raise ValueError("ids and vectors length mismatch")
+        with self._lock:
+            n0 = self._n
+            self._tab.append_bulk(ids, metadatas)
+            self._n = self._tab.n
+            self._reserve(self._n)
+            for s in range(0, vecs.shape[0], 1 << 22):
+                v, n2 = self._prepare(vecs[s:s + (1 << 22)])
+                self._X[n0 + s:n0 + s + v.shape[0]] = v
+                self._norm2[n0 + s:n0 + s + v.shape[0]] = n2
+            self._alive[n0:self._n] = True
+
+    def has(self, id) -> bool:
+        return self._tab.find(id) >= 0
 
     def delete(self, id):
         with self._lock:
-            r = self._row.pop(id)  # KeyError if absent (reference contract)
+            r = self._tab.find(id)
+            if r < 0:
+                raise KeyError(id)   # reference contract
+            self._tab.kill(r)
             self._alive[r] = False
-            self._ids[r] = None
-            self._meta[r] = None
             self._dead += 1
             if self._dead > 1024 and self._dead > self._n // 4:
                 self.compact()
@@ -257,39 +270,40 @@ class HipFlatIndex(VectorStore):
         with self._lock:
             if self._dead == 0:
                 return
-            keep = [r for r in range(self._n) if self._ids[r] is not None]
-            idx = torch.tensor(keep, dtype=torch.long, device=self.device)
-            n = len(keep)
+            keep = np.nonzero(self._tab.live)[0]
+            idx = torch.from_numpy(keep).to(self.device)
+            n = int(keep.size)
             self._X[:n] = self._X.index_select(0, idx) if n else self._X[:0]
             self._norm2[:n] = self._norm2.index_select(0, idx) if n else self._norm2[:0]
             self._alive[:n] = True
             self._alive[n:] = False
-            self._ids = [self._ids[r] for r in keep]
-            self._meta = [self._meta[r] for r in keep]
-            self._row = {i: r for r, i in enumerate(self._ids)}
+            self._tab.permute(keep)
             self._n, self._dead = n, 0
 
     def clear(self):
         with self._lock:
             self._n, self._dead = 0, 0
-            self._ids, self._row, self._meta = [], {}, []
+            self._tab.clear()
             self._alive.zero_()
 
     def count(self):
         return self._n - self._dead
 
     def get(self, id):
-        r = self._row[id]
-        return SearchResult(id, 1.0, self._X[r].float().cpu().tolist(), dict(self._meta[r]))
+        r = self._tab.find(id)
+        if r < 0:
+            raise KeyError(id)
+        return SearchResult(id, 1.0, self._X[r].float().cpu().tolist(), self._tab.meta_at(r))
 
     # ------------------------------------------------------------------ search
     def centroid_scores(self, ids):
         """Device path of VectorStore.centroid_scores: one gather of the rows, one GEMV, one copy out."""
         with self._lock:
-            have = [i for i in ids if i in self._row]
+            rows = self._tab.find_many(list(ids))
+            have = [i for i, r in zip(ids, rows) if r >= 0]
             if not have:
                 return {}
-            idx = torch.tensor([self._row[i] for i in have], dtype=torch.long, device=self.device)
+            idx = torch.from_numpy(rows[rows >= 0]).to(self.device)
             s = self.span_centroid_scores(self._X.index_select(0, idx), [(0, len(have))])
             return dict(zip(have, s.cpu().tolist()))
 
@@ -343,12 +357,13 @@ class HipFlatIndex(VectorStore):
         for qv, qi in zip(v.tolist(), i.tolist()):
             res = []
             for s, r in zip(qv, qi):
-                if r < 0 or s == float("-inf") or self._ids[r] is None:
+                rid = self._tab.id_at(r) if r >= 0 and s != float("-inf") else None
+                if rid is None:
                     continue
                 if self.metric == "l2":
                     s = 1.0 / (1.0 + max(0.0, -s)) if self.faiss_scores else -s
                 vec = self._X[r].float().cpu().tolist() if with_vectors else []
-                res.append(SearchResult(self._ids[r], float(s), vec, dict(self._meta[r])))
+                res.append(SearchResult(rid, float(s), vec, self._tab.meta_at(r)))
             out.append(res)
         return out
 
@@ -368,7 +383,8 @@ class HipFlatIndex(VectorStore):
 
     # ------------------------------------------------------------------ persistence
     def save(self, path) -> None:
-        """Index shard = safetensors blob (vectors, norms) + JSON sidecar (ids, metadata)."""
+        """Index shard = safetensors blob (vectors, norms) + the row table's .npy columns and heaps
+        (ids, metadata) + a small JSON header.  Nothing pickled."""
         from safetensors.torch import save_file
         p = Path(path)
         p.mkdir(parents=True, exist_ok=True)
@@ -376,8 +392,9 @@ class HipFlatIndex(VectorStore):
             self.compact()
             save_file({"vectors": self._X[:self._n].contiguous().cpu(), "norm2": self._norm2[:self._n].cpu()},
                       str(p / "vectors.safetensors"))
-            (p / "index.json").write_text(json.dumps({"dim": self.dim, "metric": self.metric, "ids": self._ids,
-                                                      "metadata": self._meta}))
+            self._tab.save(p)
+            (p / "index.json").write_text(json.dumps({"dim": self.dim, "metric": self.metric, "rows": self._n,
+                                                      "format": "rowtable-1"}))
 
     @classmethod
     def load(cls, path, device="cuda") -> "HipFlatIndex":
@@ -385,15 +402,16 @@ class HipFlatIndex(VectorStore):
         p = Path(path)
         meta = json.loads((p / "index.json").read_text())
         t = load_file(str(p / "vectors.safetensors"))
-        idx = cls(meta["dim"], "l2" if meta["metric"] == "l2" else meta["metric"], capacity=len(meta["ids"]) + 1024,
-                  device=device)
-        n = len(meta["ids"])
+        n = int(meta["rows"]) if "rows" in meta else len(meta["ids"])
+        idx = cls(meta["dim"], "l2" if meta["metric"] == "l2" else meta["metric"], capacity=n + 1024, device=device)
         idx._X[:n] = t["vectors"].to(idx.device)
         idx._norm2[:n] = t["norm2"].to(idx.device)
         idx._alive[:n] = True
-        idx._ids = list(meta["ids"])
-        idx._meta = list(meta["metadata"])
-        idx._row = {i: r for r, i in enumerate(idx._ids)}
+        if meta.get("format") == "rowtable-1":
+            idx._tab = RowTable.load(p)
+        else:                                  # round-3 JSON sidecar (ids / metadata lists)
+            idx._tab = RowTable(n + 1024)
+            idx._tab.append_bulk(meta["ids"], meta["metadata"])
         idx._n = n
         return idx
 
@@ -434,9 +452,10 @@ class HipIVFIndex(HipFlatIndex):
                 idx = torch.randperm(n, generator=g)[:m].to(self.device)
                 sample = self._X.index_select(0, idx)         # bf16 rows, no full-index copy
             X = sample.to(self.device).float()
+            Xb = X.to(torch.bfloat16).contiguous()
             C = X[torch.randperm(X.shape[0], generator=g)[:nlist].to(self.device)].clone()
             for _ in range(iters):
-                a = torch.argmax(X @ C.T, 1) if self.metric != "l2" else torch.argmin(torch.cdist(X, C), 1)
+                a = self._nearest(Xb, C)
                 sums = torch.zeros_like(C).index_add_(0, a, X)
                 cnt = torch.bincount(a, minlength=C.shape[0])
                 C = torch.where(cnt[:, None] > 0, sums / cnt.clamp_min(1).float()[:, None], C)   # keep empty lists' seeds
@@ -446,17 +465,34 @@ class HipIVFIndex(HipFlatIndex):
             self.nlist = C.shape[0]
             self._regroup()
 
-    def _assign(self, X: torch.Tensor) -> torch.Tensor:
-        C = self.centroids
+    def _nearest(self, X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
+        """Nearest centroid of every row of bf16 X: argmax of x.c (cosine / dot) or of
+        2 x.c - |c|^2 (L2), in ASSIGN_CHUNK-row pieces.  On the GPU the scores come from the
+        hand-written MFMA GEMM (pgemm.hip) with the -|c|^2 term in its bias epilogue (the L2 form
+        uses W = 2C) and the padding centroids' bias at -3e4; the argmax runs over bf16 scores."""
+        from ..ops import kernels as K
+        Cf = C.float()
+        bias = -Cf.pow(2).sum(1) if self.metric == "l2" else torch.zeros(C.shape[0], device=C.device)
+        Wf = 2 * Cf if self.metric == "l2" else Cf
+        use_hip = X.is_cuda and X.shape[1] % 64 == 0 and X.shape[0] >= 256
+        if use_hip:
+            npad = -(-C.shape[0] // 64) * 64
+            Wb = torch.zeros(npad, X.shape[1], dtype=torch.bfloat16, device=X.device)
+            Wb[:C.shape[0]] = Wf.to(torch.bfloat16)
+            bb = torch.full((npad,), -3e4, dtype=torch.float32, device=X.device)
+            bb[:C.shape[0]] = bias
+            bb = bb.to(torch.bfloat16)
         out = []
         for s in range(0, X.shape[0], self.ASSIGN_CHUNK):
             xc = X[s:s + self.ASSIGN_CHUNK]
-            if self.metric != "l2":
-                out.append(torch.argmax((xc @ C.T).float(), 1))
-            else:   # argmin ||x - c||^2 = argmax (2 x.c - ||c||^2)
-                cn = C.float().pow(2).sum(1)
-                out.append(torch.argmax(2 * (xc @ C.T).float() - cn[None, :], 1))
+            if use_hip and xc.shape[0] >= 256:
+                out.append(torch.argmax(K.pgemm(xc.contiguous(), Wb, "bias", bias=bb), 1))
+            else:
+                out.append(torch.argmax(xc.float() @ Wf.T + bias[None, :], 1))
         return torch.cat(out)
+
+    def _assign(self, X: torch.Tensor) -> torch.Tensor:
+        return self._nearest(X, self.centroids)
 
     def _regroup(self):
         n = self._n
@@ -465,10 +501,7 @@ class HipIVFIndex(HipFlatIndex):
         self._X[:n] = self._X[:n].index_select(0, order)
         self._norm2[:n] = self._norm2[:n].index_select(0, order)
         self._alive[:n] = self._alive[:n].index_select(0, order)
-        o = order.cpu().tolist()
-        self._ids = [self._ids[r] for r in o]
-        self._meta = [self._meta[r] for r in o]
-        self._row = {i: r for r, i in enumerate(self._ids) if i is not None}
+        self._tab.permute(order.cpu().numpy())
         counts = torch.bincount(a, minlength=self.nlist)
         off = torch.zeros(self.nlist + 1, dtype=torch.int64, device=self.device)
         off[1:] = torch.cumsum(counts, 0)

@@ -149,7 +149,7 @@ def _thread_rows(env, batches):
     idx = ShardedVectorIndex(HipFlatIndex(32, device="cpu", capacity=512))
     tids, ids, X = batches[env.rank]
     sc = idx.add_thread_rows(tids, ids, X)
-    stored = {idx.local._ids[r]: idx.local._meta[r]["thread_id"] for r in range(idx.local._n)}
+    stored = {idx.local._tab.id_at(r): idx.local._tab.meta_at(r)["thread_id"] for r in range(idx.local._n)}
     return sc.tolist(), stored
 
 

@@ -45,7 +45,7 @@ def _worker(rank, port, q, batches, Q):
         tids, ids, X = batches[rank]
         sc = idx.add_thread_rows(tids, ids, X.to(env.device))
         torch.cuda.synchronize()
-        stored = {idx.local._ids[r]: idx.local._meta[r]["thread_id"] for r in range(idx.local._n)}
+        stored = {idx.local._tab.id_at(r): idx.local._tab.meta_at(r)["thread_id"] for r in range(idx.local._n)}
         res = idx.query_batch(Q.to(env.device), 10)
         q.put((rank, {"scores": sc.cpu().tolist(), "stored": stored, "dev": str(sc.device),
                       "top": [[r.id for r in qq] for qq in res]}))
