@@ -1,0 +1,124 @@
+// Copilot-for-Consensus on Azure, MI355X-native.
+//
+// The reference deploys its services as Container Apps (no GPU on that platform) next to
+// Service Bus, Cosmos DB, Key Vault, Storage and Azure Monitor.  Here the GPU services run where
+// AMD Instinct GPUs exist on Azure -- an AKS node pool of ND-series Instinct VMs (one process per
+// GPU: services.main node under torchrun, or one pod per stage) -- and the platform services keep
+// their roles and their names so the same drivers connect (cloud/azure.py):
+//   * Service Bus: topic `copilot.events` + one subscription per consuming service, each filtered
+//     on the routing keys it subscribes to (the RabbitMQ bindings of deploy/rabbitmq/definitions.json);
+//   * Cosmos DB (NoSQL): database `copilot`, the six document collections, partition key /id;
+//   * Storage: blob container `raw-archives` (archive store driver `azureblob`);
+//   * Key Vault: JWT signing keys and OAuth secrets (secret provider `azurekeyvault`);
+//   * Log Analytics + Application Insights (metrics driver `azure_monitor`);
+//   * user-assigned identities with data-plane RBAC (no connection strings in pods).
+// Workloads: deploy/k8s/copilot-mi355x.yaml (KEDA scales the stages on subscription backlog).
+targetScope = 'resourceGroup'
+
+@description('Short prefix of every resource name')
+@minLength(3)
+@maxLength(12)
+param projectName string = 'copilot'
+
+@allowed(['dev', 'staging', 'prod'])
+param environment string = 'dev'
+
+param location string = resourceGroup().location
+
+@description('VM size of the GPU node pool (AMD Instinct; the MI355X size when the region offers it)')
+param gpuVmSize string = 'Standard_ND96isr_MI300X_v5'
+
+@minValue(0)
+param gpuNodeCount int = 1
+
+@description('CPU node pool for the gateway, ingestion, reporting, auth and the UI')
+param systemVmSize string = 'Standard_D8ds_v5'
+
+@allowed(['Standard', 'Premium'])
+param serviceBusSku string = 'Standard'
+
+@minValue(400)
+param cosmosMaxThroughput int = 4000
+
+param tags object = {
+  project: 'copilot-for-consensus'
+  platform: 'mi355x'
+}
+
+var suffix = uniqueString(resourceGroup().id, projectName, environment)
+var base = '${projectName}-${environment}'
+
+module identities 'modules/identities.bicep' = {
+  name: 'identities'
+  params: { base: base, location: location, tags: tags }
+}
+
+module monitor 'modules/monitor.bicep' = {
+  name: 'monitor'
+  params: { base: base, location: location, tags: tags }
+}
+
+module keyVault 'modules/keyvault.bicep' = {
+  name: 'keyvault'
+  params: {
+    name: take('${projectName}kv${suffix}', 24)
+    location: location
+    tags: tags
+    readerPrincipalIds: [identities.outputs.servicesPrincipalId, identities.outputs.gpuPrincipalId]
+  }
+}
+
+module serviceBus 'modules/servicebus.bicep' = {
+  name: 'servicebus'
+  params: {
+    name: '${base}-sb-${suffix}'
+    location: location
+    sku: serviceBusSku
+    tags: tags
+    principalIds: [identities.outputs.servicesPrincipalId, identities.outputs.gpuPrincipalId]
+  }
+}
+
+module cosmos 'modules/cosmos.bicep' = {
+  name: 'cosmos'
+  params: {
+    name: '${base}-cosmos-${suffix}'
+    location: location
+    maxThroughput: cosmosMaxThroughput
+    tags: tags
+    principalIds: [identities.outputs.servicesPrincipalId, identities.outputs.gpuPrincipalId]
+  }
+}
+
+module storage 'modules/storage.bicep' = {
+  name: 'storage'
+  params: {
+    name: take('${projectName}st${suffix}', 24)
+    location: location
+    tags: tags
+    principalIds: [identities.outputs.servicesPrincipalId]
+  }
+}
+
+module aks 'modules/aks.bicep' = {
+  name: 'aks'
+  params: {
+    name: '${base}-aks'
+    location: location
+    tags: tags
+    systemVmSize: systemVmSize
+    gpuVmSize: gpuVmSize
+    gpuNodeCount: gpuNodeCount
+    logAnalyticsId: monitor.outputs.workspaceId
+    kubeletIdentityId: identities.outputs.gpuIdentityId
+  }
+}
+
+output serviceBusNamespace string = serviceBus.outputs.namespaceName
+output serviceBusTopic string = serviceBus.outputs.topicName
+output cosmosEndpoint string = cosmos.outputs.endpoint
+output cosmosDatabase string = cosmos.outputs.databaseName
+output storageAccount string = storage.outputs.accountName
+output keyVaultUri string = keyVault.outputs.vaultUri
+output appInsightsConnectionString string = monitor.outputs.appInsightsConnectionString
+output aksName string = aks.outputs.clusterName

@@ -1,0 +1,29 @@
+// Key Vault with RBAC authorisation: JWT signing keys (security/jwt.py KeyVault signer) and OAuth
+// client secrets (security/secrets.py azurekeyvault provider).  Readers get "Key Vault Secrets User".
+param name string
+param location string
+param tags object
+param readerPrincipalIds array
+
+resource vault 'Microsoft.KeyVault/vaults@2023-07-01' = {
+  name: name
+  location: location
+  tags: tags
+  properties: {
+    tenantId: subscription().tenantId
+    sku: { family: 'A', name: 'standard' }
+    enableRbacAuthorization: true
+    enableSoftDelete: true
+    softDeleteRetentionInDays: 30
+  }
+}
+
+var secretsUser = subscriptionResourceId('Microsoft.Authorization/roleDefinitions', '4633458b-17de-408a-b874-0445c86b69e6')
+
+resource readers 'Microsoft.Authorization/roleAssignments@2022-04-01' = [for p in readerPrincipalIds: {
+  name: guid(vault.id, p, secretsUser)
+  scope: vault
+  properties: { roleDefinitionId: secretsUser, principalId: p, principalType: 'ServicePrincipal' }
+}]
+
+output vaultUri string = vault.properties.vaultUri
