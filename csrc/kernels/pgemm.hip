@@ -469,62 +469,101 @@ __global__ void __launch_bounds__(512, 1)
   }
   constexpr bool FLIP = (PF & 3) == 0;
 
+  // ablation probes (never in production): 4 = no LDS-DMA in the loop, 8 = no fragment ds_reads
+  // (fragments of tile 0 reused, kept live), 16 = no MFMA (fragments kept live)
+  constexpr bool DMA = (PF & 4) == 0, RD = (PF & 8) == 0, MM = (PF & 16) == 0;
   bf16x8_t wf[4][2], xf[4][2];
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = (kt & 1) * PP_BUF;
-    // ======== segment A: load part (tile kt+1's W1 / X1 into the other buffer; fragments)
-    if (kt + 1 < nk) {
-      issue_w(kt + 1, 1);
-      issue_x(kt + 1, 1);
-    }
+  if constexpr (!RD) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) wf[j][kk] = rd_w(buf, j, kk);
+      for (int kk = 0; kk < 2; ++kk) wf[j][kk] = rd_w(0, j, kk);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) xf[i][kk] = rd_x(buf, 0, i, kk);
-    // retire tile kt's X1 (segment B reads it) and this wave's ds_reads
-    if (kt + 1 < nk) pp_wait_barrier<8>();
-    else pp_wait_barrier<0>();
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (FLIP) __builtin_amdgcn_s_setprio(1);
+      for (int kk = 0; kk < 2; ++kk) xf[i][kk] = rd_x(0, 0, i, kk);
+  }
+  auto keep = [&]() {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) asm volatile("" : "+v"(wf[j][kk]), "+v"(xf[j][kk]));
+  };
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = (kt & 1) * PP_BUF;
+    // ======== segment A: load part (tile kt+1's W1 / X1 into the other buffer; fragments)
+    if (DMA && kt + 1 < nk) {
+      issue_w(kt + 1, 1);
+      issue_x(kt + 1, 1);
+    }
+    if constexpr (RD) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) wf[j][kk] = rd_w(buf, j, kk);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][kk], xf[i][kk], acc[i][j], 0, 0, 0);
+        for (int kk = 0; kk < 2; ++kk) xf[i][kk] = rd_x(buf, 0, i, kk);
+    } else {
+      keep();
+    }
+    // retire tile kt's X1 (segment B reads it) and this wave's ds_reads
+    if (DMA && kt + 1 < nk) pp_wait_barrier<8>();
+    else pp_wait_barrier<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (FLIP) __builtin_amdgcn_s_setprio(1);
+    if constexpr (MM) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][kk], xf[i][kk], acc[i][j], 0, 0, 0);
+    } else {
+      keep();
+    }
     if constexpr (FLIP) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     pp_barrier();
     // ======== segment B: load part (tile kt+2's X0 / W0 into this buffer's free halves)
-    if (kt + 2 < nk) {
+    if (DMA && kt + 2 < nk) {
       issue_x(kt + 2, 0);
       issue_w(kt + 2, 0);
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) xf[i][kk] = rd_x(buf, 1, i, kk);
-    // retire tile kt+1's X0 / W0 / W1 (next segment A reads them)
-    if (kt + 2 < nk) pp_wait_barrier<6>();
-    else if (kt + 1 < nk) pp_wait_barrier<2>();
-    else pp_wait_barrier<0>();
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (FLIP) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    if constexpr (RD) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][kk], xf[i][kk], acc[4 + i][j], 0, 0, 0);
+        for (int kk = 0; kk < 2; ++kk) xf[i][kk] = rd_x(buf, 1, i, kk);
+    } else {
+      keep();
+    }
+    // retire tile kt+1's X0 / W0 / W1 (next segment A reads them)
+    if (DMA && kt + 2 < nk) pp_wait_barrier<6>();
+    else if (DMA && kt + 1 < nk) pp_wait_barrier<2>();
+    else pp_wait_barrier<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (FLIP) __builtin_amdgcn_s_setprio(1);
+    if constexpr (MM) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][kk], xf[i][kk], acc[4 + i][j], 0, 0, 0);
+    } else {
+      keep();
+    }
     if constexpr (FLIP) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     pp_barrier();
+  }
+  if constexpr (!MM) {      // the ablation's outputs depend on its fragments (nothing is dead code)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[0][j] += __builtin_bit_cast(f32x4_t, wf[j][0]) + __builtin_bit_cast(f32x4_t, xf[j][1]);
   }
 
   // wave rows: segment A's m-tiles i = tile rows 128 grp + 16 i, segment B's = 128 grp + 64 + 16 i
@@ -814,6 +853,10 @@ __global__ void __launch_bounds__(256, 1)
   pg_epilogue<EPI>(acc, bias, out, M, N, ldo, m0 + wr * 128, n0 + wc * 128);
 }
 
+// production probe flags of the ping-pong kernel: no s_setprio (measured 1.5-2.5 % faster than the
+// per-segment flips on all four headline shapes, profiles/r04_pgemm_pp_probes.jsonl pf1 vs pf0)
+constexpr int PP_PF = 1;
+
 template <int EPI>
 int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int M, int N, int K, int ldo,
                  int variant, int wnw, hipStream_t stream) {
@@ -822,14 +865,14 @@ int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int 
   uint16_t* op = (uint16_t*)out;
   if (wnw > 0) {   // fragment-packed W: the ping-pong (default) or the 4-wave kernel
     if (variant == 4) pgemm_w4_kernel<EPI, true><<<tm * tn, 256, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, wnw);
-    else pgemm_pp_kernel<EPI, true><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, wnw);
+    else pgemm_pp_kernel<EPI, true, PP_PF><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, wnw);
     return (int)hipGetLastError();
   }
   switch (variant) {
     case 0: pgemm_ring_kernel<EPI, 5><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn); break;
     case 1: pgemm_kernel<EPI><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn); break;
     case 2: pgemm_ring_kernel<EPI, 4><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn); break;
-    case 3: pgemm_pp_kernel<EPI, false><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, 1); break;
+    case 3: pgemm_pp_kernel<EPI, false, PP_PF><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, 1); break;
     case 4: pgemm_w4_kernel<EPI, false><<<tm * tn, 256, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, 1); break;
     default: return (int)hipErrorInvalidValue;
   }
@@ -872,6 +915,11 @@ CFC_API int cfc_pgemm_probe(const void* x, const void* w, void* out, int M, int 
     case 0: PP_PROBE(0)
     case 1: PP_PROBE(1)
     case 2: PP_PROBE(2)
+    case 5: PP_PROBE(5)
+    case 9: PP_PROBE(9)
+    case 13: PP_PROBE(13)
+    case 17: PP_PROBE(17)
+    case 21: PP_PROBE(21)
     default: return (int)hipErrorInvalidValue;
   }
 #undef PP_PROBE
