@@ -446,6 +446,8 @@ class DecoderModel:
                             and mode in ("splitk", "dgemm") and weights.tp_size == 1 and gemv_shapes
                             and not self.fp8)
         self.fused_decode = mode == "dgemm"
+        # decode RoPE + KV write inside the attention kernel's prologue (one launch per layer fewer)
+        self.rope_fused = os.environ.get("CFC_DECODE_ROPE_FUSED", "1") != "0"
         # B <= 4 decode on the ggml-quantized weights (GGUF checkpoints; csrc/kernels/quant.hip)
         self.decode_qgemv = (weights.qlayers is not None and os.environ.get("CFC_DECODE_QGEMV", "1") != "0"
                              and weights.tp_size == 1 and weights.gate_up_interleaved and not self.fp8)
@@ -590,14 +592,32 @@ class DecoderModel:
             lw = w.layers[i]
             h, residual = self._layer_pre(i, x, residual)
             qkv = self._lin(i, "qkv", h)
-            q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
-                                cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
-            attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
-                                            part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
-                                            k_scale=kv.k_scale, v_scale=kv.v_scale)
+            attn = self._rope_attention(i, qkv, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
+                                        part_blocks)
             o = self._all_reduce(self._lin(i, "o", attn.view(B, -1)))
             x = self._mlp(i, o, residual)
         return K.rmsnorm(x, w.final_norm, cfg.rms_eps, residual=residual)
+
+    def _rope_attention(self, i, qkv, positions, slots, ctx_lens, block_tables, kv, attn_workspace, part_blocks):
+        """RoPE + K/V cache write + paged decode attention of layer ``i`` from the qkv projection output
+        (bf16 [B, N], or fp32 split-K slabs [split, B, N]).  Default: ONE kernel (the attention's
+        prologue does the RoPE / KV write, ``CFC_DECODE_ROPE_FUSED=1``); else rope_kv then attention.
+        Both write the same cache bytes and return the same output."""
+        cfg, w = self.cfg, self.w
+        if self.rope_fused and qkv.is_cuda:
+            return K.paged_decode_rope_attention(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], block_tables,
+                                                 ctx_lens, self.scale, w.heads, w.kv_heads, cfg.head_dim,
+                                                 part_blocks=part_blocks, workspace=attn_workspace,
+                                                 window=self.window, k_scale=kv.k_scale, v_scale=kv.v_scale)
+        if qkv.dim() == 3:
+            q = K.rope_kv_write_part(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
+                                     cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
+        else:
+            q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
+                                cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
+        return K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
+                                        part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
+                                        k_scale=kv.k_scale, v_scale=kv.v_scale)
 
     def _forward_decode_fused(self, x, positions, slots, ctx_lens, block_tables, kv, attn_workspace, part_blocks):
         """Decode layer on the hand-written decode GEMM (dgemm.hip), elementwise work in epilogues:
@@ -616,16 +636,10 @@ class DecoderModel:
             pw = w.packed[i] if w.packed is not None else lw    # fragment-packed copies when present
             wq = pw["qkv"]
             qbn, qsplit = K.dgemm_config(B, wq.shape[0], h.shape[1], bn=getattr(wq, "bn", None))
-            if qsplit > 1:   # split-K slabs straight into RoPE / KV write (the reduce folded in)
-                q = K.rope_kv_write_part(K.dgemm(h, wq, "part", qsplit, bn=qbn), positions, slots, w.cos_sin,
-                                         kv.k[i], kv.v[i], w.heads, w.kv_heads, cfg.head_dim, k_scale=kv.k_scale,
-                                         v_scale=kv.v_scale)
-            else:
-                q = K.rope_kv_write(K.dgemm_linear(h, wq), positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads,
-                                    w.kv_heads, cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
-            attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
-                                            part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
-                                            k_scale=kv.k_scale, v_scale=kv.v_scale)
+            # split-K slabs go straight into RoPE / KV write (the reduce folded in)
+            qkv = K.dgemm(h, wq, "part", qsplit, bn=qbn) if qsplit > 1 else K.dgemm_linear(h, wq)
+            attn = self._rope_attention(i, qkv, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
+                                        part_blocks)
             if tp:
                 o = self._all_reduce(K.dgemm_linear(attn.view(B, -1), pw["o"]))
                 h = K.rmsnorm(o, lw["mlp_norm"], eps, residual=residual)
@@ -658,11 +672,8 @@ class DecoderModel:
         for i in range(cfg.layers):
             lw = w.layers[i]
             qkv = F.linear(h, lw["qkv"])
-            q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
-                                cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
-            attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
-                                            part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
-                                            k_scale=kv.k_scale, v_scale=kv.v_scale)
+            attn = self._rope_attention(i, qkv, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
+                                        part_blocks)
             h = K.lib_splitk_linear_residual_rmsnorm(attn.view(B, -1), lw["o"], s_o, residual, lw["mlp_norm"], eps)
             a = K.silu_mul(F.linear(h, lw["gate_up"]), interleaved=w.gate_up_interleaved)
             nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm
@@ -682,11 +693,8 @@ class DecoderModel:
             if w.packed_only:
                 lw = dict(lw, **w.packed[i])
             qkv = K.gemv(h, lw["qkv"])
-            q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
-                                cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
-            attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
-                                            part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
-                                            k_scale=kv.k_scale, v_scale=kv.v_scale)
+            attn = self._rope_attention(i, qkv, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
+                                        part_blocks)
             h = K.gemv_residual_rmsnorm(attn.view(B, -1), lw["o"], residual, lw["mlp_norm"], eps)
             a = K.gemv(h, lw["gate_up"], "swiglu")
             nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm
@@ -714,11 +722,8 @@ class DecoderModel:
                 K.qgemv(h, ql["v"], out=qkv[:, qs + ks:], ldo=ld)
             else:
                 qkv = K.gemv(h, lw["qkv"])
-            q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
-                                cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
-            attn = K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
-                                            part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
-                                            k_scale=kv.k_scale, v_scale=kv.v_scale)
+            attn = self._rope_attention(i, qkv, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
+                                        part_blocks)
             a2 = attn.view(B, -1)
             if ql["o"] is not None and fit_o:
                 part = K._workspace(h.device, B * cfg.hidden)[:B * cfg.hidden].view(1, B, cfg.hidden)

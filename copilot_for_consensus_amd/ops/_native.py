@@ -38,6 +38,7 @@ _KERNEL_SIGS = {
     "cfc_rope_kv_write_fp8": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, P],
     "cfc_v_cache_write_runs_fp8": [P, P, I, P, I, I, I, F, P],
     "cfc_paged_decode_attention_fp8": [P, P, P, P, P, I, I, I, I, I, I, I, F, I, F, F, P, P, P, P],
+    "cfc_paged_decode_rope_attention": [P, P, I, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, I, I, F, F, P, P, P, P],
     "cfc_prefill_attention_fp8": [P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, F, F, P, P],
     "cfc_silu_mul": [P, P, I, I, I, P],
     "cfc_quant_fp8_rows": [P, P, P, I, I, P],

@@ -218,6 +218,61 @@ def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, o
     return out
 
 
+def paged_decode_rope_attention(qkv, positions, slots, cos_sin, k_cache, v_cache, block_tables, ctx_lens, scale,
+                                Hq, Hkv, D, part_blocks=-1, workspace=None, window=0, k_scale=1.0, v_scale=1.0,
+                                out=None):
+    """One decode step's RoPE + K/V cache write + paged attention in ONE kernel
+    (attention.hip ``DecRope``): ``qkv`` is the qkv projection output, bf16 [B, (Hq + 2 Hkv) D] or the
+    decode GEMM's fp32 split-K slabs [split, B, (Hq + 2 Hkv) D].  Same cache bytes and output as
+    :func:`rope_kv_write` (/ ``_part``) followed by :func:`paged_decode_attention`."""
+    if not qkv.is_cuda:
+        qb = qkv.sum(0).to(torch.bfloat16) if qkv.dim() == 3 else qkv
+        q = rope_kv_write(qb, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D, k_scale=k_scale,
+                          v_scale=v_scale)
+        return paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out=out,
+                                      part_blocks=part_blocks, workspace=workspace, window=window, k_scale=k_scale,
+                                      v_scale=v_scale)
+    if qkv.dim() == 3:
+        split, B, N = qkv.shape
+        if qkv.dtype != torch.float32:
+            raise ValueError(f"paged_decode_rope_attention: split-K slabs must be fp32, got {qkv.dtype}")
+        qkv_p, part_p = None, qkv.data_ptr()
+    else:
+        (B, N), split = qkv.shape, 0
+        _req(qkv, torch.bfloat16, "qkv")
+        qkv_p, part_p = qkv.data_ptr(), None
+    if not qkv.is_contiguous() or N != (Hq + 2 * Hkv) * D:
+        raise ValueError(f"paged_decode_rope_attention: qkv {tuple(qkv.shape)} for Hq={Hq} Hkv={Hkv} D={D}")
+    if k_cache.shape[1] != Hkv or k_cache.shape[-1] != D or v_cache.shape[-2] != D:
+        raise ValueError("paged_decode_rope_attention: cache shape mismatch")
+    _req(positions, torch.int32, "positions")
+    _req(slots, torch.int32, "slots")
+    _req(block_tables, torch.int32, "block_tables")
+    _req(ctx_lens, torch.int32, "ctx_lens")
+    if positions.numel() != B or slots.numel() != B or ctx_lens.numel() != B or block_tables.shape[0] != B:
+        raise ValueError("paged_decode_rope_attention: per-row tensors must have B entries")
+    if cos_sin.dtype != torch.float32 or tuple(cos_sin.shape[1:]) != (D // 2, 2) or not cos_sin.is_contiguous():
+        raise ValueError("paged_decode_rope_attention: cos_sin must be fp32 [max_pos, D/2, 2]")
+    max_blocks = block_tables.shape[1]
+    if part_blocks < 0:
+        Pn, part_blocks = -part_blocks, 0
+    else:
+        Pn = math.ceil(max_blocks / part_blocks)
+    out = torch.empty(B, Hq, D, dtype=torch.bfloat16, device=qkv.device) if out is None else out
+    if Pn > 1:
+        if workspace is None:
+            workspace = torch.empty(B * Hq * Pn * (D + 2), dtype=torch.float32, device=qkv.device)
+        part_o, part_ml = workspace, workspace[B * Hq * Pn * D:]
+    else:
+        part_o = part_ml = None
+    check(kernels().cfc_paged_decode_rope_attention(
+        qkv_p, part_p, split, positions.data_ptr(), slots.data_ptr(), cos_sin.data_ptr(), k_cache.data_ptr(),
+        v_cache.data_ptr(), block_tables.data_ptr(), ctx_lens.data_ptr(), B, Hq, Hkv, D, max_blocks, part_blocks, Pn,
+        float(scale), int(window or 0), int(_fp8(k_cache)), float(k_scale), float(v_scale), _p(part_o), _p(part_ml),
+        out.data_ptr(), _stream(qkv)), "cfc_paged_decode_rope_attention")
+    return out
+
+
 PREFILL_TILE_ROWS = 128   # query rows per workgroup of the legacy single-head prefill kernels
 ENCODER_TILE_ROWS = 256   # query rows per workgroup of the encoder attention kernel (attention.hip ENC_ROWS)
 

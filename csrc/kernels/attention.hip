@@ -85,12 +85,28 @@ template <> struct KvFrag<true> { typedef uint2 raw; };
 __device__ __forceinline__ bf16x8_t kv_operand(uint4 r) { return as_bf16x8(r); }
 __device__ __forceinline__ bf16x8_t kv_operand(uint2 r) { return as_bf16x8(fp8x8_to_bf16x8(r)); }
 
-template <int G, bool NT, bool F8 = false>
+// ROPE: the decode step's RoPE + KV write happens in the prologue (DecRope below): every workgroup
+// ropes the G query heads it needs straight from the qkv projection output (bf16, or the decode
+// GEMM's fp32 split-K slabs) into LDS, and the workgroup whose KV range holds the sequence's last
+// block writes the new key / value into the cache first -- the separate rope_kv launch, its q
+// round trip through HBM and its dependency edge disappear.  Same helpers (common.h) as
+// rope_kv_kernel, so the cache bytes and q values are identical to the two-kernel path.
+struct DecRope {
+  const uint16_t* qkv;     // [B, (Hq + 2 Hkv) D] bf16, or nullptr with part
+  const float* part;       // [split, B, (Hq + 2 Hkv) D] fp32 split-K slabs
+  int split;
+  const int32_t* positions;
+  const int32_t* slots;    // -1: no cache write
+  const float* cos_sin;
+  float inv_k, inv_v;
+};
+
+template <int G, bool NT, bool F8 = false, bool ROPE = false>
 __global__ void __launch_bounds__(256, F8 ? 2 : 1) paged_decode_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ kc, const void* __restrict__ vc,
     const int32_t* __restrict__ block_tables, const int32_t* __restrict__ ctx_lens, float scale_log2, int Hkv,
     int max_blocks, int part_blocks, int P, int window, float v_scale, float* __restrict__ part_o,
-    float* __restrict__ part_ml, uint16_t* __restrict__ out) {
+    float* __restrict__ part_ml, uint16_t* __restrict__ out, DecRope rp) {
   // F8: kc / vc hold e4m3 of K / k_scale and V / v_scale; k_scale is folded into scale_log2 by the
   // host, v_scale multiplies the output here
   typedef typename KvFrag<F8>::raw Raw;
@@ -119,10 +135,42 @@ __global__ void __launch_bounds__(256, F8 ? 2 : 1) paged_decode_kernel(
   // dq(c) = 32c + 8g.  FP8 cache: the head dim is visited in the order that lets ONE 16-byte load
   // carry two k-steps of a key row (64 contiguous bytes per row per wave instruction, as the bf16
   // loads have): dq(c) = 64(c >> 1) + 16g + 8(c & 1) -- any d order works as long as Q and K agree.
+  __shared__ __attribute__((aligned(16))) uint16_t sm_q[ROPE ? G : 1][D];
+  if constexpr (ROPE) {
+    constexpr int NV = D / 16;    // 8-vectors per half-head
+    const size_t stride = (size_t)(Hq + 2 * Hkv) * D;
+    const size_t row0 = (size_t)b * stride, slab = (size_t)gridDim.z * stride;
+    const int slot = rp.slots[b];
+    const bool owner = slot >= 0 && blk0 <= nblk - 1 && nblk - 1 < blk1;   // holds the new key's block
+    const float* cs = rp.cos_sin + (size_t)rp.positions[b] * (D / 2) * 2;
+    const int t = threadIdx.x;
+    if (t < (G + 1) * NV) {
+      const int hh = t / NV, c = t - hh * NV;   // hh < G: query head h*G + hh; hh == G: key head h
+      if (hh < G || owner) {
+        uint4 pa, pb;
+        rope_rot8(rp.qkv, rp.part, rp.split, slab, row0 + (size_t)(hh < G ? h * G + hh : Hq + h) * D, D / 2, c, cs,
+                  pa, pb);
+        if (hh < G) {
+          *reinterpret_cast<uint4*>(&sm_q[hh][c * 8]) = pa;
+          *reinterpret_cast<uint4*>(&sm_q[hh][D / 2 + c * 8]) = pb;
+        } else {
+          kv_write_k<F8>(const_cast<void*>(kc), slot, h, Hkv, D, c, pa, pb, rp.inv_k);
+        }
+      }
+    } else if (owner && t < (G + 1) * NV + D / 8) {
+      const int c = t - (G + 1) * NV;
+      float vf[8];
+      qkv_load8(rp.qkv, rp.part, rp.split, slab, row0 + (size_t)(Hq + Hkv + h) * D + c * 8, vf);
+      kv_write_v<F8>(const_cast<void*>(vc), slot, h, Hkv, D, c, pack8(vf), rp.inv_v);
+    }
+    // workgroup-scope release / acquire: the cache stores above are visible to this workgroup's
+    // KV loads below (same CU), and sm_q to every wave
+    __syncthreads();
+  }
   bf16x8_t qf[4];
   {
     const bool valid = col < G;
-    const uint16_t* qr = q + ((size_t)b * Hq + h * G + (valid ? col : 0)) * D;
+    const uint16_t* qr = ROPE ? &sm_q[valid ? col : 0][0] : q + ((size_t)b * Hq + h * G + (valid ? col : 0)) * D;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int dq = F8 ? 64 * (c >> 1) + 16 * g + 8 * (c & 1) : 32 * c + 8 * g;
@@ -1142,21 +1190,30 @@ template <bool F8>
 static int launch_paged_decode(const void* q, const void* k_cache, const void* v_cache, const int32_t* block_tables,
                                const int32_t* ctx_lens, int B, int Hq, int Hkv, int head_dim, int max_blocks,
                                int part_blocks, int P, float scale, int window, float v_scale, float* part_o,
-                               float* part_ml, void* out, hipStream_t stream) {
+                               float* part_ml, void* out, hipStream_t stream, const DecRope* rope = nullptr) {
   if (head_dim != 128 || Hq % Hkv != 0 || B <= 0 || P <= 0 || window < 0) return -1;
+  if (rope != nullptr && ((rope->qkv == nullptr) == (rope->part == nullptr) || (rope->part && rope->split < 1) ||
+                          !rope->positions || !rope->slots || !rope->cos_sin))
+    return -1;
+  const DecRope rp = rope ? *rope : DecRope{};
   const int G = Hq / Hkv;
   dim3 grid(P, Hkv, B);
   const float sl2 = scale * LOG2E;
 #define DEC_ARGS (const uint16_t*)q, k_cache, v_cache, block_tables, ctx_lens, sl2, Hkv, max_blocks, part_blocks, P, \
-    window, v_scale, part_o, part_ml, (uint16_t*)out
+    window, v_scale, part_o, part_ml, (uint16_t*)out, rp
   // nontemporal KV loads for large batches (B=128: 6.5 vs 5.9 TB/s; B=8: 3.8 vs 4.2 -- there the
   // plain loads win), profiles/decode_attn_partitions_r01.log; CFC_DECODE_NT=0/1 forces either
   static const int nt_env = [] { const char* e = getenv("CFC_DECODE_NT"); return e ? atoi(e) : -1; }();
   const bool nt = nt_env >= 0 ? nt_env != 0 : B >= 32;
 #define DEC_CASE(GG) \
   case GG: \
-    if (nt) paged_decode_kernel<GG, true, F8><<<grid, 256, 0, stream>>>(DEC_ARGS); \
-    else paged_decode_kernel<GG, false, F8><<<grid, 256, 0, stream>>>(DEC_ARGS); \
+    if (rope) { \
+      if (nt) paged_decode_kernel<GG, true, F8, true><<<grid, 256, 0, stream>>>(DEC_ARGS); \
+      else paged_decode_kernel<GG, false, F8, true><<<grid, 256, 0, stream>>>(DEC_ARGS); \
+    } else { \
+      if (nt) paged_decode_kernel<GG, true, F8><<<grid, 256, 0, stream>>>(DEC_ARGS); \
+      else paged_decode_kernel<GG, false, F8><<<grid, 256, 0, stream>>>(DEC_ARGS); \
+    } \
     break;
   switch (G) {
     DEC_CASE(1) DEC_CASE(2) DEC_CASE(4) DEC_CASE(8) DEC_CASE(16)
@@ -1176,6 +1233,24 @@ CFC_API int cfc_paged_decode_attention(const void* q, const void* k_cache, const
                                        float* part_o, float* part_ml, void* out, hipStream_t stream) {
   return launch_paged_decode<false>(q, k_cache, v_cache, block_tables, ctx_lens, B, Hq, Hkv, head_dim, max_blocks,
                                     part_blocks, P, scale, window, 1.f, part_o, part_ml, out, stream);
+}
+
+// Decode attention with the step's RoPE + KV write in its prologue (DecRope).  qkv [B, (Hq+2Hkv)*128]
+// bf16 OR part [split, B, (Hq+2Hkv)*128] fp32 slabs (exactly one non-null); positions / slots [B];
+// fp8 != 0: e4m3 caches (K / k_scale, V / v_scale).  Writes out [B, Hq, 128]; q never leaves the chip.
+CFC_API int cfc_paged_decode_rope_attention(const void* qkv, const float* part, int split, const int32_t* positions,
+                                            const int32_t* slots, const float* cos_sin, void* k_cache, void* v_cache,
+                                            const int32_t* block_tables, const int32_t* ctx_lens, int B, int Hq,
+                                            int Hkv, int head_dim, int max_blocks, int part_blocks, int P, float scale,
+                                            int window, int fp8, float k_scale, float v_scale, float* part_o,
+                                            float* part_ml, void* out, hipStream_t stream) {
+  const DecRope rp{(const uint16_t*)qkv, part, split, positions, slots, cos_sin, 1.f / k_scale, 1.f / v_scale};
+  if (fp8)
+    return launch_paged_decode<true>(nullptr, k_cache, v_cache, block_tables, ctx_lens, B, Hq, Hkv, head_dim,
+                                     max_blocks, part_blocks, P, scale * k_scale, window, v_scale, part_o, part_ml,
+                                     out, stream, &rp);
+  return launch_paged_decode<false>(nullptr, k_cache, v_cache, block_tables, ctx_lens, B, Hq, Hkv, head_dim,
+                                    max_blocks, part_blocks, P, scale, window, 1.f, part_o, part_ml, out, stream, &rp);
 }
 
 // FP8 (e4m3fn) caches holding K / k_scale and V / v_scale

@@ -120,4 +120,102 @@ __device__ __forceinline__ uint4 fp8x8_to_bf16x8(uint2 v) {
   return r;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Decode RoPE + paged KV write, shared by rope_kv_kernel (elementwise.hip) and the decode attention
+// kernel that does it in its prologue (attention.hip), so both write bit-identical caches.
+// Cache layouts (attention.hip header): K [blk][kvh][32][D]; V transposed [blk][kvh][D][32] with
+// key (16 hi + 4 g + j) of a block at slot 8 g + 4 hi + j.
+constexpr int CFC_KV_BS = 32;
+
+__device__ __forceinline__ int kv_v_slot(int key_in_block) {
+  const int hi = key_in_block >> 4, g = (key_in_block >> 2) & 3, j = (key_in_block & 3) + 4 * hi;
+  return 8 * g + j;
+}
+
+// 8 consecutive qkv values of token row element offset `off`: from the bf16 qkv, or summed from
+// `split` fp32 split-K slabs of the decode GEMM (slab stride `slab` elements) and rounded to bf16
+// -- the same values splitk_reduce would have written, without the round trip
+__device__ __forceinline__ void qkv_load8(const uint16_t* qkv, const float* part, int split, size_t slab, size_t off,
+                                          float* f) {
+  if (part == nullptr) {
+    unpack8(*reinterpret_cast<const uint4*>(qkv + off), f);
+    return;
+  }
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  for (int p = 0; p < split; ++p) {
+    const float4 x = *reinterpret_cast<const float4*>(part + p * slab + off);
+    const float4 y = *reinterpret_cast<const float4*>(part + p * slab + off + 4);
+    a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+    b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
+  }
+  f[0] = bf2f(f2bf(a.x)); f[1] = bf2f(f2bf(a.y)); f[2] = bf2f(f2bf(a.z)); f[3] = bf2f(f2bf(a.w));
+  f[4] = bf2f(f2bf(b.x)); f[5] = bf2f(f2bf(b.y)); f[6] = bf2f(f2bf(b.z)); f[7] = bf2f(f2bf(b.w));
+}
+
+// Rotate-half RoPE of the c-th 8-vector of each half of one head (head row at element offset
+// `head_off`); cs = cos_sin + position * half * 2 (cos, sin interleaved).  pa / pb: bf16 results
+// for [c*8, c*8+8) and [half + c*8, ...).
+__device__ __forceinline__ void rope_rot8(const uint16_t* qkv, const float* part, int split, size_t slab,
+                                          size_t head_off, int half, int c, const float* cs, uint4& pa, uint4& pb) {
+  const float4* c4 = reinterpret_cast<const float4*>(cs + (size_t)c * 16);
+  float csv[16];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float4 t = c4[j];
+    csv[4 * j] = t.x; csv[4 * j + 1] = t.y; csv[4 * j + 2] = t.z; csv[4 * j + 3] = t.w;
+  }
+  float a[8], b[8], ra[8], rb[8];
+  qkv_load8(qkv, part, split, slab, head_off + c * 8, a);
+  qkv_load8(qkv, part, split, slab, head_off + half + c * 8, b);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float cv = csv[2 * j], sv = csv[2 * j + 1];
+    ra[j] = a[j] * cv - b[j] * sv;
+    rb[j] = b[j] * cv + a[j] * sv;
+  }
+  pa = pack8(ra);
+  pb = pack8(rb);
+}
+
+// Roped key 8-vectors (c of each half) of kv-head kh into cache slot `slot`.  F8: e4m3 of the bf16
+// value times inv_k (rounded to bf16 first: the values the bf16 cache would hold).
+template <bool F8>
+__device__ __forceinline__ void kv_write_k(void* k_cache, int slot, int kh, int Hkv, int D, int c, uint4 pa, uint4 pb,
+                                           float inv_k) {
+  const int half = D / 2, blk = slot / CFC_KV_BS, off = slot % CFC_KV_BS;
+  const size_t e0 = (((size_t)blk * Hkv + kh) * CFC_KV_BS + off) * D;
+  if constexpr (F8) {
+    float qa[8], qb[8];
+    unpack8(pa, qa);
+    unpack8(pb, qb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { qa[j] *= inv_k; qb[j] *= inv_k; }
+    uint8_t* dst = reinterpret_cast<uint8_t*>(k_cache) + e0;
+    *reinterpret_cast<uint2*>(dst + c * 8) = pack8_fp8(qa);
+    *reinterpret_cast<uint2*>(dst + half + c * 8) = pack8_fp8(qb);
+  } else {
+    uint16_t* dst = reinterpret_cast<uint16_t*>(k_cache) + e0;
+    *reinterpret_cast<uint4*>(dst + c * 8) = pa;
+    *reinterpret_cast<uint4*>(dst + half + c * 8) = pb;
+  }
+}
+
+// V 8-vector c (elements [8c, 8c+8)) of kv-head kh into the transposed cache at slot `slot`.
+template <bool F8>
+__device__ __forceinline__ void kv_write_v(void* v_cache, int slot, int kh, int Hkv, int D, int c, uint4 val,
+                                           float inv_v) {
+  const int blk = slot / CFC_KV_BS, off = slot % CFC_KV_BS;
+  const size_t e0 = (((size_t)blk * Hkv + kh) * D + c * 8) * CFC_KV_BS + kv_v_slot(off);
+  const uint16_t* e = reinterpret_cast<const uint16_t*>(&val);
+  if constexpr (F8) {
+    uint8_t* dst = reinterpret_cast<uint8_t*>(v_cache) + e0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dst[j * CFC_KV_BS] = f2fp8(bf2f(e[j]) * inv_v);
+  } else {
+    uint16_t* dst = reinterpret_cast<uint16_t*>(v_cache) + e0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dst[j * CFC_KV_BS] = e[j];
+  }
+}
+
 #define CFC_CHECK_LAUNCH() (int)hipGetLastError()

@@ -11,35 +11,13 @@
 
 namespace {
 
-constexpr int KV_BS = 32;
+constexpr int KV_BS = CFC_KV_BS;
 
-__device__ __forceinline__ int v_slot(int key_in_block) {
-  const int hi = key_in_block >> 4, g = (key_in_block >> 2) & 3, j = (key_in_block & 3) + 4 * hi;
-  return 8 * g + j;
-}
+__device__ __forceinline__ int v_slot(int key_in_block) { return kv_v_slot(key_in_block); }
 
 // qkv: [T, (Hq + 2*Hkv) * D] (q heads | k heads | v heads), positions [T], slots [T] (-1 = skip
-// cache write), cos_sin [max_pos][D/2][2] fp32 (cos, sin interleaved).
-// 8 consecutive qkv values of token row `row_off` (element offset): from the bf16 qkv, or summed
-// from `split` fp32 split-K slabs of the decode GEMM (slab stride `slab` elements) and rounded to
-// bf16 -- the same values splitk_reduce would have written, without the round trip
-__device__ __forceinline__ void qkv_load8(const uint16_t* qkv, const float* part, int split, size_t slab, size_t off,
-                                          float* f) {
-  if (part == nullptr) {
-    unpack8(*reinterpret_cast<const uint4*>(qkv + off), f);
-    return;
-  }
-  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-  for (int p = 0; p < split; ++p) {
-    const float4 x = *reinterpret_cast<const float4*>(part + p * slab + off);
-    const float4 y = *reinterpret_cast<const float4*>(part + p * slab + off + 4);
-    a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
-    b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
-  }
-  f[0] = bf2f(f2bf(a.x)); f[1] = bf2f(f2bf(a.y)); f[2] = bf2f(f2bf(a.z)); f[3] = bf2f(f2bf(a.w));
-  f[4] = bf2f(f2bf(b.x)); f[5] = bf2f(f2bf(b.y)); f[6] = bf2f(f2bf(b.z)); f[7] = bf2f(f2bf(b.w));
-}
-
+// cache write), cos_sin [max_pos][D/2][2] fp32 (cos, sin interleaved); the per-item math lives in
+// common.h (rope_rot8 / kv_write_k / kv_write_v), shared with the fused decode attention.
 template <bool F8>
 __global__ void __launch_bounds__(64) rope_kv_kernel(const uint16_t* __restrict__ qkv, const int32_t* __restrict__ positions,
                                                      const int32_t* __restrict__ slots, const float* __restrict__ cos_sin,
@@ -62,65 +40,22 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const uint16_t* __restrict_
   const int slot = slots[tok];
   if (it < n_rot) {
     const int head = it / nv, c = it - head * nv;  // head < Hq: query, else key (head - Hq)
-    const float4* cs = reinterpret_cast<const float4*>(cos_sin + ((size_t)positions[tok] * half + c * 8) * 2);
-    float csv[16];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float4 t = cs[j];
-      csv[4 * j] = t.x; csv[4 * j + 1] = t.y; csv[4 * j + 2] = t.z; csv[4 * j + 3] = t.w;
-    }
-    float a[8], b[8], ra[8], rb[8];
-    qkv_load8(qkv, part, split, slab, row0 + head * D + c * 8, a);
-    qkv_load8(qkv, part, split, slab, row0 + head * D + half + c * 8, b);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float cv = csv[2 * j], sv = csv[2 * j + 1];
-      ra[j] = a[j] * cv - b[j] * sv;
-      rb[j] = b[j] * cv + a[j] * sv;
-    }
-    const uint4 pa = pack8(ra), pb = pack8(rb);
+    uint4 pa, pb;
+    rope_rot8(qkv, part, split, slab, row0 + (size_t)head * D, half, c,
+              cos_sin + (size_t)positions[tok] * half * 2, pa, pb);
     if (head < Hq) {
       uint16_t* dst = q_out + ((size_t)tok * Hq + head) * D;
       *reinterpret_cast<uint4*>(dst + c * 8) = pa;
       *reinterpret_cast<uint4*>(dst + half + c * 8) = pb;
     } else if (slot >= 0) {
-      const int kh = head - Hq;
-      const int blk = slot / KV_BS, off = slot % KV_BS;
-      const size_t e0 = (((size_t)blk * Hkv + kh) * KV_BS + off) * D;
-      if constexpr (F8) {
-        float qa[8], qb[8];
-        unpack8(pa, qa);     // round to bf16 first: the same values the bf16 cache would hold
-        unpack8(pb, qb);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { qa[j] *= inv_k; qb[j] *= inv_k; }
-        uint8_t* dst = reinterpret_cast<uint8_t*>(k_cache) + e0;
-        *reinterpret_cast<uint2*>(dst + c * 8) = pack8_fp8(qa);
-        *reinterpret_cast<uint2*>(dst + half + c * 8) = pack8_fp8(qb);
-      } else {
-        uint16_t* dst = reinterpret_cast<uint16_t*>(k_cache) + e0;
-        *reinterpret_cast<uint4*>(dst + c * 8) = pa;
-        *reinterpret_cast<uint4*>(dst + half + c * 8) = pb;
-      }
+      kv_write_k<F8>(k_cache, slot, head - Hq, Hkv, D, c, pa, pb, inv_k);
     }
   } else if (slot >= 0) {
     const int v = it - n_rot;
     const int kh = v / (D / 8), c = v % (D / 8);
     float vf[8];
-    qkv_load8(qkv, part, split, slab, row0 + (Hq + Hkv + kh) * D + c * 8, vf);
-    const uint4 val = pack8(vf);
-    const int blk = slot / KV_BS, off = slot % KV_BS;
-    const int sl = v_slot(off);
-    const size_t e0 = (((size_t)blk * Hkv + kh) * D + c * 8) * KV_BS + sl;
-    const uint16_t* e = reinterpret_cast<const uint16_t*>(&val);
-    if constexpr (F8) {
-      uint8_t* dst = reinterpret_cast<uint8_t*>(v_cache) + e0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dst[j * KV_BS] = f2fp8(bf2f(e[j]) * inv_v);
-    } else {
-      uint16_t* dst = reinterpret_cast<uint16_t*>(v_cache) + e0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dst[j * KV_BS] = e[j];
-    }
+    qkv_load8(qkv, part, split, slab, row0 + (size_t)(Hq + Hkv + kh) * D + c * 8, vf);
+    kv_write_v<F8>(v_cache, slot, kh, Hkv, D, c, pack8(vf), inv_v);
   }
 }
 

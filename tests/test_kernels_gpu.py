@@ -538,6 +538,71 @@ def test_rope_kv_write_from_splitk_slabs_matches_reduce_then_rope(split):
     assert torch.equal(q1, q2) and torch.equal(k1, k2) and torch.equal(v1, v2)
 
 
+@pytest.mark.parametrize("G", [1, 4, 8])
+@pytest.mark.parametrize("part_blocks", [4, -1, -3])
+@pytest.mark.parametrize("src", ["bf16", "slabs3"])
+@pytest.mark.parametrize("kv", ["bf16", "fp8"])
+@pytest.mark.parametrize("window", [0, 100])
+def test_paged_decode_rope_attention_fused_matches_two_kernels(G, part_blocks, src, kv, window):
+    """RoPE + KV write in the decode attention's prologue == rope_kv_write(_part) -> paged_decode_attention,
+    bit for bit: output, K cache and V cache (one row with slot -1 writes nothing); and against the
+    fp32 reference of the same step."""
+    Hkv, D = 2, 128
+    Hq = Hkv * G
+    ctx = [1, 31, 32, 33, 100, 517, 2049, 64]
+    kc, vc, bt = _fill_cache(ctx, Hkv, D)
+    ks, vs = (0.5, 0.25) if kv == "fp8" else (1.0, 1.0)
+    if kv == "fp8":
+        kc = (kc.float() / ks).clamp(-448, 448).to(F8)
+        vc = (vc.float() / vs).clamp(-448, 448).to(F8)
+    B, N = len(ctx), (Hq + 2 * Hkv) * D
+    pos = torch.tensor([n - 1 for n in ctx], dtype=torch.int32)
+    slots = torch.tensor([int(bt[b, (n - 1) // 32]) * 32 + (n - 1) % 32 for b, n in enumerate(ctx)], dtype=torch.int32)
+    slots[3] = -1
+    cs = R.rope_cos_sin(4096, D, 1e6, device=DEV)
+    if src == "bf16":
+        qkv = torch.randn(B, N, device=DEV).bfloat16()
+    else:
+        qkv = torch.randn(3, B, N, device=DEV)
+    args = (pos.to(DEV), slots.to(DEV), cs)
+    bt_d, cl = bt.to(DEV), torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    k1, v1, k2, v2 = kc.to(DEV), vc.to(DEV), kc.to(DEV), vc.to(DEV)
+    if src == "bf16":
+        q = K.rope_kv_write(qkv, *args, k1, v1, Hq, Hkv, D, k_scale=ks, v_scale=vs)
+    else:
+        q = K.rope_kv_write_part(qkv, *args, k1, v1, Hq, Hkv, D, k_scale=ks, v_scale=vs)
+    o1 = K.paged_decode_attention(q, k1, v1, bt_d, cl, 1 / math.sqrt(D), part_blocks=part_blocks, window=window,
+                                  k_scale=ks, v_scale=vs)
+    o2 = K.paged_decode_rope_attention(qkv, *args, k2, v2, bt_d, cl, 1 / math.sqrt(D), Hq, Hkv, D,
+                                       part_blocks=part_blocks, window=window, k_scale=ks, v_scale=vs)
+    torch.cuda.synchronize()
+    assert torch.equal(k1.view(torch.uint8) if kv == "fp8" else k1, k2.view(torch.uint8) if kv == "fp8" else k2)
+    assert torch.equal(v1.view(torch.uint8) if kv == "fp8" else v1, v2.view(torch.uint8) if kv == "fp8" else v2)
+    assert torch.equal(o1, o2)
+    # fp32 reference of the whole step
+    kr, vr = kc.clone(), vc.clone()
+    qb = (qkv.float().sum(0).bfloat16() if src != "bf16" else qkv).cpu()
+    qr = R.rope_kv_write(qb, pos, slots, cs.cpu(), kr, vr, Hq, Hkv, D, ks, vs)
+    ref = R.paged_decode_attention(qr, kr, vr, bt, torch.tensor(ctx, dtype=torch.int32), 1 / math.sqrt(D),
+                                   window=window, k_scale=ks, v_scale=vs)
+    _close(o2, ref, 3e-2 if kv == "fp8" else 2e-2)
+
+
+def test_paged_decode_rope_attention_rejects_bad_shapes():
+    Hq, Hkv, D = 8, 2, 128
+    kc, vc, bt = _fill_cache([40, 70], Hkv, D)
+    cs = R.rope_cos_sin(256, D, 1e4, device=DEV)
+    pos = torch.tensor([39, 69], dtype=torch.int32, device=DEV)
+    sl = torch.tensor([0, 1], dtype=torch.int32, device=DEV)
+    cl = torch.tensor([40, 70], dtype=torch.int32, device=DEV)
+    with pytest.raises(ValueError):     # wrong width
+        K.paged_decode_rope_attention(torch.randn(2, 100, device=DEV).bfloat16(), pos, sl, cs, kc.to(DEV), vc.to(DEV),
+                                      bt.to(DEV), cl, 0.1, Hq, Hkv, D)
+    with pytest.raises(ValueError):     # B mismatch between qkv and the per-row tensors
+        K.paged_decode_rope_attention(torch.randn(3, (Hq + 2 * Hkv) * D, device=DEV).bfloat16(), pos, sl, cs,
+                                      kc.to(DEV), vc.to(DEV), bt.to(DEV), cl, 0.1, Hq, Hkv, D)
+
+
 def test_dgemm_rejects_bad_shapes():
     x = torch.randn(8, 100, device=DEV).bfloat16()
     w = torch.randn(128, 100, device=DEV).bfloat16()
