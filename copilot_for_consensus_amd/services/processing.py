@@ -102,7 +102,8 @@ class ParsingService(_CleanupMixin, BaseService):
             self.publish("JSONParsed", archive_id=archive_id, message_count=1, message_doc_ids=[m["_id"]],
                          thread_count=1, thread_ids=[m["thread_id"]],
                          parsing_duration_seconds=round(time.perf_counter() - t, 6))
-        return {"messages": len(msgs), "threads": len(threads), "errors": errs}
+        return {"messages": len(msgs), "threads": len(threads), "errors": errs,
+                "message_doc_ids": [m["_id"] for m in msgs], "thread_ids": [x["_id"] for x in threads]}
 
     def on_failure(self, event_type, event, error):
         if event_type == "ArchiveIngested":
@@ -273,6 +274,12 @@ class EmbeddingService(BaseService):
             if done < len(set(chunk_ids)):
                 raise DocumentNotFoundError("chunks not visible yet")
             return 0  # already embedded (idempotent replay)
+        # each thread's chunks consecutive (first-appearance order): a thread-sharded index takes a
+        # thread's rows as one span, and the HBM index keeps them adjacent for the centroid pass
+        first: dict[str, int] = {}
+        for c in chunks:
+            first.setdefault(c["thread_id"], len(first))
+        chunks.sort(key=lambda c: first[c["thread_id"]])
         t = time.perf_counter()
         metas = [{"thread_id": c["thread_id"], "message_id": c["message_id"], "message_doc_id": c["message_doc_id"],
                   "chunk_index": c["chunk_index"]} for c in chunks]
@@ -364,6 +371,33 @@ class OrchestratorService(BaseService):
             raise DocumentNotFoundError("chunks not visible yet")
         return sorted({c["thread_id"] for c in chunks})
 
+    @staticmethod
+    def _scored(chunks: list[dict], scores: dict[str, float]) -> list[dict]:
+        missing = 0.0 if scores else 0.5        # neutral score (context_sources.py:21) only when none scored
+        out = []
+        for c in chunks:
+            cc = dict(c)
+            cc["similarity_score"] = scores.get(c["_id"], missing)
+            cc["source_type"] = "vector_store" if c["_id"] in scores else "thread_chunks"
+            out.append(cc)
+        return out
+
+    def candidates_many(self, thread_ids: list[str]) -> dict[str, list[dict]]:
+        """candidates() of many threads with ONE vector-store pass (centroid_scores_many: a single
+        gather + segment reduction on the HBM index instead of one search per thread)."""
+        chunks = {tid: self.store.query_documents("chunks", {"thread_id": tid}, limit=1 << 20) for tid in thread_ids}
+        scores: list[dict] = [{} for _ in thread_ids]
+        many = getattr(self.vectors, "centroid_scores_many", None)
+        if self.vectors is not None and many is not None and not getattr(self.vectors, "thread_sharded", False):
+            try:
+                scores = many([[c["_id"] for c in chunks[t] if c.get("embedding_generated")] for t in thread_ids])
+            except (RuntimeError, ValueError, OSError) as e:
+                self.log.warning("vector scoring failed; neutral scores", threads=len(thread_ids), error=repr(e))
+                scores = [{} for _ in thread_ids]
+        elif self.vectors is not None:
+            return {t: self.candidates(t) for t in thread_ids}
+        return {t: self._scored(chunks[t], sc) for t, sc in zip(thread_ids, scores)}
+
     def candidates(self, thread_id: str) -> list[dict]:
         """The thread's chunks scored by cosine to the thread's centroid, in ONE search restricted to
         the thread's own rows (HipFlatIndex: a device gather + GEMV; reference context_sources.py
@@ -382,17 +416,18 @@ class OrchestratorService(BaseService):
             except (RuntimeError, ValueError, OSError) as e:
                 self.log.warning("vector scoring failed; neutral scores", thread_id=thread_id, error=repr(e))
                 scores = {}
-        missing = 0.0 if scores else 0.5        # neutral score (context_sources.py:21) only when none scored
-        out = []
-        for c in chunks:
-            cc = dict(c)
-            cc["similarity_score"] = scores.get(c["_id"], missing)
-            cc["source_type"] = "vector_store" if c["_id"] in scores else "thread_chunks"
-            out.append(cc)
-        return out
+        return self._scored(chunks, scores)
+
+    def orchestrate_threads(self, thread_ids: list[str]) -> list[dict | None]:
+        """orchestrate_thread over many threads, their candidates scored in one vector-store pass
+        (the in-process batch driver, pipeline/rag.py, calls this once per batch)."""
+        cands = self.candidates_many(list(thread_ids))
+        return [self._request(t, cands[t]) for t in thread_ids]
 
     def orchestrate_thread(self, thread_id: str) -> dict | None:
-        cands = self.candidates(thread_id)
+        return self._request(thread_id, self.candidates(thread_id))
+
+    def _request(self, thread_id: str, cands: list[dict]) -> dict | None:
         if not cands or not all(c.get("embedding_generated") for c in cands):
             return None  # wait until every chunk of the thread is embedded
         sel = self.selector.select(thread_id, cands, self.top_k, self.budget)
@@ -424,11 +459,7 @@ class OrchestratorService(BaseService):
         self.metrics.increment("orchestrator_consensus_total", tags={"level": sig.level.value})
 
     def process_embeddings(self, chunk_ids: list[str]) -> int:
-        n = 0
-        for tid in self._resolve_threads(chunk_ids):
-            if self.orchestrate_thread(tid) is not None:
-                n += 1
-        return n
+        return sum(ev is not None for ev in self.orchestrate_threads(self._resolve_threads(chunk_ids)))
 
     def on_failure(self, event_type, event, error):
         if event_type == "EmbeddingsGenerated":

@@ -89,6 +89,12 @@ class VectorStore(ABC):
         return dict(zip(have, (X @ c).astype(float).tolist()))
 
 
+    def centroid_scores_many(self, groups: Sequence[Sequence[str]]) -> list[dict[str, float]]:
+        """centroid_scores of many id groups (one per thread); stores with a device path score them
+        all in one pass."""
+        return [self.centroid_scores(g) for g in groups]
+
+
 def _as_matrix(vectors, dim: int | None, device=None, dtype=torch.float32) -> torch.Tensor:
     if isinstance(vectors, torch.Tensor):
         t = vectors
@@ -306,6 +312,27 @@ class HipFlatIndex(VectorStore):
             idx = torch.from_numpy(rows[rows >= 0]).to(self.device)
             s = self.span_centroid_scores(self._X.index_select(0, idx), [(0, len(have))])
             return dict(zip(have, s.cpu().tolist()))
+
+    def centroid_scores_many(self, groups):
+        """All groups in one gather + one segment reduction (span_centroid_scores over the gathered
+        rows, one span per group) and one copy out."""
+        with self._lock:
+            have, rows_all, spans = [], [], []
+            for g in groups:
+                g = list(g)
+                rows = self._tab.find_many(g) if g else np.zeros(0, np.int64)
+                h = [i for i, r in zip(g, rows) if r >= 0]
+                a = sum(len(x) for x in have)
+                have.append(h)
+                rows_all.append(rows[rows >= 0])
+                spans.append((a, a + len(h)))
+            n = sum(len(h) for h in have)
+            if n == 0:
+                return [{} for _ in groups]
+            idx = torch.from_numpy(np.concatenate(rows_all)).to(self.device)
+            live = [(a, b) for a, b in spans if b > a]
+            s = self.span_centroid_scores(self._X.index_select(0, idx), live).cpu().tolist()
+        return [dict(zip(h, s[a:b])) for h, (a, b) in zip(have, spans)]
 
     @staticmethod
     def span_centroid_scores(X: torch.Tensor, spans) -> torch.Tensor:

@@ -108,7 +108,7 @@ def test_two_processes_share_regions_over_ipc():
         assert res["graph_max_err"] <= 0.0625, res
 
 
-def _tp_worker(rank, world, port, q, prompts, n_new):
+def _tp_worker(rank, world, port, q, prompts, n_new, cfg_name="tiny", seed=5, blocks=64):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                           LOCAL_RANK=str(rank), CFC_DIST_BACKEND="gloo")
@@ -120,12 +120,14 @@ def _tp_worker(rank, world, port, q, prompts, n_new):
         from copilot_for_consensus_amd.runtime.kv_cache import PagedKVCache
         env = init_distributed(backend="gloo")
         g = make_groups(env, tp=world)
-        cfg = get_config("tiny")
-        full = DecoderWeights.random(cfg, env.device, seed=5)
+        cfg = get_config(cfg_name)
+        full = DecoderWeights.random(cfg, env.device, seed=seed)
         w = shard_weights(full, g.tp_rank, g.tp_size)
+        del full
+        torch.cuda.empty_cache()
         ar = maybe_create(g.tp_group, env.device)
         m = DecoderModel(w, tp_group=g.tp_group, custom_ar=ar)
-        kv = PagedKVCache(cfg.layers, 64, w.kv_heads, cfg.head_dim, env.device)
+        kv = PagedKVCache(cfg.layers, blocks, w.kv_heads, cfg.head_dim, env.device)
         eng = LLMEngine(m, kv, use_graph=True)
         # greedy: every decode collective (o / down all-reduce, argmax key reduce) on the IPC
         # kernels, so the step is captured whole although the group is gloo
@@ -181,3 +183,48 @@ def test_tp2_decoder_with_oneshot_allreduce_matches_tp1():
     assert res[0]["tokens"] == res[1]["tokens"]
     agree = sum(a == b for x, y in zip(res[0]["tokens"], ref) for a, b in zip(x, y))
     assert agree >= 0.9 * sum(len(x) for x in ref), (res[0]["tokens"], ref)
+
+
+def _run_tp2(prompts, n_new, **kw):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, q, prompts, n_new), kwargs=kw) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in procs:
+            r, out = q.get(timeout=280)
+            res[r] = out
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    return res
+
+
+def test_tp2_mistral7b_matches_tp1_greedy():
+    """Mistral-7B at TP=2 (two processes sharing the GPU, 2 x 7.2 GB shards through shard_weights, the
+    packed decode GEMM's TP shard shapes, IPC all-reduce in the captured decode graph) generates the
+    same 32 greedy tokens as the unsharded model for every prompt."""
+    from copilot_for_consensus_amd.models.decoder import DecoderModel, DecoderWeights, get_config
+    from copilot_for_consensus_amd.runtime.engine import LLMEngine
+    from copilot_for_consensus_amd.runtime.kv_cache import PagedKVCache
+    cfg = get_config("mistral-7b")
+    g = torch.Generator().manual_seed(11)
+    prompts = [[1] + torch.randint(3, cfg.vocab_size, (n,), generator=g).tolist() for n in (37, 300, 5, 129, 64, 800)]
+    m1 = DecoderModel(DecoderWeights.random(cfg, "cuda:0", seed=7))
+    ref = LLMEngine(m1, PagedKVCache(cfg.layers, 256, cfg.kv_heads, cfg.head_dim, "cuda:0"), use_graph=True).generate(
+        prompts, 32, ignore_eos=True).tokens
+    del m1
+    torch.cuda.empty_cache()
+    res = _run_tp2(prompts, 32, cfg_name="mistral-7b", seed=7, blocks=256)
+    for r in range(2):
+        assert "exception" not in res[r], res[r]
+        assert res[r]["custom_ar"] and res[r]["errors"] == 0, res[r]
+        assert res[r]["graphed"], "TP=2 greedy decode should run as a captured graph"
+    assert res[0]["tokens"] == res[1]["tokens"]
+    assert res[0]["tokens"] == ref, (res[0]["tokens"], ref)

@@ -15,9 +15,10 @@ def test_rag_pipeline_end_to_end_cpu():
     rag.prepare_sources(3, [0])
     batch = rag.prepare(3, 0)
     assert len(batch.threads) == 3 and len(batch.prompts) == 3
-    for sel in batch.selections:
-        assert 1 <= len(sel.selected_chunks) <= 5
-        assert sel.total_tokens <= 2048
+    for ev in batch.selections:     # the orchestrator service's SummarizationRequested events
+        assert ev["event_type"] == "SummarizationRequested"
+        assert 1 <= len(ev["data"]["selected_chunks"]) <= 5
+        assert ev["data"]["context_selection"]["total_tokens"] <= 2048
     # prompts contain the excerpts and all placeholders were substituted
     assert all("{" not in p.split("Most relevant excerpts:")[0][-200:] for p in batch.prompt_texts)
     assert all("Message 1:" in p for p in batch.prompt_texts)
