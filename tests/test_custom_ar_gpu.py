@@ -206,25 +206,58 @@ def _run_tp2(prompts, n_new, **kw):
     return res
 
 
+def _last_logits(eng, model, prompts):
+    """fp32 logits of every prompt's last token (the prefill's sampling input), prompt order."""
+    seen = []
+    orig = model.logits
+    model.logits = lambda h: seen.append(orig(h).float()) or seen[-1]
+    try:
+        toks = eng.generate(prompts, max_new_tokens=1, ignore_eos=True).tokens
+    finally:
+        model.logits = orig
+    lg = seen[0]
+    assert lg.shape[0] == len(prompts) and lg.argmax(-1).tolist() == [t[0] for t in toks]
+    return lg
+
+
 def test_tp2_mistral7b_matches_tp1_greedy():
     """Mistral-7B at TP=2 (two processes sharing the GPU, 2 x 7.2 GB shards through shard_weights, the
-    packed decode GEMM's TP shard shapes, IPC all-reduce in the captured decode graph) generates the
-    same 32 greedy tokens as the unsharded model for every prompt."""
+    packed decode GEMM's TP shard shapes, IPC all-reduce in the captured decode graph) against the
+    unsharded model, 32 greedy tokens for 6 prompts.
+
+    Bit-equal free-running sequences are not a valid criterion: the TP all-reduce sums two fp32
+    partial products where TP=1 sums one, so bf16 hidden states differ in the last bit and a
+    near-tie between the two best tokens (random-init logits are nearly flat: 32000 Gaussian-like
+    values, top-2 gap ~0.2 sigma) can flip, after which the sequences condition on different text.
+    So every TP=2 token is checked against TP=1 teacher-forced on TP=2's own prefix: it must be
+    TP=1's argmax in >= 90 % of the 192 steps and within 0.1 sigma of TP=1's max logit in all of
+    them (an unrelated token sits ~4 sigma below the max)."""
     from copilot_for_consensus_amd.models.decoder import DecoderModel, DecoderWeights, get_config
     from copilot_for_consensus_amd.runtime.engine import LLMEngine
     from copilot_for_consensus_amd.runtime.kv_cache import PagedKVCache
     cfg = get_config("mistral-7b")
     g = torch.Generator().manual_seed(11)
     prompts = [[1] + torch.randint(3, cfg.vocab_size, (n,), generator=g).tolist() for n in (37, 300, 5, 129, 64, 800)]
-    m1 = DecoderModel(DecoderWeights.random(cfg, "cuda:0", seed=7))
-    ref = LLMEngine(m1, PagedKVCache(cfg.layers, 256, cfg.kv_heads, cfg.head_dim, "cuda:0"), use_graph=True).generate(
-        prompts, 32, ignore_eos=True).tokens
-    del m1
-    torch.cuda.empty_cache()
     res = _run_tp2(prompts, 32, cfg_name="mistral-7b", seed=7, blocks=256)
     for r in range(2):
         assert "exception" not in res[r], res[r]
         assert res[r]["custom_ar"] and res[r]["errors"] == 0, res[r]
         assert res[r]["graphed"], "TP=2 greedy decode should run as a captured graph"
-    assert res[0]["tokens"] == res[1]["tokens"]
-    assert res[0]["tokens"] == ref, (res[0]["tokens"], ref)
+        assert res[r]["tokens"] == res[r]["eager"], (res[r]["tokens"], res[r]["eager"])
+    tp2 = res[0]["tokens"]
+    assert tp2 == res[1]["tokens"]
+    assert all(len(t) == 32 for t in tp2)
+    m1 = DecoderModel(DecoderWeights.random(cfg, "cuda:0", seed=7))
+    eng = LLMEngine(m1, PagedKVCache(cfg.layers, 512, cfg.kv_heads, cfg.head_dim, "cuda:0"), use_graph=False,
+                    prefix_cache=False)
+    exact, worst = 0, 0.0
+    for j in range(32):
+        lg = _last_logits(eng, m1, [p + t[:j] for p, t in zip(prompts, tp2)])
+        sig = lg.std(-1)
+        for i, t in enumerate(tp2):
+            gap = float((lg[i].max() - lg[i, t[j]]) / sig[i])
+            worst = max(worst, gap)
+            exact += int(gap == 0.0)
+    n = 32 * len(prompts)
+    assert worst <= 0.1, f"a TP=2 token is {worst:.3f} sigma below TP=1's best (exact {exact}/{n})"
+    assert exact >= 0.9 * n, f"TP=2 matched TP=1's argmax in {exact}/{n} teacher-forced steps"
