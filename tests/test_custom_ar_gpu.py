@@ -210,7 +210,12 @@ def _last_logits(eng, model, prompts):
     """fp32 logits of every prompt's last token (the prefill's sampling input), prompt order."""
     seen = []
     orig = model.logits
-    model.logits = lambda h: seen.append(orig(h).float()) or seen[-1]
+
+    def grab(h):
+        lg = orig(h)
+        seen.append(lg.float())
+        return lg
+    model.logits = grab
     try:
         toks = eng.generate(prompts, max_new_tokens=1, ignore_eos=True).tokens
     finally:
