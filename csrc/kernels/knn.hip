@@ -280,6 +280,162 @@ __global__ void __launch_bounds__(256) knn_topk_kernel(const uint16_t* __restric
   }
 }
 
+// ------------------------------------------------------------------ streamed scan + top-k (large k)
+// With a large k the per-chunk candidates of knn_topk_kernel are a big share of the rows (k = 150
+// from 512-row chunks: 29 % of the index written as candidates and read again by the merge).  Here
+// a workgroup scans a long span (KS_SPAN rows) in KS_SUB-row sub-chunks and keeps, per query, a
+// candidate buffer in LDS behind a running threshold: only rows scoring above the k-th best key
+// the buffer held at its last cut are appended, and when the next sub-chunk could overflow the
+// buffer it is cut back to its exact top k (the threshold rises).  k candidates per query leave
+// per KS_SPAN rows (0.9 % at k = 150).  Rows equal to the threshold that arrive after a cut are
+// skipped: the buffer already holds k keys >= it, so the result is exact up to tie order.
+constexpr int KS_SUB = 256, KS_CAP = 512, KS_SPAN = 16384;
+
+// keys held KS_CAP / 64 per lane (entry lane + 64 j; 0 = empty): the exact kk-th largest
+__device__ __forceinline__ uint32_t ks_kth(const uint32_t* key, int kk) {
+  uint32_t thr = 0;
+  for (int b = 31; b >= 0; --b) {
+    const uint32_t cand = thr | (1u << b);
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < KS_CAP / 64; ++j) c += __popcll(__ballot(key[j] >= cand));
+    if (c >= kk) thr = cand;                 // wave-uniform decision
+  }
+  return thr;
+}
+
+// Cut a query's buffer (cnt > kk entries) to its exact top kk, in place (wave-level; every entry is
+// in registers before the first write).  Returns the kk-th largest key (the new threshold).
+__device__ __forceinline__ uint32_t ks_cut(uint32_t* bk, uint32_t* br, int cnt, int kk) {
+  const int lane = threadIdx.x & 63;
+  uint32_t key[KS_CAP / 64], row[KS_CAP / 64];
+#pragma unroll
+  for (int j = 0; j < KS_CAP / 64; ++j) {
+    const int i = lane + 64 * j;
+    key[j] = i < cnt ? bk[i] : 0u;
+    row[j] = i < cnt ? br[i] : 0u;
+  }
+  const uint32_t thr = ks_kth(key, kk);
+  int gt = 0;
+#pragma unroll
+  for (int j = 0; j < KS_CAP / 64; ++j) gt += __popcll(__ballot(key[j] > thr));
+  const uint32_t need = (uint32_t)(kk - gt);
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t base_gt = 0, base_eq = 0;
+#pragma unroll
+  for (int j = 0; j < KS_CAP / 64; ++j) {
+    const bool g = key[j] > thr, e = key[j] == thr && key[j] != 0u;
+    const uint64_t bg = __ballot(g), be = __ballot(e);
+    int slot = -1;
+    if (g) slot = (int)(base_gt + __popcll(bg & below));
+    else if (e) {
+      const uint32_t q = base_eq + __popcll(be & below);
+      if (q < need) slot = gt + (int)q;
+    }
+    if (slot >= 0) { bk[slot] = key[j]; br[slot] = row[j]; }
+    base_gt += __popcll(bg);
+    base_eq += __popcll(be);
+  }
+  return thr;
+}
+
+template <int KC>
+__global__ void __launch_bounds__(256) knn_topk_stream_kernel(const uint16_t* __restrict__ X,
+                                                              const uint16_t* __restrict__ Q, int N, int nq,
+                                                              const float* __restrict__ xnorm2,
+                                                              const float* __restrict__ qnorm2,
+                                                              const uint8_t* __restrict__ alive, int k, int row_lo,
+                                                              float* __restrict__ out_v, int64_t* __restrict__ out_i) {
+  constexpr int D = KC * 32;
+  __shared__ float sc[16 * KS_SUB];                                        // 16 KB scores
+  __shared__ uint32_t bk[16 * KS_CAP], br[16 * KS_CAP];                     // 64 KB buffers
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lo = row_lo + blockIdx.x * KS_SPAN, hi = min(N, lo + KS_SPAN);
+  const int col = lane & 15, g = lane >> 4;
+  const bool qv = col < nq;
+  bf16x8_t qf[KC];
+  const uint16_t* qrow = Q + (size_t)(qv ? col : 0) * D;
+#pragma unroll
+  for (int c = 0; c < KC; ++c)
+    qf[c] = as_bf16x8(qv ? *reinterpret_cast<const uint4*>(qrow + 32 * c + 8 * g) : make_uint4(0, 0, 0, 0));
+  const float qn = (qnorm2 && qv) ? qnorm2[col] : 0.f;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int cnt[4] = {0, 0, 0, 0};          // this wave's queries w, w + 4, w + 8, w + 12 (wave-uniform)
+  uint32_t thr[4] = {0u, 0u, 0u, 0u};
+  for (int s0 = lo; s0 < hi; s0 += KS_SUB) {
+    const int s1 = min(hi, s0 + KS_SUB), len = s1 - s0;
+    const int ngroups = (len + 15) / 16;
+    for (int grp = w; grp < ngroups; grp += 4) {
+      const int r0 = s0 + grp * 16;
+      const int r = min(r0 + col, s1 - 1);
+      const uint16_t* xr = X + (size_t)r * D;
+      uint4 a[KC];
+#pragma unroll
+      for (int c = 0; c < KC; ++c) a[c] = *reinterpret_cast<const uint4*>(xr + 32 * c + 8 * g);
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < KC; ++c) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[c]), qf[c], acc, 0, 0, 0);
+      if (qv) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = r0 + 4 * g + i;
+          if (row < s1) {
+            float v = acc[i];
+            if (xnorm2) v = -(xnorm2[row] + qn - 2.f * v);
+            if (alive && !alive[row]) v = -INFINITY;
+            sc[col * KS_SUB + (row - s0)] = v;
+          }
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int qi = w + 4 * t;
+      if (qi < nq) {
+        uint32_t* qk = bk + qi * KS_CAP;
+        uint32_t* qr = br + qi * KS_CAP;
+#pragma unroll
+        for (int j = 0; j < KS_SUB / 64; ++j) {
+          const int i = lane + 64 * j;
+          const uint32_t key = i < len ? f2key(sc[qi * KS_SUB + i]) : 0u;
+          const bool p = i < len && key > thr[t];
+          const uint64_t b = __ballot(p);
+          if (p) {
+            const int slot = cnt[t] + __popcll(b & below);
+            qk[slot] = key;
+            qr[slot] = (uint32_t)(s0 - lo + i);
+          }
+          cnt[t] += __popcll(b);
+        }
+        if (cnt[t] > KS_CAP - KS_SUB) {        // the next sub-chunk might not fit: cut to k (k <= 256)
+          thr[t] = ks_cut(qk, qr, cnt[t], k);
+          cnt[t] = k;
+        }
+      }
+    }
+    __syncthreads();                              // sc is the next sub-chunk's
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int qi = w + 4 * t;
+    if (qi < nq) {
+      uint32_t* qk = bk + qi * KS_CAP;
+      uint32_t* qr = br + qi * KS_CAP;
+      int n = cnt[t];
+      if (n > k) {
+        ks_cut(qk, qr, n, k);
+        n = k;
+      }
+      const size_t o = ((size_t)qi * gridDim.x + blockIdx.x) * k;
+      for (int s2 = lane; s2 < k; s2 += 64) {
+        out_v[o + s2] = s2 < n ? key2f(qk[s2]) : -INFINITY;
+        out_i[o + s2] = s2 < n ? (int64_t)lo + qr[s2] : -1;
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) l2_normalize_kernel(uint16_t* __restrict__ out, const uint16_t* __restrict__ in,
                                                            float* __restrict__ norms2, int dim) {
   __shared__ float red[16];
@@ -391,8 +547,9 @@ namespace {
 // (the candidate arrays are written and merged: k = 150 from 256-row chunks is 59 % of the index).
 // Measured on 100M x 384: 1 query 2048 rows 12.6 ms (6.1 TB/s) vs 1024 rows 14.1 ms; 16 queries
 // 256 rows 14.1 ms vs 1024 rows 23.6 ms (k = 10), 512 rows 20.7 ms vs 256 rows 22.8 ms (k = 150).
+// k > 32: the streamed kernel, k candidates per KS_SPAN rows.
 constexpr int knn_flat_rows(int nq, int k) {
-  return nq <= 4 ? 2048 : nq <= 8 ? (k > 32 ? 1024 : 512) : (k > 32 ? 512 : 256);
+  return k > 32 ? KS_SPAN : nq <= 4 ? 2048 : nq <= 8 ? 512 : 256;
 }
 
 template <int KC>
@@ -441,6 +598,18 @@ CFC_API int cfc_knn_topk(const void* X, const void* Q, int N, int row_lo, int nq
   if (nq < 1 || nq > 16 || dim % 32 != 0 || N <= row_lo || row_lo < 0 || k < 1 || k > 256) return -1;
   const int rows = knn_flat_rows(nq, k);
   const int nch = (N - row_lo + rows - 1) / rows;
+  if (rows == KS_SPAN) {
+#define KS(KC) \
+  case KC: \
+    knn_topk_stream_kernel<KC><<<nch, 256, 0, stream>>>((const uint16_t*)X, (const uint16_t*)Q, N, nq, xnorm2, qnorm2, \
+                                                       alive, k, row_lo, out_v, out_i); \
+    return CFC_CHECK_LAUNCH();
+    switch (dim / 32) {
+      KS(4) KS(8) KS(12) KS(16) KS(24) KS(32)
+      default: return -2;
+    }
+#undef KS
+  }
   return knn_topk_dispatch(dim, X, Q, N, nq, xnorm2, qnorm2, alive, k, row_lo, nullptr, 1, 1, nullptr, nch, out_v,
                            out_i, nch, nq, rows, stream);
 }

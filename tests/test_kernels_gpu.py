@@ -235,7 +235,8 @@ def test_gumbel_sampling_distribution():
 
 
 @pytest.mark.parametrize("N,nq,k,metric", [(5000, 1, 10, "dot"), (3000, 16, 100, "l2"), (1024, 7, 1, "dot"),
-                                           (70, 3, 20, "l2"), (40000, 16, 256, "dot")])
+                                           (70, 3, 20, "l2"), (40000, 16, 256, "dot"), (100000, 16, 150, "dot"),
+                                           (70000, 2, 33, "l2"), (50000, 5, 256, "l2")])
 def test_knn_topk_fused_matches_reference(N, nq, k, metric):
     """Fused scan + per-chunk radix select (+ candidate merge) vs torch.topk of fp32 scores of the
     same bf16 rows; dead rows and a row window excluded."""
