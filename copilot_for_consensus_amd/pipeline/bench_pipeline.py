@@ -7,6 +7,7 @@ local_llm_summarizer.py:107 (one thread per call); embedding one chunk per call
 from __future__ import annotations
 
 import dataclasses
+import os
 import random
 import time
 
@@ -73,7 +74,12 @@ class BenchPipeline:
         self.kv = PagedKVCache(self.cfg.layers, nblk, w.kv_heads, self.cfg.head_dim, self.device, dtype=kvd)
         self.engine = LLMEngine(self.model, self.kv, max_prefill_tokens=prefill_tokens, use_graph=use_graph)
         self.rag = None
-        self.side_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        # the next batch's encoder / kNN work runs on this stream beside the decode graph.  Its kernels
+        # only get CUs the decode's workgroups leave free, so alone 0.15 s of encoder work stretches to
+        # ~0.9 s of wall time (BENCH_r03 embed stage); CFC_PREP_STREAM_PRIORITY=high dispatches them
+        # ahead of the decode's queued workgroups instead (shorter embed stage, decode pays its GPU time)
+        prio = -1 if os.environ.get("CFC_PREP_STREAM_PRIORITY", "normal") == "high" else 0
+        self.side_stream = torch.cuda.Stream(self.device, priority=prio) if self.device.type == "cuda" else None
         self._last_gen_s: float | None = None
         self._last_prep_s = 0.0
         if not llm_only and not self.follower:

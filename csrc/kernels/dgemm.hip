@@ -118,7 +118,9 @@ __device__ __forceinline__ uint4 dg_ldw(const uint16_t* p) {
 }
 
 // ABL: ablation builds for the timing probes only (scripts/bench_dgemm.py --ablate); 0 in production.
-//   1 = no X DMA, 2 = no ds_read / MFMA (W loads kept live), 4 = no K-order rotation.
+//   1 = no X DMA, 2 = no ds_read / MFMA (W loads kept live), 4 = no K-order rotation,
+//   16 = X first: the loaders' first X stages enter the CU's memory pipeline before the compute
+//   waves' W ring fill (one extra barrier), so the first MFMAs do not wait behind ~96 KB of W.
 // PACKED: W in the fragment-packed layout of cfc_dgemm_pack for this BN: tile-major, then 32-deep
 // k group, then wave: Wp[N/BN][K/32][BN/16][64][8], so the 16 rows x 32 k of one MFMA B fragment
 // are 1 KB contiguous in lane order and a workgroup's whole W slice (BN rows x its K range) is ONE
@@ -173,6 +175,7 @@ __global__ void __launch_bounds__((64 * DgShape<BM, BN>::WAVES), 1)
 #pragma unroll
     for (int p = 0; p < S::NSX - 1; ++p)
       if (p < nst) issue(p, p);
+    if constexpr ((ABL & 16) != 0) asm volatile("s_barrier" ::: "memory");
     int slot = 0;
     for (int st = 0; st < nst; ++st) {
       if constexpr ((ABL & 1) != 0) dg_wait_barrier<0>();
@@ -208,6 +211,7 @@ __global__ void __launch_bounds__((64 * DgShape<BM, BN>::WAVES), 1)
       dst[1] = dg_ldw<NTW>(wp + s * 64 + 32);
     }
   };
+  if constexpr ((ABL & 16) != 0) asm volatile("s_barrier" ::: "memory");
 #pragma unroll
   for (int p = 0; p < D; ++p) load_stage(phys(min(p, nst - 1)), ring[p]);
   f32x4_t acc[S::MT];
@@ -385,7 +389,7 @@ CFC_API int cfc_dgemm_pack(const void* w, void* wp, int N, int K, int bn, hipStr
 // (not nontemporal) cache policy on the weight stream.
 CFC_API int cfc_dgemm_ablate(const void* x, const void* w, int M, int N, int K, int split, int bn, int abl,
                              float* part, hipStream_t stream) {
-  if (M > 128 || (abl & ~15)) return -1;
+  if (M > 128 || (abl & ~31)) return -1;
   if (const int e = dgemm_check(M, N, K, split, DG_PART, bn, part, nullptr)) return e;
   int rc;
   switch (abl) {
@@ -398,6 +402,7 @@ CFC_API int cfc_dgemm_ablate(const void* x, const void* w, int M, int N, int K, 
     case 7: DG_ABL(7, true)
     case 8: DG_ABL(0, false)
     case 11: DG_ABL(3, false)
+    case 16: DG_ABL(16, true)
 #undef DG_ABL
     default: return -3;
   }

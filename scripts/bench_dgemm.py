@@ -65,6 +65,8 @@ def main():
     ap.add_argument("--shapes", nargs="*", default=["qkv", "o", "gate_up", "down"])
     ap.add_argument("--split-sweep", action="store_true")
     ap.add_argument("--ablate", action="store_true", help="time the ablation builds (1 no-X, 2 no-MFMA, 4 packed W, 8 nt)")
+    ap.add_argument("--abl", type=int, nargs="*", default=[0, 1, 2, 3, 4, 7, 8, 11, 16],
+                    help="ablation ids for --ablate (16 = X stages issued before the W ring fill)")
     ap.add_argument("--calls", type=int, default=64)
     ap.add_argument("--out", default="gpurun_out/dgemm.jsonl")
     args = ap.parse_args()
@@ -144,7 +146,7 @@ def main():
             if args.ablate and M <= 128:
                 part = torch.empty(s_def, M, N, device="cuda", dtype=torch.float32)
                 pcalls = pcalls_for(bn_d)
-                for abl in (1, 2, 3, 4, 7, 8, 11):
+                for abl in args.abl:
                     fns = [lambda ww=ww, a=abl: K.check(K.kernels().cfc_dgemm_ablate(
                         x.data_ptr(), ww.data.data_ptr(), M, N, Kd, s_def, bn_d, a, part.data_ptr(), K._stream(x)),
                         "ablate") for ww in pcalls]
