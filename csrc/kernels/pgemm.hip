@@ -451,7 +451,11 @@ __global__ void __launch_bounds__(512, 1)
     }
   };
 
-  // ---- prologue: tile 0 whole, tile 1's {X0, W0}; tile 0's X0 / W0 / W1 landed in every wave
+  // W1E (PF & 32): tile kt+2's W1 half is issued with its X0 / W0 in segment B of tile kt (its slot is
+  // free once both groups' segment-A reads of tile kt retired) instead of in segment A of tile kt+1,
+  // so every half has ~2 segments between its issue and the wait that retires it (was 1 for W1).
+  constexpr bool W1E = (PF & 32) != 0;
+  // ---- prologue: tile 0 whole, tile 1's {X0, W0} (+ W1); tile 0's X0 / W0 / W1 landed in every wave
   issue_x(0, 0);
   issue_w(0, 0);
   issue_w(0, 1);
@@ -459,7 +463,12 @@ __global__ void __launch_bounds__(512, 1)
   if (nk > 1) {
     issue_x(1, 0);
     issue_w(1, 0);
-    pp_wait_barrier<6>();
+    if constexpr (W1E) {
+      issue_w(1, 1);
+      pp_wait_barrier<8>();
+    } else {
+      pp_wait_barrier<6>();
+    }
   } else {
     pp_wait_barrier<2>();
   }
@@ -493,7 +502,7 @@ __global__ void __launch_bounds__(512, 1)
     const int buf = (kt & 1) * PP_BUF;
     // ======== segment A: load part (tile kt+1's W1 / X1 into the other buffer; fragments)
     if (DMA && kt + 1 < nk) {
-      issue_w(kt + 1, 1);
+      if constexpr (!W1E) issue_w(kt + 1, 1);
       issue_x(kt + 1, 1);
     }
     if constexpr (RD) {
@@ -531,6 +540,7 @@ __global__ void __launch_bounds__(512, 1)
     if (DMA && kt + 2 < nk) {
       issue_x(kt + 2, 0);
       issue_w(kt + 2, 0);
+      if constexpr (W1E) issue_w(kt + 2, 1);
     }
     if constexpr (RD) {
 #pragma unroll
@@ -541,7 +551,7 @@ __global__ void __launch_bounds__(512, 1)
       keep();
     }
     // retire tile kt+1's X0 / W0 / W1 (next segment A reads them)
-    if (DMA && kt + 2 < nk) pp_wait_barrier<6>();
+    if (DMA && kt + 2 < nk) pp_wait_barrier<W1E ? 8 : 6>();
     else if (DMA && kt + 1 < nk) pp_wait_barrier<2>();
     else pp_wait_barrier<0>();
     __builtin_amdgcn_sched_barrier(0);
@@ -920,6 +930,7 @@ CFC_API int cfc_pgemm_probe(const void* x, const void* w, void* out, int M, int 
     case 13: PP_PROBE(13)
     case 17: PP_PROBE(17)
     case 21: PP_PROBE(21)
+    case 33: PP_PROBE(33)
     default: return (int)hipErrorInvalidValue;
   }
 #undef PP_PROBE
