@@ -446,8 +446,11 @@ class DecoderModel:
                             and mode in ("splitk", "dgemm") and weights.tp_size == 1 and gemv_shapes
                             and not self.fp8)
         self.fused_decode = mode == "dgemm"
-        # decode RoPE + KV write inside the attention kernel's prologue (one launch per layer fewer)
-        self.rope_fused = os.environ.get("CFC_DECODE_ROPE_FUSED", "1") != "0"
+        # decode RoPE + KV write inside the attention kernel's prologue: opt-in.  Measured in the
+        # headline (profiles/r04_ab_*.log) the fused step decodes SLOWER (6.30 vs 6.09 s per batch):
+        # every attention workgroup waits ~5 us for its q slabs, the RoPE and the K/V store before its
+        # first KV load, twice per CU, which costs more than the 10.6-us rope_kv launch it removes.
+        self.rope_fused = os.environ.get("CFC_DECODE_ROPE_FUSED", "0") == "1"
         # B <= 4 decode on the ggml-quantized weights (GGUF checkpoints; csrc/kernels/quant.hip)
         self.decode_qgemv = (weights.qlayers is not None and os.environ.get("CFC_DECODE_QGEMV", "1") != "0"
                              and weights.tp_size == 1 and weights.gate_up_interleaved and not self.fp8)

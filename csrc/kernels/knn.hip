@@ -283,7 +283,8 @@ __global__ void __launch_bounds__(256) knn_topk_kernel(const uint16_t* __restric
 // ------------------------------------------------------------------ streamed scan + top-k (large k)
 // With a large k the per-chunk candidates of knn_topk_kernel are a big share of the rows (k = 150
 // from 512-row chunks: 29 % of the index written as candidates and read again by the merge).  Here
-// a workgroup scans a long span (KS_SPAN rows) in KS_SUB-row sub-chunks and keeps, per query, a
+// a workgroup (8 waves; two workgroups per CU = 4 waves per SIMD) scans a long span (KS_SPAN rows) in
+// KS_SUB-row sub-chunks and keeps, per query, a
 // candidate buffer in LDS behind a running threshold: only rows scoring above the k-th best key
 // the buffer held at its last cut are appended, and when the next sub-chunk could overflow the
 // buffer it is cut back to its exact top k (the threshold rises).  k candidates per query leave
@@ -340,7 +341,7 @@ __device__ __forceinline__ uint32_t ks_cut(uint32_t* bk, uint32_t* br, int cnt, 
 }
 
 template <int KC>
-__global__ void __launch_bounds__(256) knn_topk_stream_kernel(const uint16_t* __restrict__ X,
+__global__ void __launch_bounds__(512) knn_topk_stream_kernel(const uint16_t* __restrict__ X,
                                                               const uint16_t* __restrict__ Q, int N, int nq,
                                                               const float* __restrict__ xnorm2,
                                                               const float* __restrict__ qnorm2,
@@ -360,12 +361,12 @@ __global__ void __launch_bounds__(256) knn_topk_stream_kernel(const uint16_t* __
     qf[c] = as_bf16x8(qv ? *reinterpret_cast<const uint4*>(qrow + 32 * c + 8 * g) : make_uint4(0, 0, 0, 0));
   const float qn = (qnorm2 && qv) ? qnorm2[col] : 0.f;
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  int cnt[4] = {0, 0, 0, 0};          // this wave's queries w, w + 4, w + 8, w + 12 (wave-uniform)
-  uint32_t thr[4] = {0u, 0u, 0u, 0u};
+  int cnt[2] = {0, 0};                // this wave's queries w, w + 8 (wave-uniform)
+  uint32_t thr[2] = {0u, 0u};
   for (int s0 = lo; s0 < hi; s0 += KS_SUB) {
     const int s1 = min(hi, s0 + KS_SUB), len = s1 - s0;
     const int ngroups = (len + 15) / 16;
-    for (int grp = w; grp < ngroups; grp += 4) {
+    for (int grp = w; grp < ngroups; grp += 8) {
       const int r0 = s0 + grp * 16;
       const int r = min(r0 + col, s1 - 1);
       const uint16_t* xr = X + (size_t)r * D;
@@ -390,8 +391,8 @@ __global__ void __launch_bounds__(256) knn_topk_stream_kernel(const uint16_t* __
     }
     __syncthreads();
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int qi = w + 4 * t;
+    for (int t = 0; t < 2; ++t) {
+      const int qi = w + 8 * t;
       if (qi < nq) {
         uint32_t* qk = bk + qi * KS_CAP;
         uint32_t* qr = br + qi * KS_CAP;
@@ -417,8 +418,8 @@ __global__ void __launch_bounds__(256) knn_topk_stream_kernel(const uint16_t* __
     __syncthreads();                              // sc is the next sub-chunk's
   }
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int qi = w + 4 * t;
+  for (int t = 0; t < 2; ++t) {
+    const int qi = w + 8 * t;
     if (qi < nq) {
       uint32_t* qk = bk + qi * KS_CAP;
       uint32_t* qr = br + qi * KS_CAP;
@@ -547,9 +548,11 @@ namespace {
 // (the candidate arrays are written and merged: k = 150 from 256-row chunks is 59 % of the index).
 // Measured on 100M x 384: 1 query 2048 rows 12.6 ms (6.1 TB/s) vs 1024 rows 14.1 ms; 16 queries
 // 256 rows 14.1 ms vs 1024 rows 23.6 ms (k = 10), 512 rows 20.7 ms vs 256 rows 22.8 ms (k = 150).
-// k > 32: the streamed kernel, k candidates per KS_SPAN rows.
+// k > 32 and more than 4 queries: the streamed kernel, k candidates per KS_SPAN rows (up to 4
+// queries the 2048-row chunks already keep k = 150 at 7 % of the rows, and the streamed kernel's two
+// workgroups per CU scan slower: 1 query, k = 150: 14.8 ms vs 12.6, profiles/r04_bench_knn_*).
 constexpr int knn_flat_rows(int nq, int k) {
-  return k > 32 ? KS_SPAN : nq <= 4 ? 2048 : nq <= 8 ? 512 : 256;
+  return nq <= 4 ? 2048 : k > 32 ? KS_SPAN : nq <= 8 ? 512 : 256;
 }
 
 template <int KC>
@@ -601,7 +604,7 @@ CFC_API int cfc_knn_topk(const void* X, const void* Q, int N, int row_lo, int nq
   if (rows == KS_SPAN) {
 #define KS(KC) \
   case KC: \
-    knn_topk_stream_kernel<KC><<<nch, 256, 0, stream>>>((const uint16_t*)X, (const uint16_t*)Q, N, nq, xnorm2, qnorm2, \
+    knn_topk_stream_kernel<KC><<<nch, 512, 0, stream>>>((const uint16_t*)X, (const uint16_t*)Q, N, nq, xnorm2, qnorm2, \
                                                        alive, k, row_lo, out_v, out_i); \
     return CFC_CHECK_LAUNCH();
     switch (dim / 32) {

@@ -6,7 +6,7 @@ Datasets (--data):
   * uniform  -- uniformly random unit vectors: no cluster structure at all, IVF's worst case;
   * minilm   -- MiniLM-L6 encoder outputs (the HIP encoder, random-init weights: no checkpoint can be
                 downloaded here) of the synthetic mailing-list chunks, tiled to N rows with a small
-                per-copy perturbation so no two rows are identical.
+                per-copy perturbation (--noise) so no two rows are identical.
 Every row carries a real id string and its metadata through the build (RowTable: add_bulk, the
 k-means regroup permutation, the search results).  For nprobe in --nprobe: recall@10 against the
 exact flat scan of the same rows, ms per 16-query batch, and the bytes the probed lists really hold
@@ -23,6 +23,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from copilot_for_consensus_amd.vectorstore import HipFlatIndex, HipIVFIndex  # noqa: E402
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
 
 
 def minilm_vectors(n_unique: int, device) -> torch.Tensor:
@@ -53,10 +58,13 @@ def main():
     ap.add_argument("--nprobe", type=int, nargs="*", default=[8, 32, 128])
     ap.add_argument("--unique", type=int, default=200_000, help="minilm: distinct encoder outputs before tiling")
     ap.add_argument("--queries", type=int, default=256)
+    ap.add_argument("--noise", type=float, default=0.01,
+                    help="minilm: per-dimension gaussian perturbation of each tiled copy (0.01 ~ norm 0.2)")
     ap.add_argument("--out", default="gpurun_out/bench_ivf.jsonl")
+    ap.add_argument("--device", default="cuda", help="cpu: a functional dry run at small --n")
     args = ap.parse_args()
-    n, dim, dev = int(args.n), 384, torch.device("cuda")
-    g = torch.Generator(device="cuda").manual_seed(0)
+    n, dim, dev = int(args.n), 384, torch.device(args.device)
+    g = torch.Generator(device=dev).manual_seed(0)
     t0 = time.perf_counter()
     base = minilm_vectors(args.unique, dev) if args.data == "minilm" else None
     enc_s = time.perf_counter() - t0
@@ -65,9 +73,9 @@ def main():
         if base is None:
             return torch.nn.functional.normalize(torch.randn(e - s, dim, device=dev, generator=g), dim=1)
         src = base[torch.arange(s, e, device=dev) % base.shape[0]]
-        return torch.nn.functional.normalize(src + 0.03 * torch.randn(e - s, dim, device=dev, generator=g), dim=1)
+        return torch.nn.functional.normalize(src + args.noise * torch.randn(e - s, dim, device=dev, generator=g), dim=1)
 
-    idx = HipIVFIndex(dim, "cosine", nlist=args.nlist, nprobe=8, device="cuda", capacity=n)
+    idx = HipIVFIndex(dim, "cosine", nlist=args.nlist, nprobe=8, device=str(dev), capacity=n)
     t0 = time.perf_counter()
     chunk = 1 << 22
     for s in range(0, n, chunk):
@@ -75,23 +83,23 @@ def main():
         ids = [f"{i:016x}" for i in range(s, e)]
         metas = [{"thread_id": f"t{i // 32:012x}"} for i in range(s, e)] if n <= 20_000_000 else None
         idx.add_bulk(ids, rows(s, e).to(torch.bfloat16), metas)
-    torch.cuda.synchronize()
+    _sync(dev)
     fill_s = time.perf_counter() - t0
     t0 = time.perf_counter()
     idx.train(iters=8)
-    torch.cuda.synchronize()
+    _sync(dev)
     train_s = time.perf_counter() - t0
     host_bytes = sum(a.nbytes for a in idx._tab._cols.values()) + idx._tab._ids.n + idx._tab._meta.n
     # queries: fresh rows from the same distribution (minilm: perturbed encoder outputs)
     qsrc = rows(0, args.queries) if base is None else torch.nn.functional.normalize(
         base[torch.randint(0, base.shape[0], (args.queries,), device=dev, generator=g)]
-        + 0.03 * torch.randn(args.queries, dim, device=dev, generator=g), dim=1)
+        + args.noise * torch.randn(args.queries, dim, device=dev, generator=g), dim=1)
     Q = qsrc.to(torch.bfloat16)
     exact = []
     t0 = time.perf_counter()
     for s in range(0, args.queries, 16):
         exact.append(HipFlatIndex.search(idx, Q[s:s + 16], 10, rows=(0, n))[1].cpu())
-    torch.cuda.synchronize()
+    _sync(dev)
     flat_ms = (time.perf_counter() - t0) * 1e3 / (args.queries // 16)
     exact = torch.cat(exact)
     sizes = (idx._list_off_t[1:] - idx._list_off_t[:-1])
@@ -112,12 +120,12 @@ def main():
         Qb = Q[:16]
         for _ in range(2):
             idx.search(Qb, 10)
-        torch.cuda.synchronize()
+        _sync(dev)
         it = 10
         t0 = time.perf_counter()
         for _ in range(it):
             idx.search(Qb, 10)
-        torch.cuda.synchronize()
+        _sync(dev)
         dt = (time.perf_counter() - t0) / it
         per_batch_rows = scanned / (args.queries / 16)
         row = {"data": args.data, "n": n, "nlist": idx.nlist, "nprobe": npb, "recall_at_10": round(recall, 4),
