@@ -420,8 +420,21 @@ class HipFlatIndex(VectorStore):
             save_file({"vectors": self._X[:self._n].contiguous().cpu(), "norm2": self._norm2[:self._n].cpu()},
                       str(p / "vectors.safetensors"))
             self._tab.save(p)
-            (p / "index.json").write_text(json.dumps({"dim": self.dim, "metric": self.metric, "rows": self._n,
-                                                      "format": "rowtable-1"}))
+            hdr = {"dim": self.dim, "metric": self.metric, "rows": self._n, "format": "rowtable-1"}
+            hdr.update(self._extra_header())
+            (p / "index.json").write_text(json.dumps(hdr))
+            extra = self._extra_tensors()
+            if extra:
+                save_file(extra, str(p / "ivf.safetensors"))
+
+    def _extra_header(self) -> dict:
+        return {}
+
+    def _extra_tensors(self) -> dict:
+        return {}
+
+    def _restore_extra(self, meta: dict, path: Path) -> None:
+        pass
 
     @classmethod
     def load(cls, path, device="cuda") -> "HipFlatIndex":
@@ -440,6 +453,7 @@ class HipFlatIndex(VectorStore):
             idx._tab = RowTable(n + 1024)
             idx._tab.append_bulk(meta["ids"], meta["metadata"])
         idx._n = n
+        idx._restore_extra(meta, p)
         return idx
 
 
@@ -451,7 +465,14 @@ class HipIVFIndex(HipFlatIndex):
     the candidates on the device -- no per-list launches, no host syncs before the results.
     Rows added after training form an unsorted tail scanned by the fused flat kernel until the
     next regroup.  k-means runs on a bf16 row sample (fp32 only for the sample and centroids:
-    a 100M x 384 index never gets an fp32 copy); assignment of all rows is chunked bf16 GEMMs."""
+    a 100M x 384 index never gets an fp32 copy); assignment of all rows is chunked bf16 GEMMs.
+
+    Cosine / dot indexes are clustered CENTERED: the sample mean mu is removed before k-means
+    (FAISS's centering pre-transform), and rows / queries are assigned by argmax (x - mu).c =
+    x.c - mu.c -- mu only enters as a per-list bias, the stored rows stay untouched.  Encoder
+    embeddings share a dominant common direction (random-init MiniLM rows are ~0.98 cosine to each
+    other); uncentered, their scores against every centroid differ below bf16 resolution and one list
+    took 74 % of a 10M-row index (profiles/r04_bench_ivf_10M.jsonl)."""
 
     SAMPLE_PER_LIST = 256
     ASSIGN_CHUNK = 1 << 20
@@ -464,6 +485,7 @@ class HipIVFIndex(HipFlatIndex):
         self._list_off_t: torch.Tensor | None = None
         self._maxc = 1
         self._trained_n = 0
+        self.center: torch.Tensor | None = None     # fp32 [dim] (cosine / dot), see the class note
 
     def train(self, sample: torch.Tensor | None = None, iters: int = 10, seed: int = 0) -> None:
         """k-means on the GPU over a sample of <= SAMPLE_PER_LIST rows per list, then regroup."""
@@ -479,8 +501,13 @@ class HipIVFIndex(HipFlatIndex):
                 idx = torch.randperm(n, generator=g)[:m].to(self.device)
                 sample = self._X.index_select(0, idx)         # bf16 rows, no full-index copy
             X = sample.to(self.device).float()
+            if self.metric != "l2":
+                self.center = X.mean(0)
+                X = X - self.center
             Xb = X.to(torch.bfloat16).contiguous()
             C = X[torch.randperm(X.shape[0], generator=g)[:nlist].to(self.device)].clone()
+            if self.metric == "cosine":
+                C = torch.nn.functional.normalize(C, dim=1)
             for _ in range(iters):
                 a = self._nearest(Xb, C)
                 sums = torch.zeros_like(C).index_add_(0, a, X)
@@ -492,7 +519,11 @@ class HipIVFIndex(HipFlatIndex):
             self.nlist = C.shape[0]
             self._regroup()
 
-    def _nearest(self, X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
+    def _center_bias(self, C: torch.Tensor) -> torch.Tensor | None:
+        """-mu.c per list (None before a centered training)."""
+        return None if self.center is None else -(C.float() @ self.center)
+
+    def _nearest(self, X: torch.Tensor, C: torch.Tensor, extra_bias: torch.Tensor | None = None) -> torch.Tensor:
         """Nearest centroid of every row of bf16 X: argmax of x.c (cosine / dot) or of
         2 x.c - |c|^2 (L2), in ASSIGN_CHUNK-row pieces.  On the GPU the scores come from the
         hand-written MFMA GEMM (pgemm.hip) with the -|c|^2 term in its bias epilogue (the L2 form
@@ -500,6 +531,8 @@ class HipIVFIndex(HipFlatIndex):
         from ..ops import kernels as K
         Cf = C.float()
         bias = -Cf.pow(2).sum(1) if self.metric == "l2" else torch.zeros(C.shape[0], device=C.device)
+        if extra_bias is not None:
+            bias = bias + extra_bias
         Wf = 2 * Cf if self.metric == "l2" else Cf
         use_hip = X.is_cuda and X.shape[1] % 64 == 0 and X.shape[0] >= 256
         if use_hip:
@@ -519,7 +552,7 @@ class HipIVFIndex(HipFlatIndex):
         return torch.cat(out)
 
     def _assign(self, X: torch.Tensor) -> torch.Tensor:
-        return self._nearest(X, self.centroids)
+        return self._nearest(X, self.centroids, self._center_bias(self.centroids))
 
     def _regroup(self):
         n = self._n
@@ -538,6 +571,51 @@ class HipIVFIndex(HipFlatIndex):
         self._maxc = max(1, -(-int(counts.max()) // R)) if n else 1
         self._trained_n = n
 
+    def compact(self) -> None:
+        """Drop deleted rows; the survivors keep their order, so every list stays one contiguous
+        range: its new offsets are the live-row prefix counts at the old ones."""
+        with self._lock:
+            if self._dead == 0 or self.centroids is None:
+                return super().compact()
+            pre = np.concatenate([[0], np.cumsum(self._tab.live.astype(np.int64))])
+            old = np.asarray(self._list_off, dtype=np.int64)
+            tn = int(pre[self._trained_n])
+            super().compact()
+            off = pre[old]
+            self._list_off = off.tolist()
+            self._list_off_t = torch.from_numpy(off).to(self.device)
+            self._maxc = max(1, -(-int(np.diff(off).max()) // 1024)) if off.size > 1 else 1
+            self._trained_n = tn
+
+    def _extra_header(self) -> dict:
+        if self.centroids is None:
+            return {"ivf": None}
+        return {"ivf": {"nlist": self.nlist, "nprobe": self.nprobe, "trained_rows": self._trained_n,
+                        "list_off": self._list_off}}
+
+    def _extra_tensors(self) -> dict:
+        if self.centroids is None:
+            return {}
+        t = {"centroids": self.centroids.float().cpu()}
+        if self.center is not None:
+            t["center"] = self.center.float().cpu()
+        return t
+
+    def _restore_extra(self, meta: dict, path: Path) -> None:
+        ivf = meta.get("ivf")
+        if not ivf:
+            return
+        from safetensors.torch import load_file
+        t = load_file(str(path / "ivf.safetensors"))
+        self.centroids = t["centroids"].to(self.device).to(torch.bfloat16)
+        self.center = t["center"].to(self.device) if "center" in t else None
+        self.nlist, self.nprobe = int(ivf["nlist"]), int(ivf["nprobe"])
+        self._trained_n = int(ivf["trained_rows"])
+        self._list_off = [int(v) for v in ivf["list_off"]]
+        self._list_off_t = torch.tensor(self._list_off, dtype=torch.int64, device=self.device)
+        self._maxc = max(1, -(-max(b - a for a, b in zip(self._list_off, self._list_off[1:])) // 1024)) \
+            if len(self._list_off) > 1 else 1
+
     def add_embeddings(self, ids, vectors, metadatas=None):
         super().add_embeddings(ids, vectors, metadatas)
         # rows appended after training form an unsorted tail scanned exhaustively until re-train
@@ -549,6 +627,8 @@ class HipIVFIndex(HipFlatIndex):
         sc = Q.float() @ self.centroids.float().T
         if self.metric == "l2":
             sc = 2 * sc - self.centroids.float().pow(2).sum(1)[None, :]
+        elif self.center is not None:
+            sc = sc + self._center_bias(self.centroids)[None, :]
         return torch.topk(sc, min(self.nprobe, self.nlist), dim=1).indices.to(torch.int32).contiguous()
 
     def search(self, Q, k, rows=None):

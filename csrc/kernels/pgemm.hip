@@ -864,8 +864,10 @@ __global__ void __launch_bounds__(256, 1)
 }
 
 // production probe flags of the ping-pong kernel: no s_setprio (measured 1.5-2.5 % faster than the
-// per-segment flips on all four headline shapes, profiles/r04_pgemm_pp_probes.jsonl pf1 vs pf0)
-constexpr int PP_PF = 1;
+// per-segment flips on all four headline shapes, profiles/r04_pgemm_pp_probes.jsonl pf1 vs pf0) and
+// W1-early (+0.6-1.7 %: qkv 580 -> 571 us, o 384 -> 378, gate_up 2665 -> 2631, down 1311 -> 1299;
+// profiles/r04_pgemm_w1e.jsonl)
+constexpr int PP_PF = 1 | 32;
 
 template <int EPI>
 int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int M, int N, int K, int ldo,

@@ -268,3 +268,63 @@ def test_gpu_produced_tensors_accepted(store):
     t = torch.randn(4, DIM)
     store.add_embeddings(["a", "b", "c", "d"], t)
     assert store.query(t[2], top_k=1)[0].id == "c"
+
+
+def _blob(n, dim, clusters, rng, spread=0.15):
+    """Embedding-like data: one dominant common direction (rows ~0.95 cosine to each other) plus
+    cluster structure around it -- the shape random-init / real encoders produce."""
+    mu = rng.standard_normal(dim).astype(np.float32)
+    mu /= np.linalg.norm(mu)
+    cent = rng.standard_normal((clusters, dim)).astype(np.float32) * spread
+    lab = rng.integers(0, clusters, n)
+    X = 4 * mu + cent[lab] + 0.02 * rng.standard_normal((n, dim)).astype(np.float32)
+    return X / np.linalg.norm(X, axis=1, keepdims=True)
+
+
+def test_ivf_centered_kmeans_spreads_a_dominant_direction_over_the_lists():
+    rng = np.random.default_rng(7)
+    X = _blob(4000, DIM, 40, rng)
+    ivf = HipIVFIndex(DIM, "cosine", nlist=32, nprobe=4, device="cpu")
+    ivf.add_embeddings([f"r{i}" for i in range(4000)], X)
+    ivf.train(iters=6)
+    sizes = np.diff(np.asarray(ivf._list_off))
+    assert ivf.center is not None
+    assert sizes.max() < 0.25 * 4000, sizes          # no list swallows the blob
+    flat = HipFlatIndex(DIM, "cosine", device="cpu")
+    flat.add_embeddings([f"r{i}" for i in range(4000)], X)
+    Q = _blob(16, DIM, 40, np.random.default_rng(7))  # same direction / clusters as the rows
+    hit = sum(len({r.id for r in a} & {r.id for r in b})
+              for a, b in zip(ivf.query_batch(Q, top_k=10), flat.query_batch(Q, top_k=10)))
+    assert hit / 160 >= 0.8, hit
+
+
+def test_ivf_compaction_keeps_lists_contiguous_and_answers_exact():
+    rng = np.random.default_rng(8)
+    X = rng.standard_normal((1200, DIM)).astype(np.float32)
+    ids = [f"v{i}" for i in range(1200)]
+    ivf = HipIVFIndex(DIM, "cosine", nlist=12, nprobe=12, device="cpu")
+    ivf.add_embeddings(ids, X)
+    ivf.train(iters=4)
+    for i in range(0, 1200, 3):
+        ivf.delete(f"v{i}")
+    ivf.compact()
+    flat = HipFlatIndex(DIM, "cosine", device="cpu")
+    live = [i for i in range(1200) if i % 3]
+    flat.add_embeddings([ids[i] for i in live], X[live])
+    assert ivf._list_off[-1] == ivf._trained_n == len(live) == ivf.count()
+    for q in rng.standard_normal((5, DIM)).astype(np.float32):
+        assert [r.id for r in ivf.query(q, top_k=8)] == [r.id for r in flat.query(q, top_k=8)]
+
+
+def test_ivf_save_load_keeps_the_trained_lists(tmp_path):
+    rng = np.random.default_rng(9)
+    X = _blob(2000, DIM, 20, rng)
+    ivf = HipIVFIndex(DIM, "cosine", nlist=16, nprobe=3, device="cpu")
+    ivf.add_embeddings([f"r{i}" for i in range(2000)], X)
+    ivf.train(iters=4)
+    ivf.save(tmp_path)
+    back = HipIVFIndex.load(tmp_path, device="cpu")
+    assert back.centroids is not None and back._list_off == ivf._list_off and back.nprobe == 3
+    assert torch.allclose(back.center, ivf.center)
+    for q in X[:6]:
+        assert [r.id for r in back.query(q, top_k=5)] == [r.id for r in ivf.query(q, top_k=5)]
