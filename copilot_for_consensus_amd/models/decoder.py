@@ -578,8 +578,11 @@ class DecoderModel:
         return K.rmsnorm(x, w.final_norm, cfg.rms_eps, residual=residual)
 
     def forward_decode(self, ids, positions, slots, ctx_lens, block_tables, kv, attn_workspace=None,
-                       part_blocks=16) -> torch.Tensor:
-        """One token per sequence. Returns final-normed hidden [B, H]."""
+                       part_blocks=16, shared_blocks=None) -> torch.Tensor:
+        """One token per sequence. Returns final-normed hidden [B, H].  ``shared_blocks`` (device int32
+        [1]): leading KV blocks every sequence shares (prefix cache) -- the attention reads them through
+        the caches instead of nontemporal."""
+        self._shared_blocks = shared_blocks
         cfg, w = self.cfg, self.w
         x = K.embedding(w.embed, ids)
         B = ids.shape[0]
@@ -607,11 +610,13 @@ class DecoderModel:
         prologue does the RoPE / KV write, ``CFC_DECODE_ROPE_FUSED=1``); else rope_kv then attention.
         Both write the same cache bytes and return the same output."""
         cfg, w = self.cfg, self.w
+        sb = getattr(self, "_shared_blocks", None)
         if self.rope_fused and qkv.is_cuda:
             return K.paged_decode_rope_attention(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], block_tables,
                                                  ctx_lens, self.scale, w.heads, w.kv_heads, cfg.head_dim,
                                                  part_blocks=part_blocks, workspace=attn_workspace,
-                                                 window=self.window, k_scale=kv.k_scale, v_scale=kv.v_scale)
+                                                 window=self.window, k_scale=kv.k_scale, v_scale=kv.v_scale,
+                                                 shared_blocks=sb)
         if qkv.dim() == 3:
             q = K.rope_kv_write_part(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
                                      cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
@@ -620,7 +625,7 @@ class DecoderModel:
                                 cfg.head_dim, k_scale=kv.k_scale, v_scale=kv.v_scale)
         return K.paged_decode_attention(q, kv.k[i], kv.v[i], block_tables, ctx_lens, self.scale,
                                         part_blocks=part_blocks, workspace=attn_workspace, window=self.window,
-                                        k_scale=kv.k_scale, v_scale=kv.v_scale)
+                                        k_scale=kv.k_scale, v_scale=kv.v_scale, shared_blocks=sb)
 
     def _forward_decode_fused(self, x, positions, slots, ctx_lens, block_tables, kv, attn_workspace, part_blocks):
         """Decode layer on the hand-written decode GEMM (dgemm.hip), elementwise work in epilogues:

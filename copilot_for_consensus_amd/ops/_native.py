@@ -26,7 +26,7 @@ F = c_float
 _KERNEL_SIGS = {
     "cfc_rmsnorm": [P, P, P, P, I, I, F, I, P],
     "cfc_layernorm": [P, P, P, P, P, P, P, P, P, P, I, I, F, I, P],
-    "cfc_paged_decode_attention": [P, P, P, P, P, I, I, I, I, I, I, I, F, I, P, P, P, P],
+    "cfc_paged_decode_attention": [P, P, P, P, P, I, I, I, I, I, I, I, F, I, P, P, P, P, P],
     "cfc_prefill_attention": [P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, P, P],
     "cfc_prefill_rows": [I, I],
     "cfc_encoder_rows": [],
@@ -37,8 +37,9 @@ _KERNEL_SIGS = {
     "cfc_decode_advance_cb": [P, P, I, P, P, P, P, P, P, P, I, P, P, I, I] + [P] * 6 + [I] * 4 + [P] * 4,
     "cfc_rope_kv_write_fp8": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, P],
     "cfc_v_cache_write_runs_fp8": [P, P, I, P, I, I, I, F, P],
-    "cfc_paged_decode_attention_fp8": [P, P, P, P, P, I, I, I, I, I, I, I, F, I, F, F, P, P, P, P],
-    "cfc_paged_decode_rope_attention": [P, P, I, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, I, I, F, F, P, P, P, P],
+    "cfc_paged_decode_attention_fp8": [P, P, P, P, P, I, I, I, I, I, I, I, F, I, F, F, P, P, P, P, P],
+    "cfc_paged_decode_rope_attention": [P, P, I, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, I, I, F, F, P, P, P, P,
+                                        P],
     "cfc_prefill_attention_fp8": [P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, I, F, F, P, P],
     "cfc_silu_mul": [P, P, I, I, I, P],
     "cfc_quant_fp8_rows": [P, P, P, I, I, P],

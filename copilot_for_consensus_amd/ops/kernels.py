@@ -177,12 +177,14 @@ def decode_partitions(max_ctx: int, part_blocks: int) -> int:
 
 
 def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out=None, part_blocks=16,
-                           num_partitions=None, workspace=None, window=0, k_scale=1.0, v_scale=1.0):
+                           num_partitions=None, workspace=None, window=0, k_scale=1.0, v_scale=1.0, shared_blocks=None):
     """q [B, Hq, D]; caches [nblk, Hkv, 32, D] / [nblk, Hkv, D, 32]; returns [B, Hq, D].
 
     ``part_blocks`` > 0: split-KV partitions of that many blocks; ``part_blocks`` = -P: P balanced
     partitions of each sequence's own context (what the engine uses).  ``window`` > 0: sliding-window
-    attention over the last ``window`` keys (Mistral v0.1)."""
+    attention over the last ``window`` keys (Mistral v0.1).  ``shared_blocks`` (device int32 [1]):
+    every sequence's first that-many blocks are read through the caches (the batch's shared prefix
+    blocks), the rest nontemporal."""
     if not q.is_cuda:
         return ref.paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, window=window,
                                           k_scale=k_scale, v_scale=v_scale)
@@ -209,18 +211,20 @@ def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, o
                                                        block_tables.data_ptr(), ctx_lens.data_ptr(), B, Hq, Hkv, D,
                                                        max_blocks, part_blocks, Pn, float(scale), int(window or 0),
                                                        float(k_scale), float(v_scale), _p(part_o), _p(part_ml),
-                                                       out.data_ptr(), _stream(q)), "cfc_paged_decode_attention_fp8")
+                                                       out.data_ptr(), _p(shared_blocks), _stream(q)),
+              "cfc_paged_decode_attention_fp8")
         return out
     check(kernels().cfc_paged_decode_attention(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                                                block_tables.data_ptr(), ctx_lens.data_ptr(), B, Hq, Hkv, D,
                                                max_blocks, part_blocks, Pn, float(scale), int(window or 0), _p(part_o),
-                                               _p(part_ml), out.data_ptr(), _stream(q)), "cfc_paged_decode_attention")
+                                               _p(part_ml), out.data_ptr(), _p(shared_blocks), _stream(q)),
+          "cfc_paged_decode_attention")
     return out
 
 
 def paged_decode_rope_attention(qkv, positions, slots, cos_sin, k_cache, v_cache, block_tables, ctx_lens, scale,
                                 Hq, Hkv, D, part_blocks=-1, workspace=None, window=0, k_scale=1.0, v_scale=1.0,
-                                out=None):
+                                out=None, shared_blocks=None):
     """One decode step's RoPE + K/V cache write + paged attention in ONE kernel
     (attention.hip ``DecRope``): ``qkv`` is the qkv projection output, bf16 [B, (Hq + 2 Hkv) D] or the
     decode GEMM's fp32 split-K slabs [split, B, (Hq + 2 Hkv) D].  Same cache bytes and output as
@@ -231,7 +235,7 @@ def paged_decode_rope_attention(qkv, positions, slots, cos_sin, k_cache, v_cache
                           v_scale=v_scale)
         return paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, scale, out=out,
                                       part_blocks=part_blocks, workspace=workspace, window=window, k_scale=k_scale,
-                                      v_scale=v_scale)
+                                      v_scale=v_scale, shared_blocks=shared_blocks)
     if qkv.dim() == 3:
         split, B, N = qkv.shape
         if qkv.dtype != torch.float32:
@@ -269,7 +273,7 @@ def paged_decode_rope_attention(qkv, positions, slots, cos_sin, k_cache, v_cache
         qkv_p, part_p, split, positions.data_ptr(), slots.data_ptr(), cos_sin.data_ptr(), k_cache.data_ptr(),
         v_cache.data_ptr(), block_tables.data_ptr(), ctx_lens.data_ptr(), B, Hq, Hkv, D, max_blocks, part_blocks, Pn,
         float(scale), int(window or 0), int(_fp8(k_cache)), float(k_scale), float(v_scale), _p(part_o), _p(part_ml),
-        out.data_ptr(), _stream(qkv)), "cfc_paged_decode_rope_attention")
+        out.data_ptr(), _p(shared_blocks), _stream(qkv)), "cfc_paged_decode_rope_attention")
     return out
 
 

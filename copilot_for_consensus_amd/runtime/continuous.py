@@ -102,6 +102,9 @@ class ContinuousEngine:
         self.done = torch.ones(B, **i32)
         self.next_ids = torch.zeros(B, **i32)
         self.step_t = torch.zeros(1, **i32)     # sampler RNG salt
+        # leading KV blocks every occupied slot shares (prefix cache): read through the caches
+        self.shared = torch.zeros(1, **i32)
+        self._slot_shared = [0] * B
         self.stop_t = torch.tensor(self.stop_ids, **i32)
         # stop strings matched on the device (runtime/stops.py): a slot finishes at the token that
         # completes one, so the slot is freed and refilled instead of decoding to its limit
@@ -293,6 +296,9 @@ class ContinuousEngine:
             self.slot_req[s] = r
             r.slot = s
             self.slot_tables[s] = (tbl, fresh[i])
+            self._slot_shared[s] = start[i] // KV_BLOCK
+        occupied = [self._slot_shared[q] for q in range(self.B) if self.slot_req[q] is not None]
+        self.shared.fill_(min(occupied) if occupied and self.engine.shared_cached else 0)
         idx = torch.tensor(slots, dtype=torch.long, device=self.device)
         rows_t = torch.from_numpy(rows).to(self.device)
         self.block_tables.index_copy_(0, idx, torch.from_numpy(bt).to(self.device))
@@ -307,7 +313,8 @@ class ContinuousEngine:
 
     def _decode_step(self) -> None:
         hidden = self.model.forward_decode(self.ids, self.positions, self.slots, self.ctx_lens, self.block_tables,
-                                           self.kv, attn_workspace=self.workspace, part_blocks=self.part_blocks)
+                                           self.kv, attn_workspace=self.workspace, part_blocks=self.part_blocks,
+                                           shared_blocks=self.shared)
         self.engine._next_tokens(hidden, self.next_ids, self.sampling, self.seed, self.step_t)
         K.decode_advance_cb(self.next_ids, self.tokens, self.gen, self.limit, self.ids, self.positions,
                             self.ctx_lens, self.slots, self.block_tables, self.done, self.stop_t, self.stop_state)

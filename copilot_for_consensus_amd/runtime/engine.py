@@ -75,6 +75,7 @@ class _DecodeState:
         self.slots = torch.zeros(B, **i32)
         self.block_tables = torch.zeros(B, max_blocks, **i32)
         self.step = torch.zeros(1, **i32)
+        self.shared = torch.zeros(1, **i32)     # leading KV blocks all rows share (read cached)
         self.tokens = torch.zeros(B, max_new, **i32)
         self.done = torch.zeros(B, **i32)
         self.next_ids = torch.zeros(B, **i32)
@@ -117,6 +118,8 @@ class LLMEngine:
         if prefix_cache is None:
             prefix_cache = os.environ.get("CFC_PREFIX_CACHE", "1") != "0"
         self.prefix_cache = PrefixCache(kv.pool) if prefix_cache else None
+        # CFC_DECODE_SHARED_CACHED=0: every KV block nontemporal, shared prefix included
+        self.shared_cached = os.environ.get("CFC_DECODE_SHARED_CACHED", "1") != "0"
         if self.device.type == "cuda":
             from .gemm_tuning import enable_tuned_gemms
             self.tuned_gemms = enable_tuned_gemms()
@@ -221,7 +224,8 @@ class LLMEngine:
 
     def _decode_step(self, st: _DecodeState, part_blocks, temperature, seed):
         hidden = self.model.forward_decode(st.ids, st.positions, st.slots, st.ctx_lens, st.block_tables, self.kv,
-                                           attn_workspace=st.workspace, part_blocks=part_blocks)
+                                           attn_workspace=st.workspace, part_blocks=part_blocks,
+                                           shared_blocks=st.shared)
         self._next_tokens(hidden, st.next_ids, temperature, seed, st.step)
         K.decode_advance(st.next_ids, st.tokens, st.step, st.ids, st.positions, st.ctx_lens, st.slots,
                          st.block_tables, st.done, st.stop_ids, st.stop_state)
@@ -356,6 +360,9 @@ class LLMEngine:
             st.tokens.zero_()
             st.tokens[:, 0].copy_(f)
             st.step.fill_(1)
+            # the prefix blocks every sequence maps to the same physical blocks: the decode attention
+            # reads them through L2 / MALL (once for the batch) instead of nontemporal per sequence
+            st.shared.fill_(min(start) // KV_BLOCK if start and self.shared_cached else 0)
             done0 = torch.isin(f, st.stop_ids.cpu()).to(torch.int32) if stop_ids else torch.zeros(B, dtype=torch.int32)
             if stop_strings is not None:
                 # the prefill's token is the first of every sequence: fed on the host

@@ -101,12 +101,45 @@ struct DecRope {
   float inv_k, inv_v;
 };
 
+// One KV block's K fragments (bf16: 8 x 16 B per lane; fp8: 4 x 16 B) and V^T fragments (8) of
+// kv-head block `base` (elements), loaded nontemporal (NT) or through the caches.
+template <bool NT, bool F8>
+__device__ __forceinline__ void dec_load_blk(const void* kc, const void* vc, size_t base, int col, int g, uint4* kk,
+                                             typename KvFrag<F8>::raw* vv) {
+  constexpr int D = 128;
+  if constexpr (F8) {
+    const uint8_t* kb = reinterpret_cast<const uint8_t*>(kc) + base;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp)
+        kk[st * 2 + pp] = kv_load<NT>(reinterpret_cast<const uint16_t*>(kb + (16 * st + col) * D + 64 * pp + 16 * g));
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+      vv[dt] = kv_load8<NT>(reinterpret_cast<const uint8_t*>(vc) + base + (16 * dt + col) * KV_BS + 8 * g);
+  } else {
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        kk[st * 4 + c] = kv_load<NT>(reinterpret_cast<const uint16_t*>(kc) + base + (16 * st + col) * D + 32 * c + 8 * g);
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+      vv[dt] = kv_load<NT>(reinterpret_cast<const uint16_t*>(vc) + base + (16 * dt + col) * KV_BS + 8 * g);
+  }
+}
+
+// NT: the KV stream is read nontemporal (each block once per step, kept out of the caches' LRU) --
+// except the first *shared_blocks blocks of every sequence (shared_blocks: device int, may be null):
+// the prefix-cache blocks that every sequence of the batch maps to the SAME physical blocks (system
+// prompt + template head, ~10 blocks of a 2.9k-token context).  Those go through L2 / MALL, so the
+// 128 sequences' reads of them cost one HBM read instead of 128.
 template <int G, bool NT, bool F8 = false, bool ROPE = false>
 __global__ void __launch_bounds__(256, F8 ? 2 : 1) paged_decode_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ kc, const void* __restrict__ vc,
     const int32_t* __restrict__ block_tables, const int32_t* __restrict__ ctx_lens, float scale_log2, int Hkv,
     int max_blocks, int part_blocks, int P, int window, float v_scale, float* __restrict__ part_o,
-    float* __restrict__ part_ml, uint16_t* __restrict__ out, DecRope rp) {
+    float* __restrict__ part_ml, uint16_t* __restrict__ out, DecRope rp, const int32_t* __restrict__ shared_blocks) {
   // F8: kc / vc hold e4m3 of K / k_scale and V / v_scale; k_scale is folded into scale_log2 by the
   // host, v_scale multiplies the output here
   typedef typename KvFrag<F8>::raw Raw;
@@ -191,29 +224,11 @@ __global__ void __launch_bounds__(256, F8 ? 2 : 1) paged_decode_kernel(
   constexpr int NK = F8 ? 4 : 8;
   uint4 kr[NK];
   Raw vr[8];
-  auto ld = [&](const void* base, size_t e) -> Raw {
-    if constexpr (F8) return kv_load8<NT>(reinterpret_cast<const uint8_t*>(base) + e);
-    else return kv_load<NT>(reinterpret_cast<const uint16_t*>(base) + e);
-  };
+  const int temporal = (NT && shared_blocks != nullptr) ? shared_blocks[0] : 0;   // blocks read cached
   auto load_blk = [&](int bi, uint4* kk, Raw* vv) {
     const size_t base = ((size_t)bt[bi] * Hkv + h) * head_stride;
-    if constexpr (F8) {
-      const uint8_t* kb = reinterpret_cast<const uint8_t*>(kc) + base;
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int pp = 0; pp < 2; ++pp)
-          kk[st * 2 + pp] = kv_load<NT>(reinterpret_cast<const uint16_t*>(kb + (16 * st + col) * D + 64 * pp + 16 * g));
-    } else {
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          kk[st * 4 + c] = kv_load<NT>(reinterpret_cast<const uint16_t*>(kc) + base + (16 * st + col) * D + 32 * c + 8 * g);
-    }
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt)
-      vv[dt] = ld(vc, base + (16 * dt + col) * KV_BS + 8 * g);
+    if (NT && bi >= temporal) dec_load_blk<NT, F8>(kc, vc, base, col, g, kk, vv);
+    else dec_load_blk<false, F8>(kc, vc, base, col, g, kk, vv);
   };
   // K operand of (st, k-step c)
   auto kop = [&](const uint4* kk, int st, int c) -> bf16x8_t {
@@ -1190,7 +1205,8 @@ template <bool F8>
 static int launch_paged_decode(const void* q, const void* k_cache, const void* v_cache, const int32_t* block_tables,
                                const int32_t* ctx_lens, int B, int Hq, int Hkv, int head_dim, int max_blocks,
                                int part_blocks, int P, float scale, int window, float v_scale, float* part_o,
-                               float* part_ml, void* out, hipStream_t stream, const DecRope* rope = nullptr) {
+                               float* part_ml, void* out, hipStream_t stream, const DecRope* rope = nullptr,
+                               const int32_t* shared_blocks = nullptr) {
   if (head_dim != 128 || Hq % Hkv != 0 || B <= 0 || P <= 0 || window < 0) return -1;
   if (rope != nullptr && ((rope->qkv == nullptr) == (rope->part == nullptr) || (rope->part && rope->split < 1) ||
                           !rope->positions || !rope->slots || !rope->cos_sin))
@@ -1200,7 +1216,7 @@ static int launch_paged_decode(const void* q, const void* k_cache, const void* v
   dim3 grid(P, Hkv, B);
   const float sl2 = scale * LOG2E;
 #define DEC_ARGS (const uint16_t*)q, k_cache, v_cache, block_tables, ctx_lens, sl2, Hkv, max_blocks, part_blocks, P, \
-    window, v_scale, part_o, part_ml, (uint16_t*)out, rp
+    window, v_scale, part_o, part_ml, (uint16_t*)out, rp, shared_blocks
   // nontemporal KV loads for large batches (B=128: 6.5 vs 5.9 TB/s; B=8: 3.8 vs 4.2 -- there the
   // plain loads win), profiles/decode_attn_partitions_r01.log; CFC_DECODE_NT=0/1 forces either
   static const int nt_env = [] { const char* e = getenv("CFC_DECODE_NT"); return e ? atoi(e) : -1; }();
@@ -1227,12 +1243,16 @@ static int launch_paged_decode(const void* q, const void* k_cache, const void* v
 
 // q: [B, Hq, 128] bf16; caches per layer as documented above; out: [B, Hq, 128] bf16.
 // part_o / part_ml: fp32 workspaces of B*Hq*P*128 and B*Hq*P*2 floats (unused when P == 1).
+// shared_blocks (device int32, may be null): leading blocks of every sequence read through the
+// caches (the batch's shared prefix blocks), the rest nontemporal.
 CFC_API int cfc_paged_decode_attention(const void* q, const void* k_cache, const void* v_cache,
                                        const int32_t* block_tables, const int32_t* ctx_lens, int B, int Hq, int Hkv,
                                        int head_dim, int max_blocks, int part_blocks, int P, float scale, int window,
-                                       float* part_o, float* part_ml, void* out, hipStream_t stream) {
+                                       float* part_o, float* part_ml, void* out, const int32_t* shared_blocks,
+                                       hipStream_t stream) {
   return launch_paged_decode<false>(q, k_cache, v_cache, block_tables, ctx_lens, B, Hq, Hkv, head_dim, max_blocks,
-                                    part_blocks, P, scale, window, 1.f, part_o, part_ml, out, stream);
+                                    part_blocks, P, scale, window, 1.f, part_o, part_ml, out, stream, nullptr,
+                                    shared_blocks);
 }
 
 // Decode attention with the step's RoPE + KV write in its prologue (DecRope).  qkv [B, (Hq+2Hkv)*128]
@@ -1243,14 +1263,16 @@ CFC_API int cfc_paged_decode_rope_attention(const void* qkv, const float* part, 
                                             const int32_t* block_tables, const int32_t* ctx_lens, int B, int Hq,
                                             int Hkv, int head_dim, int max_blocks, int part_blocks, int P, float scale,
                                             int window, int fp8, float k_scale, float v_scale, float* part_o,
-                                            float* part_ml, void* out, hipStream_t stream) {
+                                            float* part_ml, void* out, const int32_t* shared_blocks,
+                                            hipStream_t stream) {
   const DecRope rp{(const uint16_t*)qkv, part, split, positions, slots, cos_sin, 1.f / k_scale, 1.f / v_scale};
   if (fp8)
     return launch_paged_decode<true>(nullptr, k_cache, v_cache, block_tables, ctx_lens, B, Hq, Hkv, head_dim,
                                      max_blocks, part_blocks, P, scale * k_scale, window, v_scale, part_o, part_ml,
-                                     out, stream, &rp);
+                                     out, stream, &rp, shared_blocks);
   return launch_paged_decode<false>(nullptr, k_cache, v_cache, block_tables, ctx_lens, B, Hq, Hkv, head_dim,
-                                    max_blocks, part_blocks, P, scale, window, 1.f, part_o, part_ml, out, stream, &rp);
+                                    max_blocks, part_blocks, P, scale, window, 1.f, part_o, part_ml, out, stream, &rp,
+                                    shared_blocks);
 }
 
 // FP8 (e4m3fn) caches holding K / k_scale and V / v_scale
@@ -1258,9 +1280,10 @@ CFC_API int cfc_paged_decode_attention_fp8(const void* q, const void* k_cache, c
                                            const int32_t* block_tables, const int32_t* ctx_lens, int B, int Hq,
                                            int Hkv, int head_dim, int max_blocks, int part_blocks, int P, float scale,
                                            int window, float k_scale, float v_scale, float* part_o, float* part_ml,
-                                           void* out, hipStream_t stream) {
+                                           void* out, const int32_t* shared_blocks, hipStream_t stream) {
   return launch_paged_decode<true>(q, k_cache, v_cache, block_tables, ctx_lens, B, Hq, Hkv, head_dim, max_blocks,
-                                   part_blocks, P, scale * k_scale, window, v_scale, part_o, part_ml, out, stream);
+                                   part_blocks, P, scale * k_scale, window, v_scale, part_o, part_ml, out, stream,
+                                   nullptr, shared_blocks);
 }
 
 CFC_API int cfc_prefill_tile_rows() { return PF_ROWS; }

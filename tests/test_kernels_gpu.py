@@ -136,6 +136,27 @@ def test_paged_decode(G, part_blocks):
     _close(out, ref, 2e-2)
 
 
+@pytest.mark.parametrize("shared", [0, 2, 5, 1000])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_paged_decode_shared_prefix_blocks_read_cached_same_result(shared, fp8):
+    """The leading `shared` blocks of every sequence are loaded through the caches (the batch's
+    shared prefix), the rest nontemporal: a cache-policy change only -- bit-identical output."""
+    Hkv, D, G = 8, 128, 4
+    ctx = [300, 31, 2049, 64, 700] * 8          # 40 rows: the nontemporal path (B >= 32)
+    kc, vc, bt = _fill_cache(ctx, Hkv, D)
+    bt[:, :2] = bt[0, :2]                        # two physical prefix blocks shared by every row
+    kw = {}
+    if fp8:
+        kc, vc = (kc.float() / 0.5).clamp(-448, 448).to(F8), (vc.float() / 0.25).clamp(-448, 448).to(F8)
+        kw = dict(k_scale=0.5, v_scale=0.25)
+    q = torch.randn(len(ctx), Hkv * G, D).bfloat16().to(DEV)
+    args = (q, kc.to(DEV), vc.to(DEV), bt.to(DEV), torch.tensor(ctx, dtype=torch.int32, device=DEV), 1 / math.sqrt(D))
+    a = K.paged_decode_attention(*args, part_blocks=-1, **kw)
+    b = K.paged_decode_attention(*args, part_blocks=-1, shared_blocks=torch.tensor([shared], dtype=torch.int32,
+                                                                                   device=DEV), **kw)
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("G", [1, 4])
 @pytest.mark.parametrize("part_blocks", [4, -1, -3])
 @pytest.mark.parametrize("window", [1, 33, 100])
