@@ -276,9 +276,11 @@ class HipLLMSummarizer(Summarizer):
         ce = self._ce
         try:
             while True:
+                t_idle = time.perf_counter()
                 with self._cv:
                     while not self._ce_stop and not self._inbox and not ce.pending():
                         self._cv.wait(0.5)
+                    ce.stats["idle_s"] = ce.stats.get("idle_s", 0.0) + time.perf_counter() - t_idle
                     if self._ce_stop:
                         break
                     new = list(self._inbox)
@@ -300,12 +302,17 @@ class HipLLMSummarizer(Summarizer):
                     self._ce = ce = self._reset_continuous(ce, leader=True)
                     continue
                 if not finished and all(x is None for x in ce.slot_req):
+                    t_idle = time.perf_counter()
                     with self._cv:      # admission is waiting for more requests: do not spin on the GIL
                         self._cv.wait(0.005)
+                    ce.stats["idle_s"] = ce.stats.get("idle_s", 0.0) + time.perf_counter() - t_idle
+                t_del = time.perf_counter()
                 for r in finished:
                     item = self._live.pop(r.rid, None)
                     if item is not None:
                         self._finish(*item, r.tokens or [])
+                if finished:    # detokenize + the service's callback (SummaryComplete publish) per thread
+                    ce.stats["deliver_s"] = ce.stats.get("deliver_s", 0.0) + time.perf_counter() - t_del
         finally:
             # stopped (or the thread died): every thread still queued or running gets its failure, so
             # the service publishes SummarizationFailed and releases its in-flight key -- none is
