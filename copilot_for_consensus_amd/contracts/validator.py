@@ -80,6 +80,14 @@ class SchemaRegistry:
 
 
 _PATTERN_CACHE: dict[str, re.Pattern] = {}
+_ANNOTATIONS = {"type", "description", "title", "$comment", "examples"}
+
+
+def _simple_type(s: Any) -> str | None:
+    """The type name of an items schema that only constrains the JSON type (else None)."""
+    if isinstance(s, dict) and isinstance(s.get("type"), str) and s["type"] in _TYPES and s.keys() <= _ANNOTATIONS:
+        return s["type"]
+    return None
 
 
 def _validate(v: Any, s: Any, path: str, errs: list[str], reg: SchemaRegistry | None, root: dict) -> None:
@@ -129,8 +137,18 @@ def _validate(v: Any, s: Any, path: str, errs: list[str], reg: SchemaRegistry | 
         if s.get("uniqueItems") and len({repr(x) for x in v}) != len(v):
             errs.append(f"{path}: items not unique")
         if "items" in s:
-            for i, x in enumerate(v):
-                _validate(x, s["items"], f"{path}[{i}]", errs, reg, root)
+            it = s["items"]
+            simple = _simple_type(it)
+            if simple is not None:
+                # fast path for id lists ({"type": "string"} items): one type check per item, no
+                # recursion or path formatting unless an item fails
+                ok = _TYPES[simple]
+                for i, x in enumerate(v):
+                    if not ok(x):
+                        errs.append(f"{path}[{i}]: expected {simple}, got {type(x).__name__}")
+            else:
+                for i, x in enumerate(v):
+                    _validate(x, it, f"{path}[{i}]", errs, reg, root)
     if isinstance(v, dict):
         props = s.get("properties", {})
         for k in s.get("required", []):

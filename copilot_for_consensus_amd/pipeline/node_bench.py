@@ -129,6 +129,9 @@ class NodeBench:
         deadline = time.time() + timeout_s
         pending = list(steps)
         last_note = time.time()
+        tids_of: dict = {}
+        # the poll runs on the main thread beside the services' threads and the engine thread: it
+        # counts (no document copies) and sleeps 0.1 s, so it never competes for the GIL noticeably
         while pending:
             if time.time() - last_note > 15:      # a visible heartbeat of the pipeline's progress
                 last_note = time.time()
@@ -139,11 +142,18 @@ class NodeBench:
                 raise TimeoutError(f"node bench: steps {pending} unfinished after {timeout_s}s")
             s = pending[0]
             aids, t0 = subs[s]
-            tids = self._thread_ids(aids)
-            reports = self.store.query_documents("summaries", {"thread_id": {"$in": tids}}, limit=1 << 20) \
-                if tids else []
-            if len(tids) < self.threads_per_step or len({r["thread_id"] for r in reports}) < len(tids):
-                time.sleep(0.05)
+            tids = tids_of.get(s)
+            if tids is None:
+                if self.store.count_documents("threads", {"archive_id": {"$in": aids}}) < self.threads_per_step:
+                    time.sleep(0.1)
+                    continue
+                tids = tids_of[s] = self._thread_ids(aids)
+            if self.store.count_documents("summaries", {"thread_id": {"$in": tids}}) < len(tids):
+                time.sleep(0.1)
+                continue
+            reports = self.store.query_documents("summaries", {"thread_id": {"$in": tids}}, limit=1 << 20)
+            if len({r["thread_id"] for r in reports}) < len(tids):
+                time.sleep(0.1)
                 continue
             lat = [max(0.0, datetime.fromisoformat(r["generated_at"].replace("Z", "+00:00")).timestamp() - t0)
                    for r in reports]

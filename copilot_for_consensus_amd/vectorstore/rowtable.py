@@ -61,6 +61,7 @@ class RowTable:
         self._sorted_h = np.zeros(0, np.uint64)
         self._sorted_r = np.zeros(0, np.int64)
         self._recent: dict[int, list[int]] = {}
+        self._nrecent = 0
 
     # ------------------------------------------------------------ columns
     def _grow(self, cap: int) -> None:
@@ -105,10 +106,10 @@ class RowTable:
 
     def _index(self, r: int, h: int) -> None:
         self._recent.setdefault(h, []).append(r)
+        self._nrecent += 1
 
     def _maybe_merge(self) -> None:
-        nrec = sum(len(v) for v in self._recent.values())
-        if nrec > max(self.MERGE_MIN, self._sorted_h.size // 8):
+        if self._nrecent > max(self.MERGE_MIN, self._sorted_h.size // 8):
             self.rebuild()
 
     def rebuild(self) -> None:
@@ -118,6 +119,7 @@ class RowTable:
         o = np.argsort(h, kind="stable")
         self._sorted_h, self._sorted_r = h[o], live[o].astype(np.int64)
         self._recent = {}
+        self._nrecent = 0
 
     # ------------------------------------------------------------ writes
     def upsert(self, keys, metas=None) -> np.ndarray:
