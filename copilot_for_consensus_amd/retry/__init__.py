@@ -57,12 +57,17 @@ class RetryContext:
         return (datetime.now(timezone.utc) - self.start_time).total_seconds()
 
 
+# one jitter RNG for every policy: a policy is built per handled event, and random.Random() seeds
+# itself from os.urandom each time (thousands of events per batch in the node)
+_JITTER_RNG = random.Random()
+
+
 class RetryPolicy:
     def __init__(self, config: RetryConfig | None = None, sleeper: Callable[[float], None] = time.sleep,
                  rng: random.Random | None = None):
         self.config = config or RetryConfig()
         self._sleep = sleeper
-        self._rng = rng or random.Random()
+        self._rng = rng or _JITTER_RNG
 
     def calculate_delay_ms(self, attempt_number: int) -> int:
         if attempt_number <= 1:

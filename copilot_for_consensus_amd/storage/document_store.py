@@ -15,7 +15,7 @@ from abc import ABC, abstractmethod
 from collections import defaultdict
 from typing import Any
 
-from .query import apply_update, get_path, matches, simple_equality_keys
+from .query import apply_update, get_path, matches, prepare_filter, simple_equality_keys
 
 SYSTEM_FIELDS = ("_rid", "_self", "_etag", "_attachments", "_ts")
 
@@ -258,6 +258,7 @@ class InMemoryDocumentStore(DocumentStore):
             return sanitize_document(_jcopy(d)) if d is not None else None
 
     def _select(self, collection, filter_dict):
+        filter_dict = prepare_filter(filter_dict)
         coll = self.collections[collection]
         cand = self._candidates(collection, filter_dict)
         if cand is not None:

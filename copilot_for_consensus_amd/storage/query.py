@@ -48,6 +48,41 @@ def _cmp(a, b, op) -> bool:
     raise ValueError(op)
 
 
+_SCALARS = (str, int, float, bool, type(None))
+
+
+class _InSet(frozenset):
+    """A ``$in`` list of hashable scalars, pre-hashed once per query (prepare_filter): membership
+    instead of a linear scan per document (an $in over 1,700 chunk ids against 1,700 candidates was
+    millions of comparisons under the store lock)."""
+
+
+def _in_set(v, arg: _InSet) -> bool:
+    if v is _MISSING:
+        return None in arg
+    if isinstance(v, list):
+        return any(type(x) in _SCALARS and x in arg for x in v)
+    return type(v) in _SCALARS and v in arg
+
+
+def prepare_filter(flt):
+    """Same filter with every ``$in`` / ``$nin`` list of hashable scalars as a pre-hashed set; the
+    result matches exactly the same documents (Mongo equality of scalars == Python hash equality)."""
+    if isinstance(flt, dict):
+        out = {}
+        for k, v in flt.items():
+            if k in ("$in", "$nin") and isinstance(v, (list, tuple)) and all(type(a) in _SCALARS for a in v):
+                out[k] = _InSet(v)
+            elif k in ("$and", "$or", "$nor") and isinstance(v, list):
+                out[k] = [prepare_filter(c) for c in v]
+            elif isinstance(v, dict):
+                out[k] = prepare_filter(v)
+            else:
+                out[k] = v
+        return out
+    return flt
+
+
 def _eq(v, target) -> bool:
     if v is _MISSING:
         return target is None
@@ -65,9 +100,9 @@ def _match_ops(v, cond: dict) -> bool:
         elif op in ("$gt", "$gte", "$lt", "$lte"):
             ok = any(_cmp(x, arg, op) for x in v) if isinstance(v, list) else _cmp(v, arg, op)
         elif op == "$in":
-            ok = any(_eq(v, a) for a in arg)
+            ok = _in_set(v, arg) if isinstance(arg, _InSet) else any(_eq(v, a) for a in arg)
         elif op == "$nin":
-            ok = not any(_eq(v, a) for a in arg)
+            ok = not (_in_set(v, arg) if isinstance(arg, _InSet) else any(_eq(v, a) for a in arg))
         elif op == "$exists":
             ok = (v is not _MISSING) == bool(arg)
         elif op == "$regex":
