@@ -12,10 +12,25 @@ Routing key = dotted lower-case event type ("JSONParsed" -> "json.parsed"), exch
 """
 from __future__ import annotations
 
+import random
 import re
+import threading
 import uuid
 from datetime import datetime, timezone
 from typing import Any
+
+_TLS = threading.local()
+
+
+def _event_uuid() -> str:
+    """A version-4 (random) UUID for an event id from a per-thread PRNG seeded once from the OS:
+    ``uuid.uuid4()`` reads os.urandom on every call, a syscall per event on the bus's hot path.
+    Event ids need uniqueness, not secrecy (nothing authenticates with them)."""
+    rng = getattr(_TLS, "rng", None)
+    if rng is None:
+        rng = _TLS.rng = random.Random(int.from_bytes(uuid.uuid4().bytes, "big") ^ threading.get_ident())
+    return str(uuid.UUID(int=rng.getrandbits(128), version=4))
+
 
 SCHEMA_BASE = "https://alan-jowett.github.io/CoPilot-For-Consensus/schemas/events/"
 EXCHANGE = "copilot.events"
@@ -208,7 +223,7 @@ class Event:
             raise ValueError(f"unknown event type {event_type!r}")
         self.event_type = event_type
         self.data = dict(data or {})
-        self.event_id = event_id or str(uuid.uuid4())
+        self.event_id = event_id or _event_uuid()
         self.timestamp = timestamp or utc_now_iso()
         self.version = version
 
