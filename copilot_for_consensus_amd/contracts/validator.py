@@ -90,90 +90,142 @@ def _simple_type(s: Any) -> str | None:
     return None
 
 
-def _validate(v: Any, s: Any, path: str, errs: list[str], reg: SchemaRegistry | None, root: dict) -> None:
+# ---------------------------------------------------------------------------------------------
+# Schemas are compiled once into closures (one per schema node): validating an event then costs a
+# few attribute-free checks per field instead of re-reading every keyword of the schema dict on
+# every value (~30 dict lookups per node; thousands of events per batch go through this).  The
+# error messages and the keyword semantics are those of the original interpreter.
+_COMPILED: dict[tuple[int, int, int], tuple] = {}
+
+
+def _compiled(s: Any, reg: SchemaRegistry | None, root: Any) -> Callable:
+    key = (id(s), id(reg), id(root))
+    hit = _COMPILED.get(key)
+    if hit is None or hit[1] is not s or hit[3] is not root:
+        # the schema / root objects are kept alive with the entry, so their ids cannot be reused
+        hit = _COMPILED[key] = (_build(s, reg, root), s, reg, root)
+    return hit[0]
+
+
+def _noop(v, path, errs):
+    return None
+
+
+def _build(s: Any, reg: SchemaRegistry | None, root: Any) -> Callable:
     if s is True or s is None:
-        return
+        return _noop
     if s is False:
-        errs.append(f"{path}: not allowed")
-        return
+        return lambda v, path, errs: errs.append(f"{path}: not allowed")
+    ref_fn = None
     if "$ref" in s:
-        if reg is None and not s["$ref"].startswith("#"):
-            raise KeyError(f"$ref {s['$ref']!r} needs a registry")
-        target = (reg or SchemaRegistry()).resolve(s["$ref"], root)
-        _validate(v, target, path, errs, reg, target if not s["$ref"].startswith("#") else root)
+        ref = s["$ref"]
+        if reg is None and not ref.startswith("#"):
+            raise KeyError(f"$ref {ref!r} needs a registry")
+        target = (reg or SchemaRegistry()).resolve(ref, root)
+        troot = target if not ref.startswith("#") else root
+
+        def ref_fn(v, path, errs, target=target, troot=troot):     # lazy: schemas may recurse
+            _compiled(target, reg, troot)(v, path, errs)
     t = s.get("type")
-    if t is not None:
-        types = t if isinstance(t, list) else [t]
-        if not any(_TYPES[x](v) for x in types):
+    types = tuple(_TYPES[x] for x in (t if isinstance(t, list) else [t])) if t is not None else None
+    has_const, const = "const" in s, s.get("const")
+    enum = s.get("enum")
+    min_len, max_len = s.get("minLength"), s.get("maxLength")
+    pat = re.compile(s["pattern"]) if "pattern" in s else None
+    fmt = s.get("format")
+    str_checks = min_len is not None or max_len is not None or pat is not None or fmt is not None
+    minimum, maximum = s.get("minimum"), s.get("maximum")
+    num_checks = minimum is not None or maximum is not None
+    min_items, max_items, unique = s.get("minItems"), s.get("maxItems"), bool(s.get("uniqueItems"))
+    items = s.get("items")
+    has_items = "items" in s
+    simple = _simple_type(items) if has_items else None
+    items_fn = _compiled(items, reg, root) if has_items and simple is None and items is not True else None
+    list_checks = min_items is not None or max_items is not None or unique or has_items
+    props = {k: _compiled(sub, reg, root) for k, sub in s.get("properties", {}).items()}
+    required = tuple(s.get("required", ()))
+    has_ap = "additionalProperties" in s
+    ap = s.get("additionalProperties")
+    ap_fn = _compiled(ap, reg, root) if isinstance(ap, dict) else None
+    dict_checks = bool(props) or bool(required) or has_ap
+    all_of = tuple(_compiled(x, reg, root) for x in s.get("allOf", ()))
+    any_of = tuple(_compiled(x, reg, root) for x in s["anyOf"]) if "anyOf" in s else None
+    one_of = tuple(_compiled(x, reg, root) for x in s["oneOf"]) if "oneOf" in s else None
+    not_fn = _compiled(s["not"], reg, root) if "not" in s else None
+    is_num = _TYPES["number"]
+
+    def fails(fn, v, path):
+        e: list[str] = []
+        fn(v, path, e)
+        return bool(e)
+
+    def f(v, path, errs):
+        if ref_fn is not None:
+            ref_fn(v, path, errs)
+        if types is not None and not any(tf(v) for tf in types):
             errs.append(f"{path}: expected {t}, got {type(v).__name__}")
             return
-    if "const" in s and v != s["const"]:
-        errs.append(f"{path}: must equal {s['const']!r}")
-    if "enum" in s and v not in s["enum"]:
-        errs.append(f"{path}: {v!r} not in {s['enum']}")
-    if isinstance(v, str):
-        if "minLength" in s and len(v) < s["minLength"]:
-            errs.append(f"{path}: shorter than {s['minLength']}")
-        if "maxLength" in s and len(v) > s["maxLength"]:
-            errs.append(f"{path}: longer than {s['maxLength']}")
-        if "pattern" in s:
-            pat = _PATTERN_CACHE.get(s["pattern"])
-            if pat is None:
-                pat = _PATTERN_CACHE[s["pattern"]] = re.compile(s["pattern"])
-            if not pat.search(v):
-                errs.append(f"{path}: {v!r} does not match {s['pattern']}")
-        if "format" in s and not _check_format(s["format"], v):
-            errs.append(f"{path}: not a valid {s['format']}")
-    if _TYPES["number"](v):
-        if "minimum" in s and v < s["minimum"]:
-            errs.append(f"{path}: {v} < minimum {s['minimum']}")
-        if "maximum" in s and v > s["maximum"]:
-            errs.append(f"{path}: {v} > maximum {s['maximum']}")
-    if isinstance(v, list):
-        if "minItems" in s and len(v) < s["minItems"]:
-            errs.append(f"{path}: fewer than {s['minItems']} items")
-        if "maxItems" in s and len(v) > s["maxItems"]:
-            errs.append(f"{path}: more than {s['maxItems']} items")
-        if s.get("uniqueItems") and len({repr(x) for x in v}) != len(v):
-            errs.append(f"{path}: items not unique")
-        if "items" in s:
-            it = s["items"]
-            simple = _simple_type(it)
+        if has_const and v != const:
+            errs.append(f"{path}: must equal {const!r}")
+        if enum is not None and v not in enum:
+            errs.append(f"{path}: {v!r} not in {enum}")
+        if str_checks and isinstance(v, str):
+            if min_len is not None and len(v) < min_len:
+                errs.append(f"{path}: shorter than {min_len}")
+            if max_len is not None and len(v) > max_len:
+                errs.append(f"{path}: longer than {max_len}")
+            if pat is not None and not pat.search(v):
+                errs.append(f"{path}: {v!r} does not match {pat.pattern}")
+            if fmt is not None and not _check_format(fmt, v):
+                errs.append(f"{path}: not a valid {fmt}")
+        if num_checks and is_num(v):
+            if minimum is not None and v < minimum:
+                errs.append(f"{path}: {v} < minimum {minimum}")
+            if maximum is not None and v > maximum:
+                errs.append(f"{path}: {v} > maximum {maximum}")
+        if list_checks and isinstance(v, list):
+            if min_items is not None and len(v) < min_items:
+                errs.append(f"{path}: fewer than {min_items} items")
+            if max_items is not None and len(v) > max_items:
+                errs.append(f"{path}: more than {max_items} items")
+            if unique and len({repr(x) for x in v}) != len(v):
+                errs.append(f"{path}: items not unique")
             if simple is not None:
-                # fast path for id lists ({"type": "string"} items): one type check per item, no
-                # recursion or path formatting unless an item fails
                 ok = _TYPES[simple]
                 for i, x in enumerate(v):
                     if not ok(x):
                         errs.append(f"{path}[{i}]: expected {simple}, got {type(x).__name__}")
-            else:
+            elif items_fn is not None:
                 for i, x in enumerate(v):
-                    _validate(x, it, f"{path}[{i}]", errs, reg, root)
-    if isinstance(v, dict):
-        props = s.get("properties", {})
-        for k in s.get("required", []):
-            if k not in v:
-                errs.append(f"{path}: missing required '{k}'")
-        for k, x in v.items():
-            if k in props:
-                _validate(x, props[k], f"{path}.{k}", errs, reg, root)
-            elif "additionalProperties" in s:
-                ap = s["additionalProperties"]
-                if ap is False:
-                    errs.append(f"{path}: unexpected property '{k}'")
-                elif isinstance(ap, dict):
-                    _validate(x, ap, f"{path}.{k}", errs, reg, root)
-    for sub in s.get("allOf", []):
-        _validate(v, sub, path, errs, reg, root)
-    if "anyOf" in s:
-        if not any(not _collect(v, sub, path, reg, root) for sub in s["anyOf"]):
+                    items_fn(x, f"{path}[{i}]", errs)
+        if dict_checks and isinstance(v, dict):
+            for k in required:
+                if k not in v:
+                    errs.append(f"{path}: missing required '{k}'")
+            for k, x in v.items():
+                pf = props.get(k)
+                if pf is not None:
+                    pf(x, f"{path}.{k}", errs)
+                elif has_ap:
+                    if ap is False:
+                        errs.append(f"{path}: unexpected property '{k}'")
+                    elif ap_fn is not None:
+                        ap_fn(x, f"{path}.{k}", errs)
+        for sub in all_of:
+            sub(v, path, errs)
+        if any_of is not None and not any(not fails(sub, v, path) for sub in any_of):
             errs.append(f"{path}: matches none of anyOf")
-    if "oneOf" in s:
-        n = sum(1 for sub in s["oneOf"] if not _collect(v, sub, path, reg, root))
-        if n != 1:
-            errs.append(f"{path}: matches {n} of oneOf (need exactly 1)")
-    if "not" in s and not _collect(v, s["not"], path, reg, root):
-        errs.append(f"{path}: matches 'not' schema")
+        if one_of is not None:
+            n = sum(1 for sub in one_of if not fails(sub, v, path))
+            if n != 1:
+                errs.append(f"{path}: matches {n} of oneOf (need exactly 1)")
+        if not_fn is not None and not fails(not_fn, v, path):
+            errs.append(f"{path}: matches 'not' schema")
+    return f
+
+
+def _validate(v: Any, s: Any, path: str, errs: list[str], reg: SchemaRegistry | None, root: dict) -> None:
+    _compiled(s, reg, root)(v, path, errs)
 
 
 def _collect(v, s, path, reg, root) -> list[str]:
