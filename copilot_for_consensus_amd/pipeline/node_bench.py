@@ -89,6 +89,7 @@ class NodeBench:
         self.generator = SyntheticArchive(seed=seed)
         self.threads_per_step = threads_per_step
         self.sources: dict[int, Path] = {}
+        self.submitted: dict[int, float] = {}
 
     def prepare_sources(self, steps) -> None:
         """The steps' archives as local mailing-list sources (outside the timed region)."""
@@ -100,6 +101,7 @@ class NodeBench:
 
     def _submit(self, step: int) -> tuple[list[str], float]:
         t0 = time.time()
+        self.submitted[step] = t0
         ids = self.ingestion.ingest_archive({"name": f"bench-{step}", "source_type": "local",
                                             "url": str(self.sources[step]), "enabled": True})
         return ids, t0
@@ -175,6 +177,13 @@ class NodeBench:
 
     def close(self) -> None:
         print(f"[bench-node] continuous engine: {self.engine_stats()}", file=sys.stderr, flush=True)
+        llm = getattr(self.node.services.get("summarization"), "summarizer", None)
+        ce = getattr(llm, "_ce", None)
+        if ce is not None:
+            subs = {s: round(t0, 3) for s, t0 in self.submitted.items()}
+            print(f"[bench-node] step submit times: {subs}", file=sys.stderr, flush=True)
+            print(f"[bench-node] admissions (t, n, first arrival, last arrival): {ce.admit_log}", file=sys.stderr,
+                  flush=True)
         self.node.stop()
         import shutil
         shutil.rmtree(self.tmp, ignore_errors=True)

@@ -124,6 +124,7 @@ class ContinuousEngine:
         self._cancel_slots: list[int] = []     # running requests to stop at the next step
         self._rid = 0
         self.stats = {"steps": 0, "admitted": 0, "finished": 0, "prefill_s": 0.0, "decode_s": 0.0}
+        self.admit_log: list[tuple] = []     # (admit time, requests, first arrival, last arrival), epoch s
 
     # ------------------------------------------------------------------ API
     def submit(self, prompt: list[int], max_new: int) -> Request:
@@ -309,6 +310,10 @@ class ContinuousEngine:
             self.stop_state.set_slots(slots, sstates)
         self.tokens.index_copy_(0, idx, torch.nn.functional.pad(rows_t[:, :1], (0, self.cap - 1)))
         self.stats["admitted"] += len(take)
+        # admission timeline (wall clock): when, how many, first / last arrival of the admitted requests
+        sub = [r.submitted_s for r in take]
+        off = time.time() - time.perf_counter()
+        self.admit_log.append((round(t + off, 3), len(take), round(min(sub) + off, 3), round(max(sub) + off, 3)))
         self.stats["admissions"] = self.stats.get("admissions", 0) + 1
 
     def _decode_step(self) -> None:
