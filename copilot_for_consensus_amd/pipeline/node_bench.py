@@ -121,9 +121,21 @@ class NodeBench:
             max_inflight = int(os.environ.get("CFC_NODE_MAX_INFLIGHT", "2"))
         todo = list(steps)
         subs = {}
+        ce = self._engine()
+        base = ce.stats["admitted"] if ce is not None else 0
+
+        def upstream_done() -> bool:
+            # with the continuous engine: every thread submitted so far has been admitted, i.e. at
+            # most one step is upstream (ingest..orchestrate) at a time.  Submitting two at once made
+            # their threads interleave into both engine batches, so the pair finished together and
+            # the next pair's upstream ran with the GPU idle (profiles/r04_bench_node_*timeline*)
+            if ce is None or ce.stats["admitted"] - base >= self.threads_per_step * len(subs):
+                return True
+            # a step whose threads cannot all reach the engine must not stall the source for good
+            return bool(subs) and time.time() - max(t0 for _, t0 in subs.values()) > 30.0
 
         def refill():
-            while todo and (max_inflight <= 0 or len(subs) - len(out) < max_inflight):
+            while todo and (max_inflight <= 0 or (len(subs) - len(out) < max_inflight and upstream_done())):
                 s = todo.pop(0)
                 subs[s] = self._submit(s)
         out: list[NodeStepResult] = []
@@ -135,6 +147,7 @@ class NodeBench:
         # the poll runs on the main thread beside the services' threads and the engine thread: it
         # counts (no document copies) and sleeps 0.1 s, so it never competes for the GIL noticeably
         while pending:
+            refill()                              # the next step once the last one was admitted
             if time.time() - last_note > 15:      # a visible heartbeat of the pipeline's progress
                 last_note = time.time()
                 c = {k: self.store.count_documents(k, {}) for k in ("messages", "threads", "chunks", "summaries")}
@@ -168,6 +181,10 @@ class NodeBench:
             pending.pop(0)
             refill()
         return out
+
+    def _engine(self):
+        llm = getattr(self.node.services.get("summarization"), "summarizer", None)
+        return getattr(llm, "_ce", None)
 
     def engine_stats(self) -> dict:
         """The summarizer's continuous-engine counters (admissions, decode steps, prefill / decode s)."""
