@@ -134,8 +134,22 @@ class NodeBench:
             # a step whose threads cannot all reach the engine must not stall the source for good
             return bool(subs) and time.time() - max(t0 for _, t0 in subs.values()) > 30.0
 
+        def just_in_time() -> bool:
+            # the next step enters the source so its upstream (ingest .. orchestrate, measured on the
+            # previous step) completes as the running batch drains -- the bench pipeline's policy:
+            # its threads do not wait in the engine queue for a whole batch (p50), and the engine
+            # is never idle for lack of them (throughput)
+            log = ce.admit_log if ce is not None else []
+            if len(log) < 2 or not self.submitted:
+                return True
+            batch_s = log[-1][0] - log[-2][0]
+            last_sub = max(self.submitted.values())
+            upstream_s = max(0.5, log[-1][3] - last_sub) if log[-1][3] >= last_sub else 1.0
+            return time.time() >= log[-1][0] + batch_s - (2.0 * upstream_s + 0.5)
+
         def refill():
-            while todo and (max_inflight <= 0 or (len(subs) - len(out) < max_inflight and upstream_done())):
+            while todo and (max_inflight <= 0 or (len(subs) - len(out) < max_inflight and upstream_done()
+                                                  and just_in_time())):
                 s = todo.pop(0)
                 subs[s] = self._submit(s)
         out: list[NodeStepResult] = []
