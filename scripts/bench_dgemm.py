@@ -150,7 +150,9 @@ def main():
                     fns = [lambda ww=ww, a=abl: K.check(K.kernels().cfc_dgemm_ablate(
                         x.data_ptr(), ww.data.data_ptr(), M, N, Kd, s_def, bn_d, a, part.data_ptr(), K._stream(x)),
                         "ablate") for ww in pcalls]
-                    row[f"pk_abl{abl}_us"] = round(timed(fns), 1)
+                    key = f"pk_abl{abl}_us"
+                    n = sum(1 for k in row if k.startswith(key))
+                    row[key if n == 0 else f"{key}_{n}"] = round(timed(fns), 1)   # repeated ids: A/B/A/B
             if name.startswith("gate_up"):
                 row["lib_silu_us"] = round(timed([lambda ww=ww: K.silu_mul(F.linear(x, ww), interleaved=True)
                                                   for ww in calls]), 1)
