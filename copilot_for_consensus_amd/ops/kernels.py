@@ -581,7 +581,7 @@ def pgemm_ok(x: torch.Tensor, w) -> bool:
             and w.shape[0] % 64 == 0 and x.shape[0] >= 1 and x.numel() * 2 < 2 ** 32 and w.numel() * 2 < 2 ** 32)
 
 
-PGEMM_VARIANTS = {"ring5": 0, "stage2": 1, "ring4": 2, "pp": 3, "w4": 4}
+PGEMM_VARIANTS = {"ring5": 0, "stage2": 1, "ring4": 2, "pp": 3, "w4": 4, "pps": 5}
 # row-major W default K loop (a PackedWeight always runs the ping-pong kernel "pp")
 PGEMM_VARIANT = os.environ.get("CFC_PGEMM_VARIANT", "stage2")
 

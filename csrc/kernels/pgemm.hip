@@ -107,6 +107,65 @@ __device__ __forceinline__ void pg_epilogue(const f32x4_t (&acc)[8][NJ], const u
   }
 }
 
+// LDS-staged epilogue of one wave's 128 x 64 accumulator tile (bf16 and SwiGLU outputs only): the
+// values go to the wave's private 16-KB LDS region (8-byte writes, 16-byte units XOR-swizzled by the
+// row), come back as 16-byte row pieces and leave as full 128-byte (bf16: 64 output columns) or
+// 64-byte (SwiGLU: 32 output columns) row segments -- instead of 8-byte pieces with 32 / 16 bytes
+// contiguous per row (and half the lanes idle for SwiGLU).  Same values, same rounding as
+// pg_epilogue.  The caller guarantees no other wave reads or DMAs into that region any more.
+template <int EPI>
+__device__ __forceinline__ void pg_epilogue_staged(const f32x4_t (&acc)[8][4], uint16_t* __restrict__ out, int M,
+                                                   int N, int ldo, int mw, int nw, char* region) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, rl = lane & 15;
+  constexpr int OC = EPI == PG_SWIGLU ? 32 : 64;     // output columns of this wave
+  constexpr int UPR = OC / 8;                         // 16-byte units per row
+  constexpr int RB = OC * 2;                          // bytes per staged row
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = 16 * i + rl;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if constexpr (EPI == PG_SWIGLU) {
+        float u[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) u[e] = __shfl_xor(v[e], 32, 64);
+        if (g < 2) {
+          float y[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float gg = pg_bfr(v[e]);
+            y[e] = gg / (1.f + __expf(-gg)) * pg_bfr(u[e]);
+          }
+          // output columns 8 j + 4 g .. +3: unit j, half g
+          const int unit = j ^ (r & (UPR - 1));
+          *reinterpret_cast<uint2*>(region + r * RB + unit * 16 + g * 8) =
+              make_uint2(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]));
+        }
+      } else {
+        // columns 16 j + 4 g .. +3: unit 2 j + (g >> 1), half g & 1
+        const int unit = (2 * j + (g >> 1)) ^ (r & (UPR - 1));
+        *reinterpret_cast<uint2*>(region + r * RB + unit * 16 + (g & 1) * 8) =
+            make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  constexpr int RPI = 64 / UPR;                       // rows per store instruction
+  const int ncol0 = EPI == PG_SWIGLU ? nw / 2 : nw;   // first output column of this wave
+#pragma unroll
+  for (int s = 0; s < 128 / RPI; ++s) {
+    const int r = RPI * s + lane / UPR, unit = lane % UPR;
+    const uint4 val = *reinterpret_cast<const uint4*>(region + r * RB + ((unit ^ (r & (UPR - 1))) * 16));
+    const int m = mw + r, n = ncol0 + unit * 8;
+    if (m < M && n < (EPI == PG_SWIGLU ? N / 2 : N))
+      *reinterpret_cast<uint4*>(out + (size_t)m * ldo + n) = val;
+  }
+}
+
 template <int EPI>
 __global__ void __launch_bounds__(512, 1)
     pgemm_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W, const uint16_t* __restrict__ bias,
@@ -576,8 +635,15 @@ __global__ void __launch_bounds__(512, 1)
     for (int j = 0; j < 4; ++j) acc[0][j] += __builtin_bit_cast(f32x4_t, wf[j][0]) + __builtin_bit_cast(f32x4_t, xf[j][1]);
   }
 
-  // wave rows: segment A's m-tiles i = tile rows 128 grp + 16 i, segment B's = 128 grp + 64 + 16 i
-  pg_epilogue<EPI>(acc, bias, out, M, N, ldo, m0 + grp * 128, n0 + wc * 64);
+  // wave rows: segment A's m-tiles i = tile rows 128 grp + 16 i, segment B's = 128 grp + 64 + 16 i.
+  // STG (PF & 64): the bf16 / SwiGLU outputs leave through LDS as whole row segments.  After this
+  // wave's last barrier of the loop no wave reads LDS any more (the lagging group's last reads were
+  // retired before it) and every DMA landed, so each wave may use its own 16-KB slice.
+  constexpr bool STG = (PF & 64) != 0 && (EPI == PG_BF16 || EPI == PG_SWIGLU);
+  if constexpr (STG)
+    pg_epilogue_staged<EPI>(acc, out, M, N, ldo, m0 + grp * 128, n0 + wc * 64, smem + w * 16384);
+  else
+    pg_epilogue<EPI>(acc, bias, out, M, N, ldo, m0 + grp * 128, n0 + wc * 64);
   if (grp == 0) pp_barrier();   // matches group 1's stagger barrier
 }
 
@@ -877,6 +943,8 @@ int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int 
   uint16_t* op = (uint16_t*)out;
   if (wnw > 0) {   // fragment-packed W: the ping-pong (default) or the 4-wave kernel
     if (variant == 4) pgemm_w4_kernel<EPI, true><<<tm * tn, 256, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, wnw);
+    else if (variant == 5)   // LDS-staged bf16 / SwiGLU epilogue
+      pgemm_pp_kernel<EPI, true, PP_PF | 64><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, wnw);
     else pgemm_pp_kernel<EPI, true, PP_PF><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, wnw);
     return (int)hipGetLastError();
   }
@@ -886,6 +954,7 @@ int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int 
     case 2: pgemm_ring_kernel<EPI, 4><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn); break;
     case 3: pgemm_pp_kernel<EPI, false, PP_PF><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, 1); break;
     case 4: pgemm_w4_kernel<EPI, false><<<tm * tn, 256, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, 1); break;
+    case 5: pgemm_pp_kernel<EPI, false, PP_PF | 64><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, 1); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
@@ -895,7 +964,7 @@ int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int 
 
 // epi & 15: 0 bf16, 1 + bias, 2 + bias -> GELU, 3 SwiGLU (out [M, N/2]); epi >> 4: K-loop variant
 // for a row-major W (0 BK = 32 ring of 5 slots, 1 the 2-stage BK = 64 kernel, 2 ring of 4 slots,
-// 3 the ping-pong kernel); ldo = output row stride.  wnw > 0: W is in the decode GEMM's
+// 3 the ping-pong kernel, 5 the same with the LDS-staged bf16 / SwiGLU epilogue); ldo = output row stride.  wnw > 0: W is in the decode GEMM's
 // fragment-packed layout for bn = 16 wnw (cfc_dgemm_pack; N % (16 wnw) == 0) and runs on the
 // ping-pong kernel whatever the variant.
 CFC_API int cfc_pgemm(const void* x, const void* w, const void* bias, void* out, int M, int N, int K, int epi_v,
@@ -933,6 +1002,7 @@ CFC_API int cfc_pgemm_probe(const void* x, const void* w, void* out, int M, int 
     case 17: PP_PROBE(17)
     case 21: PP_PROBE(21)
     case 33: PP_PROBE(33)
+    case 97: PP_PROBE(97)
     default: return (int)hipErrorInvalidValue;
   }
 #undef PP_PROBE

@@ -24,7 +24,7 @@ from copilot_for_consensus_amd.runtime.gemm_tuning import enable_tuned_gemms  # 
 
 SHAPES = {"qkv": (16384, 6144, 4096), "o": (16384, 4096, 4096), "gate_up": (16384, 28672, 4096),
           "down": (16384, 4096, 14336)}
-PROBES = {"pf0_g8": (0, 8), "pf1_g8": (1, 8), "w1e_g8": (33, 8), "pf2_g8": (2, 8), "pf0_g4": (0, 4), "pf0_g16": (0, 16),
+PROBES = {"pf0_g8": (0, 8), "pf1_g8": (1, 8), "w1e_g8": (33, 8), "stg_g8": (97, 8), "pf2_g8": (2, 8), "pf0_g4": (0, 4), "pf0_g16": (0, 16),
           # ablations (wrong results by construction; timing only): no DMA / no ds_read / no MFMA
           "abl_nodma": (5, 8), "abl_noread": (9, 8), "abl_mfma_only": (13, 8), "abl_nomfma": (17, 8),
           "abl_read_only": (21, 8)}

@@ -455,7 +455,7 @@ def test_dgemm_packed_swiglu_and_norm(M, split):
 @pytest.mark.parametrize("M,N,Kd,epi", [(512, 512, 256, "bf16"), (300, 1152, 384, "bias"), (257, 1536, 384, "bias_gelu"),
                                        (1000, 768, 1536, "bf16"), (129, 2048, 512, "swiglu"), (64, 320, 128, "bf16"),
                                        (2048, 4096, 1024, "bf16"), (513, 640, 4096, "swiglu")])
-@pytest.mark.parametrize("variant", ["ring5", "ring4", "stage2", "pp", "w4"])
+@pytest.mark.parametrize("variant", ["ring5", "ring4", "stage2", "pp", "w4", "pps"])
 def test_pgemm(M, N, Kd, epi, variant):
     """Prefill / encoder GEMM with its fused epilogue vs the fp32 reference of the same op: edge
     tiles in M and N (rows/cols past the edge never stored), bias, bias+GELU, SwiGLU."""
@@ -475,7 +475,7 @@ def test_pgemm(M, N, Kd, epi, variant):
     _close(y, ref, 3e-2)
 
 
-@pytest.mark.parametrize("variant", ["ring5", "ring4", "stage2", "pp", "w4"])
+@pytest.mark.parametrize("variant", ["ring5", "ring4", "stage2", "pp", "w4", "pps"])
 def test_pgemm_exact_and_strided_out(variant):
     """Small-integer operands: bit-exact; output written into a wider buffer (ldo > N) leaves the
     other columns untouched."""
@@ -492,7 +492,7 @@ def test_pgemm_exact_and_strided_out(variant):
 @pytest.mark.parametrize("M,N,Kd,epi,bn", [(512, 768, 256, "bf16", 64), (300, 1152, 384, "bias", 96),
                                           (257, 1536, 448, "bias_gelu", 128), (129, 2240, 512, "swiglu", 112),
                                           (1000, 6144, 1024, "bf16", 96), (513, 1792, 2048, "swiglu", 64)])
-@pytest.mark.parametrize("variant", ["pp", "w4"])
+@pytest.mark.parametrize("variant", ["pp", "w4", "pps"])
 def test_pgemm_packed_weight(M, N, Kd, epi, bn, variant):
     """The ping-pong prefill GEMM reading the decode GEMM's fragment-packed weight (one weight copy
     for prefill and decode) vs the fp32 reference, for every packing width bn; bit-identical to the
@@ -513,7 +513,7 @@ def test_pgemm_packed_weight(M, N, Kd, epi, bn, variant):
     assert torch.equal(y, K.pgemm(x, w, epi, bias=b, variant=variant))
 
 
-@pytest.mark.parametrize("variant", ["pp", "w4"])
+@pytest.mark.parametrize("variant", ["pp", "w4", "pps"])
 def test_pgemm_packed_exact(variant):
     """Small-integer operands through the packed weight: bit-exact."""
     M, N, Kd = 700, 576, 320
@@ -522,6 +522,24 @@ def test_pgemm_packed_exact(variant):
     w[:, :5] += torch.arange(N, device=DEV).bfloat16().unsqueeze(1) % 7
     y = K.pgemm(x, K.pack_dgemm_weight(w, bn=96), variant=variant)
     assert torch.equal(y.float(), x.float() @ w.float().T)
+
+
+@pytest.mark.parametrize("epi", ["bf16", "swiglu"])
+@pytest.mark.parametrize("M", [300, 512, 1000])
+def test_pgemm_staged_epilogue_bit_identical(epi, M):
+    """The LDS-staged epilogue (variant pps) writes exactly the bytes of the register epilogue (pp),
+    partial row tiles and a strided output included; nothing outside the output columns."""
+    N, Kd = 1536 if epi == "swiglu" else 768, 512
+    x = (torch.rand(M, Kd, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(N, Kd, device=DEV) * 2 - 1) / Kd ** 0.5).bfloat16()
+    pw = K.pack_dgemm_weight(w, swiglu=epi == "swiglu")
+    oc = N // 2 if epi == "swiglu" else N
+    a = torch.full((M, oc + 64), 7.0, device=DEV).bfloat16()
+    b = a.clone()
+    K.pgemm(x, pw, epi, out=a[:, :oc], variant="pp")
+    K.pgemm(x, pw, epi, out=b[:, :oc], variant="pps")
+    assert torch.equal(a, b)
+    assert bool((b[:, oc:] == 7.0).all())
 
 
 @pytest.mark.parametrize("M", [1, 2, 3, 4])
