@@ -215,6 +215,13 @@ _filters = st.one_of(
     st.builds(lambda v, n: {"archive_id": v, "n": {"$gte": n}}, _vals, st.integers(-5, 5)),
     st.builds(lambda v: {"tags": v}, st.sampled_from(["p", "q"])),
     st.builds(lambda a, b: {"$or": [{"thread_id": a}, {"archive_id": b}]}, _vals, _vals),
+    # pre-hashed $in / $nin sets (query.prepare_filter) against the linear matcher: array fields,
+    # missing fields (None in the set), $nin, nested under $or / $and
+    st.builds(lambda vs: {"tags": {"$in": vs}}, st.lists(st.sampled_from(["p", "q", "r"]), max_size=3)),
+    st.builds(lambda vs: {"archive_id": {"$nin": vs}}, st.lists(_vals, max_size=3)),
+    st.builds(lambda vs: {"absent": {"$in": vs}}, st.lists(_vals, max_size=2)),
+    st.builds(lambda a, vs: {"$and": [{"thread_id": {"$in": vs}}, {"n": {"$gte": a}}]}, st.integers(-5, 5),
+              st.lists(_vals, max_size=3)),
 )
 
 
