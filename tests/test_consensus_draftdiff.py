@@ -134,3 +134,22 @@ def test_register_custom_draft_diff_provider():
         register_draft_diff_provider("bad", dict)
     with pytest.raises(ValueError):
         register_draft_diff_provider(" ", Echo)
+
+
+def test_literal_prefilter_counts_exactly_what_the_regexes_match():
+    """The ASCII literal prefilter in front of the pattern regexes never changes a count (mixed case,
+    word boundaries, +1 / -1, non-ASCII text falling back to the regexes)."""
+    import random
+    import re
+
+    from copilot_for_consensus_amd.consensus import AGREEMENT_PATTERNS, DISSENT_PATTERNS
+    words = ["+1", "-1", "LGTM", "lgtm!", "I Agree", "agreed", "disagree", "Oppose", "concerned", "wait",
+             "waiting", "hold on", "not sure", "sounds GOOD", "makes sense", "approve", "Concur", "x+1y",
+             "issue with", "problem with", "support this", "İ agree", "naïve", "", "\n", "---1"]
+    rng = random.Random(5)
+    naive = [re.compile(p, re.IGNORECASE) for p in AGREEMENT_PATTERNS + DISSENT_PATTERNS]
+    fast = HeuristicConsensusDetector._AGREE + HeuristicConsensusDetector._DISSENT
+    for _ in range(400):
+        text = " ".join(rng.choice(words) for _ in range(rng.randint(0, 12)))
+        want = sum(1 for rx in naive if rx.search(text))
+        assert HeuristicConsensusDetector._count(fast, text) == want, text
