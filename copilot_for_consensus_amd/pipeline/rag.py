@@ -6,7 +6,7 @@ There is ONE implementation of every stage: the service classes the deployed nod
 batch entry points directly, in order, once per batch of threads, instead of letting each
 service's consumer loop receive the previous stage's event from the bus:
 
-  IngestionService._record -> ParsingService.process_archive -> ChunkingService.process_messages ->
+  IngestionService.record_archive -> ParsingService.process_archive -> ChunkingService.process_messages ->
   EmbeddingService.process_chunks -> OrchestratorService.orchestrate_threads ->
   SummarizationService.prepare -> (LLM engine) -> SummarizationService._publish_summary ->
   ReportingService.process_summary
@@ -129,11 +129,10 @@ class RagPipeline:
 
     # ------------------------------------------------------------------ stages
     def prepare(self, n_threads: int, step: int) -> PreparedBatch:
-        from ..contracts.events import utc_now_iso
         st: dict[str, float] = {}
         t = time.perf_counter()
         raw = self.sources.pop(step, None) or self.generator.mbox(n_threads)
-        aid = self.ingestion._record(self.source, raw, f"/bench/step{step}.mbox", utc_now_iso())
+        aid = self.ingestion.record_archive(self.source, raw, f"/bench/step{step}.mbox")
         if aid is None:   # identical content already ingested (IngestionService dedupes by hash)
             raise ValueError(f"step {step}: archive already ingested")
         st["ingest"] = time.perf_counter() - t

@@ -127,6 +127,11 @@ class IngestionService(BaseService):
         self.metrics.increment("ingestion_files_total", tags={"source": cfg.name, "status": "success"})
         return aid
 
+    def record_archive(self, source: SourceConfig, content: bytes, file_path: str) -> str | None:
+        """Store one fetched archive and announce it (ArchiveIngested); None when identical content was
+        already ingested.  The fetch-free entry point of the batched driver (pipeline/rag.py)."""
+        return self._record(source, content, file_path, utc_now_iso())
+
     def ingest_archive(self, source: dict | SourceConfig, max_retries: int | None = None) -> list[str]:
         cfg = source if isinstance(source, SourceConfig) else SourceConfig.from_mapping(source)
         started = utc_now_iso()
