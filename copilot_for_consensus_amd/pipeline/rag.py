@@ -8,7 +8,7 @@ service's consumer loop receive the previous stage's event from the bus:
 
   IngestionService.record_archive -> ParsingService.process_archive -> ChunkingService.process_messages ->
   EmbeddingService.process_chunks -> OrchestratorService.orchestrate_threads ->
-  SummarizationService.prepare -> (LLM engine) -> SummarizationService._publish_summary ->
+  SummarizationService.prepare -> (LLM engine) -> SummarizationService.publish_summary ->
   ReportingService.process_summary
 
 so documents, ids, events (every one schema-validated on publish) and the store layout are exactly
@@ -184,7 +184,7 @@ class RagPipeline:
             text = self.bpe.decode(toks).strip() or "(empty summary)"
             s = Summary(th["_id"], text, llm_backend="hip", llm_model=self.llm_model, tokens_prompt=len(p),
                         tokens_completion=len(toks), latency_ms=int(1000 * gen.total_s))
-            ev = self.summarization._publish_summary(th["_id"], ctx, s)
+            ev = self.summarization.publish_summary(th["_id"], ctx, s)
             rid = self.reporting.process_summary(ev["data"], ev)
             reports.append(self.docs.get_document("summaries", rid))
         return reports

@@ -582,6 +582,10 @@ class SummarizationService(BaseService):
             self.metrics.gauge(f"summarization_gpu_{k}", float(v))
         return [self._publish_summary(tid, ctx, s) for (tid, ctx, _), s in zip(prepared, summaries)]
 
+    def publish_summary(self, tid: str, ctx: dict, s) -> dict:
+        """SummaryComplete for one summarized thread (citations from its context); returns the event."""
+        return self._publish_summary(tid, ctx, s)
+
     def _publish_summary(self, tid: str, ctx: dict, s) -> dict:
         cites = format_citations(ctx["chunks"], self.citation_count)
         sid = cids.summary_id(tid, [c["chunk_id"] for c in cites])
