@@ -10,7 +10,8 @@ MI355X layout choices:
     up rows interleaved in 8-row groups), so a layer is 4 GEMMs + RoPE/paged-KV write + attention
     + 2 fused split-K-reduce/residual/RMSNorm kernels;
   * decode (B > 4) projections on the hand-written weight-streaming MFMA GEMM (csrc/kernels/
-    dgemm.hip) with SwiGLU in the gate/up epilogue; B <= 4 on the GEMV; prefill on hipBLASLt;
+    dgemm.hip) with SwiGLU in the gate/up epilogue; B <= 4 on the GEMV; prefill on the hand-written
+    ping-pong MFMA GEMM (pgemm.hip) reading the same fragment-packed weights (one copy);
   * tensor parallel (Megatron column/row split) with one all-reduce after o_proj and one after
     down_proj, vocab-parallel lm_head + all-gather of logits -- see :mod:`..parallel.tp`;
   * weights random-initialised directly on the device (no network: BASELINE "random-init

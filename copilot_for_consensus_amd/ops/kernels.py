@@ -420,8 +420,9 @@ DGEMM_X_RATE = 90e9              # per-CU L2 -> LDS rate of the X re-reads (abla
 class PackedWeight:
     """A projection weight in the decode GEMM's fragment-packed layout for bn-row workgroups
     (cfc_dgemm_pack): [N/bn][K/32][bn/16][64 lanes][8] bf16 -- every 16-row x 32-k MFMA B fragment
-    1 KB contiguous in lane order, each workgroup's W slice one contiguous span.  The row-major
-    copy stays for prefill (hipBLASLt) and the B <= 4 GEMV."""
+    1 KB contiguous in lane order, each workgroup's W slice one contiguous span.  The prefill GEMM
+    (pgemm ping-pong) and the B <= 4 GEMV read it too, so by default it is the ONLY copy
+    (DecoderWeights.pack_decode(drop_rowmajor=True))."""
 
     __slots__ = ("data", "N", "K", "bn")
 

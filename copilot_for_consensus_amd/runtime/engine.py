@@ -4,7 +4,7 @@ The reference summarizes one thread at a time per replica with a blocking HTTP c
 Ollama/llama.cpp (summarization/app/service.py:289; local_llm_summarizer.py:107).  Here a
 batch of threads is generated together:
 
-  1. packed varlen prefill in chunks of ``max_prefill_tokens`` (large GEMMs for hipBLASLt, our
+  1. packed varlen prefill in chunks of ``max_prefill_tokens`` (large GEMMs for the ping-pong MFMA GEMM, our
      flash prefill kernel over the paged cache; long prompts are split = chunked prefill);
   2. one decode step = embedding -> 32 x (RMSNorm, QKV GEMM, RoPE+KV write, paged decode
      attention, O GEMM, RMSNorm, gate|up GEMM, SwiGLU, down GEMM) -> lm_head -> sampler ->
