@@ -447,11 +447,13 @@ class DecoderModel:
                             and mode in ("splitk", "dgemm") and weights.tp_size == 1 and gemv_shapes
                             and not self.fp8)
         self.fused_decode = mode == "dgemm"
-        # decode RoPE + KV write inside the attention kernel's prologue: opt-in.  Measured in the
-        # headline (profiles/r04_ab_*.log) the fused step decodes SLOWER (6.30 vs 6.09 s per batch):
-        # every attention workgroup waits ~5 us for its q slabs, the RoPE and the K/V store before its
-        # first KV load, twice per CU, which costs more than the 10.6-us rope_kv launch it removes.
-        self.rope_fused = os.environ.get("CFC_DECODE_ROPE_FUSED", "0") == "1"
+        # decode RoPE + KV write inside the attention kernel's prologue: CFC_DECODE_ROPE_FUSED "1"
+        # always, "0" never, unset: for B <= 4.  Measured in the headline (profiles/r04_ab_*.log) the
+        # fused BATCHED step decodes slower (6.30 vs 6.09 s per batch): every attention workgroup
+        # waits ~5 us for its q slabs, the RoPE and the K/V store before its first KV load, twice
+        # per CU, which costs more than the 10.6-us rope_kv launch it removes.  At B = 1 the launch
+        # is the larger cost: 296.5 -> 299.9 tok/s Mistral-7B (profiles/r04_latprof_*).
+        self.rope_fused = os.environ.get("CFC_DECODE_ROPE_FUSED", "")
         # B <= 4 decode on the ggml-quantized weights (GGUF checkpoints; csrc/kernels/quant.hip)
         self.decode_qgemv = (weights.qlayers is not None and os.environ.get("CFC_DECODE_QGEMV", "1") != "0"
                              and weights.tp_size == 1 and weights.gate_up_interleaved and not self.fp8)
@@ -612,7 +614,9 @@ class DecoderModel:
         Both write the same cache bytes and return the same output."""
         cfg, w = self.cfg, self.w
         sb = getattr(self, "_shared_blocks", None)
-        if self.rope_fused and qkv.is_cuda:
+        B = qkv.shape[-2]
+        fused = self.rope_fused == "1" or (self.rope_fused == "" and B <= K.GEMV_MAX_M)
+        if fused and qkv.is_cuda:
             return K.paged_decode_rope_attention(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], block_tables,
                                                  ctx_lens, self.scale, w.heads, w.kv_heads, cfg.head_dim,
                                                  part_blocks=part_blocks, workspace=attn_workspace,
@@ -701,7 +705,8 @@ class DecoderModel:
             lw = w.layers[i]
             if w.packed_only:
                 lw = dict(lw, **w.packed[i])
-            qkv = K.gemv(h, lw["qkv"])
+            # packed qkv: k-slice slabs straight into the slab-reading RoPE / KV write
+            qkv = K.gemv_part(h, lw["qkv"]) if isinstance(lw["qkv"], K.PackedWeight) else K.gemv(h, lw["qkv"])
             attn = self._rope_attention(i, qkv, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
                                         part_blocks)
             h = K.gemv_residual_rmsnorm(attn.view(B, -1), lw["o"], residual, lw["mlp_norm"], eps)

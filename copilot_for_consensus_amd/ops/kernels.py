@@ -661,7 +661,46 @@ def pgemm_ln(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, residual: tor
 GEMV_MAX_M = 4   # decode batches up to this size take the weight-streaming GEMV (gemm.hip: gemv_kernel)
 
 
-def gemv(x: torch.Tensor, w, epi: str = "bf16", out: torch.Tensor | None = None) -> torch.Tensor:
+GEMV_TILE_CUS = 256      # the packed GEMV's slab form aims at one workgroup per CU
+
+
+def gemv_packed_config(N: int, K: int, nw: int, M: int = 1, slab: bool = True) -> tuple[int, int]:
+    """(k-slices, waves per workgroup) of the packed GEMV (gemm.hip: gemv_tile_kernel).  Fitted to a
+    (split x waves) sweep on the 7B / 13B decode projections (profiles/r04_gemv_grid.jsonl): the
+    fastest points put ONE 8-wave workgroup on each CU -- split = the largest with tiles x split
+    <= 256 (qkv 7B: 4, down: 8, 13B down: 6) -- within 3% of the best of the grid; a partial
+    second round (tiles x split just over 256, e.g. 13B down at 7) costs up to 30%, and fewer
+    slabs also keep the consumer's one-workgroup-per-row reduce short.  Each wave keeps >= one
+    step of U kg.  In-kernel epilogues (slab=False) take split 1, 16 waves at M = 1 (VGPRs)."""
+    u = 2 if M > 2 else (3 if nw >= 7 else 4)
+    tiles, kg = N // (16 * nw), K // 32
+    if not slab:
+        return 1, (16 if M == 1 and kg >= 16 * u else 8 if kg >= 8 * u else 4)
+    split = max(1, min(GEMV_TILE_CUS // tiles, kg // (8 * u)))
+    return split, (8 if kg // split >= 8 * u else 4)
+
+
+def gemv_part(x: torch.Tensor, w: "PackedWeight", split: int | None = None, waves: int | None = None) -> torch.Tensor:
+    """x [M <= 4, K] @ W^T over a PackedWeight as fp32 k-slice slabs [split, M, N] (sum over dim 0 =
+    the product) in the split-K workspace: the packed GEMV's full-chip form, consumed by the
+    slab-reading RoPE / KV write and residual + RMSNorm reduce."""
+    M, Kd = x.shape
+    N = w.N
+    if not isinstance(w, PackedWeight) or w.K != Kd or not (1 <= M <= GEMV_MAX_M):
+        raise ValueError(f"gemv_part: x {tuple(x.shape)}, packed W [{N}, {w.K}] needed (M <= {GEMV_MAX_M})")
+    cs, cw = gemv_packed_config(N, Kd, w.bn // 16, M)
+    split, waves = split or cs, waves or cw
+    if not x.is_cuda:
+        y = torch.nn.functional.linear(x.float(), _rowmajor(w).float())
+        return torch.cat([y[None], torch.zeros(split - 1, M, N)]) if split > 1 else y[None]
+    _req(x, torch.bfloat16, "x")
+    part = _workspace(x.device, split * M * N)[:split * M * N].view(split, M, N)
+    check(kernels().cfc_gemv_packed(x.data_ptr(), w.data.data_ptr(), M, N, Kd, w.bn // 16, 0, part.data_ptr(), None,
+                                    N, split, waves, _stream(x)), "cfc_gemv_packed")
+    return part
+
+
+def gemv(x: torch.Tensor, w, epi: str = "bf16", out: torch.Tensor | None = None, waves: int | None = None) -> torch.Tensor:
     """x [M <= 4, K] @ w[N, K]^T on the GEMV kernel.  ``epi``: "bf16" -> bf16 [M, N]; "f32" -> fp32
     [M, N]; "swiglu" -> bf16 [M, N/2] = silu(gate) * up for 8-row interleaved gate/up weights.
     ``w``: row-major bf16 or a PackedWeight (the packed-weight GEMV: one weight copy)."""
@@ -684,8 +723,9 @@ def gemv(x: torch.Tensor, w, epi: str = "bf16", out: torch.Tensor | None = None)
         out = torch.empty(shape, dtype=torch.float32 if epi == "f32" else torch.bfloat16, device=x.device)
     yf, yb = (out.data_ptr(), None) if epi == "f32" else (None, out.data_ptr())
     if packed:
+        waves = waves or gemv_packed_config(N, Kd, w.bn // 16, M, slab=False)[1]
         check(kernels().cfc_gemv_packed(x.data_ptr(), w.data.data_ptr(), M, N, Kd, w.bn // 16, mode, yf, yb,
-                                        out.shape[1], _stream(x)), "cfc_gemv_packed")
+                                        out.shape[1], 1, waves, _stream(x)), "cfc_gemv_packed")
     else:
         check(kernels().cfc_gemv(x.data_ptr(), w.data_ptr(), M, N, Kd, mode, yf, yb, out.shape[1], _stream(x)),
               "cfc_gemv")
@@ -699,10 +739,13 @@ def gemv_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tens
     if not x.is_cuda:
         return _linear_residual_rmsnorm_ref(x, _rowmajor(w), residual, norm_w, eps)
     M, N = x.shape[0], w.shape[0]
-    part = _workspace(x.device, M * N)[:M * N].view(M, N)
-    gemv(x, w, "f32", out=part)
+    if isinstance(w, PackedWeight):
+        part = gemv_part(x, w)                      # [split, M, N] slabs, summed by the reduce below
+    else:
+        part = _workspace(x.device, M * N)[:M * N].view(1, M, N)
+        gemv(x, w, "f32", out=part[0])
     out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-    check(kernels().cfc_splitk_residual_rmsnorm(part.data_ptr(), 1, M, N, residual.data_ptr(), norm_w.data_ptr(),
+    check(kernels().cfc_splitk_residual_rmsnorm(part.data_ptr(), part.shape[0], M, N, residual.data_ptr(), norm_w.data_ptr(),
                                                 float(eps), out.data_ptr(), _stream(x)), "cfc_splitk_residual_rmsnorm")
     return out
 

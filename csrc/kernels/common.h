@@ -135,6 +135,29 @@ __device__ __forceinline__ int kv_v_slot(int key_in_block) {
 // 8 consecutive qkv values of token row element offset `off`: from the bf16 qkv, or summed from
 // `split` fp32 split-K slabs of the decode GEMM (slab stride `slab` elements) and rounded to bf16
 // -- the same values splitk_reduce would have written, without the round trip
+// a += sum_p part[p slab + off .. + 4], b += ... [+ 4 .. + 8], p ascending: the split-K slab sum of
+// one 8-column group.  Loads go out 8 slabs at a time (a plain loop waits one load latency per
+// slab: 12 us for 32 slabs of a 4096-wide row in one workgroup, profiles/r04_latprof_*).
+__device__ __forceinline__ void slab_sum8(const float* part, int split, size_t slab, size_t off, float4& a,
+                                          float4& b) {
+  for (int p0 = 0; p0 < split; p0 += 8) {
+    float4 x[8], y[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const size_t o = (size_t)min(p0 + u, split - 1) * slab + off;
+      x[u] = *reinterpret_cast<const float4*>(part + o);
+      y[u] = *reinterpret_cast<const float4*>(part + o + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (p0 + u < split) {
+        a.x += x[u].x; a.y += x[u].y; a.z += x[u].z; a.w += x[u].w;
+        b.x += y[u].x; b.y += y[u].y; b.z += y[u].z; b.w += y[u].w;
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ void qkv_load8(const uint16_t* qkv, const float* part, int split, size_t slab, size_t off,
                                           float* f) {
   if (part == nullptr) {
@@ -142,12 +165,7 @@ __device__ __forceinline__ void qkv_load8(const uint16_t* qkv, const float* part
     return;
   }
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-  for (int p = 0; p < split; ++p) {
-    const float4 x = *reinterpret_cast<const float4*>(part + p * slab + off);
-    const float4 y = *reinterpret_cast<const float4*>(part + p * slab + off + 4);
-    a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
-    b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
-  }
+  slab_sum8(part, split, slab, off, a, b);
   f[0] = bf2f(f2bf(a.x)); f[1] = bf2f(f2bf(a.y)); f[2] = bf2f(f2bf(a.z)); f[3] = bf2f(f2bf(a.w));
   f[4] = bf2f(f2bf(b.x)); f[5] = bf2f(f2bf(b.y)); f[6] = bf2f(f2bf(b.z)); f[7] = bf2f(f2bf(b.w));
 }

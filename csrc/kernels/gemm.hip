@@ -80,11 +80,9 @@ __global__ void __launch_bounds__(1024) splitk_residual_rmsnorm_kernel(const flo
         s[4] += b[p].x; s[5] += b[p].y; s[6] += b[p].z; s[7] += b[p].w;
       }
     } else {
-      for (int p = 0; p < split; ++p) {
-        const float4* row = reinterpret_cast<const float4*>(part + ((size_t)p * M + m) * N + c * 8);
-        const float4 a = row[0], b = row[1];
-        s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w; s[4] += b.x; s[5] += b.y; s[6] += b.z; s[7] += b.w;
-      }
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+      slab_sum8(part, split, (size_t)M * N, (size_t)m * N + c * 8, a, b);
+      s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w; s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
     }
     float r[8];
     unpack8(rr, r);
@@ -205,88 +203,113 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
   }
 }
 
-// GEMV over the decode GEMM's fragment-packed weight (cfc_dgemm_pack, bn = 16 nw): the B <= 4
+// GEMV over the decode GEMM's fragment-packed weight (cfc_dgemm_pack, bn = 16 NW): the B <= 4
 // decode path when only the packed copy of a projection exists (one weight copy for prefill,
 // batched and single-stream decode).  A packed fragment = 16 W rows x 32 k, lane l holding row
-// l & 15, k = 8 (l >> 4) .. +8 -- one 16-byte load per lane, 1 KB per wave instruction, the
-// contiguous pieces the stream reads fastest.
-//   * one workgroup per 16-row group g, its 4 waves split the K/32 fragments of the group (wave w
-//     streams fragments [w KG / 4, (w + 1) KG / 4) at stride nw KB: kg-major inside the span of the
-//     group's bn-row tile), GVP_U fragments in flight per wave, nontemporal buffer loads;
-//   * each lane dots its 8 weights with x[m][32 kg + 8 (l >> 4) ..] (16-byte loads of the L1/L2-
-//     resident activation rows, one address per 16 lanes);
-//   * lanes of one row are summed with two xor-shuffles, the 4 waves through LDS; epilogues as the
-//     row-major GEMV (fp32 / bf16 / SwiGLU over the 8-row interleaved gate/up groups: lanes r and
-//     r + 8 of a group hold gate and up row r of output column 8 g + r).
-constexpr int GVP_U = 8;
-
-template <int MT, int EPI>
-__global__ void __launch_bounds__(256) gemv_packed_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wp,
-                                                          int N, int K, int nw, float* __restrict__ yf,
-                                                          uint16_t* __restrict__ yb, int ldo) {
-  __shared__ float red[4][MT][16];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int g = blockIdx.x;                        // 16-row group
+// l & 15, k = 8 (l >> 4) .. +8 -- one 16-byte load per lane, 1 KB per wave instruction; a bn-row
+// tile is kg-major: the NW fragments of one kg (NW KB) are contiguous, then the next kg.
+//   * workgroup (tile, s) streams k-slice s of one tile: the tile's kg range split S ways, each
+//     slice ONE contiguous run of (KG / S) NW KB; its 4 waves take U consecutive kg each per
+//     step (a step of the workgroup = 4 U NW contiguous KB), all U NW loads of a step in flight
+//     at once (nontemporal buffer loads), one 16-byte activation load per kg shared by the NW
+//     fragments of that kg;
+//   * S > 1 (host: gemv_packed_split, tiles x S ~ 1024 workgroups) writes fp32 slice partials
+//     part[S, M, N] that the consumer sums -- the split-K reduce the decode already runs: RoPE / KV
+//     write from slabs for qkv, the residual + RMSNorm reduce for o / down.  A first build summed
+//     them in-kernel (last workgroup of a tile, agent-scope fence + ticket): the agent-scope
+//     release writes back the whole L2 per workgroup on gfx950 and the GEMV fell to 0.5-2 TB/s
+//     (profiles/r04_gemv_bench_fence.jsonl);
+//   * the first build -- one workgroup per 16-row group, its waves each streaming one group's
+//     1 KB pieces at NW KB stride -- reached 4.0 TB/s at 4 waves x 8 KB in flight and 3.8 TB/s at
+//     8 x 16 KB: scattered 1 KB pieces, not bytes in flight, were the limit (single-stream
+//     Mistral-7B 261-276 tok/s vs 330 on the row-major GEMV, profiles/r04_latency*);
+//   * per lane acc[NW][M]: two xor-shuffles sum the lanes of a row, LDS the 4 waves; epilogues
+//     (S = 1) as cfc_gemv: fp32 / bf16 / SwiGLU over the 8-row interleaved gate/up groups (rows
+//     16 g + r and 16 g + 8 + r -> output column 8 g + r); fp32 with S > 1 = the slab of slice s.
+template <int NW, int MT, int WAVES>
+__global__ void __launch_bounds__(64 * WAVES) gemv_tile_kernel(const uint16_t* __restrict__ X,
+                                                        const uint16_t* __restrict__ Wp, int N, int K, int S, int epi,
+                                                        float* __restrict__ yf, uint16_t* __restrict__ yb, int ldo) {
+  constexpr int U = MT > 2 ? 2 : (NW >= 7 ? 3 : 4);
+  constexpr int R = NW * MT * 16;                  // (group, m, row) values of one tile
+  __shared__ float red[WAVES][R];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane >> 4;
+  const int tile = blockIdx.x / S, s = blockIdx.x - tile * S;
   const int KG = K / 32;
-  const int kb = w * KG / 4, ke = (w + 1) * KG / 4;
-  const int q = lane >> 4;
-  // byte offset of fragment (g, kg): (((g / nw) * KG + kg) * nw + g % nw) KB; + 16 per lane
-  const uint16_t* span = Wp + (size_t)(g / nw) * KG * nw * 512 + (size_t)(g % nw) * 512;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)span);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)span >> 32));
+  const int kb = s * KG / S, ke = (s + 1) * KG / S;
+  const uint16_t* base = Wp + (size_t)tile * KG * NW * 512;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)base);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)base >> 32));
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(((uintptr_t)hi << 32) | lo), (short)0, (int)((size_t)KG * nw * 1024 - (size_t)(g % nw) * 1024), 0x00020000);
+      (void*)(((uintptr_t)hi << 32) | lo), (short)0, (int)((size_t)KG * NW * 1024), 0x00020000);
   const int voff = 16 * lane;
-  float acc[MT];
+  float acc[NW][MT];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) acc[m] = 0.f;
-  for (int k0 = kb; k0 < ke; k0 += GVP_U) {
-    uint4 wv[GVP_U], xv[GVP_U][MT];
+  for (int j = 0; j < NW; ++j)
 #pragma unroll
-    for (int u = 0; u < GVP_U; ++u) {
-      const int kg = min(k0 + u, ke - 1);          // tail: re-read the last fragment, weight 0 below
-      const gv_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, kg * nw * 1024, 2);
-      wv[u] = make_uint4(v.x, v.y, v.z, v.w);
+    for (int m = 0; m < MT; ++m) acc[j][m] = 0.f;
+  for (int k0 = kb + w * U; k0 < ke; k0 += WAVES * U) {
+    uint4 wv[U][NW], xv[U][MT];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kg = min(k0 + u, ke - 1);          // tail: re-read the last kg, weight 0 below
+#pragma unroll
+      for (int j = 0; j < NW; ++j) {
+        const gv_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + j * 1024, kg * NW * 1024, 2);
+        wv[u][j] = make_uint4(v.x, v.y, v.z, v.w);
+      }
     }
 #pragma unroll
-    for (int u = 0; u < GVP_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int kg = min(k0 + u, ke - 1);
 #pragma unroll
       for (int m = 0; m < MT; ++m) xv[u][m] = *reinterpret_cast<const uint4*>(X + (size_t)m * K + 32 * kg + 8 * q);
     }
 #pragma unroll
-    for (int u = 0; u < GVP_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       if (k0 + u < ke) {
 #pragma unroll
-        for (int m = 0; m < MT; ++m) acc[m] += dot8(wv[u], xv[u][m]);
+        for (int j = 0; j < NW; ++j)
+#pragma unroll
+          for (int m = 0; m < MT; ++m) acc[j][m] += dot8(wv[u][j], xv[u][m]);
       }
     }
   }
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    acc[m] += __shfl_xor(acc[m], 16, 64);
-    acc[m] += __shfl_xor(acc[m], 32, 64);
-  }
+  for (int j = 0; j < NW; ++j)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      acc[j][m] += __shfl_xor(acc[j][m], 16, 64);
+      acc[j][m] += __shfl_xor(acc[j][m], 32, 64);
+    }
   if (q == 0) {
 #pragma unroll
-    for (int m = 0; m < MT; ++m) red[w][m][lane] = acc[m];
+    for (int j = 0; j < NW; ++j)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) red[w][(j * MT + m) * 16 + lane] = acc[j][m];
   }
   __syncthreads();
-  if (w != 0 || q != 0) return;
-  const int r = lane;                              // row 16 g + r
+  const int row0 = tile * NW * 16;
+  // t = (j MT + m) 16 + r  ->  row row0 + 16 j + r of batch row m
+  for (int t = threadIdx.x; t < R; t += 64 * WAVES) {
+    float v = red[0][t];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    const float v = red[0][m][r] + red[1][m][r] + red[2][m][r] + red[3][m][r];
-    if constexpr (EPI == GV_SWIGLU) {
-      const float up = __shfl_xor(v, 8, 64);
-      if (r < 8) {
-        const float gg = bf2f(f2bf(v)), uu = bf2f(f2bf(up));
-        yb[(size_t)m * ldo + 8 * g + r] = f2bf(gg / (1.f + __expf(-gg)) * uu);
-      }
-    } else if constexpr (EPI == GV_BF16) {
-      yb[(size_t)m * ldo + 16 * g + r] = f2bf(v);
-    } else {
-      yf[(size_t)m * N + 16 * g + r] = v;
+    for (int ww = 1; ww < WAVES; ++ww) v += red[ww][t];
+    red[0][t] = v;
+  }
+  __syncthreads();
+  if (epi == GV_SWIGLU) {
+    for (int t = threadIdx.x; t < R / 2; t += 64 * WAVES) {
+      const int r = t & 7, jm = t >> 3, j = jm / MT, m = jm - j * MT;
+      const float gg = bf2f(f2bf(red[0][jm * 16 + r])), uu = bf2f(f2bf(red[0][jm * 16 + 8 + r]));
+      yb[(size_t)m * ldo + 8 * (tile * NW + j) + r] = f2bf(gg / (1.f + __expf(-gg)) * uu);
+    }
+  } else {
+    for (int t = threadIdx.x; t < R; t += 64 * WAVES) {
+      const int r = t & 15, jm = t >> 4, j = jm / MT, m = jm - j * MT;
+      const int row = row0 + 16 * j + r;
+      if (epi == GV_BF16) yb[(size_t)m * ldo + row] = f2bf(red[0][t]);
+      else yf[((size_t)s * MT + m) * N + row] = red[0][t];
     }
   }
 }
@@ -341,22 +364,41 @@ CFC_API int cfc_gemv(const void* x, const void* w, int M, int N, int K, int epi,
   return CFC_CHECK_LAUNCH();
 }
 
-// M <= 4 GEMV over a fragment-packed W (cfc_dgemm_pack layout for bn = 16 nw): epilogues as
-// cfc_gemv.  N % (16 nw) == 0, K % 64 == 0.
+namespace {
+template <int NW, int MT>
+void gemv_tile_launch(dim3 grid, int waves, hipStream_t stream, const uint16_t* x, const uint16_t* wp, int N, int K,
+                      int split, int epi, float* yf, uint16_t* yb, int ldo) {
+  if (waves == 4) gemv_tile_kernel<NW, MT, 4><<<grid, 256, 0, stream>>>(x, wp, N, K, split, epi, yf, yb, ldo);
+  else if (waves == 8) gemv_tile_kernel<NW, MT, 8><<<grid, 512, 0, stream>>>(x, wp, N, K, split, epi, yf, yb, ldo);
+  else if constexpr (MT == 1)   // 16 waves: 4 per SIMD, so <= 128 VGPRs -- single-row only
+    gemv_tile_kernel<NW, MT, 16><<<grid, 1024, 0, stream>>>(x, wp, N, K, split, epi, yf, yb, ldo);
+}
+}  // namespace
+
+// M <= 4 GEMV over a fragment-packed W (cfc_dgemm_pack layout for bn = 16 nw, nw in {4, 6, 7, 8}):
+// epilogues as cfc_gemv; split > 1 (fp32 only): yf = slabs [split, M, N] of the k-slice partial
+// sums.  N % (16 nw) == 0, K % 32 == 0, 1 <= split <= K / 32.
 CFC_API int cfc_gemv_packed(const void* x, const void* wp, int M, int N, int K, int nw, int epi, float* yf, void* yb,
-                            int ldo, hipStream_t stream) {
-  if (M < 1 || M > 4 || N <= 0 || nw <= 0 || N % (16 * nw) || K <= 0 || K % 64) return -1;
-  if ((epi == GV_F32 && !yf) || (epi != GV_F32 && !yb)) return -2;
-  const dim3 grid(N / 16);
-#define GVP_ARGS (const uint16_t*)x, (const uint16_t*)wp, N, K, nw, yf, (uint16_t*)yb, ldo
-#define GVP_CASE(MT)                                                                                 \
-  case MT:                                                                                           \
-    if (epi == GV_F32) gemv_packed_kernel<MT, GV_F32><<<grid, 256, 0, stream>>>(GVP_ARGS);           \
-    else if (epi == GV_BF16) gemv_packed_kernel<MT, GV_BF16><<<grid, 256, 0, stream>>>(GVP_ARGS);    \
-    else if (epi == GV_SWIGLU) gemv_packed_kernel<MT, GV_SWIGLU><<<grid, 256, 0, stream>>>(GVP_ARGS); \
-    else return -3;                                                                                  \
+                            int ldo, int split, int waves, hipStream_t stream) {
+  if (M < 1 || M > 4 || N <= 0 || nw <= 0 || N % (16 * nw) || K <= 0 || K % 32) return -1;
+  if ((epi == GV_F32 && !yf) || (epi != GV_F32 && !yb) || epi < 0 || epi > 2) return -2;
+  if (split < 1 || split > K / 32 || (split > 1 && epi != GV_F32)) return -4;
+  if (waves != 4 && waves != 8 && !(waves == 16 && M == 1)) return -5;
+  const dim3 grid((N / (16 * nw)) * split);
+#define GVP_ARGS (const uint16_t*)x, (const uint16_t*)wp, N, K, split, epi, yf, (uint16_t*)yb, ldo
+#define GVP_CASE(NW)                                                                         \
+  case NW:                                                                                   \
+    switch (M) {                                                                             \
+      case 1: gemv_tile_launch<NW, 1>(grid, waves, stream, GVP_ARGS); break;                 \
+      case 2: gemv_tile_launch<NW, 2>(grid, waves, stream, GVP_ARGS); break;                 \
+      case 3: gemv_tile_launch<NW, 3>(grid, waves, stream, GVP_ARGS); break;                 \
+      default: gemv_tile_launch<NW, 4>(grid, waves, stream, GVP_ARGS); break;                \
+    }                                                                                        \
     break;
-  switch (M) { GVP_CASE(1) GVP_CASE(2) GVP_CASE(3) GVP_CASE(4) }
+  switch (nw) {
+    GVP_CASE(4) GVP_CASE(6) GVP_CASE(7) GVP_CASE(8)
+    default: return -3;
+  }
 #undef GVP_CASE
 #undef GVP_ARGS
   return CFC_CHECK_LAUNCH();

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """GEMV (gemm.hip: gemv_kernel) vs hipBLASLt (F.linear) on the Mistral-7B / Llama-2-13B decode
-projections at M = 1..4: microseconds per call and achieved weight-stream bandwidth."""
+projections at M = 1..4: microseconds per call and achieved weight-stream bandwidth; plus the
+packed-weight GEMV (gemv_tile_kernel, the layout the model keeps) at several workgroup targets."""
 import json
 import os
 import sys
@@ -35,6 +36,7 @@ def main():
     for name, (N, Kd) in SHAPES.items():
         copies = max(2, int(1e9 // (N * Kd * 2)))
         ws = [torch.randn(N, Kd, device="cuda").bfloat16() for _ in range(copies)]
+        ps = [K.pack_dgemm_weight(w, swiglu="gate_up" in name) for w in ws]
         for M in (1, 2, 4):
             x = torch.randn(M, Kd, device="cuda").bfloat16()
             it = iter(range(1 << 30))
@@ -42,9 +44,32 @@ def main():
             epi = "swiglu" if "gate_up" in name else "bf16"
             gv = timeit(lambda: K.gemv(x, ws[next(it) % copies], epi))
             tb = N * Kd * 2 / 1e6
-            print(json.dumps({"shape": name, "N": N, "K": Kd, "M": M, "lib_us": round(lib, 1), "gemv_us": round(gv, 1),
-                              "lib_TB_s": round(tb / lib, 2), "gemv_TB_s": round(tb / gv, 2)}), flush=True)
-        del ws
+            rec = {"shape": name, "N": N, "K": Kd, "M": M, "lib_us": round(lib, 1), "gemv_us": round(gv, 1),
+                   "lib_TB_s": round(tb / lib, 2), "gemv_TB_s": round(tb / gv, 2)}
+            # packed weight (the copy the model keeps): split 1 with the epilogue in-kernel at 4 / 8 / 16
+            # waves per workgroup, and the k-slice slab form over (split, waves) plus its consumer (the
+            # residual + RMSNorm reduce, one workgroup per row, as o / down run it)
+            nw = ps[0].bn // 16
+            for wv in ((4, 8, 16) if M == 1 else (4, 8)):
+                pv = timeit(lambda: K.gemv(x, ps[next(it) % copies], epi, waves=wv))
+                rec[f"s1w{wv}_us"] = round(pv, 1)
+            auto = K.gemv_packed_config(N, Kd, nw, M)
+            rec["auto"] = auto
+            cfgs = {auto, (auto[0] * 2, 4), (auto[0] * 2, auto[1]), (max(1, auto[0] // 2), min(auto[1] * 2, 16 if M == 1 else 8))}
+            res = torch.zeros(M, N, device="cuda").bfloat16()
+            nrm = torch.ones(N, device="cuda").bfloat16()
+            for sp, wv in sorted(cfgs):
+                if sp > Kd // 32:
+                    continue
+                pv = timeit(lambda: K.gemv_part(x, ps[next(it) % copies], sp, wv))
+                part = K.gemv_part(x, ps[0], sp, wv)
+                if epi == "swiglu" or N // 8 > 1024:   # qkv-like: the slab RoPE reads them instead
+                    red = timeit(lambda: K.splitk_reduce(part, swiglu=epi == "swiglu"))
+                else:
+                    red = timeit(lambda: K.splitk_residual_rmsnorm(part, res, nrm, 1e-5))
+                rec[f"slab_s{sp}w{wv}"] = [round(pv, 1), round(red, 1)]
+            print(json.dumps(rec), flush=True)
+        del ws, ps
         torch.cuda.empty_cache()
 
 

@@ -559,6 +559,32 @@ def test_gemv_packed_weight(M, N, Kd, bn):
         _close(K.gemv(x, pw, "swiglu"), want, 3e-2)
 
 
+@pytest.mark.parametrize("split", [1, 2, 5, 32])
+@pytest.mark.parametrize("M,waves", [(1, 4), (1, 16), (3, 8)])
+def test_gemv_packed_slabs(split, M, waves):
+    """The packed GEMV's k-slice slab form (split 1 .. K / 32): the slabs sum to the product, the
+    residual + RMSNorm reduce over them matches the row-major GEMV route, and repeated launches
+    are bit-identical."""
+    N, Kd, bn = 896, 1024, 112
+    x = (torch.rand(M, Kd, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(N, Kd, device=DEV) * 2 - 1) / Kd ** 0.5).bfloat16()
+    pw = K.pack_dgemm_weight(w, bn=bn)
+    part = K.gemv_part(x, pw, split, waves).clone()
+    assert part.shape == (split, M, N)
+    _close(part.sum(0), _ref_linear(x, w), 1e-3)
+    assert torch.equal(part, K.gemv_part(x, pw, split, waves))
+    for epi in ("f32", "bf16", "swiglu"):      # split-1 epilogues at this wave count
+        want = K.gemv(x, w, epi).float()
+        torch.testing.assert_close(K.gemv(x, pw, epi, waves=waves).float(), want, rtol=2e-2, atol=2e-2)
+    norm = torch.rand(N, device=DEV).bfloat16()
+    r1 = (torch.rand(M, N, device=DEV) * 2 - 1).bfloat16()
+    r2 = r1.clone()
+    o1 = K.gemv_residual_rmsnorm(x, pw, r1, norm, 1e-5)
+    o2 = K.gemv_residual_rmsnorm(x, w, r2, norm, 1e-5)
+    torch.testing.assert_close(r1.float(), r2.float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(o1.float(), o2.float(), rtol=2e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("split", [1, 3, 4])
 def test_rope_kv_write_from_splitk_slabs_matches_reduce_then_rope(split):
     """rope_kv_write_part == splitk_reduce -> rope_kv_write, bit for bit (q, K cache, V cache)."""
