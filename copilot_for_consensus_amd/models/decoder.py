@@ -472,7 +472,9 @@ class DecoderModel:
 
     PACKED_FREE_FRACTION = 0.3   # HBM left free after packing when both copies are kept
     PREFILL_GEMM_DEFAULT = "hip"
-    PGEMM_VARIANT_DEFAULT = "pp"
+    # "pps": the ping-pong K loop with the LDS-staged 16-byte-store epilogue -- bit-identical to
+    # "pp", +2.0% qkv / +1.0% o / +0.3% down / -0.2% gate_up (profiles/r04_pgemm_pps.jsonl)
+    PGEMM_VARIANT_DEFAULT = "pps"
     PGEMM_MIN_ROWS = 256         # fewer prompt rows than one 256-row tile: the decode GEMM (packed) or the library
 
     def _packing(self) -> str | None:

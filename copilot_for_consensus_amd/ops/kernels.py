@@ -368,13 +368,16 @@ def _workspace(device, numel: int) -> torch.Tensor:
     """Grow-only fp32 split-K workspace per device (sized during the eager warm-up, so hipGraph
     capture sees a fixed pointer; see _retired_workspaces for why old ones stay allocated)."""
     device = torch.device(device)
-    ws = _workspaces.get(device)
+    # one per (device, stream): two streams' kernels in flight at once (a prefill beside a decode,
+    # the node's consumer threads) must not share their split-K slabs
+    key = (device, torch.cuda.current_stream(device).cuda_stream if device.type == "cuda" else 0)
+    ws = _workspaces.get(key)
     if ws is None or ws.numel() < numel:
         size = max(numel, 1 << 20, 2 * ws.numel() if ws is not None else 0)
         if ws is not None:
             _retired_workspaces.append(ws)
         ws = torch.empty(size, dtype=torch.float32, device=device)
-        _workspaces[device] = ws
+        _workspaces[key] = ws
     return ws
 
 
@@ -593,10 +596,11 @@ def pgemm(x: torch.Tensor, w, epi: str = "bf16", bias: torch.Tensor | None = Non
     elementwise op fused into the epilogue.  ``epi``: "bf16"; "bias" (+ bias[N]); "bias_gelu"
     (gelu_erf(y + bias)); "swiglu" (8-row interleaved gate/up weights -> [M, N/2] =
     silu(gate) * up with the unfused path's bf16 rounding of gate and up).  ``w``: row-major bf16
-    [N, K], or the decode GEMM's PackedWeight (one weight copy for prefill and decode: the "w4" or,
-    for any other variant, the "pp" kernel).  ``variant``: the K loop ("stage2": 2 LDS stages of
-    BK=64; "ring5" / "ring4": BK=32 rings of 5 / 4 LDS slots; "pp": two wave groups ping-ponging
-    over half-tile stages; "w4": four 128x128 waves software-pipelined over a 4-stage ring),
+    [N, K], or the decode GEMM's PackedWeight (one weight copy for prefill and decode: the "w4",
+    "pps" or, for any other variant, the "pp" kernel).  ``variant``: the K loop ("stage2": 2 LDS
+    stages of BK=64; "ring5" / "ring4": BK=32 rings of 5 / 4 LDS slots; "pp": two wave groups
+    ping-ponging over half-tile stages; "pps": "pp" with the LDS-staged 16-byte-store epilogue, the
+    decoder's default; "w4": four 128x128 waves software-pipelined over a 4-stage ring),
     $CFC_PGEMM_VARIANT when None."""
     mode = PGEMM_EPI[epi]
     packed = isinstance(w, PackedWeight)

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Session 3 check: every GPU test, smoke, then the headline bench (5 steps) with the pps prefill
+# default, 8-at-a-time slab sums and the packed tile GEMV.
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_s3.log 2>&1 || { tail -40 gpurun_out/pytest_gpu_s3.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu_s3.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_s3.log 2>&1 || { tail -30 gpurun_out/smoke_s3.log; exit 1; }
+tail -1 gpurun_out/smoke_s3.log
+timeout -k 10 700 python -u bench.py --steps 5 --warmup 1 > gpurun_out/bench_s3.log 2>&1 || { tail -30 gpurun_out/bench_s3.log; exit 1; }
+grep -E '^\[bench\] step|"metric"' gpurun_out/bench_s3.log | cut -c1-600

@@ -172,9 +172,12 @@ def test_small_graph_survives_workspace_growth():
     g = torch.Generator().manual_seed(4)
     big = [[1] + torch.randint(3, cfg.vocab_size, (200,), generator=g).tolist() for _ in range(64)]
     eng.generate(big, 4, ignore_eos=True)
-    ws = K._workspaces[torch.device("cuda", torch.cuda.current_device())]
-    K._workspace(ws.device, 4 * ws.numel())           # force a growth past anything captured so far
-    junk = torch.full((ws.numel(),), float("nan"), device="cuda")   # likely reuses freed memory
+    grown = 0
+    for key, ws in list(K._workspaces.items()):       # every stream's: force a growth past anything captured
+        K._retired_workspaces.append(ws)
+        K._workspaces[key] = torch.empty(4 * ws.numel(), device=ws.device)
+        grown = max(grown, ws.numel())
+    junk = torch.full((grown,), float("nan"), device="cuda")   # likely reuses freed memory
     again = eng.generate(small, 16, ignore_eos=True).tokens
     del junk
     kv2 = PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, "cuda")
