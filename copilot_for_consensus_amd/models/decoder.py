@@ -454,6 +454,11 @@ class DecoderModel:
         # per CU, which costs more than the 10.6-us rope_kv launch it removes.  At B = 1 the launch
         # is the larger cost: 296.5 -> 299.9 tok/s Mistral-7B (profiles/r04_latprof_*).
         self.rope_fused = os.environ.get("CFC_DECODE_ROPE_FUSED", "")
+        # B <= 4 over packed weights: residual + RMSNorm folded into the next GEMV (K.gemv_norm).
+        # Opt-in: bit-identical, two launches fewer per layer, but slower -- the prologue's slab reads
+        # (written by another XCD, served from the MALL) stall the weight stream behind them:
+        # Mistral-7B 307.7 vs 313.5 tok/s, Llama-2-13B 177.1 vs 190.9 (profiles/r04_gemv_norm_ab.log)
+        self.gemv_norm_fused = os.environ.get("CFC_DECODE_GEMV_NORM", "0") == "1"
         # B <= 4 decode on the ggml-quantized weights (GGUF checkpoints; csrc/kernels/quant.hip)
         self.decode_qgemv = (weights.qlayers is not None and os.environ.get("CFC_DECODE_QGEMV", "1") != "0"
                              and weights.tp_size == 1 and weights.gate_up_interleaved and not self.fp8)
@@ -702,6 +707,9 @@ class DecoderModel:
         residual + next-RMSNorm reduce.  Same rounding points as _forward_decode_splitk."""
         cfg, w = self.cfg, self.w
         B, eps = h.shape[0], cfg.rms_eps
+        if w.packed_only and h.is_cuda and self.gemv_norm_fused and cfg.hidden <= 8192:
+            return self._forward_decode_gemv_fused(h, residual, positions, slots, ctx_lens, block_tables, kv,
+                                                   attn_workspace, part_blocks)
         for i in range(cfg.layers):
             # packed-only weights: the packed-weight GEMV reads the packed copies
             lw = w.layers[i]
@@ -716,6 +724,49 @@ class DecoderModel:
             nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm
             h = K.gemv_residual_rmsnorm(a, lw["down"], residual, nxt, eps)
         return h
+
+    def _forward_decode_gemv_fused(self, h, residual, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
+                                   part_blocks):
+        """B <= 4 decode over the packed weights with the residual + RMSNorm reduces folded into the
+        next GEMV's prologue (K.gemv_norm): per layer qkv (slabs, its input norm fused from the
+        previous down's slabs) -> RoPE / attention -> o (slabs) -> gate_up + SwiGLU (its input norm
+        fused from o's slabs) -> down (slabs).  Two launches fewer per layer than
+        _forward_decode_gemv, bit-identical to it: the prologue repeats the reduce kernel's
+        arithmetic.  The residual alternates between two buffers (a fused norm reads one while its
+        workgroup 0 writes the other); consecutive slab producers alternate two halves of the
+        split-K workspace (a producer's input slabs are still being read while it writes)."""
+        cfg, w = self.cfg, self.w
+        B, eps = h.shape[0], cfg.rms_eps
+        P = [w.packed[i] for i in range(cfg.layers)]
+
+        def nslab(W):
+            return K.gemv_packed_config(W.N, W.K, W.bn // 16, B)[0] * B * W.N
+        size = max(nslab(P[0][k]) for k in ("qkv", "o", "down"))
+        ws = K._workspace(h.device, 2 * size)
+        bufs, nb = (ws[:size], ws[size:2 * size]), 0
+        res, cur = (residual, torch.empty_like(residual)), 0
+        pend = None
+        for i in range(cfg.layers):
+            lw, pw = w.layers[i], P[i]
+
+            def out(W):
+                sp = K.gemv_packed_config(W.N, W.K, W.bn // 16, B)[0]
+                return bufs[nb][:sp * B * W.N].view(sp, B, W.N)
+            if pend is None:
+                qkv = K.gemv_part(h, pw["qkv"], out=out(pw["qkv"]))
+            else:
+                qkv = K.gemv_norm(pend, res[cur], res[1 - cur], lw["attn_norm"], eps, pw["qkv"], out=out(pw["qkv"]))
+                cur ^= 1
+            nb ^= 1
+            attn = self._rope_attention(i, qkv, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
+                                        part_blocks)
+            o = K.gemv_part(attn.view(B, -1), pw["o"], out=out(pw["o"]))
+            nb ^= 1
+            a = K.gemv_norm(o, res[cur], res[1 - cur], lw["mlp_norm"], eps, pw["gate_up"], "swiglu")
+            cur ^= 1
+            pend = K.gemv_part(a, pw["down"], out=out(pw["down"]))
+            nb ^= 1
+        return K.splitk_residual_rmsnorm(pend, res[cur], w.final_norm, eps)
 
     def _forward_decode_qgemv(self, h, residual, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
                               part_blocks):

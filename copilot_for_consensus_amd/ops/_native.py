@@ -68,7 +68,7 @@ _KERNEL_SIGS = {
     "cfc_dgemm_pack": [P, P, I, I, I, P],
     "cfc_dgemm_ablate": [P, P, I, I, I, I, I, I, P, P],
     "cfc_gemv": [P, P, I, I, I, I, P, P, I, P],
-    "cfc_gemv_packed": [P, P, I, I, I, I, I, P, P, I, I, I, P],
+    "cfc_gemv_packed": [P, P, I, I, I, I, I, P, P, I, I, I, P, I, P, P, P, F, P],
     "cfc_qgemv": [P, I, I, I, I, P, P, c_int64, c_int64, c_int64, I, P, P, I, P],
     "cfc_dequant_bf16": [P, I, c_int64, P, P],
     "cfc_splitk_residual_rmsnorm": [P, I, I, I, P, P, F, P, P],

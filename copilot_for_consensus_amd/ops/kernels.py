@@ -666,6 +666,7 @@ GEMV_MAX_M = 4   # decode batches up to this size take the weight-streaming GEMV
 
 
 GEMV_TILE_CUS = 256      # the packed GEMV's slab form aims at one workgroup per CU
+GEMV_NORM_WAVES = 8      # fused-norm GEMV at M = 1 (4 measured slower)
 
 
 def gemv_packed_config(N: int, K: int, nw: int, M: int = 1, slab: bool = True) -> tuple[int, int]:
@@ -684,7 +685,8 @@ def gemv_packed_config(N: int, K: int, nw: int, M: int = 1, slab: bool = True) -
     return split, (8 if kg // split >= 8 * u else 4)
 
 
-def gemv_part(x: torch.Tensor, w: "PackedWeight", split: int | None = None, waves: int | None = None) -> torch.Tensor:
+def gemv_part(x: torch.Tensor, w: "PackedWeight", split: int | None = None, waves: int | None = None,
+              out: torch.Tensor | None = None) -> torch.Tensor:
     """x [M <= 4, K] @ W^T over a PackedWeight as fp32 k-slice slabs [split, M, N] (sum over dim 0 =
     the product) in the split-K workspace: the packed GEMV's full-chip form, consumed by the
     slab-reading RoPE / KV write and residual + RMSNorm reduce."""
@@ -698,10 +700,55 @@ def gemv_part(x: torch.Tensor, w: "PackedWeight", split: int | None = None, wave
         y = torch.nn.functional.linear(x.float(), _rowmajor(w).float())
         return torch.cat([y[None], torch.zeros(split - 1, M, N)]) if split > 1 else y[None]
     _req(x, torch.bfloat16, "x")
-    part = _workspace(x.device, split * M * N)[:split * M * N].view(split, M, N)
+    part = out if out is not None else _workspace(x.device, split * M * N)[:split * M * N].view(split, M, N)
+    if part.shape != (split, M, N) or part.dtype != torch.float32 or not part.is_contiguous():
+        raise ValueError(f"gemv_part: out {tuple(part.shape)} {part.dtype}, fp32 [{split}, {M}, {N}] needed")
     check(kernels().cfc_gemv_packed(x.data_ptr(), w.data.data_ptr(), M, N, Kd, w.bn // 16, 0, part.data_ptr(), None,
-                                    N, split, waves, _stream(x)), "cfc_gemv_packed")
+                                    N, split, waves, None, 0, None, None, None, 0.0, _stream(x)), "cfc_gemv_packed")
     return part
+
+
+def gemv_norm(part: torch.Tensor, res_in: torch.Tensor, res_out: torch.Tensor, norm_w: torch.Tensor, eps: float,
+              w: "PackedWeight", epi: str = "slabs", split: int | None = None, waves: int | None = None,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """The packed GEMV with the residual + RMSNorm that produces its input folded into its prologue:
+    x = RMSNorm(res_in + sum(part)) * norm_w, exactly as splitk_residual_rmsnorm computes it, then
+    x @ W^T.  res_out <- res_in + sum(part) (bf16); res_in is left unchanged (it must be a different
+    buffer: the other workgroups still read it).  ``epi``: "slabs" -> fp32 k-slice slabs
+    [split, M, N] (in ``out`` or the split-K workspace); "bf16" / "swiglu" -> split 1, in-kernel
+    epilogue.  One launch instead of the reduce kernel plus the GEMV (gemm.hip: gemv_tile_kernel)."""
+    S_in, M, Kd = part.shape
+    N = w.N
+    if not isinstance(w, PackedWeight) or w.K != Kd or not (1 <= M <= GEMV_MAX_M):
+        raise ValueError(f"gemv_norm: slabs {tuple(part.shape)}, packed W [{N}, {w.K}] needed (M <= {GEMV_MAX_M})")
+    slab = epi == "slabs"
+    cs, cw = gemv_packed_config(N, Kd, w.bn // 16, M, slab=slab)
+    split = (split or cs) if slab else 1
+    # the prologue's registers: 16-wave groups spill; at M > 1 so do 8-wave ones
+    waves = waves or min(cw, GEMV_NORM_WAVES if M == 1 else 4)
+    if not part.is_cuda:      # splitk_residual_rmsnorm's CPU arithmetic
+        x, r = ref.rmsnorm(part.sum(0).to(res_in.dtype), norm_w, eps, res_in)
+        res_out.copy_(r)
+        if slab:
+            return gemv_part(x, w, split)
+        return gemv(x, w, epi)
+    for t, nm in ((res_in, "res_in"), (res_out, "res_out"), (norm_w, "norm_w")):
+        _req(t, torch.bfloat16, nm)
+    if res_in.data_ptr() == res_out.data_ptr():
+        raise ValueError("gemv_norm: res_out must be a different buffer from res_in")
+    if slab:
+        if out is None:
+            out = _workspace(part.device, split * M * N)[:split * M * N].view(split, M, N)
+        yf, yb, mode, ldo = out.data_ptr(), None, 0, N
+    else:
+        mode = {"bf16": 1, "swiglu": 2}[epi]
+        if out is None:
+            out = torch.empty(M, N // 2 if epi == "swiglu" else N, dtype=torch.bfloat16, device=part.device)
+        yf, yb, ldo = None, out.data_ptr(), out.shape[1]
+    check(kernels().cfc_gemv_packed(None, w.data.data_ptr(), M, N, Kd, w.bn // 16, mode, yf, yb, ldo, split, waves,
+                                    part.data_ptr(), S_in, res_in.data_ptr(), res_out.data_ptr(), norm_w.data_ptr(),
+                                    float(eps), _stream(part)), "cfc_gemv_packed")
+    return out
 
 
 def gemv(x: torch.Tensor, w, epi: str = "bf16", out: torch.Tensor | None = None, waves: int | None = None) -> torch.Tensor:
@@ -729,7 +776,8 @@ def gemv(x: torch.Tensor, w, epi: str = "bf16", out: torch.Tensor | None = None,
     if packed:
         waves = waves or gemv_packed_config(N, Kd, w.bn // 16, M, slab=False)[1]
         check(kernels().cfc_gemv_packed(x.data_ptr(), w.data.data_ptr(), M, N, Kd, w.bn // 16, mode, yf, yb,
-                                        out.shape[1], 1, waves, _stream(x)), "cfc_gemv_packed")
+                                        out.shape[1], 1, waves, None, 0, None, None, None, 0.0, _stream(x)),
+              "cfc_gemv_packed")
     else:
         check(kernels().cfc_gemv(x.data_ptr(), w.data_ptr(), M, N, Kd, mode, yf, yb, out.shape[1], _stream(x)),
               "cfc_gemv")

@@ -226,13 +226,32 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
 //   * per lane acc[NW][M]: two xor-shuffles sum the lanes of a row, LDS the 4 waves; epilogues
 //     (S = 1) as cfc_gemv: fp32 / bf16 / SwiGLU over the 8-row interleaved gate/up groups (rows
 //     16 g + r and 16 g + 8 + r -> output column 8 g + r); fp32 with S > 1 = the slab of slice s.
-template <int NW, int MT, int WAVES>
+// The residual + RMSNorm that produces this GEMV's input, folded into its prologue (XN): the
+// input is the previous projection's fp32 k-slice slabs, and every workgroup rebuilds the whole
+// normalised row in LDS -- h = bf16(bf16(sum of slabs) + residual), x = bf16(h rsqrt(mean h^2 +
+// eps) w) -- with the reduce kernel's exact arithmetic (slabs summed in order, the sum of squares
+// as its 64-lane waves and their in-order total), so x is bit-identical to
+// cfc_splitk_residual_rmsnorm's.  Workgroup 0 stores h to res_out (a different buffer from
+// res_in: the other workgroups are still reading it).  The first step's weight loads are issued
+// before the prologue, so its slab reads hide under the weight stream instead of a launch.
+struct GvNorm {
+  const float* part;
+  int split;
+  const uint16_t* res_in;
+  uint16_t* res_out;
+  const uint16_t* w;
+  float eps;
+};
+
+template <int NW, int MT, int WAVES, bool XN>
 __global__ void __launch_bounds__(64 * WAVES) gemv_tile_kernel(const uint16_t* __restrict__ X,
                                                         const uint16_t* __restrict__ Wp, int N, int K, int S, int epi,
-                                                        float* __restrict__ yf, uint16_t* __restrict__ yb, int ldo) {
+                                                        float* __restrict__ yf, uint16_t* __restrict__ yb, int ldo,
+                                                        GvNorm nm) {
   constexpr int U = MT > 2 ? 2 : (NW >= 7 ? 3 : 4);
   constexpr int R = NW * MT * 16;                  // (group, m, row) values of one tile
   __shared__ float red[WAVES][R];
+  extern __shared__ uint4 xs[];                    // XN: the normalised rows [MT][K] (bf16)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane >> 4;
   const int tile = blockIdx.x / S, s = blockIdx.x - tile * S;
   const int KG = K / 32;
@@ -248,33 +267,92 @@ __global__ void __launch_bounds__(64 * WAVES) gemv_tile_kernel(const uint16_t* _
   for (int j = 0; j < NW; ++j)
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[j][m] = 0.f;
-  for (int k0 = kb + w * U; k0 < ke; k0 += WAVES * U) {
-    uint4 wv[U][NW], xv[U][MT];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kg = min(k0 + u, ke - 1);          // tail: re-read the last kg, weight 0 below
-#pragma unroll
-      for (int j = 0; j < NW; ++j) {
-        const gv_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + j * 1024, kg * NW * 1024, 2);
-        wv[u][j] = make_uint4(v.x, v.y, v.z, v.w);
-      }
+#define GVT_LOAD_W(K0)                                                                                 \
+  uint4 wv[U][NW];                                                                                     \
+  _Pragma("unroll") for (int u = 0; u < U; ++u) {                                                      \
+    const int kg = min((K0) + u, ke - 1);          /* tail: re-read the last kg, weight 0 below */     \
+    _Pragma("unroll") for (int j = 0; j < NW; ++j) {                                                   \
+      const gv_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + j * 1024, kg * NW * 1024, 2); \
+      wv[u][j] = make_uint4(v.x, v.y, v.z, v.w);                                                       \
+    }                                                                                                  \
+  }
+#define GVT_DOT(K0)                                                                                    \
+  {                                                                                                    \
+    uint4 xv[U][MT];                                                                                   \
+    _Pragma("unroll") for (int u = 0; u < U; ++u) {                                                    \
+      const int kg = min((K0) + u, ke - 1);                                                            \
+      _Pragma("unroll") for (int m = 0; m < MT; ++m) {                                                 \
+        if constexpr (XN) xv[u][m] = xs[(m * K + 32 * kg + 8 * q) >> 3];                              \
+        else xv[u][m] = *reinterpret_cast<const uint4*>(X + (size_t)m * K + 32 * kg + 8 * q);          \
+      }                                                                                                \
+    }                                                                                                  \
+    _Pragma("unroll") for (int u = 0; u < U; ++u) {                                                    \
+      if ((K0) + u < ke) {                                                                             \
+        _Pragma("unroll") for (int j = 0; j < NW; ++j)                                                 \
+          _Pragma("unroll") for (int m = 0; m < MT; ++m) acc[j][m] += dot8(wv[u][j], xv[u][m]);       \
+      }                                                                                                \
+    }                                                                                                  \
+  }
+  if constexpr (!XN) {
+    for (int k0 = kb + w * U; k0 < ke; k0 += WAVES * U) {
+      GVT_LOAD_W(k0)
+      GVT_DOT(k0)
     }
+  } else {
+    // every wave runs the same step count (a wave past the slice re-reads its last kg, masked), so
+    // all of them reach the prologue's barriers; the first step's weight loads go out before it.
+    // (Issuing the prologue's first slab / residual / norm loads ahead of the weights, so its wait
+    // does not include the weight stream, needs ~64 more VGPRs: it spilled and measured slower.)
+    __shared__ float red_ss[MT][32];
+    const int nsteps = (ke - kb + WAVES * U - 1) / (WAVES * U);
+    for (int st = 0; st < nsteps; ++st) {
+      const int k0 = kb + st * WAVES * U + w * U;
+      GVT_LOAD_W(k0)
+      if (st == 0) {
+        const int G = K / 8, nvw = (G + 63) / 64;  // the reduce kernel's block: one 8-column group per thread
+        for (int m = 0; m < MT; ++m) {
+          for (int vw = w; vw < nvw; vw += WAVES) {
+            const int c = vw * 64 + lane;
+            float ss = 0.f;
+            if (c < G) {
+              float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+              slab_sum8(nm.part, nm.split, (size_t)MT * K, (size_t)m * K + 8 * c, a, b);
+              const float sv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+              float r[8], v[8];
+              unpack8(*reinterpret_cast<const uint4*>(nm.res_in + (size_t)m * K + 8 * c), r);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kg = min(k0 + u, ke - 1);
+              for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(sv[j])) + r[j];
+              const uint4 pk = pack8(v);
+              xs[(m * K + 8 * c) >> 3] = pk;
+              if (blockIdx.x == 0) *reinterpret_cast<uint4*>(nm.res_out + (size_t)m * K + 8 * c) = pk;
+              unpack8(pk, v);
 #pragma unroll
-      for (int m = 0; m < MT; ++m) xv[u][m] = *reinterpret_cast<const uint4*>(X + (size_t)m * K + 32 * kg + 8 * q);
-    }
+              for (int j = 0; j < 8; ++j) ss += v[j] * v[j];
+            }
+            ss = wave_sum(ss);
+            if (lane == 0) red_ss[m][vw] = ss;
+          }
+        }
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < MT * G; idx += 64 * WAVES) {
+          const int m = idx / G, c = idx - m * G;
+          float t = 0.f;
+          for (int i = 0; i < nvw; ++i) t += red_ss[m][i];
+          const float inv = rsqrtf(t / (float)K + nm.eps);
+          float v[8], gw[8], o[8];
+          unpack8(xs[idx], v);
+          unpack8(reinterpret_cast<const uint4*>(nm.w)[c], gw);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (k0 + u < ke) {
-#pragma unroll
-        for (int j = 0; j < NW; ++j)
-#pragma unroll
-          for (int m = 0; m < MT; ++m) acc[j][m] += dot8(wv[u][j], xv[u][m]);
+          for (int j = 0; j < 8; ++j) o[j] = v[j] * inv * gw[j];
+          xs[idx] = pack8(o);
+        }
+        __syncthreads();
       }
+      GVT_DOT(k0)
     }
   }
+#undef GVT_LOAD_W
+#undef GVT_DOT
 #pragma unroll
   for (int j = 0; j < NW; ++j)
 #pragma unroll
@@ -365,13 +443,32 @@ CFC_API int cfc_gemv(const void* x, const void* w, int M, int N, int K, int epi,
 }
 
 namespace {
+template <int NW, int MT, int WAVES, bool XN>
+void gemv_tile_go(dim3 grid, hipStream_t stream, const uint16_t* x, const uint16_t* wp, int N, int K, int split, int epi,
+                  float* yf, uint16_t* yb, int ldo, const GvNorm& nm) {
+  const size_t lds = XN ? (size_t)MT * K * 2 : 0;
+  if constexpr (XN) {
+    static bool raised = false;                    // dynamic LDS past 64 KB (Llama-70B rows at M = 4)
+    if (!raised) {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&gemv_tile_kernel<NW, MT, WAVES, XN>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+      raised = true;
+    }
+  }
+  gemv_tile_kernel<NW, MT, WAVES, XN><<<grid, 64 * WAVES, lds, stream>>>(x, wp, N, K, split, epi, yf, yb, ldo, nm);
+}
+
 template <int NW, int MT>
 void gemv_tile_launch(dim3 grid, int waves, hipStream_t stream, const uint16_t* x, const uint16_t* wp, int N, int K,
-                      int split, int epi, float* yf, uint16_t* yb, int ldo) {
-  if (waves == 4) gemv_tile_kernel<NW, MT, 4><<<grid, 256, 0, stream>>>(x, wp, N, K, split, epi, yf, yb, ldo);
-  else if (waves == 8) gemv_tile_kernel<NW, MT, 8><<<grid, 512, 0, stream>>>(x, wp, N, K, split, epi, yf, yb, ldo);
-  else if constexpr (MT == 1)   // 16 waves: 4 per SIMD, so <= 128 VGPRs -- single-row only
-    gemv_tile_kernel<NW, MT, 16><<<grid, 1024, 0, stream>>>(x, wp, N, K, split, epi, yf, yb, ldo);
+                      int split, int epi, float* yf, uint16_t* yb, int ldo, const GvNorm& nm) {
+  const bool xn = nm.part != nullptr;
+#define GVT(WV)                                                                                    \
+  if (xn) gemv_tile_go<NW, MT, WV, true>(grid, stream, x, wp, N, K, split, epi, yf, yb, ldo, nm);  \
+  else gemv_tile_go<NW, MT, WV, false>(grid, stream, x, wp, N, K, split, epi, yf, yb, ldo, nm);
+  if (waves == 4) { GVT(4) }
+  else if (waves == 8) { GVT(8) }
+  else if constexpr (MT == 1) { GVT(16) }         // 16 waves: 4 per SIMD, so <= 128 VGPRs -- single-row only
+#undef GVT
 }
 }  // namespace
 
@@ -379,13 +476,18 @@ void gemv_tile_launch(dim3 grid, int waves, hipStream_t stream, const uint16_t* 
 // epilogues as cfc_gemv; split > 1 (fp32 only): yf = slabs [split, M, N] of the k-slice partial
 // sums.  N % (16 nw) == 0, K % 32 == 0, 1 <= split <= K / 32.
 CFC_API int cfc_gemv_packed(const void* x, const void* wp, int M, int N, int K, int nw, int epi, float* yf, void* yb,
-                            int ldo, int split, int waves, hipStream_t stream) {
+                            int ldo, int split, int waves, const float* xpart, int xsplit, const void* res_in,
+                            void* res_out, const void* norm_w, float eps, hipStream_t stream) {
   if (M < 1 || M > 4 || N <= 0 || nw <= 0 || N % (16 * nw) || K <= 0 || K % 32) return -1;
   if ((epi == GV_F32 && !yf) || (epi != GV_F32 && !yb) || epi < 0 || epi > 2) return -2;
   if (split < 1 || split > K / 32 || (split > 1 && epi != GV_F32)) return -4;
   if (waves != 4 && waves != 8 && !(waves == 16 && M == 1)) return -5;
+  // the fused-norm prologue holds the first step's weights across the slab sums: <= 8 waves (VGPRs)
+  if (xpart ? (xsplit < 1 || !res_in || !res_out || !norm_w || res_in == res_out || K > 8192 || waves > 8) : !x)
+    return -6;
+  const GvNorm nm{xpart, xsplit, (const uint16_t*)res_in, (uint16_t*)res_out, (const uint16_t*)norm_w, eps};
   const dim3 grid((N / (16 * nw)) * split);
-#define GVP_ARGS (const uint16_t*)x, (const uint16_t*)wp, N, K, split, epi, yf, (uint16_t*)yb, ldo
+#define GVP_ARGS (const uint16_t*)x, (const uint16_t*)wp, N, K, split, epi, yf, (uint16_t*)yb, ldo, nm
 #define GVP_CASE(NW)                                                                         \
   case NW:                                                                                   \
     switch (M) {                                                                             \

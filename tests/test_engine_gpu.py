@@ -272,3 +272,20 @@ def test_prefill_beside_decode_on_cu_partitions_matches_generate():
         jb = fut.result()
     got_b = eng.finish(jb).tokens
     assert got_a == want_a and got_b == want_b
+
+
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_single_stream_fused_norm_decode_bit_identical(use_graph):
+    """B <= 4 decode over packed weights with the residual + RMSNorm reduces folded into the next
+    GEMV (K.gemv_norm, two buffers alternating) == the unfused reduce-then-GEMV path, token for token."""
+    cfg = get_config("small")
+    w = DecoderWeights.random(cfg, "cuda", seed=23)
+    m = DecoderModel(w)
+    assert m.w.packed_only
+    prompts = [[1] + list(range(40, 140)), [1, 5, 9] * 30, [1] + list(range(900, 960))]
+    toks = []
+    for fused in (True, False):
+        m.gemv_norm_fused = fused
+        kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, "cuda")
+        toks.append(LLMEngine(m, kv, use_graph=use_graph).generate(prompts, 24, ignore_eos=True).tokens)
+    assert toks[0] == toks[1]

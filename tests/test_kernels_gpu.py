@@ -585,6 +585,34 @@ def test_gemv_packed_slabs(split, M, waves):
     torch.testing.assert_close(o1.float(), o2.float(), rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("N,Kd,bn,s_in", [(896, 5120, 112, 6), (768, 1024, 128, 1), (1536, 2048, 96, 8)])
+def test_gemv_norm_equals_reduce_then_gemv(M, N, Kd, bn, s_in):
+    """The residual + RMSNorm folded into the packed GEMV's prologue == splitk_residual_rmsnorm then
+    the GEMV, bit for bit: the new residual, the slabs (split 1 and > 1) and the bf16 / SwiGLU
+    epilogues; res_in is left untouched."""
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + N)
+    part = torch.randn(s_in, M, Kd, device=DEV, generator=g)
+    res = torch.randn(M, Kd, device=DEV, generator=g).bfloat16()
+    norm = (torch.rand(Kd, device=DEV, generator=g) + 0.5).bfloat16()
+    w = ((torch.rand(N, Kd, device=DEV, generator=g) * 2 - 1) / Kd ** 0.5).bfloat16()
+    pw = K.pack_dgemm_weight(w, bn=bn)
+    r1 = res.clone()
+    x = K.splitk_residual_rmsnorm(part, r1, norm, 1e-5)
+    for waves in (4, 8):
+        for split in (1, 3):
+            r_in, r_out = res.clone(), torch.empty_like(res)
+            got = K.gemv_norm(part, r_in, r_out, norm, 1e-5, pw, split=split, waves=waves).clone()
+            assert torch.equal(r_out, r1) and torch.equal(r_in, res)
+            assert torch.equal(got, K.gemv_part(x, pw, split, waves))
+        for epi in ("bf16", "swiglu"):
+            r_in, r_out = res.clone(), torch.empty_like(res)
+            got = K.gemv_norm(part, r_in, r_out, norm, 1e-5, pw, epi, waves=waves)
+            assert torch.equal(got, K.gemv(x, pw, epi, waves=waves)) and torch.equal(r_out, r1)
+    with pytest.raises(ValueError):
+        K.gemv_norm(part, res, res, norm, 1e-5, pw)
+
+
 @pytest.mark.parametrize("split", [1, 3, 4])
 def test_rope_kv_write_from_splitk_slabs_matches_reduce_then_rope(split):
     """rope_kv_write_part == splitk_reduce -> rope_kv_write, bit for bit (q, K cache, V cache)."""
