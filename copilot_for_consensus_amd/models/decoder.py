@@ -529,12 +529,24 @@ class DecoderModel:
         wt = pw if pw is not None else self.w.layers[i][name]
         if self.prefill_gemm == "hip" and x.is_cuda and x.is_contiguous() and (
                 epi != "swiglu" or self.w.gate_up_interleaved):
-            if x.shape[0] >= self.PGEMM_MIN_ROWS and K.pgemm_ok(x, wt):
+            dg = pw is not None and K.dgemm_ok(x, pw)
+            if (x.shape[0] >= self.PGEMM_MIN_ROWS and K.pgemm_ok(x, wt)
+                    and not (dg and self._dgemm_faster(x.shape[0], wt.shape[0], x.shape[1]))):
                 return K.pgemm(x, wt, epi, variant=self.pgemm_variant)
-            if pw is not None and K.dgemm_ok(x, pw):
+            if dg:
                 return K.dgemm_swiglu(x, pw) if epi == "swiglu" else K.dgemm_linear(x, pw)
         y = self._lin(i, name, x)
         return K.silu_mul(y, interleaved=self.w.gate_up_interleaved) if epi == "swiglu" else y
+
+    PGEMM_MIN_TILES = 96   # fewer 256 x 256 output tiles than this: the decode GEMM is as fast or faster
+
+    def _dgemm_faster(self, M: int, N: int, Kd: int) -> bool:
+        """A prompt chunk too short to fill the chip with pgemm's 256 x 256 tiles runs on the decode
+        GEMM (one W pass per 256-row tile, ~450-870 TF/s): measured crossover at ~96 tiles
+        (profiles/r04_prefill_small_m.jsonl, Mistral-7B packed weights): qkv at 1024 rows (96
+        tiles) 76 vs 79 us, o at 1024 (64) 71 vs 72, down at 1024 (64) 220 vs 150 and at 2048
+        (128) 244 vs 298.  A 512-token prompt: 70 -> 40 (qkv), 68 -> 33 (o), 211 -> 83 us (down)."""
+        return -(-M // 256) * -(-N // 256) < self.PGEMM_MIN_TILES
 
     def _all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         if self.w.tp_size > 1:

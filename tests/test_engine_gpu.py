@@ -223,6 +223,7 @@ def test_prefill_gemm_modes_match_reference_logits(mode, monkeypatch):
     monkeypatch.setenv("CFC_PREFILL_GEMM", mode)
     m = DecoderModel(w)
     m.PGEMM_MIN_ROWS = 64
+    m.PGEMM_MIN_TILES = 0           # tiny shapes: pgemm even where the decode GEMM would be faster
     assert m.prefill_gemm == mode
     prompts = [[1] + list(range(7, 7 + 150)), [1] + list(range(40, 40 + 130)), [1, 5, 9] * 20]
     calls = []
