@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-4 session-3 headline profile: one 128-thread batch, no latency probe, current defaults.
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+rm -rf gpurun_out/prof_r04c
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r04c -o run -- \
+  python bench.py --steps 1 --warmup 0 --latency-rate 0 > gpurun_out/prof_r04c_bench.log 2>&1; rc=$?
+tail -2 gpurun_out/prof_r04c_bench.log; [ $rc -eq 0 ] || exit $rc
+python scripts/prof_summary.py gpurun_out/prof_r04c gpurun_out/prof_r04c_summary.txt > /dev/null
+find gpurun_out/prof_r04c -name '*kernel_trace.csv' -delete
+head -36 gpurun_out/prof_r04c_summary.txt | cut -c1-200
