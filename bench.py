@@ -56,6 +56,10 @@ def parse_args(argv=None):
                     help="latency half of the metric: Poisson arrivals per second per GPU served by the continuous "
                          "engine after the timed throughput steps (0 = skip)")
     ap.add_argument("--latency-steps", type=int, default=2, help="batches of threads the latency probe replays")
+    ap.add_argument("--latency-low-rate", type=float, default=0.5,
+                    help="a second latency point at a light load (the reference's one-thread-at-a-time regime): "
+                         "Poisson arrivals per second per GPU (0 = skip)")
+    ap.add_argument("--latency-low-threads", type=int, default=12, help="threads the light-load probe serves")
     ap.add_argument("--pipeline", choices=["bench", "node"], default="bench",
                     help="bench: the stage code with a static LLM batch (headline); node: the real services "
                          "(Node, in-proc bus, continuous summarization engine), pipeline/node_bench.py")
@@ -93,7 +97,8 @@ def main(argv=None):
 
     probe_steps = list(range(args.warmup + args.steps, args.warmup + args.steps + args.latency_steps)) \
         if args.latency_rate > 0 and args.tp == 1 and not args.llm_only else []
-    pipe.prepare_sources(list(range(args.warmup + args.steps)) + probe_steps)
+    low_steps = [args.warmup + args.steps + args.latency_steps] if probe_steps and args.latency_low_rate > 0 else []
+    pipe.prepare_sources(list(range(args.warmup + args.steps)) + probe_steps + low_steps)
 
     def barrier():
         if world > 1:
@@ -158,6 +163,23 @@ def main(argv=None):
                        p50_s=round(statistics.median([p["p50_s"] for p in probe]), 3),
                        p95_s=round(max(p["p95_s"] for p in probe), 3),
                        throughput_threads_per_s=round(sum(p["throughput_threads_per_s"] for p in probe), 3))
+    latency_low = None
+    if low_steps:
+        # light load: a few threads, far apart -- the regime of the reference's published 3-4 s per thread
+        barrier()
+        low = pipe.latency_probe(low_steps, args.latency_low_rate, seed=args.seed + 7919 + 104729 * groups.dp_rank,
+                                 max_threads=args.latency_low_threads)
+        if world > 1:
+            parts = [None] * world
+            dist.all_gather_object(parts, low)
+            low = parts
+        else:
+            low = [low]
+        latency_low = dict(low[0])
+        latency_low.update(threads=sum(p["threads"] for p in low),
+                           p50_s=round(statistics.median([p["p50_s"] for p in low]), 3),
+                           p95_s=round(max(p["p95_s"] for p in low), 3),
+                           throughput_threads_per_s=round(sum(p["throughput_threads_per_s"] for p in low), 3))
     if rank == 0:
         out = {
             "metric": "end-to-end threads summarized/sec + p50 summary latency, Mistral-7B TP=1/8",
@@ -189,6 +211,7 @@ def main(argv=None):
             "p50_summary_latency_s": round(p50, 3) if p50 is not None else None,
             # latency half of the metric at a stated arrival rate below saturation (continuous engine)
             "latency_mode": latency,
+            "latency_mode_light": latency_low,
             "generated_tokens_per_s": round(gen_tokens / elapsed, 1),
             "prompt_tokens_per_s": round(prompt_tokens / elapsed, 1),
             "baseline_threads_per_s": round(BASELINE_THREADS_PER_S, 4),

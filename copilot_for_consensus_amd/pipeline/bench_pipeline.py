@@ -252,7 +252,8 @@ class BenchPipeline:
     def run_step(self, step: int) -> StepResult:
         return self.run_steps([step], overlap=False)[0]
 
-    def latency_probe(self, steps: list[int], rate_per_s: float, seed: int = 0, steps_per_sync: int = 16) -> dict:
+    def latency_probe(self, steps: list[int], rate_per_s: float, seed: int = 0, steps_per_sync: int = 16,
+                      max_threads: int | None = None) -> dict:
         """The latency half of the metric under load below saturation: the threads of ``steps``
         (prepared by the same RAG path as the throughput steps) arrive as a Poisson process of
         ``rate_per_s`` and are served by the continuous engine (runtime/continuous.py -- the
@@ -271,6 +272,8 @@ class BenchPipeline:
         if not prompts:
             return {}
         per_thread_prep = prep_s / len(prompts)
+        if max_threads is not None:
+            prompts = prompts[:max_threads]
         ce = ContinuousEngine(self.engine, max_slots=self.threads_per_step, max_new_cap=self.max_new,
                               max_prompt=max(len(x) for x in prompts), steps_per_sync=steps_per_sync, stop_ids=(),
                               min_admit=1, max_wait_s=0.05)

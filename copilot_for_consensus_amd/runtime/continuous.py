@@ -110,12 +110,19 @@ class ContinuousEngine:
         # completes one, so the slot is freed and refilled instead of decoding to its limit
         self.stop_strings = stop_strings
         self.stop_state = stop_strings.new_state(B, dev) if stop_strings is not None else None
-        self.part_blocks = engine._part_blocks(B, self.max_blocks)
-        P = -self.part_blocks
-        ws = B * self.model.w.heads * P * (self.model.cfg.head_dim + 2) if P > 1 else 1
+        # decode width: a burst runs the captured step over the first W slots only (admission takes
+        # the lowest free slot), W the smallest bucket holding every occupied slot -- one request
+        # alone decodes at B = 1 on the GEMV path, not as 1 live row of a 128-row batched GEMM
+        # (light load: 6.5 -> ~3.3 ms per token).  One graph, split-KV partitioning and attention
+        # workspace per width.
+        self.widths = sorted({w for w in (1, 2, 4, 8, 16, 32, 64) if w < B} | {B})
+        self._pb = {w: engine._part_blocks(w, self.max_blocks) for w in self.widths}
+        ws = max(w * self.model.w.heads * -pb * (self.model.cfg.head_dim + 2) if -pb > 1 else 1
+                 for w, pb in self._pb.items())
         self.workspace = torch.empty(max(1, ws), dtype=torch.float32, device=dev)
+        self.part_blocks = self._pb[B]
         self.use_graph = engine._graph_for(B, self.sampling)
-        self.graph = None
+        self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.queue: collections.deque[Request] = collections.deque()
         self.slot_req: list[Request | None] = [None] * B
         self.slot_tables: list[tuple[list[int], list[int]] | None] = [None] * B
@@ -316,13 +323,19 @@ class ContinuousEngine:
         self.admit_log.append((round(t + off, 3), len(take), round(min(sub) + off, 3), round(max(sub) + off, 3)))
         self.stats["admissions"] = self.stats.get("admissions", 0) + 1
 
-    def _decode_step(self) -> None:
-        hidden = self.model.forward_decode(self.ids, self.positions, self.slots, self.ctx_lens, self.block_tables,
-                                           self.kv, attn_workspace=self.workspace, part_blocks=self.part_blocks,
-                                           shared_blocks=self.shared)
-        self.engine._next_tokens(hidden, self.next_ids, self.sampling, self.seed, self.step_t)
-        K.decode_advance_cb(self.next_ids, self.tokens, self.gen, self.limit, self.ids, self.positions,
-                            self.ctx_lens, self.slots, self.block_tables, self.done, self.stop_t, self.stop_state)
+    def _width(self) -> int:
+        hi = max((s for s in range(self.B) if self.slot_req[s] is not None), default=0) + 1
+        return next(w for w in self.widths if w >= hi)
+
+    def _decode_step(self, W: int) -> None:
+        ss = self.stop_state.view(W) if self.stop_state is not None else None
+        hidden = self.model.forward_decode(self.ids[:W], self.positions[:W], self.slots[:W], self.ctx_lens[:W],
+                                           self.block_tables[:W], self.kv, attn_workspace=self.workspace,
+                                           part_blocks=self._pb[W], shared_blocks=self.shared)
+        self.engine._next_tokens(hidden, self.next_ids[:W], self.sampling, self.seed, self.step_t)
+        K.decode_advance_cb(self.next_ids[:W], self.tokens[:W], self.gen[:W], self.limit[:W], self.ids[:W],
+                            self.positions[:W], self.ctx_lens[:W], self.slots[:W], self.block_tables[:W],
+                            self.done[:W], self.stop_t, ss)
         self.step_t.add_(1)
 
     def _state(self):
@@ -331,12 +344,13 @@ class ContinuousEngine:
                 self.next_ids, self.step_t] + extra
 
     def _burst(self, n: int) -> None:
-        if self.use_graph and self.graph is None:
+        W = self._width()          # no admission inside a burst: the occupied slots only shrink
+        if self.use_graph and W not in self.graphs:
             saved = [t.clone() for t in self._state()]
             s = torch.cuda.Stream(device=self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(s):
-                self._decode_step()        # warm-up (workspaces, library handles) outside capture
+                self._decode_step(W)       # warm-up (workspaces, library handles) outside capture
             torch.cuda.current_stream(self.device).wait_stream(s)
             for t, v in zip(self._state(), saved):
                 t.copy_(v)
@@ -344,16 +358,18 @@ class ContinuousEngine:
             # thread_local: other service threads keep launching / syncing their own streams while
             # this step is captured (global mode would invalidate the capture)
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                self._decode_step()
+                self._decode_step(W)
             for t, v in zip(self._state(), saved):
                 t.copy_(v)
-            self.graph = g
+            self.graphs[W] = g
+        g = self.graphs.get(W)
         for _ in range(n):
-            if self.graph is not None:
-                self.graph.replay()
+            if g is not None:
+                g.replay()
             else:
-                self._decode_step()
+                self._decode_step(W)
         self.stats["steps"] += n
+        self.stats["width_steps"] = self.stats.get("width_steps", 0) + n * W
 
     def _harvest(self) -> list[Request]:
         done = self.done.cpu().numpy()
@@ -390,3 +406,4 @@ class ContinuousEngine:
         self.slot_tables[s] = None
         self.slot_req[s] = None
         self.free.append(s)
+        self.free.sort(reverse=True)     # pop() takes the lowest free slot: the decode width stays small

@@ -18,6 +18,8 @@ reference of the same automaton (the CPU path, the prefill's first token, and th
 """
 from __future__ import annotations
 
+import copy
+
 import numpy as np
 import torch
 
@@ -139,6 +141,12 @@ class StopState:
         kp = torch.full((len(idx),), self.cap, dtype=torch.int32) if keep is None else \
             torch.as_tensor(keep, dtype=torch.int32)
         self.keep.index_copy_(0, it, kp.to(self.win.device))
+
+    def view(self, W: int) -> "StopState":
+        """The same state restricted to the first W slots (row views of the same buffers)."""
+        v = copy.copy(self)
+        v.win, v.wlen, v.keep = self.win[:W], self.wlen[:W], self.keep[:W]
+        return v
 
     def kernel_args(self) -> dict:
         t = self.tables

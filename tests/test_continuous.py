@@ -191,3 +191,26 @@ def test_raising_done_callback_is_not_called_twice():
     time.sleep(0.2)
     s.stop_continuous()
     assert seen == [(True, None)], seen
+
+
+def test_decode_width_follows_the_occupied_slots_cpu():
+    """A burst decodes only the first W slots (W the smallest width bucket holding every occupied
+    slot; admission takes the lowest free slot): one request alone runs at width 1, tokens still
+    equal generate(), and a freed low slot is refilled before a higher one."""
+    model, kv = _setup("cpu")
+    eng = LLMEngine(model, kv, max_prefill_tokens=128, use_graph=False)
+    ce = ContinuousEngine(eng, max_slots=16, max_new_cap=24, max_prompt=256, steps_per_sync=4)
+    assert ce.widths == [1, 2, 4, 8, 16]
+    p = [1] + list(range(30, 90))
+    r = ce.submit(p, 9)
+    ce.run()
+    assert ce.stats["width_steps"] == ce.stats["steps"]          # width 1 throughout
+    assert r.tokens == eng.generate([p], 9, ignore_eos=True).tokens[0]
+    a, b, c = ce.submit(p, 20), ce.submit([1, 7, 7, 3] * 9, 2), ce.submit([1] + list(range(5, 25)), 20)
+    ce.step()                                      # b (2 tokens) finishes in this burst: slot 1 free
+    assert (a.slot, c.slot) == (0, 2) and b.finished_s is not None and ce._width() == 4
+    d = ce.submit([1, 9] * 12, 20)
+    ce.step()
+    assert d.slot == 1
+    ce.run()
+    ce.close()
