@@ -56,6 +56,29 @@ __device__ __forceinline__ float pg_gelu(float v) { return 0.5f * v * (1.f + erf
 
 __device__ __forceinline__ float pg_bfr(float v) { return bf2f(f2bf(v)); }
 
+// SwiGLU of one 4-value accumulator group (16-row n-tile = 8 gate rows then 8 up rows: lane groups
+// g = 0, 1 hold gate columns, g = 2, 3 the matching up columns).  Both lane halves share the math:
+// after swapping values with lane ^ 32, lanes g < 2 compute elements 0, 1 and lanes g >= 2 elements
+// 2, 3 of the same (gate, up) pairs, and one more swap brings the packed pair back -- the exp and
+// the IEEE division are the epilogue's VALU cost, and the first version left half the lanes idle
+// (gate_up 1.32 vs 1.45 PF/s with the bf16 epilogue).  Same values and rounding as before: bf16 of
+// gate and up, silu(g) * u in fp32.  Returns (y0 y1, y2 y3) packed bf16 -- valid in lanes g < 2.
+__device__ __forceinline__ uint2 pg_swiglu4(const float (&v)[4], int g) {
+  float u[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) u[e] = __shfl_xor(v[e], 32, 64);
+  const bool lo = g < 2;
+  float y[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float gate = lo ? v[k] : u[2 + k], up = lo ? u[k] : v[2 + k];
+    const float gg = pg_bfr(gate);
+    y[k] = gg * __builtin_amdgcn_rcpf(1.f + __expf(-gg)) * pg_bfr(up);
+  }
+  const uint32_t mine = pack2bf(y[0], y[1]);
+  return make_uint2(mine, (uint32_t)__shfl_xor((int)mine, 32, 64));
+}
+
 // Epilogue of every kernel here: lane holds rows m = mw + 16 i + (lane & 15), columns
 // n = nw + 16 j + 4 (lane >> 4) + 0..3 of the wave's 128 x 16 NJ block.
 template <int EPI, int NJ>
@@ -72,21 +95,9 @@ __device__ __forceinline__ void pg_epilogue(const f32x4_t (&acc)[8][NJ], const u
       const int n = nb + 4 * g;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if constexpr (EPI == PG_SWIGLU) {
-        // 16-row n-tile = 8 gate rows then 8 up rows: groups 0,1 hold gate cols 0..7, groups 2,3
-        // the matching up cols; bf16 rounding of g and u as the unfused GEMM -> silu_mul path
-        float u[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) u[e] = __shfl_xor(v[e], 32, 64);
-        if (g < 2 && m < M && nb < N) {
-          float y[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float gg = pg_bfr(v[e]);
-            y[e] = gg / (1.f + __expf(-gg)) * pg_bfr(u[e]);
-          }
-          *reinterpret_cast<uint2*>(out + (size_t)m * ldo + nb / 2 + 4 * g) =
-              make_uint2(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]));
-        }
+        // bf16 rounding of g and u as the unfused GEMM -> silu_mul path
+        const uint2 y = pg_swiglu4(v, g);
+        if (g < 2 && m < M && nb < N) *reinterpret_cast<uint2*>(out + (size_t)m * ldo + nb / 2 + 4 * g) = y;
       } else {
         if (m < M && n < N) {
           if constexpr (EPI == PG_BIAS || EPI == PG_BIAS_GELU) {
@@ -128,20 +139,11 @@ __device__ __forceinline__ void pg_epilogue_staged(const f32x4_t (&acc)[8][4], u
     for (int j = 0; j < 4; ++j) {
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if constexpr (EPI == PG_SWIGLU) {
-        float u[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) u[e] = __shfl_xor(v[e], 32, 64);
+        const uint2 y = pg_swiglu4(v, g);
         if (g < 2) {
-          float y[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float gg = pg_bfr(v[e]);
-            y[e] = gg / (1.f + __expf(-gg)) * pg_bfr(u[e]);
-          }
           // output columns 8 j + 4 g .. +3: unit j, half g
           const int unit = j ^ (r & (UPR - 1));
-          *reinterpret_cast<uint2*>(region + r * RB + unit * 16 + g * 8) =
-              make_uint2(pack2bf(y[0], y[1]), pack2bf(y[2], y[3]));
+          *reinterpret_cast<uint2*>(region + r * RB + unit * 16 + g * 8) = y;
         }
       } else {
         // columns 16 j + 4 g .. +3: unit 2 j + (g >> 1), half g & 1
@@ -639,7 +641,9 @@ __global__ void __launch_bounds__(512, 1)
   // STG (PF & 64): the bf16 / SwiGLU outputs leave through LDS as whole row segments.  After this
   // wave's last barrier of the loop no wave reads LDS any more (the lagging group's last reads were
   // retired before it) and every DMA landed, so each wave may use its own 16-KB slice.
-  constexpr bool STG = (PF & 64) != 0 && (EPI == PG_BF16 || EPI == PG_SWIGLU);
+  // staged stores for the bf16 epilogue; SwiGLU (half the columns, 8-byte pieces) measured 0.7 %
+  // faster with the direct stores once its math was spread over both lane halves
+  constexpr bool STG = (PF & 64) != 0 && EPI == PG_BF16;
   if constexpr (STG)
     pg_epilogue_staged<EPI>(acc, out, M, N, ldo, m0 + grp * 128, n0 + wc * 64, smem + w * 16384);
   else
