@@ -170,6 +170,47 @@ __device__ __forceinline__ void qkv_load8(const uint16_t* qkv, const float* part
   f[4] = bf2f(f2bf(b.x)); f[5] = bf2f(f2bf(b.y)); f[6] = bf2f(f2bf(b.z)); f[7] = bf2f(f2bf(b.w));
 }
 
+// qkv_load8 of two offsets with every load of both in flight at once (4 slabs of each per round):
+// the two halves a RoPE rotation pairs no longer wait one slab round trip after the other
+// (rope_kv_kernel at B = 128 decode, split 4: 11.2 us in the step).  Same sums, same order.
+__device__ __forceinline__ void qkv_load8x2(const uint16_t* qkv, const float* part, int split, size_t slab,
+                                            size_t off_a, size_t off_b, float* fa, float* fb) {
+  if (part == nullptr) {
+    const uint4 ua = *reinterpret_cast<const uint4*>(qkv + off_a), ub = *reinterpret_cast<const uint4*>(qkv + off_b);
+    unpack8(ua, fa);
+    unpack8(ub, fb);
+    return;
+  }
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, b0 = a0, b1 = a0;
+  for (int p0 = 0; p0 < split; p0 += 4) {
+    float4 x[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t o = (size_t)min(p0 + u, split - 1) * slab;
+      x[u][0] = *reinterpret_cast<const float4*>(part + o + off_a);
+      x[u][1] = *reinterpret_cast<const float4*>(part + o + off_a + 4);
+      x[u][2] = *reinterpret_cast<const float4*>(part + o + off_b);
+      x[u][3] = *reinterpret_cast<const float4*>(part + o + off_b + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (p0 + u < split) {
+        a0.x += x[u][0].x; a0.y += x[u][0].y; a0.z += x[u][0].z; a0.w += x[u][0].w;
+        a1.x += x[u][1].x; a1.y += x[u][1].y; a1.z += x[u][1].z; a1.w += x[u][1].w;
+        b0.x += x[u][2].x; b0.y += x[u][2].y; b0.z += x[u][2].z; b0.w += x[u][2].w;
+        b1.x += x[u][3].x; b1.y += x[u][3].y; b1.z += x[u][3].z; b1.w += x[u][3].w;
+      }
+    }
+  }
+  const float sa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+  const float sb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    fa[j] = bf2f(f2bf(sa[j]));
+    fb[j] = bf2f(f2bf(sb[j]));
+  }
+}
+
 // Rotate-half RoPE of the c-th 8-vector of each half of one head (head row at element offset
 // `head_off`); cs = cos_sin + position * half * 2 (cos, sin interleaved).  pa / pb: bf16 results
 // for [c*8, c*8+8) and [half + c*8, ...).
@@ -183,8 +224,7 @@ __device__ __forceinline__ void rope_rot8(const uint16_t* qkv, const float* part
     csv[4 * j] = t.x; csv[4 * j + 1] = t.y; csv[4 * j + 2] = t.z; csv[4 * j + 3] = t.w;
   }
   float a[8], b[8], ra[8], rb[8];
-  qkv_load8(qkv, part, split, slab, head_off + c * 8, a);
-  qkv_load8(qkv, part, split, slab, head_off + half + c * 8, b);
+  qkv_load8x2(qkv, part, split, slab, head_off + c * 8, head_off + half + c * 8, a, b);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float cv = csv[2 * j], sv = csv[2 * j + 1];
