@@ -166,9 +166,11 @@ class BenchPipeline:
                 with span(f"bench.llm.step{step}"):
                     res = self.engine.generate(prompts, self.max_new, temperature=0.0, ignore_eos=True)
                 self._last_gen_s = time.perf_counter() - tg
-                self._last_prep_s = sum(v for k, v in stages.items())
+                self._last_prep_s = sum(v for k, v in stages.items() if k != "wait_prep")
                 stages["prefill"] = res.prefill_s
                 stages["decode"] = res.decode_s
+                # engine time outside its prefill / decode windows (setup, first-token sync, harvest)
+                stages["llm_other"] = self._last_gen_s - res.prefill_s - res.decode_s
                 t2 = time.perf_counter()
                 if ctx is not None:
                     self.rag.finish(ctx, res)
@@ -180,10 +182,13 @@ class BenchPipeline:
                                           sum(res.prompt_lens), stages))
                 if on_step is not None:   # progress report (host-side print, no device sync)
                     on_step(n, results[-1])
+                tw = time.perf_counter()
                 if fut is not None:
                     pending = fut.result()
                 elif n + 1 < len(steps):
                     pending = self._prepare(steps[n + 1])
+                if n + 1 < len(steps):       # the next batch's preparation not hidden behind this one
+                    pending[3]["wait_prep"] = time.perf_counter() - tw
         finally:
             if pool:
                 pool.shutdown(wait=True)
