@@ -666,7 +666,6 @@ GEMV_MAX_M = 4   # decode batches up to this size take the weight-streaming GEMV
 
 
 GEMV_TILE_CUS = 256      # the packed GEMV's slab form aims at one workgroup per CU
-GEMV_NORM_WAVES = 8      # fused-norm GEMV at M = 1 (4 measured slower)
 
 
 def gemv_packed_config(N: int, K: int, nw: int, M: int = 1, slab: bool = True) -> tuple[int, int]:
@@ -724,8 +723,9 @@ def gemv_norm(part: torch.Tensor, res_in: torch.Tensor, res_out: torch.Tensor, n
     slab = epi == "slabs"
     cs, cw = gemv_packed_config(N, Kd, w.bn // 16, M, slab=slab)
     split = (split or cs) if slab else 1
-    # the prologue's registers: 16-wave groups spill; at M > 1 so do 8-wave ones
-    waves = waves or min(cw, GEMV_NORM_WAVES if M == 1 else 4)
+    # the prologue's registers: 16-wave groups spill (<= 8 waves); otherwise the unfused GEMV's own
+    # wave count, so the slabs (and a split-1 epilogue at M > 1) match the unfused path bit for bit
+    waves = waves or min(cw, 8)
     if not part.is_cuda:      # splitk_residual_rmsnorm's CPU arithmetic
         x, r = ref.rmsnorm(part.sum(0).to(res_in.dtype), norm_w, eps, res_in)
         res_out.copy_(r)
