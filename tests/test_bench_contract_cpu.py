@@ -48,6 +48,10 @@ def _check(d, n, latency=True):
     lm = d["latency_mode"]
     assert lm["threads"] == 2 * 2 * n and lm["arrival_rate_per_gpu"] == 8.0
     assert 0 < lm["p50_s"] <= lm["p95_s"]
+    # and the light-load point (one step's threads per rank, far apart)
+    ll = d["latency_mode_light"]
+    assert ll["threads"] == 2 * n and ll["arrival_rate_per_gpu"] == 0.5
+    assert 0 < ll["p50_s"] <= ll["p95_s"]
 
 
 def test_bench_single_process_contract():
