@@ -347,7 +347,7 @@ class ContinuousEngine:
         W = self._width()          # no admission inside a burst: the occupied slots only shrink
         if self.use_graph and W not in self.graphs:
             saved = [t.clone() for t in self._state()]
-            s = torch.cuda.Stream(device=self.device)
+            s = self.engine.capture_stream()
             s.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(s):
                 self._decode_step(W)       # warm-up (workspaces, library handles) outside capture
@@ -357,7 +357,7 @@ class ContinuousEngine:
             g = torch.cuda.CUDAGraph()
             # thread_local: other service threads keep launching / syncing their own streams while
             # this step is captured (global mode would invalidate the capture)
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                 self._decode_step(W)
             for t, v in zip(self._state(), saved):
                 t.copy_(v)

@@ -245,9 +245,17 @@ class LLMEngine:
             self._states[key] = st
         return st
 
+    def capture_stream(self):
+        """One side stream per engine for every decode-graph warm-up AND capture: the split-K
+        workspaces are per stream (ops.kernels._workspace), so the warm-up sizes exactly the
+        buffers the capture then records, and captures do not mint a workspace per stream."""
+        if getattr(self, "_capture_s", None) is None:
+            self._capture_s = torch.cuda.Stream(device=self.device)
+        return self._capture_s
+
     def _capture(self, st, part_blocks, temperature, seed):
         saved = [t.clone() for t in st.tensors()]
-        s = torch.cuda.Stream(device=self.device)
+        s = self.capture_stream()
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             for _ in range(2):
@@ -256,7 +264,8 @@ class LLMEngine:
         for t, v in zip(st.tensors(), saved):
             t.copy_(v)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):   # other threads may use the GPU
+        # other threads may use the GPU (thread_local); captured on the warm-up's stream
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
             self._decode_step(st, part_blocks, temperature, seed)
         for t, v in zip(st.tensors(), saved):
             t.copy_(v)
