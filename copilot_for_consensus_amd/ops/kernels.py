@@ -691,8 +691,8 @@ def gemv_part(x: torch.Tensor, w: "PackedWeight", split: int | None = None, wave
     slab-reading RoPE / KV write and residual + RMSNorm reduce."""
     M, Kd = x.shape
     N = w.N
-    if not isinstance(w, PackedWeight) or w.K != Kd or not (1 <= M <= GEMV_MAX_M):
-        raise ValueError(f"gemv_part: x {tuple(x.shape)}, packed W [{N}, {w.K}] needed (M <= {GEMV_MAX_M})")
+    if not isinstance(w, PackedWeight) or w.K != Kd or not (1 <= M <= GEMV_MAX_M) or not x.is_contiguous():
+        raise ValueError(f"gemv_part: x {tuple(x.shape)}, packed W [{N}, {w.K}] needed (M <= {GEMV_MAX_M}, contiguous x)")
     cs, cw = gemv_packed_config(N, Kd, w.bn // 16, M)
     split, waves = split or cs, waves or cw
     if not x.is_cuda:
@@ -718,8 +718,11 @@ def gemv_norm(part: torch.Tensor, res_in: torch.Tensor, res_out: torch.Tensor, n
     epilogue.  One launch instead of the reduce kernel plus the GEMV (gemm.hip: gemv_tile_kernel)."""
     S_in, M, Kd = part.shape
     N = w.N
-    if not isinstance(w, PackedWeight) or w.K != Kd or not (1 <= M <= GEMV_MAX_M):
-        raise ValueError(f"gemv_norm: slabs {tuple(part.shape)}, packed W [{N}, {w.K}] needed (M <= {GEMV_MAX_M})")
+    if (not isinstance(w, PackedWeight) or w.K != Kd or not (1 <= M <= GEMV_MAX_M) or part.dtype != torch.float32
+            or not (part.is_contiguous() and res_in.is_contiguous() and res_out.is_contiguous())
+            or res_in.shape != (M, Kd) or res_out.shape != (M, Kd) or norm_w.numel() != Kd):
+        raise ValueError(f"gemv_norm: fp32 slabs {tuple(part.shape)}, residuals [{M}, {Kd}], packed W [{N}, {w.K}] "
+                         f"needed (M <= {GEMV_MAX_M}, contiguous)")
     slab = epi == "slabs"
     cs, cw = gemv_packed_config(N, Kd, w.bn // 16, M, slab=slab)
     split = (split or cs) if slab else 1
