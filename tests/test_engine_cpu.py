@@ -216,3 +216,35 @@ def test_pack_layout_fragment_order():
     for nb, kb, t, lane, j in [(0, 0, 0, 0, 0), (1, 2, 3, 63, 7), (0, 1, 2, 17, 5), (1, 0, 1, 40, 3)]:
         assert p[nb, kb, t, lane, j] == w[nb * bn + 16 * t + lane % 16, 32 * kb + 8 * (lane // 16) + j]
     assert torch.equal(R.unpack_dgemm_weight(p), w)
+
+
+def test_gemv_packed_config_fills_the_chip_and_keeps_whole_steps():
+    """The packed GEMV's (split, waves): slab form -> at most one workgroup per CU (tiles x split <=
+    256 unless one tile already exceeds it), every wave >= one whole step of U kg; in-kernel
+    epilogues take split 1 (16 waves only at M = 1)."""
+    from copilot_for_consensus_amd.ops import kernels as K
+    shapes = [(6144, 4096, 6), (4096, 4096, 4), (28672, 4096, 7), (4096, 14336, 8), (15360, 5120, 8),
+              (5120, 5120, 4), (27648, 5120, 8), (5120, 13824, 8), (768, 512, 8), (1024, 1536, 4)]
+    for N, Kd, nw in shapes:
+        tiles, kg = N // (16 * nw), Kd // 32
+        for M in (1, 2, 3, 4):
+            u = 2 if M > 2 else (3 if nw >= 7 else 4)
+            split, waves = K.gemv_packed_config(N, Kd, nw, M)
+            assert 1 <= split <= kg and waves in (4, 8)
+            assert tiles * split <= max(256, tiles)
+            assert split == 1 or kg // split >= waves * u
+            s1, w1 = K.gemv_packed_config(N, Kd, nw, M, slab=False)
+            assert s1 == 1 and w1 in ((4, 8, 16) if M == 1 else (4, 8))
+    # the measured points the rule was fitted to (profiles/r04_gemv_grid.jsonl)
+    assert K.gemv_packed_config(6144, 4096, 6) == (4, 8)
+    assert K.gemv_packed_config(4096, 14336, 8) == (8, 8)
+    assert K.gemv_packed_config(5120, 13824, 8) == (6, 8)
+
+
+def test_prefill_routes_short_chunks_to_the_decode_gemm():
+    """_dgemm_faster: fewer than 96 pgemm tiles -> the decode GEMM (profiles/r04_prefill_small_m.jsonl)."""
+    from copilot_for_consensus_amd.models.decoder import DecoderModel
+    m = DecoderModel.__new__(DecoderModel)
+    assert m._dgemm_faster(512, 6144, 4096) and m._dgemm_faster(1024, 4096, 14336)
+    assert not m._dgemm_faster(1024, 6144, 4096) and not m._dgemm_faster(16384, 4096, 4096)
+    assert not m._dgemm_faster(512, 28672, 4096)
