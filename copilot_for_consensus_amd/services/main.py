@@ -162,7 +162,9 @@ def _distributed() -> dict | None:
         worker = DPNodeWorker(store, groups.dp_rank, groups.dp_size, embedder, index, local)
         ctx.update(worker=worker, embedder=embedder)
         if serve:
-            vs, summ = build_rank0(store, groups.dp_size, worker)
+            # a rank whose heartbeat is older than this is taken for dead and its threads move
+            hb = float(os.environ.get("CFC_DP_HEARTBEAT_TIMEOUT", "10"))
+            vs, summ = build_rank0(store, groups.dp_size, worker, heartbeat_timeout=hb)
             ctx.update(vector_store=vs, summarizer=summ)
             worker.start(serve=False)
     return ctx

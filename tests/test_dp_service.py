@@ -135,6 +135,10 @@ def _dp_node_rank(rank, world, port, src_dir, n_threads, q, kill_rank=None):
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     if kill_rank is not None and rank == kill_rank:
         os.environ["MOCK_LATENCY_MS"] = "600000"            # never finishes a thread: killed holding work
+    if kill_rank is None:
+        # nothing is killed here: a rank stalled by a loaded CPU (parallel test workers) must not be
+        # taken for dead, which would move its threads and break the both-ranks-worked checks
+        os.environ["CFC_DP_HEARTBEAT_TIMEOUT"] = "120"
     try:
         from copilot_for_consensus_amd.services import main as M
         ctx = M._distributed()
