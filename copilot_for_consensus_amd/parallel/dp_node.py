@@ -14,12 +14,19 @@ data on its owner GPU:
 * every DP rank (rank 0 included) runs a :class:`DPNodeWorker`: its own encoder, its own HBM index
   shard (the thread's vectors never leave the GPU that embedded them) and its own LLM engine
   (continuous batching when the summarizer streams);
-* the control plane is the job's TCPStore (:class:`StoreRPC`): small JSON requests (chunk texts,
-  chunk ids, a query vector) and replies (counts, scores, summaries); no tensor crosses ranks;
+* the control plane is the job's TCPStore (:class:`StoreRPC`): small JSON requests (chunk ids, a
+  query vector) and replies (counts, scores, summaries); every request, reply and result key is
+  deleted once it is consumed, so rank 0's store stays bounded however long the node runs.  Each
+  rank serves two inboxes on two threads: ``bulk`` (encoder forwards, bulk inserts) and ``ctl``
+  (summary submits, relevance / topic reads), so a read never queues behind an embedding batch;
+* the data plane for chunk texts is a socket: rank 0 serves its document store
+  (storage/server.py) and an owner rank reads the texts of the chunk ids it was sent;
 * summaries stream: a thread is submitted to its owner's engine and its summary comes back through
   the owner's result stream; a rank whose heartbeat stops has its in-flight threads resubmitted to
-  a live rank (at-least-once processing, exactly-once results: rank 0 keeps the first summary of a
-  thread and drops late duplicates).
+  a live rank (at-least-once processing, exactly-once results: a result is matched to its request
+  key and a late duplicate of a resubmitted request is dropped).  Only a stale heartbeat marks a
+  rank dead -- a slow reply or a handler error does not -- and it is re-checked on every routing
+  decision, so a rank whose heartbeat resumes gets its threads back.
 
 Nothing here is a collective, so a dead rank cannot hang the others.
 """
@@ -27,6 +34,7 @@ from __future__ import annotations
 
 import dataclasses
 import json
+import os
 import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
@@ -38,6 +46,13 @@ from .resilience import Heartbeat, _get
 
 RPC_PREFIX = "dprpc/"
 SUM_PREFIX = "dpsum/"
+DATA_KEY = "dpnode/docstore"          # [host, port] of the chunk-text server rank 0 publishes
+# ops that run an encoder forward or move many rows: served from their own inbox
+BULK_OPS = frozenset({"embed_index", "add"})
+
+
+class RemoteError(RuntimeError):
+    """A DP rank's handler raised: the rank is alive, the request failed."""
 
 
 def _wait_key(store, key: str, timeout: float) -> bool:
@@ -55,46 +70,94 @@ def _wait_key(store, key: str, timeout: float) -> bool:
         nap = min(0.02, nap * 1.5)
 
 
-class StoreRPC:
-    """Request / reply over a key-value store.  ``call(rank, op, args)`` appends a request to
-    ``rank``'s inbox (``<prefix><rank>/req/<seq>``, seq from an atomic counter, so any thread of
-    any process may call) and waits for ``<prefix><rank>/res/<seq>``; :meth:`serve` executes a
-    rank's requests in order.  Calls to the caller's own rank run in place."""
+def _delete(store, key: str) -> bool:
+    try:
+        return bool(store.delete_key(key))
+    except Exception:  # noqa: BLE001 -- stores without delete / the store is gone
+        return False
 
-    def __init__(self, store, rank: int, prefix: str = RPC_PREFIX):
+
+class StoreRPC:
+    """Request / reply over a key-value store.  ``call(rank, op, args)`` appends a request to one of
+    ``rank``'s inboxes (``<prefix><rank>/<lane>/req/<seq>``, seq from an atomic counter, so any
+    thread of any process may call) and waits for ``.../res/<seq>``; :meth:`serve` executes one
+    inbox's requests in order.  Both keys are deleted once read (the server deletes the request,
+    the caller the reply; a reply that arrives after its caller timed out is deleted by that
+    caller's next call).  Calls to the caller's own rank run in place."""
+
+    LANES = ("ctl", "bulk")
+
+    def __init__(self, store, rank: int, prefix: str = RPC_PREFIX, skip_grace_s: float = 10.0):
         self.store, self.rank, self.prefix = store, int(rank), prefix
+        self.skip_grace_s = float(skip_grace_s)
         self.handlers: dict = {}
+        self.skipped = 0
+        self._abandoned: list[str] = []
+        self._alock = threading.Lock()
+
+    @staticmethod
+    def lane(op: str) -> str:
+        return "bulk" if op in BULK_OPS else "ctl"
+
+    def _base(self, rank: int, lane: str) -> str:
+        return f"{self.prefix}{rank}/{lane}/"
 
     def call(self, rank: int, op: str, args=None, timeout: float = 120.0):
         if rank == self.rank and op in self.handlers:
             return self.handlers[op](args)
-        seq = int(self.store.add(f"{self.prefix}{rank}/seq", 1))
-        self.store.set(f"{self.prefix}{rank}/req/{seq}", json.dumps([op, args]))
-        key = f"{self.prefix}{rank}/res/{seq}"
+        self._sweep()
+        base = self._base(rank, self.lane(op))
+        seq = int(self.store.add(base + "seq", 1))
+        self.store.set(f"{base}req/{seq}", json.dumps([op, args]))
+        key = f"{base}res/{seq}"
         if not _wait_key(self.store, key, timeout):
+            with self._alock:
+                self._abandoned.append(key)
             raise TimeoutError(f"DP rank {rank} did not answer {op!r} within {timeout:.0f}s")
         res = json.loads(self.store.get(key))
+        _delete(self.store, key)
         if not res.get("ok"):
-            raise RuntimeError(f"DP rank {rank} {op!r} failed: {res.get('err')}")
+            raise RemoteError(f"DP rank {rank} {op!r} failed: {res.get('err')}")
         return res.get("v")
 
-    def serve(self, stop: threading.Event, poll_s: float = 0.5) -> int:
-        """Run this rank's requests until ``stop`` is set; returns how many were served."""
-        seq, n = 0, 0
+    def _sweep(self) -> None:
+        """Delete the replies of timed-out calls that have arrived since (bounded list)."""
+        with self._alock:
+            if not self._abandoned:
+                return
+            self._abandoned = [k for k in self._abandoned if not _delete(self.store, k)][-1024:]
+
+    def serve(self, stop: threading.Event, poll_s: float = 0.5, lane: str = "ctl") -> int:
+        """Run this rank's ``lane`` inbox until ``stop`` is set; returns how many were served.  A
+        sequence number whose request never appears (its caller died between reserving it and
+        writing it) is skipped once a later request exists and ``skip_grace_s`` has passed."""
+        base = self._base(self.rank, lane)
+        seq, n, missing_since = 0, 0, None
         while not stop.is_set():
-            key = f"{self.prefix}{self.rank}/req/{seq + 1}"
+            key = f"{base}req/{seq + 1}"
             try:
                 if not _wait_key(self.store, key, poll_s):
+                    if int(self.store.add(base + "seq", 0)) > seq + 1:
+                        now = time.monotonic()
+                        missing_since = missing_since or now
+                        if now - missing_since >= self.skip_grace_s:
+                            seq, missing_since = seq + 1, None
+                            self.skipped += 1
                     continue
+                raw = self.store.get(key)
             except Exception:  # noqa: BLE001 -- the store (rank 0's TCPStore) is gone: the job ended
                 return n
-            seq += 1
-            op, args = json.loads(self.store.get(key))
+            seq, missing_since = seq + 1, None
+            _delete(self.store, key)
+            op, args = json.loads(raw)
             try:
                 res = {"ok": True, "v": self.handlers[op](args)}
             except Exception as e:  # noqa: BLE001 -- reported to the caller
                 res = {"ok": False, "err": f"{type(e).__name__}: {e}"}
-            self.store.set(f"{self.prefix}{self.rank}/res/{seq}", json.dumps(res))
+            try:
+                self.store.set(f"{base}res/{seq}", json.dumps(res))
+            except Exception:  # noqa: BLE001
+                return n
             n += 1
         return n
 
@@ -114,6 +177,18 @@ def _summary_from_json(d: dict) -> Summary:
     return Summary(**d)
 
 
+def _store_texts(store):
+    """ids -> texts of those chunks, read from a document store (one $in query)."""
+    def texts(ids: list[str]) -> list[str]:
+        docs = store.query_documents("chunks", {"_id": {"$in": list(ids)}}, limit=max(1, len(ids)))
+        by = {d["_id"]: d.get("text", "") for d in docs}
+        missing = [i for i in ids if i not in by]
+        if missing:
+            raise KeyError(f"{len(missing)} chunk(s) not in the document store, e.g. {missing[0]!r}")
+        return [by[i] for i in ids]
+    return texts
+
+
 class DPNodeWorker:
     """One DP rank's model side: encoder, HBM index shard, summarizer, served over :class:`StoreRPC`.
     Rank 0 runs one too (its handlers are called in place)."""
@@ -125,15 +200,20 @@ class DPNodeWorker:
         self.rpc = StoreRPC(store, self.rank)
         self.rpc.handlers.update({
             "embed_index": self._embed_index, "add": self._add, "centroid": self._centroid, "query": self._query,
-            "delete": self._delete, "count": self._count, "get": self._get, "info": self._info,
-            "sum_submit": self._sum_submit})
+            "delete": self._delete, "clear": self._clear, "count": self._count, "get": self._get,
+            "info": self._info, "sum_submit": self._sum_submit})
         self.hb = Heartbeat(_PrefixedStore(store, SUM_PREFIX), self.rank, interval=heartbeat_interval)
         self._out_seq = 0
         self._out_lock = threading.Lock()
+        # index reads (ctl inbox) and writes (bulk inbox) run on different threads
+        self._index_lock = threading.RLock()
+        # ids -> chunk texts: rank 0's document store (attached) or its socket server (lazy)
+        self.text_source = None
+        self._text_lock = threading.Lock()
         self._pool: ThreadPoolExecutor | None = None
         self.stats = {"embedded": 0, "summaries": 0, "queries": 0}
         self._stop = threading.Event()
-        self._server: threading.Thread | None = None
+        self._servers: list[threading.Thread] = []
 
     # ---------------------------------------------------------------- lifecycle
     def start(self, serve: bool = True) -> "DPNodeWorker":
@@ -144,15 +224,17 @@ class DPNodeWorker:
         else:
             self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"dp{self.rank}-sum")
         if serve:
-            self._server = threading.Thread(target=self.rpc.serve, args=(self._stop,), name=f"dp{self.rank}-rpc",
-                                            daemon=True)
-            self._server.start()
+            for lane in StoreRPC.LANES:
+                t = threading.Thread(target=self.rpc.serve, args=(self._stop,), kwargs={"lane": lane},
+                                     name=f"dp{self.rank}-rpc-{lane}", daemon=True)
+                t.start()
+                self._servers.append(t)
         return self
 
     def stop(self) -> None:
         self._stop.set()
-        if self._server is not None:
-            self._server.join(timeout=5)
+        for t in self._servers:
+            t.join(timeout=5)
         stop = getattr(self.summarizer, "stop_continuous", None)
         if callable(stop):
             stop()
@@ -165,7 +247,7 @@ class DPNodeWorker:
         self.start()
         try:
             while _get(self.store, f"{SUM_PREFIX}shutdown") is None:
-                if self._server is not None and not self._server.is_alive():
+                if self._servers and not all(t.is_alive() for t in self._servers):
                     break
                 time.sleep(poll_s)
         finally:
@@ -173,46 +255,74 @@ class DPNodeWorker:
         return dict(self.stats)
 
     # ---------------------------------------------------------------- index / encoder
+    def _texts(self, ids: list[str]) -> list[str]:
+        with self._text_lock:
+            if self.text_source is None:
+                addr = _get(self.store, DATA_KEY)
+                if addr is None:
+                    raise RuntimeError("no chunk-text server published (DPNodeVectorStore.attach_document_store)")
+                from ..storage.server import RemoteDocumentStore
+                host, port = json.loads(addr)
+                rs = RemoteDocumentStore(host, int(port))
+                rs.connect()
+                self.text_source = _store_texts(rs)
+        return self.text_source(ids)
+
     def _embed_index(self, args):
-        chunks = args["chunks"]
-        vecs = self.embedder.embed_tensor([c["text"] for c in chunks])
-        self.index.add_embeddings([c["id"] for c in chunks], vecs, [c["meta"] for c in chunks])
+        ids = [c["id"] for c in args["chunks"]] if "chunks" in args else list(args["ids"])
+        texts = [c["text"] for c in args["chunks"]] if "chunks" in args else self._texts(ids)
+        metas = [c["meta"] for c in args["chunks"]] if "chunks" in args else list(args["metas"])
+        vecs = self.embedder.embed_tensor(texts)           # the encoder forward runs outside the index lock
+        with self._index_lock:
+            self.index.add_embeddings(ids, vecs, metas)
         if getattr(vecs, "is_cuda", False):
             import torch
             torch.cuda.current_stream(vecs.device).synchronize()   # rows in HBM before the reply
-        self.stats["embedded"] += len(chunks)
-        return len(chunks)
+        self.stats["embedded"] += len(ids)
+        return len(ids)
 
     def _add(self, args):
-        self.index.add_embeddings(args["ids"], args["vectors"], args["metas"])
+        with self._index_lock:
+            self.index.add_embeddings(args["ids"], args["vectors"], args["metas"])
         return len(args["ids"])
 
     def _centroid(self, args):
-        return self.index.centroid_scores(args["ids"])
+        with self._index_lock:
+            return self.index.centroid_scores(args["ids"])
 
     def _query(self, args):
         self.stats["queries"] += 1
-        res = self.index.query(args["vector"], int(args["k"]))
+        with self._index_lock:
+            res = self.index.query(args["vector"], int(args["k"]))
         return [[r.id, float(r.score), r.metadata] for r in res]
 
     def _delete(self, args):
         n = 0
-        for i in args["ids"]:
-            try:
-                self.index.delete(i)
-                n += 1
-            except KeyError:
-                pass
+        with self._index_lock:
+            for i in args["ids"]:
+                try:
+                    self.index.delete(i)
+                    n += 1
+                except KeyError:
+                    pass
+        return n
+
+    def _clear(self, _):
+        with self._index_lock:
+            n = int(self.index.count())
+            self.index.clear()
         return n
 
     def _count(self, _):
-        return int(self.index.count())
+        with self._index_lock:
+            return int(self.index.count())
 
     def _get(self, args):
-        try:
-            r = self.index.get(args["id"])
-        except KeyError:
-            return None
+        with self._index_lock:
+            try:
+                r = self.index.get(args["id"])
+            except KeyError:
+                return None
         return [r.id, float(r.score), list(map(float, r.vector)), r.metadata]
 
     def _info(self, _):
@@ -265,22 +375,24 @@ class _PrefixedStore:
 
 
 class _Router:
-    """Rank 0's view of the DP ranks: owner of a thread among the live ones."""
+    """Rank 0's view of the DP ranks: owner of a thread among the live ones.  A rank is live while
+    its heartbeat is fresh -- re-read on every decision (cached ``cache_s``), never latched, so a
+    rank that only answered slowly, or whose handler failed, keeps its threads and shard."""
 
-    def __init__(self, store, world: int, timeout: float):
-        self.store, self.world, self.timeout = store, int(world), float(timeout)
-        self.dead: set[int] = set()
+    def __init__(self, store, world: int, timeout: float, cache_s: float = 0.25):
+        self.store, self.world, self.timeout, self.cache_s = store, int(world), float(timeout), float(cache_s)
+        self._seen: dict[int, tuple[float, bool]] = {}
 
     def alive(self, rank: int) -> bool:
-        if rank in self.dead:
-            return False
+        now = time.monotonic()
+        c = self._seen.get(rank)
+        if c is not None and now - c[0] < self.cache_s:
+            return c[1]
         v = _get(self.store, f"{SUM_PREFIX}hb/{rank}")
-        if v is None:
-            return True                           # not started yet: give it the benefit of the doubt
-        if time.time() - json.loads(v)["t"] > self.timeout:
-            self.dead.add(rank)
-            return False
-        return True
+        # not started yet: give it the benefit of the doubt
+        ok = v is None or time.time() - json.loads(v)["t"] <= self.timeout
+        self._seen[rank] = (now, ok)
+        return ok
 
     def owner(self, thread_id: str) -> int:
         r = owner_of(thread_id, self.world)
@@ -304,32 +416,63 @@ class DPNodeVectorStore(VectorStore):
         self.w, self.router = worker, router
         self.rpc = worker.rpc
         self.dim = int(getattr(worker.index, "dim", 0) or 0)
-        self._pool = ThreadPoolExecutor(max_workers=max(2, router.world), thread_name_prefix="dpvs")
+        self._pool = ThreadPoolExecutor(max_workers=max(2, 2 * router.world), thread_name_prefix="dpvs")
+        self._data_server = None
+        self.stats = {"partial_reads": 0}
+
+    def attach_document_store(self, store) -> None:
+        """Chunk texts go to the owner ranks over a socket from rank 0's document store: embed
+        requests then carry chunk ids only.  An in-process store is served by a
+        :class:`~..storage.server.DocumentStoreServer` on an ephemeral port; a networked one
+        (``cfcstore``) is published as is."""
+        from ..storage.server import DocumentStoreServer, RemoteDocumentStore
+        if isinstance(store, RemoteDocumentStore):
+            host, port = store.host, store.port
+        else:
+            host = os.environ.get("CFC_DP_DATA_HOST", "127.0.0.1")
+            self._data_server = DocumentStoreServer(store, host=host, port=0).start()
+            port = self._data_server.port
+        self.w.text_source = _store_texts(store)
+        self.w.store.set(DATA_KEY, json.dumps([host, int(port)]))
+
+    def close(self) -> None:
+        if self._data_server is not None:
+            self._data_server.server.shutdown()
+            self._data_server.server.server_close()
+            self._data_server = None
+        self._pool.shutdown(wait=False)
 
     def _fan(self, ranks, op, args_for, required: bool = True):
-        """``op`` on every rank in parallel.  ``required`` False (reads: search, count): a rank that
-        does not answer within the heartbeat timeout is marked dead and left out (its shard's rows
-        are missing from the answer until it is back), instead of failing the request."""
+        """``op`` on every rank in parallel.  A handler error is raised to the caller.  A rank that
+        does not answer in time fails the call when ``required``; for reads (search, count) it is
+        left out of THIS answer only (its rows are missing from it) -- whether it is dead is the
+        heartbeat's call, not a timeout's."""
         timeout = 120.0 if required else self.router.timeout
         futs = {r: self._pool.submit(self.rpc.call, r, op, args_for(r), timeout) for r in ranks}
         out = {}
         for r, f in futs.items():
             try:
                 out[r] = f.result()
-            except (TimeoutError, RuntimeError):
+            except TimeoutError:
                 if required:
                     raise
-                self.router.dead.add(r)
+                self.stats["partial_reads"] += 1
         return out
 
     def embed_and_store(self, chunks: list[dict]) -> dict:
         """Embed ``chunks`` ({id, thread_id, text, meta}) on their threads' owner ranks and store the
-        vectors there.  Returns {count, model, backend, dimension}."""
+        vectors there.  With a document store attached only the ids (and metadata) travel through
+        the control plane.  Returns {count, model, backend, dimension}."""
         by: dict[int, list] = {}
         for c in chunks:
-            by.setdefault(self.router.owner(c["thread_id"]), []).append(
-                {"id": c["id"], "text": c["text"], "meta": c["meta"]})
-        done = self._fan(list(by), "embed_index", lambda r: {"chunks": by[r]})
+            by.setdefault(self.router.owner(c["thread_id"]), []).append(c)
+        if self.w.text_source is not None:
+            def args_for(r):
+                return {"ids": [c["id"] for c in by[r]], "metas": [c["meta"] for c in by[r]]}
+        else:
+            def args_for(r):
+                return {"chunks": [{"id": c["id"], "text": c["text"], "meta": c["meta"]} for c in by[r]]}
+        done = self._fan(list(by), "embed_index", args_for)
         info = self.w._info(None)
         return {"count": sum(done.values()), **info}
 
@@ -366,7 +509,8 @@ class DPNodeVectorStore(VectorStore):
             raise KeyError(id)
 
     def clear(self) -> None:
-        raise NotImplementedError("clear() of a DP-sharded index: delete by id")
+        """Empty every live shard (copilot_vectorstore interface.py:99-102)."""
+        self._fan(self.router.live(), "clear", lambda r: None)
 
     def count(self) -> int:
         return sum(self._fan(self.router.live(), "count", lambda r: None, False).values())
@@ -381,27 +525,36 @@ class DPNodeVectorStore(VectorStore):
 class DPNodeSummarizer(Summarizer):
     """Rank 0's streaming summarizer over the DP ranks: ``submit(thread, done)`` sends the thread to
     its owner's engine; a collector thread per rank reads that rank's result stream and calls
-    ``done`` once per thread; a rank found dead (stale heartbeat) has its in-flight threads
-    resubmitted to the live ranks."""
+    ``done`` once per request; a request whose rank's heartbeat went stale, or whose send failed,
+    is (re)sent to a live rank by the watchdog.  Results are matched by request key only: a
+    thread may be submitted any number of times (different context, or twice in one batch) and
+    every submit gets its own result; a late duplicate of a RESENT request is dropped."""
 
-    def __init__(self, worker: DPNodeWorker, router: _Router, poll_s: float = 0.2):
+    SEND_RETRY_S = 1.0
+
+    def __init__(self, worker: DPNodeWorker, router: _Router, poll_s: float = 0.2,
+                 batch_timeout_s: float | None = None):
         local = worker.summarizer
         self.backend, self.model = getattr(local, "backend", "hip"), getattr(local, "model", "unknown")
         self.w, self.router, self.poll_s = worker, router, poll_s
+        self.batch_timeout_s = float(batch_timeout_s if batch_timeout_s is not None
+                                     else os.environ.get("CFC_DP_SUMMARY_TIMEOUT", "1800"))
         self.rpc = worker.rpc
         self._lock = threading.Lock()
-        self._inflight: dict[str, tuple[Thread, object, int]] = {}   # key -> (thread, done, rank)
-        self._delivered: set[str] = set()
+        # key -> (thread, done, rank, retry_at): rank -1 = being sent, -2 = send failed (retry at retry_at)
+        self._inflight: dict[str, tuple[Thread, object, int, float]] = {}
         self._seq = 0
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
-        self.stats = {"submitted": 0, "completed": 0, "resubmitted": 0, "duplicates": 0,
+        self._sender = ThreadPoolExecutor(max_workers=2, thread_name_prefix="dpsum-send")
+        self.stats = {"submitted": 0, "completed": 0, "resubmitted": 0, "duplicates": 0, "send_failures": 0,
                       "per_rank": [0] * router.world}
 
     # the SummarizationService's streaming protocol (start_async -> start_continuous, submit, stop)
     def start_continuous(self, **_) -> None:
         if self._threads:
             return
+        self._stop.clear()
         for r in range(self.router.world):
             t = threading.Thread(target=self._collect, args=(r,), name=f"dpsum-collect-{r}", daemon=True)
             t.start()
@@ -418,45 +571,50 @@ class DPNodeSummarizer(Summarizer):
         with self._lock:
             left, self._inflight = list(self._inflight.values()), {}
         err = RuntimeError("DP summarizer stopped before the thread finished")
-        for _, done, _ in left:
+        for _, done, _, _ in left:
             _deliver(done, None, err)
 
-    def submit(self, thread: Thread, done) -> None:
+    def submit(self, thread: Thread, done) -> str:
         with self._lock:
             self._seq += 1
             key = f"{thread.thread_id}#{self._seq}"
-            self._inflight[key] = (thread, done, -1)
+            self._inflight[key] = (thread, done, -1, 0.0)
         self.stats["submitted"] += 1
         self._send(key)
+        return key
 
     def _send(self, key: str) -> None:
         with self._lock:
             item = self._inflight.get(key)
             if item is None:
                 return
-            thread, done, _ = item
+            thread, done, _, _ = item
             rank = self.router.owner(thread.thread_id)
-            self._inflight[key] = (thread, done, rank)
+            self._inflight[key] = (thread, done, rank, 0.0)
         try:
             self.rpc.call(rank, "sum_submit", {"thread": _thread_to_json(thread), "key": key}, timeout=30.0)
-        except Exception:  # noqa: BLE001 -- the rank is gone: the watchdog resubmits
-            self.router.dead.add(rank)
+        except Exception:  # noqa: BLE001 -- not delivered (or not confirmed): the watchdog resends
+            self.stats["send_failures"] += 1
+            with self._lock:
+                if key in self._inflight:
+                    self._inflight[key] = (thread, done, -2, time.monotonic() + self.SEND_RETRY_S)
 
     def _collect(self, rank: int) -> None:
         seq = 0
+        store = self.w.store
         while not self._stop.is_set():
             key = f"{SUM_PREFIX}out/{rank}/{seq + 1}"
-            if not _wait_key(self.w.store, key, self.poll_s):
-                continue
+            try:
+                if not _wait_key(store, key, self.poll_s):
+                    continue
+                rec = json.loads(store.get(key))
+            except Exception:  # noqa: BLE001 -- the store is gone: the node is shutting down
+                return
             seq += 1
-            rec = json.loads(self.w.store.get(key))
+            _delete(store, key)
             with self._lock:
                 item = self._inflight.pop(rec["key"], None)
-                tid = rec["key"].rsplit("#", 1)[0]
-                dup = item is None or tid in self._delivered
-                if not dup:
-                    self._delivered.add(tid)
-            if dup:
+            if item is None:                  # the other copy of a resent request finished first
                 self.stats["duplicates"] += 1
                 continue
             self.stats["completed"] += 1
@@ -466,31 +624,43 @@ class DPNodeSummarizer(Summarizer):
 
     def _watch(self) -> None:
         while not self._stop.wait(self.poll_s):
+            now = time.monotonic()
             with self._lock:
-                lost = [k for k, (_, _, r) in self._inflight.items() if r >= 0 and not self.router.alive(r)]
+                lost = [k for k, (_, _, r, at) in self._inflight.items()
+                        if (r >= 0 and not self.router.alive(r)) or (r == -2 and now >= at)]
+                for k in lost:
+                    t, d, _, _ = self._inflight[k]
+                    self._inflight[k] = (t, d, -1, 0.0)      # being resent: not picked again meanwhile
             for k in lost:
                 self.stats["resubmitted"] += 1
-                self._send(k)
+                self._sender.submit(self._send, k)
 
-    # batch API (DP-aware callers without streaming): submit all, wait for all
+    # batch API (DP-aware callers without streaming): submit all, wait for all (bounded)
     def summarize_batch(self, threads: list[Thread]) -> list[Summary]:
         box: dict[int, tuple] = {}
         ev = threading.Event()
+        blk = threading.Lock()
 
         def cb(i):
             def done(s, e):
-                box[i] = (s, e)
-                if len(box) == len(threads):
-                    ev.set()
+                with blk:
+                    box[i] = (s, e)
+                    if len(box) == len(threads):
+                        ev.set()
             return done
         started = bool(self._threads)
         if not started:
             self.start_continuous()
+        keys = []
         try:
             for i, t in enumerate(threads):
-                self.submit(t, cb(i))
-            if threads:
-                ev.wait()
+                keys.append(self.submit(t, cb(i)))
+            if threads and not ev.wait(self.batch_timeout_s):
+                with self._lock:
+                    for k in keys:
+                        self._inflight.pop(k, None)
+                raise TimeoutError(f"DP summarizer: {len(threads) - len(box)} of {len(threads)} threads not "
+                                   f"summarized within {self.batch_timeout_s:.0f}s")
         finally:
             if not started:
                 self.stop_continuous()

@@ -193,6 +193,8 @@ def _close_distributed(ctx: dict | None) -> None:
         from ..parallel.dp_node import shutdown_workers
         shutdown_workers(ctx["store"])      # DP workers leave their serve loops
         ctx["worker"].stop()
+        if ctx.get("vector_store") is not None:
+            ctx["vector_store"].close()     # the chunk-text server
     if ctx["tp_bcast"] is not None:
         ctx["tp_bcast"].stop()
 

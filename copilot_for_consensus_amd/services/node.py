@@ -63,6 +63,10 @@ class Node:
                 int(ecfg.vector_store.driver_config.get("dimension") or
                     ecfg.vector_store.driver_config.get("vector_size") or 384)
             self.vectors = create_vector_store(ecfg.vector_store, dimension=dim)
+        # a DP-sharded index (parallel/dp_node.py) reads chunk texts from this node's store by id
+        attach = getattr(self.vectors, "attach_document_store", None)
+        if callable(attach):
+            attach(self.store)
         self.summarizer = summarizer or (create_llm_backend(cfgs["summarization"].llm_backend)
                                          if "summarizer" in need else None)
         rcfg = next((c.event_retry for c in cfgs.values() if hasattr(c, "event_retry")), None)

@@ -18,14 +18,24 @@ from __future__ import annotations
 import json
 from pathlib import Path
 
+import hashlib
+
 import numpy as np
-import xxhash
+
+try:
+    import xxhash
+except ImportError:  # optional: the standard library's blake2b gives the same 64-bit lookup key
+    xxhash = None
 
 _EMPTY = np.zeros(0, np.uint8)
+# which 64-bit hash the "hash" column holds (saved with the table; a load under the other one rehashes)
+HASH_NAME = "xxh3_64" if xxhash is not None else "blake2b_64"
 
 
 def _hash(b: bytes) -> int:
-    return xxhash.xxh3_64_intdigest(b)
+    if xxhash is not None:
+        return xxhash.xxh3_64_intdigest(b)
+    return int.from_bytes(hashlib.blake2b(b, digest_size=8).digest(), "little")
 
 
 class _Heap:
@@ -213,6 +223,7 @@ class RowTable:
             np.save(p / f"rows_{k}.npy", a[:self.n])
         np.save(p / "rows_idheap.npy", self._ids.buf[:self._ids.n])
         np.save(p / "rows_metaheap.npy", self._meta.buf[:self._meta.n])
+        (p / "rows_hash.txt").write_text(HASH_NAME)
 
     @classmethod
     def load(cls, path) -> "RowTable":
@@ -227,5 +238,11 @@ class RowTable:
             b = np.load(p / f"rows_{name}.npy")
             heap.buf = np.concatenate([b, np.zeros(max(1024, b.size), np.uint8)])
             heap.n = b.size
+        saved = (p / "rows_hash.txt").read_text().strip() if (p / "rows_hash.txt").exists() else "xxh3_64"
+        if saved != HASH_NAME:
+            # written under the other hash function (xxhash present there, absent here or vice versa)
+            c = t._cols
+            c["hash"][:t.n] = np.fromiter(
+                (_hash(t._ids.get(int(c["ioff"][r]), int(c["ilen"][r]))) for r in range(t.n)), np.uint64, t.n)
         t.rebuild()
         return t

@@ -1,0 +1,190 @@
+"""The DP node's control plane (parallel/dp_node.py) over a real TCPStore with 3 ranks on the CPU:
+every request / reply / result key is deleted once consumed (the store stays bounded over many
+batches), chunk texts travel over the document-store socket (only ids through the store), the
+same thread summarized twice gets two results, handler errors reach the caller without marking
+the rank dead, reads never queue behind a long embed, and clear() empties every shard."""
+from __future__ import annotations
+
+import datetime
+import socket
+import threading
+import time
+
+import pytest
+import torch.multiprocessing as mp
+from torch.distributed import TCPStore
+
+from copilot_for_consensus_amd.summarization import Summarizer, Summary, Thread
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class _Sum(Summarizer):
+    backend, model = "mock", "rank-mock"
+
+    def __init__(self, rank):
+        self.rank = rank
+
+    def summarize(self, thread):
+        return self.summarize_batch([thread])[0]
+
+    def summarize_batch(self, threads):
+        return [Summary(t.thread_id, f"rank{self.rank}:{t.thread_id}:{t.prompt}", [], self.backend, self.model,
+                        1, 1, 0) for t in threads]
+
+
+class _SlowEmbedder:
+    """Mock embedder; texts starting with 'SLOW' take 3 s (an encoder forward on a big batch)."""
+    model_name, backend, dimension = "mock-16", "mock", 16
+
+    def __init__(self):
+        from copilot_for_consensus_amd.embedding import MockEmbeddingProvider
+        self.inner = MockEmbeddingProvider(16)
+
+    def embed_tensor(self, texts):
+        if any(t.startswith("SLOW") for t in texts):
+            time.sleep(3.0)
+        if any(t.startswith("FAIL") for t in texts):
+            raise ValueError("encoder rejected the batch")
+        return self.inner.embed_tensor(texts)
+
+
+def _make_worker(store, rank, world):
+    from copilot_for_consensus_amd.parallel.dp_node import DPNodeWorker
+    from copilot_for_consensus_amd.vectorstore import InMemoryVectorStore
+    return DPNodeWorker(store, rank, world, _SlowEmbedder(), InMemoryVectorStore(16), _Sum(rank),
+                        heartbeat_interval=0.2)
+
+
+def _rank_main(port, rank, world, q):
+    store = TCPStore("127.0.0.1", port, is_master=False, timeout=datetime.timedelta(seconds=60))
+    stats = _make_worker(store, rank, world).run_until_shutdown(poll_s=0.05)
+    q.put((rank, stats))
+
+
+@pytest.fixture
+def node3():
+    from copilot_for_consensus_amd.parallel.dp_node import build_rank0
+    from copilot_for_consensus_amd.storage.document_store import InMemoryDocumentStore
+    world = 3
+    port = _free_port()
+    store = TCPStore("127.0.0.1", port, is_master=True, wait_for_workers=False, timeout=datetime.timedelta(seconds=60))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_main, args=(port, r, world, q), daemon=True) for r in range(1, world)]
+    for p in procs:
+        p.start()
+    w0 = _make_worker(store, 0, world)
+    vs, summ = build_rank0(store, world, w0, heartbeat_timeout=30.0)
+    docs = InMemoryDocumentStore()
+    docs.connect()
+    vs.attach_document_store(docs)
+    w0.start(serve=False)
+    summ.start_continuous()
+    deadline = time.time() + 120
+    while not all(store.check([f"dpsum/hb/{r}"]) for r in range(world)):
+        assert time.time() < deadline, "DP ranks never started"
+        time.sleep(0.05)
+    try:
+        yield store, vs, summ, docs, w0, q, procs
+    finally:
+        from copilot_for_consensus_amd.parallel.dp_node import shutdown_workers
+        summ.stop_continuous()
+        shutdown_workers(store)
+        w0.stop()
+        vs.close()
+        for p in procs:
+            p.join(timeout=20)
+            if p.is_alive():
+                p.kill()
+
+
+def _chunks(docs, batch, n_threads=6, per_thread=3, prefix=""):
+    out = []
+    for t in range(n_threads):
+        tid = f"{batch:03d}{t:02d}" + "0" * 11
+        for c in range(per_thread):
+            cid = f"c{batch:03d}-{t}-{c}"
+            text = f"{prefix}batch {batch} thread {t} chunk {c} about consensus"
+            docs.insert_document("chunks", {"_id": cid, "thread_id": tid, "text": text})
+            out.append({"id": cid, "thread_id": tid, "text": text, "meta": {"thread_id": tid, "chunk_index": c}})
+    return out
+
+
+def test_dp_node_store_keys_stay_bounded_over_50_batches(node3):
+    store, vs, summ, docs, w0, q, procs = node3
+    counts = []
+    for b in range(50):
+        chunks = _chunks(docs, b)
+        assert vs.embed_and_store(chunks)["count"] == len(chunks)
+        hits = vs.query([0.5] * 16, top_k=5)
+        assert len(hits) == 5
+        tids = sorted({c["thread_id"] for c in chunks})
+        sc = vs.centroid_scores([c["id"] for c in chunks if c["thread_id"] == tids[0]], thread_id=tids[0])
+        assert len(sc) == 3
+        # the same thread twice in one batch, with different context: two results, none dropped
+        threads = [Thread(tids[0], ["m"], prompt="ctx-a"), Thread(tids[0], ["m"], prompt="ctx-b"),
+                   Thread(tids[1], ["m"], prompt="p")]
+        out = summ.summarize_batch(threads)
+        assert [s.summary_markdown.rsplit(":", 1)[1] for s in out] == ["ctx-a", "ctx-b", "p"]
+        counts.append(store.num_keys())
+    assert vs.count() == 50 * 18
+    # nothing accumulates: request / reply / result keys are deleted once consumed
+    assert max(counts[10:]) <= max(counts[:10]) + 2, counts
+    assert max(counts) < 40, counts
+    assert summ.stats["completed"] == 150 and summ.stats["duplicates"] == 0, summ.stats
+    # every rank embedded its threads' chunks, reading the texts by id over the socket
+    vs.clear()
+    assert vs.count() == 0
+    from copilot_for_consensus_amd.parallel.dp_node import shutdown_workers
+    shutdown_workers(store)
+    got = dict(q.get(timeout=60) for _ in procs)
+    assert all(got[r]["embedded"] > 0 for r in (1, 2)), got
+    assert w0.stats["embedded"] + got[1]["embedded"] + got[2]["embedded"] == 50 * 18
+
+
+def test_dp_node_handler_error_is_not_rank_death_and_reads_skip_bulk_queue(node3):
+    from copilot_for_consensus_amd.parallel.dp_node import RemoteError
+    store, vs, summ, docs, w0, q, procs = node3
+    # a failing embed on a worker rank: the caller sees the error, the rank stays routable
+    bad = [c for c in _chunks(docs, 900, n_threads=12, prefix="FAIL ")]
+    with pytest.raises((RemoteError, ValueError)):     # rank 0's share raises in place
+        vs.embed_and_store(bad)
+    assert vs.router.live() == [0, 1, 2]
+    good = _chunks(docs, 901)
+    assert vs.embed_and_store(good)["count"] == len(good)
+    # a slow embed (3 s encoder forward) on every rank: topic reads answer meanwhile
+    slow = _chunks(docs, 902, n_threads=12, prefix="SLOW ")
+    th = threading.Thread(target=vs.embed_and_store, args=(slow,))
+    th.start()
+    time.sleep(0.5)
+    t0 = time.perf_counter()
+    n = vs.count()
+    dt = time.perf_counter() - t0
+    th.join()
+    assert n >= len(good) and dt < 1.5, (n, dt)
+    assert vs.count() == len(good) + len(slow)
+    assert vs.stats["partial_reads"] == 0
+
+
+def test_store_rpc_skips_a_sequence_number_whose_caller_died():
+    from copilot_for_consensus_amd.parallel.dp_node import StoreRPC
+    store = TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False, timeout=datetime.timedelta(seconds=10))
+    srv = StoreRPC(store, 1, skip_grace_s=0.3)
+    srv.handlers["echo"] = lambda a: a
+    stop = threading.Event()
+    t = threading.Thread(target=srv.serve, args=(stop,), kwargs={"poll_s": 0.05})
+    t.start()
+    try:
+        store.add("dprpc/1/ctl/seq", 1)         # a caller reserved seq 1 and died before writing it
+        cli = StoreRPC(store, 0)
+        assert cli.call(1, "echo", {"x": 1}, timeout=10) == {"x": 1}
+        assert srv.skipped == 1
+        assert not store.check(["dprpc/1/ctl/req/2"]) and not store.check(["dprpc/1/ctl/res/2"])
+    finally:
+        stop.set()
+        t.join()

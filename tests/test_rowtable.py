@@ -72,3 +72,24 @@ def test_bulk_build_of_a_million_ids_is_compact_and_fast():
     assert dt < 30, dt
     t.permute(np.arange(n - 1, -1, -1))
     assert t.find(ids[0]) == n - 1 and t.id_at(0) == ids[-1]
+
+
+def test_table_saved_under_one_hash_loads_under_the_other(tmp_path, monkeypatch):
+    """xxhash is optional (blake2b fallback): a table saved with either hash finds its ids after a
+    load under the other one (the hash column is recomputed)."""
+    import copilot_for_consensus_amd.vectorstore.rowtable as RT
+    t = RT.RowTable(4)
+    t.upsert([f"id{i}" for i in range(50)], [{"i": i} for i in range(50)])
+    t.save(tmp_path / "x")
+    other = "blake2b_64" if RT.HASH_NAME == "xxh3_64" else "xxh3_64"
+    if other == "xxh3_64":
+        pytest.importorskip("xxhash")
+    monkeypatch.setattr(RT, "HASH_NAME", other)
+    if other == "blake2b_64":
+        monkeypatch.setattr(RT, "xxhash", None)
+    else:
+        import xxhash
+        monkeypatch.setattr(RT, "xxhash", xxhash)
+    u = RT.RowTable.load(tmp_path / "x")
+    assert [u.find(f"id{i}") for i in range(50)] == list(range(50))
+    assert u.meta_at(7) == {"i": 7}
