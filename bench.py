@@ -5,7 +5,8 @@ BASELINE.json metric: "end-to-end threads summarized/sec + p50 summary latency, 
 One step = one batch of mailing-list threads per GPU taken through the whole pipeline of the
 reference (ingest bytes -> parse mbox -> thread -> chunk -> embed (HIP encoder) -> index (HIP kNN)
 -> orchestrator top-k context selection -> prompt -> Mistral-7B prefill + 512-token greedy decode
-(HIP kernels + hipBLASLt, hipGraph decode) -> summary + citations).  Synthetic .mbox data and
+(hand-written HIP kernels only -- MFMA prefill / decode GEMMs, flash prefill, paged decode
+attention; hipGraph decode) -> summary + citations).  Synthetic .mbox data and
 random-init bf16 weights (no network).  Data parallel over ranks (one process per GPU, RCCL
 barrier/all-reduce for timing): weak scaling, per-GPU work fixed.
 
@@ -95,8 +96,9 @@ def main(argv=None):
                          index_group=groups.dp_group if groups.dp_size > 1 and not args.llm_only else None,
                          overlap_prefill=args.overlap_prefill == "on" and not args.no_overlap)
 
+    # the latency half runs at every TP degree (the TP followers replay the continuous engine's steps)
     probe_steps = list(range(args.warmup + args.steps, args.warmup + args.steps + args.latency_steps)) \
-        if args.latency_rate > 0 and args.tp == 1 and not args.llm_only else []
+        if args.latency_rate > 0 and not args.llm_only else []
     low_steps = [args.warmup + args.steps + args.latency_steps] if probe_steps and args.latency_low_rate > 0 else []
     pipe.prepare_sources(list(range(args.warmup + args.steps)) + probe_steps + low_steps)
 
@@ -147,39 +149,29 @@ def main(argv=None):
 
     value = threads / elapsed
     p50 = statistics.median(lat_all) if lat_all else None
-    latency = None
-    if probe_steps:
-        # after the timed window: the same GPUs at a load below saturation (Poisson arrivals)
+
+    def probe_point(steps, rate, seed, max_threads=None):
+        """One latency point: every DP replica's continuous engine under Poisson arrivals; the TP
+        followers' empty dicts are dropped before the aggregate."""
         barrier()
-        probe = pipe.latency_probe(probe_steps, args.latency_rate, seed=args.seed + 104729 * groups.dp_rank)
+        probe = pipe.latency_probe(steps, rate, seed=seed, max_threads=max_threads)
         if world > 1:
             parts = [None] * world
             dist.all_gather_object(parts, probe)
-            probe = parts
+            probe = [p for p in parts if p]
         else:
             probe = [probe]
-        latency = dict(probe[0])
-        latency.update(threads=sum(p["threads"] for p in probe),
-                       p50_s=round(statistics.median([p["p50_s"] for p in probe]), 3),
-                       p95_s=round(max(p["p95_s"] for p in probe), 3),
-                       throughput_threads_per_s=round(sum(p["throughput_threads_per_s"] for p in probe), 3))
-    latency_low = None
-    if low_steps:
-        # light load: a few threads, far apart -- the regime of the reference's published 3-4 s per thread
-        barrier()
-        low = pipe.latency_probe(low_steps, args.latency_low_rate, seed=args.seed + 7919 + 104729 * groups.dp_rank,
-                                 max_threads=args.latency_low_threads)
-        if world > 1:
-            parts = [None] * world
-            dist.all_gather_object(parts, low)
-            low = parts
-        else:
-            low = [low]
-        latency_low = dict(low[0])
-        latency_low.update(threads=sum(p["threads"] for p in low),
-                           p50_s=round(statistics.median([p["p50_s"] for p in low]), 3),
-                           p95_s=round(max(p["p95_s"] for p in low), 3),
-                           throughput_threads_per_s=round(sum(p["throughput_threads_per_s"] for p in low), 3))
+        agg = dict(probe[0])
+        agg.update(threads=sum(p["threads"] for p in probe),
+                   p50_s=round(statistics.median([p["p50_s"] for p in probe]), 3),
+                   p95_s=round(max(p["p95_s"] for p in probe), 3),
+                   throughput_threads_per_s=round(sum(p["throughput_threads_per_s"] for p in probe), 3))
+        return agg
+    # after the timed window: the same GPUs at a load below saturation (Poisson arrivals), then a
+    # light load -- a few threads far apart, the regime of the reference's published 3-4 s per thread
+    latency = probe_point(probe_steps, args.latency_rate, args.seed + 104729 * groups.dp_rank) if probe_steps else None
+    latency_low = (probe_point(low_steps, args.latency_low_rate, args.seed + 7919 + 104729 * groups.dp_rank,
+                               max_threads=args.latency_low_threads) if low_steps else None)
     if rank == 0:
         out = {
             "metric": "end-to-end threads summarized/sec + p50 summary latency, Mistral-7B TP=1/8",
@@ -209,6 +201,9 @@ def main(argv=None):
                              else "prefill then decode per batch (next batch's preparation overlapped)"),
             },
             "p50_summary_latency_s": round(p50, 3) if p50 is not None else None,
+            "p50_summary_latency_regime": ("saturated: every thread of a timed batch, from its batch's "
+                                           "preparation start to its last token (see latency_mode* for "
+                                           "stated arrival rates below saturation)"),
             # latency half of the metric at a stated arrival rate below saturation (continuous engine)
             "latency_mode": latency,
             "latency_mode_light": latency_low,

@@ -81,7 +81,10 @@ def make_groups(env: DistEnv, tp: int) -> Groups:
     for s in range(0, env.world, tp):  # every rank must create every group, in the same order
         ranks = list(range(s, s + tp))
         tp_groups.append(dist.new_group(ranks))
-        tp_cpu.append(dist.new_group(ranks, backend="gloo") if env.backend != "gloo" else tp_groups[-1])
+        # a SEPARATE gloo group even when the job runs on gloo: host objects (prompts, engine steps)
+        # are broadcast from another thread than the TP all-reduces, and two threads issuing
+        # collectives on one group can order them differently on different ranks (deadlock)
+        tp_cpu.append(dist.new_group(ranks, backend="gloo"))
     for i in range(tp):
         dp_groups.append(dist.new_group(list(range(i, env.world, tp))))
     g = env.rank // tp

@@ -263,25 +263,47 @@ class BenchPipeline:
         (prepared by the same RAG path as the throughput steps) arrive as a Poisson process of
         ``rate_per_s`` and are served by the continuous engine (runtime/continuous.py -- the
         summarization service's engine): a thread joins the running decode batch at the next burst
-        boundary and leaves it after its 512 tokens.  Latency = the thread's share of the pipeline
-        preparation (its batch's parse / chunk / embed / select time / threads) + arrival ->
-        last token.  Not in the timed throughput window."""
+        boundary and leaves it after its 512 tokens.  Latency = its batch's whole preparation time
+        (parse / chunk / embed / select of the step it came from: the thread could not be submitted
+        before that batch was prepared) + arrival -> last token.  Not in the timed throughput window.
+        Under tensor parallelism the TP followers replay every engine step the leader takes (the
+        leader's ``sync`` messages over the TP group's CPU twin, as the summarization service's
+        followers do) and return {}."""
         import numpy as np
 
         from ..runtime.continuous import ContinuousEngine
-        prompts, prep_s = [], 0.0
+        prompts, prep_of = [], []
         for st in steps:
             _, ctx, p, stages = self._prepare(st)
-            prep_s += sum(stages.values())
+            prep = sum(v for k, v in stages.items() if k != "wait_prep")
             prompts.extend(p)
+            prep_of.extend([prep] * len(p))
         if not prompts:
             return {}
-        per_thread_prep = prep_s / len(prompts)
         if max_threads is not None:
-            prompts = prompts[:max_threads]
-        ce = ContinuousEngine(self.engine, max_slots=self.threads_per_step, max_new_cap=self.max_new,
-                              max_prompt=max(len(x) for x in prompts), steps_per_sync=steps_per_sync, stop_ids=(),
-                              min_admit=1, max_wait_s=0.05)
+            prompts, prep_of = prompts[:max_threads], prep_of[:max_threads]
+        params = dict(max_slots=self.threads_per_step, max_new_cap=self.max_new, max_prompt=max(len(x) for x in prompts),
+                      steps_per_sync=steps_per_sync, stop_ids=(), min_admit=1, max_wait_s=0.05)
+        tp = self.groups is not None and self.groups.tp_size > 1
+        if tp:
+            import torch.distributed as dist
+            g = self.groups
+
+            def bcast(msg):
+                box = [msg]
+                dist.broadcast_object_list(box, src=g.tp_src, group=g.tp_cpu_group)
+                return box[0]
+            if self.follower:
+                ce = ContinuousEngine(self.engine, **params)
+                try:
+                    while (msg := bcast(None)) is not None:
+                        ce.follow(msg)
+                finally:
+                    ce.close()
+                return {}
+            ce = ContinuousEngine(self.engine, **params, sync=bcast)
+        else:
+            ce = ContinuousEngine(self.engine, **params)
         rng = np.random.default_rng(seed)
         arrive = np.cumsum(rng.exponential(1.0 / float(rate_per_s), len(prompts)))
         t0 = time.perf_counter()
@@ -291,19 +313,24 @@ class BenchPipeline:
                 now = time.perf_counter() - t0
                 while nxt < len(prompts) and arrive[nxt] <= now:
                     r = ce.submit(prompts[nxt], self.max_new)
-                    arrival_of[r.rid] = t0 + float(arrive[nxt])
+                    arrival_of[r.rid] = (t0 + float(arrive[nxt]), prep_of[nxt])
                     nxt += 1
                 if ce.pending():
                     for r in ce.step():
-                        lat.append(r.finished_s - arrival_of.pop(r.rid))
+                        at, prep = arrival_of.pop(r.rid)
+                        lat.append(r.finished_s - at + prep)
                 elif nxt < len(prompts):
                     time.sleep(max(0.0, float(arrive[nxt]) - (time.perf_counter() - t0)))
         finally:
+            if tp:
+                bcast(None)               # the followers leave their replay loop
             ce.close()
         wall = time.perf_counter() - t0
-        lat = np.asarray(lat) + per_thread_prep
+        lat = np.asarray(lat)
         return {"arrival_rate_per_gpu": float(rate_per_s), "threads": int(len(lat)),
                 "p50_s": round(float(np.percentile(lat, 50)), 3), "p95_s": round(float(np.percentile(lat, 95)), 3),
                 "throughput_threads_per_s": round(len(lat) / wall, 3),
-                "prep_per_thread_s": round(per_thread_prep, 4),
-                "engine": f"continuous ({self.threads_per_step} slots, {steps_per_sync} decode steps per admission)"}
+                "prep_per_thread_s": round(float(np.mean(prep_of)), 4),
+                "prep_charged": "the thread's whole batch preparation",
+                "engine": f"continuous ({self.threads_per_step} slots, {steps_per_sync} decode steps per admission)"
+                          + (f", TP={self.groups.tp_size}" if tp else "")}

@@ -66,6 +66,20 @@ def test_bench_two_ranks_under_torchrun():
     assert d["config"]["index"].startswith("sharded over 2 GPUs")    # the DP data plane ran
 
 
+def test_bench_tp2_two_ranks_reports_both_halves():
+    """--tp 2 over 2 ranks (one DP replica of a TP=2 engine): the throughput half and both latency
+    points, the TP follower replaying the continuous engine's steps."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", "--tp", "2", *ARGS]
+    d = _run(cmd)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp1xtp2" and d["config"]["global_batch"] == 2
+    assert d["value"] == pytest.approx(2 * 2 / (d["ms_per_step"] * 2 / 1000), rel=0.02)
+    lm, ll = d["latency_mode"], d["latency_mode_light"]
+    assert lm["threads"] == 2 * 2 and ll["threads"] == 2 and "TP=2" in lm["engine"]
+    assert 0 < lm["p50_s"] <= lm["p95_s"] and 0 < ll["p50_s"] <= ll["p95_s"]
+    assert lm["prep_charged"] == "the thread's whole batch preparation"
+
+
 def test_bench_node_pipeline_contract():
     """--pipeline node: the same JSON contract measured through the real services (Node on the
     in-proc bus, continuous summarization engine), every thread of every step reported."""
