@@ -54,6 +54,44 @@ def shard_weights(full: DecoderWeights, tp_rank: int, tp_size: int, device=None)
     return w.finalize()
 
 
+def unshard_weights(shards: list[DecoderWeights], device=None) -> DecoderWeights:
+    """The inverse of :func:`shard_weights`: one unsharded model from the TP shards of ranks 0..T-1
+    (e.g. the reference of a TP run whose shards were generated per rank by random_sharded).  Each
+    shard's layer tensors are released as they are consumed, so peak memory is the full model plus
+    one layer."""
+    from ..ops.reference import deinterleave_gate_up
+    s0 = shards[0]
+    cfg: DecoderConfig = s0.cfg
+    dev = device or s0.device
+    T, D = len(shards), cfg.head_dim
+    w = DecoderWeights(cfg, dev)
+    for i in range(cfg.layers):
+        parts = [sh.rowmajor_layer(i) for sh in shards]
+        hq, hk = shards[0].heads, shards[0].kv_heads
+        qkv = [p["qkv"].to(dev) for p in parts]
+        gus = [deinterleave_gate_up(p["gate_up"].to(dev)) if sh.gate_up_interleaved else p["gate_up"].to(dev)
+               for p, sh in zip(parts, shards)]
+        f = gus[0].shape[0] // 2
+        w.layers.append({
+            "attn_norm": parts[0]["attn_norm"].to(dev),
+            "qkv": torch.cat([t[:hq * D] for t in qkv] + [t[hq * D:(hq + hk) * D] for t in qkv]
+                             + [t[(hq + hk) * D:] for t in qkv]).contiguous(),
+            "o": torch.cat([p["o"].to(dev) for p in parts], 1).contiguous(),
+            "mlp_norm": parts[0]["mlp_norm"].to(dev),
+            "gate_up": torch.cat([g[:f] for g in gus] + [g[f:] for g in gus]).contiguous(),
+            "down": torch.cat([p["down"].to(dev) for p in parts], 1).contiguous(),
+        })
+        del parts, qkv, gus
+        for sh in shards:                      # free the consumed layer of every shard
+            sh.layers[i] = {}
+            if sh.packed is not None:
+                sh.packed[i] = {}
+    w.embed = s0.embed.to(dev)
+    w.final_norm = s0.final_norm.to(dev)
+    w.lm_head = torch.cat([sh.lm_head.to(dev) for sh in shards]).contiguous()
+    return w.finalize()
+
+
 def random_sharded(cfg: DecoderConfig, device, seed: int, tp_rank: int, tp_size: int) -> DecoderWeights:
     """Random-init weights of a TP shard without materialising the full model on any rank.
 

@@ -108,7 +108,7 @@ def test_two_processes_share_regions_over_ipc():
         assert res["graph_max_err"] <= 0.0625, res
 
 
-def _tp_worker(rank, world, port, q, prompts, n_new, cfg_name="tiny", seed=5, blocks=64):
+def _tp_worker(rank, world, port, q, prompts, n_new, cfg_name="tiny", seed=5, blocks=64, sharded_init=False):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                           LOCAL_RANK=str(rank), CFC_DIST_BACKEND="gloo")
@@ -121,9 +121,13 @@ def _tp_worker(rank, world, port, q, prompts, n_new, cfg_name="tiny", seed=5, bl
         env = init_distributed(backend="gloo")
         g = make_groups(env, tp=world)
         cfg = get_config(cfg_name)
-        full = DecoderWeights.random(cfg, env.device, seed=seed)
-        w = shard_weights(full, g.tp_rank, g.tp_size)
-        del full
+        if sharded_init:
+            # only this rank's shard is generated (a 70B shard is half the GPU; the full model is not)
+            w = DecoderWeights.random(cfg, env.device, seed=seed, tp_rank=g.tp_rank, tp_size=g.tp_size)
+        else:
+            full = DecoderWeights.random(cfg, env.device, seed=seed)
+            w = shard_weights(full, g.tp_rank, g.tp_size)
+            del full
         torch.cuda.empty_cache()
         ar = maybe_create(g.tp_group, env.device)
         m = DecoderModel(w, tp_group=g.tp_group, custom_ar=ar)
@@ -264,5 +268,51 @@ def test_tp2_mistral7b_matches_tp1_greedy():
             worst = max(worst, gap)
             exact += int(gap == 0.0)
     n = 32 * len(prompts)
+    assert worst <= 0.1, f"a TP=2 token is {worst:.3f} sigma below TP=1's best (exact {exact}/{n})"
+    assert exact >= 0.9 * n, f"TP=2 matched TP=1's argmax in {exact}/{n} teacher-forced steps"
+
+
+def test_tp2_llama3_70b_matches_tp1_teacher_forced():
+    """Llama-3-70B at TP=2 as two processes on the one GPU (each generates only its 70.5 GB shard:
+    32 q / 4 kv heads, FFN 14336 per rank, vocab shard 64128), greedy decode in the captured graph
+    with the IPC all-reduces, against the unsharded model assembled from the same shards
+    (parallel/tp.unshard_weights, 141 GB) teacher-forced on TP=2's own tokens -- the criterion of
+    test_tp2_mistral7b_matches_tp1_greedy."""
+    from copilot_for_consensus_amd.models.decoder import DecoderModel, DecoderWeights, get_config
+    from copilot_for_consensus_amd.parallel.tp import unshard_weights
+    from copilot_for_consensus_amd.runtime.engine import LLMEngine
+    from copilot_for_consensus_amd.runtime.kv_cache import PagedKVCache
+    cfg = get_config("llama-3-70b")
+    free, _ = torch.cuda.mem_get_info()
+    if free < 200e9:
+        pytest.skip(f"needs ~150 GB of free HBM, {free / 1e9:.0f} GB free")
+    g = torch.Generator().manual_seed(12)
+    prompts = [[cfg.bos_id] + torch.randint(3, cfg.vocab_size, (n,), generator=g).tolist() for n in (37, 300, 5, 129)]
+    n_new = 16
+    res = _run_tp2(prompts, n_new, cfg_name="llama-3-70b", seed=3, blocks=128, sharded_init=True)
+    for r in range(2):
+        assert "exception" not in res[r], res[r]
+        assert res[r]["custom_ar"] and res[r]["errors"] == 0, res[r]
+        assert res[r]["graphed"] and res[r]["tokens"] == res[r]["eager"], res[r]
+    tp2 = res[0]["tokens"]
+    assert tp2 == res[1]["tokens"] and all(len(t) == n_new for t in tp2)
+    shards = [DecoderWeights.random(cfg, "cuda:0", seed=3, tp_rank=r, tp_size=2) for r in range(2)]
+    full = unshard_weights(shards)
+    del shards
+    torch.cuda.empty_cache()
+    m1 = DecoderModel(full)
+    eng = LLMEngine(m1, PagedKVCache(cfg.layers, 128, cfg.kv_heads, cfg.head_dim, "cuda:0"), use_graph=False,
+                    prefix_cache=False)
+    exact, worst = 0, 0.0
+    for j in range(n_new):
+        lg = _last_logits(eng, m1, [p + t[:j] for p, t in zip(prompts, tp2)])
+        sig = lg.std(-1)
+        for i, t in enumerate(tp2):
+            gap = float((lg[i].max() - lg[i, t[j]]) / sig[i])
+            worst = max(worst, gap)
+            exact += int(gap == 0.0)
+    n = n_new * len(prompts)
+    del m1, eng, full
+    torch.cuda.empty_cache()
     assert worst <= 0.1, f"a TP=2 token is {worst:.3f} sigma below TP=1's best (exact {exact}/{n})"
     assert exact >= 0.9 * n, f"TP=2 matched TP=1's argmax in {exact}/{n} teacher-forced steps"

@@ -294,3 +294,22 @@ def test_argmax_keys_reduce_equals_global_argmax():
         ids = (0xFFFFFFFF - (keys & 0xFFFFFFFF)).to(torch.int32)
         want = torch.tensor([int(torch.nonzero(row == row.max())[0]) for row in x.float()], dtype=torch.int32)
         assert torch.equal(ids, want), (ids, want)
+
+
+def test_unshard_inverts_shard_and_random_sharded():
+    """unshard_weights(shards) is the model whose shard_weights are those shards: exact on a full
+    model, and it assembles per-rank random_sharded shards into the model a TP run computes."""
+    from copilot_for_consensus_amd.models.decoder import DecoderWeights, get_config
+    from copilot_for_consensus_amd.parallel.tp import random_sharded, shard_weights, unshard_weights
+    cfg = get_config("tiny-70b-heads")
+    full = DecoderWeights.random(cfg, "cpu", seed=2)
+    back = unshard_weights([shard_weights(full, r, 4) for r in range(4)])
+    for a, b in zip(full.layers, back.layers):
+        assert all(torch.equal(a[k], b[k]) for k in a)
+    assert torch.equal(full.lm_head, back.lm_head)
+    shards = [random_sharded(cfg, "cpu", 9, r, 2) for r in range(2)]
+    ref = [{k: v.clone() for k, v in sh.layers[1].items()} for sh in shards]
+    u = unshard_weights(shards)
+    for r in range(2):
+        again = shard_weights(u, r, 2).layers[1]
+        assert all(torch.equal(again[k], ref[r][k]) for k in again)
