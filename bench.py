@@ -217,50 +217,57 @@ def main(argv=None):
 
 
 def _main_node(args, env, groups):
-    """--pipeline node: the same metric through the deployment's services (one node per rank)."""
+    """--pipeline node: the same metric through the deployment's services.  One rank: a whole node
+    on the GPU.  Under torchrun: the topology ``services.main node`` deploys -- rank 0 runs the
+    services with the DP facades, every rank a DPNodeWorker (its own encoder, HBM index shard and
+    continuous LLM engine); a step is one archive of threads-per-gpu x world threads."""
     import torch
     import torch.distributed as dist
 
     from copilot_for_consensus_amd.pipeline.node_bench import NodeBench
     if args.tp > 1:
-        raise SystemExit("--pipeline node runs one model per rank (use torchrun ranks for DP)")
+        raise SystemExit("--pipeline node runs one model per rank (DP over ranks)")
     world, rank, dev = env.world, env.rank, env.device
+    dp = None
+    cpu = None
+    if world > 1:
+        # host-side barriers / gathers on their own gloo group: the DP workers' serve threads keep
+        # using the GPU (and the job's store) while the main thread waits here
+        cpu = dist.new_group(backend="gloo")
+        dp = {"store": dist.distributed_c10d._get_default_store(), "rank": rank, "world": world}
     nb = NodeBench(model=args.model, encoder=args.encoder, device=dev, threads_per_step=args.threads_per_gpu,
-                   max_new_tokens=args.max_new, seed=args.seed + 7919 * groups.dp_rank, index_prefill=args.index_prefill)
-    nb.prepare_sources(list(range(args.warmup + args.steps)))
+                   max_new_tokens=args.max_new, seed=args.seed, index_prefill=args.index_prefill, dp=dp)
+    if rank == 0:
+        nb.prepare_sources(list(range(args.warmup + args.steps)))
 
     def report(kind):
         def f(i, r):
             if rank == 0:
                 print(f"[bench-node] {kind} {i}: {r.summary()}", file=sys.stderr, flush=True)
         return f
-    if args.warmup:
-        nb.run_steps(list(range(args.warmup)), on_step=report("warmup"))
 
     def barrier():
         if world > 1:
-            dist.barrier()
+            dist.barrier(group=cpu)
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
+    barrier()                                   # every rank's models and index built
+    if args.warmup and rank == 0:
+        nb.run_steps(list(range(args.warmup)), on_step=report("warmup"))
     barrier()
     t0 = time.perf_counter()
-    results = nb.run_steps(list(range(args.warmup, args.warmup + args.steps)), on_step=report("step"))
+    results = nb.run_steps(list(range(args.warmup, args.warmup + args.steps)), on_step=report("step")) \
+        if rank == 0 else []
     barrier()
     elapsed = time.perf_counter() - t0
     threads = sum(r.threads for r in results)
     gen = sum(r.generated_tokens for r in results)
     prompt = sum(r.prompt_tokens for r in results)
     lats = [x for r in results for x in r.latencies_s]
+    per_rank = [nb.dp_stats()]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor([threads, gen, prompt], dtype=torch.float64, device=dev)
-        dist.all_reduce(c)
-        threads, gen, prompt = (float(x) for x in c.tolist())
-        parts = [None] * world
-        dist.all_gather_object(parts, lats)
-        lats = [x for p in parts for x in p]
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, nb.dp_stats(), group=cpu)
     nb.close()
     if rank == 0:
         value = threads / elapsed
@@ -273,8 +280,13 @@ def _main_node(args, env, groups):
             "config": {"model": args.model, "encoder": args.encoder, "global_batch": args.threads_per_gpu * world,
                        "seq_len": round(prompt / max(threads, 1)), "max_new_tokens": args.max_new, "kv_cache": "bf16",
                        "parallelism": f"dp{world}",
-                       "pipeline": "node: ingestion+parse+chunk+embed+index+select+continuous prefill/decode+report"},
+                       "pipeline": "node: ingestion+parse+chunk+embed+index+select+continuous prefill/decode+report",
+                       "topology": ("services.main node: rank-0 services + a DPNodeWorker per rank (encoder, HBM "
+                                    "index shard, continuous engine) over the TCPStore control plane"
+                                    if world > 1 else "one node on the GPU")},
             "p50_summary_latency_s": round(statistics.median(lats), 3) if lats else None,
+            "p50_summary_latency_regime": "archive submit -> report stored, paced source (<= 2 steps in flight)",
+            "per_rank": per_rank if world > 1 else None,
             "generated_tokens_per_s": round(gen / elapsed, 1), "prompt_tokens_per_s": round(prompt / elapsed, 1),
             "baseline_threads_per_s": round(BASELINE_THREADS_PER_S, 4)}), flush=True)
     if world > 1:

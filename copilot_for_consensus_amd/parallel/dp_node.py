@@ -194,8 +194,11 @@ class DPNodeWorker:
     Rank 0 runs one too (its handlers are called in place)."""
 
     def __init__(self, store, dp_rank: int, dp_size: int, embedder=None, index=None, summarizer=None,
-                 heartbeat_interval: float = 1.0):
+                 heartbeat_interval: float = 1.0, continuous: dict | None = None):
         self.store, self.rank, self.world = store, int(dp_rank), int(dp_size)
+        # the local continuous engine's admission (min_admit, max_wait_s): the summarization
+        # service's settings, which rank 0's service cannot hand to the other ranks' engines itself
+        self.continuous = dict(continuous or {})
         self.embedder, self.index, self.summarizer = embedder, index, summarizer
         self.rpc = StoreRPC(store, self.rank)
         self.rpc.handlers.update({
@@ -220,7 +223,7 @@ class DPNodeWorker:
         self.hb.start()
         start = getattr(self.summarizer, "start_continuous", None)
         if callable(start):
-            start()
+            start(**self.continuous)
         else:
             self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"dp{self.rank}-sum")
         if serve:

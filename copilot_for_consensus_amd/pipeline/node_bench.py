@@ -11,6 +11,13 @@ paced: at most two steps in flight (``CFC_NODE_MAX_INFLIGHT``; 0 queues every st
 backfill's backlog), so stages overlap the way the event-driven services overlap them and the
 reported latency is a step's own.
 
+Under torchrun (``world > 1``) the bench runs the topology ``services.main node`` deploys
+(services/main.py ``_distributed``): global rank 0 runs the services with the DP facades over the
+ranks (parallel/dp_node.py), EVERY rank runs a :class:`~..parallel.dp_node.DPNodeWorker` with its
+own HIP encoder, HBM index shard (1M resident vectors each) and continuous LLM engine; a step is
+one archive of ``threads_per_step x world`` threads (weak scaling), its threads embedded, indexed
+and summarized on their owner GPUs through the node's control plane.
+
 Same model, encoder, threads per step, generated tokens (``LLM_IGNORE_EOS`` as the bench
 pipeline's ``ignore_eos``: random-init weights would otherwise stop at arbitrary points) and
 selection settings (top-5 chunks, 2048-token context) as the bench pipeline.
@@ -46,10 +53,15 @@ class NodeStepResult:
 class NodeBench:
     def __init__(self, model: str = "mistral-7b", encoder: str = "minilm-l6", device="cuda",
                  threads_per_step: int = 128, max_new_tokens: int = 512, seed: int = 0,
-                 index_prefill: int = 1_000_000, continuous: bool = True):
+                 index_prefill: int = 1_000_000, continuous: bool = True, dp: dict | None = None):
+        """``dp`` (torchrun): {"store": the job's TCPStore, "rank": DP rank, "world": DP size} -- the
+        services.main DP topology (rank 0 services + a DPNodeWorker on every rank)."""
         from ..services.node import Node
         from ..utils.synthetic import SyntheticArchive
         dev = str(device)
+        self.dp = dp
+        world = int(dp["world"]) if dp else 1
+        self.rank = int(dp["rank"]) if dp else 0
         self.tmp = Path(tempfile.mkdtemp(prefix="cfc-node-bench-"))
         enc_name = {"minilm-l6": "all-MiniLM-L6-v2"}.get(encoder, encoder)
         self.env = {
@@ -63,8 +75,10 @@ class NodeBench:
             "LLM_KV_CACHE_TOKENS": str(max(65536, threads_per_step * (4096 + max_new_tokens))),
             "SUMMARIZATION_CONTINUOUS_BATCHING": "true" if continuous else "false",
             "SUMMARIZATION_MAX_BATCH_THREADS": str(threads_per_step),
-            # admission: wait for a full batch (or 3 s) -- overridable for A/B runs
-            "SUMMARIZATION_MIN_ADMIT": os.environ.get("CFC_NODE_MIN_ADMIT", str(threads_per_step)),
+            # admission: wait for a full batch (or 3 s) -- overridable for A/B runs.  Under DP a rank
+            # receives ~threads_per_step of a step's threads (hash ownership), not exactly that many
+            "SUMMARIZATION_MIN_ADMIT": os.environ.get(
+                "CFC_NODE_MIN_ADMIT", str(threads_per_step if world == 1 else max(1, (9 * threads_per_step) // 10))),
             "SUMMARIZATION_ADMIT_WAIT_MS": os.environ.get("CFC_NODE_ADMIT_WAIT_MS", "3000"),
             "ORCHESTRATOR_TOP_K": "5", "ORCHESTRATOR_CONTEXT_WINDOW_TOKENS": "2048",
             "INGESTION_STORAGE_PATH": str(self.tmp / "ingest"), "INGESTION_SCHEDULE_INTERVAL_SECONDS": "0",
@@ -72,31 +86,68 @@ class NodeBench:
             "DOCUMENT_STORE_TYPE": "inmemory", "MESSAGE_BUS_TYPE": "inproc",
         }
         t0 = time.time()
-        self.node = Node(env=self.env)
-        print(f"[bench-node] services and models built in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
-        if index_prefill and hasattr(self.node.vectors, "add_embeddings"):
-            # the same 1M-vector resident index the bench pipeline searches next to (rows of other lists)
-            g = torch.Generator(device=dev).manual_seed(seed + 99)
-            dim = int(self.node.embedder.dimension)
-            for s in range(0, index_prefill, 1 << 18):
-                n = min(1 << 18, index_prefill - s)
-                v = torch.randn(n, dim, device=dev, generator=g)
-                self.node.vectors.add_embeddings([f"prefill-{s + i}" for i in range(n)], v, [{} for _ in range(n)])
-        self.node.start(threaded=True)
-        print(f"[bench-node] node running ({time.time() - t0:.1f}s)", file=sys.stderr, flush=True)
-        self.ingestion = self.node.services["ingestion"]
-        self.store = self.node.store
-        self.generator = SyntheticArchive(seed=seed)
+        self.node, self.worker = None, None
+        if dp:
+            self._build_dp(dev, seed, index_prefill, threads_per_step)
+        else:
+            self.node = Node(env=self.env)
+            if index_prefill and hasattr(self.node.vectors, "add_embeddings"):
+                self._prefill_index(self.node.vectors, int(self.node.embedder.dimension), dev, seed, index_prefill)
+        print(f"[bench-node] rank {self.rank}: services and models built in {time.time() - t0:.1f}s",
+              file=sys.stderr, flush=True)
         self.threads_per_step = threads_per_step
+        self.step_threads = threads_per_step * world     # one archive per step for the whole node
+        self.generator = SyntheticArchive(seed=seed)
         self.sources: dict[int, Path] = {}
         self.submitted: dict[int, float] = {}
+        if self.node is not None:
+            self.node.start(threaded=True)
+            print(f"[bench-node] node running ({time.time() - t0:.1f}s)", file=sys.stderr, flush=True)
+            self.ingestion = self.node.services["ingestion"]
+            self.store = self.node.store
+
+    @staticmethod
+    def _prefill_index(index, dim, dev, seed, n_rows):
+        """The same 1M-vector resident index the bench pipeline searches next to (rows of other lists)."""
+        g = torch.Generator(device=dev).manual_seed(seed + 99)
+        for s in range(0, n_rows, 1 << 18):
+            n = min(1 << 18, n_rows - s)
+            v = torch.randn(n, dim, device=dev, generator=g)
+            index.add_embeddings([f"prefill-{s + i}" for i in range(n)], v, [{} for _ in range(n)])
+
+    def _build_dp(self, dev, seed, index_prefill, threads_per_step):
+        """services.main's DP roles on this rank (see the module doc)."""
+        from ..config.loader import get_config
+        from ..embedding import create_embedding_provider
+        from ..parallel.dp_node import DPNodeWorker, build_rank0
+        from ..services.node import Node
+        from ..summarization import create_llm_backend
+        from ..vectorstore import create_vector_store
+        env, dp = self.env, self.dp
+        ecfg, scfg = get_config("embedding", env=env), get_config("summarization", env=env)
+        embedder = create_embedding_provider(ecfg.embedding_backend)
+        index = create_vector_store(ecfg.vector_store, dimension=int(embedder.dimension))
+        if index_prefill:
+            self._prefill_index(index, int(embedder.dimension), dev, seed + 7919 * self.rank, index_prefill)
+        local = create_llm_backend(scfg.llm_backend)
+        self.worker = DPNodeWorker(dp["store"], self.rank, int(dp["world"]), embedder, index, local,
+                                   continuous=dict(min_admit=int(scfg.min_admit),
+                                                   max_wait_s=scfg.admit_wait_ms / 1000.0))
+        if self.rank == 0:
+            vs, summ = build_rank0(dp["store"], int(dp["world"]), self.worker,
+                                   heartbeat_timeout=float(os.environ.get("CFC_DP_HEARTBEAT_TIMEOUT", "60")))
+            self.dp_facades = (vs, summ)
+            self.node = Node(env=env, summarizer=summ, vector_store=vs, embedding_provider=embedder)
+            self.worker.start(serve=False)
+        else:
+            self.worker.start(serve=True)
 
     def prepare_sources(self, steps) -> None:
         """The steps' archives as local mailing-list sources (outside the timed region)."""
         for s in steps:
             d = self.tmp / f"src{s}"
             d.mkdir(parents=True, exist_ok=True)
-            (d / f"step{s}.mbox").write_bytes(self.generator.mbox(self.threads_per_step))
+            (d / f"step{s}.mbox").write_bytes(self.generator.mbox(self.step_threads))
             self.sources[s] = d
 
     def _submit(self, step: int) -> tuple[list[str], float]:
@@ -129,7 +180,7 @@ class NodeBench:
             # most one step is upstream (ingest..orchestrate) at a time.  Submitting two at once made
             # their threads interleave into both engine batches, so the pair finished together and
             # the next pair's upstream ran with the GPU idle (profiles/r04_bench_node_*timeline*)
-            if ce is None or ce.stats["admitted"] - base >= self.threads_per_step * len(subs):
+            if ce is None or ce.stats["admitted"] - base >= self.step_threads * len(subs):
                 return True
             # a step whose threads cannot all reach the engine must not stall the source for good
             return bool(subs) and time.time() - max(t0 for _, t0 in subs.values()) > 30.0
@@ -173,7 +224,7 @@ class NodeBench:
             aids, t0 = subs[s]
             tids = tids_of.get(s)
             if tids is None:
-                if self.store.count_documents("threads", {"archive_id": {"$in": aids}}) < self.threads_per_step:
+                if self.store.count_documents("threads", {"archive_id": {"$in": aids}}) < self.step_threads:
                     time.sleep(0.1)
                     continue
                 tids = tids_of[s] = self._thread_ids(aids)
@@ -197,25 +248,41 @@ class NodeBench:
         return out
 
     def _engine(self):
+        if self.node is None:
+            return None
         llm = getattr(self.node.services.get("summarization"), "summarizer", None)
         return getattr(llm, "_ce", None)
 
     def engine_stats(self) -> dict:
         """The summarizer's continuous-engine counters (admissions, decode steps, prefill / decode s)."""
-        llm = getattr(self.node.services.get("summarization"), "summarizer", None)
-        ce = getattr(llm, "_ce", None)
+        ce = self._engine() if self.node is not None else getattr(getattr(self.worker, "summarizer", None), "_ce", None)
         return dict(ce.stats) if ce is not None else {}
 
+    def dp_stats(self) -> dict:
+        """This rank's DP worker counters (embedded chunks, summaries, topic queries) + its engine's."""
+        if self.worker is None:
+            return {}
+        eng = getattr(getattr(self.worker, "summarizer", None), "_ce", None)
+        out = {"rank": self.rank, **dict(self.worker.stats)}
+        if eng is not None:
+            out.update(admitted=eng.stats.get("admitted"), finished=eng.stats.get("finished"))
+        return out
+
     def close(self) -> None:
-        print(f"[bench-node] continuous engine: {self.engine_stats()}", file=sys.stderr, flush=True)
-        llm = getattr(self.node.services.get("summarization"), "summarizer", None)
-        ce = getattr(llm, "_ce", None)
-        if ce is not None:
-            subs = {s: round(t0, 3) for s, t0 in self.submitted.items()}
-            print(f"[bench-node] step submit times: {subs}", file=sys.stderr, flush=True)
-            print(f"[bench-node] admissions (t, n, first arrival, last arrival): {ce.admit_log}", file=sys.stderr,
-                  flush=True)
-        self.node.stop()
+        print(f"[bench-node] rank {self.rank} continuous engine: {self.engine_stats()}", file=sys.stderr, flush=True)
+        if self.node is not None:
+            ce = self._engine()
+            if ce is not None:
+                subs = {s: round(t0, 3) for s, t0 in self.submitted.items()}
+                print(f"[bench-node] step submit times: {subs}", file=sys.stderr, flush=True)
+                print(f"[bench-node] admissions (t, n, first arrival, last arrival): {ce.admit_log}",
+                      file=sys.stderr, flush=True)
+            self.node.stop()
+        if self.worker is not None:
+            if self.rank == 0:
+                from ..parallel.dp_node import shutdown_workers
+                shutdown_workers(self.dp["store"])
+                self.dp_facades[0].close()
+            self.worker.stop()
         import shutil
         shutil.rmtree(self.tmp, ignore_errors=True)
-

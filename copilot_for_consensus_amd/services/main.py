@@ -159,7 +159,8 @@ def _distributed() -> dict | None:
         ecfg = get_config("embedding")
         embedder = create_embedding_provider(ecfg.embedding_backend)
         index = create_vector_store(ecfg.vector_store, dimension=int(embedder.dimension))
-        worker = DPNodeWorker(store, groups.dp_rank, groups.dp_size, embedder, index, local)
+        worker = DPNodeWorker(store, groups.dp_rank, groups.dp_size, embedder, index, local,
+                              continuous=dict(min_admit=int(scfg.min_admit), max_wait_s=scfg.admit_wait_ms / 1000.0))
         ctx.update(worker=worker, embedder=embedder)
         if serve:
             # a rank whose heartbeat is older than this is taken for dead and its threads move

@@ -86,3 +86,17 @@ def test_bench_node_pipeline_contract():
     d = _run([sys.executable, "bench.py", "--gpus", "1", "--pipeline", "node", *ARGS])
     _check(d, 1, latency=False)
     assert d["config"]["pipeline"].startswith("node:")
+
+
+def test_bench_node_pipeline_dp_topology_two_ranks():
+    """--pipeline node under torchrun: services.main's DP topology (rank-0 services + a DPNodeWorker on
+    each rank); every thread of every step reported, both ranks embedded and summarized threads."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", "--pipeline", "node", *ARGS]
+    d = _run(cmd)
+    _check(d, 2, latency=False)
+    assert d["config"]["topology"].startswith("services.main node")
+    pr = d["per_rank"]
+    assert [p["rank"] for p in pr] == [0, 1]
+    assert all(p["embedded"] > 0 and p["summaries"] > 0 for p in pr), pr
+    assert sum(p["summaries"] for p in pr) == 2 * 2 * 3      # (warmup + 2 steps) x 2 threads x 2 ranks
