@@ -11,7 +11,11 @@
 //   * Storage: blob container `raw-archives` (archive store driver `azureblob`);
 //   * Key Vault: JWT signing keys and OAuth secrets (secret provider `azurekeyvault`);
 //   * Log Analytics + Application Insights (metrics driver `azure_monitor`);
-//   * user-assigned identities with data-plane RBAC (no connection strings in pods).
+//   * user-assigned identities with data-plane RBAC (no connection strings in pods);
+//   * networking: a vnet (AKS subnet + private-endpoint subnet), private endpoints and private DNS
+//     zones for Cosmos / Key Vault / Storage (and Service Bus on Premium), public access off;
+//   * the auth service's RS256 key pair generated into Key Vault, an Entra ID app registration for
+//     its Microsoft OIDC provider, diagnostic settings and a portal dashboard.
 // Workloads: deploy/k8s/copilot-mi355x.yaml (KEDA scales the stages on subscription backlog).
 targetScope = 'resourceGroup'
 
@@ -40,6 +44,15 @@ param serviceBusSku string = 'Standard'
 @minValue(400)
 param cosmosMaxThroughput int = 4000
 
+@description('Private endpoints + private DNS; the platform services refuse public traffic')
+param enablePrivateNetworking bool = false
+
+@description('Register an Entra ID app for the auth service (needs Graph Application.ReadWrite.OwnedBy)')
+param enableEntraApp bool = false
+
+@description('Public base URL of the gateway (OIDC redirect: <url>/auth/callback)')
+param gatewayUrl string = ''
+
 param tags object = {
   project: 'copilot-for-consensus'
   platform: 'mi355x'
@@ -47,6 +60,14 @@ param tags object = {
 
 var suffix = uniqueString(resourceGroup().id, projectName, environment)
 var base = '${projectName}-${environment}'
+var publicAccess = enablePrivateNetworking ? 'Disabled' : 'Enabled'
+var sbPrivate = enablePrivateNetworking && serviceBusSku == 'Premium'
+var aksSubnet = enablePrivateNetworking ? network.outputs.aksSubnetId : ''
+
+module network 'modules/network.bicep' = if (enablePrivateNetworking) {
+  name: 'network'
+  params: { base: base, location: location, tags: tags }
+}
 
 module identities 'modules/identities.bicep' = {
   name: 'identities'
@@ -65,6 +86,8 @@ module keyVault 'modules/keyvault.bicep' = {
     location: location
     tags: tags
     readerPrincipalIds: [identities.outputs.servicesPrincipalId, identities.outputs.gpuPrincipalId]
+    writerPrincipalIds: [identities.outputs.deployerPrincipalId]
+    publicNetworkAccess: publicAccess
   }
 }
 
@@ -76,6 +99,7 @@ module serviceBus 'modules/servicebus.bicep' = {
     sku: serviceBusSku
     tags: tags
     principalIds: [identities.outputs.servicesPrincipalId, identities.outputs.gpuPrincipalId]
+    publicNetworkAccess: sbPrivate ? 'Disabled' : 'Enabled'
   }
 }
 
@@ -87,6 +111,7 @@ module cosmos 'modules/cosmos.bicep' = {
     maxThroughput: cosmosMaxThroughput
     tags: tags
     principalIds: [identities.outputs.servicesPrincipalId, identities.outputs.gpuPrincipalId]
+    publicNetworkAccess: publicAccess
   }
 }
 
@@ -97,6 +122,7 @@ module storage 'modules/storage.bicep' = {
     location: location
     tags: tags
     principalIds: [identities.outputs.servicesPrincipalId]
+    publicNetworkAccess: publicAccess
   }
 }
 
@@ -111,7 +137,69 @@ module aks 'modules/aks.bicep' = {
     gpuNodeCount: gpuNodeCount
     logAnalyticsId: monitor.outputs.workspaceId
     kubeletIdentityId: identities.outputs.gpuIdentityId
+    subnetId: aksSubnet
   }
+}
+
+module privateDns 'modules/privatedns.bicep' = if (enablePrivateNetworking) {
+  name: 'privatedns'
+  params: { base: base, vnetId: network.outputs.vnetId, tags: tags, includeServiceBus: sbPrivate }
+}
+
+module privateEndpoints 'modules/privateendpoints.bicep' = if (enablePrivateNetworking) {
+  name: 'privateendpoints'
+  params: {
+    base: base
+    location: location
+    tags: tags
+    subnetId: network.outputs.endpointSubnetId
+    targets: concat([
+      { name: 'cosmos', resourceId: cosmos.outputs.accountId, groupId: 'Sql', zoneId: privateDns.outputs.zoneIds.cosmos }
+      { name: 'vault', resourceId: keyVault.outputs.vaultId, groupId: 'vault', zoneId: privateDns.outputs.zoneIds.vault }
+      { name: 'blob', resourceId: storage.outputs.accountId, groupId: 'blob', zoneId: privateDns.outputs.zoneIds.blob }
+    ], sbPrivate ? [
+      { name: 'servicebus', resourceId: serviceBus.outputs.namespaceId, groupId: 'namespace', zoneId: privateDns.outputs.zoneIds.servicebus }
+    ] : [])
+  }
+}
+
+module jwtKeys 'modules/jwtkeys.bicep' = {
+  name: 'jwtkeys'
+  params: {
+    location: location
+    tags: tags
+    vaultName: keyVault.outputs.vaultName
+    identityId: identities.outputs.deployerIdentityId
+  }
+}
+
+module oidcApp 'modules/oidc-app.bicep' = if (enableEntraApp) {
+  name: 'oidc-app'
+  params: {
+    location: location
+    tags: tags
+    appName: '${base}-auth'
+    redirectUris: ['${gatewayUrl}/auth/callback']
+    vaultName: keyVault.outputs.vaultName
+    identityId: identities.outputs.deployerIdentityId
+  }
+}
+
+module diagnostics 'modules/diagnostics.bicep' = {
+  name: 'diagnostics'
+  params: {
+    workspaceId: monitor.outputs.workspaceId
+    cosmosName: '${base}-cosmos-${suffix}'
+    serviceBusName: serviceBus.outputs.namespaceName
+    vaultName: keyVault.outputs.vaultName
+    storageName: storage.outputs.accountName
+    aksName: aks.outputs.clusterName
+  }
+}
+
+module dashboard 'modules/dashboard.bicep' = {
+  name: 'dashboard'
+  params: { base: base, location: location, tags: tags, appInsightsId: monitor.outputs.appInsightsId }
 }
 
 output serviceBusNamespace string = serviceBus.outputs.namespaceName
@@ -122,3 +210,6 @@ output storageAccount string = storage.outputs.accountName
 output keyVaultUri string = keyVault.outputs.vaultUri
 output appInsightsConnectionString string = monitor.outputs.appInsightsConnectionString
 output aksName string = aks.outputs.clusterName
+output jwtPrivateKeySecret string = jwtKeys.outputs.privateKeySecret
+output oidcClientId string = enableEntraApp ? oidcApp.outputs.clientId : ''
+output dashboardId string = dashboard.outputs.dashboardId

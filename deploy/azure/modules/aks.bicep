@@ -12,6 +12,8 @@ param gpuVmSize string
 param gpuNodeCount int
 param logAnalyticsId string
 param kubeletIdentityId string
+@description('Subnet of both node pools (Azure CNI); empty = the cluster-managed network')
+param subnetId string = ''
 
 resource cluster 'Microsoft.ContainerService/managedClusters@2024-05-01' = {
   name: name
@@ -27,6 +29,14 @@ resource cluster 'Microsoft.ContainerService/managedClusters@2024-05-01' = {
     addonProfiles: {
       omsagent: { enabled: true, config: { logAnalyticsWorkspaceResourceID: logAnalyticsId } }
     }
+    // Azure CNI on the project vnet when a subnet is given: pods get vnet addresses and reach the
+    // platform services through their private endpoints
+    networkProfile: empty(subnetId) ? null : {
+      networkPlugin: 'azure'
+      networkPolicy: 'azure'
+      serviceCidr: '10.1.0.0/16'
+      dnsServiceIP: '10.1.0.10'
+    }
     agentPoolProfiles: [
       {
         name: 'system'
@@ -35,6 +45,7 @@ resource cluster 'Microsoft.ContainerService/managedClusters@2024-05-01' = {
         count: 2
         osType: 'Linux'
         osSKU: 'Ubuntu'
+        vnetSubnetID: empty(subnetId) ? null : subnetId
       }
       {
         name: 'instinct'
@@ -43,6 +54,7 @@ resource cluster 'Microsoft.ContainerService/managedClusters@2024-05-01' = {
         count: gpuNodeCount
         osType: 'Linux'
         osSKU: 'Ubuntu'
+        vnetSubnetID: empty(subnetId) ? null : subnetId
         nodeTaints: ['amd.com/gpu=present:NoSchedule']
         nodeLabels: { 'accelerator': 'amd-instinct' }
       }
@@ -51,3 +63,4 @@ resource cluster 'Microsoft.ContainerService/managedClusters@2024-05-01' = {
 }
 
 output clusterName string = cluster.name
+output clusterId string = cluster.id

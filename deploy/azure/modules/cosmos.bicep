@@ -7,6 +7,8 @@ param location string
 param maxThroughput int
 param tags object
 param principalIds array
+@allowed(['Enabled', 'Disabled'])
+param publicNetworkAccess string = 'Enabled'
 
 var databaseName = 'copilot'
 var collections = ['archives', 'messages', 'threads', 'chunks', 'summaries', 'sources']
@@ -21,6 +23,7 @@ resource account 'Microsoft.DocumentDB/databaseAccounts@2024-05-15' = {
     consistencyPolicy: { defaultConsistencyLevel: 'Session' }
     locations: [{ locationName: location, failoverPriority: 0 }]
     disableLocalAuth: true
+    publicNetworkAccess: publicNetworkAccess
   }
 }
 
@@ -58,3 +61,4 @@ resource rbac 'Microsoft.DocumentDB/databaseAccounts/sqlRoleAssignments@2024-05-
 
 output endpoint string = account.properties.documentEndpoint
 output databaseName string = db.name
+output accountId string = account.id

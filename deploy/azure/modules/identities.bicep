@@ -15,6 +15,15 @@ resource gpu 'Microsoft.ManagedIdentity/userAssignedIdentities@2023-01-31' = {
   tags: tags
 }
 
+// the deployment scripts' identity (JWT key generation, OIDC app registration)
+resource deployer 'Microsoft.ManagedIdentity/userAssignedIdentities@2023-01-31' = {
+  name: '${base}-deploy-id'
+  location: location
+  tags: tags
+}
+
+output deployerIdentityId string = deployer.id
+output deployerPrincipalId string = deployer.properties.principalId
 output servicesPrincipalId string = services.properties.principalId
 output gpuPrincipalId string = gpu.properties.principalId
 output gpuIdentityId string = gpu.id

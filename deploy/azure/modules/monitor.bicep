@@ -26,4 +26,5 @@ resource insights 'Microsoft.Insights/components@2020-02-02' = {
 }
 
 output workspaceId string = workspace.id
+output appInsightsId string = insights.id
 output appInsightsConnectionString string = insights.properties.ConnectionString

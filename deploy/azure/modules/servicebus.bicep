@@ -10,6 +10,9 @@ param location string
 param sku string
 param tags object
 param principalIds array
+@description('Disabled needs the Premium tier (private endpoint)')
+@allowed(['Enabled', 'Disabled'])
+param publicNetworkAccess string = 'Enabled'
 
 var topicName = 'copilot.events'
 var subscriptions = [
@@ -26,7 +29,7 @@ resource ns 'Microsoft.ServiceBus/namespaces@2022-10-01-preview' = {
   location: location
   tags: tags
   sku: { name: sku, tier: sku }
-  properties: { disableLocalAuth: true, minimumTlsVersion: '1.2' }
+  properties: { disableLocalAuth: true, minimumTlsVersion: '1.2', publicNetworkAccess: publicNetworkAccess }
 }
 
 resource topic 'Microsoft.ServiceBus/namespaces/topics@2022-10-01-preview' = {
@@ -71,3 +74,4 @@ resource access 'Microsoft.Authorization/roleAssignments@2022-04-01' = [for p in
 
 output namespaceName string = ns.name
 output topicName string = topic.name
+output namespaceId string = ns.id

@@ -4,6 +4,8 @@ param name string
 param location string
 param tags object
 param principalIds array
+@allowed(['Enabled', 'Disabled'])
+param publicNetworkAccess string = 'Enabled'
 
 resource account 'Microsoft.Storage/storageAccounts@2023-05-01' = {
   name: name
@@ -16,6 +18,7 @@ resource account 'Microsoft.Storage/storageAccounts@2023-05-01' = {
     allowSharedKeyAccess: false
     minimumTlsVersion: 'TLS1_2'
     supportsHttpsTrafficOnly: true
+    publicNetworkAccess: publicNetworkAccess
   }
 }
 
@@ -44,3 +47,4 @@ resource access 'Microsoft.Authorization/roleAssignments@2022-04-01' = [for p in
 }]
 
 output accountName string = account.name
+output accountId string = account.id

@@ -43,7 +43,8 @@ def _top_keys(obj):
 def test_modules_exist_and_parameters_match():
     main = (AZ / "main.bicep").read_text()
     seen = set()
-    for m in re.finditer(r"^module\s+(\w+)\s+'([^']+)'\s*=\s*\{", main, re.M):
+    # `module x 'path' = {` or a conditional `module x 'path' = if (cond) {`
+    for m in re.finditer(r"^module\s+(\w+)\s+'([^']+)'\s*=\s*(?:if\s*\([^)]*\)\s*)?\{", main, re.M):
         path = AZ / m.group(2)
         assert path.exists(), path
         seen.add(path.name)
@@ -91,3 +92,21 @@ def test_cosmos_containers_are_the_document_collections():
     cos = (AZ / "modules" / "cosmos.bicep").read_text()
     got = re.search(r"var collections = \[([^\]]*)\]", cos).group(1)
     assert set(re.findall(r"'(\w+)'", got)) == set(COLLECTIONS)
+
+
+def test_deployment_scripts_write_the_secrets_the_drivers_read():
+    """The JWT key pair and the Entra app credentials land under the Key Vault names the secret-
+    sourced driver configs ask for (the azurekeyvault provider maps _ to -)."""
+    cfg = AZ.parent / "schemas" / "configs" / "adapters" / "drivers"
+    jwt = json.loads((cfg / "jwt_signer" / "local.json").read_text())["properties"]
+    ms = json.loads((cfg / "oidc_providers" / "microsoft.json").read_text())["properties"]
+    keys = (AZ / "modules" / "jwtkeys.bicep").read_text()
+    app = (AZ / "modules" / "oidc-app.bicep").read_text()
+    for field in ("private_key", "public_key"):
+        if field in jwt and jwt[field].get("secret_name"):
+            assert f"-n {jwt[field]['secret_name'].replace('_', '-')} " in keys, field
+    for field in ("microsoft_client_id", "microsoft_client_secret"):
+        assert f"-n {ms[field]['secret_name'].replace('_', '-')} " in app, field
+    main = (AZ / "main.bicep").read_text()
+    for mod in ("network", "privatedns", "privateendpoints", "jwtkeys", "oidc-app", "diagnostics", "dashboard"):
+        assert f"'modules/{mod}.bicep'" in main, mod
