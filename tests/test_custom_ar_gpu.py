@@ -272,6 +272,7 @@ def test_tp2_mistral7b_matches_tp1_greedy():
     assert exact >= 0.9 * n, f"TP=2 matched TP=1's argmax in {exact}/{n} teacher-forced steps"
 
 
+@pytest.mark.timeout(900)
 def test_tp2_llama3_70b_matches_tp1_teacher_forced():
     """Llama-3-70B at TP=2 as two processes on the one GPU (each generates only its 70.5 GB shard:
     32 q / 4 kv heads, FFN 14336 per rank, vocab shard 64128), greedy decode in the captured graph
