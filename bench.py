@@ -61,6 +61,10 @@ def parse_args(argv=None):
                     help="a second latency point at a light load (the reference's one-thread-at-a-time regime): "
                          "Poisson arrivals per second per GPU (0 = skip)")
     ap.add_argument("--latency-low-threads", type=int, default=12, help="threads the light-load probe serves")
+    ap.add_argument("--service-latency-rate", type=float, default=0.5,
+                    help="the light-load point through the real services (pipeline/node_bench.py: archive submit "
+                         "-> report stored), Poisson arrivals per second per GPU (0 = skip; TP=1 only)")
+    ap.add_argument("--service-latency-threads", type=int, default=12)
     ap.add_argument("--pipeline", choices=["bench", "node"], default="bench",
                     help="bench: the stage code with a static LLM batch (headline); node: the real services "
                          "(Node, in-proc bus, continuous summarization engine), pipeline/node_bench.py")
@@ -172,6 +176,30 @@ def main(argv=None):
     latency = probe_point(probe_steps, args.latency_rate, args.seed + 104729 * groups.dp_rank) if probe_steps else None
     latency_low = (probe_point(low_steps, args.latency_low_rate, args.seed + 7919 + 104729 * groups.dp_rank,
                                max_threads=args.latency_low_threads) if low_steps else None)
+    service_light = None
+    if args.service_latency_rate > 0 and args.tp == 1 and not args.llm_only:
+        # the light-load point again, through the deployment's services on this GPU (a node beside
+        # the bench pipeline's model: its own encoder, index and decoder), admitting each thread on
+        # arrival as a lightly loaded summarization service does
+        from copilot_for_consensus_amd.pipeline.node_bench import NodeBench
+        barrier()
+        nb = NodeBench(model=args.model, encoder=args.encoder, device=dev, threads_per_step=args.threads_per_gpu,
+                       max_new_tokens=args.max_new, seed=args.seed + 7919 * groups.dp_rank,
+                       index_prefill=args.index_prefill, min_admit=1, admit_wait_ms=50)
+        try:
+            sp = nb.light_load_probe(args.service_latency_rate, args.service_latency_threads,
+                                     seed=args.seed + 271 * groups.dp_rank)
+        finally:
+            nb.close()
+        if world > 1:
+            parts = [None] * world
+            dist.all_gather_object(parts, sp)
+        else:
+            parts = [sp]
+        service_light = dict(parts[0])
+        service_light.update(threads=sum(p["threads"] for p in parts),
+                             p50_s=round(statistics.median([p["p50_s"] for p in parts]), 3),
+                             p95_s=round(max(p["p95_s"] for p in parts), 3))
     if rank == 0:
         out = {
             "metric": "end-to-end threads summarized/sec + p50 summary latency, Mistral-7B TP=1/8",
@@ -207,6 +235,8 @@ def main(argv=None):
             # latency half of the metric at a stated arrival rate below saturation (continuous engine)
             "latency_mode": latency,
             "latency_mode_light": latency_low,
+            # the same light load through the real services (archive submit -> report stored)
+            "latency_service_light": service_light,
             "generated_tokens_per_s": round(gen_tokens / elapsed, 1),
             "prompt_tokens_per_s": round(prompt_tokens / elapsed, 1),
             "baseline_threads_per_s": round(BASELINE_THREADS_PER_S, 4),

@@ -53,7 +53,8 @@ class NodeStepResult:
 class NodeBench:
     def __init__(self, model: str = "mistral-7b", encoder: str = "minilm-l6", device="cuda",
                  threads_per_step: int = 128, max_new_tokens: int = 512, seed: int = 0,
-                 index_prefill: int = 1_000_000, continuous: bool = True, dp: dict | None = None):
+                 index_prefill: int = 1_000_000, continuous: bool = True, dp: dict | None = None,
+                 min_admit: int | None = None, admit_wait_ms: int | None = None):
         """``dp`` (torchrun): {"store": the job's TCPStore, "rank": DP rank, "world": DP size} -- the
         services.main DP topology (rank 0 services + a DPNodeWorker on every rank)."""
         from ..services.node import Node
@@ -77,9 +78,10 @@ class NodeBench:
             "SUMMARIZATION_MAX_BATCH_THREADS": str(threads_per_step),
             # admission: wait for a full batch (or 3 s) -- overridable for A/B runs.  Under DP a rank
             # receives ~threads_per_step of a step's threads (hash ownership), not exactly that many
-            "SUMMARIZATION_MIN_ADMIT": os.environ.get(
+            "SUMMARIZATION_MIN_ADMIT": str(min_admit) if min_admit is not None else os.environ.get(
                 "CFC_NODE_MIN_ADMIT", str(threads_per_step if world == 1 else max(1, (9 * threads_per_step) // 10))),
-            "SUMMARIZATION_ADMIT_WAIT_MS": os.environ.get("CFC_NODE_ADMIT_WAIT_MS", "3000"),
+            "SUMMARIZATION_ADMIT_WAIT_MS": str(admit_wait_ms) if admit_wait_ms is not None else os.environ.get(
+                "CFC_NODE_ADMIT_WAIT_MS", "3000"),
             "ORCHESTRATOR_TOP_K": "5", "ORCHESTRATOR_CONTEXT_WINDOW_TOKENS": "2048",
             "INGESTION_STORAGE_PATH": str(self.tmp / "ingest"), "INGESTION_SCHEDULE_INTERVAL_SECONDS": "0",
             "ARCHIVE_STORE_TYPE": "local", "ARCHIVE_BASE_PATH": str(self.tmp / "archives"),
@@ -246,6 +248,58 @@ class NodeBench:
             pending.pop(0)
             refill()
         return out
+
+    def light_load_probe(self, rate_per_s: float, n_threads: int, seed: int = 0, timeout_s: float = 600.0) -> dict:
+        """The latency half through the services at a light load: ``n_threads`` one-thread archives
+        enter the ingestion service as a Poisson process of ``rate_per_s`` (each a local source, as a
+        mailing list delivering one new thread); a thread's latency is archive submit -> its report
+        stored by the reporting service (ingest, parse, chunk, embed, index, select, prefill +
+        decode, report: every hop on the in-process bus).  The reference's figure of merit at one
+        thread at a time (summarization/app/service.py:329-345 summarization_latency_seconds covers
+        the LLM call only; this covers the whole path)."""
+        import numpy as np
+        from ..utils.synthetic import SyntheticArchive
+        gen = SyntheticArchive(seed=seed + 31337)
+        srcs = []
+        for i in range(n_threads):
+            d = self.tmp / f"light{seed}-{i}"
+            d.mkdir(parents=True, exist_ok=True)
+            (d / "one.mbox").write_bytes(gen.mbox(1))
+            srcs.append(d)
+        rng = np.random.default_rng(seed)
+        arrive = np.cumsum(rng.exponential(1.0 / float(rate_per_s), n_threads))
+        t0 = time.time()
+        sub: dict[int, tuple[list[str], float]] = {}
+        lat: dict[int, float] = {}
+        nxt = 0
+        deadline = t0 + float(arrive[-1]) + timeout_s
+        while len(lat) < n_threads:
+            now = time.time()
+            if now > deadline:
+                raise TimeoutError(f"light-load probe: {n_threads - len(lat)} threads unfinished")
+            while nxt < n_threads and t0 + arrive[nxt] <= now:
+                ts = time.time()
+                ids = self.ingestion.ingest_archive({"name": f"light-{seed}-{nxt}", "source_type": "local",
+                                                    "url": str(srcs[nxt]), "enabled": True})
+                sub[nxt] = (ids, ts)
+                nxt += 1
+            for i, (aids, ts) in list(sub.items()):
+                if i in lat:
+                    continue
+                tids = self._thread_ids(aids)
+                if not tids:
+                    continue
+                reps = self.store.query_documents("summaries", {"thread_id": {"$in": tids}}, limit=len(tids) + 4)
+                if len({r["thread_id"] for r in reps}) < len(tids):
+                    continue
+                done = max(datetime.fromisoformat(r["generated_at"].replace("Z", "+00:00")).timestamp() for r in reps)
+                lat[i] = max(0.0, done - ts)
+            time.sleep(0.02)
+        v = np.asarray([lat[i] for i in range(n_threads)])
+        return {"arrival_rate_per_gpu": float(rate_per_s), "threads": int(n_threads),
+                "p50_s": round(float(np.percentile(v, 50)), 3), "p95_s": round(float(np.percentile(v, 95)), 3),
+                "path": "services: archive submit (ingestion) -> report stored (reporting), in-proc bus, "
+                        "continuous engine admitting each thread on arrival"}
 
     def _engine(self):
         if self.node is None:

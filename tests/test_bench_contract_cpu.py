@@ -14,7 +14,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ARGS = ["--model", "tiny", "--encoder", "tiny", "--threads-per-gpu", "2", "--max-new", "3", "--steps", "2",
-        "--warmup", "1", "--index-prefill", "0", "--prefill-tokens", "4096"]
+        "--warmup", "1", "--index-prefill", "0", "--prefill-tokens", "4096", "--service-latency-threads", "3"]
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
         "vs_baseline", "dtype", "data", "config"}
 
@@ -52,6 +52,10 @@ def _check(d, n, latency=True):
     ll = d["latency_mode_light"]
     assert ll["threads"] == 2 * n and ll["arrival_rate_per_gpu"] == 0.5
     assert 0 < ll["p50_s"] <= ll["p95_s"]
+    # and through the services: archive submit -> report stored, one-thread archives at 0.5 / s
+    sl = d["latency_service_light"]
+    assert sl["threads"] == 3 * n and sl["arrival_rate_per_gpu"] == 0.5 and sl["path"].startswith("services")
+    assert 0 < sl["p50_s"] <= sl["p95_s"]
 
 
 def test_bench_single_process_contract():
