@@ -223,6 +223,9 @@ class NodeBench:
             if time.time() > deadline:
                 raise TimeoutError(f"node bench: steps {pending} unfinished after {timeout_s}s")
             s = pending[0]
+            if s not in subs:                     # paced: not submitted yet (the running step drains first)
+                time.sleep(0.05)
+                continue
             aids, t0 = subs[s]
             tids = tids_of.get(s)
             if tids is None:
