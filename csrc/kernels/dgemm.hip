@@ -46,10 +46,12 @@ template <int BN>
 constexpr int dg_loaders() { return BN / 16 >= 7 ? 1 : 8 - BN / 16 > 2 ? 2 : 8 - BN / 16; }
 enum { DG_PART = 0, DG_BF16 = 1, DG_SILU = 2 };
 
-template <int BM, int BN>
+// MX (ablation 64): two X-loader waves and an 8-slot X ring whatever BN -- one loader wave's
+// vmcnt window (63 pieces = 3 stages at BM = 128) may cap the X stream of the wide-BN shapes.
+template <int BM, int BN, bool MX = false>
 struct DgShape {
   static constexpr int NW = BN / 16;                  // compute waves
-  static constexpr int LOADERS = dg_loaders<BN>();
+  static constexpr int LOADERS = MX ? 2 : dg_loaders<BN>();
   static constexpr int WAVES = NW + LOADERS;
   static constexpr int MT = BM / 16;                  // m-tiles per compute wave
   // W register ring depth (64-deep stages); 9 waves (BN = 128) leave 168 VGPRs per lane
@@ -58,7 +60,7 @@ struct DgShape {
   static constexpr int XP = BM / 8 / LOADERS;         // 1-KB DMA pieces per loader wave per stage
   // X ring slots (64-128 KB); a loader keeps NSX - 2 stages in flight at its wait, and vmcnt
   // counts at most 63 of its pieces
-  static constexpr int NSX_BASE = BM == 256 ? 4 : (BM == 128 ? 6 : 8);
+  static constexpr int NSX_BASE = MX ? 8 : (BM == 256 ? 4 : (BM == 128 ? 6 : 8));
   static constexpr int NSX = (NSX_BASE - 2 <= 63 / XP ? NSX_BASE : 2 + 63 / XP);
 };
 
@@ -120,7 +122,10 @@ __device__ __forceinline__ uint4 dg_ldw(const uint16_t* p) {
 // ABL: ablation builds for the timing probes only (scripts/bench_dgemm.py --ablate); 0 in production.
 //   1 = no X DMA, 2 = no ds_read / MFMA (W loads kept live), 4 = no K-order rotation,
 //   16 = X first: the loaders' first X stages enter the CU's memory pipeline before the compute
-//   waves' W ring fill (one extra barrier), so the first MFMAs do not wait behind ~96 KB of W.
+//   waves' W ring fill (one extra barrier), so the first MFMAs do not wait behind ~96 KB of W;
+//   32 = contiguous W pieces: wave w loads fragments 2w, 2w+1 of the stage's 2 NW KB region (one
+//   2-KB run per wave) instead of its own group's two 1-KB fragments NW KB apart (wrong sums);
+//   64 = two X-loader waves + an 8-slot X ring (DgShape MX).
 // PACKED: W in the fragment-packed layout of cfc_dgemm_pack for this BN: tile-major, then 32-deep
 // k group, then wave: Wp[N/BN][K/32][BN/16][64][8], so the 16 rows x 32 k of one MFMA B fragment
 // are 1 KB contiguous in lane order and a workgroup's whole W slice (BN rows x its K range) is ONE
@@ -131,10 +136,10 @@ __device__ __forceinline__ uint4 dg_ldw(const uint16_t* p) {
 // the workgroup's span) so the cache policy can be set: NTW = nontemporal for these once-read
 // bytes (guide "nt-weights").
 template <int BM, int BN, int EPI, bool NTW, int ABL = 0, bool PACKED = true>
-__global__ void __launch_bounds__((64 * DgShape<BM, BN>::WAVES), 1)
+__global__ void __launch_bounds__((64 * DgShape<BM, BN, (ABL & 64) != 0>::WAVES), 1)
     dgemm_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W, int M, int N, int K, int ntiles,
                  int split, float* __restrict__ part, uint16_t* __restrict__ out, int ldo) {
-  using S = DgShape<BM, BN>;
+  using S = DgShape<BM, BN, (ABL & 64) != 0>;
   constexpr int NW = S::NW;
   constexpr int D = S::D;
   __shared__ __attribute__((aligned(16))) char smem[S::NSX * S::XSTAGE];
@@ -197,7 +202,7 @@ __global__ void __launch_bounds__((64 * DgShape<BM, BN>::WAVES), 1)
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(((uintptr_t)span_hi << 32) | span_lo), (short)0, PACKED ? BN * K * 2 : 0, 0x00020000);
   const int wvoff = lane * 16;                                                   // per-lane byte offset
-  const int wsoff = __builtin_amdgcn_readfirstlane(((kb * 2) * NW + w) * 1024);  // k group 2 kb, wave w
+  const int wsoff = __builtin_amdgcn_readfirstlane(((kb * 2) * NW + ((ABL & 32) ? 2 * w : w)) * 1024);
   // row-major: this lane's row and k offset
   const uint16_t* wp = W + (size_t)(n0 + 16 * w + (lane & 15)) * K + (size_t)kb * 64 + 8 * kq;
   // stage s of this lane: the kk = 0 and kk = 1 halves of its B fragments
@@ -205,7 +210,7 @@ __global__ void __launch_bounds__((64 * DgShape<BM, BN>::WAVES), 1)
     if constexpr (PACKED) {
       const int so = __builtin_amdgcn_readfirstlane(wsoff + s * 2 * NW * 1024);
       dst[0] = dg_ldw_buf<NTW>(wrs, wvoff, so);
-      dst[1] = dg_ldw_buf<NTW>(wrs, wvoff, so + NW * 1024);
+      dst[1] = dg_ldw_buf<NTW>(wrs, wvoff, so + ((ABL & 32) ? 1024 : NW * 1024));
     } else {
       dst[0] = dg_ldw<NTW>(wp + s * 64);
       dst[1] = dg_ldw<NTW>(wp + s * 64 + 32);
@@ -295,7 +300,7 @@ int dgemm_launch_bn(const void* x, const void* w, int M, int N, int K, int split
                     int ldo, hipStream_t stream) {
   const int ntiles = N / BN;
   const dim3 grid(ntiles * split, (M + BM - 1) / BM);
-  const int threads = 64 * DgShape<BM, BN>::WAVES;
+  const int threads = 64 * DgShape<BM, BN, (ABL & 64) != 0>::WAVES;
 #define DG_ARGS (const uint16_t*)x, (const uint16_t*)w, M, N, K, ntiles, split, part, (uint16_t*)out, ldo
   switch (epi) {
     case DG_PART: dgemm_kernel<BM, BN, DG_PART, NTW, ABL, PK><<<grid, threads, 0, stream>>>(DG_ARGS); break;
@@ -389,7 +394,7 @@ CFC_API int cfc_dgemm_pack(const void* w, void* wp, int N, int K, int bn, hipStr
 // (not nontemporal) cache policy on the weight stream.
 CFC_API int cfc_dgemm_ablate(const void* x, const void* w, int M, int N, int K, int split, int bn, int abl,
                              float* part, hipStream_t stream) {
-  if (M > 128 || (abl & ~31)) return -1;
+  if (M > 128 || (abl & ~127)) return -1;
   if (const int e = dgemm_check(M, N, K, split, DG_PART, bn, part, nullptr)) return e;
   int rc;
   switch (abl) {
@@ -403,6 +408,10 @@ CFC_API int cfc_dgemm_ablate(const void* x, const void* w, int M, int N, int K, 
     case 8: DG_ABL(0, false)
     case 11: DG_ABL(3, false)
     case 16: DG_ABL(16, true)
+    case 32: DG_ABL(32, true)
+    case 35: DG_ABL(35, true)
+    case 64: DG_ABL(64, true)
+    case 96: DG_ABL(96, true)
 #undef DG_ABL
     default: return -3;
   }

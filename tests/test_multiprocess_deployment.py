@@ -31,12 +31,31 @@ FIX = os.path.join(ROOT, "tests", "fixtures", "sample.mbox")
 SERVICES = ("ingestion", "parsing", "chunking", "embedding", "orchestrator", "summarization", "reporting")
 
 
+_TAKEN: set[int] = set()
+
+
 def _free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A free port BELOW the kernel's ephemeral range: a port bind(0) hands out stays in that range,
+    so another process's outgoing connection could take it before the service binds it (seen as
+    "address already in use" when the services start one after another)."""
+    import random
+    try:
+        lo = int(open("/proc/sys/net/ipv4/ip_local_port_range").read().split()[0])
+    except (OSError, ValueError):
+        lo = 32768
+    rng = random.Random()
+    for _ in range(1000):
+        p = rng.randrange(max(1024, lo - 12000), lo)
+        if p in _TAKEN:
+            continue
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", p))
+            except OSError:
+                continue
+        _TAKEN.add(p)
+        return p
+    raise RuntimeError("no free port below the ephemeral range")
 
 
 def _http(method: str, url: str, body=None, headers=None, timeout=10):
