@@ -463,6 +463,8 @@ class DecoderModel:
         # (written by another XCD, served from the MALL) stall the weight stream behind them:
         # Mistral-7B 307.7 vs 313.5 tok/s, Llama-2-13B 177.1 vs 190.9 (profiles/r04_gemv_norm_ab.log)
         self.gemv_norm_fused = os.environ.get("CFC_DECODE_GEMV_NORM", "0") == "1"
+        # split-K of the batched qkv decode GEMM (its slabs feed rope_kv): 0 = the cost model's pick
+        self.qkv_split = int(os.environ.get("CFC_DECODE_QKV_SPLIT", "0"))
         # B <= 4 decode on the ggml-quantized weights (GGUF checkpoints; csrc/kernels/quant.hip)
         self.decode_qgemv = (weights.qlayers is not None and os.environ.get("CFC_DECODE_QGEMV", "1") != "0"
                              and weights.tp_size == 1 and weights.gate_up_interleaved and not self.fp8)
@@ -672,6 +674,7 @@ class DecoderModel:
             pw = w.packed[i] if w.packed is not None else lw    # fragment-packed copies when present
             wq = pw["qkv"]
             qbn, qsplit = K.dgemm_config(B, wq.shape[0], h.shape[1], bn=getattr(wq, "bn", None))
+            qsplit = self.qkv_split or qsplit
             # split-K slabs go straight into RoPE / KV write (the reduce folded in)
             qkv = K.dgemm(h, wq, "part", qsplit, bn=qbn) if qsplit > 1 else K.dgemm_linear(h, wq)
             attn = self._rope_attention(i, qkv, positions, slots, ctx_lens, block_tables, kv, attn_workspace,

@@ -162,8 +162,12 @@ class EncoderModel:
 
     # projection GEMMs: the hand-written pgemm (csrc/kernels/pgemm.hip, bias / bias+GELU fused in
     # its epilogue) where it measured at or above hipBLASLt -- the small-K (K <= 512) shapes of the
-    # MiniLM-class encoders (qkv 1.10x, o 1.06x, up+GELU 0.98x vs library GEMM + bias_gelu:
-    # profiles/r03_pgemm_v1_vs_hipblaslt.log); the library GEMM for K >= 768 (BGE-base).
+    # MiniLM-class encoders (profiles/r03_pgemm_v1_vs_hipblaslt.log); the library GEMM for K >= 768
+    # (BGE-base).  Re-measured in round 5 with the decoder's ping-pong kernels in the race
+    # (profiles/r05_pgemm_encoder_variants.jsonl, 32k rows): MiniLM qkv+bias 442 TF/s (2-stage) vs
+    # 433 library, up+GELU 426 vs 407 -- the ping-pong variants lose there (313 / 287: K = 384 is six
+    # K-tiles, too short for their pipeline); BGE-base qkv+bias 746 vs 938 library, up+GELU 668 vs
+    # 675, down 1166 (pps) vs 1195 -- so the K <= 512 threshold stands.
     # CFC_ENCODER_GEMM = auto | hip | lib.
     PGEMM_MAX_K = 512
 
