@@ -98,9 +98,14 @@ class RagPipeline:
             vectors = _ShardedRows(self.sharded)
         self.index = self.local_index
         if index_prefill:
+            # in 16M-row pieces: a 100M-row index (BASELINE config 5) would need 154 GB of fp32 noise
+            # at once next to its own 77 GB
             g = torch.Generator(device=self.device).manual_seed(seed + 99)
-            noise = torch.randn(index_prefill, self.embedder.dimension, device=self.device, generator=g)
-            self.index.add_bulk([f"prefill-{i}" for i in range(index_prefill)], noise)
+            for s in range(0, index_prefill, 1 << 24):
+                n = min(1 << 24, index_prefill - s)
+                noise = torch.randn(n, self.embedder.dimension, device=self.device, generator=g)
+                self.index.add_bulk([f"prefill-{i}" for i in range(s, s + n)], noise)
+                del noise
         pub = publisher or NoopPublisher()
         self.pub = ValidatingEventPublisher(pub) if validate_events else pub
         # the node's services over one store; no subscriber: this driver hands each stage its input
