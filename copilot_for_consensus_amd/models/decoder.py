@@ -96,6 +96,10 @@ PRESETS: dict[str, DecoderConfig] = {
     "tiny-mha": DecoderConfig("tiny-mha", 512, 256, 2, 2, 2, 128, 512, rope_theta=1e4, max_positions=4096),
     "tiny": DecoderConfig("tiny", 512, 256, 2, 4, 2, 128, 512, rope_theta=1e4, max_positions=4096),
     "small": DecoderConfig("small", 32000, 1024, 4, 8, 2, 128, 2816, rope_theta=1e6, max_positions=8192),
+    # Mistral / Llama-3-8B's head layout (32 q / 8 kv, head_dim 128) at GPU-test size: TP=8 leaves one
+    # kv head per rank and every per-rank projection still fits the decode / prefill GEMMs (N, K % 64)
+    "tiny-gqa8": DecoderConfig("tiny-gqa8", 32768, 1024, 2, 32, 8, 128, 2048, rope_theta=1e6,
+                               max_positions=4096),
     # Llama-3-70B's head layout (64 q / 8 kv heads: TP=8 leaves ONE kv head per rank) at CPU-test
     # size, for the TP=4 / TP=8 shard paths on gloo (tests/test_tp_wide_cpu.py)
     "tiny-70b-heads": DecoderConfig("tiny-70b-heads", 512, 512, 2, 64, 8, 32, 1024, rope_theta=5e5,

@@ -189,18 +189,19 @@ def test_tp2_decoder_with_oneshot_allreduce_matches_tp1():
     assert agree >= 0.9 * sum(len(x) for x in ref), (res[0]["tokens"], ref)
 
 
-def _run_tp2(prompts, n_new, **kw):
+def _run_tp2(prompts, n_new, world=2, **kw):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, q, prompts, n_new), kwargs=kw) for r in range(2)]
+    procs = [ctx.Process(target=_tp_worker, args=(r, world, port, q, prompts, n_new), kwargs=kw)
+             for r in range(world)]
     for p in procs:
         p.start()
     res = {}
     try:
         for _ in procs:
-            r, out = q.get(timeout=280)
+            r, out = q.get(timeout=280 if world <= 2 else 400)
             res[r] = out
     finally:
         for p in procs:
@@ -322,3 +323,41 @@ def test_tp2_llama3_70b_matches_tp1_teacher_forced():
     torch.cuda.empty_cache()
     assert worst <= 0.5, f"a TP=2 token is {worst:.3f} sigma below TP=1's best (exact {exact}/{n})"
     assert exact >= 0.8 * n, f"TP=2 matched TP=1's argmax in {exact}/{n} teacher-forced steps"
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("tp", [4, 8])
+def test_tp_wide_one_kv_head_per_rank_oneshot_ar_gpu(tp):
+    """TP=4 / TP=8 as 4 / 8 processes sharing the GPU (preset tiny-gqa8: 32 q / 8 kv heads of 128, so
+    TP=8 leaves ONE kv head and 4 q heads per rank): the decode attention, RoPE / KV write and
+    split-K GEMMs at those per-rank shapes, the one-shot IPC all-reduce and the argmax key-max over
+    4 / 8 peers inside the captured decode graph; every rank's greedy tokens equal, teacher-forced
+    against the unsharded model as in test_tp2_mistral7b_matches_tp1_greedy."""
+    from copilot_for_consensus_amd.models.decoder import DecoderModel, DecoderWeights, get_config
+    from copilot_for_consensus_amd.runtime.engine import LLMEngine
+    from copilot_for_consensus_amd.runtime.kv_cache import PagedKVCache
+    cfg = get_config("tiny-gqa8")
+    g = torch.Generator().manual_seed(13)
+    prompts = [[1] + torch.randint(3, cfg.vocab_size, (n,), generator=g).tolist() for n in (37, 300, 5, 129, 64, 800)]
+    n_new = 16
+    res = _run_tp2(prompts, n_new, world=tp, cfg_name="tiny-gqa8", seed=9, blocks=256)
+    for r in range(tp):
+        assert "exception" not in res[r], res[r]
+        assert res[r]["custom_ar"] and res[r]["errors"] == 0, (r, res[r])
+        assert res[r]["graphed"] and res[r]["tokens"] == res[r]["eager"], (r, res[r])
+        assert res[r]["tokens"] == res[0]["tokens"]
+    toks = res[0]["tokens"]
+    m1 = DecoderModel(DecoderWeights.random(cfg, "cuda:0", seed=9))
+    eng = LLMEngine(m1, PagedKVCache(cfg.layers, 256, cfg.kv_heads, cfg.head_dim, "cuda:0"), use_graph=False,
+                    prefix_cache=False)
+    exact, worst = 0, 0.0
+    for j in range(n_new):
+        lg = _last_logits(eng, m1, [p + t[:j] for p, t in zip(prompts, toks)])
+        sig = lg.std(-1)
+        for i, t in enumerate(toks):
+            gap = float((lg[i].max() - lg[i, t[j]]) / sig[i])
+            worst = max(worst, gap)
+            exact += int(gap == 0.0)
+    n = n_new * len(prompts)
+    assert worst <= 0.1, f"a TP={tp} token is {worst:.3f} sigma below TP=1's best (exact {exact}/{n})"
+    assert exact >= 0.9 * n, f"TP={tp} matched TP=1's argmax in {exact}/{n} teacher-forced steps"
