@@ -188,3 +188,22 @@ def test_store_rpc_skips_a_sequence_number_whose_caller_died():
     finally:
         stop.set()
         t.join()
+
+
+def test_router_liveness_is_the_heartbeat_only_and_never_latched():
+    """A rank is dead while its heartbeat is stale and routable again once it beats: nothing marks it
+    dead permanently (a slow reply or a handler error never does)."""
+    import json as _json
+
+    from copilot_for_consensus_amd.parallel.dp_node import SUM_PREFIX, _Router
+    store = TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False, timeout=datetime.timedelta(seconds=10))
+    r = _Router(store, 3, timeout=1.0, cache_s=0.0)
+    now = time.time()
+    for k, t in ((0, now), (1, now - 5.0), (2, now)):
+        store.set(f"{SUM_PREFIX}hb/{k}", _json.dumps({"t": t}))
+    assert r.live() == [0, 2]
+    tid = next(f"t{i}" for i in range(100) if __import__("copilot_for_consensus_amd.parallel.dp",
+                                                            fromlist=["owner_of"]).owner_of(f"t{i}", 3) == 1)
+    assert r.owner(tid) == 2                      # rank 1's thread goes to the next live rank
+    store.set(f"{SUM_PREFIX}hb/1", _json.dumps({"t": time.time()}))
+    assert r.live() == [0, 1, 2] and r.owner(tid) == 1   # it beats again: its threads come back
