@@ -418,6 +418,8 @@ DGEMM_CUS = 256                  # one workgroup per CU
 DGEMM_CU_RATE = 25e9             # W bytes/s one workgroup streams (6.4 TB/s over 256 CUs)
 DGEMM_PART_RATE = 6e12           # fp32 partial slab traffic, bytes/s
 DGEMM_X_RATE = 90e9              # per-CU L2 -> LDS rate of the X re-reads (ablation: X costs ~12 us of gate/up)
+# split-K slabs stored write-through (dgemm.hip DG_PART_WT) when CFC_DGEMM_SLAB_WT=1
+DGEMM_PART_MODE = 3 if os.environ.get("CFC_DGEMM_SLAB_WT", "0") == "1" else 0
 
 
 class PackedWeight:
@@ -506,17 +508,17 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, epi: str = "bf16", split: int = 1, b
         raise ValueError(f"dgemm: x {tuple(x.shape)} {x.dtype} w {tuple(w.shape)} {getattr(w, 'dtype', 'packed')}")
     packed = isinstance(w, PackedWeight)
     wptr = w.data.data_ptr() if packed else w.data_ptr()
-    mode = {"part": 0, "bf16": 1, "swiglu": 2}[epi]
+    mode = {"part": DGEMM_PART_MODE, "bf16": 1, "swiglu": 2}[epi]
     if packed:
         if bn not in (None, w.bn):
             raise ValueError(f"dgemm: weight packed for bn={w.bn}, asked for bn={bn}")
         bn = w.bn
     bn = bn or dgemm_config(M, N, Kd, swiglu=mode == 2)[0]
     st = _stream(x)
-    if mode == 0:
+    if mode in (0, 3):
         part = _workspace(x.device, split * M * N)[:split * M * N].view(split, M, N) if part is None else part
-        check(kernels().cfc_dgemm(x.data_ptr(), wptr, M, N, Kd, split, 0, bn, int(packed), part.data_ptr(), None, 0,
-                                  st), "cfc_dgemm")
+        check(kernels().cfc_dgemm(x.data_ptr(), wptr, M, N, Kd, split, mode, bn, int(packed), part.data_ptr(), None,
+                                  0, st), "cfc_dgemm")
         return part
     if out is None:
         out = torch.empty(M, N // 2 if mode == 2 else N, dtype=torch.bfloat16, device=x.device)

@@ -44,7 +44,11 @@ typedef unsigned int dg_u32x4 __attribute__((ext_vector_type(4)));
 // least one
 template <int BN>
 constexpr int dg_loaders() { return BN / 16 >= 7 ? 1 : 8 - BN / 16 > 2 ? 2 : 8 - BN / 16; }
-enum { DG_PART = 0, DG_BF16 = 1, DG_SILU = 2 };
+// DG_PART_WT: the split-K slabs stored write-through (sc1): they reach memory while the kernel
+// runs instead of as dirty L2 lines the kernel boundary must write back before the consumer (the
+// residual + RMSNorm reduce, rope_kv) may start -- MI355X_MICROARCH "boundary": +B / 6 TB/s behind
+// B dirty bytes, 2.8-3.8 us behind 12.6-16.8 MB of fp32 partials.
+enum { DG_PART = 0, DG_BF16 = 1, DG_SILU = 2, DG_PART_WT = 3 };
 
 // MX (ablation 64): two X-loader waves and an 8-slot X ring whatever BN -- one loader wave's
 // vmcnt window (63 pieces = 3 stages at BM = 128) may cap the X stream of the wide-BN shapes.
@@ -287,6 +291,10 @@ __global__ void __launch_bounds__((64 * DgShape<BM, BN, (ABL & 64) != 0>::WAVES)
         const int m = mb + 16 * i + r;
         if (m < M) {
           if constexpr (EPI == DG_PART) part[((size_t)ks * M + m) * N + n] = acc[i][r];
+          else if constexpr (EPI == DG_PART_WT)      // vector store with sc1 (agent-scope relaxed)
+            __hip_atomic_store(reinterpret_cast<uint32_t*>(part + ((size_t)ks * M + m) * N + n),
+                               __builtin_bit_cast(uint32_t, acc[i][r]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
           else out[(size_t)m * ldo + n] = f2bf(acc[i][r]);
         }
       }
@@ -304,6 +312,7 @@ int dgemm_launch_bn(const void* x, const void* w, int M, int N, int K, int split
 #define DG_ARGS (const uint16_t*)x, (const uint16_t*)w, M, N, K, ntiles, split, part, (uint16_t*)out, ldo
   switch (epi) {
     case DG_PART: dgemm_kernel<BM, BN, DG_PART, NTW, ABL, PK><<<grid, threads, 0, stream>>>(DG_ARGS); break;
+    case DG_PART_WT: dgemm_kernel<BM, BN, DG_PART_WT, NTW, ABL, PK><<<grid, threads, 0, stream>>>(DG_ARGS); break;
     case DG_BF16: dgemm_kernel<BM, BN, DG_BF16, NTW, ABL, PK><<<grid, threads, 0, stream>>>(DG_ARGS); break;
     case DG_SILU: dgemm_kernel<BM, BN, DG_SILU, NTW, ABL, PK><<<grid, threads, 0, stream>>>(DG_ARGS); break;
     default: return -3;
@@ -353,8 +362,9 @@ int dgemm_check(int M, int N, int K, int split, int epi, int bn, const float* pa
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || split < 1 || split > K / 64) return -1;
   if (bn != 64 && bn != 96 && bn != 112 && bn != 128) return -5;
   if (N % bn) return -1;
-  if (epi != DG_PART && split != 1) return -2;
-  if ((epi == DG_PART && !part) || (epi != DG_PART && !out)) return -2;
+  const bool slabs = epi == DG_PART || epi == DG_PART_WT;
+  if (!slabs && split != 1) return -2;
+  if ((slabs && !part) || (!slabs && !out)) return -2;
   return 0;
 }
 
@@ -364,7 +374,8 @@ int dgemm_check(int M, int N, int K, int split, int epi, int bn, const float* pa
 CFC_API int cfc_dgemm_bm(int M) { return M <= 64 ? 64 : (M <= 128 ? 128 : 256); }
 
 // epi 0: fp32 split-K partials into part[split][M][N]; 1: bf16 into out (row stride ldo, split 1);
-// 2: SwiGLU over 8-row interleaved gate/up W -> bf16 [M, N/2] into out (split 1).
+// 2: SwiGLU over 8-row interleaved gate/up W -> bf16 [M, N/2] into out (split 1); 3: as 0 with
+// write-through (sc1) slab stores.
 // bn (W rows per workgroup) in {64, 96, 112, 128}, N % bn == 0, K % 64 == 0, 1 <= split <= K / 64.
 // packed: w is in the fragment-packed layout cfc_dgemm_pack wrote for this same bn (else row-major [N][K]).
 CFC_API int cfc_dgemm(const void* x, const void* w, int M, int N, int K, int split, int epi, int bn, int packed,

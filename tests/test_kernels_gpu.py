@@ -433,6 +433,20 @@ def test_dgemm_packed_exact():
                 assert torch.equal(part.sum(0), ref), (bn, split)
 
 
+@pytest.mark.parametrize("M,N,Kd,split", [(128, 6144, 4096, 4), (128, 4096, 14336, 8), (77, 448, 512, 3)])
+def test_dgemm_write_through_slabs_equal_plain(M, N, Kd, split, monkeypatch):
+    """DG_PART_WT (sc1 slab stores, CFC_DGEMM_SLAB_WT=1) writes the same fp32 partials as the plain
+    slab epilogue, bit for bit, and they sum to the fp32 reference."""
+    x = torch.randn(M, Kd, device=DEV).bfloat16()
+    w = (torch.randn(N, Kd, device=DEV) * 0.02).bfloat16()
+    pw = K.pack_dgemm_weight(w)
+    plain = K.dgemm(x, pw, "part", split).clone()
+    monkeypatch.setattr(K, "DGEMM_PART_MODE", 3)
+    wt = K.dgemm(x, pw, "part", split).clone()
+    assert torch.equal(plain, wt)
+    _close(wt.sum(0).bfloat16(), _ref_linear(x, w), 3e-2)
+
+
 @pytest.mark.parametrize("M,split", [(128, None), (5, None), (128, 2), (256, None)])
 def test_dgemm_packed_swiglu_and_norm(M, split):
     F, Kd = 1024, 512
