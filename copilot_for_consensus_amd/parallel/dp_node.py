@@ -433,7 +433,7 @@ class DPNodeVectorStore(VectorStore):
             host, port = store.host, store.port
         else:
             host = os.environ.get("CFC_DP_DATA_HOST", "127.0.0.1")
-            self._data_server = DocumentStoreServer(store, host=host, port=0).start()
+            self._data_server = DocumentStoreServer(store, host=host, port=0, read_only=True).start()
             port = self._data_server.port
         self.w.text_source = _store_texts(store)
         self.w.store.set(DATA_KEY, json.dumps([host, int(port)]))

@@ -63,7 +63,11 @@ def _recv(sock: socket.socket) -> Any:
 
 class DocumentStoreServer:
     def __init__(self, store: InMemoryDocumentStore | None = None, host: str = "0.0.0.0", port: int = 27027,
-                 data_dir: str | os.PathLike | None = None, fsync: bool = False, snapshot_every: int = 50_000):
+                 data_dir: str | os.PathLike | None = None, fsync: bool = False, snapshot_every: int = 50_000,
+                 read_only: bool = False):
+        """``read_only``: refuse every write (a view of another component's store, e.g. the chunk
+        texts the DP node's owner ranks read: parallel/dp_node.py)."""
+        self.read_only = bool(read_only)
         self.store = store or InMemoryDocumentStore()
         self.store.connect()
         self.data_dir = Path(data_dir) if data_dir else None
@@ -155,6 +159,8 @@ class DocumentStoreServer:
                 return {"id": rid, "ok": True, "result": getattr(self.store, op)(*args, **kwargs)}
             if op not in WRITE_OPS:
                 raise DocumentStoreError(f"unknown operation {op!r}")
+            if self.read_only:
+                raise DocumentStoreError(f"{op}: this document store is served read-only")
             # ids are fixed here so the log replays to the same documents
             if op == "insert_document" and not args[1].get("_id"):
                 args[1] = {**args[1], "_id": str(uuid.uuid4())}

@@ -207,3 +207,24 @@ def test_router_liveness_is_the_heartbeat_only_and_never_latched():
     assert r.owner(tid) == 2                      # rank 1's thread goes to the next live rank
     store.set(f"{SUM_PREFIX}hb/1", _json.dumps({"t": time.time()}))
     assert r.live() == [0, 1, 2] and r.owner(tid) == 1   # it beats again: its threads come back
+
+
+def test_chunk_text_server_is_read_only():
+    """The DP data plane serves rank 0's store to the other ranks for reads only."""
+    from copilot_for_consensus_amd.storage.document_store import DocumentStoreError, InMemoryDocumentStore
+    from copilot_for_consensus_amd.storage.server import DocumentStoreServer, RemoteDocumentStore
+    docs = InMemoryDocumentStore()
+    docs.connect()
+    docs.insert_document("chunks", {"_id": "c1", "text": "hello"})
+    srv = DocumentStoreServer(docs, host="127.0.0.1", port=0, read_only=True).start()
+    try:
+        cli = RemoteDocumentStore("127.0.0.1", srv.port)
+        cli.connect()
+        assert cli.get_document("chunks", "c1")["text"] == "hello"
+        with pytest.raises(DocumentStoreError):
+            cli.insert_document("chunks", {"_id": "c2", "text": "x"})
+        assert docs.get_document("chunks", "c2") is None
+        cli.disconnect()
+    finally:
+        srv.server.shutdown()
+        srv.server.server_close()
