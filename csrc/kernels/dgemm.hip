@@ -291,10 +291,13 @@ __global__ void __launch_bounds__((64 * DgShape<BM, BN, (ABL & 64) != 0>::WAVES)
         const int m = mb + 16 * i + r;
         if (m < M) {
           if constexpr (EPI == DG_PART) part[((size_t)ks * M + m) * N + n] = acc[i][r];
-          else if constexpr (EPI == DG_PART_WT)      // vector store with sc1 (agent-scope relaxed)
-            __hip_atomic_store(reinterpret_cast<uint32_t*>(part + ((size_t)ks * M + m) * N + n),
-                               __builtin_bit_cast(uint32_t, acc[i][r]), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+          else if constexpr (EPI == DG_PART_WT) {    // vector store with sc1 (agent-scope relaxed)
+            // the element goes through a scalar temporary: __builtin_bit_cast of the vector element
+            // expression acc[i][r] itself compiled to element 0 for every r (hipcc, ROCm 7.2)
+            const float v = acc[i][r];
+            __hip_atomic_store(reinterpret_cast<uint32_t*>(part + ((size_t)ks * M + m) * N + n), __float_as_uint(v),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
           else out[(size_t)m * ldo + n] = f2bf(acc[i][r]);
         }
       }
