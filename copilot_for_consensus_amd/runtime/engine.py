@@ -62,6 +62,7 @@ class _Job:
     seed: int
     prefill_s: float
     ready: object = None          # event recorded after the state setup (stream handoff)
+    order: list | None = None     # slot s holds caller prompt order[s] (longest-first slots)
 
 
 class _DecodeState:
@@ -120,6 +121,11 @@ class LLMEngine:
         self.prefix_cache = PrefixCache(kv.pool) if prefix_cache else None
         # CFC_DECODE_SHARED_CACHED=0: every KV block nontemporal, shared prefix included
         self.shared_cached = os.environ.get("CFC_DECODE_SHARED_CACHED", "1") != "0"
+        # CFC_DECODE_LPT=1: slots filled longest prompt first.  The decode attention grid walks the
+        # slots in order (blockIdx.z = slot), so the longest sequences' workgroups are dispatched
+        # first and the short ones fill the CUs that free up (longest-processing-time-first list
+        # scheduling) instead of a random long one ending the kernel alone
+        self.lpt = os.environ.get("CFC_DECODE_LPT", "0") == "1"
         if self.device.type == "cuda":
             from .gemm_tuning import enable_tuned_gemms
             self.tuned_gemms = enable_tuned_gemms()
@@ -314,6 +320,10 @@ class LLMEngine:
             if ignore_eos:
                 stop_ids = ()
         B = len(prompts)
+        order = None
+        if self.lpt and B > 1:
+            order = sorted(range(B), key=lambda i: -len(prompts[i]))
+            prompts = [prompts[i] for i in order]
         lens = [len(p) for p in prompts]
         if max(lens) + max_new_tokens > self.cfg.max_positions:
             raise ValueError("prompt + max_new_tokens exceeds max_positions")
@@ -393,7 +403,7 @@ class LLMEngine:
                 self._release(tables, fresh, failed=True)
             raise
         return _Job(st, tables, fresh, lens, start, B, max_new_tokens, tuple(stop_ids), stop_strings, part_blocks,
-                    temperature, seed, t1 - t0, ready)
+                    temperature, seed, t1 - t0, ready, order)
 
     @torch.inference_mode()
     def finish(self, job: _Job, switch=None) -> GenerationResult:
@@ -459,7 +469,13 @@ class LLMEngine:
                     row = row[:j]
                     break
             out.append(row)
-        return GenerationResult(out, job.lens, prefill_s=job.prefill_s, decode_s=t2 - t1, ttft_s=job.prefill_s,
+        lens = job.lens
+        if job.order is not None:            # back to the caller's prompt order
+            inv = [0] * B
+            for slot, i in enumerate(job.order):
+                inv[i] = slot
+            out, lens = [out[inv[i]] for i in range(B)], [lens[inv[i]] for i in range(B)]
+        return GenerationResult(out, lens, prefill_s=job.prefill_s, decode_s=t2 - t1, ttft_s=job.prefill_s,
                                 decode_steps=steps, cached_prompt_tokens=sum(job.start))
 
     def _release(self, tables, fresh, failed: bool = False):

@@ -248,3 +248,15 @@ def test_prefill_routes_short_chunks_to_the_decode_gemm():
     assert m._dgemm_faster(512, 6144, 4096) and m._dgemm_faster(1024, 4096, 14336)
     assert not m._dgemm_faster(1024, 6144, 4096) and not m._dgemm_faster(16384, 4096, 4096)
     assert not m._dgemm_faster(512, 28672, 4096)
+
+
+def test_longest_first_slots_return_caller_order(monkeypatch):
+    """CFC_DECODE_LPT=1 fills the decode slots longest prompt first; tokens and prompt lengths come
+    back in the caller's order, equal to the default slot order's."""
+    prompts = [[1, 5], [1] + list(range(3, 90)), [1, 9, 9, 9, 9], [1] + list(range(40, 70))]
+    ref = _engine().generate(prompts, 5, ignore_eos=True)
+    monkeypatch.setenv("CFC_DECODE_LPT", "1")
+    eng = _engine()
+    assert eng.lpt
+    got = eng.generate(prompts, 5, ignore_eos=True)
+    assert got.tokens == ref.tokens and got.prompt_lens == ref.prompt_lens == [len(p) for p in prompts]
