@@ -418,8 +418,10 @@ DGEMM_CUS = 256                  # one workgroup per CU
 DGEMM_CU_RATE = 25e9             # W bytes/s one workgroup streams (6.4 TB/s over 256 CUs)
 DGEMM_PART_RATE = 6e12           # fp32 partial slab traffic, bytes/s
 DGEMM_X_RATE = 90e9              # per-CU L2 -> LDS rate of the X re-reads (ablation: X costs ~12 us of gate/up)
-# split-K slabs stored write-through (dgemm.hip DG_PART_WT) when CFC_DGEMM_SLAB_WT=1
-DGEMM_PART_MODE = 3 if os.environ.get("CFC_DGEMM_SLAB_WT", "0") == "1" else 0
+# split-K slabs stored write-through (dgemm.hip DG_PART_WT; CFC_DGEMM_SLAB_WT=0 for plain stores): the
+# kernel boundary no longer writes back 8-17 MB of dirty partials before the reduce / rope_kv may
+# start -- decode 6.48 -> 6.42 s per 128-thread batch, bit-identical (profiles/r05_ab_slab_wt.log)
+DGEMM_PART_MODE = 0 if os.environ.get("CFC_DGEMM_SLAB_WT", "1") == "0" else 3
 
 
 class PackedWeight:

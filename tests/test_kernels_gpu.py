@@ -440,6 +440,7 @@ def test_dgemm_write_through_slabs_equal_plain(M, N, Kd, split, monkeypatch):
     x = torch.randn(M, Kd, device=DEV).bfloat16()
     w = (torch.randn(N, Kd, device=DEV) * 0.02).bfloat16()
     pw = K.pack_dgemm_weight(w)
+    monkeypatch.setattr(K, "DGEMM_PART_MODE", 0)
     plain = K.dgemm(x, pw, "part", split).clone()
     monkeypatch.setattr(K, "DGEMM_PART_MODE", 3)
     wt = K.dgemm(x, pw, "part", split).clone()
