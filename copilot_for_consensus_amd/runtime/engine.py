@@ -121,11 +121,12 @@ class LLMEngine:
         self.prefix_cache = PrefixCache(kv.pool) if prefix_cache else None
         # CFC_DECODE_SHARED_CACHED=0: every KV block nontemporal, shared prefix included
         self.shared_cached = os.environ.get("CFC_DECODE_SHARED_CACHED", "1") != "0"
-        # CFC_DECODE_LPT=1: slots filled longest prompt first.  The decode attention grid walks the
-        # slots in order (blockIdx.z = slot), so the longest sequences' workgroups are dispatched
-        # first and the short ones fill the CUs that free up (longest-processing-time-first list
-        # scheduling) instead of a random long one ending the kernel alone
-        self.lpt = os.environ.get("CFC_DECODE_LPT", "0") == "1"
+        # slots filled longest prompt first (CFC_DECODE_LPT=0: caller order).  The decode attention
+        # grid walks the slots in order (blockIdx.z = slot), so the longest sequences' workgroups are
+        # dispatched first and the short ones fill the CUs that free up (longest-processing-time-
+        # first list scheduling) instead of a random long one ending the kernel alone: decode 6.03 ->
+        # 5.88 s per 128-thread batch (profiles/r05_ab_decode_lpt.log)
+        self.lpt = os.environ.get("CFC_DECODE_LPT", "1") != "0"
         if self.device.type == "cuda":
             from .gemm_tuning import enable_tuned_gemms
             self.tuned_gemms = enable_tuned_gemms()

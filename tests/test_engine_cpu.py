@@ -254,6 +254,7 @@ def test_longest_first_slots_return_caller_order(monkeypatch):
     """CFC_DECODE_LPT=1 fills the decode slots longest prompt first; tokens and prompt lengths come
     back in the caller's order, equal to the default slot order's."""
     prompts = [[1, 5], [1] + list(range(3, 90)), [1, 9, 9, 9, 9], [1] + list(range(40, 70))]
+    monkeypatch.setenv("CFC_DECODE_LPT", "0")
     ref = _engine().generate(prompts, 5, ignore_eos=True)
     monkeypatch.setenv("CFC_DECODE_LPT", "1")
     eng = _engine()
