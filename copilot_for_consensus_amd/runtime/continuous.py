@@ -277,6 +277,12 @@ class ContinuousEngine:
             raise
         if not take:
             return
+        if self.engine.lpt and len(take) > 1:
+            # longest prompt into the lowest free slot: the decode attention grid walks slots in
+            # order, so long contexts start first (list scheduling; engine.py's CFC_DECODE_LPT).
+            # A stable sort on the admitted list, so TP followers replaying it place the same slots.
+            order = sorted(range(len(take)), key=lambda i: -len(take[i].prompt))
+            take, tables, fresh, start = ([v[i] for i in order] for v in (take, tables, fresh, start))
         t = time.perf_counter()
         try:
             first = self.engine._prefill([r.prompt for r in take], tables, self.sampling, self.seed, start)

@@ -47,10 +47,12 @@ def _prefix_logits(eng, model, prefixes):
         got.append(model.logits(hidden).float().clone())
         return orig(hidden, out, temperature, seed, step)
     eng._next_tokens = cap
+    eng.lpt = False           # the captured rows in the caller's prompt order, not longest-first
     try:
         eng.generate(prefixes, 1, ignore_eos=True)
     finally:
         eng._next_tokens = orig
+        eng.lpt = True
     assert len(got) == 1
     return got[0]
 
