@@ -312,7 +312,9 @@ class NodeBench:
 
     def engine_stats(self) -> dict:
         """The summarizer's continuous-engine counters (admissions, decode steps, prefill / decode s)."""
-        ce = self._engine() if self.node is not None else getattr(getattr(self.worker, "summarizer", None), "_ce", None)
+        # DP: every rank's engine sits in its worker (rank 0's node summarizer is the DP router)
+        ce = getattr(getattr(self.worker, "summarizer", None), "_ce", None) if self.worker is not None \
+            else self._engine()
         return dict(ce.stats) if ce is not None else {}
 
     def dp_stats(self) -> dict:
