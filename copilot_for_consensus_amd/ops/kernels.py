@@ -112,6 +112,23 @@ def _fp8(cache) -> bool:
     return cache.dtype == torch.float8_e4m3fn
 
 
+# decode V stores write-through by default: the partial V lines leave L2 during rope_kv, not at its
+# end (8.7 -> 7.7 us per decode call in place, bit-identical; profiles/r05_rope_kv_step_prof.txt)
+_KV_VSTORE = {"mode": int(os.environ.get("CFC_KV_VSTORE", "1")), "applied": None}
+
+
+def set_kv_vstore_mode(mode: int) -> None:
+    """Decode V-cache store mode of the rope_kv kernels: 0 plain, 1 write-through, 2 nontemporal
+    (elementwise.hip cfc_set_kv_vstore_mode).  Applies to launches (and graph captures) after it."""
+    check(kernels().cfc_set_kv_vstore_mode(int(mode)), "cfc_set_kv_vstore_mode")
+    _KV_VSTORE.update(mode=int(mode), applied=int(mode))
+
+
+def _apply_vstore():
+    if _KV_VSTORE["applied"] != _KV_VSTORE["mode"]:
+        set_kv_vstore_mode(_KV_VSTORE["mode"])
+
+
 def rope_kv_write_part(part, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D, k_scale=1.0, v_scale=1.0):
     """Decode RoPE + K/V write reading the qkv projection's fp32 split-K slabs ``part``
     [split, T, (Hq + 2 Hkv) D] directly (the split-K reduce folded in; same bf16 values)."""
@@ -124,6 +141,7 @@ def rope_kv_write_part(part, positions, slots, cos_sin, k_cache, v_cache, Hq, Hk
         raise ValueError(f"rope_kv_write_part: part {tuple(part.shape)} {part.dtype}")
     _req(positions, torch.int32, "positions")
     _req(slots, torch.int32, "slots")
+    _apply_vstore()
     q_out = torch.empty(T, Hq, D, dtype=torch.bfloat16, device=part.device)
     check(kernels().cfc_rope_kv_write_part(part.data_ptr(), split, positions.data_ptr(), slots.data_ptr(),
                                            cos_sin.data_ptr(), q_out.data_ptr(), k_cache.data_ptr(),
@@ -153,6 +171,7 @@ def rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D, 
         _req(runs, torch.int32, "runs")
     q_out = torch.empty(T, Hq, D, dtype=qkv.dtype, device=qkv.device) if q_out is None else q_out
     write_v = 0 if runs is not None else 1
+    _apply_vstore()
     if _fp8(k_cache):
         check(kernels().cfc_rope_kv_write_fp8(qkv.data_ptr(), positions.data_ptr(), slots.data_ptr(),
                                               cos_sin.data_ptr(), q_out.data_ptr(), k_cache.data_ptr(),

@@ -258,8 +258,11 @@ __device__ __forceinline__ void kv_write_k(void* k_cache, int slot, int kh, int 
   }
 }
 
-// V 8-vector c (elements [8c, 8c+8)) of kv-head kh into the transposed cache at slot `slot`.
-template <bool F8>
+// V 8-vector c (elements [8c, 8c+8)) of kv-head kh into the transposed cache at slot `slot`:
+// eight 1-2 byte stores, each into a different 32-slot row (a partial cache line).  VM: 0 plain
+// stores; 1 write-through (the partial lines leave L2 during the kernel instead of at its end);
+// 2 nontemporal.
+template <bool F8, int VM = 0>
 __device__ __forceinline__ void kv_write_v(void* v_cache, int slot, int kh, int Hkv, int D, int c, uint4 val,
                                            float inv_v) {
   const int blk = slot / CFC_KV_BS, off = slot % CFC_KV_BS;
@@ -268,11 +271,21 @@ __device__ __forceinline__ void kv_write_v(void* v_cache, int slot, int kh, int 
   if constexpr (F8) {
     uint8_t* dst = reinterpret_cast<uint8_t*>(v_cache) + e0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dst[j * CFC_KV_BS] = f2fp8(bf2f(e[j]) * inv_v);
+    for (int j = 0; j < 8; ++j) {
+      const uint8_t b = f2fp8(bf2f(e[j]) * inv_v);
+      if constexpr (VM == 1) __hip_atomic_store(dst + j * CFC_KV_BS, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else if constexpr (VM == 2) __builtin_nontemporal_store(b, dst + j * CFC_KV_BS);
+      else dst[j * CFC_KV_BS] = b;
+    }
   } else {
     uint16_t* dst = reinterpret_cast<uint16_t*>(v_cache) + e0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dst[j * CFC_KV_BS] = e[j];
+    for (int j = 0; j < 8; ++j) {
+      const uint16_t h = e[j];
+      if constexpr (VM == 1) __hip_atomic_store(dst + j * CFC_KV_BS, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else if constexpr (VM == 2) __builtin_nontemporal_store(h, dst + j * CFC_KV_BS);
+      else dst[j * CFC_KV_BS] = h;
+    }
   }
 }
 

@@ -18,7 +18,7 @@ __device__ __forceinline__ int v_slot(int key_in_block) { return kv_v_slot(key_i
 // qkv: [T, (Hq + 2*Hkv) * D] (q heads | k heads | v heads), positions [T], slots [T] (-1 = skip
 // cache write), cos_sin [max_pos][D/2][2] fp32 (cos, sin interleaved); the per-item math lives in
 // common.h (rope_rot8 / kv_write_k / kv_write_v), shared with the fused decode attention.
-template <bool F8>
+template <bool F8, int VM = 0>
 __global__ void __launch_bounds__(64) rope_kv_kernel(const uint16_t* __restrict__ qkv, const int32_t* __restrict__ positions,
                                                      const int32_t* __restrict__ slots, const float* __restrict__ cos_sin,
                                                      uint16_t* __restrict__ q_out, void* __restrict__ k_cache,
@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(64) rope_kv_kernel(const uint16_t* __restrict_
     const int kh = v / (D / 8), c = v % (D / 8);
     float vf[8];
     qkv_load8(qkv, part, split, slab, row0 + (size_t)(Hq + Hkv + kh) * D + c * 8, vf);
-    kv_write_v<F8>(v_cache, slot, kh, Hkv, D, c, pack8(vf), inv_v);
+    kv_write_v<F8, VM>(v_cache, slot, kh, Hkv, D, c, pack8(vf), inv_v);
   }
 }
 
@@ -600,15 +600,33 @@ inline int ew_grid(size_t total) {
 
 }  // namespace
 
+// decode V-cache store mode for the rope_kv launches (kv_write_v's VM: 0 plain, 1 write-through,
+// 2 nontemporal); read at launch, so a captured graph keeps the mode it was captured with
+static int g_kv_vstore_mode = 0;
+
+CFC_API int cfc_set_kv_vstore_mode(int mode) {
+  if (mode < 0 || mode > 2) return -1;
+  g_kv_vstore_mode = mode;
+  return 0;
+}
+
 CFC_API int cfc_rope_kv_write(const void* qkv, const int32_t* positions, const int32_t* slots, const float* cos_sin,
                               void* q_out, void* k_cache, void* v_cache, int T, int Hq, int Hkv, int head_dim,
                               int write_v, hipStream_t stream) {
   if (head_dim % 16 != 0 || T < 0) return -1;
   if (T == 0) return 0;
   const int items = (Hq + Hkv) * (head_dim / 16) + (write_v ? Hkv * (head_dim / 8) : 0);
-  rope_kv_kernel<false><<<dim3(T, (items + 63) / 64), 64, 0, stream>>>(
-      (const uint16_t*)qkv, positions, slots, cos_sin, (uint16_t*)q_out, k_cache, v_cache, Hq, Hkv, head_dim, write_v,
-      1.f, 1.f);
+  const dim3 grid(T, (items + 63) / 64);
+  const auto* x = (const uint16_t*)qkv;
+  if (write_v && g_kv_vstore_mode == 1)
+    rope_kv_kernel<false, 1><<<grid, 64, 0, stream>>>(x, positions, slots, cos_sin, (uint16_t*)q_out, k_cache,
+                                                      v_cache, Hq, Hkv, head_dim, 1, 1.f, 1.f);
+  else if (write_v && g_kv_vstore_mode == 2)
+    rope_kv_kernel<false, 2><<<grid, 64, 0, stream>>>(x, positions, slots, cos_sin, (uint16_t*)q_out, k_cache,
+                                                      v_cache, Hq, Hkv, head_dim, 1, 1.f, 1.f);
+  else
+    rope_kv_kernel<false><<<grid, 64, 0, stream>>>(x, positions, slots, cos_sin, (uint16_t*)q_out, k_cache, v_cache,
+                                                   Hq, Hkv, head_dim, write_v, 1.f, 1.f);
   return CFC_CHECK_LAUNCH();
 }
 
@@ -743,13 +761,19 @@ CFC_API int cfc_rope_kv_write_part(const float* part, int split, const int32_t* 
   if (head_dim % 16 != 0 || T < 0 || split < 1 || part == nullptr) return -1;
   if (T == 0) return 0;
   const int items = (Hq + Hkv) * (head_dim / 16) + Hkv * (head_dim / 8);
-  if (fp8)
-    rope_kv_kernel<true><<<dim3(T, (items + 63) / 64), 64, 0, stream>>>(
-        nullptr, positions, slots, cos_sin, (uint16_t*)q_out, k_cache, v_cache, Hq, Hkv, head_dim, 1, inv_k, inv_v,
-        part, split);
-  else
-    rope_kv_kernel<false><<<dim3(T, (items + 63) / 64), 64, 0, stream>>>(
-        nullptr, positions, slots, cos_sin, (uint16_t*)q_out, k_cache, v_cache, Hq, Hkv, head_dim, 1, 1.f, 1.f,
-        part, split);
+  const dim3 grid(T, (items + 63) / 64);
+#define ROPE_PART(F8, VM)                                                                                          \
+  rope_kv_kernel<F8, VM><<<grid, 64, 0, stream>>>(nullptr, positions, slots, cos_sin, (uint16_t*)q_out, k_cache,   \
+                                                  v_cache, Hq, Hkv, head_dim, 1, F8 ? inv_k : 1.f, F8 ? inv_v : 1.f, \
+                                                  part, split)
+  switch (g_kv_vstore_mode * 2 + (fp8 ? 1 : 0)) {
+    case 2: ROPE_PART(false, 1); break;
+    case 3: ROPE_PART(true, 1); break;
+    case 4: ROPE_PART(false, 2); break;
+    case 5: ROPE_PART(true, 2); break;
+    case 1: ROPE_PART(true, 0); break;
+    default: ROPE_PART(false, 0); break;
+  }
+#undef ROPE_PART
   return CFC_CHECK_LAUNCH();
 }

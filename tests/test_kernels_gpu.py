@@ -645,6 +645,19 @@ def test_rope_kv_write_from_splitk_slabs_matches_reduce_then_rope(split):
     k2, v2 = caches()
     q2 = K.rope_kv_write_part(part, pos, slots, cs, k2, v2, Hq, Hkv, D)
     assert torch.equal(q1, q2) and torch.equal(k1, k2) and torch.equal(v1, v2)
+    # every V store mode (CFC_KV_VSTORE: plain, write-through, nontemporal) writes the same bytes
+    orig = K._KV_VSTORE["mode"]
+    try:
+        for mode in (0, 1, 2):
+            K.set_kv_vstore_mode(mode)
+            k3, v3 = caches()
+            q3 = K.rope_kv_write_part(part, pos, slots, cs, k3, v3, Hq, Hkv, D)
+            k4, v4 = caches()
+            K.rope_kv_write(K.splitk_reduce(part), pos, slots, cs, k4, v4, Hq, Hkv, D)
+            assert torch.equal(q1, q3) and torch.equal(k1, k3) and torch.equal(v1, v3), mode
+            assert torch.equal(k1, k4) and torch.equal(v1, v4), mode
+    finally:
+        K.set_kv_vstore_mode(orig)
 
 
 @pytest.mark.parametrize("G", [1, 4, 8])
