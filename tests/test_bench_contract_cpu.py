@@ -62,12 +62,15 @@ def test_bench_single_process_contract():
     _check(_run([sys.executable, "bench.py", "--gpus", "1", *ARGS]), 1)
 
 
-def test_bench_two_ranks_under_torchrun():
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", *ARGS]
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_bench_dp_ranks_under_torchrun(n):
+    """The driver's N = 2, 4, 8 runs, one rank per (here virtual) GPU: the DP data plane (index
+    sharded by thread owner, all_to_all inserts / query merges) at every world size it will see."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(n), *ARGS]
     d = _run(cmd)
-    _check(d, 2)
-    assert d["config"]["index"].startswith("sharded over 2 GPUs")    # the DP data plane ran
+    _check(d, n)
+    assert d["config"]["index"].startswith(f"sharded over {n} GPUs")    # the DP data plane ran
 
 
 def test_bench_tp2_two_ranks_reports_both_halves():
