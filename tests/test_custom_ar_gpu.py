@@ -221,10 +221,12 @@ def _last_logits(eng, model, prompts):
         seen.append(lg.float())
         return lg
     model.logits = grab
+    lpt, eng.lpt = eng.lpt, False        # captured rows in prompt order, not longest-first
     try:
         toks = eng.generate(prompts, max_new_tokens=1, ignore_eos=True).tokens
     finally:
         model.logits = orig
+        eng.lpt = lpt
     lg = seen[0]
     assert lg.shape[0] == len(prompts) and lg.argmax(-1).tolist() == [t[0] for t in toks]
     return lg
