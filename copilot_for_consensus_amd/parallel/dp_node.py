@@ -382,8 +382,15 @@ class _Router:
     its heartbeat is fresh -- re-read on every decision (cached ``cache_s``), never latched, so a
     rank that only answered slowly, or whose handler failed, keeps its threads and shard."""
 
-    def __init__(self, store, world: int, timeout: float, cache_s: float = 0.25):
+    def __init__(self, store, world: int, timeout: float, cache_s: float = 0.25,
+                 startup_grace_s: float | None = None):
         self.store, self.world, self.timeout, self.cache_s = store, int(world), float(timeout), float(cache_s)
+        # a rank with no heartbeat yet is still loading its models: live for this long after the
+        # router starts, dead after it (its threads go to the next live rank instead of waiting on
+        # a rank that never came up)
+        self.startup_grace_s = float(startup_grace_s if startup_grace_s is not None
+                                     else os.environ.get("CFC_DP_STARTUP_GRACE_S", "600"))
+        self._t0 = time.monotonic()
         self._seen: dict[int, tuple[float, bool]] = {}
 
     def alive(self, rank: int) -> bool:
@@ -392,8 +399,10 @@ class _Router:
         if c is not None and now - c[0] < self.cache_s:
             return c[1]
         v = _get(self.store, f"{SUM_PREFIX}hb/{rank}")
-        # not started yet: give it the benefit of the doubt
-        ok = v is None or time.time() - json.loads(v)["t"] <= self.timeout
+        if v is None:                 # not started yet: live during the start-up grace only
+            ok = now - self._t0 <= self.startup_grace_s
+        else:
+            ok = time.time() - json.loads(v)["t"] <= self.timeout
         self._seen[rank] = (now, ok)
         return ok
 

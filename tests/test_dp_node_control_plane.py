@@ -209,6 +209,20 @@ def test_router_liveness_is_the_heartbeat_only_and_never_latched():
     assert r.live() == [0, 1, 2] and r.owner(tid) == 1   # it beats again: its threads come back
 
 
+def test_router_rank_that_never_starts_is_dead_after_the_startup_grace():
+    import json as _json
+
+    from copilot_for_consensus_amd.parallel.dp_node import SUM_PREFIX, _Router
+    store = TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False, timeout=datetime.timedelta(seconds=10))
+    store.set(f"{SUM_PREFIX}hb/0", _json.dumps({"t": time.time() + 60}))
+    r = _Router(store, 2, timeout=30.0, cache_s=0.0, startup_grace_s=0.3)
+    assert r.live() == [0, 1]                     # rank 1 still loading its models
+    time.sleep(0.4)
+    assert r.live() == [0]                        # never came up: its threads go elsewhere
+    store.set(f"{SUM_PREFIX}hb/1", _json.dumps({"t": time.time()}))
+    assert r.live() == [0, 1]                     # late start: routable from its first beat
+
+
 def test_chunk_text_server_is_read_only():
     """The DP data plane serves rank 0's store to the other ranks for reads only."""
     from copilot_for_consensus_amd.storage.document_store import DocumentStoreError, InMemoryDocumentStore
