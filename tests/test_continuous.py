@@ -214,3 +214,24 @@ def test_decode_width_follows_the_occupied_slots_cpu():
     assert d.slot == 1
     ce.run()
     ce.close()
+
+
+@pytest.mark.parametrize("lpt", [True, False])
+def test_admission_places_longest_prompt_in_lowest_slot(lpt):
+    """One admission of several prompts: with the engine's longest-first setting the longest prompt
+    takes the lowest free slot (the decode attention grid walks slots in order); either way every
+    request's tokens equal its own generate()."""
+    model, kv = _setup("cpu")
+    eng = LLMEngine(model, kv, max_prefill_tokens=512, use_graph=False)
+    eng.lpt = lpt
+    reqs = [([1] + list(range(5, 5 + n)), 6) for n in (20, 90, 7, 140, 55)]
+    ce = ContinuousEngine(eng, max_slots=8, max_new_cap=8, max_prompt=256, steps_per_sync=2, min_admit=5)
+    hs = [ce.submit(p, m) for p, m in reqs]
+    ce.step()                                            # one admission of all five
+    assert all(h.slot is not None for h in hs)          # 6 tokens: none finished in a 2-step burst
+    by_len = sorted(range(len(reqs)), key=lambda i: -len(reqs[i][0]))
+    want = by_len if lpt else list(range(len(reqs)))
+    assert [hs[i].slot for i in want] == list(range(len(reqs)))
+    ce.run()
+    ce.close()
+    assert [h.tokens for h in hs] == [eng.generate([p], m, ignore_eos=True).tokens[0] for p, m in reqs]
