@@ -120,6 +120,8 @@ def main(argv=None):
                 print(f"[bench] {kind} {i}: {r.summary()}", file=sys.stderr, flush=True)
         return report
 
+    overlap_prefill = pipe.overlap_prefill
+
     def run(steps, kind):
         if pipe.overlap_prefill:
             return pipe.run_steps_overlapped(steps, on_step=progress(kind))
@@ -182,6 +184,13 @@ def main(argv=None):
         # the bench pipeline's model: its own encoder, index and decoder), admitting each thread on
         # arrival as a lightly loaded summarization service does
         from copilot_for_consensus_amd.pipeline.node_bench import NodeBench
+        # the bench pipeline is finished: free its model, KV pool and index before the node builds
+        # its own, so the peak is one stack per rank (two ranks sharing one GPU fit too)
+        del pipe
+        import gc
+        gc.collect()
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
         barrier()
         nb = NodeBench(model=args.model, encoder=args.encoder, device=dev, threads_per_step=args.threads_per_gpu,
                        max_new_tokens=args.max_new, seed=args.seed + 7919 * groups.dp_rank,
@@ -225,7 +234,7 @@ def main(argv=None):
                 "pipeline": "llm-only" if args.llm_only else "parse+chunk+embed+knn+select+prefill+decode",
                 "index": (f"sharded over {groups.dp_size} GPUs by thread (RCCL all_to_all insert + relevance)"
                           if groups.dp_size > 1 and not args.llm_only else "one HBM index per GPU"),
-                "schedule": ("prefill of batch i+1 on half the CUs beside batch i's decode" if pipe.overlap_prefill
+                "schedule": ("prefill of batch i+1 on half the CUs beside batch i's decode" if overlap_prefill
                              else "prefill then decode per batch (next batch's preparation overlapped)"),
             },
             "p50_summary_latency_s": round(p50, 3) if p50 is not None else None,
