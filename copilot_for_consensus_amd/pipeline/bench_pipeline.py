@@ -82,6 +82,15 @@ class BenchPipeline:
         self.side_stream = torch.cuda.Stream(self.device, priority=prio) if self.device.type == "cuda" else None
         self._last_gen_s: float | None = None
         self._last_prep_s = 0.0
+        # just-in-time preparation: batch i+1's CPU + encoder stages start so they end
+        # ``margin`` x (the slowest of the last 4 preparations) + ``slack`` s before batch i's LLM
+        # work does -- a thread's latency counts from its preparation's start, so an early start is
+        # latency with no throughput in it (wait_prep in the step summary shows a late one).
+        # 2.0 / 0.25 -> 1.25 / 0.1: saturated p50 10.8-11.0 -> 10.3 s at unchanged throughput, 0.01-0.09 s
+        # of wait_prep over 20 steps (profiles/r05_ab_prep_margin.log)
+        self._prep_hist: list[float] = []
+        self.prep_margin = float(os.environ.get("CFC_PREP_MARGIN", "1.25"))
+        self.prep_slack_s = float(os.environ.get("CFC_PREP_SLACK_S", "0.1"))
         if not llm_only and not self.follower:
             from ..bus import CountingPublisher
             from .rag import RagPipeline
@@ -160,13 +169,15 @@ class BenchPipeline:
                 if pool and n + 1 < len(steps):
                     start_at = None
                     if self._last_gen_s is not None:
-                        start_at = time.perf_counter() + max(0.0, self._last_gen_s - 2.0 * self._last_prep_s - 0.25)
+                        lead = self.prep_margin * max(self._prep_hist) + self.prep_slack_s
+                        start_at = time.perf_counter() + max(0.0, self._last_gen_s - lead)
                     fut = pool.submit(self._prepare, steps[n + 1], start_at)
                 tg = time.perf_counter()
                 with span(f"bench.llm.step{step}"):
                     res = self.engine.generate(prompts, self.max_new, temperature=0.0, ignore_eos=True)
                 self._last_gen_s = time.perf_counter() - tg
                 self._last_prep_s = sum(v for k, v in stages.items() if k != "wait_prep")
+                self._prep_hist = (self._prep_hist + [self._last_prep_s])[-4:]
                 stages["prefill"] = res.prefill_s
                 stages["decode"] = res.decode_s
                 # engine time outside its prefill / decode windows (setup, first-token sync, harvest)
