@@ -68,6 +68,10 @@ def split_mbox(data: bytes) -> list[bytes]:
 
 # ------------------------------------------------------------------------------ normaliser
 
+_WS_RUN = re.compile(r"[ \t]+")
+_BLANK_RUN = re.compile(r"\n{3,}")
+
+
 class TextNormalizer:
     SIGNATURE_DELIMITERS = ("\n-- \n", "\n--\n", "\n___\n", "\n___________\n",
                             "\n________________________________________\n")
@@ -89,8 +93,8 @@ class TextNormalizer:
         if self.strip_quoted:
             text = "\n".join(ln for ln in text.split("\n")
                              if not ln.strip() or not ln.strip().startswith((">", "|")))
-        text = re.sub(r"[ \t]+", " ", text)
-        text = re.sub(r"\n{3,}", "\n\n", text)
+        text = _WS_RUN.sub(" ", text)
+        text = _BLANK_RUN.sub("\n\n", text)
         return text.strip()
 
     @staticmethod
@@ -108,10 +112,18 @@ class DraftDetector:
 
     def __init__(self, pattern: str | None = None):
         self.regex = re.compile(pattern or self.DEFAULT_PATTERN, re.IGNORECASE)
+        # the default pattern only matches where "draft-" or "rfc" occurs (any case): most bodies
+        # mention neither, and one lower() + two substring scans are far cheaper than the
+        # case-insensitive three-way alternation tried at every position
+        self._prefilter = pattern is None
 
     def detect(self, text: str) -> list[str]:
         if not text:
             return []
+        if self._prefilter:
+            low = text.lower()
+            if "rfc" not in low and "draft-" not in low:
+                return []
         out, seen = [], set()
         for m in self.regex.finditer(text):
             g = next(x for x in m.groups() if x)
