@@ -68,7 +68,7 @@ def split_mbox(data: bytes) -> list[bytes]:
 
 # ------------------------------------------------------------------------------ normaliser
 
-_WS_RUN = re.compile(r"[ \t]+")
+_WS_RUN = re.compile(r" [ \t]+|\t[ \t]*")   # = [ \t]+ -> " ", without rewriting every single space
 _BLANK_RUN = re.compile(r"\n{3,}")
 
 
