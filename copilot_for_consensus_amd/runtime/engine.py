@@ -127,6 +127,14 @@ class LLMEngine:
         # first list scheduling) instead of a random long one ending the kernel alone: decode 6.03 ->
         # 5.88 s per 128-thread batch (profiles/r05_ab_decode_lpt.log)
         self.lpt = os.environ.get("CFC_DECODE_LPT", "1") != "0"
+        # TP > 1, opt-in (CFC_TP_PREFILL_OVERLAP=1): prefill chunks as two interleaved halves, each
+        # half's all-reduces (async RCCL, their own stream) under the other half's GEMMs.  Numerics
+        # checked against the one-pass prefill on the CPU (tests/test_parallel_cpu.py); not measured
+        # on a multi-GPU node, and never with a gloo TP group on GPU tensors (the one-GPU rehearsal
+        # mode): there a TP=2 run stalled in the decode graph after an overlapped prefill
+        # (scripts/dbg_tp_overlap.sh), so that combination keeps the one-pass prefill
+        self.tp_overlap = (os.environ.get("CFC_TP_PREFILL_OVERLAP", "0") == "1"
+                           and not (self._gloo_tp and self.device.type == "cuda"))
         if self.device.type == "cuda":
             from .gemm_tuning import enable_tuned_gemms
             self.tuned_gemms = enable_tuned_gemms()
@@ -163,54 +171,83 @@ class LLMEngine:
                     order.remove(s)
                 else:
                     break  # a split sequence ends the chunk
-            cu, ctx, rows, last_rows, finishing = [0], [], [], [], []
-            ids_np, pos_np, slot_np = [], [], []
-            for (s, a, b) in chunk:
-                ids_np.append(np.asarray(prompts[s][a:b], dtype=np.int32))
-                p = np.arange(a, b, dtype=np.int32)
-                pos_np.append(p)
-                slot_np.append(np.asarray(tables[s], dtype=np.int32)[p // KV_BLOCK] * KV_BLOCK + p % KV_BLOCK)
-                cu.append(cu[-1] + (b - a))
-                ctx.append(b)
-                rows.append(s)
-                if b == len(prompts[s]):
-                    last_rows.append(cu[-1] - 1)
-                    finishing.append(s)
+            halves = self._overlap_split(chunk)
+            metas = [self._chunk_meta(prompts, tables, part) for part in halves]
+            if len(metas) == 2:
+                hiddens = self.model.forward_prefill_overlap([m[0] for m in metas], self.kv)
+            else:
+                hiddens = [self.model.forward_prefill(**metas[0][0], kv=self.kv)]
+            for (_, finishing, d_fin), hidden in zip(metas, hiddens):
+                if finishing:
+                    out = torch.empty(len(finishing), dtype=torch.int32, device=self.device)
+                    self._next_tokens(hidden, out, temperature, seed,
+                                      torch.zeros(1, dtype=torch.int32, device=self.device))
+                    first_dev.index_copy_(0, d_fin.long(), out)
+            for (s, _, b) in chunk:
                 pos[s] = b
-            maxb = max(len(tables[s]) for s in rows)
-            bt = np.zeros((len(rows), maxb), dtype=np.int32)
-            for r, s in enumerate(rows):
-                bt[r, :len(tables[s])] = tables[s]
-            tseq, tq0 = K.prefill_tiles(cu, self._prefill_rows, ctx)
-            # everything the chunk needs in ONE pinned host buffer and one non-blocking copy: a
-            # pageable torch.tensor(..., device=cuda) synchronises the stream, so the GPU would idle
-            # while the host builds the next chunk
-            slots_np = np.concatenate(slot_np)
-            runs = K.v_runs(slots_np)
-            parts = [np.concatenate(ids_np), np.concatenate(pos_np), slots_np,
-                     np.asarray(cu, np.int32), np.asarray(ctx, np.int32), np.asarray(tseq, np.int32),
-                     np.asarray(tq0, np.int32), np.asarray(last_rows, np.int32),
-                     np.asarray(finishing, np.int32), bt.reshape(-1), runs.reshape(-1)]
-            dev = self._h2d(np.concatenate(parts))
-            offs = np.cumsum([0] + [len(x) for x in parts]).tolist()
-            d_ids, d_pos, d_slots, d_cu, d_ctx, d_tseq, d_tq0, d_last, d_fin, d_bt, d_runs = (
-                dev[offs[i]:offs[i + 1]] for i in range(len(parts)))
-            hidden = self.model.forward_prefill(
-                d_ids, d_pos, d_slots, d_cu, d_ctx, d_bt.view(len(rows), maxb), self.kv, tiles=(d_tseq, d_tq0),
-                last_idx=d_last.long() if last_rows else None, v_runs=d_runs.view(-1, 4))
-            if finishing:
-                out = torch.empty(len(finishing), dtype=torch.int32, device=self.device)
-                self._next_tokens(hidden, out, temperature, seed, torch.zeros(1, dtype=torch.int32, device=self.device))
-                first_dev.index_copy_(0, d_fin.long(), out)
         return first_dev.tolist()      # the one host sync of the prefill
+
+    def _overlap_split(self, chunk):
+        """TP > 1: a prefill chunk of >= 2 sequences as two halves of whole sequences (token counts
+        balanced), run interleaved so each half's row-parallel all-reduces hide under the other
+        half's GEMMs (DecoderModel.forward_prefill_overlap); opt-in, CFC_TP_PREFILL_OVERLAP=1."""
+        if (len(chunk) < 2 or not self.tp_overlap
+                or not getattr(self.model, "supports_prefill_overlap", lambda: False)()):
+            return [chunk]
+        sizes = [b - a for (_, a, b) in chunk]
+        total, acc, best = sum(sizes), 0, (None, 1)
+        for k in range(1, len(chunk)):
+            acc += sizes[k - 1]
+            d = abs(2 * acc - total)
+            if best[0] is None or d < best[0]:
+                best = (d, k)
+        k = best[1]
+        return [chunk[:k], chunk[k:]]
+
+    def _chunk_meta(self, prompts, tables, chunk):
+        """Device metadata of one packed prefill pass over ``chunk`` [(seq, first, end)]: the
+        forward_prefill keyword arguments, the sequences finishing in it, and their ids on device."""
+        cu, ctx, rows, last_rows, finishing = [0], [], [], [], []
+        ids_np, pos_np, slot_np = [], [], []
+        for (s, a, b) in chunk:
+            ids_np.append(np.asarray(prompts[s][a:b], dtype=np.int32))
+            p = np.arange(a, b, dtype=np.int32)
+            pos_np.append(p)
+            slot_np.append(np.asarray(tables[s], dtype=np.int32)[p // KV_BLOCK] * KV_BLOCK + p % KV_BLOCK)
+            cu.append(cu[-1] + (b - a))
+            ctx.append(b)
+            rows.append(s)
+            if b == len(prompts[s]):
+                last_rows.append(cu[-1] - 1)
+                finishing.append(s)
+        maxb = max(len(tables[s]) for s in rows)
+        bt = np.zeros((len(rows), maxb), dtype=np.int32)
+        for r, s in enumerate(rows):
+            bt[r, :len(tables[s])] = tables[s]
+        tseq, tq0 = K.prefill_tiles(cu, self._prefill_rows, ctx)
+        # everything the pass needs in ONE pinned host buffer and one non-blocking copy: a
+        # pageable torch.tensor(..., device=cuda) synchronises the stream, so the GPU would idle
+        # while the host builds the next chunk
+        slots_np = np.concatenate(slot_np)
+        runs = K.v_runs(slots_np)
+        parts = [np.concatenate(ids_np), np.concatenate(pos_np), slots_np,
+                 np.asarray(cu, np.int32), np.asarray(ctx, np.int32), np.asarray(tseq, np.int32),
+                 np.asarray(tq0, np.int32), np.asarray(last_rows, np.int32),
+                 np.asarray(finishing, np.int32), bt.reshape(-1), runs.reshape(-1)]
+        dev = self._h2d(np.concatenate(parts))
+        offs = np.cumsum([0] + [len(x) for x in parts]).tolist()
+        d_ids, d_pos, d_slots, d_cu, d_ctx, d_tseq, d_tq0, d_last, d_fin, d_bt, d_runs = (
+            dev[offs[i]:offs[i + 1]] for i in range(len(parts)))
+        kw = dict(ids=d_ids, positions=d_pos, slots=d_slots, cu_q=d_cu, ctx_lens=d_ctx,
+                  block_tables=d_bt.view(len(rows), maxb), tiles=(d_tseq, d_tq0),
+                  last_idx=d_last.long() if last_rows else None, v_runs=d_runs.view(-1, 4))
+        return kw, finishing, d_fin
 
     def _h2d(self, a: np.ndarray) -> torch.Tensor:
         t = torch.from_numpy(a)
         if self.device.type != "cuda":
             return t.clone()
         return t.pin_memory().to(self.device, non_blocking=True)
-
-        return first
 
     def _tp_greedy(self, temperature) -> bool:
         return getattr(self.model.w, "tp_size", 1) > 1 and K.SamplingParams.of(temperature).temperature <= 0

@@ -90,6 +90,54 @@ def test_tp2_decoder_matches_unsharded():
     assert agree >= 0.9 * sum(len(x) for x in ref), (outs[0], ref)
 
 
+def _tp_prefill_overlap(env, prompts):
+    """Last-token prefill hidden states of every prompt at TP = world, one pass vs two overlapped
+    halves (async all-reduces interleaved with the other half's compute)."""
+    from copilot_for_consensus_amd.models.decoder import DecoderModel, DecoderWeights, get_config
+    from copilot_for_consensus_amd.parallel import make_groups
+    from copilot_for_consensus_amd.parallel.tp import shard_weights
+    from copilot_for_consensus_amd.runtime.engine import LLMEngine
+    from copilot_for_consensus_amd.runtime.kv_cache import PagedKVCache
+
+    cfg = get_config("tiny")
+    g = make_groups(env, tp=env.world)
+    m = DecoderModel(shard_weights(DecoderWeights.random(cfg, "cpu", seed=5), g.tp_rank, g.tp_size),
+                     tp_group=g.tp_group)
+    out = {}
+    for overlap in (False, True):
+        eng = LLMEngine(m, PagedKVCache(cfg.layers, 64, m.w.kv_heads, cfg.head_dim, "cpu"), prefix_cache=False)
+        eng.tp_overlap, eng.lpt = overlap, False
+        seen, calls = [], []
+        orig_next, orig_ov = eng._next_tokens, m.forward_prefill_overlap
+
+        def cap(hidden, o, t, s, st, orig_next=orig_next, seen=seen):
+            seen.append(hidden.float().clone())
+            return orig_next(hidden, o, t, s, st)
+
+        def ov(*a, orig_ov=orig_ov, calls=calls, **k):
+            calls.append(1)
+            return orig_ov(*a, **k)
+        eng._next_tokens, m.forward_prefill_overlap = cap, ov
+        try:
+            toks = eng.generate(prompts, 1, ignore_eos=True).tokens
+        finally:
+            m.forward_prefill_overlap = orig_ov
+        out[overlap] = (torch.cat(seen).numpy(), toks, len(calls))    # by value: the rank exits first
+    return out
+
+
+def test_tp2_prefill_overlapped_halves_match_one_pass():
+    prompts = [[1, 5, 9, 200, 17, 33], [1] + list(range(40, 110)), [1, 2], [1] + [7] * 40]
+    outs = _run(_tp_prefill_overlap, 2, prompts)
+    for r in outs:
+        (h1, t1, c1), (h2, t2, c2) = r[False], r[True]
+        h1, h2 = torch.from_numpy(h1), torch.from_numpy(h2)
+        assert c1 == 0 and c2 == 1                       # the overlapped path ran (one chunk, two halves)
+        assert h1.shape == h2.shape == (len(prompts), h1.shape[1])
+        assert float((h1 - h2).abs().max()) <= 2e-2 * float(h1.abs().max()), float((h1 - h2).abs().max())
+        assert t1 == t2
+
+
 def test_shard_weights_reassemble():
     from copilot_for_consensus_amd.models.decoder import DecoderWeights, get_config
     from copilot_for_consensus_amd.parallel.tp import shard_weights

@@ -53,8 +53,8 @@ def _prefix_logits(eng, model, prefixes):
     finally:
         eng._next_tokens = orig
         eng.lpt = True
-    assert len(got) == 1
-    return got[0]
+    assert len(got) in (1, 2)       # TP: the chunk may run as two overlapped halves, rows in order
+    return torch.cat(got)
 
 
 def _full_weights():
