@@ -290,3 +290,20 @@ def test_single_stream_fused_norm_decode_bit_identical(use_graph):
         kv = PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, "cuda")
         toks.append(LLMEngine(m, kv, use_graph=use_graph).generate(prompts, 24, ignore_eos=True).tokens)
     assert toks[0] == toks[1]
+
+
+def test_longest_first_slots_give_every_prompt_the_same_tokens():
+    """The engine's longest-first slot order (decode attention list scheduling) is a placement
+    only: each prompt's greedy tokens are bit-identical to the caller-order run (the decode GEMMs,
+    attention and sampler are row-independent), and come back in the caller's order."""
+    cfg = get_config("tiny")
+    m = DecoderModel(DecoderWeights.random(cfg, "cuda", seed=5))
+    prompts = PROMPTS8 + [[1] + list(range(10, 10 + n)) for n in (3, 90, 41, 160, 12, 77, 5, 120)]
+    out = {}
+    for lpt in (False, True):
+        eng = LLMEngine(m, PagedKVCache(cfg.layers, 128, cfg.kv_heads, cfg.head_dim, "cuda"), max_prefill_tokens=8192)
+        eng.lpt = lpt
+        r = eng.generate(prompts, 24, ignore_eos=True)
+        out[lpt] = (r.tokens, r.prompt_lens)
+    assert out[True] == out[False]
+    assert out[True][1] == [len(p) for p in prompts]
