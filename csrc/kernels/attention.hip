@@ -929,11 +929,14 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
     const int key0 = kt * PF_KT;
     const bool below = window > 0 && key0 + PF_KT - 1 <= wave_min_pos - window;  // all keys out of window
     if (key0 <= wave_min_pos + 31 && !below) {     // else every key of the tile is masked for this wave
+      // scores come out of the MFMA already shifted by the running max (the accumulator starts at
+      // -m): a tile that needs no rescale goes straight to exp2, without 32 subtractions per lane
+      const float mref0 = m == -INFINITY ? 0.f : m;
       f32x16_t sc[2];
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sc[hf][r] = 0.f;
+        for (int r = 0; r < 16; ++r) sc[hf][r] = -mref0;
         const int row = 32 * hf + l32;
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks)
@@ -953,24 +956,28 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
           for (int r = 0; r < 16; ++r)
             if (key0 + 32 * hf + 8 * (r >> 2) + 4 * hi + (r & 3) <= my_pos - window) sc[hf][r] = -INFINITY;
       }
-      float tmax = fmaxf(sc[0][0], sc[1][0]);
+      float tmax = fmaxf(sc[0][0], sc[1][0]);     // the tile's row max minus mref0
 #pragma unroll
       for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, fmaxf(sc[0][r], sc[1][r]));
       tmax = pair_max(tmax);
-      if (!__all(tmax - m <= RESCALE_THR)) {
-        const float mn = fmaxf(m, tmax);
+      if (!__all(m != -INFINITY && tmax <= RESCALE_THR)) {
+        const float mn = fmaxf(m, mref0 + tmax);
         const float alpha = __builtin_amdgcn_exp2f(m - (mn == -INFINITY ? 0.f : mn));
         l *= alpha;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
         m = mn;
+        const float shift = (m == -INFINITY ? 0.f : m) - mref0;
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sc[hf][r] -= shift;
       }
-      const float mref = m == -INFINITY ? 0.f : m;
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float e = __builtin_amdgcn_exp2f(sc[hf][r] - mref);
+          const float e = __builtin_amdgcn_exp2f(sc[hf][r]);
           sc[hf][r] = e;
           l += e;
         }
