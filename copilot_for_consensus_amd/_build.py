@@ -35,6 +35,10 @@ CXX = os.environ.get("CXX", shutil.which("g++") or "c++")
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={OFFLOAD_ARCH}", "-ffp-contract=fast",
              "-Wno-unused-result"]
 CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
+# per-source additions.  attention.hip: no NaN ever enters the softmax (masked scores are -inf,
+# which stays honoured), and without NaN semantics fmaxf needs no canonicalising v_max_f32 in front
+# of every MFMA output it reads -- 33 fewer VALU instructions per prefill KV tile
+FILE_FLAGS = {"attention.hip": ["-fno-honor-nans"]}
 
 KERNELS_LIB = LIB_DIR / "libcfc_kernels.so"
 RUNTIME_LIB = LIB_DIR / "libcfc_runtime.so"
@@ -70,8 +74,9 @@ def _build_lib(sources: list[Path], headers: list[Path], compiler: str, flags: l
         for src in sources:
             obj = OBJ_DIR / (src.stem + (".hip.o" if src.suffix == ".hip" else ".o"))
             stamp = obj.with_suffix(obj.suffix + ".stamp")
-            digest = _digest([src, *headers], flags)
-            cmd = [compiler, *flags, f"-I{src.parent}"]
+            fflags = [*flags, *FILE_FLAGS.get(src.name, [])]
+            digest = _digest([src, *headers], fflags)
+            cmd = [compiler, *fflags, f"-I{src.parent}"]
             tasks.append(pool.submit(_compile, cmd, src, obj, stamp, digest))
             objs.append(obj)
         for t in tasks:
