@@ -396,6 +396,10 @@ __global__ void __launch_bounds__(128) decode_combine_kernel(const float* __rest
 //   * The host orders tiles heaviest-first (most keys) so the causal triangle drains evenly.
 // ------------------------------------------------------------------------------------------
 constexpr int PF_KT = 64;     // keys per tile
+#ifndef CFC_PF_QK_PIPE
+#define CFC_PF_QK_PIPE 1
+#endif
+constexpr bool PF_QK_PIPE = CFC_PF_QK_PIPE;   // prefill v5: K fragments of a half-tile read ahead of its MFMAs
 constexpr int PF_WAVES = 8;
 constexpr int PF_ROWS = 16 * PF_WAVES;
 constexpr float RESCALE_THR = 8.0f;
@@ -915,6 +919,9 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
   float m = -INFINITY, l = 0.f;   // l: this lane's partial row sum (its 32 of every 64 keys)
+  // l in 4 interleaved partial sums: one serial chain of 32 dependent v_add_f32 per tile was
+  // on the critical path between the exp2s and the next tile (ISA); summed once at the end
+  float lp[4] = {0.f, 0.f, 0.f, 0.f};
 
   gload(kt_begin);
   lwrite(kt_begin & 1, kt_begin);
@@ -938,9 +945,22 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) sc[hf][r] = -mref0;
         const int row = 32 * hf + l32;
+        // all 8 K fragments of the half in flight before its MFMA chain (PF_QK_PIPE): left to
+        // itself hipcc issued read -> lgkmcnt(0) -> MFMA sixteen times, one LDS round trip each
+        if constexpr (PF_QK_PIPE) {
+          uint4 kf[8];
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks)
-          sc[hf] = mfma32(as_bf16x8(*reinterpret_cast<const uint4*>(kb + k_lds_off(row, 2 * ks + hi))), qf[ks], sc[hf]);
+          for (int ks = 0; ks < 8; ++ks) kf[ks] = *reinterpret_cast<const uint4*>(kb + k_lds_off(row, 2 * ks + hi));
+#pragma unroll
+          for (int ks = 0; ks < 8; ++ks) sc[hf] = mfma32(as_bf16x8(kf[ks]), qf[ks], sc[hf]);
+          __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);   // 8 DS reads, then
+          __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);   // the 8 MFMAs (counted lgkmcnt waits)
+        } else {
+#pragma unroll
+          for (int ks = 0; ks < 8; ++ks)
+            sc[hf] = mfma32(as_bf16x8(*reinterpret_cast<const uint4*>(kb + k_lds_off(row, 2 * ks + hi))), qf[ks],
+                            sc[hf]);
+        }
       }
       if (key0 + PF_KT - 1 > wave_min_pos) {  // diagonal tile: causal mask
 #pragma unroll
@@ -963,7 +983,8 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
       if (!__all(m != -INFINITY && tmax <= RESCALE_THR)) {
         const float mn = fmaxf(m, mref0 + tmax);
         const float alpha = __builtin_amdgcn_exp2f(m - (mn == -INFINITY ? 0.f : mn));
-        l *= alpha;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) lp[u] *= alpha;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
         m = mn;
@@ -979,7 +1000,7 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
         for (int r = 0; r < 16; ++r) {
           const float e = __builtin_amdgcn_exp2f(sc[hf][r]);
           sc[hf][r] = e;
-          l += e;
+          lp[r & 3] += e;
         }
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf)
@@ -1001,7 +1022,7 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
     __syncthreads();
   }
 
-  l = pair_sum(l);
+  l = pair_sum((lp[0] + lp[1]) + (lp[2] + lp[3]));
   if (my_row < q_len) {
     const float inv = l > 0.f ? v_scale / l : 0.f;
     uint16_t* orow = out + ((size_t)(q_begin + my_row) * Hq + hq) * D;
