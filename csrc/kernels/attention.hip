@@ -399,7 +399,7 @@ constexpr int PF_KT = 64;     // keys per tile
 #ifndef CFC_PF_QK_PIPE
 #define CFC_PF_QK_PIPE 1
 #endif
-constexpr bool PF_QK_PIPE = CFC_PF_QK_PIPE;   // prefill v5: K fragments of a half-tile read ahead of its MFMAs
+constexpr int PF_QK_PIPE = CFC_PF_QK_PIPE;   // prefill v5: K fragments of a half-tile read ahead of its MFMAs
 constexpr int PF_WAVES = 8;
 constexpr int PF_ROWS = 16 * PF_WAVES;
 constexpr float RESCALE_THR = 8.0f;
@@ -940,6 +940,25 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
       // -m): a tile that needs no rescale goes straight to exp2, without 32 subtractions per lane
       const float mref0 = m == -INFINITY ? 0.f : m;
       f32x16_t sc[2];
+      if constexpr (PF_QK_PIPE == 2) {
+        // both halves' 16 K fragments in flight before the 16 MFMAs (246 VGPRs; measured equal to
+        // one half at a time, profiles/r05_ab_prefill_attn_qkpipe2.log)
+        uint4 kf[2][8];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+          for (int ks = 0; ks < 8; ++ks)
+            kf[hf][ks] = *reinterpret_cast<const uint4*>(kb + k_lds_off(32 * hf + l32, 2 * ks + hi));
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sc[hf][r] = -mref0;
+#pragma unroll
+          for (int ks = 0; ks < 8; ++ks) sc[hf] = mfma32(as_bf16x8(kf[hf][ks]), qf[ks], sc[hf]);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+      } else
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
 #pragma unroll
