@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B of two builds of libcfc_kernels.so (build/ab/old.so vs build/ab/new.so) on the prefill
-# attention micro-benchmark, interleaved; restores new.so at the end.
+# attention micro-benchmark, interleaved; restores new.so at the end.  build/ab is listed in
+# .gpurunignore (20 MB per call otherwise): drop that line for the call that runs this script.
 set -o pipefail
 mkdir -p gpurun_out
 LIB=copilot_for_consensus_amd/_lib/libcfc_kernels.so
