@@ -399,7 +399,12 @@ constexpr int PF_KT = 64;     // keys per tile
 #ifndef CFC_PF_QK_PIPE
 #define CFC_PF_QK_PIPE 1
 #endif
-constexpr int PF_QK_PIPE = CFC_PF_QK_PIPE;   // prefill v5: K fragments of a half-tile read ahead of its MFMAs
+constexpr int PF_QK_PIPE = CFC_PF_QK_PIPE;
+#ifndef CFC_PF_V_EARLY
+#define CFC_PF_V_EARLY 1
+#endif
+constexpr bool PF_V_EARLY = CFC_PF_V_EARLY;   // prefill v5: first half's V fragments read before the softmax
+   // prefill v5: K fragments of a half-tile read ahead of its MFMAs
 constexpr int PF_WAVES = 8;
 constexpr int PF_ROWS = 16 * PF_WAVES;
 constexpr float RESCALE_THR = 8.0f;
@@ -981,6 +986,15 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
                             sc[hf]);
         }
       }
+      // the first half's 8 V^T fragments read now, under the softmax's VALU work (PF_V_EARLY)
+      uint4 vf0[2][4];
+      if constexpr (PF_V_EARLY) {
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt)
+            vf0[ss][dt] = *reinterpret_cast<const uint4*>(vb + v5_off(32 * dt + l32, 2 * ss + hi));
+      }
       if (key0 + PF_KT - 1 > wave_min_pos) {  // diagonal tile: causal mask
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf)
@@ -995,9 +1009,16 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
           for (int r = 0; r < 16; ++r)
             if (key0 + 32 * hf + 8 * (r >> 2) + 4 * hi + (r & 3) <= my_pos - window) sc[hf][r] = -INFINITY;
       }
-      float tmax = fmaxf(sc[0][0], sc[1][0]);     // the tile's row max minus mref0
+      // the tile's row max minus mref0: two interleaved v_max3 chains (16 instructions for 32
+      // values; the pairwise form compiled to 16 v_max + 8 v_max3)
+      float ta = fmaxf(fmaxf(sc[0][0], sc[0][1]), sc[0][2]);
+      float tb = fmaxf(fmaxf(sc[1][0], sc[1][1]), sc[1][2]);
 #pragma unroll
-      for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, fmaxf(sc[0][r], sc[1][r]));
+      for (int r = 3; r < 15; r += 2) {
+        ta = fmaxf(fmaxf(ta, sc[0][r]), sc[0][r + 1]);
+        tb = fmaxf(fmaxf(tb, sc[1][r]), sc[1][r + 1]);
+      }
+      float tmax = fmaxf(fmaxf(ta, sc[0][15]), fmaxf(tb, sc[1][15]));
       tmax = pair_max(tmax);
       if (!__all(m != -INFINITY && tmax <= RESCALE_THR)) {
         const float mn = fmaxf(m, mref0 + tmax);
@@ -1034,7 +1055,9 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
           const int c = 4 * hf + 2 * ss + hi;
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt)
-            o[dt] = mfma32(as_bf16x8(*reinterpret_cast<const uint4*>(vb + v5_off(32 * dt + l32, c))), pf, o[dt]);
+            o[dt] = mfma32(as_bf16x8(PF_V_EARLY && hf == 0 ? vf0[ss][dt]
+                                                           : *reinterpret_cast<const uint4*>(vb + v5_off(32 * dt + l32, c))),
+                           pf, o[dt]);
         }
     }
     if (more) lwrite(cur ^ 1, kt + 1);
