@@ -403,7 +403,7 @@ constexpr int PF_QK_PIPE = CFC_PF_QK_PIPE;
 #ifndef CFC_PF_V_EARLY
 #define CFC_PF_V_EARLY 1
 #endif
-constexpr bool PF_V_EARLY = CFC_PF_V_EARLY;   // prefill v5: first half's V fragments read before the softmax
+constexpr int PF_V_EARLY = CFC_PF_V_EARLY;   // prefill v5: V fragments of the first PF_V_EARLY half-tiles read before the softmax (2: 251 VGPRs, 1 % slower, profiles/r05_ab_prefill_attn_vearly2_rejected.log)
    // prefill v5: K fragments of a half-tile read ahead of its MFMAs
 constexpr int PF_WAVES = 8;
 constexpr int PF_ROWS = 16 * PF_WAVES;
@@ -987,13 +987,15 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
         }
       }
       // the first half's 8 V^T fragments read now, under the softmax's VALU work (PF_V_EARLY)
-      uint4 vf0[2][4];
+      uint4 vf0[2][2][4];
       if constexpr (PF_V_EARLY) {
 #pragma unroll
-        for (int ss = 0; ss < 2; ++ss)
+        for (int hf = 0; hf < PF_V_EARLY; ++hf)
 #pragma unroll
-          for (int dt = 0; dt < 4; ++dt)
-            vf0[ss][dt] = *reinterpret_cast<const uint4*>(vb + v5_off(32 * dt + l32, 2 * ss + hi));
+          for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+              vf0[hf][ss][dt] = *reinterpret_cast<const uint4*>(vb + v5_off(32 * dt + l32, 4 * hf + 2 * ss + hi));
       }
       if (key0 + PF_KT - 1 > wave_min_pos) {  // diagonal tile: causal mask
 #pragma unroll
@@ -1055,8 +1057,8 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
           const int c = 4 * hf + 2 * ss + hi;
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt)
-            o[dt] = mfma32(as_bf16x8(PF_V_EARLY && hf == 0 ? vf0[ss][dt]
-                                                           : *reinterpret_cast<const uint4*>(vb + v5_off(32 * dt + l32, c))),
+            o[dt] = mfma32(as_bf16x8(hf < PF_V_EARLY ? vf0[hf][ss][dt]
+                                                     : *reinterpret_cast<const uint4*>(vb + v5_off(32 * dt + l32, c))),
                            pf, o[dt]);
         }
     }
