@@ -158,6 +158,7 @@ struct BPE {
 struct WordPiece {
   std::unordered_map<std::string, int> vocab;
   int unk_id, cls_id, sep_id, max_chars;
+  size_t max_piece = 0;   // longest vocabulary entry in bytes: longer substrings are never looked up
   bool lower;
 
   static bool is_punct(uint32_t cp) {
@@ -169,9 +170,8 @@ struct WordPiece {
     return (cp >= 0x4E00 && cp <= 0x9FFF) || (cp >= 0x3400 && cp <= 0x4DBF) || (cp >= 0xF900 && cp <= 0xFAFF) ||
            (cp >= 0x20000 && cp <= 0x2FA1F);
   }
-  static uint32_t decode_cp(const std::string& ch) {
-    const unsigned char* s = (const unsigned char*)ch.data();
-    switch (ch.size()) {
+  static uint32_t decode_cp(const unsigned char* s, int n) {
+    switch (n) {
       case 1: return s[0];
       case 2: return ((s[0] & 0x1F) << 6) | (s[1] & 0x3F);
       case 3: return ((s[0] & 0x0F) << 12) | ((s[1] & 0x3F) << 6) | (s[2] & 0x3F);
@@ -179,46 +179,75 @@ struct WordPiece {
     }
   }
 
-  void basic_split(const std::string& text, std::vector<std::string>& words) const {
-    std::string cur;
-    auto flush = [&] { if (!cur.empty()) { words.push_back(cur); cur.clear(); } };
-    for (auto& ch : utf8_chars(text)) {
-      const uint32_t cp = decode_cp(ch);
-      if (cp == ' ' || cp == '\t' || cp == '\n' || cp == '\r' || cp == 0xA0) { flush(); continue; }
-      if (cp == 0 || cp == 0xFFFD || (cp < 32)) continue;
-      if (is_punct(cp) || is_cjk(cp)) { flush(); words.push_back(ch); continue; }
-      if (lower && ch.size() == 1) cur.push_back((char)std::tolower((unsigned char)ch[0]));
-      else cur += ch;
+  // Per-thread scratch: the encode loop allocates nothing once these have grown.
+  struct Scratch {
+    std::string word, sub;
+    std::vector<int> bounds, pieces;
+  };
+
+  // Greedy longest-match-first pieces of one basic-split word (bytes in sc.word).
+  void encode_word(Scratch& sc, std::vector<int>& out) const {
+    const std::string& w = sc.word;
+    sc.bounds.clear();
+    for (size_t i = 0; i < w.size();) {
+      sc.bounds.push_back((int)i);
+      i += (size_t)std::min<int>(utf8_len((unsigned char)w[i]), (int)(w.size() - i));
     }
-    flush();
+    const int nch = (int)sc.bounds.size();
+    sc.bounds.push_back((int)w.size());
+    if (nch > max_chars) { out.push_back(unk_id); return; }
+    sc.pieces.clear();
+    int start = 0;
+    while (start < nch) {
+      const size_t pre = start > 0 ? 2 : 0;
+      int end = nch, found = -1;
+      // substrings longer than the longest vocabulary entry cannot match: start below them
+      while (end > start && (size_t)(sc.bounds[end] - sc.bounds[start]) + pre > max_piece) --end;
+      for (; end > start; --end) {
+        sc.sub.assign(start > 0 ? "##" : "");
+        sc.sub.append(w, (size_t)sc.bounds[start], (size_t)(sc.bounds[end] - sc.bounds[start]));
+        auto it = vocab.find(sc.sub);
+        if (it != vocab.end()) { found = it->second; break; }
+      }
+      if (found < 0) { out.push_back(unk_id); return; }
+      sc.pieces.push_back(found);
+      start = end;
+    }
+    out.insert(out.end(), sc.pieces.begin(), sc.pieces.end());
   }
 
-  void encode(const std::string& text, std::vector<int>& out) const {
-    std::vector<std::string> words;
-    basic_split(text, words);
-    for (const auto& w : words) {
-      auto chars = utf8_chars(w);
-      if ((int)chars.size() > max_chars) { out.push_back(unk_id); continue; }
-      std::vector<int> pieces;
-      size_t start = 0;
-      bool bad = false;
-      while (start < chars.size()) {
-        size_t end = chars.size();
-        int found = -1;
-        while (start < end) {
-          std::string sub = start > 0 ? "##" : "";
-          for (size_t c = start; c < end; ++c) sub += chars[c];
-          auto it = vocab.find(sub);
-          if (it != vocab.end()) { found = it->second; break; }
-          --end;
-        }
-        if (found < 0) { bad = true; break; }
-        pieces.push_back(found);
-        start = end;
+  // BERT basic split (whitespace, control characters dropped, punctuation and CJK as single
+  // words, ASCII lower-casing) fused with the WordPiece pass; stops once out holds `limit` ids
+  // (the callers truncate there), so a long chunk is not encoded past its model's max length.
+  void encode(const std::string& text, std::vector<int>& out, Scratch& sc, size_t limit = SIZE_MAX) const {
+    sc.word.clear();
+    auto flush = [&] {
+      if (!sc.word.empty()) { encode_word(sc, out); sc.word.clear(); }
+    };
+    const unsigned char* t = (const unsigned char*)text.data();
+    const size_t n = text.size();
+    for (size_t i = 0; i < n && out.size() < limit;) {
+      const int len = std::min<int>(utf8_len(t[i]), (int)(n - i));
+      const uint32_t cp = decode_cp(t + i, len);
+      if (cp == ' ' || cp == '\t' || cp == '\n' || cp == '\r' || cp == 0xA0) {
+        flush();
+      } else if (cp == 0 || cp == 0xFFFD || cp < 32) {
+      } else if (is_punct(cp) || is_cjk(cp)) {
+        flush();
+        sc.word.assign((const char*)t + i, (size_t)len);
+        flush();
+      } else if (lower && len == 1) {
+        sc.word.push_back((char)std::tolower(t[i]));
+      } else {
+        sc.word.append((const char*)t + i, (size_t)len);
       }
-      if (bad) out.push_back(unk_id);
-      else out.insert(out.end(), pieces.begin(), pieces.end());
+      i += (size_t)len;
     }
+    if (out.size() < limit) flush();
+  }
+  void encode(const std::string& text, std::vector<int>& out) const {
+    Scratch sc;
+    encode(text, out, sc);
   }
 };
 
@@ -401,7 +430,9 @@ CFC_API void* cfc_wp_create(int unk_id, int cls_id, int sep_id, int lowercase) {
 }
 CFC_API int cfc_wp_destroy(void* h) { delete static_cast<WordPiece*>(h); return 0; }
 CFC_API int cfc_wp_add_token(void* h, const char* tok, int len, int id) {
-  static_cast<WordPiece*>(h)->vocab[std::string(tok, len)] = id;
+  auto* w = static_cast<WordPiece*>(h);
+  w->vocab[std::string(tok, len)] = id;
+  w->max_piece = std::max(w->max_piece, (size_t)len);
   return 0;
 }
 CFC_API int cfc_wp_finalize(void*) { return 0; }
@@ -461,12 +492,17 @@ CFC_API int cfc_bpe_encode_pieces(void* h, const char* buf, const int64_t* offs,
 
 CFC_API int cfc_wp_encode_batch(void* h, const char* buf, const int64_t* offs, int n, int cap, int32_t* out,
                                 int32_t* lens, int nthreads) {
+  // every caller truncates to cap (the model's max length): encoding stops there, and lens[i]
+  // holds at least min(full length, cap) -- callers use min(lens[i], cap)
   const auto* w = static_cast<const WordPiece*>(h);
   parallel_texts(n, nthreads, [&](int t, int nt) {
     std::vector<int> ids;
+    WordPiece::Scratch sc;
+    std::string text;
     for (int i = t; i < n; i += nt) {
       ids.clear();
-      w->encode(std::string(buf + offs[i], (size_t)(offs[i + 1] - offs[i])), ids);
+      text.assign(buf + offs[i], (size_t)(offs[i + 1] - offs[i]));
+      w->encode(text, ids, sc, (size_t)cap);
       lens[i] = (int32_t)ids.size();
       const int m = std::min((int)ids.size(), cap);
       for (int k = 0; k < m; ++k) out[(size_t)i * cap + k] = ids[k];
