@@ -406,15 +406,15 @@ def synthetic_bpe(vocab_size: int = 32000, corpus_words: int = 800_000) -> BPETo
         return tok
 
 
-_ASCII_CTRL = re.compile(r"[\x00-\x08\x0b\x0c\x0e-\x1f\x7f]")
 
 
 def bert_normalize(text: str, lowercase: bool = True) -> str:
     """HF BertNormalizer + the Unicode part of BertPreTokenizer, for non-ASCII text: drop control
     characters, map Unicode spaces to ' ', strip accents (NFD, drop Mn) and lower-case (uncased
     models), and space-pad Unicode punctuation so the C++ splitter isolates it.  Pure-ASCII text
-    without control characters is returned unchanged -- the C++ tokenizer handles it natively."""
-    if text.isascii() and not _ASCII_CTRL.search(text):
+    is returned unchanged: the C++ splitter treats \t \n \r as spaces and drops the other ASCII
+    control characters (and DEL) itself, as HF does -- no per-text regex scan."""
+    if text.isascii():
         return text
     out = []
     for c in text:

@@ -231,7 +231,7 @@ struct WordPiece {
       const uint32_t cp = decode_cp(t + i, len);
       if (cp == ' ' || cp == '\t' || cp == '\n' || cp == '\r' || cp == 0xA0) {
         flush();
-      } else if (cp == 0 || cp == 0xFFFD || cp < 32) {
+      } else if (cp == 0 || cp == 0xFFFD || cp < 32 || cp == 0x7F) {   // control characters dropped (HF: Cc)
       } else if (is_punct(cp) || is_cjk(cp)) {
         flush();
         sc.word.assign((const char*)t + i, (size_t)len);

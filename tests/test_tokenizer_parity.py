@@ -172,3 +172,14 @@ def test_bytelevel_bpe_matches_hf(bytelevel, corpus):
 def test_fuzz_bytelevel(bytelevel, text):
     ref, mine = bytelevel
     assert mine.encode(text, add_bos=False) == ref.encode(text).ids
+
+
+@pytest.mark.parametrize("text", ["a\x7fb c", "x\x0by\x0cz", "one\x1ctwo\x1dthree\x1e four\x1f", "tab\there\nnew\rline",
+                                  "del\x7f\x7f end", "\x00nul\x01soh\x08bs word", "mixed \x7fDEL, and ctrl\x0b."])
+def test_wordpiece_ascii_control_characters_match_hf(wordpiece, text):
+    """Pure-ASCII text skips the Python normaliser: the C++ splitter must treat \\t \\n \\r as spaces
+    and drop every other ASCII control character and DEL exactly as HF's BertNormalizer does."""
+    ref, ours = wordpiece
+    assert ours.encode(text)[1:-1] == ref.encode(text).ids             # ours adds [CLS] ... [SEP]
+    ids, cu = ours.encode_packed([text, text + " tail"])
+    assert ids[cu[0] + 1:cu[1] - 1].tolist() == ref.encode(text).ids
