@@ -120,12 +120,17 @@ class DraftDetector:
     def detect(self, text: str) -> list[str]:
         if not text:
             return []
+        matches = self.regex.finditer(text)
         if self._prefilter:
             low = text.lower()
             if "rfc" not in low and "draft-" not in low:
                 return []
+            if len(low) == len(text):
+                # the default pattern can only start where "draft-" or "rfc" does (any case): run it
+                # at those positions only, left to right and non-overlapping as finditer would
+                matches = self._anchored(text, low)
         out, seen = [], set()
-        for m in self.regex.finditer(text):
+        for m in matches:
             g = next(x for x in m.groups() if x)
             if g.lower().startswith("rfc"):
                 g = "RFC " + re.search(r"\d+", g).group()
@@ -133,6 +138,22 @@ class DraftDetector:
                 seen.add(g)
                 out.append(g)
         return out
+
+    def _anchored(self, text: str, low: str):
+        starts = []
+        for needle in ("draft-", "rfc"):
+            i = low.find(needle)
+            while i >= 0:
+                starts.append(i)
+                i = low.find(needle, i + 1)
+        end = 0
+        for i in sorted(starts):
+            if i < end:
+                continue
+            m = self.regex.match(text, i)
+            if m is not None and m.end() > m.start():
+                yield m
+                end = m.end()
 
 
 # ------------------------------------------------------------------------------ message parser
