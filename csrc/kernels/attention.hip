@@ -1229,26 +1229,32 @@ __global__ void __launch_bounds__(256) encoder_attn_kernel(const uint16_t* __res
       float tmax = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
                          fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
       tmax = quad_max(tmax);
-      const float mn = fmaxf(m[rg], tmax);
-      const float alpha = __builtin_amdgcn_exp2f(m[rg] - mn);
+      // deferred rescale (guide T13, as in the prefill kernel): O and l are rescaled only when the
+      // running max grows by more than RESCALE_THR, not on every 32-key step -- the per-step
+      // multiply of O (held in AGPRs) cost a read / multiply / write per register
+      if (!__all(tmax - m[rg] <= RESCALE_THR)) {
+        const float mn = fmaxf(m[rg], tmax);
+        const float alpha = __builtin_amdgcn_exp2f(m[rg] - (mn == -INFINITY ? 0.f : mn));
+        l[rg] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[rg][dt] *= alpha;
+        m[rg] = mn;
+      }
+      const float mref = m[rg] == -INFINITY ? 0.f : m[rg];
       float rs = 0.f;
 #pragma unroll
       for (int st = 0; st < 2; ++st)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float e = __builtin_amdgcn_exp2f(sc[st][i] - mn);
+          const float e = __builtin_amdgcn_exp2f(sc[st][i] - mref);
           sc[st][i] = e;
           rs += e;
         }
       rs = quad_sum(rs);
-      l[rg] = l[rg] * alpha + rs;
-      m[rg] = mn;
+      l[rg] += rs;
       const bf16x8_t pf = pack_p(sc[0], sc[1]);
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        o[rg][dt] *= alpha;
-        o[rg][dt] = mfma16(vf[dt], pf, o[rg][dt]);
-      }
+      for (int dt = 0; dt < DT; ++dt) o[rg][dt] = mfma16(vf[dt], pf, o[rg][dt]);
     }
   }
 
