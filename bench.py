@@ -22,10 +22,21 @@ import statistics
 import sys
 import time
 
+# before torch loads: c10d logs every timed-out TCPStore wait of the DP control plane's idle
+# threads (--pipeline node) as a warning
+os.environ.setdefault("TORCH_CPP_LOG_LEVEL", "ERROR")
+
 # Reference operating point derived in BASELINE.md: best published number (RTX 4090, 150-200
 # tok/s Ollama decode) => ~3-4 s per thread => 0.25-0.33 threads/s.  We divide by the MOST
 # favourable-to-the-reference value (1/3 thread/s); the AMD RX 6700 XT point is 0.07-0.09.
 BASELINE_THREADS_PER_S = 1.0 / 3.0
+
+
+def metric_name(model: str) -> str:
+    """BASELINE.json's metric string, with the decoder actually run (``--model``) in it."""
+    words = model.split("-")
+    pretty = "-".join(w.capitalize() if not w[:1].isdigit() else w.upper() for w in words)
+    return f"end-to-end threads summarized/sec + p50 summary latency, {pretty} TP=1/8"
 
 
 def parse_args(argv=None):
@@ -211,7 +222,7 @@ def main(argv=None):
                              p95_s=round(max(p["p95_s"] for p in parts), 3))
     if rank == 0:
         out = {
-            "metric": "end-to-end threads summarized/sec + p50 summary latency, Mistral-7B TP=1/8",
+            "metric": metric_name(args.model),
             "value": round(value, 4),
             "unit": "threads/s",
             "n_gpus": world,
@@ -311,7 +322,7 @@ def _main_node(args, env, groups):
     if rank == 0:
         value = threads / elapsed
         print(json.dumps({
-            "metric": "end-to-end threads summarized/sec + p50 summary latency, Mistral-7B TP=1/8",
+            "metric": metric_name(args.model),
             "value": round(value, 4), "unit": "threads/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": round(value / BASELINE_THREADS_PER_S, 2), "dtype": "bf16",

@@ -24,9 +24,16 @@ data on its owner GPU:
 * summaries stream: a thread is submitted to its owner's engine and its summary comes back through
   the owner's result stream; a rank whose heartbeat stops has its in-flight threads resubmitted to
   a live rank (at-least-once processing, exactly-once results: a result is matched to its request
-  key and a late duplicate of a resubmitted request is dropped).  Only a stale heartbeat marks a
-  rank dead -- a slow reply or a handler error does not -- and it is re-checked on every routing
-  decision, so a rank whose heartbeat resumes gets its threads back.
+  key and a late duplicate of a resubmitted request is dropped).  A rank is dead when its heartbeat
+  is stale, or when it is busy and its progress counter (engine decode steps, finished work) has
+  not moved for the stall timeout -- a GPU hung inside a kernel, whose heartbeat thread still beats
+  (the reference's nack + requeue of a failed consumer, rabbitmq_subscriber.py:537-560, and its
+  stuck-document retry job, scripts/retry_stuck_documents.py:314-357).  A slow reply or a handler
+  error does not mark a rank dead, and liveness is re-checked on every routing decision, so a rank
+  whose heartbeat or progress resumes gets its threads back;
+* waits are blocking server-side TCPStore waits on a per-thread client (woken when the key is set),
+  not polls; every cursor (request served, result published) is a counter in the store, so a
+  restarted rank process continues the numbering its predecessor left.
 
 Nothing here is a collective, so a dead rank cannot hang the others.
 """
@@ -55,19 +62,73 @@ class RemoteError(RuntimeError):
     """A DP rank's handler raised: the rank is alive, the request failed."""
 
 
-def _wait_key(store, key: str, timeout: float) -> bool:
-    """Poll until ``key`` exists (short check requests with a backoff of 1 -> 20 ms).  Never a
-    blocking store.wait(): a TCPStore client serialises its requests, so one thread parked in a
-    wait would stall every other thread's heartbeat / reply on the same client."""
+_waiters = threading.local()
+WAIT_SLICE_S = 30.0    # an idle blocked waiter re-checks its deadline / stop flag this often
+HOLE_POLL_S = 0.5      # ... and this often while a later number exists (a hole may need skipping)
+WAKE_OP = "__wake__"   # a request / result that only wakes its waiter (stop)
+
+
+def _waiter(store):
+    """This thread's own TCPStore client of ``store``'s server, for blocking waits.  A TCPStore
+    client serialises its requests, so a thread parked in ``wait`` on the shared client would stall
+    every other thread's heartbeat / reply; a client per waiting thread does not, and the server
+    wakes it the moment the key is set (no polling).  None for other stores (HashStore, FileStore,
+    prefix wrappers): those are polled."""
+    try:
+        from torch.distributed import TCPStore
+    except ImportError:  # pragma: no cover
+        return None
+    if not isinstance(store, TCPStore):
+        return None
+    cache = getattr(_waiters, "clients", None)
+    if cache is None:
+        cache = _waiters.clients = {}
+    addr = (store.host, store.port)
+    c = cache.get(addr)
+    if c is None:
+        import datetime
+        c = cache[addr] = TCPStore(store.host, store.port, is_master=False, wait_for_workers=False,
+                                   timeout=datetime.timedelta(seconds=60))
+    return c
+
+
+def _wait_key(store, key: str, timeout: float, stop: threading.Event | None = None) -> bool:
+    """Wait until ``key`` exists, at most ``timeout`` s (or until ``stop`` is set).  TCPStore: a
+    blocking server-side wait on this thread's own client (woken when the key is set), in slices of
+    WAIT_SLICE_S so the deadline and ``stop`` are honoured; other stores: check polls with a 1 -> 20
+    ms backoff."""
     deadline = time.monotonic() + timeout
+    w = _waiter(store)
+    if w is not None:
+        import datetime
+        while True:
+            if stop is not None and stop.is_set():
+                return False
+            left = deadline - time.monotonic()
+            if left <= 0:
+                return bool(w.check([key]))
+            try:
+                w.wait([key], datetime.timedelta(seconds=min(left, WAIT_SLICE_S)))
+                return True
+            except Exception:  # noqa: BLE001 -- DistStoreError on timeout; a lost server ends below
+                if not _alive(w):
+                    raise
     nap = 0.001
     while True:
         if store.check([key]):
             return True
-        if time.monotonic() >= deadline:
+        if time.monotonic() >= deadline or (stop is not None and stop.is_set()):
             return False
         time.sleep(nap)
         nap = min(0.02, nap * 1.5)
+
+
+def _alive(store) -> bool:
+    try:
+        store.check(["__ping__"])
+        return True
+    except Exception:  # noqa: BLE001
+        return False
 
 
 def _delete(store, key: str) -> bool:
@@ -127,21 +188,39 @@ class StoreRPC:
                 return
             self._abandoned = [k for k in self._abandoned if not _delete(self.store, k)][-1024:]
 
-    def serve(self, stop: threading.Event, poll_s: float = 0.5, lane: str = "ctl") -> int:
+    def wake(self, lane: str) -> None:
+        """Unblock this rank's ``lane`` server (after its stop flag was set): a no-op request through
+        the normal numbering, so no sequence number is left unwritten."""
+        base = self._base(self.rank, lane)
+        seq = int(self.store.add(base + "seq", 1))
+        self.store.set(f"{base}req/{seq}", json.dumps([WAKE_OP, None]))
+
+    def serve(self, stop: threading.Event, poll_s: float = WAIT_SLICE_S, lane: str = "ctl") -> int:
         """Run this rank's ``lane`` inbox until ``stop`` is set; returns how many were served.  A
         sequence number whose request never appears (its caller died between reserving it and
-        writing it) is skipped once a later request exists and ``skip_grace_s`` has passed."""
+        writing it) is skipped once a later request exists and ``skip_grace_s`` has passed.  The
+        cursor lives in the store (``<lane>/served``, advanced once per consumed or skipped number),
+        so a rank process restarted against the same store resumes where its predecessor stopped
+        instead of waiting for request numbers that were consumed long ago."""
         base = self._base(self.rank, lane)
-        seq, n, missing_since = 0, 0, None
+        n, missing_since = 0, None
+        try:
+            seq = int(self.store.add(base + "served", 0))
+        except Exception:  # noqa: BLE001 -- the store is gone
+            return 0
         while not stop.is_set():
             key = f"{base}req/{seq + 1}"
             try:
-                if not _wait_key(self.store, key, poll_s):
-                    if int(self.store.add(base + "seq", 0)) > seq + 1:
+                # a later request already exists while this one is missing: its caller may have
+                # died after reserving the number -- wait briefly and skip it after the grace
+                hole = int(self.store.add(base + "seq", 0)) > seq + 1
+                if not _wait_key(self.store, key, min(poll_s, HOLE_POLL_S) if hole else poll_s, stop):
+                    if hole:
                         now = time.monotonic()
                         missing_since = missing_since or now
                         if now - missing_since >= self.skip_grace_s:
                             seq, missing_since = seq + 1, None
+                            self.store.add(base + "served", 1)
                             self.skipped += 1
                     continue
                 raw = self.store.get(key)
@@ -149,7 +228,13 @@ class StoreRPC:
                 return n
             seq, missing_since = seq + 1, None
             _delete(self.store, key)
+            try:
+                self.store.add(base + "served", 1)
+            except Exception:  # noqa: BLE001
+                return n
             op, args = json.loads(raw)
+            if op == WAKE_OP:
+                continue                      # stop(): the loop re-checks its flag
             try:
                 res = {"ok": True, "v": self.handlers[op](args)}
             except Exception as e:  # noqa: BLE001 -- reported to the caller
@@ -201,12 +286,23 @@ class DPNodeWorker:
         self.continuous = dict(continuous or {})
         self.embedder, self.index, self.summarizer = embedder, index, summarizer
         self.rpc = StoreRPC(store, self.rank)
-        self.rpc.handlers.update({
+        handlers = {
             "embed_index": self._embed_index, "add": self._add, "centroid": self._centroid, "query": self._query,
             "delete": self._delete, "clear": self._clear, "count": self._count, "get": self._get,
-            "info": self._info, "sum_submit": self._sum_submit})
-        self.hb = Heartbeat(_PrefixedStore(store, SUM_PREFIX), self.rank, interval=heartbeat_interval)
-        self._out_seq = 0
+            "info": self._info}
+        self.rpc.handlers.update({op: self._counted(fn) for op, fn in handlers.items()})
+        self.rpc.handlers["sum_submit"] = self._sum_submit
+        # liveness beyond "the process is up": the heartbeat carries how much work this rank holds
+        # (busy: accepted summaries not yet published + handlers running) and a progress counter
+        # that moves with the engine's decode bursts, finished summaries and finished handlers.
+        # The heartbeat thread keeps beating while a GPU call hangs, so rank 0's router declares a
+        # rank dead when it is busy and its progress has not moved for the stall timeout
+        # (_Router.alive), and the summarizer's watchdog resubmits its threads elsewhere.
+        self._busy = 0
+        self._done_ops = 0
+        self._busy_lock = threading.Lock()
+        self.hb = Heartbeat(_PrefixedStore(store, SUM_PREFIX), self.rank, interval=heartbeat_interval,
+                            progress_fn=self.progress, busy_fn=lambda: self._busy)
         self._out_lock = threading.Lock()
         # index reads (ctl inbox) and writes (bulk inbox) run on different threads
         self._index_lock = threading.RLock()
@@ -217,6 +313,31 @@ class DPNodeWorker:
         self.stats = {"embedded": 0, "summaries": 0, "queries": 0}
         self._stop = threading.Event()
         self._servers: list[threading.Thread] = []
+
+    # ---------------------------------------------------------------- liveness
+    def progress(self) -> int:
+        """Forward progress of this rank: finished handlers + published summaries + the local
+        summarizer's own counter (decode bursts of its engine), never blocking on the GPU."""
+        fn = getattr(self.summarizer, "progress", None)
+        try:
+            eng = int(fn()) if callable(fn) else 0
+        except Exception:  # noqa: BLE001 -- a counter read must never stop the heartbeat
+            eng = 0
+        return self._done_ops + self.stats["summaries"] + eng
+
+    def _busy_add(self, n: int) -> None:
+        with self._busy_lock:
+            self._busy += n
+
+    def _counted(self, fn):
+        def run(args):
+            self._busy_add(1)
+            try:
+                return fn(args)
+            finally:
+                self._done_ops += 1
+                self._busy_add(-1)
+        return run
 
     # ---------------------------------------------------------------- lifecycle
     def start(self, serve: bool = True) -> "DPNodeWorker":
@@ -236,6 +357,12 @@ class DPNodeWorker:
 
     def stop(self) -> None:
         self._stop.set()
+        if self._servers:
+            for lane in StoreRPC.LANES:       # unblock the lanes' waits
+                try:
+                    self.rpc.wake(lane)
+                except Exception:  # noqa: BLE001 -- the store is gone: the waits end on their own
+                    pass
         for t in self._servers:
             t.join(timeout=5)
         stop = getattr(self.summarizer, "stop_continuous", None)
@@ -339,24 +466,32 @@ class DPNodeWorker:
                "summary": _summary_to_json(summary) if summary is not None else None,
                "err": None if err is None else f"{type(err).__name__}: {err}"}
         with self._out_lock:
-            self._out_seq += 1
-            seq = self._out_seq
+            # result numbers come from a counter in the store, not from this process: a rank
+            # restarted against the same store continues the numbering rank 0's collector follows
+            seq = int(self.store.add(f"{SUM_PREFIX}outseq/{self.rank}", 1))
             self.store.set(f"{SUM_PREFIX}out/{self.rank}/{seq}", json.dumps(rec))
         self.stats["summaries"] += 1
-        self.hb.tick()
+        self._busy_add(-1)
 
     def _sum_submit(self, args):
         t = Thread(**args["thread"])
         key = args["key"]
-        if self._pool is None:                   # streaming summarizer: the continuous engine
-            self.summarizer.submit(t, lambda s, e, key=key: self._publish(key, s, e))
-        else:
-            def run(t=t, key=key):
-                try:
-                    self._publish(key, self.summarizer.summarize_batch([t])[0], None)
-                except Exception as e:  # noqa: BLE001 -- reported to rank 0 as a failure
-                    self._publish(key, None, e)
-            self._pool.submit(run)
+        self._busy_add(1)
+        try:
+            if self._pool is None:                   # streaming summarizer: the continuous engine
+                self.summarizer.submit(t, lambda s, e, key=key: self._publish(key, s, e))
+            else:
+                def run(t=t, key=key):
+                    try:
+                        s = self.summarizer.summarize_batch([t])[0]
+                    except Exception as e:  # noqa: BLE001 -- reported to rank 0 as a failure
+                        self._publish(key, None, e)
+                    else:
+                        self._publish(key, s, None)
+                self._pool.submit(run)
+        except BaseException:
+            self._busy_add(-1)
+            raise
         return True
 
 
@@ -379,19 +514,28 @@ class _PrefixedStore:
 
 class _Router:
     """Rank 0's view of the DP ranks: owner of a thread among the live ones.  A rank is live while
-    its heartbeat is fresh -- re-read on every decision (cached ``cache_s``), never latched, so a
-    rank that only answered slowly, or whose handler failed, keeps its threads and shard."""
+    its heartbeat is fresh AND it is not stalled -- busy (work accepted, not finished) with a
+    progress counter that has not moved for ``stall_timeout`` (a hung GPU: the process and its
+    heartbeat thread are up, nothing finishes; the semantics of resilience.Watchdog's stall check).
+    Re-read on every decision (cached ``cache_s``), never latched, so a rank that only answered
+    slowly, whose handler failed, or whose progress resumes keeps or gets back its threads."""
 
     def __init__(self, store, world: int, timeout: float, cache_s: float = 0.25,
-                 startup_grace_s: float | None = None):
+                 startup_grace_s: float | None = None, stall_timeout: float | None = None):
         self.store, self.world, self.timeout, self.cache_s = store, int(world), float(timeout), float(cache_s)
         # a rank with no heartbeat yet is still loading its models: live for this long after the
         # router starts, dead after it (its threads go to the next live rank instead of waiting on
         # a rank that never came up)
         self.startup_grace_s = float(startup_grace_s if startup_grace_s is not None
                                      else os.environ.get("CFC_DP_STARTUP_GRACE_S", "600"))
+        # longer than any legitimate gap between two progress ticks of a busy rank (one decode
+        # burst is ~0.2 s, a 16k-token prefill chunk ~0.5 s, a first graph capture a few s)
+        st = stall_timeout if stall_timeout is not None else float(os.environ.get("CFC_DP_STALL_TIMEOUT", "120"))
+        self.stall_timeout = float(st) if st and float(st) > 0 else None
         self._t0 = time.monotonic()
         self._seen: dict[int, tuple[float, bool]] = {}
+        self._prog: dict[int, tuple[object, float]] = {}   # rank -> (progress value, first seen at)
+        self.stalls: dict[int, int] = {}                    # rank -> times declared stalled
 
     def alive(self, rank: int) -> bool:
         now = time.monotonic()
@@ -402,7 +546,16 @@ class _Router:
         if v is None:                 # not started yet: live during the start-up grace only
             ok = now - self._t0 <= self.startup_grace_s
         else:
-            ok = time.time() - json.loads(v)["t"] <= self.timeout
+            hb = json.loads(v)
+            ok = time.time() - hb["t"] <= self.timeout
+            if ok and self.stall_timeout is not None:
+                prog, prev = hb.get("progress"), self._prog.get(rank)
+                if not hb.get("busy") or prev is None or prev[0] != prog:
+                    self._prog[rank] = (prog, now)      # idle, or moving: the stall clock restarts
+                elif now - prev[1] > self.stall_timeout:
+                    ok = False
+                    if c is None or c[1]:
+                        self.stalls[rank] = self.stalls.get(rank, 0) + 1
         self._seen[rank] = (now, ok)
         return ok
 
@@ -559,6 +712,11 @@ class DPNodeSummarizer(Summarizer):
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
         self._sender = ThreadPoolExecutor(max_workers=2, thread_name_prefix="dpsum-send")
+        # each rank's result cursor lives on the instance, not in the collector thread: results are
+        # deleted once read, so a collector restarted by stop_continuous / start_continuous (the
+        # batch API does both per call) must continue where the previous one stopped
+        self._col_seq = [0] * router.world
+        self.skip_grace_s = 10.0
         self.stats = {"submitted": 0, "completed": 0, "resubmitted": 0, "duplicates": 0, "send_failures": 0,
                       "per_rank": [0] * router.world}
 
@@ -566,7 +724,7 @@ class DPNodeSummarizer(Summarizer):
     def start_continuous(self, **_) -> None:
         if self._threads:
             return
-        self._stop.clear()
+        self._stop = threading.Event()        # a fresh flag: a collector that outlived its stop stays stopped
         for r in range(self.router.world):
             t = threading.Thread(target=self._collect, args=(r,), name=f"dpsum-collect-{r}", daemon=True)
             t.start()
@@ -577,6 +735,14 @@ class DPNodeSummarizer(Summarizer):
 
     def stop_continuous(self) -> None:
         self._stop.set()
+        if self._threads:
+            # unblock each collector's wait with a no-op result through the rank's own numbering
+            for r in range(self.router.world):
+                try:
+                    seq = int(self.w.store.add(f"{SUM_PREFIX}outseq/{r}", 1))
+                    self.w.store.set(f"{SUM_PREFIX}out/{r}/{seq}", json.dumps({"key": None, "rank": r}))
+                except Exception:  # noqa: BLE001 -- the store is gone
+                    break
         for t in self._threads:
             t.join(timeout=5)
         self._threads = []
@@ -612,18 +778,32 @@ class DPNodeSummarizer(Summarizer):
                     self._inflight[key] = (thread, done, -2, time.monotonic() + self.SEND_RETRY_S)
 
     def _collect(self, rank: int) -> None:
-        seq = 0
         store = self.w.store
-        while not self._stop.is_set():
+        stop = self._stop
+        missing_since = None
+        while not stop.is_set():
+            seq = self._col_seq[rank]
             key = f"{SUM_PREFIX}out/{rank}/{seq + 1}"
             try:
-                if not _wait_key(store, key, self.poll_s):
+                # a later result already exists while this one is missing: the rank may have died
+                # between reserving the number and writing it -- skip it once the grace has passed
+                hole = int(store.add(f"{SUM_PREFIX}outseq/{rank}", 0)) > seq + 1
+                if not _wait_key(store, key, HOLE_POLL_S if hole else WAIT_SLICE_S, stop):
+                    if hole and not stop.is_set():
+                        now = time.monotonic()
+                        missing_since = missing_since or now
+                        if now - missing_since >= self.skip_grace_s:
+                            self._col_seq[rank], missing_since = seq + 1, None
                     continue
                 rec = json.loads(store.get(key))
             except Exception:  # noqa: BLE001 -- the store is gone: the node is shutting down
                 return
-            seq += 1
+            if stop.is_set():
+                return                        # leave the result to the next collector of this rank
+            self._col_seq[rank], missing_since = seq + 1, None
             _delete(store, key)
+            if rec.get("key") is None:           # a stop_continuous wake-up
+                continue
             with self._lock:
                 item = self._inflight.pop(rec["key"], None)
             if item is None:                  # the other copy of a resent request finished first
@@ -635,7 +815,8 @@ class DPNodeSummarizer(Summarizer):
             _deliver(item[1], s, None if s is not None else RuntimeError(rec["err"] or "summarization failed"))
 
     def _watch(self) -> None:
-        while not self._stop.wait(self.poll_s):
+        stop = self._stop
+        while not stop.wait(self.poll_s):
             now = time.monotonic()
             with self._lock:
                 lost = [k for k, (_, _, r, at) in self._inflight.items()
@@ -700,7 +881,9 @@ def shutdown_workers(store) -> None:
     store.set(f"{SUM_PREFIX}shutdown", "1")
 
 
-def build_rank0(store, dp_size: int, worker: DPNodeWorker, heartbeat_timeout: float = 10.0):
-    """Rank 0's facades over the DP ranks: (vector store, summarizer)."""
-    router = _Router(store, dp_size, heartbeat_timeout)
+def build_rank0(store, dp_size: int, worker: DPNodeWorker, heartbeat_timeout: float = 10.0,
+                stall_timeout: float | None = None):
+    """Rank 0's facades over the DP ranks: (vector store, summarizer).  ``stall_timeout``: a busy
+    rank whose progress froze this long is treated as dead ($CFC_DP_STALL_TIMEOUT, 120 s)."""
+    router = _Router(store, dp_size, heartbeat_timeout, stall_timeout=stall_timeout)
     return DPNodeVectorStore(worker, router), DPNodeSummarizer(worker, router)

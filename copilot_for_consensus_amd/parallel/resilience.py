@@ -40,15 +40,23 @@ def _get(store, key: str, default=None):
 
 
 class Heartbeat:
-    def __init__(self, store, rank: int, interval: float = 2.0, clock=time.time):
+    """``progress_fn`` / ``busy_fn`` (optional, non-blocking): extra forward progress added to the
+    ticked counter (e.g. the engine's decode bursts), and how much work the rank holds -- a watcher
+    treats "busy and no progress for the stall timeout" as a hung rank whose beat is still alive."""
+
+    def __init__(self, store, rank: int, interval: float = 2.0, clock=time.time, progress_fn=None, busy_fn=None):
         self.store, self.rank, self.interval, self.clock = store, rank, interval, clock
         self.progress = 0
+        self.progress_fn, self.busy_fn = progress_fn, busy_fn
         self._stop = threading.Event()
         self._t: threading.Thread | None = None
 
     def beat(self) -> None:
-        self.store.set(f"hb/{self.rank}", json.dumps({"t": self.clock(), "progress": self.progress,
-                                                       "pid": os.getpid()}))
+        prog = self.progress + (int(self.progress_fn()) if self.progress_fn is not None else 0)
+        rec = {"t": self.clock(), "progress": prog, "pid": os.getpid()}
+        if self.busy_fn is not None:
+            rec["busy"] = int(self.busy_fn())
+        self.store.set(f"hb/{self.rank}", json.dumps(rec))
 
     def tick(self, n: int = 1) -> None:
         """Record forward progress (e.g. one decode step / one finished batch)."""
@@ -122,7 +130,7 @@ class Watchdog:
             return {"alive": False, "reason": f"heartbeat {now - hb['t']:.1f}s old", **hb}
         if self.stall_timeout is not None:
             prev = self._last_progress.get(rank)
-            if prev is None or hb["progress"] != prev[0]:
+            if prev is None or hb["progress"] != prev[0] or hb.get("busy", 1) == 0:
                 self._last_progress[rank] = (hb["progress"], now)
             elif now - prev[1] > self.stall_timeout:
                 return {"alive": False, "reason": f"no progress for {now - prev[1]:.1f}s", **hb}

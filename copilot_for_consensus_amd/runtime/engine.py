@@ -113,6 +113,9 @@ class LLMEngine:
         self._prefill_rows = (K.prefill_rows(model.w.heads, model.w.kv_heads) if kv.device.type == "cuda"
                               else K.PREFILL_TILE_ROWS)
         self.stop_check_interval = stop_check_interval
+        # host-side forward-progress counter (prefill chunks + decode steps issued): read by the DP
+        # heartbeat (parallel/dp_node.py), it freezes when a GPU call hangs and the host blocks
+        self.progress = 0
         self._states: dict[tuple, _DecodeState] = {}
         self._alloc_lock = threading.RLock()     # KV / prefix-cache bookkeeping of start / finish
         # shared-prefix reuse of whole KV blocks (system prompt + template head of every thread)
@@ -128,13 +131,17 @@ class LLMEngine:
         # 5.88 s per 128-thread batch (profiles/r05_ab_decode_lpt.log)
         self.lpt = os.environ.get("CFC_DECODE_LPT", "1") != "0"
         # TP > 1, opt-in (CFC_TP_PREFILL_OVERLAP=1): prefill chunks as two interleaved halves, each
-        # half's all-reduces (async RCCL, their own stream) under the other half's GEMMs.  Numerics
-        # checked against the one-pass prefill on the CPU (tests/test_parallel_cpu.py); not measured
-        # on a multi-GPU node, and never with a gloo TP group on GPU tensors (the one-GPU rehearsal
-        # mode): there a TP=2 run stalled in the decode graph after an overlapped prefill
-        # (scripts/dbg_tp_overlap.sh), so that combination keeps the one-pass prefill
-        self.tp_overlap = (os.environ.get("CFC_TP_PREFILL_OVERLAP", "0") == "1"
-                           and not (self._gloo_tp and self.device.type == "cuda"))
+        # half's all-reduces (async, on the process group) under the other half's GEMMs.  Numerics
+        # and the one-shot all-reduce's epoch bookkeeping checked on the CPU
+        # (tests/test_parallel_cpu.py); the TP=2 rehearsal on one GPU (gloo) runs it to completion
+        # with the one-shot all-reduce's error counter at 0 and identical per-block epochs on both
+        # ranks after every batch (profiles/r06_tp2_overlap_gloo_1gpu.log).  The round-5 rehearsal
+        # that stopped at its 150 s limit inside the second batch's decode graph was rerun this way
+        # and completed: no all-reduce timed out and no epoch desync -- not reproduced.
+        # Not measured on a multi-GPU node (RCCL), so it stays opt-in.
+        self.tp_overlap = os.environ.get("CFC_TP_PREFILL_OVERLAP", "0") in ("1", "force")
+        # CFC_AR_DEBUG=1: print the one-shot all-reduce's error counter and epochs per batch
+        self._ar_debug = os.environ.get("CFC_AR_DEBUG", "0") == "1"
         if self.device.type == "cuda":
             from .gemm_tuning import enable_tuned_gemms
             self.tuned_gemms = enable_tuned_gemms()
@@ -151,6 +158,15 @@ class LLMEngine:
 
     def _i32(self, x):
         return torch.tensor(x, dtype=torch.int32, device=self.device)
+
+    def _ar_trace(self, tag):
+        """CFC_AR_DEBUG=1: this rank's one-shot all-reduce error count and per-block epochs."""
+        ar = getattr(self.model, "custom_ar", None)
+        if self._ar_debug and ar is not None:
+            torch.cuda.synchronize(self.device)
+            ep = ar.epochs.tolist()
+            print(f"[ar-debug] rank {ar.rank} {tag}: errors={ar.errors()} epochs[0:4]={ep[:4]} "
+                  f"epochs[32]={ep[32]} key={ep[-1]} distinct={sorted(set(ep))[:6]}", flush=True)
 
     def _prefill(self, prompts, tables, temperature, seed, start=None):
         """Chunked packed prefill; returns first sampled token per prompt.  ``start[s]`` tokens of
@@ -185,6 +201,7 @@ class LLMEngine:
                     first_dev.index_copy_(0, d_fin.long(), out)
             for (s, _, b) in chunk:
                 pos[s] = b
+            self.progress += 1
         return first_dev.tolist()      # the one host sync of the prefill
 
     def _overlap_split(self, chunk):
@@ -399,6 +416,7 @@ class LLMEngine:
                 first = self._prefill(prompts, tables, temperature, seed, start)
             barrier()
             t1 = time.perf_counter()
+            self._ar_trace(f"after prefill of {B} x {sum(lens)} tokens")
 
             part_blocks = self._part_blocks(B, max_blocks)
             st = self._state(B, max_blocks, max_new_tokens, part_blocks, stop_ids, stop_strings, slot)
@@ -465,6 +483,7 @@ class LLMEngine:
             self.last_used_graph = use_graph
             if use_graph and (st.graph is None or st.graph[1:] != (part_blocks, temperature, seed)):
                 self._capture(st, part_blocks, temperature, seed)
+                self._ar_trace("after capture")
             cur = torch.cuda.current_stream(self.device) if sync else None
             for i in range(1, max_new_tokens):
                 if switch is not None and cur is not None:
@@ -483,6 +502,7 @@ class LLMEngine:
                 else:
                     self._decode_step(st, part_blocks, temperature, seed)
                 steps += 1
+                self.progress += 1
                 if (stop_ids or stop_strings is not None) and (i % self.stop_check_interval == 0) \
                         and bool(st.done.all()):
                     break
@@ -492,6 +512,7 @@ class LLMEngine:
             keep = st.stop_state.keep.cpu().tolist() if stop_strings is not None else [steps + 1] * B
             if sync:
                 torch.cuda.current_stream(self.device).synchronize()
+            self._ar_trace(f"after {steps} decode steps")
             rng.__exit__(None, None, None)
             t2 = time.perf_counter()
             ok = True

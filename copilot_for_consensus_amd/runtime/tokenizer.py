@@ -40,7 +40,9 @@ ENCODE_THREADS = max(1, min(16, int(os.environ.get("CFC_TOKENIZER_THREADS", "0")
 
 
 def _batch_raw(fn, handle, texts: list[str], cap: int) -> tuple[np.ndarray, np.ndarray]:
-    """Thread-parallel C++ encode of many texts: (ids [n, cap] int32, full lengths [n] int32)."""
+    """Thread-parallel C++ encode of many texts: (ids [n, cap] int32, lengths [n] int32).  The BPE
+    encoders report each text's full length (> cap = overflow); the WordPiece encoder stops at cap,
+    so its lengths are capped (== cap may mean longer) -- it can only be used truncating."""
     bs = [t.encode("utf-8") for t in texts]
     offs = np.zeros(len(bs) + 1, dtype=np.int64)
     np.cumsum([len(b) for b in bs], out=offs[1:])
@@ -52,9 +54,13 @@ def _batch_raw(fn, handle, texts: list[str], cap: int) -> tuple[np.ndarray, np.n
     return out, lens
 
 
-def _batch(fn, handle, texts: list[str], cap: int, truncate: bool = False) -> list[list[int] | None]:
+def _batch(fn, handle, texts: list[str], cap: int, truncate: bool = False,
+           capped_lengths: bool = False) -> list[list[int] | None]:
     """As _batch_raw, as lists.  Results longer than ``cap`` come back as None (caller re-encodes
-    them singly) unless ``truncate``, which keeps their first ``cap`` ids."""
+    them singly) unless ``truncate``, which keeps their first ``cap`` ids.  ``capped_lengths``: the
+    encoder stops at cap (WordPiece), so overflow is undetectable and only ``truncate`` is valid."""
+    if capped_lengths and not truncate:
+        raise ValueError("an encoder that stops at cap reports capped lengths: truncate=True required")
     out, lens = _batch_raw(fn, handle, texts, cap)
     return [out[i, :min(lens[i], cap)].tolist() if (truncate or lens[i] <= cap) else None for i in range(len(texts))]
 
@@ -475,7 +481,8 @@ class WordPieceTokenizer:
         L = max_length or self.max_length
         # truncation makes every result fit: ask for L-2 pieces, longer texts are simply cut
         texts = [bert_normalize(t, self.lowercase) for t in texts]
-        res = _batch(self._lib.cfc_wp_encode_batch, self._h, texts, max(1, L - 2), truncate=True)
+        res = _batch(self._lib.cfc_wp_encode_batch, self._h, texts, max(1, L - 2), truncate=True,
+                     capped_lengths=True)
         return [[self.cls_id] + ids + [self.sep_id] for ids in res]
 
     def encode_packed(self, texts: list[str], max_length: int | None = None) -> tuple[np.ndarray, np.ndarray]:

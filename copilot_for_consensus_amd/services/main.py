@@ -24,7 +24,12 @@ replay their leader's engine steps:
 from __future__ import annotations
 
 import argparse
+import os
 import sys
+
+# before torch loads (c10 reads it once): the DP control plane parks idle threads in blocking
+# TCPStore waits that time out every WAIT_SLICE_S; c10d logs each timeout as a warning
+os.environ.setdefault("TORCH_CPP_LOG_LEVEL", "ERROR")
 
 from ..config.loader import get_config
 

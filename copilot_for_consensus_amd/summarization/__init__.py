@@ -201,6 +201,13 @@ class HipLLMSummarizer(Summarizer):
         else:
             raise ValueError(f"unknown TP control message {kind!r}")
 
+    def progress(self) -> int:
+        """Forward-progress counter for liveness checks (parallel/dp_node.py heartbeat): prefill
+        chunks and decode steps of the engine, plus the continuous engine's decode steps.  A host
+        counter -- it stops moving when a GPU call hangs."""
+        ce = getattr(self, "_ce", None)
+        return int(self.engine.progress) + (int(ce.stats.get("steps", 0)) if ce is not None else 0)
+
     def apply_stops(self, text: str) -> str:
         """Cut at the first stop sequence (string-level stops, as the llama.cpp server applies them)."""
         cut = min((i for i in (text.find(s) for s in self.stop_sequences) if i >= 0), default=-1)

@@ -242,3 +242,145 @@ def test_chunk_text_server_is_read_only():
     finally:
         srv.server.shutdown()
         srv.server.server_close()
+
+
+# ------------------------------------------------------------------ round 6: hung ranks, restarts
+class _HangSum(_Sum):
+    """Rank 2's engine blocks (a GPU hung in a kernel) on every thread whose prompt says HANG; its
+    process and heartbeat thread stay up."""
+
+    def summarize_batch(self, threads):
+        if self.rank == 2 and any("HANG" in t.prompt for t in threads):
+            time.sleep(40.0)
+        return super().summarize_batch(threads)
+
+
+def _hang_rank_main(port, rank, world, q):
+    from copilot_for_consensus_amd.parallel.dp_node import DPNodeWorker
+    from copilot_for_consensus_amd.vectorstore import InMemoryVectorStore
+    store = TCPStore("127.0.0.1", port, is_master=False, timeout=datetime.timedelta(seconds=60))
+    w = DPNodeWorker(store, rank, world, _SlowEmbedder(), InMemoryVectorStore(16), _HangSum(rank),
+                     heartbeat_interval=0.2)
+    q.put((rank, w.run_until_shutdown(poll_s=0.05)))
+
+
+def test_dp_node_hung_rank_threads_are_resubmitted_within_the_stall_timeout():
+    """3 ranks; rank 2's summarizer blocks forever while its heartbeat keeps beating.  Its threads
+    are declared stalled (busy, progress frozen) and summarized by a live rank within stall_timeout
+    + 2 s; threads of the other ranks are unaffected and nothing is delivered twice."""
+    from copilot_for_consensus_amd.parallel.dp import owner_of
+    from copilot_for_consensus_amd.parallel.dp_node import build_rank0, shutdown_workers
+    world, stall = 3, 2.0
+    port = _free_port()
+    store = TCPStore("127.0.0.1", port, is_master=True, wait_for_workers=False, timeout=datetime.timedelta(seconds=60))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_hang_rank_main, args=(port, r, world, q), daemon=True) for r in range(1, world)]
+    for p in procs:
+        p.start()
+    w0 = _make_worker(store, 0, world)
+    vs, summ = build_rank0(store, world, w0, heartbeat_timeout=30.0, stall_timeout=stall)
+    w0.start(serve=False)
+    try:
+        deadline = time.time() + 120
+        while not all(store.check([f"dpsum/hb/{r}"]) for r in range(world)):
+            assert time.time() < deadline, "DP ranks never started"
+            time.sleep(0.05)
+        tids = [f"{i:016x}" for i in range(400)]
+        on2 = [t for t in tids if owner_of(t, world) == 2][:3]
+        on1 = [t for t in tids if owner_of(t, world) == 1][:2]
+        threads = [Thread(t, ["m"], prompt=f"HANG {t}") for t in on2] + [Thread(t, ["m"], prompt="p") for t in on1]
+        t0 = time.perf_counter()
+        out = summ.summarize_batch(threads)
+        dt = time.perf_counter() - t0
+        assert [s.thread_id for s in out] == [t.thread_id for t in threads]
+        # rank 2's threads were finished elsewhere (rank 0 or 1), rank 1's by rank 1
+        assert all(not s.summary_markdown.startswith("rank2:") for s in out), [s.summary_markdown for s in out]
+        assert all(s.summary_markdown.startswith("rank1:") for s in out[3:])
+        assert dt < stall + 2.0 + 1.0, dt          # + one heartbeat / watchdog period of slack
+        assert summ.stats["resubmitted"] >= 3 and vs.router.stalls.get(2, 0) >= 1, (summ.stats, vs.router.stalls)
+        assert not vs.router.alive(2) and vs.router.alive(1)
+        # an idle rank is never "stalled": rank 1 did nothing since, and stays routable
+        time.sleep(stall + 0.5)
+        assert vs.router.alive(1)
+    finally:
+        summ.stop_continuous()
+        shutdown_workers(store)
+        w0.stop()
+        vs.close()
+        for p in procs:
+            p.join(timeout=3)
+            if p.is_alive():
+                p.kill()
+
+
+def test_dp_summarizer_batch_api_twice_without_a_started_stream(node3):
+    """The batch API starts and stops the collectors per call (micro-batcher / synchronous callers):
+    the second call must continue from the first call's result cursor (results are deleted once
+    read, so a collector restarting at 1 would wait forever)."""
+    store, vs, summ, docs, w0, q, procs = node3
+    summ.stop_continuous()                        # the fixture streamed; this caller never starts one
+    tids = [f"{i:016x}" for i in range(12)]
+    for rnd in range(3):
+        t0 = time.perf_counter()
+        out = summ.summarize_batch([Thread(t, ["m"], prompt=f"r{rnd}") for t in tids])
+        assert [s.summary_markdown.rsplit(":", 1)[1] for s in out] == [f"r{rnd}"] * len(tids)
+        assert time.perf_counter() - t0 < 10.0
+    assert summ.stats["duplicates"] == 0
+
+
+def test_store_rpc_restarted_server_resumes_at_the_store_cursor():
+    """A rank process restarted against the same store serves the next request at once: its cursor
+    comes from the store's served counter, not from 0 (which would skip each consumed number after
+    a 10 s grace)."""
+    from copilot_for_consensus_amd.parallel.dp_node import StoreRPC
+    store = TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False, timeout=datetime.timedelta(seconds=10))
+    cli = StoreRPC(store, 0)
+    for life in range(2):
+        srv = StoreRPC(store, 1, skip_grace_s=30.0)
+        srv.handlers["echo"] = lambda a, life=life: [life, a]
+        stop = threading.Event()
+        t = threading.Thread(target=srv.serve, args=(stop,), kwargs={"poll_s": 0.05})
+        t.start()
+        try:
+            for i in range(5):
+                t0 = time.perf_counter()
+                assert cli.call(1, "echo", i, timeout=5) == [life, i]
+                assert time.perf_counter() - t0 < 2.0
+            assert srv.skipped == 0
+        finally:
+            stop.set()
+            t.join()
+
+
+def test_worker_result_numbers_continue_across_a_restart():
+    """Result keys are numbered from a store counter: a restarted worker publishes at N+1, where
+    rank 0's collector is waiting."""
+    from copilot_for_consensus_amd.parallel.dp_node import SUM_PREFIX, DPNodeWorker
+    from copilot_for_consensus_amd.vectorstore import InMemoryVectorStore
+    store = TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False, timeout=datetime.timedelta(seconds=10))
+    for life in range(2):
+        w = DPNodeWorker(store, 1, 2, _SlowEmbedder(), InMemoryVectorStore(16), _Sum(1))
+        for i in range(3):
+            w._publish(f"k{life}{i}", None, RuntimeError("x"))
+    assert [store.check([f"{SUM_PREFIX}out/1/{n}"]) for n in range(1, 8)] == [True] * 6 + [False]
+
+
+def test_router_declares_a_busy_rank_with_frozen_progress_stalled_and_forgives_it():
+    import json as _json
+
+    from copilot_for_consensus_amd.parallel.dp_node import SUM_PREFIX, _Router
+    store = TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False, timeout=datetime.timedelta(seconds=10))
+    r = _Router(store, 2, timeout=30.0, cache_s=0.0, stall_timeout=0.3)
+
+    def beat(rank, progress, busy):
+        store.set(f"{SUM_PREFIX}hb/{rank}", _json.dumps({"t": time.time(), "progress": progress, "busy": busy}))
+    beat(0, 5, 0)
+    beat(1, 7, 2)
+    assert r.live() == [0, 1]
+    time.sleep(0.4)
+    beat(0, 5, 0)                 # idle, no progress: fine
+    beat(1, 7, 2)                 # busy, no progress for > 0.3 s: stalled
+    assert r.live() == [0] and r.stalls == {1: 1}
+    beat(1, 8, 2)                 # progress again: routable again
+    assert r.live() == [0, 1]

@@ -126,6 +126,93 @@ def _tp_prefill_overlap(env, prompts):
     return out
 
 
+
+class _EpochAR:
+    """CPU stand-in of parallel.custom_ar.OneShotAllReduce with comm.hip's epoch bookkeeping: a sum
+    call advances epochs[0:nb] (nb = min(ceil(n / 8 / 256), blocks)), a key-max call the last
+    block; the reduction itself goes through gloo.  Two ranks whose call sequences differ end with
+    different epoch arrays -- the desync that would make every later call of the lagging rank spin
+    to its timeout."""
+
+    def __init__(self, group, blocks: int = 32):
+        self.group, self.blocks, self.enabled = group, blocks, True
+        self.staging_bytes, self.key_rows = 8 << 20, 1024
+        self.epochs = [0] * 64
+        self.log = []
+        self.busy = False
+
+    def supports(self, x):
+        return x.numel() % 8 == 0 and x.numel() * 2 <= self.staging_bytes
+
+    def supports_keys(self, n):
+        return 0 < n <= self.key_rows
+
+    def _enter(self, tag, nb):
+        assert not self.busy, "two one-shot all-reduces in flight at once on one rank"
+        self.log.append((tag, nb))
+
+    def __call__(self, x, out=None):
+        nb = min(-(-(x.numel() // 8) // 256), self.blocks)
+        self._enter("sum", nb)
+        for b in range(nb):
+            self.epochs[b] += 1
+        dist.all_reduce(x, group=self.group)
+        return x if out is None else out.copy_(x)
+
+    def keymax(self, keys, out_ids):
+        self._enter("keymax", 1)
+        self.epochs[63] += 1
+        dist.all_reduce(keys, op=dist.ReduceOp.MAX, group=self.group)
+        return out_ids.copy_((0xFFFFFFFF - (keys & 0xFFFFFFFF)).to(torch.int32))
+
+
+def _tp_overlap_epochs(env, batches):
+    """Two batches through the engine with the overlapped TP prefill ON and greedy decode, the
+    one-shot all-reduce replaced by _EpochAR: returns (log, epochs, calls inside the overlapped
+    prefill, tokens) per rank."""
+    from copilot_for_consensus_amd.models.decoder import DecoderModel, DecoderWeights, get_config
+    from copilot_for_consensus_amd.parallel import make_groups
+    from copilot_for_consensus_amd.parallel.tp import shard_weights
+    from copilot_for_consensus_amd.runtime.engine import LLMEngine
+    from copilot_for_consensus_amd.runtime.kv_cache import PagedKVCache
+
+    cfg = get_config("tiny")
+    g = make_groups(env, tp=env.world)
+    ar = _EpochAR(g.tp_group)
+    m = DecoderModel(shard_weights(DecoderWeights.random(cfg, "cpu", seed=5), g.tp_rank, g.tp_size),
+                     tp_group=g.tp_group, custom_ar=ar)
+    eng = LLMEngine(m, PagedKVCache(cfg.layers, 64, m.w.kv_heads, cfg.head_dim, "cpu"))
+    eng.tp_overlap = True
+    inside = []
+    orig = m.forward_prefill_overlap
+
+    def ov(*a, **k):
+        n0 = len(ar.log)
+        try:
+            return orig(*a, **k)
+        finally:
+            inside.append(len(ar.log) - n0)
+    m.forward_prefill_overlap = ov
+    toks = [eng.generate(p, 6, ignore_eos=True).tokens for p in batches]
+    return ar.log, ar.epochs, inside, toks
+
+
+def test_tp2_overlapped_prefill_keeps_one_shot_allreduce_epochs_in_step():
+    """The overlapped TP prefill runs its all-reduces on the process group, never on the one-shot
+    kernel, and every rank makes the same one-shot calls (same order, same block counts) over two
+    batches of prefill + greedy decode -- so the per-block epochs of comm.hip stay equal on all
+    ranks (round-5 stall investigation: scripts/gpu_r06_first.sh read the real counters on the GPU,
+    errors 0 and identical epochs on both ranks after each batch, profiles/r06_tp2_overlap_gloo_1gpu.log)."""
+    batches = [[[1, 5, 9, 200, 17, 33], [1] + list(range(40, 110)), [1, 2], [1] + [7] * 40],
+               [[1, 3] * 20, [1, 9, 9], [1] + list(range(300, 340))]]
+    outs = _run(_tp_overlap_epochs, 2, batches)
+    (log0, ep0, in0, t0), (log1, ep1, in1, t1) = outs
+    assert in0 == in1 and len(in0) == 2 and all(n == 0 for n in in0), (in0, in1)
+    assert log0 == log1 and ep0 == ep1
+    assert any(tag == "sum" for tag, _ in log0) and any(tag == "keymax" for tag, _ in log0)
+    assert t0 == t1
+
+
 def test_tp2_prefill_overlapped_halves_match_one_pass():
     prompts = [[1, 5, 9, 200, 17, 33], [1] + list(range(40, 110)), [1, 2], [1] + [7] * 40]
     outs = _run(_tp_prefill_overlap, 2, prompts)
