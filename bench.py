@@ -76,6 +76,9 @@ def parse_args(argv=None):
                     help="the light-load point through the real services (pipeline/node_bench.py: archive submit "
                          "-> report stored), Poisson arrivals per second per GPU (0 = skip; TP=1 only)")
     ap.add_argument("--service-latency-threads", type=int, default=12)
+    ap.add_argument("--search-queries", type=int, default=64,
+                    help="topic searches timed after the throughput steps (GET /api/reports/search through "
+                         "ReportingService: HIP encoder + HIP kNN top-150 over the resident index; 0 = skip)")
     ap.add_argument("--pipeline", choices=["bench", "node"], default="bench",
                     help="bench: the stage code with a static LLM batch (headline); node: the real services "
                          "(Node, in-proc bus, continuous summarization engine), pipeline/node_bench.py")
@@ -184,6 +187,23 @@ def main(argv=None):
                    p95_s=round(max(p["p95_s"] for p in probe), 3),
                    throughput_threads_per_s=round(sum(p["throughput_threads_per_s"] for p in probe), 3))
         return agg
+    # after the timed window: the reference's one live vector query, the reporting topic search
+    # (embed + kNN top-150 over the resident index + enrichment), on an otherwise idle GPU
+    search = None
+    if args.search_queries > 0 and not args.llm_only:
+        barrier()
+        sp = pipe.search_probe(args.search_queries, limit=50, seed=args.seed + 31 * groups.dp_rank)
+        if world > 1:
+            parts = [None] * world
+            dist.all_gather_object(parts, sp)
+            parts = [p for p in parts if p]
+        else:
+            parts = [sp] if sp else []
+        if parts:
+            search = dict(parts[0])
+            search.update(queries=sum(p["queries"] for p in parts),
+                          p50_ms=round(statistics.median([p["p50_ms"] for p in parts]), 2),
+                          p95_ms=round(max(p["p95_ms"] for p in parts), 2), max_ms=round(max(p["max_ms"] for p in parts), 2))
     # after the timed window: the same GPUs at a load below saturation (Poisson arrivals), then a
     # light load -- a few threads far apart, the regime of the reference's published 3-4 s per thread
     latency = probe_point(probe_steps, args.latency_rate, args.seed + 104729 * groups.dp_rank) if probe_steps else None
@@ -242,7 +262,12 @@ def main(argv=None):
                 "max_new_tokens": args.max_new,
                 "kv_cache": "bf16" if args.kv_dtype == "bf16" else "fp8_e4m3fn (opt-in, reduced-precision KV)",
                 "parallelism": f"dp{groups.dp_size}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
-                "pipeline": "llm-only" if args.llm_only else "parse+chunk+embed+knn+select+prefill+decode",
+                # "index": the chunk vectors go into the HBM kNN index; "centroid-select": the
+                # orchestrator scores each thread's own rows against their centroid (the reference's
+                # ThreadChunksSource reads a thread's chunks, orchestrator/app/context_sources.py:40);
+                # the HIP kNN query path is timed separately in search_latency
+                "pipeline": ("llm-only" if args.llm_only
+                             else "parse+chunk+embed+index+centroid-select+prefill+decode"),
                 "index": (f"sharded over {groups.dp_size} GPUs by thread (RCCL all_to_all insert + relevance)"
                           if groups.dp_size > 1 and not args.llm_only else "one HBM index per GPU"),
                 "schedule": ("prefill of batch i+1 on half the CUs beside batch i's decode" if overlap_prefill
@@ -257,6 +282,8 @@ def main(argv=None):
             "latency_mode_light": latency_low,
             # the same light load through the real services (archive submit -> report stored)
             "latency_service_light": service_light,
+            # GET /api/reports/search (topic search: HIP encoder + HIP kNN + enrichment) vs the P95 0.5 s SLO
+            "search_latency": search,
             "generated_tokens_per_s": round(gen_tokens / elapsed, 1),
             "prompt_tokens_per_s": round(prompt_tokens / elapsed, 1),
             "baseline_threads_per_s": round(BASELINE_THREADS_PER_S, 4),

@@ -268,6 +268,16 @@ class BenchPipeline:
     def run_step(self, step: int) -> StepResult:
         return self.run_steps([step], overlap=False)[0]
 
+    def search_probe(self, n_queries: int = 64, limit: int = 50, seed: int = 0) -> dict | None:
+        """Topic-search latency through the reporting service (RagPipeline.search_probe); None on
+        ranks without the RAG stages (TP followers, --llm-only)."""
+        if self.rag is None:
+            return None
+        if self.device.type == "cuda":
+            with torch.cuda.stream(self.side_stream):
+                return self.rag.search_probe(n_queries, limit, seed)
+        return self.rag.search_probe(n_queries, limit, seed)
+
     def latency_probe(self, steps: list[int], rate_per_s: float, seed: int = 0, steps_per_sync: int = 16,
                       max_threads: int | None = None) -> dict:
         """The latency half of the metric under load below saturation: the threads of ``steps``

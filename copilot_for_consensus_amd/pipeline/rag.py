@@ -24,6 +24,7 @@ summarization request path (summarization/app/service.py:289).
 from __future__ import annotations
 
 import dataclasses
+import random
 import time
 
 import torch
@@ -171,6 +172,39 @@ class RagPipeline:
         prompts = [self._clip(ids) for ids in self.bpe.encode_batch(texts)]
         st["tokenize"] = time.perf_counter() - t
         return PreparedBatch(threads, prompts, texts, requests, ctxs, st, aid)
+
+    def search_probe(self, n_queries: int = 64, limit: int = 50, seed: int = 0) -> dict:
+        """The reference's one live vector-query path, timed: ``GET /api/reports/search`` ->
+        ReportingService.search_reports_by_topic (reporting/app/service.py:797-828): embed the topic
+        on the HIP encoder, HIP kNN top-(limit x 3) over the whole resident index (the prefill rows +
+        every chunk the run embedded), group by thread, enrich from the document store.  Topics
+        are thread subjects of the run; ``min_score`` 0 so every hit thread is enriched (the most
+        work per query).  Against the reporting P95 SLO of 0.5 s
+        (infra/prometheus/alerts/slo_latency.yml:249).  With a DP-sharded index this is the local
+        shard (the cross-rank merge is a collective, parallel/knn.py)."""
+        from ..services.reporting import ReportingService
+        rep = ReportingService(self.pub, None, self.docs, vector_store=self.local_index,
+                               embedding_provider=self.embedder)
+        subjects = sorted({t["subject"] for t in self.docs.query_documents("threads", {}, limit=1 << 30)
+                           if t.get("subject")})
+        if not subjects:
+            return {}
+        rng = random.Random(seed)
+        rep.search_reports_by_topic(subjects[0], limit=limit, min_score=0.0)     # warm-up
+        lat, found = [], 0
+        for _ in range(n_queries):
+            topic = rng.choice(subjects)
+            t = time.perf_counter()
+            res = rep.search_reports_by_topic(topic, limit=limit, min_score=0.0)
+            lat.append(time.perf_counter() - t)
+            found += len(res)
+        lat.sort()
+        return {"queries": n_queries, "limit": limit, "top_k": 3 * limit, "index_rows": int(self.local_index.count()),
+                "p50_ms": round(1e3 * lat[len(lat) // 2], 2), "p95_ms": round(1e3 * lat[int(0.95 * (len(lat) - 1))], 2),
+                "max_ms": round(1e3 * lat[-1], 2), "reports_per_query": round(found / n_queries, 1),
+                "path": "ReportingService.search_reports_by_topic: HIP encoder embed -> HIP kNN (flat cosine, "
+                        "fused top-k) over the HBM index -> group by thread -> document-store enrichment",
+                "slo_p95_ms": 500}
 
     def _clip(self, ids: list[int]) -> list[int]:
         """Keep the instructions (head) and the latest excerpts (tail) if a prompt exceeds the context."""

@@ -129,7 +129,9 @@ __device__ __forceinline__ uint4 dg_ldw(const uint16_t* p) {
 //   waves' W ring fill (one extra barrier), so the first MFMAs do not wait behind ~96 KB of W;
 //   32 = contiguous W pieces: wave w loads fragments 2w, 2w+1 of the stage's 2 NW KB region (one
 //   2-KB run per wave) instead of its own group's two 1-KB fragments NW KB apart (wrong sums);
-//   64 = two X-loader waves + an 8-slot X ring (DgShape MX).
+//   64 = two X-loader waves + an 8-slot X ring (DgShape MX);
+//   128 = no workgroup barrier in the compute waves' stage loop (with 1 only: the loader waves
+//   return at once) -- is the per-stage lockstep of the compute waves what slows the W stream?
 // PACKED: W in the fragment-packed layout of cfc_dgemm_pack for this BN: tile-major, then 32-deep
 // k group, then wave: Wp[N/BN][K/32][BN/16][64][8], so the 16 rows x 32 k of one MFMA B fragment
 // are 1 KB contiguous in lane order and a workgroup's whole W slice (BN rows x its K range) is ONE
@@ -164,7 +166,10 @@ __global__ void __launch_bounds__((64 * DgShape<BM, BN, (ABL & 64) != 0>::WAVES)
   const int rot = (ABL & 4) ? 0 : (int)((unsigned)lid * 37u % (unsigned)nst);
   auto phys = [&](int s) { s += rot; return s >= nst ? s - nst : s; };
 
+  constexpr bool NOBAR = (ABL & 128) != 0;
+  static_assert(!NOBAR || (ABL & 1), "no-barrier probe only without the X stream");
   if (w >= NW) {
+    if constexpr (NOBAR) return;
     // ---------------- X loader wave, LDS-DMA: rows 8 XP l .. 8 XP (l+1) - 1 of the X stage image
     const int l = w - NW;
     const int prow = lane >> 3, pch = (lane & 7) ^ prow;   // row & 7 == prow for every piece
@@ -252,7 +257,7 @@ __global__ void __launch_bounds__((64 * DgShape<BM, BN, (ABL & 64) != 0>::WAVES)
   for (; st + D <= nst; st += D) {
 #pragma unroll
     for (int u = 0; u < D; ++u) {
-      dg_barrier();                 // X stage st+u is in LDS
+      if constexpr (!NOBAR) dg_barrier();   // X stage st+u is in LDS
       compute(ring[u]);
       load_stage(phys(min(st + u + D, nst - 1)), ring[u]);   // unconditional: the tail re-reads the last stage
     }
@@ -260,7 +265,7 @@ __global__ void __launch_bounds__((64 * DgShape<BM, BN, (ABL & 64) != 0>::WAVES)
 #pragma unroll
   for (int u = 0; u < D; ++u) {
     if (st + u < nst) {
-      dg_barrier();
+      if constexpr (!NOBAR) dg_barrier();
       compute(ring[u]);
     }
   }
@@ -408,7 +413,7 @@ CFC_API int cfc_dgemm_pack(const void* w, void* wp, int N, int K, int bn, hipStr
 // (not nontemporal) cache policy on the weight stream.
 CFC_API int cfc_dgemm_ablate(const void* x, const void* w, int M, int N, int K, int split, int bn, int abl,
                              float* part, hipStream_t stream) {
-  if (M > 128 || (abl & ~127)) return -1;
+  if (M > 128 || (abl & ~255)) return -1;
   if (const int e = dgemm_check(M, N, K, split, DG_PART, bn, part, nullptr)) return e;
   int rc;
   switch (abl) {
@@ -426,6 +431,8 @@ CFC_API int cfc_dgemm_ablate(const void* x, const void* w, int M, int N, int K, 
     case 35: DG_ABL(35, true)
     case 64: DG_ABL(64, true)
     case 96: DG_ABL(96, true)
+    case 129: DG_ABL(129, true)
+    case 131: DG_ABL(131, true)
 #undef DG_ABL
     default: return -3;
   }

@@ -56,6 +56,11 @@ def _check(d, n, latency=True):
     sl = d["latency_service_light"]
     assert sl["threads"] == 3 * n and sl["arrival_rate_per_gpu"] == 0.5 and sl["path"].startswith("services")
     assert 0 < sl["p50_s"] <= sl["p95_s"]
+    # the reporting topic search (embed + kNN top-150 + enrichment) against the P95 0.5 s SLO
+    se = d["search_latency"]
+    assert se["queries"] == 64 * n and se["top_k"] == 150 and se["slo_p95_ms"] == 500
+    assert 0 < se["p50_ms"] <= se["p95_ms"] <= se["max_ms"] and se["reports_per_query"] > 0
+    assert "centroid-select" in d["config"]["pipeline"] and "knn" not in d["config"]["pipeline"]
 
 
 def test_bench_single_process_contract():
