@@ -163,13 +163,31 @@ module privateEndpoints 'modules/privateendpoints.bicep' = if (enablePrivateNetw
   }
 }
 
+// private networking: the deployment scripts write Key Vault secrets from inside the vnet (the vault
+// refuses public traffic); their file share lives in a storage account that admits that subnet only
+module scriptStorage 'modules/scriptstorage.bicep' = if (enablePrivateNetworking) {
+  name: 'scriptstorage'
+  params: {
+    name: take('${projectName}ds${suffix}', 24)
+    location: location
+    tags: tags
+    subnetId: network.outputs.scriptsSubnetId
+  }
+}
+
+var scriptsSubnet = enablePrivateNetworking ? network.outputs.scriptsSubnetId : ''
+var scriptsStorage = enablePrivateNetworking ? scriptStorage.outputs.accountName : ''
+
 module jwtKeys 'modules/jwtkeys.bicep' = {
   name: 'jwtkeys'
+  dependsOn: [privateEndpoints]
   params: {
     location: location
     tags: tags
     vaultName: keyVault.outputs.vaultName
     identityId: identities.outputs.deployerIdentityId
+    subnetId: scriptsSubnet
+    storageAccountName: scriptsStorage
   }
 }
 
@@ -182,7 +200,10 @@ module oidcApp 'modules/oidc-app.bicep' = if (enableEntraApp) {
     redirectUris: ['${gatewayUrl}/auth/callback']
     vaultName: keyVault.outputs.vaultName
     identityId: identities.outputs.deployerIdentityId
+    subnetId: scriptsSubnet
+    storageAccountName: scriptsStorage
   }
+  dependsOn: [privateEndpoints]
 }
 
 module diagnostics 'modules/diagnostics.bicep' = {

@@ -17,6 +17,16 @@ param rotate bool = false
 @description('Changes on every deployment so the (idempotent) script runs again')
 param forceUpdateTag string = utcNow()
 
+@description('Private networking: the script container joins this delegated subnet (the vault admits no public traffic)')
+param subnetId string = ''
+
+@description('Private networking: storage account for the script files, reachable from subnetId')
+param storageAccountName string = ''
+
+resource scriptStorage 'Microsoft.Storage/storageAccounts@2023-05-01' existing = if (!empty(storageAccountName)) {
+  name: storageAccountName
+}
+
 resource keyScript 'Microsoft.Resources/deploymentScripts@2023-08-01' = {
   name: 'jwt-keys-${vaultName}'
   location: location
@@ -29,6 +39,11 @@ resource keyScript 'Microsoft.Resources/deploymentScripts@2023-08-01' = {
     retentionInterval: 'PT1H'
     timeout: 'PT15M'
     cleanupPreference: 'OnSuccess'
+    containerSettings: empty(subnetId) ? null : { subnetIds: [ { id: subnetId } ] }
+    storageAccountSettings: empty(storageAccountName) ? null : {
+      storageAccountName: storageAccountName
+      storageAccountKey: scriptStorage.listKeys().keys[0].value
+    }
     environmentVariables: [
       { name: 'VAULT', value: vaultName }
       { name: 'BITS', value: string(keyBits) }
@@ -36,11 +51,15 @@ resource keyScript 'Microsoft.Resources/deploymentScripts@2023-08-01' = {
     ]
     scriptContent: '''
       set -euo pipefail
-      # RBAC role assignments on the vault can take a minute to reach the data plane
+      # RBAC role assignments on the vault can take a minute to reach the data plane; a vault
+      # still unreachable after 5 minutes (role or network) fails the deployment here, instead of
+      # reading as "no key" below
+      ok=0
       for i in $(seq 1 20); do
-        if az keyvault secret list --vault-name "$VAULT" -o none 2>/dev/null; then break; fi
+        if az keyvault secret list --vault-name "$VAULT" -o none 2>/dev/null; then ok=1; break; fi
         sleep 15
       done
+      if [ "$ok" != "1" ]; then echo "key vault $VAULT not reachable from the script" >&2; exit 1; fi
       if [ "$ROTATE" != "1" ] && az keyvault secret show --vault-name "$VAULT" -n jwt-private-key -o none 2>/dev/null; then
         echo "jwt key pair present: kept"
       else

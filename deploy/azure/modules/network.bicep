@@ -15,8 +15,12 @@ param aksSubnetPrefix string = '10.20.0.0/18'
 @description('Private endpoints of the platform services')
 param endpointSubnetPrefix string = '10.20.64.0/24'
 
+@description('Deployment-script containers (JWT keys, OIDC app): they write Key Vault secrets, so with public access off they must run inside the vnet')
+param scriptsSubnetPrefix string = '10.20.65.0/27'
+
 var aksSubnetName = 'aks'
 var endpointSubnetName = 'private-endpoints'
+var scriptsSubnetName = 'deployment-scripts'
 
 resource nsg 'Microsoft.Network/networkSecurityGroups@2024-01-01' = {
   name: '${base}-aks-nsg'
@@ -63,6 +67,18 @@ resource vnet 'Microsoft.Network/virtualNetworks@2024-01-01' = {
           privateEndpointNetworkPolicies: 'Disabled'
         }
       }
+      {
+        // Azure Container Instances run the deployment scripts; the Storage service endpoint lets
+        // them mount the scripts' file share from a storage account that admits this subnet only
+        name: scriptsSubnetName
+        properties: {
+          addressPrefix: scriptsSubnetPrefix
+          serviceEndpoints: [ { service: 'Microsoft.Storage' } ]
+          delegations: [
+            { name: 'aci', properties: { serviceName: 'Microsoft.ContainerInstance/containerGroups' } }
+          ]
+        }
+      }
     ]
   }
 }
@@ -70,3 +86,4 @@ resource vnet 'Microsoft.Network/virtualNetworks@2024-01-01' = {
 output vnetId string = vnet.id
 output aksSubnetId string = '${vnet.id}/subnets/${aksSubnetName}'
 output endpointSubnetId string = '${vnet.id}/subnets/${endpointSubnetName}'
+output scriptsSubnetId string = '${vnet.id}/subnets/${scriptsSubnetName}'

@@ -110,3 +110,26 @@ def test_deployment_scripts_write_the_secrets_the_drivers_read():
     main = (AZ / "main.bicep").read_text()
     for mod in ("network", "privatedns", "privateendpoints", "jwtkeys", "oidc-app", "diagnostics", "dashboard"):
         assert f"'modules/{mod}.bicep'" in main, mod
+
+
+def test_deployment_scripts_reach_a_private_vault():
+    """With private networking the vault refuses public traffic, so both secret-writing deployment
+    scripts run in the vnet's delegated subnet with a storage account that admits it; the JWT
+    script fails loudly when the vault stays unreachable; the OIDC script rotates its client
+    secret only near expiry and deletes the older ones (no pile-up of valid secrets)."""
+    main = (AZ / "main.bicep").read_text()
+    net = (AZ / "modules" / "network.bicep").read_text()
+    assert "Microsoft.ContainerInstance/containerGroups" in net and "scriptsSubnetId" in net
+    for mod in ("jwtkeys", "oidc-app"):
+        t = (AZ / "modules" / f"{mod}.bicep").read_text()
+        assert "containerSettings: empty(subnetId) ? null : { subnetIds: [ { id: subnetId } ] }" in t, mod
+        assert "storageAccountSettings:" in t and "listKeys()" in t, mod
+        i = main.index(f"'modules/{mod}.bicep'")
+        body = _block(main, main.index("{", i))
+        assert "subnetId: scriptsSubnet" in body and "storageAccountName: scriptsStorage" in body, mod
+    jwt = (AZ / "modules" / "jwtkeys.bicep").read_text()
+    assert 'if [ "$ok" != "1" ]' in jwt and "exit 1" in jwt
+    oidc = (AZ / "modules" / "oidc-app.bicep").read_text()
+    assert "RENEW_DAYS" in oidc and "az ad app credential delete" in oidc and "--expires" in oidc
+    # the reset only happens in the renewal branch
+    assert oidc.index("credential reset") > oidc.index("else")
