@@ -1,0 +1,13 @@
+#!/bin/bash
+# Decode GEMM: the no-reload ring tail (abl 0 / 3) against the round-5 re-reading tail (abl 256 / 259),
+# A/B/A/B in one process; then the GPU kernel tests of the decode GEMM.
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 400 python -u scripts/bench_dgemm.py --ablate --abl 0 256 3 259 0 256 3 259 --out gpurun_out/r06_dgemm_tail.jsonl > gpurun_out/r06_dgemm_tail.log 2>&1 || { tail -20 gpurun_out/r06_dgemm_tail.log; exit 1; }
+python - <<'PY'
+import json
+for l in open("gpurun_out/r06_dgemm_tail.jsonl"):
+    r = json.loads(l); print(r["shape"], {k: v for k, v in r.items() if "abl" in k or k.startswith("pk_bn") or "err_packed" in k})
+PY
+timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -k "dgemm" --timeout 300 --timeout-method thread > gpurun_out/r06_dgemm_tests.log 2>&1; rc=$?; tail -3 gpurun_out/r06_dgemm_tests.log; exit $rc
