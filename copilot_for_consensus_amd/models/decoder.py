@@ -467,6 +467,14 @@ class DecoderModel:
         # (written by another XCD, served from the MALL) stall the weight stream behind them:
         # Mistral-7B 307.7 vs 313.5 tok/s, Llama-2-13B 177.1 vs 190.9 (profiles/r04_gemv_norm_ab.log)
         self.gemv_norm_fused = os.environ.get("CFC_DECODE_GEMV_NORM", "0") == "1"
+        # TP > 1: the row-parallel (o / down) partials are all-reduced in fp32 and rounded to bf16
+        # ONCE, as TP = 1 rounds the full sum (CFC_TP_AR_DTYPE=fp32, default); "bf16" rounds each
+        # rank's partial first and halves the prefill all-reduce bytes (round 5's behaviour).  The
+        # batched decode always sums fp32 (one-shot kernel: latency-bound, bytes do not matter)
+        ard = os.environ.get("CFC_TP_AR_DTYPE", "fp32")
+        if ard not in ("fp32", "bf16"):
+            raise ValueError(f"CFC_TP_AR_DTYPE={ard!r}: expected fp32 or bf16")
+        self.tp_fp32 = weights.tp_size > 1 and ard == "fp32" and not (weights.fp8_layers is not None)
         # split-K of the batched qkv decode GEMM (its slabs feed rope_kv): 0 = the cost model's pick
         self.qkv_split = int(os.environ.get("CFC_DECODE_QKV_SPLIT", "0"))
         # B <= 4 decode on the ggml-quantized weights (GGUF checkpoints; csrc/kernels/quant.hip)
@@ -531,6 +539,11 @@ class DecoderModel:
             return K.linear_fp8(x, w8, s)
         return F.linear(x, self.w.layers[i][name])
 
+    def _lin32(self, i: int, name: str, x: torch.Tensor) -> torch.Tensor:
+        """Projection ``name`` of layer ``i`` as an fp32 [M, N] (library / CPU path): a row-parallel
+        partial that is all-reduced before its one bf16 rounding."""
+        return F.linear(x.float(), K._rowmajor(self.w.layers[i][name]).float())
+
     def _plin(self, i: int, name: str, x: torch.Tensor, epi: str = "bf16") -> torch.Tensor:
         """Prefill projection (``epi`` "swiglu" returns silu(gate) * up of the interleaved gate/up
         weights): the hand-written pgemm on the packed weight when selected and the shape fits;
@@ -547,6 +560,36 @@ class DecoderModel:
                 return K.dgemm_swiglu(x, pw) if epi == "swiglu" else K.dgemm_linear(x, pw)
         y = self._lin(i, name, x)
         return K.silu_mul(y, interleaved=self.w.gate_up_interleaved) if epi == "swiglu" else y
+
+    def _plin32(self, i: int, name: str, x: torch.Tensor) -> torch.Tensor:
+        """A row-parallel projection's fp32 partial [M, N] (TP > 1, CFC_TP_AR_DTYPE=fp32): pgemm's fp32
+        epilogue on the packed weight, the decode GEMM's split-1 fp32 output for short chunks, else an
+        fp32 GEMM.  A fresh tensor (the decode GEMM's output lives in a per-stream workspace that the
+        next call would reuse under an asynchronous all-reduce)."""
+        pw = self.w.packed[i][name] if self.w.packed is not None else None
+        wt = pw if pw is not None else self.w.layers[i][name]
+        if self.prefill_gemm == "hip" and x.is_cuda and x.is_contiguous():
+            dg = pw is not None and K.dgemm_ok(x, pw)
+            if (x.shape[0] >= self.PGEMM_MIN_ROWS and K.pgemm_ok(x, wt)
+                    and not (dg and self._dgemm_faster(x.shape[0], wt.shape[0], x.shape[1]))):
+                return K.pgemm(x, wt, "f32", variant=self.pgemm_variant)
+            if dg:
+                return K.dgemm(x, pw, "part", 1)[0].clone()
+        return F.linear(x.float(), K._rowmajor(wt).float())
+
+    def _tp_norm(self, part: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:
+        """residual += bf16(sum over the TP group of this rank's fp32 partial(s)); returns
+        RMSNorm(residual) * norm_w -- TP = 1's split-K reduce arithmetic, the projection rounded to
+        bf16 once.  ``part``: [M, N] or k-slice slabs [S, M, N].  One launch on the one-shot IPC
+        kernel when the rows fit its staging (decode; short prefill chunks), else an fp32
+        all-reduce of the row sums + the reduce kernel."""
+        p3 = part if part.dim() == 3 else part[None]
+        ar = self.custom_ar
+        if ar is not None and ar.supports_slabs(p3):
+            return ar.residual_rmsnorm(p3, residual, norm_w, self.cfg.rms_eps)
+        t = p3.sum(0, keepdim=True) if p3.shape[0] > 1 else p3.contiguous()
+        torch.distributed.all_reduce(t, group=self.tp_group)
+        return K.splitk_residual_rmsnorm(t, residual, norm_w, self.cfg.rms_eps)
 
     PGEMM_MIN_TILES = 96   # fewer 256 x 256 output tiles than this: the decode GEMM is as fast or faster
 
@@ -594,16 +637,31 @@ class DecoderModel:
         cfg, w = self.cfg, self.w
         x = K.embedding(w.embed, ids)
         residual = None
+        x32 = None                     # TP fp32: this rank's fp32 partial of the previous layer's down
+        eps = cfg.rms_eps
         for i in range(cfg.layers):
             lw = w.layers[i]
-            h, residual = self._layer_pre(i, x, residual)
+            if x32 is not None:
+                h = self._tp_norm(x32, residual, lw["attn_norm"])
+            else:
+                h, residual = self._layer_pre(i, x, residual)
             qkv = self._plin(i, "qkv", h)
             q = K.rope_kv_write(qkv, positions, slots, w.cos_sin, kv.k[i], kv.v[i], w.heads, w.kv_heads,
                                 cfg.head_dim, runs=v_runs, k_scale=kv.k_scale, v_scale=kv.v_scale)
             attn = K.prefill_attention(q, kv.k[i], kv.v[i], block_tables, cu_q, ctx_lens, self.scale, tiles=tiles,
                                        window=self.window, k_scale=kv.k_scale, v_scale=kv.v_scale)
-            o = self._all_reduce(self._plin(i, "o", attn.view(attn.shape[0], -1)))
+            a2 = attn.view(attn.shape[0], -1)
+            if self.tp_fp32:
+                # row-parallel o / down: fp32 partials summed over the ranks, rounded once in the reduce
+                h = self._tp_norm(self._plin32(i, "o", a2), residual, lw["mlp_norm"])
+                x32 = self._plin32(i, "down", self._plin(i, "gate_up", h, "swiglu"))
+                continue
+            o = self._all_reduce(self._plin(i, "o", a2))
             x = self._mlp(i, o, residual)
+        if x32 is not None:
+            if last_idx is not None:
+                x32, residual = x32.index_select(0, last_idx), residual.index_select(0, last_idx)
+            return self._tp_norm(x32.contiguous(), residual, w.final_norm)
         if last_idx is not None:
             x = x.index_select(0, last_idx)
             residual = residual.index_select(0, last_idx)
@@ -625,6 +683,8 @@ class DecoderModel:
         cfg, w = self.cfg, self.w
         dist = torch.distributed
         st = [{"m": m, "x": K.embedding(w.embed, m["ids"]), "res": None, "work": None} for m in halves]
+        f32 = self.tp_fp32
+        eps = cfg.rms_eps
 
         def start(s, t):
             s["work"] = dist.all_reduce(t, group=self.tp_group, async_op=True)
@@ -639,7 +699,10 @@ class DecoderModel:
             for s in st:
                 m = s["m"]
                 wait(s)                                          # x: the previous layer's reduced down
-                h, s["res"] = self._layer_pre(i, s["x"], s["res"])
+                if f32 and i > 0:
+                    h = K.splitk_residual_rmsnorm(s["x"][None], s["res"], lw["attn_norm"], eps)
+                else:
+                    h, s["res"] = self._layer_pre(i, s["x"], s["res"])
                 qkv = self._plin(i, "qkv", h)
                 q = K.rope_kv_write(qkv, m["positions"], m["slots"], w.cos_sin, kv.k[i], kv.v[i], w.heads,
                                     w.kv_heads, cfg.head_dim, runs=m["v_runs"], k_scale=kv.k_scale,
@@ -647,13 +710,17 @@ class DecoderModel:
                 attn = K.prefill_attention(q, kv.k[i], kv.v[i], m["block_tables"], m["cu_q"], m["ctx_lens"],
                                            self.scale, tiles=m["tiles"], window=self.window, k_scale=kv.k_scale,
                                            v_scale=kv.v_scale)
-                s["o"] = self._plin(i, "o", attn.view(attn.shape[0], -1))
+                a2 = attn.view(attn.shape[0], -1)
+                s["o"] = self._plin32(i, "o", a2) if f32 else self._plin(i, "o", a2)
                 start(s, s["o"])
             for s in st:
                 wait(s)
-                h = K.rmsnorm(s["o"], lw["mlp_norm"], cfg.rms_eps, residual=s["res"])
+                if f32:
+                    h = K.splitk_residual_rmsnorm(s["o"][None], s["res"], lw["mlp_norm"], eps)
+                else:
+                    h = K.rmsnorm(s["o"], lw["mlp_norm"], eps, residual=s["res"])
                 a = self._plin(i, "gate_up", h, "swiglu")
-                s["x"] = self._plin(i, "down", a)
+                s["x"] = self._plin32(i, "down", a) if f32 else self._plin(i, "down", a)
                 s["o"] = None
                 start(s, s["x"])
         out = []
@@ -662,7 +729,10 @@ class DecoderModel:
             x, res, last = s["x"], s["res"], s["m"]["last_idx"]
             if last is not None:
                 x, res = x.index_select(0, last), res.index_select(0, last)
-            out.append(K.rmsnorm(x, w.final_norm, cfg.rms_eps, residual=res))
+            if f32:
+                out.append(K.splitk_residual_rmsnorm(x[None].contiguous(), res, w.final_norm, eps))
+            else:
+                out.append(K.rmsnorm(x, w.final_norm, eps, residual=res))
         return out
 
     def forward_decode(self, ids, positions, slots, ctx_lens, block_tables, kv, attn_workspace=None,
@@ -682,14 +752,25 @@ class DecoderModel:
             return self._forward_decode_splitk(x, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
                                                part_blocks)
         residual = None
+        x32 = None
         for i in range(cfg.layers):
             lw = w.layers[i]
-            h, residual = self._layer_pre(i, x, residual)
+            if x32 is not None:
+                h = self._tp_norm(x32, residual, lw["attn_norm"])
+            else:
+                h, residual = self._layer_pre(i, x, residual)
             qkv = self._lin(i, "qkv", h)
             attn = self._rope_attention(i, qkv, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
                                         part_blocks)
+            if self.tp_fp32:
+                h = self._tp_norm(self._lin32(i, "o", attn.view(B, -1)), residual, lw["mlp_norm"])
+                gu = self._lin(i, "gate_up", h)
+                x32 = self._lin32(i, "down", K.silu_mul(gu, interleaved=w.gate_up_interleaved))
+                continue
             o = self._all_reduce(self._lin(i, "o", attn.view(B, -1)))
             x = self._mlp(i, o, residual)
+        if x32 is not None:
+            return self._tp_norm(x32, residual, w.final_norm)
         return K.rmsnorm(x, w.final_norm, cfg.rms_eps, residual=residual)
 
     def _rope_attention(self, i, qkv, positions, slots, ctx_lens, block_tables, kv, attn_workspace, part_blocks):
@@ -740,18 +821,27 @@ class DecoderModel:
             attn = self._rope_attention(i, qkv, positions, slots, ctx_lens, block_tables, kv, attn_workspace,
                                         part_blocks)
             if tp:
-                o = self._all_reduce(K.dgemm_linear(attn.view(B, -1), pw["o"]))
-                h = K.rmsnorm(o, lw["mlp_norm"], eps, residual=residual)
+                h = self._tp_residual_rmsnorm(attn.view(B, -1), pw["o"], residual, lw["mlp_norm"], eps)
             else:
                 h = K.dgemm_residual_rmsnorm(attn.view(B, -1), pw["o"], residual, lw["mlp_norm"], eps)
             a = K.dgemm_swiglu(h, pw["gate_up"])
             nxt = w.layers[i + 1]["attn_norm"] if i + 1 < cfg.layers else w.final_norm
             if tp:
-                d = self._all_reduce(K.dgemm_linear(a, pw["down"]))
-                h = K.rmsnorm(d, nxt, eps, residual=residual)
+                h = self._tp_residual_rmsnorm(a, pw["down"], residual, nxt, eps)
             else:
                 h = K.dgemm_residual_rmsnorm(a, pw["down"], residual, nxt, eps)
         return h
+
+    def _tp_residual_rmsnorm(self, x, w, residual, norm_w, eps):
+        """Row-parallel projection + all-reduce + residual + RMSNorm at TP > 1 with TP = 1's
+        rounding points: the decode GEMM's fp32 k-slice slabs of this rank's K shard are summed over
+        the TP group in fp32 and rounded to bf16 once (as TP = 1's split-K reduce does), never per
+        rank.  On the one-shot IPC kernel: ONE launch after the GEMM (comm.hip:
+        oneshot_ar_residual_rmsnorm_kernel); else an fp32 all-reduce of the rank's row sums (RCCL /
+        gloo) and the split = 1 reduce kernel."""
+        B, Kd = x.shape
+        bn, split = K.dgemm_config(B, w.shape[0], Kd, bn=getattr(w, "bn", None))
+        return self._tp_norm(K.dgemm(x, w, "part", split, bn=bn), residual, norm_w)
 
     def _forward_decode_splitk(self, x, positions, slots, ctx_lens, block_tables, kv, attn_workspace, part_blocks):
         """Library GEMMs; o and down as batched split-K with residual + next RMSNorm in the reduce."""
@@ -913,9 +1003,9 @@ class DecoderModel:
         ar = self.custom_ar
         if self.w.tp_size == 1:
             return True
-        n = B * self.cfg.hidden       # the o / down all-reduces: B x hidden bf16
+        n = B * self.cfg.hidden       # the o / down all-reduces: B x hidden fp32 row sums
         return (ar is not None and ar.enabled and ar.supports_keys(B) and n % 8 == 0
-                and n * 2 <= ar.staging_bytes)
+                and n * 4 <= ar.staging_bytes and self.cfg.hidden <= 8192)
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         """[B, V] logits (all-gathered over the vocab-parallel shards)."""

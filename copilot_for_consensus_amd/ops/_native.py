@@ -83,6 +83,7 @@ _KERNEL_SIGS = {
     "cfc_ar_max_blocks": [],
     "cfc_oneshot_allreduce": [P, P, c_int64, P, I, I, c_int64, I, P, P, P],
     "cfc_oneshot_keymax": [P, P, I, P, I, I, c_int64, P, P, P],
+    "cfc_oneshot_ar_residual_rmsnorm": [P, I, I, I, P, P, F, P, P, I, I, c_int64, I, P, P, P],
     "cfc_ar_key_rows": [],
 }
 

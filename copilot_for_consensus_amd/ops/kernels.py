@@ -593,7 +593,7 @@ def dgemm_residual_rmsnorm(x: torch.Tensor, w: torch.Tensor, residual: torch.Ten
 
 
 # ------------------------------------------------------------------ prefill / encoder GEMM
-PGEMM_EPI = {"bf16": 0, "bias": 1, "bias_gelu": 2, "swiglu": 3}
+PGEMM_EPI = {"bf16": 0, "bias": 1, "bias_gelu": 2, "swiglu": 3, "f32": 4}
 
 
 def pgemm_ok(x: torch.Tensor, w) -> bool:
@@ -635,6 +635,8 @@ def pgemm(x: torch.Tensor, w, epi: str = "bf16", bias: torch.Tensor | None = Non
             y = torch.nn.functional.gelu(y)
         if mode == 3:
             return ref.silu_mul_interleaved(y.to(x.dtype))
+        if mode == 4:
+            return y
         return y.to(x.dtype)
     if not pgemm_ok(x, w):
         raise ValueError(f"pgemm: x {tuple(x.shape)} {x.dtype} w {tuple(w.shape)} {getattr(w, 'dtype', 'packed')}")
@@ -644,8 +646,11 @@ def pgemm(x: torch.Tensor, w, epi: str = "bf16", bias: torch.Tensor | None = Non
         _req(bias, torch.bfloat16, "bias")
         if bias.numel() != N:
             raise ValueError(f"pgemm: bias of {bias.numel()} for N = {N}")
+    if mode == 4 and (variant or PGEMM_VARIANT) not in ("pp", "pps") and not packed:
+        variant = "pp"              # the fp32 epilogue is built for the ping-pong kernel only
     if out is None:
-        out = torch.empty(M, N // 2 if mode == 3 else N, dtype=torch.bfloat16, device=x.device)
+        out = torch.empty(M, N // 2 if mode == 3 else N, dtype=torch.float32 if mode == 4 else torch.bfloat16,
+                          device=x.device)
     wptr = w.data.data_ptr() if packed else w.data_ptr()
     check(kernels().cfc_pgemm(x.data_ptr(), wptr, bias.data_ptr() if bias is not None else None,
                               out.data_ptr(), M, N, Kd, mode | (PGEMM_VARIANTS[variant or PGEMM_VARIANT] << 4),

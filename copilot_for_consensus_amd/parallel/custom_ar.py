@@ -106,6 +106,29 @@ class OneShotAllReduce:
         _check(rc, "cfc_oneshot_allreduce")
         return out
 
+    def supports_slabs(self, part: torch.Tensor) -> bool:
+        """fp32 split-K slabs [split, M, N] the fused all-reduce + residual + RMSNorm takes."""
+        if not self.enabled or part.dim() != 3 or part.dtype != torch.float32 or not part.is_contiguous():
+            return False
+        _, M, N = part.shape
+        return N % 8 == 0 and N <= 8192 and M * N * 4 <= self.staging_bytes and part.data_ptr() % 16 == 0
+
+    def residual_rmsnorm(self, part: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor, eps: float,
+                         out: torch.Tensor | None = None) -> torch.Tensor:
+        """The row-parallel projection's epilogue over the TP group in ONE kernel: this rank's fp32
+        k-slice slabs are summed, exchanged and added over the ranks in fp32, then residual +=
+        bf16(sum) and out = RMSNorm(residual) * norm_w -- the TP = 1 reduce kernel's arithmetic
+        (cfc_splitk_residual_rmsnorm) with the projection summed over every rank before its one
+        bf16 rounding (comm.hip: oneshot_ar_residual_rmsnorm_kernel)."""
+        split, M, N = part.shape
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=part.device) if out is None else out
+        rc = _lib().cfc_oneshot_ar_residual_rmsnorm(
+            part.data_ptr(), split, M, N, residual.data_ptr(), norm_w.data_ptr(), float(eps), out.data_ptr(),
+            self._bases, self.world, self.rank, self.staging_bytes, self.blocks, self.epochs.data_ptr(),
+            self.err.data_ptr(), torch.cuda.current_stream(part.device).cuda_stream)
+        _check(rc, "cfc_oneshot_ar_residual_rmsnorm")
+        return out
+
     def supports_keys(self, n: int) -> bool:
         return self.enabled and 0 < n <= self.key_rows
 

@@ -130,6 +130,7 @@ __device__ __forceinline__ uint4 dg_ldw(const uint16_t* p) {
 //   32 = contiguous W pieces: wave w loads fragments 2w, 2w+1 of the stage's 2 NW KB region (one
 //   2-KB run per wave) instead of its own group's two 1-KB fragments NW KB apart (wrong sums);
 //   64 = two X-loader waves + an 8-slot X ring (DgShape MX);
+//   256 = the round-5 tail (re-reads the last stage instead of issuing no loads);
 //   128 = no workgroup barrier in the compute waves' stage loop (with 1 only: the loader waves
 //   return at once) -- is the per-stage lockstep of the compute waves what slows the W stream?
 // PACKED: W in the fragment-packed layout of cfc_dgemm_pack for this BN: tile-major, then 32-deep
@@ -225,9 +226,19 @@ __global__ void __launch_bounds__((64 * DgShape<BM, BN, (ABL & 64) != 0>::WAVES)
       dst[1] = dg_ldw<NTW>(wp + s * 64 + 32);
     }
   };
+  // packed: logical stage s of the slice, or -- past its end -- zeros from an out-of-range buffer
+  // offset (no memory access); the condition is wave-uniform, so this is a scalar select, no branch
+  auto load_stage_past = [&](int s, uint4 (&dst)[2]) {
+    const int so = __builtin_amdgcn_readfirstlane(s < nst ? wsoff + phys(s) * 2 * NW * 1024 : 0x40000000);
+    dst[0] = dg_ldw_buf<NTW>(wrs, wvoff, so);
+    dst[1] = dg_ldw_buf<NTW>(wrs, wvoff, so + ((ABL & 32) ? 1024 : NW * 1024));
+  };
   if constexpr ((ABL & 16) != 0) asm volatile("s_barrier" ::: "memory");
 #pragma unroll
-  for (int p = 0; p < D; ++p) load_stage(phys(min(p, nst - 1)), ring[p]);
+  for (int p = 0; p < D; ++p) {
+    if constexpr (PACKED && (ABL & 256) == 0) load_stage_past(p, ring[p]);
+    else load_stage(phys(min(p, nst - 1)), ring[p]);
+  }
   f32x4_t acc[S::MT];
 #pragma unroll
   for (int i = 0; i < S::MT; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -253,13 +264,22 @@ __global__ void __launch_bounds__((64 * DgShape<BM, BN, (ABL & 64) != 0>::WAVES)
     xslot = xslot + 1 == S::NSX ? 0 : xslot + 1;
   };
 
+  // Stage s lives in ring slot s % D; after computing stage s the slot is refilled with stage
+  // s + D.  Every load is unconditional (a branch around a load makes hipcc drain the ring at the
+  // join), so the last D refills of a slice name stages past its end: on the packed path they are
+  // buffer loads at an offset past the descriptor's range, which return zeros without touching
+  // memory (round 5 and before re-read the last stage D times instead: up to half of a small
+  // slice's loads, e.g. 8 redundant 2-KB stages per wave of qkv's 16 at split 4).  The ring is never
+  // read past the slice (the tail computes only real stages).
+  constexpr bool TAIL_RELOAD = (ABL & 256) != 0;    // probe: the round-5 re-reading tail
   int st = 0;
   for (; st + D <= nst; st += D) {
 #pragma unroll
     for (int u = 0; u < D; ++u) {
       if constexpr (!NOBAR) dg_barrier();   // X stage st+u is in LDS
       compute(ring[u]);
-      load_stage(phys(min(st + u + D, nst - 1)), ring[u]);   // unconditional: the tail re-reads the last stage
+      if constexpr (PACKED && !TAIL_RELOAD) load_stage_past(st + u + D, ring[u]);
+      else load_stage(phys(min(st + u + D, nst - 1)), ring[u]);
     }
   }
 #pragma unroll
@@ -413,7 +433,7 @@ CFC_API int cfc_dgemm_pack(const void* w, void* wp, int N, int K, int bn, hipStr
 // (not nontemporal) cache policy on the weight stream.
 CFC_API int cfc_dgemm_ablate(const void* x, const void* w, int M, int N, int K, int split, int bn, int abl,
                              float* part, hipStream_t stream) {
-  if (M > 128 || (abl & ~255)) return -1;
+  if (M > 128 || (abl & ~511)) return -1;
   if (const int e = dgemm_check(M, N, K, split, DG_PART, bn, part, nullptr)) return e;
   int rc;
   switch (abl) {
@@ -433,6 +453,8 @@ CFC_API int cfc_dgemm_ablate(const void* x, const void* w, int M, int N, int K, 
     case 96: DG_ABL(96, true)
     case 129: DG_ABL(129, true)
     case 131: DG_ABL(131, true)
+    case 256: DG_ABL(256, true)
+    case 259: DG_ABL(259, true)
 #undef DG_ABL
     default: return -3;
   }

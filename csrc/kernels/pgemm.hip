@@ -34,7 +34,9 @@ namespace {
 
 typedef __attribute__((address_space(3))) void pg_lds_t;
 
-enum { PG_BF16 = 0, PG_BIAS = 1, PG_BIAS_GELU = 2, PG_SWIGLU = 3 };
+// PG_F32: the fp32 accumulators themselves (row stride ldo in floats): a tensor-parallel row-parallel
+// projection's partial, all-reduced in fp32 and rounded to bf16 once, as TP = 1 rounds the full sum
+enum { PG_BF16 = 0, PG_BIAS = 1, PG_BIAS_GELU = 2, PG_SWIGLU = 3, PG_F32 = 4 };
 
 constexpr int PG_BM = 256, PG_BN = 256, PG_BK = 64;
 constexpr int PG_STAGE = (PG_BM + PG_BN) * PG_BK * 2;   // 64 KB: A image then B image
@@ -98,6 +100,9 @@ __device__ __forceinline__ void pg_epilogue(const f32x4_t (&acc)[8][NJ], const u
         // bf16 rounding of g and u as the unfused GEMM -> silu_mul path
         const uint2 y = pg_swiglu4(v, g);
         if (g < 2 && m < M && nb < N) *reinterpret_cast<uint2*>(out + (size_t)m * ldo + nb / 2 + 4 * g) = y;
+      } else if constexpr (EPI == PG_F32) {
+        if (m < M && n < N)
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + (size_t)m * ldo + n) = make_float4(v[0], v[1], v[2], v[3]);
       } else {
         if (m < M && n < N) {
           if constexpr (EPI == PG_BIAS || EPI == PG_BIAS_GELU) {
@@ -964,6 +969,17 @@ int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int 
   return (int)hipGetLastError();
 }
 
+// fp32 output: the ping-pong kernel only (packed or row-major W)
+int pgemm_launch_f32(const void* x, const void* w, void* out, int M, int N, int K, int ldo, int wnw,
+                     hipStream_t stream) {
+  const int tm = (M + PG_BM - 1) / PG_BM, tn = (N + PG_BN - 1) / PG_BN;
+  const uint16_t *xp = (const uint16_t*)x, *wp = (const uint16_t*)w;
+  uint16_t* op = (uint16_t*)out;
+  if (wnw > 0) pgemm_pp_kernel<PG_F32, true, PP_PF><<<tm * tn, 512, 0, stream>>>(xp, wp, nullptr, op, M, N, K, ldo, tm, tn, wnw);
+  else pgemm_pp_kernel<PG_F32, false, PP_PF><<<tm * tn, 512, 0, stream>>>(xp, wp, nullptr, op, M, N, K, ldo, tm, tn, 1);
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 // epi & 15: 0 bf16, 1 + bias, 2 + bias -> GELU, 3 SwiGLU (out [M, N/2]); epi >> 4: K-loop variant
@@ -983,6 +999,7 @@ CFC_API int cfc_pgemm(const void* x, const void* w, const void* bias, void* out,
     case 1: return pgemm_launch<PG_BIAS>(x, w, bias, out, M, N, K, ldo, variant, wnw, stream);
     case 2: return pgemm_launch<PG_BIAS_GELU>(x, w, bias, out, M, N, K, ldo, variant, wnw, stream);
     case 3: return pgemm_launch<PG_SWIGLU>(x, w, bias, out, M, N, K, ldo, variant, wnw, stream);
+    case 4: return pgemm_launch_f32(x, w, out, M, N, K, ldo, wnw, stream);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -185,8 +185,23 @@ def test_tp2_decoder_with_oneshot_allreduce_matches_tp1():
         assert res[r]["graphed"], "TP=2 greedy decode should run as a captured graph"
         assert res[r]["tokens"] == res[r]["eager"], (res[r]["tokens"], res[r]["eager"])
     assert res[0]["tokens"] == res[1]["tokens"]
-    agree = sum(a == b for x, y in zip(res[0]["tokens"], ref) for a, b in zip(x, y))
-    assert agree >= 0.9 * sum(len(x) for x in ref), (res[0]["tokens"], ref)
+    # teacher-forced against TP=1 on TP=2's own prefix (as the Mistral / 70B / wide tests): every
+    # token within 0.1 sigma of TP=1's best and TP=1's argmax in >= 90 % of the steps
+    tp2 = res[0]["tokens"]
+    m1 = DecoderModel(DecoderWeights.random(cfg, "cuda:0", seed=5))
+    eng = LLMEngine(m1, PagedKVCache(cfg.layers, 64, cfg.kv_heads, cfg.head_dim, "cuda:0"), use_graph=False,
+                    prefix_cache=False)
+    exact, worst = 0, 0.0
+    for j in range(8):
+        lg = _last_logits(eng, m1, [p + t[:j] for p, t in zip(prompts, tp2)])
+        sig = lg.std(-1)
+        for i, t in enumerate(tp2):
+            gap = float((lg[i].max() - lg[i, t[j]]) / sig[i])
+            worst = max(worst, gap)
+            exact += int(gap == 0.0)
+    n = 8 * len(prompts)
+    assert worst <= 0.1, f"a TP=2 token is {worst:.3f} sigma below TP=1's best (exact {exact}/{n}; {tp2} vs {ref})"
+    assert exact >= 0.9 * n, f"TP=2 matched TP=1's argmax in {exact}/{n} teacher-forced steps"
 
 
 def _run_tp2(prompts, n_new, world=2, **kw):
@@ -281,12 +296,11 @@ def test_tp2_llama3_70b_matches_tp1_teacher_forced():
     32 q / 4 kv heads, FFN 14336 per rank, vocab shard 64128), greedy decode in the captured graph
     with the IPC all-reduces, against the unsharded model assembled from the same shards
     (parallel/tp.unshard_weights, 141 GB) teacher-forced on TP=2's own tokens, as
-    test_tp2_mistral7b_matches_tp1_greedy does.  The bound is wider than Mistral's: each of the 80
-    layers rounds its row-parallel o / down outputs to bf16 before the all-reduce (TP=1 keeps the
-    fp32 split-K slabs to the residual add), so the hidden states drift further apart than over 32
-    layers and near-ties among 128256 nearly flat random-init logits flip more often (measured
-    first run: worst 0.22 sigma, 57 / 64 exact).  A wrong shard would give ~0 % exact and tokens ~4
-    sigma below the best."""
+    test_tp2_mistral7b_matches_tp1_greedy does, at the same bound.  The decode's row-parallel o /
+    down projections are all-reduced as fp32 split-K sums and rounded to bf16 once, as TP=1 rounds
+    them (comm.hip: oneshot_ar_residual_rmsnorm_kernel); round 5 rounded each rank's partial to
+    bf16 first and needed a 0.5 sigma / 80 % bound over the 80 layers (worst 0.22 sigma, 57 / 64
+    exact).  A wrong shard would give ~0 % exact and tokens ~4 sigma below the best."""
     from copilot_for_consensus_amd.models.decoder import DecoderModel, DecoderWeights, get_config
     from copilot_for_consensus_amd.parallel.tp import unshard_weights
     from copilot_for_consensus_amd.runtime.engine import LLMEngine
@@ -323,8 +337,8 @@ def test_tp2_llama3_70b_matches_tp1_teacher_forced():
     n = n_new * len(prompts)
     del m1, eng, full
     torch.cuda.empty_cache()
-    assert worst <= 0.5, f"a TP=2 token is {worst:.3f} sigma below TP=1's best (exact {exact}/{n})"
-    assert exact >= 0.8 * n, f"TP=2 matched TP=1's argmax in {exact}/{n} teacher-forced steps"
+    assert worst <= 0.1, f"a TP=2 token is {worst:.3f} sigma below TP=1's best (exact {exact}/{n})"
+    assert exact >= 0.9 * n, f"TP=2 matched TP=1's argmax in {exact}/{n} teacher-forced steps"
 
 
 @pytest.mark.timeout(900)

@@ -894,3 +894,37 @@ def test_pgemm_ln(M, Kd):
     # the same as the unfused kernels on the device
     unf = K.layernorm(K.pgemm(x, w), g, be, 1e-12, bias=b, residual=res)
     assert float((y.float() - unf.float()).abs().max()) <= 0.0625
+
+
+@pytest.mark.parametrize("M,N,Kd,bn", [(300, 1024, 512, 128), (1000, 4096, 1024, 64), (257, 2048, 2048, 128)])
+def test_pgemm_f32_epilogue_packed_and_rowmajor(M, N, Kd, bn):
+    """The prefill GEMM's fp32 epilogue (a tensor-parallel row-parallel partial, all-reduced in fp32
+    before its one bf16 rounding): the fp32 accumulators vs the fp32 reference within fp32
+    summation-order error, rows past M never stored; the bf16 epilogue is exactly its rounding."""
+    x = (torch.rand(M, Kd, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(N, Kd, device=DEV) * 2 - 1) / Kd ** 0.5).bfloat16()
+    ref = _ref_linear(x, w)
+    pw = K.pack_dgemm_weight(w, bn=bn)
+    for wt in (pw, w):
+        y = K.pgemm(x, wt, "f32")
+        assert y.dtype == torch.float32 and y.shape == (M, N)
+        err = float((y.cpu() - ref).abs().max())
+        assert err <= 1e-4 * float(ref.abs().max()) + 1e-5, err
+        assert torch.equal(y.bfloat16(), K.pgemm(x, wt, "bf16", variant="pp"))
+
+
+def test_dgemm_tail_past_slice_loads_change_nothing():
+    """The decode GEMM's ring refills past a k-slice's end are out-of-range buffer loads (zeros, no
+    memory traffic): split-K slabs equal the round-5 re-reading tail's bit for bit, for slices that
+    are whole multiples of the ring (qkv-like) and not (down-like: 28 stages)."""
+    for (N, Kd, split, bn) in ((768, 4096, 4, 96), (512, 14336, 8, 128), (1024, 512, 1, 64)):
+        x = (torch.rand(128, Kd, device=DEV) * 2 - 1).bfloat16()
+        w = ((torch.rand(N, Kd, device=DEV) * 2 - 1) / Kd ** 0.5).bfloat16()
+        pw = K.pack_dgemm_weight(w, bn=bn)
+        a = K.dgemm(x, pw, "part", split).clone()
+        b = torch.empty_like(a)
+        K.check(K.kernels().cfc_dgemm_ablate(x.data_ptr(), pw.data.data_ptr(), 128, N, Kd, split, bn, 256,
+                                             b.data_ptr(), K._stream(x)), "ablate")
+        torch.cuda.synchronize()
+        assert torch.equal(a, b), (N, Kd, split)
+        _close(a.sum(0), _ref_linear(x, w), 1e-2)

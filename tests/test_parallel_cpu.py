@@ -154,10 +154,23 @@ class _EpochAR:
     def __call__(self, x, out=None):
         nb = min(-(-(x.numel() // 8) // 256), self.blocks)
         self._enter("sum", nb)
-        for b in range(nb):
+        for b in range(63):          # every sum-type launch advances all 63 sum blocks' epochs
             self.epochs[b] += 1
         dist.all_reduce(x, group=self.group)
         return x if out is None else out.copy_(x)
+
+    def supports_slabs(self, part):
+        return part.shape[1] * part.shape[2] * 4 <= self.staging_bytes
+
+    def residual_rmsnorm(self, part, residual, norm_w, eps):
+        """The fused fp32 all-reduce + residual + RMSNorm (comm.hip oneshot_ar_residual_rmsnorm)."""
+        from copilot_for_consensus_amd.ops import kernels as K
+        self._enter("norm", min(part.shape[1], self.blocks))
+        for b in range(63):
+            self.epochs[b] += 1
+        t = part.sum(0, keepdim=True)
+        dist.all_reduce(t, group=self.group)
+        return K.splitk_residual_rmsnorm(t, residual, norm_w, eps)
 
     def keymax(self, keys, out_ids):
         self._enter("keymax", 1)
@@ -209,7 +222,7 @@ def test_tp2_overlapped_prefill_keeps_one_shot_allreduce_epochs_in_step():
     (log0, ep0, in0, t0), (log1, ep1, in1, t1) = outs
     assert in0 == in1 and len(in0) == 2 and all(n == 0 for n in in0), (in0, in1)
     assert log0 == log1 and ep0 == ep1
-    assert any(tag == "sum" for tag, _ in log0) and any(tag == "keymax" for tag, _ in log0)
+    assert any(tag == "norm" for tag, _ in log0) and any(tag == "keymax" for tag, _ in log0)
     assert t0 == t1
 
 
