@@ -202,6 +202,7 @@ def main(argv=None):
         if parts:
             search = dict(parts[0])
             search.update(queries=sum(p["queries"] for p in parts),
+                          reports_per_query=round(statistics.mean(p["reports_per_query"] for p in parts), 1),
                           p50_ms=round(statistics.median([p["p50_ms"] for p in parts]), 2),
                           p95_ms=round(max(p["p95_ms"] for p in parts), 2), max_ms=round(max(p["max_ms"] for p in parts), 2))
     # after the timed window: the same GPUs at a load below saturation (Poisson arrivals), then a

@@ -180,10 +180,13 @@ class RagPipeline:
         every chunk the run embedded), group by thread, enrich from the document store.  Topics
         are thread subjects of the run; ``min_score`` 0 so every hit thread is enriched (the most
         work per query).  Against the reporting P95 SLO of 0.5 s
-        (infra/prometheus/alerts/slo_latency.yml:249).  With a DP-sharded index this is the local
-        shard (the cross-rank merge is a collective, parallel/knn.py)."""
+        (infra/prometheus/alerts/slo_latency.yml:249).  With a DP-sharded index the query is the
+        global exact top-k over every rank's shard (parallel/knn.py ShardedVectorIndex.query: local
+        HIP scan + all-gather of the candidates + merge), a collective every DP rank runs in step
+        with the same query count; enrichment finds the summaries this rank's store holds."""
         from ..services.reporting import ReportingService
-        rep = ReportingService(self.pub, None, self.docs, vector_store=self.local_index,
+        rep = ReportingService(self.pub, None, self.docs,
+                               vector_store=self.sharded if self.sharded is not None else self.local_index,
                                embedding_provider=self.embedder)
         subjects = sorted({t["subject"] for t in self.docs.query_documents("threads", {}, limit=1 << 30)
                            if t.get("subject")})
@@ -199,7 +202,10 @@ class RagPipeline:
             lat.append(time.perf_counter() - t)
             found += len(res)
         lat.sort()
-        return {"queries": n_queries, "limit": limit, "top_k": 3 * limit, "index_rows": int(self.local_index.count()),
+        rows = int(self.local_index.count())
+        if self.sharded is not None:
+            rows = int(self.sharded.count())
+        return {"queries": n_queries, "limit": limit, "top_k": 3 * limit, "index_rows": rows,
                 "p50_ms": round(1e3 * lat[len(lat) // 2], 2), "p95_ms": round(1e3 * lat[int(0.95 * (len(lat) - 1))], 2),
                 "max_ms": round(1e3 * lat[-1], 2), "reports_per_query": round(found / n_queries, 1),
                 "path": "ReportingService.search_reports_by_topic: HIP encoder embed -> HIP kNN (flat cosine, "
