@@ -342,6 +342,15 @@ def _main_node(args, env, groups):
     gen = sum(r.generated_tokens for r in results)
     prompt = sum(r.prompt_tokens for r in results)
     lats = [x for r in results for x in r.latencies_s]
+    # the light-load point through the same topology (rank 0's services, every rank's worker serving
+    # its owned threads): one-thread archives at a Poisson rate, archive submit -> report stored
+    service_light = None
+    if args.service_latency_rate > 0:
+        barrier()
+        if rank == 0:
+            service_light = nb.light_load_probe(args.service_latency_rate, args.service_latency_threads,
+                                                seed=args.seed + 271)
+        barrier()
     per_rank = [nb.dp_stats()]
     if world > 1:
         per_rank = [None] * world
@@ -365,6 +374,8 @@ def _main_node(args, env, groups):
             "p50_summary_latency_s": round(statistics.median(lats), 3) if lats else None,
             "p50_summary_latency_regime": "archive submit -> report stored, paced source (<= 2 steps in flight)",
             "per_rank": per_rank if world > 1 else None,
+            "latency_service_light": service_light,
+            "dp_wait": os.environ.get("CFC_DP_WAIT", "block") if world > 1 else None,
             "generated_tokens_per_s": round(gen / elapsed, 1), "prompt_tokens_per_s": round(prompt / elapsed, 1),
             "baseline_threads_per_s": round(BASELINE_THREADS_PER_S, 4)}), flush=True)
     if world > 1:

@@ -78,8 +78,8 @@ def _waiter(store):
         from torch.distributed import TCPStore
     except ImportError:  # pragma: no cover
         return None
-    if not isinstance(store, TCPStore):
-        return None
+    if not isinstance(store, TCPStore) or os.environ.get("CFC_DP_WAIT", "block") == "poll":
+        return None                   # CFC_DP_WAIT=poll: round 5's check polling (A/B)
     cache = getattr(_waiters, "clients", None)
     if cache is None:
         cache = _waiters.clients = {}

@@ -168,6 +168,9 @@ __global__ void __launch_bounds__((64 * DgShape<BM, BN, (ABL & 64) != 0>::WAVES)
   auto phys = [&](int s) { s += rot; return s >= nst ? s - nst : s; };
 
   constexpr bool NOBAR = (ABL & 128) != 0;
+  // XT: the MFMA's A operand is the W fragment, B the X fragment (probe 512: the round-5
+  // orientation, X as A, one output element per lane per row -> 4-byte epilogue stores)
+  constexpr bool XT = (ABL & 512) == 0;
   static_assert(!NOBAR || (ABL & 1), "no-barrier probe only without the X stream");
   if (w >= NW) {
     if constexpr (NOBAR) return;
@@ -257,7 +260,9 @@ __global__ void __launch_bounds__((64 * DgShape<BM, BN, (ABL & 64) != 0>::WAVES)
 #pragma unroll
         for (int i = 0; i < S::MT; ++i) {
           const uint4 a = *reinterpret_cast<const uint4*>(ximg + i * 16 * 128 + chunk);
-          acc[i] = dg_mfma(a, b[kk], acc[i]);
+          // W fragment as the A operand: the 16 x 16 output tile comes out with four consecutive
+          // W rows (output columns) of one X row per lane -> 16-byte epilogue stores
+          acc[i] = XT ? dg_mfma(b[kk], a, acc[i]) : dg_mfma(a, b[kk], acc[i]);
         }
       }
     }
@@ -290,7 +295,64 @@ __global__ void __launch_bounds__((64 * DgShape<BM, BN, (ABL & 64) != 0>::WAVES)
     }
   }
 
-  // ---- epilogue: lane holds rows m0 + 16 i + 4 (lane >> 4) + r of W row (output column) n
+  if constexpr (XT) {
+    // ---- epilogue: lane holds X row m0 + 16 i + (lane & 15) at the four consecutive W rows (output
+    // columns) n0 + 16 w + 4 (lane >> 4) + r, r = 0..3 -- one 16-byte (fp32) / 8-byte (bf16) store per
+    // lane and m-tile, 16 rows x 64 B per wave instruction (the round-5 orientation stored 4 bytes
+    // per lane: 4x the store instructions, the epilogue's store-issue tail of a small-N projection)
+    const int mr = m0 + (lane & 15);
+    const int nq = n0 + 16 * w + 4 * kq;
+    if constexpr (EPI == DG_SILU) {
+      // 8-row interleave: W rows 0-7 of each 16-row group are gate, 8-15 the matching up rows, so the
+      // lanes with kq < 2 hold gate rows and lane ^ 32 the up rows of the same output columns
+      const bool gate = kq < 2;
+      const int oc = (n0 >> 1) + 8 * w + 4 * kq;
+#pragma unroll
+      for (int i = 0; i < S::MT; ++i) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float up = __shfl_xor(acc[i][r], 32, 64);
+          const float gt = bf2f(f2bf(acc[i][r])), u = bf2f(f2bf(up));
+          o[r] = gt / (1.f + __expf(-gt)) * u;
+        }
+        const int m = mr + 16 * i;
+        if (gate && m < M)
+          *reinterpret_cast<uint2*>(out + (size_t)m * ldo + oc) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+      }
+    } else if constexpr (EPI == DG_PART_WT) {
+      // write-through (sc1) 16-byte stores through a buffer descriptor of the slab array (the
+      // guide's R1 form: the consumer kernel reads them from memory, no dirty lines at the boundary)
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)part);
+      const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)part >> 32));
+      const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(((uintptr_t)hi << 32) | lo), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < S::MT; ++i) {
+        const int m = mr + 16 * i;
+        if (m < M) {
+          const dg_u32x4 v = {__float_as_uint(acc[i][0]), __float_as_uint(acc[i][1]), __float_as_uint(acc[i][2]),
+                              __float_as_uint(acc[i][3])};
+          __builtin_amdgcn_raw_buffer_store_b128(v, prs, (int)((((size_t)ks * M + m) * N + nq) * 4), 0, 16);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < S::MT; ++i) {
+        const int m = mr + 16 * i;
+        if (m < M) {
+          if constexpr (EPI == DG_PART)
+            *reinterpret_cast<float4*>(part + ((size_t)ks * M + m) * N + nq) =
+                make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+          else
+            *reinterpret_cast<uint2*>(out + (size_t)m * ldo + nq) =
+                make_uint2(pack2bf(acc[i][0], acc[i][1]), pack2bf(acc[i][2], acc[i][3]));
+        }
+      }
+    }
+    return;
+  }
+  // ---- epilogue (round-5 orientation): lane holds rows m0 + 16 i + 4 (lane >> 4) + r of W row n
   const int n = n0 + 16 * w + (lane & 15);
   const int mb = m0 + 4 * kq;
   if constexpr (EPI == DG_SILU) {
@@ -386,13 +448,15 @@ __global__ void dgemm_pack_kernel(const uint16_t* __restrict__ W, uint16_t* __re
   reinterpret_cast<uint4*>(Wp)[i] = v;
 }
 
-int dgemm_check(int M, int N, int K, int split, int epi, int bn, const float* part, const void* out) {
+int dgemm_check(int M, int N, int K, int split, int epi, int bn, const float* part, const void* out, int ldo) {
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || split < 1 || split > K / 64) return -1;
   if (bn != 64 && bn != 96 && bn != 112 && bn != 128) return -5;
   if (N % bn) return -1;
   const bool slabs = epi == DG_PART || epi == DG_PART_WT;
   if (!slabs && split != 1) return -2;
   if ((slabs && !part) || (!slabs && !out)) return -2;
+  // the epilogue stores 4 consecutive outputs per lane: 16-byte fp32 / 8-byte bf16 aligned rows
+  if ((slabs && ((uintptr_t)part & 15)) || (!slabs && (((uintptr_t)out & 7) || ldo % 4))) return -2;
   return 0;
 }
 
@@ -408,7 +472,7 @@ CFC_API int cfc_dgemm_bm(int M) { return M <= 64 ? 64 : (M <= 128 ? 128 : 256); 
 // packed: w is in the fragment-packed layout cfc_dgemm_pack wrote for this same bn (else row-major [N][K]).
 CFC_API int cfc_dgemm(const void* x, const void* w, int M, int N, int K, int split, int epi, int bn, int packed,
                       float* part, void* out, int ldo, hipStream_t stream) {
-  if (const int e = dgemm_check(M, N, K, split, epi, bn, part, out)) return e;
+  if (const int e = dgemm_check(M, N, K, split, epi, bn, part, out, ldo)) return e;
   int rc;
   switch (cfc_dgemm_bm(M)) {
     case 64: rc = dgemm_launch<64>(x, w, M, N, K, split, epi, bn, packed, part, out, ldo, stream); break;
@@ -433,8 +497,8 @@ CFC_API int cfc_dgemm_pack(const void* w, void* wp, int N, int K, int bn, hipStr
 // (not nontemporal) cache policy on the weight stream.
 CFC_API int cfc_dgemm_ablate(const void* x, const void* w, int M, int N, int K, int split, int bn, int abl,
                              float* part, hipStream_t stream) {
-  if (M > 128 || (abl & ~511)) return -1;
-  if (const int e = dgemm_check(M, N, K, split, DG_PART, bn, part, nullptr)) return e;
+  if (M > 128 || (abl & ~1023)) return -1;
+  if (const int e = dgemm_check(M, N, K, split, DG_PART, bn, part, nullptr, N)) return e;
   int rc;
   switch (abl) {
 #define DG_ABL(A, NT) rc = dgemm_launch_pk<128, NT, A, true>(x, w, M, N, K, split, 0, bn, part, nullptr, 0, stream); break;
@@ -455,6 +519,7 @@ CFC_API int cfc_dgemm_ablate(const void* x, const void* w, int M, int N, int K, 
     case 131: DG_ABL(131, true)
     case 256: DG_ABL(256, true)
     case 259: DG_ABL(259, true)
+    case 512: DG_ABL(512, true)
 #undef DG_ABL
     default: return -3;
   }

@@ -111,4 +111,7 @@ def test_bench_node_pipeline_dp_topology_two_ranks():
     pr = d["per_rank"]
     assert [p["rank"] for p in pr] == [0, 1]
     assert all(p["embedded"] > 0 and p["summaries"] > 0 for p in pr), pr
-    assert sum(p["summaries"] for p in pr) == 2 * 2 * 3      # (warmup + 2 steps) x 2 threads x 2 ranks
+    # (warmup + 2 steps) x 2 threads x 2 ranks, + the 3 one-thread archives of the light-load probe
+    assert sum(p["summaries"] for p in pr) == 2 * 2 * 3 + 3
+    sl = d["latency_service_light"]
+    assert sl["threads"] == 3 and 0 < sl["p50_s"] <= sl["p95_s"] and d["dp_wait"] == "block"
