@@ -541,8 +541,16 @@ class DecoderModel:
 
     def _lin32(self, i: int, name: str, x: torch.Tensor) -> torch.Tensor:
         """Projection ``name`` of layer ``i`` as an fp32 [M, N] (library / CPU path): a row-parallel
-        partial that is all-reduced before its one bf16 rounding."""
-        return F.linear(x.float(), K._rowmajor(self.w.layers[i][name]).float())
+        partial that is all-reduced before its one bf16 rounding.  GPU: the library GEMM with an
+        fp32 output (bf16 operands, fp32 accumulate) or the decode GEMM's fp32 split-1 output."""
+        w = self.w.layers[i].get(name)
+        if x.is_cuda:
+            if w is not None:
+                return torch.mm(x, w.t(), out_dtype=torch.float32)
+            pw = self.w.packed[i][name] if self.w.packed is not None else None
+            if pw is not None and K.dgemm_ok(x, pw):
+                return K.dgemm(x, pw, "part", 1)[0].clone()
+        return F.linear(x.float(), K._rowmajor(w if w is not None else self.w.packed[i][name]).float())
 
     def _plin(self, i: int, name: str, x: torch.Tensor, epi: str = "bf16") -> torch.Tensor:
         """Prefill projection (``epi`` "swiglu" returns silu(gate) * up of the interleaved gate/up
@@ -575,6 +583,8 @@ class DecoderModel:
                 return K.pgemm(x, wt, "f32", variant=self.pgemm_variant)
             if dg:
                 return K.dgemm(x, pw, "part", 1)[0].clone()
+        if x.is_cuda and not isinstance(wt, K.PackedWeight):
+            return torch.mm(x, wt.t(), out_dtype=torch.float32)
         return F.linear(x.float(), K._rowmajor(wt).float())
 
     def _tp_norm(self, part: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:
