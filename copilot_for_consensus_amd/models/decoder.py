@@ -440,14 +440,18 @@ class DecoderModel:
         self.decode_gemm = mode
         # prefill GEMM (packed prompt rows): "hip" = the hand-written MFMA GEMM (csrc/kernels/pgemm.hip,
         # SwiGLU fused into gate/up, reading the packed weights), "lib" = the library GEMM + silu_mul
-        # (CFC_PREFILL_GEMM); CFC_PGEMM_VARIANT picks pgemm's K loop
+        # (CFC_PREFILL_GEMM); CFC_PGEMM_VARIANT picks pgemm's K loop (CFC_PGEMM_VARIANT_SWIGLU the
+        # gate/up projection's, CFC_PGEMM_VARIANT when unset)
         pm = os.environ.get("CFC_PREFILL_GEMM", self.PREFILL_GEMM_DEFAULT)
         if pm not in ("hip", "lib"):
             raise ValueError(f"CFC_PREFILL_GEMM={pm!r}: expected hip or lib")
         self.prefill_gemm = "lib" if self.fp8 else pm
         self.pgemm_variant = os.environ.get("CFC_PGEMM_VARIANT", self.PGEMM_VARIANT_DEFAULT)
-        if self.pgemm_variant not in K.PGEMM_VARIANTS:
-            raise ValueError(f"CFC_PGEMM_VARIANT={self.pgemm_variant!r}: expected one of {sorted(K.PGEMM_VARIANTS)}")
+        self.pgemm_variant_swiglu = os.environ.get("CFC_PGEMM_VARIANT_SWIGLU", os.environ.get(
+            "CFC_PGEMM_VARIANT", self.PGEMM_VARIANT_SWIGLU_DEFAULT))
+        for var, v in (("CFC_PGEMM_VARIANT", self.pgemm_variant), ("CFC_PGEMM_VARIANT_SWIGLU", self.pgemm_variant_swiglu)):
+            if v not in K.PGEMM_VARIANTS:
+                raise ValueError(f"{var}={v!r}: expected one of {sorted(K.PGEMM_VARIANTS)}")
         # B <= 4 decode steps on the GEMV kernel (needs the interleaved gate/up layout for SwiGLU)
         gemv_shapes = (self.cfg.hidden % 8 == 0 and (weights.heads * self.cfg.head_dim) % 8 == 0
                        and weights.ffn % 8 == 0 and self.cfg.head_dim % 2 == 0)
@@ -498,6 +502,11 @@ class DecoderModel:
     # "pps": the ping-pong K loop with the LDS-staged 16-byte-store epilogue -- bit-identical to
     # "pp", +2.0% qkv / +1.0% o / +0.3% down / -0.2% gate_up (profiles/r04_pgemm_pps.jsonl)
     PGEMM_VARIANT_DEFAULT = "pps"
+    # gate/up + SwiGLU: "ppp", the persistent ping-pong kernel (one workgroup per CU walking the
+    # tiles, the DMA stream running on across tile boundaries) -- bit-identical, 1.4-1.5 % faster
+    # on the 16k-row chunk (profiles/r06_pgemm_ppp.jsonl, r06_pgemm_k2.jsonl); on the bf16
+    # projections it loses the LDS-staged stores and is 2 % slower than "pps"
+    PGEMM_VARIANT_SWIGLU_DEFAULT = "ppp"
     PGEMM_MIN_ROWS = 256         # fewer prompt rows than one 256-row tile: the decode GEMM (packed) or the library
 
     def _packing(self) -> str | None:
@@ -563,7 +572,7 @@ class DecoderModel:
             dg = pw is not None and K.dgemm_ok(x, pw)
             if (x.shape[0] >= self.PGEMM_MIN_ROWS and K.pgemm_ok(x, wt)
                     and not (dg and self._dgemm_faster(x.shape[0], wt.shape[0], x.shape[1]))):
-                return K.pgemm(x, wt, epi, variant=self.pgemm_variant)
+                return K.pgemm(x, wt, epi, variant=self.pgemm_variant_swiglu if epi == "swiglu" else self.pgemm_variant)
             if dg:
                 return K.dgemm_swiglu(x, pw) if epi == "swiglu" else K.dgemm_linear(x, pw)
         y = self._lin(i, name, x)

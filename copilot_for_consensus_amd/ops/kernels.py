@@ -608,7 +608,7 @@ def pgemm_ok(x: torch.Tensor, w) -> bool:
             and w.shape[0] % 64 == 0 and x.shape[0] >= 1 and x.numel() * 2 < 2 ** 32 and w.numel() * 2 < 2 ** 32)
 
 
-PGEMM_VARIANTS = {"ring5": 0, "stage2": 1, "ring4": 2, "pp": 3, "w4": 4, "pps": 5}
+PGEMM_VARIANTS = {"ring5": 0, "stage2": 1, "ring4": 2, "pp": 3, "w4": 4, "pps": 5, "ppp": 6}
 # row-major W default K loop (a PackedWeight always runs the ping-pong kernel "pp")
 PGEMM_VARIANT = os.environ.get("CFC_PGEMM_VARIANT", "stage2")
 
@@ -620,10 +620,11 @@ def pgemm(x: torch.Tensor, w, epi: str = "bf16", bias: torch.Tensor | None = Non
     (gelu_erf(y + bias)); "swiglu" (8-row interleaved gate/up weights -> [M, N/2] =
     silu(gate) * up with the unfused path's bf16 rounding of gate and up).  ``w``: row-major bf16
     [N, K], or the decode GEMM's PackedWeight (one weight copy for prefill and decode: the "w4",
-    "pps" or, for any other variant, the "pp" kernel).  ``variant``: the K loop ("stage2": 2 LDS
+    "pps", "ppp" or, for any other variant, the "pp" kernel).  ``variant``: the K loop ("stage2": 2 LDS
     stages of BK=64; "ring5" / "ring4": BK=32 rings of 5 / 4 LDS slots; "pp": two wave groups
-    ping-ponging over half-tile stages; "pps": "pp" with the LDS-staged 16-byte-store epilogue, the
-    decoder's default; "w4": four 128x128 waves software-pipelined over a 4-stage ring),
+    ping-ponging over half-tile stages; "pps": "pp" with the LDS-staged 16-byte-store epilogue;
+    "ppp": "pp" made persistent (one workgroup per CU walking the tiles, the DMA stream running on
+    across tile boundaries; packed W, bf16 / SwiGLU epilogues, "pp" otherwise); "w4": four 128x128 waves software-pipelined over a 4-stage ring),
     $CFC_PGEMM_VARIANT when None."""
     mode = PGEMM_EPI[epi]
     packed = isinstance(w, PackedWeight)
@@ -646,7 +647,7 @@ def pgemm(x: torch.Tensor, w, epi: str = "bf16", bias: torch.Tensor | None = Non
         _req(bias, torch.bfloat16, "bias")
         if bias.numel() != N:
             raise ValueError(f"pgemm: bias of {bias.numel()} for N = {N}")
-    if mode == 4 and (variant or PGEMM_VARIANT) not in ("pp", "pps") and not packed:
+    if mode == 4 and (variant or PGEMM_VARIANT) not in ("pp", "pps", "ppp") and not packed:
         variant = "pp"              # the fp32 epilogue is built for the ping-pong kernel only
     if out is None:
         out = torch.empty(M, N // 2 if mode == 3 else N, dtype=torch.float32 if mode == 4 else torch.bfloat16,

@@ -656,6 +656,222 @@ __global__ void __launch_bounds__(512, 1)
   if (grp == 0) pp_barrier();   // matches group 1's stagger barrier
 }
 
+// ---- v4: the ping-pong kernel made persistent (packed W; bf16 and SwiGLU epilogues) ----------------
+// Fitting t = a + b K over K = 1k..8k at M = 16384 (scripts/probe_pgemm_k.py, profiles/
+// r06_pgemm_k.jsonl) puts a fixed ~7 us (qkv) to ~16-20 us (gate_up) on every wave of 256 tiles:
+// each new workgroup starts with an idle prologue (its first two K-tiles' DMA round trip, every CU
+// at once) and ends with a store tail nothing covers.  Here one workgroup per CU walks the tiles
+// vb = blockIdx.x, + gridDim.x, ... (the same XCD-remapped order, so the same XCD sees the same
+// tiles), and the half-tile stream simply runs on across the tile boundary: the last two K-tiles of
+// a tile issue the next tile's first ones with its DMA offsets (the slot-free analysis of the stream
+// is per position, so it holds unchanged), and the epilogue stores of tile t are issued without a
+// drain while tile t+1's first DMA is in flight.
+//   * interior wave blocks store with exactly S = 32 `global_store_dwordx2` (asm, so the count is
+//     exact; SwiGLU: both lanes of a gate/up pair store the same 8 bytes), and the two waits of the
+//     next tile's K-tile 0 keep those S stores outstanding (vmcnt(8 + S)); the next waits see them
+//     older than the DMA they retire, so the stores have one MFMA segment to drain;
+//   * an edge block (rows past M / columns past N) stores through pg_epilogue and drains (vmcnt(0)).
+constexpr int PPP_S = 32;   // epilogue store instructions per wave (8 m-tiles x 4 n-tiles)
+
+__device__ __forceinline__ void ppp_st8(void* p, uint2 v) {
+  asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(512, 1)
+    pgemm_ppp_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W, uint16_t* __restrict__ out,
+                     int M, int N, int K, int ldo, int tiles_m, int tiles_n, int wnw) {
+  static_assert(EPI == PG_BF16 || EPI == PG_SWIGLU, "bf16 / SwiGLU epilogues");
+  __shared__ __attribute__((aligned(16))) char smem[2 * PP_BUF];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = w >> 2, wc = w & 3;
+  const int nwg = tiles_m * tiles_n, G = gridDim.x;
+  const int per_group = PG_GROUP_M * tiles_n;
+  const int nk = K / PG_BK, kg_all = K / 32;
+
+  auto coords = [&](int vb, int& m0, int& n0) {
+    const int id = xcd_remap(vb, nwg);
+    const int first_m = (id / per_group) * PG_GROUP_M;
+    const int gsz = min(tiles_m - first_m, PG_GROUP_M);
+    const int in_group = id % per_group;
+    m0 = (first_m + in_group % gsz) * PG_BM;
+    n0 = (in_group / gsz) * PG_BN;
+  };
+  // DMA source offsets of one tile (as pgemm_pp_kernel, packed W)
+  auto offsets = [&](int m0, int n0, uint32_t (&vx)[2][2], uint32_t (&vw)[2][2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = 8 * (w + 8 * i) + (lane >> 3);
+        const int trow = (r >> 6) * 128 + 64 * h + (r & 63);
+        const int c = (lane & 7) ^ (r & 7);
+        vx[h][i] = ((uint32_t)min(m0 + trow, M - 1) * (uint32_t)K + 8u * c) * 2u;
+        const int f = w + 8 * i;
+        const int g = min(n0 / 16 + 8 * h + (f >> 1), N / 16 - 1);
+        vw[h][i] = (uint32_t)(((g / wnw) * kg_all + (f & 1)) * wnw + g % wnw) * 1024u + 16u * lane;
+      }
+  };
+  int vb = blockIdx.x, m0, n0, m0n = 0, n0n = 0;
+  uint32_t vx[2][2], vw[2][2], nx[2][2], nwv[2][2];
+  coords(vb, m0, n0);
+  offsets(m0, n0, vx, vw);
+  bool has_next = vb + G < nwg;
+  if (has_next) {
+    coords(vb + G, m0n, n0n);
+    offsets(m0n, n0n, nx, nwv);
+  }
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(pg_lds_t*)smem + w * 1024);
+  const size_t wstep = (size_t)2 * wnw * 512;
+  auto issue_x = [&](int kt, int slot, const uint32_t (&o)[2][2], int h) {
+    const uint16_t* src = X + (size_t)kt * PG_BK;
+    const uint32_t la = lds0 + slot * PP_BUF + h * PP_HALF;
+    pg_glds16(o[h][0], src, la);
+    pg_glds16(o[h][1], src, la + 8192);
+  };
+  auto issue_w = [&](int kt, int slot, const uint32_t (&o)[2][2], int h) {
+    const uint16_t* src = W + (size_t)kt * wstep;
+    const uint32_t la = lds0 + slot * PP_BUF + (2 + h) * PP_HALF;
+    pg_glds16(o[h][0], src, la);
+    pg_glds16(o[h][1], src, la + 8192);
+  };
+  const int xrd = (64 * grp + (lane & 15)) * 128;
+  const int sw = lane & 7;
+  auto rd_x = [&](int buf, int h, int i, int kk) {
+    return *reinterpret_cast<const bf16x8_t*>(smem + buf + h * PP_HALF + xrd + i * 16 * 128 +
+                                              (((4 * kk + (lane >> 4)) ^ sw) << 4));
+  };
+  auto rd_w = [&](int buf, int j, int kk) {
+    const int T = 4 * wc + j;
+    return *reinterpret_cast<const bf16x8_t*>(smem + buf + (2 + (T >> 3)) * PP_HALF + (2 * (T & 7) + kk) * 1024 +
+                                              16 * lane);
+  };
+
+  // prologue (nk >= 2, checked by the launcher): K-tile 0 whole, K-tile 1's X0 / W0 / W1
+  issue_x(0, 0, vx, 0);
+  issue_w(0, 0, vw, 0);
+  issue_w(0, 0, vw, 1);
+  issue_x(0, 0, vx, 1);
+  issue_x(1, 1, vx, 0);
+  issue_w(1, 1, vw, 0);
+  issue_w(1, 1, vw, 1);
+  pp_wait_barrier<8>();
+  if (grp == 1) pp_barrier();   // the stagger: group 1 runs one barrier behind group 0
+
+  f32x4_t acc[8][4];
+  bf16x8_t wf[4][2], xf[4][2];
+  int par = 0;          // LDS slot of K-tile 0 of the current tile (stream position parity)
+  bool st = false;      // S epilogue stores of the previous tile still counted in vmcnt
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      const int s0 = (kt + par) & 1, s1 = s0 ^ 1;   // slots of K-tiles kt (and kt + 2), kt + 1
+      const int buf = s0 * PP_BUF;
+      const bool more1 = kt + 1 < nk || has_next, more2 = kt + 2 < nk || has_next;
+      const bool held = st && kt == 0;
+      // ======== segment A: position kt+1's X1; fragments of K-tile kt
+      if (kt + 1 < nk) issue_x(kt + 1, s1, vx, 1);
+      else if (has_next) issue_x(kt + 1 - nk, s1, nx, 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) wf[j][kk] = rd_w(buf, j, kk);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) xf[i][kk] = rd_x(buf, 0, i, kk);
+      if (held) pp_wait_barrier<8 + PPP_S>();
+      else if (more1) pp_wait_barrier<8>();
+      else pp_wait_barrier<0>();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][kk], xf[i][kk], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      pp_barrier();
+      // ======== segment B: position kt+2's X0 / W0 / W1 (slot s0); K-tile kt's X1 fragments
+      if (kt + 2 < nk) {
+        issue_x(kt + 2, s0, vx, 0);
+        issue_w(kt + 2, s0, vw, 0);
+        issue_w(kt + 2, s0, vw, 1);
+      } else if (has_next) {
+        issue_x(kt + 2 - nk, s0, nx, 0);
+        issue_w(kt + 2 - nk, s0, nwv, 0);
+        issue_w(kt + 2 - nk, s0, nwv, 1);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) xf[i][kk] = rd_x(buf, 1, i, kk);
+      if (held) pp_wait_barrier<8 + PPP_S>();
+      else if (more2) pp_wait_barrier<8>();
+      else if (more1) pp_wait_barrier<2>();
+      else pp_wait_barrier<0>();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][kk], xf[i][kk], acc[4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      pp_barrier();
+    }
+    // ---- epilogue of this tile (no LDS: the next tile's DMA is already landing there)
+    const int mw = m0 + grp * 128, nw0 = n0 + wc * 64;
+    if (mw + 128 <= M && nw0 + 64 <= N) {
+      const int g = lane >> 4;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = mw + i * 16 + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int nb = nw0 + j * 16;
+          float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          if constexpr (EPI == PG_SWIGLU) {
+            const uint2 y = pg_swiglu4(v, g);
+            ppp_st8(out + (size_t)m * ldo + nb / 2 + 4 * (g & 1), g < 2 ? y : make_uint2(y.y, y.x));
+          } else {
+            ppp_st8(out + (size_t)m * ldo + nb + 4 * g, make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3])));
+          }
+        }
+      }
+      st = true;
+    } else {
+      pg_epilogue<EPI>(acc, nullptr, out, M, N, ldo, mw, nw0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      st = false;
+    }
+    if (!has_next) break;
+    par ^= nk & 1;
+    vb += G;
+    m0 = m0n;
+    n0 = n0n;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        vx[h][i] = nx[h][i];
+        vw[h][i] = nwv[h][i];
+      }
+    has_next = vb + G < nwg;
+    if (has_next) {
+      coords(vb + G, m0n, n0n);
+      offsets(m0n, n0n, nx, nwv);
+    }
+  }
+  if (grp == 0) pp_barrier();   // matches group 1's stagger barrier
+}
+
 
 // ---- encoder sub-layer epilogue: Y = LayerNorm(X . W^T + bias + residual) --------------------------
 // The post-LN BERT projections whose output width is the hidden size (o-proj K = hidden, FFN down
@@ -944,6 +1160,19 @@ __global__ void __launch_bounds__(256, 1)
 // profiles/r04_pgemm_w1e.jsonl)
 constexpr int PP_PF = 1 | 32;
 
+// compute units of the current device (the persistent kernel's grid), looked up once per device
+int pg_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
 template <int EPI>
 int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int M, int N, int K, int ldo,
                  int variant, int wnw, hipStream_t stream) {
@@ -954,6 +1183,16 @@ int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int 
     if (variant == 4) pgemm_w4_kernel<EPI, true><<<tm * tn, 256, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, wnw);
     else if (variant == 5)   // LDS-staged bf16 / SwiGLU epilogue
       pgemm_pp_kernel<EPI, true, PP_PF | 64><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, wnw);
+    else if (variant == 6) {   // persistent: one workgroup per CU walking the tiles
+      // (bias epilogues and K < 128 take the non-persistent kernel)
+      if constexpr (EPI == PG_BF16 || EPI == PG_SWIGLU) {
+        if (K >= 2 * PG_BK) {
+          pgemm_ppp_kernel<EPI><<<min(tm * tn, pg_cus()), 512, 0, stream>>>(xp, wp, op, M, N, K, ldo, tm, tn, wnw);
+          return (int)hipGetLastError();
+        }
+      }
+      pgemm_pp_kernel<EPI, true, PP_PF><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, wnw);
+    }
     else pgemm_pp_kernel<EPI, true, PP_PF><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, wnw);
     return (int)hipGetLastError();
   }
@@ -964,6 +1203,7 @@ int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int 
     case 3: pgemm_pp_kernel<EPI, false, PP_PF><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, 1); break;
     case 4: pgemm_w4_kernel<EPI, false><<<tm * tn, 256, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, 1); break;
     case 5: pgemm_pp_kernel<EPI, false, PP_PF | 64><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, 1); break;
+    case 6: pgemm_pp_kernel<EPI, false, PP_PF><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, 1); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
@@ -984,7 +1224,8 @@ int pgemm_launch_f32(const void* x, const void* w, void* out, int M, int N, int 
 
 // epi & 15: 0 bf16, 1 + bias, 2 + bias -> GELU, 3 SwiGLU (out [M, N/2]); epi >> 4: K-loop variant
 // for a row-major W (0 BK = 32 ring of 5 slots, 1 the 2-stage BK = 64 kernel, 2 ring of 4 slots,
-// 3 the ping-pong kernel, 5 the same with the LDS-staged bf16 / SwiGLU epilogue); ldo = output row stride.  wnw > 0: W is in the decode GEMM's
+// 3 the ping-pong kernel, 5 the same with the LDS-staged bf16 / SwiGLU epilogue, 6 the persistent
+// ping-pong kernel for a packed W -- the ping-pong kernel otherwise); ldo = output row stride.  wnw > 0: W is in the decode GEMM's
 // fragment-packed layout for bn = 16 wnw (cfc_dgemm_pack; N % (16 wnw) == 0) and runs on the
 // ping-pong kernel whatever the variant.
 CFC_API int cfc_pgemm(const void* x, const void* w, const void* bias, void* out, int M, int N, int K, int epi_v,

@@ -507,7 +507,7 @@ def test_pgemm_exact_and_strided_out(variant):
 @pytest.mark.parametrize("M,N,Kd,epi,bn", [(512, 768, 256, "bf16", 64), (300, 1152, 384, "bias", 96),
                                           (257, 1536, 448, "bias_gelu", 128), (129, 2240, 512, "swiglu", 112),
                                           (1000, 6144, 1024, "bf16", 96), (513, 1792, 2048, "swiglu", 64)])
-@pytest.mark.parametrize("variant", ["pp", "w4", "pps"])
+@pytest.mark.parametrize("variant", ["pp", "w4", "pps", "ppp"])
 def test_pgemm_packed_weight(M, N, Kd, epi, bn, variant):
     """The ping-pong prefill GEMM reading the decode GEMM's fragment-packed weight (one weight copy
     for prefill and decode) vs the fp32 reference, for every packing width bn; bit-identical to the
@@ -528,7 +528,7 @@ def test_pgemm_packed_weight(M, N, Kd, epi, bn, variant):
     assert torch.equal(y, K.pgemm(x, w, epi, bias=b, variant=variant))
 
 
-@pytest.mark.parametrize("variant", ["pp", "w4", "pps"])
+@pytest.mark.parametrize("variant", ["pp", "w4", "pps", "ppp"])
 def test_pgemm_packed_exact(variant):
     """Small-integer operands through the packed weight: bit-exact."""
     M, N, Kd = 700, 576, 320
@@ -553,6 +553,28 @@ def test_pgemm_staged_epilogue_bit_identical(epi, M):
     b = a.clone()
     K.pgemm(x, pw, epi, out=a[:, :oc], variant="pp")
     K.pgemm(x, pw, epi, out=b[:, :oc], variant="pps")
+    assert torch.equal(a, b)
+    assert bool((b[:, oc:] == 7.0).all())
+
+
+@pytest.mark.parametrize("epi,M,N,Kd", [("bf16", 8192, 8192, 256), ("bf16", 4100, 4352, 448),
+                                       ("swiglu", 4097, 7168, 320), ("swiglu", 16384, 2240, 128),
+                                       ("bf16", 300, 768, 64)])
+def test_pgemm_persistent_bit_identical(epi, M, N, Kd):
+    """The persistent ping-pong kernel (variant ppp: one workgroup per CU walking the tiles, the DMA
+    stream running on across tile boundaries, epilogue stores left in flight) writes exactly the
+    bytes of the one-tile-per-workgroup kernel (pp): up to 4 tiles per workgroup, odd K-tile
+    counts (the LDS slot parity flips per tile), edge tiles in M and N (the drained epilogue),
+    a strided output, and K = 64 (the non-persistent fallback)."""
+    x = (torch.rand(M, Kd, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(N, Kd, device=DEV) * 2 - 1) / Kd ** 0.5).bfloat16()
+    pw = K.pack_dgemm_weight(w, swiglu=epi == "swiglu")
+    oc = N // 2 if epi == "swiglu" else N
+    a = torch.full((M, oc + 64), 7.0, device=DEV).bfloat16()
+    b = a.clone()
+    K.pgemm(x, pw, epi, out=a[:, :oc], variant="pp")
+    K.pgemm(x, pw, epi, out=b[:, :oc], variant="ppp")
+    torch.cuda.synchronize()
     assert torch.equal(a, b)
     assert bool((b[:, oc:] == 7.0).all())
 
