@@ -671,18 +671,30 @@ __global__ void __launch_bounds__(512, 1)
 //     next tile's K-tile 0 keep those S stores outstanding (vmcnt(8 + S)); the next waits see them
 //     older than the DMA they retire, so the stores have one MFMA segment to drain;
 //   * an edge block (rows past M / columns past N) stores through pg_epilogue and drains (vmcnt(0)).
-constexpr int PPP_S = 32;   // epilogue store instructions per wave (8 m-tiles x 4 n-tiles)
+//   * STG (bf16 only): the interior block leaves as whole 128-byte row segments through a private
+//     4-KB LDS region per wave (the 32 KB the stream's two 64-KB buffers leave free), 32 rows at a
+//     time: 16 `global_store_dwordx4` instead of 32 8-byte stores (what "pps" does with the stream's
+//     own buffers, which stay busy here).
+constexpr int PPP_REGION = 4096;   // bytes of one wave's staging region (STG)
 
 __device__ __forceinline__ void ppp_st8(void* p, uint2 v) {
   asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
 }
 
-template <int EPI>
+// 16-byte stores stay compiler-issued: a store of more than 8 bytes needs a wait state before its
+// data registers are rewritten, which the compiler only inserts for instructions it can see (the
+// full-exec, unconditional stores below compile to exactly one global_store_dwordx4 each)
+__device__ __forceinline__ void ppp_st16(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+
+template <int EPI, bool STG = false>
 __global__ void __launch_bounds__(512, 1)
     pgemm_ppp_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W, uint16_t* __restrict__ out,
                      int M, int N, int K, int ldo, int tiles_m, int tiles_n, int wnw) {
   static_assert(EPI == PG_BF16 || EPI == PG_SWIGLU, "bf16 / SwiGLU epilogues");
-  __shared__ __attribute__((aligned(16))) char smem[2 * PP_BUF];
+  static_assert(!STG || EPI == PG_BF16, "staged stores for the bf16 epilogue");
+  // epilogue store instructions per wave in the interior (counted in the next tile's first waits)
+  constexpr int PPP_S = STG ? 16 : 32;
+  __shared__ __attribute__((aligned(16))) char smem[2 * PP_BUF + (STG ? 8 * PPP_REGION : 0)];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int grp = w >> 2, wc = w & 3;
@@ -840,9 +852,43 @@ __global__ void __launch_bounds__(512, 1)
           if constexpr (EPI == PG_SWIGLU) {
             const uint2 y = pg_swiglu4(v, g);
             ppp_st8(out + (size_t)m * ldo + nb / 2 + 4 * (g & 1), g < 2 ? y : make_uint2(y.y, y.x));
-          } else {
+          } else if constexpr (!STG) {
             ppp_st8(out + (size_t)m * ldo + nb + 4 * g, make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3])));
           }
+        }
+      }
+      if constexpr (STG) {
+        // 4 chunks of 32 rows (m-tiles 2q, 2q+1): 16-byte units XOR-swizzled by the row (8 per row),
+        // written as 8-byte halves, read back as whole units, stored as 128-byte row segments
+        char* region = smem + 2 * PP_BUF + w * PPP_REGION;
+        const int rl = lane & 15;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii) {
+            const int r = 16 * ii + rl;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const f32x4_t& a = acc[2 * q + ii][j];
+              const int unit = (2 * j + (g >> 1)) ^ (r & 7);
+              *reinterpret_cast<uint2*>(region + r * 128 + unit * 16 + (g & 1) * 8) =
+                  make_uint2(pack2bf(a[0], a[1]), pack2bf(a[2], a[3]));
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const int r = 8 * s4 + (lane >> 3), unit = lane & 7;
+            const uint4 val = *reinterpret_cast<const uint4*>(region + r * 128 + ((unit ^ (r & 7)) << 4));
+            ppp_st16(out + (size_t)(mw + 32 * q + r) * ldo + nw0 + unit * 8, val);
+          }
+          // the next chunk rewrites the region: every lane's reads of this one returned (the stores
+          // above consumed them), and the wave's LDS operations stay in order
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
       }
       st = true;
@@ -1187,7 +1233,10 @@ int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int 
       // (bias epilogues and K < 128 take the non-persistent kernel)
       if constexpr (EPI == PG_BF16 || EPI == PG_SWIGLU) {
         if (K >= 2 * PG_BK) {
-          pgemm_ppp_kernel<EPI><<<min(tm * tn, pg_cus()), 512, 0, stream>>>(xp, wp, op, M, N, K, ldo, tm, tn, wnw);
+          if constexpr (EPI == PG_BF16)
+            pgemm_ppp_kernel<EPI, true><<<min(tm * tn, pg_cus()), 512, 0, stream>>>(xp, wp, op, M, N, K, ldo, tm, tn, wnw);
+          else
+            pgemm_ppp_kernel<EPI><<<min(tm * tn, pg_cus()), 512, 0, stream>>>(xp, wp, op, M, N, K, ldo, tm, tn, wnw);
           return (int)hipGetLastError();
         }
       }
