@@ -666,8 +666,8 @@ __global__ void __launch_bounds__(512, 1)
 // a tile issue the next tile's first ones with its DMA offsets (the slot-free analysis of the stream
 // is per position, so it holds unchanged), and the epilogue stores of tile t are issued without a
 // drain while tile t+1's first DMA is in flight.
-//   * interior wave blocks store with exactly S = 32 `global_store_dwordx2` (asm, so the count is
-//     exact; SwiGLU: both lanes of a gate/up pair store the same 8 bytes), and the two waits of the
+//   * interior wave blocks store with exactly S = 32 `global_store_dwordx2` (unconditional, so the
+//     count is exact; SwiGLU: both lanes of a gate/up pair store the same 8 bytes), and the two waits of the
 //     next tile's K-tile 0 keep those S stores outstanding (vmcnt(8 + S)); the next waits see them
 //     older than the DMA they retire, so the stores have one MFMA segment to drain;
 //   * an edge block (rows past M / columns past N) stores through pg_epilogue and drains (vmcnt(0)).
@@ -677,13 +677,11 @@ __global__ void __launch_bounds__(512, 1)
 //     own buffers, which stay busy here).
 constexpr int PPP_REGION = 4096;   // bytes of one wave's staging region (STG)
 
-__device__ __forceinline__ void ppp_st8(void* p, uint2 v) {
-  asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
-}
+// The epilogue stores are compiler-issued (full exec, unconditional: exactly one global_store_dwordx2
+// / _dwordx4 each, checked in the ISA): a store of more than 8 bytes needs wait states before its
+// registers are rewritten, which the compiler inserts only for instructions it can see.
+__device__ __forceinline__ void ppp_st8(void* p, uint2 v) { *reinterpret_cast<uint2*>(p) = v; }
 
-// 16-byte stores stay compiler-issued: a store of more than 8 bytes needs a wait state before its
-// data registers are rewritten, which the compiler only inserts for instructions it can see (the
-// full-exec, unconditional stores below compile to exactly one global_store_dwordx4 each)
 __device__ __forceinline__ void ppp_st16(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
 
 template <int EPI, bool STG = false>
