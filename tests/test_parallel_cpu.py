@@ -214,7 +214,8 @@ def test_tp2_overlapped_prefill_keeps_one_shot_allreduce_epochs_in_step():
     """The overlapped TP prefill runs its all-reduces on the process group, never on the one-shot
     kernel, and every rank makes the same one-shot calls (same order, same block counts) over two
     batches of prefill + greedy decode -- so the per-block epochs of comm.hip stay equal on all
-    ranks (round-5 stall investigation: scripts/gpu_r06_first.sh read the real counters on the GPU,
+    ranks (round-5 stall investigation: scripts/tp_rehearsal.sh with CFC_TP_PREFILL_OVERLAP=force
+    CFC_AR_DEBUG=1 read the real counters on the GPU,
     errors 0 and identical epochs on both ranks after each batch, profiles/r06_tp2_overlap_gloo_1gpu.log)."""
     batches = [[[1, 5, 9, 200, 17, 33], [1] + list(range(40, 110)), [1, 2], [1] + [7] * 40],
                [[1, 3] * 20, [1, 9, 9], [1] + list(range(300, 340))]]
