@@ -499,13 +499,12 @@ class DecoderModel:
 
     PACKED_FREE_FRACTION = 0.3   # HBM left free after packing when both copies are kept
     PREFILL_GEMM_DEFAULT = "hip"
-    # "pps": the ping-pong K loop with the LDS-staged 16-byte-store epilogue -- bit-identical to
-    # "pp", +2.0% qkv / +1.0% o / +0.3% down / -0.2% gate_up (profiles/r04_pgemm_pps.jsonl)
-    PGEMM_VARIANT_DEFAULT = "pps"
-    # gate/up + SwiGLU: "ppp", the persistent ping-pong kernel (one workgroup per CU walking the
-    # tiles, the DMA stream running on across tile boundaries) -- bit-identical, 1.4-1.5 % faster
-    # on the 16k-row chunk (profiles/r06_pgemm_ppp.jsonl, r06_pgemm_k2.jsonl); on the bf16
-    # projections it loses the LDS-staged stores and is 2 % slower than "pps"
+    # "ppp": the persistent ping-pong kernel (one workgroup per CU walking the tiles, the DMA
+    # stream running on across tile boundaries, LDS-staged 16-byte stores for bf16) --
+    # bit-identical to "pp" / "pps"; against "pps" (the ping-pong K loop with the LDS-staged
+    # epilogue, round 4's default) on the 16k-row chunk: qkv -3.3 %, o -2.3 %, gate_up + SwiGLU
+    # -3.9 %, down -1.0 % (profiles/r06_pgemm_ppp_v2.jsonl, r06_pgemm_k3.jsonl)
+    PGEMM_VARIANT_DEFAULT = "ppp"
     PGEMM_VARIANT_SWIGLU_DEFAULT = "ppp"
     PGEMM_MIN_ROWS = 256         # fewer prompt rows than one 256-row tile: the decode GEMM (packed) or the library
 

@@ -28,6 +28,8 @@
 // Bounds: K % 64 == 0, N % 64 == 0, ldo % 4 == 0; M and N need not be tile multiples (rows past
 // the edge read the last valid row, their results are never stored).  X, W byte spans < 4 GiB
 // (32-bit DMA offsets).
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -670,7 +672,10 @@ __global__ void __launch_bounds__(512, 1)
 //     count is exact; SwiGLU: both lanes of a gate/up pair store the same 8 bytes), and the two waits of the
 //     next tile's K-tile 0 keep those S stores outstanding (vmcnt(8 + S)); the next waits see them
 //     older than the DMA they retire, so the stores have one MFMA segment to drain;
-//   * an edge block (rows past M / columns past N) stores through pg_epilogue and drains (vmcnt(0)).
+//   * an edge block (rows past M / columns past N) stores through pg_epilogue and drains (vmcnt(0));
+//   * the steady K-tiles (kt + 2 < nk) run a branch-free copy of the K step; only the last two run
+//     the copy whose DMA continues into the next tile (its offsets computed there), so the loop
+//     the MFMAs wait on carries no tile-boundary logic (71 scalar instructions per K-tile, "pp" 102);
 //   * STG (bf16 only): the interior block leaves as whole 128-byte row segments through a private
 //     4-KB LDS region per wave (the 32 KB the stream's two 64-KB buffers leave free), 32 rows at a
 //     time: 16 `global_store_dwordx4` instead of 32 8-byte stores (what "pps" does with the stream's
@@ -728,10 +733,7 @@ __global__ void __launch_bounds__(512, 1)
   coords(vb, m0, n0);
   offsets(m0, n0, vx, vw);
   bool has_next = vb + G < nwg;
-  if (has_next) {
-    coords(vb + G, m0n, n0n);
-    offsets(m0n, n0n, nx, nwv);
-  }
+  if (has_next) coords(vb + G, m0n, n0n);   // its DMA offsets: computed where first needed (MODE 1)
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(pg_lds_t*)smem + w * 1024);
   const size_t wstep = (size_t)2 * wnw * 512;
   auto issue_x = [&](int kt, int slot, const uint32_t (&o)[2][2], int h) {
@@ -778,14 +780,20 @@ __global__ void __launch_bounds__(512, 1)
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nk; ++kt) {
+    // K-tile kt of this tile.  TAIL false: kt + 2 < nk (this tile's DMA only, no branches); TAIL
+    // true: the last two K-tiles, whose DMA issues continue into the next tile (its K-tile 0 in
+    // segment B of kt = nk - 2 and segment A of kt = nk - 1, its K-tile 1 in segment B of nk - 1).
+    // Each wait keeps exactly the younger operations that exist in flight: A retires X1(kt) under
+    // [X0 W0 W1 (kt+1), held stores, X1 (kt+1)]; B retires X0 W0 W1 (kt+1) under [held stores,
+    // X1 (kt+1), X0 W0 W1 (kt+2)], where a position past this tile exists only with a next tile.
+    auto step = [&](int kt, auto tail_tag, bool held) {
+      constexpr bool TAIL = decltype(tail_tag)::value;
       const int s0 = (kt + par) & 1, s1 = s0 ^ 1;   // slots of K-tiles kt (and kt + 2), kt + 1
       const int buf = s0 * PP_BUF;
-      const bool more1 = kt + 1 < nk || has_next, more2 = kt + 2 < nk || has_next;
-      const bool held = st && kt == 0;
+      const bool e1 = !TAIL || kt + 1 < nk || has_next;   // position kt + 1 exists
       // ======== segment A: position kt+1's X1; fragments of K-tile kt
-      if (kt + 1 < nk) issue_x(kt + 1, s1, vx, 1);
-      else if (has_next) issue_x(kt + 1 - nk, s1, nx, 1);
+      if (!TAIL || kt + 1 < nk) issue_x(kt + 1, s1, vx, 1);
+      else if (has_next) issue_x(0, s1, nx, 1);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -794,8 +802,8 @@ __global__ void __launch_bounds__(512, 1)
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) xf[i][kk] = rd_x(buf, 0, i, kk);
-      if (held) pp_wait_barrier<8 + PPP_S>();
-      else if (more1) pp_wait_barrier<8>();
+      if (held) pp_wait_barrier<8 + PPP_S>();   // (held: kt = 0, so kt + 1 exists)
+      else if (e1) pp_wait_barrier<8>();
       else pp_wait_barrier<0>();
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -808,11 +816,13 @@ __global__ void __launch_bounds__(512, 1)
       __builtin_amdgcn_sched_barrier(0);
       pp_barrier();
       // ======== segment B: position kt+2's X0 / W0 / W1 (slot s0); K-tile kt's X1 fragments
-      if (kt + 2 < nk) {
+      if constexpr (!TAIL) {
         issue_x(kt + 2, s0, vx, 0);
         issue_w(kt + 2, s0, vw, 0);
         issue_w(kt + 2, s0, vw, 1);
       } else if (has_next) {
+        // the next tile's offsets, live from kt = nk - 2 to the tile switch only
+        if (kt == nk - 2) offsets(m0n, n0n, nx, nwv);
         issue_x(kt + 2 - nk, s0, nx, 0);
         issue_w(kt + 2 - nk, s0, nwv, 0);
         issue_w(kt + 2 - nk, s0, nwv, 1);
@@ -821,10 +831,17 @@ __global__ void __launch_bounds__(512, 1)
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) xf[i][kk] = rd_x(buf, 1, i, kk);
-      if (held) pp_wait_barrier<8 + PPP_S>();
-      else if (more2) pp_wait_barrier<8>();
-      else if (more1) pp_wait_barrier<2>();
-      else pp_wait_barrier<0>();
+      const bool e2 = !TAIL || has_next;   // position kt + 2 exists
+      if (held) {
+        if (e2) pp_wait_barrier<8 + PPP_S>();
+        else pp_wait_barrier<2 + PPP_S>();
+      } else if (e2) {
+        pp_wait_barrier<8>();
+      } else if (e1) {
+        pp_wait_barrier<2>();
+      } else {
+        pp_wait_barrier<0>();
+      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
@@ -835,7 +852,10 @@ __global__ void __launch_bounds__(512, 1)
             acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][kk], xf[i][kk], acc[4 + i][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       pp_barrier();
-    }
+    };
+    int kt = 0;
+    for (; kt < nk - 2; ++kt) step(kt, std::false_type{}, st && kt == 0);
+    for (; kt < nk; ++kt) step(kt, std::true_type{}, st && kt == 0);
     // ---- epilogue of this tile (no LDS: the next tile's DMA is already landing there)
     const int mw = m0 + grp * 128, nw0 = n0 + wc * 64;
     if (mw + 128 <= M && nw0 + 64 <= N) {
@@ -908,10 +928,7 @@ __global__ void __launch_bounds__(512, 1)
         vw[h][i] = nwv[h][i];
       }
     has_next = vb + G < nwg;
-    if (has_next) {
-      coords(vb + G, m0n, n0n);
-      offsets(m0n, n0n, nx, nwv);
-    }
+    if (has_next) coords(vb + G, m0n, n0n);
   }
   if (grp == 0) pp_barrier();   // matches group 1's stagger barrier
 }
