@@ -65,6 +65,7 @@ _KERNEL_SIGS = {
     "cfc_pgemm": [P, P, P, P, I, I, I, I, I, I, P],
     "cfc_pgemm_ln": [P, P, P, P, P, P, P, I, I, I, F, P],
     "cfc_pgemm_probe": [P, P, P, I, I, I, I, I, I, P],
+    "cfc_pgemm_ppp_probe": [P, P, P, I, I, I, I, I, I, I, P],
     "cfc_dgemm_bm": [I],
     "cfc_dgemm_pack": [P, P, I, I, I, P],
     "cfc_dgemm_ablate": [P, P, I, I, I, I, I, I, P, P],

@@ -692,7 +692,7 @@ __device__ __forceinline__ void ppp_st16(void* p, uint4 v) { *reinterpret_cast<u
 template <int EPI, bool STG = false>
 __global__ void __launch_bounds__(512, 1)
     pgemm_ppp_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W, uint16_t* __restrict__ out,
-                     int M, int N, int K, int ldo, int tiles_m, int tiles_n, int wnw) {
+                     int M, int N, int K, int ldo, int tiles_m, int tiles_n, int wnw, int gm) {
   static_assert(EPI == PG_BF16 || EPI == PG_SWIGLU, "bf16 / SwiGLU epilogues");
   static_assert(!STG || EPI == PG_BF16, "staged stores for the bf16 epilogue");
   // epilogue store instructions per wave in the interior (counted in the next tile's first waits)
@@ -702,13 +702,13 @@ __global__ void __launch_bounds__(512, 1)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int grp = w >> 2, wc = w & 3;
   const int nwg = tiles_m * tiles_n, G = gridDim.x;
-  const int per_group = PG_GROUP_M * tiles_n;
+  const int per_group = gm * tiles_n;
   const int nk = K / PG_BK, kg_all = K / 32;
 
   auto coords = [&](int vb, int& m0, int& n0) {
     const int id = xcd_remap(vb, nwg);
-    const int first_m = (id / per_group) * PG_GROUP_M;
-    const int gsz = min(tiles_m - first_m, PG_GROUP_M);
+    const int first_m = (id / per_group) * gm;
+    const int gsz = min(tiles_m - first_m, gm);
     const int in_group = id % per_group;
     m0 = (first_m + in_group % gsz) * PG_BM;
     n0 = (in_group / gsz) * PG_BN;
@@ -1234,6 +1234,23 @@ int pg_cus() {
   return cus[dev];
 }
 
+// M-tiles per N sweep of the persistent kernel's tile order.  Measured (scripts/probe_ppp_gm.py,
+// profiles/r06_ppp_gm.jsonl, gm 2 / 4 / 8 / 16): 8 is best on qkv, o and gate_up; the long-K,
+// narrow-N down projection (K = 14336, 16 N-tiles) runs 2.3 % faster at 4 (round 4 saw the same
+// on the one-tile kernel: r04_pgemm_pp_probes.jsonl)
+int ppp_group_m(int tiles_n, int K) { return (K >= 8192 && tiles_n <= 16) ? 4 : PG_GROUP_M; }
+
+template <int EPI>
+int ppp_launch(const uint16_t* xp, const uint16_t* wp, uint16_t* op, int M, int N, int K, int ldo, int wnw, int gm,
+               hipStream_t stream) {
+  const int tm = (M + PG_BM - 1) / PG_BM, tn = (N + PG_BN - 1) / PG_BN;
+  if constexpr (EPI == PG_BF16)
+    pgemm_ppp_kernel<EPI, true><<<min(tm * tn, pg_cus()), 512, 0, stream>>>(xp, wp, op, M, N, K, ldo, tm, tn, wnw, gm);
+  else
+    pgemm_ppp_kernel<EPI><<<min(tm * tn, pg_cus()), 512, 0, stream>>>(xp, wp, op, M, N, K, ldo, tm, tn, wnw, gm);
+  return (int)hipGetLastError();
+}
+
 template <int EPI>
 int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int M, int N, int K, int ldo,
                  int variant, int wnw, hipStream_t stream) {
@@ -1247,13 +1264,7 @@ int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int 
     else if (variant == 6) {   // persistent: one workgroup per CU walking the tiles
       // (bias epilogues and K < 128 take the non-persistent kernel)
       if constexpr (EPI == PG_BF16 || EPI == PG_SWIGLU) {
-        if (K >= 2 * PG_BK) {
-          if constexpr (EPI == PG_BF16)
-            pgemm_ppp_kernel<EPI, true><<<min(tm * tn, pg_cus()), 512, 0, stream>>>(xp, wp, op, M, N, K, ldo, tm, tn, wnw);
-          else
-            pgemm_ppp_kernel<EPI><<<min(tm * tn, pg_cus()), 512, 0, stream>>>(xp, wp, op, M, N, K, ldo, tm, tn, wnw);
-          return (int)hipGetLastError();
-        }
+        if (K >= 2 * PG_BK) return ppp_launch<EPI>(xp, wp, op, M, N, K, ldo, wnw, ppp_group_m(tn, K), stream);
       }
       pgemm_pp_kernel<EPI, true, PP_PF><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, wnw);
     }
@@ -1333,6 +1344,19 @@ CFC_API int cfc_pgemm_probe(const void* x, const void* w, void* out, int M, int 
   }
 #undef PP_PROBE
   return (int)hipGetLastError();
+}
+
+// Timing probe only (scripts/bench_pgemm.py --ppp-gm): the persistent kernel (packed W, bf16 or
+// SwiGLU epilogue: epi 0 / 3) with an explicit tile-order group gm (M-tiles per N sweep).
+CFC_API int cfc_pgemm_ppp_probe(const void* x, const void* w, void* out, int M, int N, int K, int epi, int ldo, int wnw,
+                                int gm, hipStream_t stream) {
+  if (M < 1 || K < 2 * PG_BK || K % 64 || N % 64 || wnw < 1 || N % (16 * wnw) || gm < 1 || (epi != 0 && epi != 3) ||
+      ldo < (epi == 3 ? N / 2 : N) || ldo % 4 || (uint64_t)M * K * 2 >= (1ull << 32) || (uint64_t)N * K * 2 >= (1ull << 32))
+    return (int)hipErrorInvalidValue;
+  const uint16_t *xp = (const uint16_t*)x, *wp = (const uint16_t*)w;
+  uint16_t* op = (uint16_t*)out;
+  return epi == 0 ? ppp_launch<PG_BF16>(xp, wp, op, M, N, K, ldo, wnw, gm, stream)
+                  : ppp_launch<PG_SWIGLU>(xp, wp, op, M, N, K, ldo, wnw, gm, stream);
 }
 
 // Y[M, N] = LayerNorm(X[M, K] . W[N, K]^T + bias + residual) * gamma + beta, N = 384 (the encoder
