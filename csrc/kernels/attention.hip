@@ -267,8 +267,8 @@ __global__ void __launch_bounds__(256, F8 ? 2 : 1) paged_decode_kernel(
         s[st][i] = v;
         tmax = fmaxf(tmax, v);
       }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    tmax = xor16_max(tmax);
+    tmax = xor32_max(tmax);
     const float mn = fmaxf(m, tmax);
     const float alpha = exp2f(m - mn);
     float rs = 0.f;
@@ -276,8 +276,8 @@ __global__ void __launch_bounds__(256, F8 ? 2 : 1) paged_decode_kernel(
     for (int st = 0; st < 2; ++st)
 #pragma unroll
       for (int i = 0; i < 4; ++i) { const float e = exp2f(s[st][i] - mn); s[st][i] = e; rs += e; }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
+    rs = xor16_sum(rs);
+    rs = xor32_sum(rs);
     l = l * alpha + rs;
     m = mn;
     const bf16x8_t pf = pack_p(s[0], s[1]);
@@ -526,8 +526,8 @@ __global__ void __launch_bounds__(512, MINW) prefill_paged_kernel(
                          fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
       tmax = fmaxf(tmax, fmaxf(fmaxf(fmaxf(sc[2][0], sc[2][1]), fmaxf(sc[2][2], sc[2][3])),
                                fmaxf(fmaxf(sc[3][0], sc[3][1]), fmaxf(sc[3][2], sc[3][3]))));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax = xor16_max(tmax);
+      tmax = xor32_max(tmax);
       // deferred rescale: keep the old max unless some row of the wave grew by > THR
       if (!__all(tmax - m <= RESCALE_THR)) {
         const float mn = fmaxf(m, tmax);
@@ -544,8 +544,8 @@ __global__ void __launch_bounds__(512, MINW) prefill_paged_kernel(
       for (int st = 0; st < 4; ++st)
 #pragma unroll
         for (int i = 0; i < 4; ++i) { const float e = exp2f(sc[st][i] - mref); sc[st][i] = e; rs += e; }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
+      rs = xor16_sum(rs);
+      rs = xor32_sum(rs);
       l += rs;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -712,7 +712,7 @@ __global__ void __launch_bounds__(256, MINW) prefill_paged_kernel_v4(
       for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
         for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sc[hf][r]);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax = xor32_max(tmax);
       if (!__all(tmax - m <= RESCALE_THR)) {
         const float mn = fmaxf(m, tmax);
         const float mref = mn == -INFINITY ? 0.f : mn;
@@ -728,7 +728,7 @@ __global__ void __launch_bounds__(256, MINW) prefill_paged_kernel_v4(
       for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
         for (int r = 0; r < 16; ++r) { const float e = exp2f(sc[hf][r] - mref); sc[hf][r] = e; rs += e; }
-      rs += __shfl_xor(rs, 32, 64);
+      rs = xor32_sum(rs);
       l += rs;
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf)

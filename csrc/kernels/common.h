@@ -46,15 +46,41 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
   return r;
 }
 
+// gfx950 lane swaps, VALU only (a __shfl_xor is an LDS-crossbar ds_bpermute: LDS issue, lgkmcnt wait):
+// v_permlane32_swap trades lanes 32-63 of a with lanes 0-31 of b; v_permlane16_swap trades the odd
+// 16-lane rows of a with the even rows of b.  With a = b = x every lane then holds its own value in one
+// result and its lane ^ 32 (^ 16) partner's in the other, so one butterfly step of a commutative op is
+// one swap + one op -- the same bits as x op __shfl_xor(x, 32 / 16).
+__device__ __forceinline__ void swap32(float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+
+__device__ __forceinline__ void swap16(float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+
+__device__ __forceinline__ float xor32_sum(float x) { float a = x, b = x; swap32(a, b); return a + b; }
+__device__ __forceinline__ float xor32_max(float x) { float a = x, b = x; swap32(a, b); return fmaxf(a, b); }
+__device__ __forceinline__ float xor16_sum(float x) { float a = x, b = x; swap16(a, b); return a + b; }
+__device__ __forceinline__ float xor16_max(float x) { float a = x, b = x; swap16(a, b); return fmaxf(a, b); }
+
 __device__ __forceinline__ float wave_sum(float v) {
+  v = xor32_sum(v);
+  v = xor16_sum(v);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 
 __device__ __forceinline__ float wave_max(float v) {
+  v = xor32_max(v);
+  v = xor16_max(v);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
 

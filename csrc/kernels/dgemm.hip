@@ -304,21 +304,22 @@ __global__ void __launch_bounds__((64 * DgShape<BM, BN, (ABL & 64) != 0>::WAVES)
     const int nq = n0 + 16 * w + 4 * kq;
     if constexpr (EPI == DG_SILU) {
       // 8-row interleave: W rows 0-7 of each 16-row group are gate, 8-15 the matching up rows, so the
-      // lanes with kq < 2 hold gate rows and lane ^ 32 the up rows of the same output columns
-      const bool gate = kq < 2;
-      const int oc = (n0 >> 1) + 8 * w + 4 * kq;
+      // lanes with kq < 2 hold gate rows and lane ^ 32 the up rows of the same output columns.  One
+      // VALU lane swap (v_permlane32_swap) of (acc[0], acc[2])
+      // hands every lane a (gate, up) pair -- column 0 in lanes kq < 2, column 2 in lanes kq >= 2 --
+      // and one of (acc[1], acc[3]) columns 1 / 3: each lane computes and stores two outputs
+      const int oc = (n0 >> 1) + 8 * w + 4 * (kq & 1) + 2 * (kq >> 1);
+      auto silu_mul = [](float gate, float up) {
+        const float gt = bf2f(f2bf(gate)), u = bf2f(f2bf(up));
+        return gt / (1.f + __expf(-gt)) * u;
+      };
 #pragma unroll
       for (int i = 0; i < S::MT; ++i) {
-        float o[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float up = __shfl_xor(acc[i][r], 32, 64);
-          const float gt = bf2f(f2bf(acc[i][r])), u = bf2f(f2bf(up));
-          o[r] = gt / (1.f + __expf(-gt)) * u;
-        }
+        float g0 = acc[i][0], u0 = acc[i][2], g1 = acc[i][1], u1 = acc[i][3];
+        swap32(g0, u0);
+        swap32(g1, u1);
         const int m = mr + 16 * i;
-        if (gate && m < M)
-          *reinterpret_cast<uint2*>(out + (size_t)m * ldo + oc) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+        if (m < M) *reinterpret_cast<uint32_t*>(out + (size_t)m * ldo + oc) = pack2bf(silu_mul(g0, u0), silu_mul(g1, u1));
       }
     } else if constexpr (EPI == DG_PART_WT) {
       // write-through (sc1) 16-byte stores through a buffer descriptor of the slab array (the

@@ -357,8 +357,8 @@ __global__ void __launch_bounds__(64 * WAVES) gemv_tile_kernel(const uint16_t* _
   for (int j = 0; j < NW; ++j)
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      acc[j][m] += __shfl_xor(acc[j][m], 16, 64);
-      acc[j][m] += __shfl_xor(acc[j][m], 32, 64);
+      acc[j][m] = xor16_sum(acc[j][m]);
+      acc[j][m] = xor32_sum(acc[j][m]);
     }
   if (q == 0) {
 #pragma unroll

@@ -18,7 +18,7 @@
 //     bank-conflict free (guide rule 21 / T2) -- the same image as the decode GEMM's X stage;
 //   * operands swapped in the MFMA (W fragment as A, X fragment as B) so each lane's accumulator
 //     holds 4 CONSECUTIVE output columns of one row: the epilogue stores 8 bytes per lane straight
-//     from registers, and SwiGLU's gate/up pairs are one lane swap (__shfl_xor 32) away;
+//     from registers, and SwiGLU's gate/up pairs are one lane swap (v_permlane32_swap) away;
 //   * blockIdx -> tile: bijective XCD remap (guide T1), then groups of 8 M-tiles sweep the N-tiles,
 //     so the ~32 workgroups resident on one XCD share X rows and W rows in that XCD's L2.
 //
@@ -60,28 +60,25 @@ __device__ __forceinline__ float pg_gelu(float v) { return 0.5f * v * (1.f + erf
 
 __device__ __forceinline__ float pg_bfr(float v) { return bf2f(f2bf(v)); }
 
-// SwiGLU of one 4-value accumulator group (16-row n-tile = 8 gate rows then 8 up rows: lane groups
-// g = 0, 1 hold gate columns, g = 2, 3 the matching up columns).  Both lane halves share the math:
-// after swapping values with lane ^ 32, lanes g < 2 compute elements 0, 1 and lanes g >= 2 elements
-// 2, 3 of the same (gate, up) pairs, and one more swap brings the packed pair back -- the exp and
-// the IEEE division are the epilogue's VALU cost, and the first version left half the lanes idle
-// (gate_up 1.32 vs 1.45 PF/s with the bf16 epilogue).  Same values and rounding as before: bf16 of
-// gate and up, silu(g) * u in fp32.  Returns (y0 y1, y2 y3) packed bf16 -- valid in lanes g < 2.
-__device__ __forceinline__ uint2 pg_swiglu4(const float (&v)[4], int g) {
-  float u[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) u[e] = __shfl_xor(v[e], 32, 64);
-  const bool lo = g < 2;
-  float y[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const float gate = lo ? v[k] : u[2 + k], up = lo ? u[k] : v[2 + k];
+// SwiGLU of one 4-value accumulator group (16-row n-tile = 8 gate rows then 8 up rows: lanes
+// g = 0, 1 hold gate columns, lanes g = 2, 3 -- lane ^ 32 -- the matching up columns).  One VALU lane
+// swap (v_permlane32_swap, common.h) of (v[0], v[2]) gives every lane a (gate, up) pair -- element 0
+// in lanes g < 2, element 2 in lanes g >= 2 -- and one of (v[1], v[3]) elements 1 / 3, so every lane
+// computes two outputs (no idle lane half, no LDS-crossbar shuffles) and returns them packed: output
+// columns pg_swiglu_col(g) + {0, 1} of the n-tile's 8.  Same values and rounding as the unfused
+// GEMM -> silu_mul path: bf16 of gate and up, silu(g) * u in fp32.
+__device__ __forceinline__ uint32_t pg_swiglu2(const float (&v)[4]) {
+  float g0 = v[0], u0 = v[2], g1 = v[1], u1 = v[3];
+  swap32(g0, u0);
+  swap32(g1, u1);
+  auto f = [](float gate, float up) {
     const float gg = pg_bfr(gate);
-    y[k] = gg * __builtin_amdgcn_rcpf(1.f + __expf(-gg)) * pg_bfr(up);
-  }
-  const uint32_t mine = pack2bf(y[0], y[1]);
-  return make_uint2(mine, (uint32_t)__shfl_xor((int)mine, 32, 64));
+    return gg * __builtin_amdgcn_rcpf(1.f + __expf(-gg)) * pg_bfr(up);
+  };
+  return pack2bf(f(g0, u0), f(g1, u1));
 }
+
+__device__ __forceinline__ int pg_swiglu_col(int g) { return 4 * (g & 1) + 2 * (g >> 1); }
 
 // Epilogue of every kernel here: lane holds rows m = mw + 16 i + (lane & 15), columns
 // n = nw + 16 j + 4 (lane >> 4) + 0..3 of the wave's 128 x 16 NJ block.
@@ -100,8 +97,8 @@ __device__ __forceinline__ void pg_epilogue(const f32x4_t (&acc)[8][NJ], const u
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if constexpr (EPI == PG_SWIGLU) {
         // bf16 rounding of g and u as the unfused GEMM -> silu_mul path
-        const uint2 y = pg_swiglu4(v, g);
-        if (g < 2 && m < M && nb < N) *reinterpret_cast<uint2*>(out + (size_t)m * ldo + nb / 2 + 4 * g) = y;
+        const uint32_t y = pg_swiglu2(v);
+        if (m < M && nb < N) *reinterpret_cast<uint32_t*>(out + (size_t)m * ldo + nb / 2 + pg_swiglu_col(g)) = y;
       } else if constexpr (EPI == PG_F32) {
         if (m < M && n < N)
           *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + (size_t)m * ldo + n) = make_float4(v[0], v[1], v[2], v[3]);
@@ -146,12 +143,9 @@ __device__ __forceinline__ void pg_epilogue_staged(const f32x4_t (&acc)[8][4], u
     for (int j = 0; j < 4; ++j) {
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if constexpr (EPI == PG_SWIGLU) {
-        const uint2 y = pg_swiglu4(v, g);
-        if (g < 2) {
-          // output columns 8 j + 4 g .. +3: unit j, half g
-          const int unit = j ^ (r & (UPR - 1));
-          *reinterpret_cast<uint2*>(region + r * RB + unit * 16 + g * 8) = y;
-        }
+        // output columns 8 j + pg_swiglu_col(g) .. +1: unit j
+        const int unit = j ^ (r & (UPR - 1));
+        *reinterpret_cast<uint32_t*>(region + r * RB + unit * 16 + 2 * pg_swiglu_col(g)) = pg_swiglu2(v);
       } else {
         // columns 16 j + 4 g .. +3: unit 2 j + (g >> 1), half g & 1
         const int unit = (2 * j + (g >> 1)) ^ (r & (UPR - 1));
@@ -668,8 +662,8 @@ __global__ void __launch_bounds__(512, 1)
 // a tile issue the next tile's first ones with its DMA offsets (the slot-free analysis of the stream
 // is per position, so it holds unchanged), and the epilogue stores of tile t are issued without a
 // drain while tile t+1's first DMA is in flight.
-//   * interior wave blocks store with exactly S = 32 `global_store_dwordx2` (unconditional, so the
-//     count is exact; SwiGLU: both lanes of a gate/up pair store the same 8 bytes), and the two waits of the
+//   * interior wave blocks store with exactly S = 32 stores (unconditional, so the count is exact:
+//     `global_store_dwordx2`, SwiGLU 4-byte `global_store_dword`), and the two waits of the
 //     next tile's K-tile 0 keep those S stores outstanding (vmcnt(8 + S)); the next waits see them
 //     older than the DMA they retire, so the stores have one MFMA segment to drain;
 //   * an edge block (rows past M / columns past N) stores through pg_epilogue and drains (vmcnt(0));
@@ -685,6 +679,8 @@ constexpr int PPP_REGION = 4096;   // bytes of one wave's staging region (STG)
 // The epilogue stores are compiler-issued (full exec, unconditional: exactly one global_store_dwordx2
 // / _dwordx4 each, checked in the ISA): a store of more than 8 bytes needs wait states before its
 // registers are rewritten, which the compiler inserts only for instructions it can see.
+__device__ __forceinline__ void ppp_st4(void* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
+
 __device__ __forceinline__ void ppp_st8(void* p, uint2 v) { *reinterpret_cast<uint2*>(p) = v; }
 
 __device__ __forceinline__ void ppp_st16(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
@@ -868,8 +864,7 @@ __global__ void __launch_bounds__(512, 1)
           const int nb = nw0 + j * 16;
           float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
           if constexpr (EPI == PG_SWIGLU) {
-            const uint2 y = pg_swiglu4(v, g);
-            ppp_st8(out + (size_t)m * ldo + nb / 2 + 4 * (g & 1), g < 2 ? y : make_uint2(y.y, y.x));
+            ppp_st4(out + (size_t)m * ldo + nb / 2 + pg_swiglu_col(g), pg_swiglu2(v));
           } else if constexpr (!STG) {
             ppp_st8(out + (size_t)m * ldo + nb + 4 * g, make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3])));
           }
@@ -1033,10 +1028,10 @@ __global__ void __launch_bounds__(512, 1)
       }
     }
     // the row's 4 column groups of this wave (lanes l, l ^ 16, l ^ 32, l ^ 48)
-    s1[i] += __shfl_xor(s1[i], 16, 64);
-    s1[i] += __shfl_xor(s1[i], 32, 64);
-    s2[i] += __shfl_xor(s2[i], 16, 64);
-    s2[i] += __shfl_xor(s2[i], 32, 64);
+    s1[i] = xor16_sum(s1[i]);
+    s1[i] = xor32_sum(s1[i]);
+    s2[i] = xor16_sum(s2[i]);
+    s2[i] = xor32_sum(s2[i]);
   }
   // the 4 waves of a row band through LDS: red[wc][row][2] (the stages are free after the barrier)
   float* red = reinterpret_cast<float*>(smem);
