@@ -690,9 +690,9 @@ __global__ void __launch_bounds__(512, 1)
     pgemm_ppp_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W, uint16_t* __restrict__ out,
                      int M, int N, int K, int ldo, int tiles_m, int tiles_n, int wnw, int gm) {
   static_assert(EPI == PG_BF16 || EPI == PG_SWIGLU, "bf16 / SwiGLU epilogues");
-  static_assert(!STG || EPI == PG_BF16, "staged stores for the bf16 epilogue");
-  // epilogue store instructions per wave in the interior (counted in the next tile's first waits)
-  constexpr int PPP_S = STG ? 16 : 32;
+  // epilogue store instructions per wave in the interior (counted in the next tile's first waits):
+  // staged bf16 16 x 16 B (128 rows x 128 B), staged SwiGLU 8 x 16 B (128 rows x 64 B), else 32
+  constexpr int PPP_S = STG ? (EPI == PG_SWIGLU ? 8 : 16) : 32;
   __shared__ __attribute__((aligned(16))) char smem[2 * PP_BUF + (STG ? 8 * PPP_REGION : 0)];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -863,14 +863,47 @@ __global__ void __launch_bounds__(512, 1)
         for (int j = 0; j < 4; ++j) {
           const int nb = nw0 + j * 16;
           float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-          if constexpr (EPI == PG_SWIGLU) {
+          if constexpr (EPI == PG_SWIGLU && !STG) {
             ppp_st4(out + (size_t)m * ldo + nb / 2 + pg_swiglu_col(g), pg_swiglu2(v));
           } else if constexpr (!STG) {
             ppp_st8(out + (size_t)m * ldo + nb + 4 * g, make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3])));
           }
         }
       }
-      if constexpr (STG) {
+      if constexpr (STG && EPI == PG_SWIGLU) {
+        // 2 chunks of 64 rows (m-tiles 4q .. 4q+3): 64-byte rows (32 output columns), 16-byte units
+        // XOR-swizzled by the row (4 per row); each lane's two outputs (4 bytes) land at column
+        // 8 j + pg_swiglu_col(g) of the chunk row, read back as whole units, stored as 64-byte row
+        // segments (8 x 16 B per wave instead of 32 x 4 B)
+        char* region = smem + 2 * PP_BUF + w * PPP_REGION;
+        const int rl = lane & 15;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) {
+            const int r = 16 * ii + rl;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const f32x4_t& a = acc[4 * q + ii][j];
+              const float v[4] = {a[0], a[1], a[2], a[3]};
+              *reinterpret_cast<uint32_t*>(region + r * 64 + ((j ^ (r & 3)) << 4) + 2 * pg_swiglu_col(g)) =
+                  pg_swiglu2(v);
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const int r = 16 * s4 + (lane >> 2), unit = lane & 3;
+            const uint4 val = *reinterpret_cast<const uint4*>(region + r * 64 + ((unit ^ (r & 3)) << 4));
+            ppp_st16(out + (size_t)(mw + 64 * q + r) * ldo + nw0 / 2 + unit * 8, val);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+      } else if constexpr (STG) {
         // 4 chunks of 32 rows (m-tiles 2q, 2q+1): 16-byte units XOR-swizzled by the row (8 per row),
         // written as 8-byte halves, read back as whole units, stored as 128-byte row segments
         char* region = smem + 2 * PP_BUF + w * PPP_REGION;
@@ -1229,6 +1262,9 @@ int pg_cus() {
   return cus[dev];
 }
 
+// LDS-staged 16-byte epilogue stores in the persistent kernel (bf16 and SwiGLU)
+constexpr bool PPP_STG = true;
+
 // M-tiles per N sweep of the persistent kernel's tile order.  Measured (scripts/probe_ppp_gm.py,
 // profiles/r06_ppp_gm.jsonl, gm 2 / 4 / 8 / 16): 8 is best on qkv, o and gate_up; the long-K,
 // narrow-N down projection (K = 14336, 16 N-tiles) runs 2.3 % faster at 4 (round 4 saw the same
@@ -1237,12 +1273,12 @@ int ppp_group_m(int tiles_n, int K) { return (K >= 8192 && tiles_n <= 16) ? 4 : 
 
 template <int EPI>
 int ppp_launch(const uint16_t* xp, const uint16_t* wp, uint16_t* op, int M, int N, int K, int ldo, int wnw, int gm,
-               hipStream_t stream) {
+               bool stg, hipStream_t stream) {
   const int tm = (M + PG_BM - 1) / PG_BM, tn = (N + PG_BN - 1) / PG_BN;
-  if constexpr (EPI == PG_BF16)
+  if (stg)
     pgemm_ppp_kernel<EPI, true><<<min(tm * tn, pg_cus()), 512, 0, stream>>>(xp, wp, op, M, N, K, ldo, tm, tn, wnw, gm);
   else
-    pgemm_ppp_kernel<EPI><<<min(tm * tn, pg_cus()), 512, 0, stream>>>(xp, wp, op, M, N, K, ldo, tm, tn, wnw, gm);
+    pgemm_ppp_kernel<EPI, false><<<min(tm * tn, pg_cus()), 512, 0, stream>>>(xp, wp, op, M, N, K, ldo, tm, tn, wnw, gm);
   return (int)hipGetLastError();
 }
 
@@ -1259,7 +1295,7 @@ int pgemm_launch(const void* x, const void* w, const void* bias, void* out, int 
     else if (variant == 6) {   // persistent: one workgroup per CU walking the tiles
       // (bias epilogues and K < 128 take the non-persistent kernel)
       if constexpr (EPI == PG_BF16 || EPI == PG_SWIGLU) {
-        if (K >= 2 * PG_BK) return ppp_launch<EPI>(xp, wp, op, M, N, K, ldo, wnw, ppp_group_m(tn, K), stream);
+        if (K >= 2 * PG_BK) return ppp_launch<EPI>(xp, wp, op, M, N, K, ldo, wnw, ppp_group_m(tn, K), PPP_STG, stream);
       }
       pgemm_pp_kernel<EPI, true, PP_PF><<<tm * tn, 512, 0, stream>>>(xp, wp, bp, op, M, N, K, ldo, tm, tn, wnw);
     }
@@ -1341,17 +1377,20 @@ CFC_API int cfc_pgemm_probe(const void* x, const void* w, void* out, int M, int 
   return (int)hipGetLastError();
 }
 
-// Timing probe only (scripts/bench_pgemm.py --ppp-gm): the persistent kernel (packed W, bf16 or
-// SwiGLU epilogue: epi 0 / 3) with an explicit tile-order group gm (M-tiles per N sweep).
-CFC_API int cfc_pgemm_ppp_probe(const void* x, const void* w, void* out, int M, int N, int K, int epi, int ldo, int wnw,
-                                int gm, hipStream_t stream) {
+// Timing probe only (scripts/probe_ppp_gm.py): the persistent kernel (packed W, bf16 or SwiGLU
+// epilogue: epi 0 / 3, +16 for register-direct instead of LDS-staged stores) with an explicit
+// tile-order group gm (M-tiles per N sweep).
+CFC_API int cfc_pgemm_ppp_probe(const void* x, const void* w, void* out, int M, int N, int K, int epi_s, int ldo,
+                                int wnw, int gm, hipStream_t stream) {
+  const int epi = epi_s & 15;
+  const bool stg = (epi_s & 16) == 0;   // +16: register-direct epilogue stores
   if (M < 1 || K < 2 * PG_BK || K % 64 || N % 64 || wnw < 1 || N % (16 * wnw) || gm < 1 || (epi != 0 && epi != 3) ||
       ldo < (epi == 3 ? N / 2 : N) || ldo % 4 || (uint64_t)M * K * 2 >= (1ull << 32) || (uint64_t)N * K * 2 >= (1ull << 32))
     return (int)hipErrorInvalidValue;
   const uint16_t *xp = (const uint16_t*)x, *wp = (const uint16_t*)w;
   uint16_t* op = (uint16_t*)out;
-  return epi == 0 ? ppp_launch<PG_BF16>(xp, wp, op, M, N, K, ldo, wnw, gm, stream)
-                  : ppp_launch<PG_SWIGLU>(xp, wp, op, M, N, K, ldo, wnw, gm, stream);
+  return epi == 0 ? ppp_launch<PG_BF16>(xp, wp, op, M, N, K, ldo, wnw, gm, stg, stream)
+                  : ppp_launch<PG_SWIGLU>(xp, wp, op, M, N, K, ldo, wnw, gm, stg, stream);
 }
 
 // Y[M, N] = LayerNorm(X[M, K] . W[N, K]^T + bias + residual) * gamma + beta, N = 384 (the encoder

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Tile-order group of the persistent prefill GEMM (cfc_pgemm_ppp_probe): M-tiles per N sweep gm,
-A/B interleaved in one process on the headline's four 16k-row shapes (random operands, hipGraph
-timing).  Prints / appends one JSON line per shape."""
+"""Persistent prefill GEMM probes (cfc_pgemm_ppp_probe), A/B interleaved in one process on the
+headline's four 16k-row shapes (random operands, hipGraph timing): the tile-order group gm (M-tiles
+per N sweep; "s<gm>" = the same with register-direct instead of LDS-staged epilogue stores).
+Usage: probe_ppp_gm.py OUT.jsonl 2,4,8,16 | 8,s8 ...   One JSON line per shape."""
 import json
 import os
 import sys
@@ -14,7 +15,7 @@ from bench_pgemm import SHAPES, timed  # noqa: E402
 
 if __name__ == "__main__":
     out = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/ppp_gm.jsonl"
-    gms = [int(g) for g in (sys.argv[2] if len(sys.argv) > 2 else "2,4,8,16").split(",")]
+    gms = (sys.argv[2] if len(sys.argv) > 2 else "2,4,8,16").split(",")
     fh = open(out, "a")
     torch.manual_seed(0)
     for name in ("qkv", "o", "gate_up", "down"):
@@ -28,8 +29,10 @@ if __name__ == "__main__":
         ref = K.pgemm(x, pw, epi, variant="ppp").clone()
 
         def run(gm):
+            direct = gm.startswith("s")
             K.check(K.kernels().cfc_pgemm_ppp_probe(x.data_ptr(), pw.data.data_ptr(), y.data_ptr(), M, N, Kd,
-                                                   3 if epi == "swiglu" else 0, oc, pw.bn // 16, gm, K._stream(x)),
+                                                   (3 if epi == "swiglu" else 0) | (16 if direct else 0), oc,
+                                                   pw.bn // 16, int(gm.lstrip("s")), K._stream(x)),
                     "cfc_pgemm_ppp_probe")
         row = {"shape": name, "M": M, "N": N, "K": Kd, "tiles_n": (N + 255) // 256}
         for gm in gms:
