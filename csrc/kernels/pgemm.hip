@@ -662,18 +662,18 @@ __global__ void __launch_bounds__(512, 1)
 // a tile issue the next tile's first ones with its DMA offsets (the slot-free analysis of the stream
 // is per position, so it holds unchanged), and the epilogue stores of tile t are issued without a
 // drain while tile t+1's first DMA is in flight.
-//   * interior wave blocks store with exactly S = 32 stores (unconditional, so the count is exact:
-//     `global_store_dwordx2`, SwiGLU 4-byte `global_store_dword`), and the two waits of the
-//     next tile's K-tile 0 keep those S stores outstanding (vmcnt(8 + S)); the next waits see them
-//     older than the DMA they retire, so the stores have one MFMA segment to drain;
+//   * interior wave blocks store with exactly S unconditional stores (16 x 16 B staged bf16, 8 x 16 B
+//     staged SwiGLU, 32 without staging; the counts are pinned by tests/test_ppp_isa.py), and the
+//     waits of the next tile's K-tile 0 keep those S stores outstanding (vmcnt(8 + S), or 2 + S in
+//     segment B of a two-K-tile last tile); the next waits see them older than the DMA they retire,
+//     so the stores have one MFMA segment to drain;
 //   * an edge block (rows past M / columns past N) stores through pg_epilogue and drains (vmcnt(0));
 //   * the steady K-tiles (kt + 2 < nk) run a branch-free copy of the K step; only the last two run
 //     the copy whose DMA continues into the next tile (its offsets computed there), so the loop
 //     the MFMAs wait on carries no tile-boundary logic (71 scalar instructions per K-tile, "pp" 102);
-//   * STG (bf16 only): the interior block leaves as whole 128-byte row segments through a private
-//     4-KB LDS region per wave (the 32 KB the stream's two 64-KB buffers leave free), 32 rows at a
-//     time: 16 `global_store_dwordx4` instead of 32 8-byte stores (what "pps" does with the stream's
-//     own buffers, which stay busy here).
+//   * STG: the interior block leaves as whole row segments (bf16 128 B, SwiGLU 64 B) through a
+//     private 4-KB LDS region per wave (the 32 KB the stream's two 64-KB buffers leave free), 32 /
+//     64 rows at a time -- what "pps" does with the stream's own buffers, which stay busy here.
 constexpr int PPP_REGION = 4096;   // bytes of one wave's staging region (STG)
 
 // The epilogue stores are compiler-issued (full exec, unconditional: exactly one global_store_dwordx2
