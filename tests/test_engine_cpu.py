@@ -261,3 +261,35 @@ def test_longest_first_slots_return_caller_order(monkeypatch):
     assert eng.lpt
     got = eng.generate(prompts, 5, ignore_eos=True)
     assert got.tokens == ref.tokens and got.prompt_lens == ref.prompt_lens == [len(p) for p in prompts]
+
+
+def test_prefill_tile_order_groups_sequences_by_l2_budget_heaviest_first_inside():
+    """The prefill attention's tile order (ops.kernels.prefill_tiles with ctx_lens): consecutive
+    sequences in groups of at most PREFILL_GROUP_CTX context tokens, groups in order, each group's
+    tiles heaviest-first (most keys under the causal mask); every tile exactly once."""
+    from copilot_for_consensus_amd.ops import kernels as K
+    lens = [2800, 2600, 3000, 700, 700, 700, 9000, 64]
+    ctx = [n + (128 if i % 2 else 0) for i, n in enumerate(lens)]     # some with cached prefix keys
+    cu = [0]
+    for n in lens:
+        cu.append(cu[-1] + n)
+    seqs, q0 = K.prefill_tiles(cu, 64, ctx)
+    want = {(s, r) for s, n in enumerate(lens) for r in range(0, n, 64)}
+    assert sorted(zip(seqs, q0)) == sorted(want)
+    # the groups the order must follow
+    groups, acc, g = [], 0, 0
+    for c in ctx:
+        if acc and acc + c > K.PREFILL_GROUP_CTX:
+            g, acc = g + 1, 0
+        acc += c
+        groups.append(g)
+    order_groups = [groups[s] for s in seqs]
+    assert order_groups == sorted(order_groups)
+    keys = [ctx[s] - lens[s] + min(r + 64, lens[s]) for s, r in zip(seqs, q0)]
+    for g in set(groups):
+        ks = [k for k, og in zip(keys, order_groups) if og == g]
+        assert ks == sorted(ks, reverse=True)
+    assert len(set(groups)) > 2          # the 6144-token budget splits this batch
+    # without ctx_lens: plain sequence order (encoder / bidirectional use)
+    s2, r2 = K.prefill_tiles(cu, 64)
+    assert list(zip(s2, r2)) == [(s, r) for s, n in enumerate(lens) for r in range(0, n, 64)]
