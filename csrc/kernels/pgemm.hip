@@ -28,6 +28,7 @@
 // Bounds: K % 64 == 0, N % 64 == 0, ldo % 4 == 0; M and N need not be tile multiples (rows past
 // the edge read the last valid row, their results are never stored).  X, W byte spans < 4 GiB
 // (32-bit DMA offsets).
+#include <atomic>
 #include <type_traits>
 
 #include "common.h"
@@ -1250,16 +1251,17 @@ __global__ void __launch_bounds__(256, 1)
 constexpr int PP_PF = 1 | 32;
 
 // compute units of the current device (the persistent kernel's grid), looked up once per device
+// (relaxed atomics: concurrent first calls store the same value)
 int pg_cus() {
-  static int cus[64] = {0};
+  static std::atomic<int> cus[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cus[dev] == 0) {
-    int n = 0;
+  int n = cus[dev].load(std::memory_order_relaxed);
+  if (n == 0) {
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
-    cus[dev] = n;
+    cus[dev].store(n, std::memory_order_relaxed);
   }
-  return cus[dev];
+  return n;
 }
 
 // LDS-staged 16-byte epilogue stores in the persistent kernel (bf16 and SwiGLU)
