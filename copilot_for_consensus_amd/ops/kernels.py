@@ -321,8 +321,9 @@ def prefill_tiles(cu_q: list[int], tile: int = PREFILL_TILE_ROWS, ctx_lens: list
     PREFILL_GROUP_CTX context tokens, the groups in order, each group's tiles heaviest-first (most
     keys to visit under the causal mask) so its long diagonal tiles start first and the grid drains
     evenly.  Against one global heaviest-first order, which interleaves every sequence's K / V in L2
-    (scripts/probe_prefill_attn_order.py, profiles/r06_prefill_attn_order.log): 6 x 2800 tokens
-    437 -> 415 us, 24 x 700 208 -> 159 us (groups of two), one 16.8k sequence unchanged."""
+    (scripts/probe_prefill_attn_order.py, profiles/r06_prefill_attn_order*.log): 24 x 700 tokens
+    208-213 -> 159-168 us, 6 x 2800 437 -> 415 us on one box and level on another, one 16.8k
+    sequence unchanged."""
     tiles = []
     group, acc = 0, 0
     for s in range(len(cu_q) - 1):
