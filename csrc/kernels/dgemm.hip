@@ -305,9 +305,9 @@ __global__ void __launch_bounds__((64 * DgShape<BM, BN, (ABL & 64) != 0>::WAVES)
     if constexpr (EPI == DG_SILU) {
       // 8-row interleave: W rows 0-7 of each 16-row group are gate, 8-15 the matching up rows, so the
       // lanes with kq < 2 hold gate rows and lane ^ 32 the up rows of the same output columns.  One
-      // VALU lane swap (v_permlane32_swap) of (acc[0], acc[2])
-      // hands every lane a (gate, up) pair -- column 0 in lanes kq < 2, column 2 in lanes kq >= 2 --
-      // and one of (acc[1], acc[3]) columns 1 / 3: each lane computes and stores two outputs
+      // VALU lane swap (v_permlane32_swap) of (acc[0], acc[2]) hands every lane a (gate, up) pair --
+      // column 0 in lanes kq < 2, column 2 in lanes kq >= 2 -- and one of (acc[1], acc[3]) columns
+      // 1 / 3: each lane computes and stores two outputs
       const int oc = (n0 >> 1) + 8 * w + 4 * (kq & 1) + 2 * (kq >> 1);
       auto silu_mul = [](float gate, float up) {
         const float gt = bf2f(f2bf(gate)), u = bf2f(f2bf(up));
