@@ -579,6 +579,25 @@ def test_pgemm_persistent_bit_identical(epi, M, N, Kd):
     assert bool((b[:, oc:] == 7.0).all())
 
 
+@pytest.mark.parametrize("epi,M,N,Kd", [("bf16", 4100, 4352, 448), ("swiglu", 2049, 7168, 256)])
+def test_pgemm_persistent_tile_orders_and_direct_stores_bit_identical(epi, M, N, Kd):
+    """The persistent kernel through its probe entry: every tile-order group gm (M-tiles per N
+    sweep) and the register-direct epilogue stores write the same bytes as the one-tile kernel."""
+    x = (torch.rand(M, Kd, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(N, Kd, device=DEV) * 2 - 1) / Kd ** 0.5).bfloat16()
+    pw = K.pack_dgemm_weight(w, swiglu=epi == "swiglu")
+    oc = N // 2 if epi == "swiglu" else N
+    ref = K.pgemm(x, pw, epi, variant="pp")
+    for gm in (1, 2, 4, 8, 16):
+        for direct in (False, True):
+            y = torch.full((M, oc), 7.0, device=DEV).bfloat16()
+            K.check(K.kernels().cfc_pgemm_ppp_probe(x.data_ptr(), pw.data.data_ptr(), y.data_ptr(), M, N, Kd,
+                                                   (3 if epi == "swiglu" else 0) | (16 if direct else 0), oc,
+                                                   pw.bn // 16, gm, K._stream(x)), "cfc_pgemm_ppp_probe")
+            torch.cuda.synchronize()
+            assert torch.equal(y, ref), (gm, direct)
+
+
 @pytest.mark.parametrize("M", [1, 2, 3, 4])
 @pytest.mark.parametrize("N,Kd,bn", [(6144, 4096, 96), (1024, 1536, 64), (2240, 512, 112), (768, 448 + 64, 128)])
 def test_gemv_packed_weight(M, N, Kd, bn):
