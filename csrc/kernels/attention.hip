@@ -169,12 +169,46 @@ __global__ void __launch_bounds__(256, F8 ? 2 : 1) paged_decode_kernel(
   // carry two k-steps of a key row (64 contiguous bytes per row per wave instruction, as the bf16
   // loads have): dq(c) = 64(c >> 1) + 16g + 8(c & 1) -- any d order works as long as Q and K agree.
   __shared__ __attribute__((aligned(16))) uint16_t sm_q[ROPE ? G : 1][D];
+  f32x4_t o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+
+  const int32_t* bt = block_tables + (size_t)b * max_blocks;
+  const size_t head_stride = (size_t)KV_BS * D;  // elements per (block, kv-head)
+
+  // K fragments: bf16 -> 8 x 16 B (st, c); fp8 -> 4 x 16 B (st, pair p of k-steps 2p, 2p+1)
+  constexpr int NK = F8 ? 4 : 8;
+  uint4 kr[NK];
+  Raw vr[8];
+  const int temporal = (NT && shared_blocks != nullptr) ? shared_blocks[0] : 0;   // blocks read cached
+  auto load_blk = [&](int bi, uint4* kk, Raw* vv) {
+    const size_t base = ((size_t)bt[bi] * Hkv + h) * head_stride;
+    if (NT && bi >= temporal) dec_load_blk<NT, F8>(kc, vc, base, col, g, kk, vv);
+    else dec_load_blk<false, F8>(kc, vc, base, col, g, kk, vv);
+  };
+  // K operand of (st, k-step c)
+  auto kop = [&](const uint4* kk, int st, int c) -> bf16x8_t {
+    if constexpr (F8) {
+      const uint4 r = kk[st * 2 + (c >> 1)];
+      return kv_operand((c & 1) ? make_uint2(r.z, r.w) : make_uint2(r.x, r.y));
+    } else {
+      return as_bf16x8(kk[st * 4 + c]);
+    }
+  };
+
+  // ROPE: every wave issues its first KV block before the prologue, so the block's HBM latency
+  // overlaps the slab reads / RoPE / cache write instead of following them -- except the wave whose
+  // first block is the one receiving the new key / value (it loads after the barrier below).
+  const int slot = ROPE ? rp.slots[b] : -1;
+  const bool owner = ROPE && slot >= 0 && blk0 <= nblk - 1 && nblk - 1 < blk1;   // holds the new key's block
+  int bi = blk0 + w;
+  const bool early = ROPE && bi < blk1 && !(owner && bi == nblk - 1);
+  if (early) load_blk(bi, kr, vr);
   if constexpr (ROPE) {
     constexpr int NV = D / 16;    // 8-vectors per half-head
     const size_t stride = (size_t)(Hq + 2 * Hkv) * D;
     const size_t row0 = (size_t)b * stride, slab = (size_t)gridDim.z * stride;
-    const int slot = rp.slots[b];
-    const bool owner = slot >= 0 && blk0 <= nblk - 1 && nblk - 1 < blk1;   // holds the new key's block
     const float* cs = rp.cos_sin + (size_t)rp.positions[b] * (D / 2) * 2;
     const int t = threadIdx.x;
     if (t < (G + 1) * NV) {
@@ -212,36 +246,7 @@ __global__ void __launch_bounds__(256, F8 ? 2 : 1) paged_decode_kernel(
     }
   }
 
-  f32x4_t o[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) o[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
-
-  const int32_t* bt = block_tables + (size_t)b * max_blocks;
-  const size_t head_stride = (size_t)KV_BS * D;  // elements per (block, kv-head)
-
-  // K fragments: bf16 -> 8 x 16 B (st, c); fp8 -> 4 x 16 B (st, pair p of k-steps 2p, 2p+1)
-  constexpr int NK = F8 ? 4 : 8;
-  uint4 kr[NK];
-  Raw vr[8];
-  const int temporal = (NT && shared_blocks != nullptr) ? shared_blocks[0] : 0;   // blocks read cached
-  auto load_blk = [&](int bi, uint4* kk, Raw* vv) {
-    const size_t base = ((size_t)bt[bi] * Hkv + h) * head_stride;
-    if (NT && bi >= temporal) dec_load_blk<NT, F8>(kc, vc, base, col, g, kk, vv);
-    else dec_load_blk<false, F8>(kc, vc, base, col, g, kk, vv);
-  };
-  // K operand of (st, k-step c)
-  auto kop = [&](const uint4* kk, int st, int c) -> bf16x8_t {
-    if constexpr (F8) {
-      const uint4 r = kk[st * 2 + (c >> 1)];
-      return kv_operand((c & 1) ? make_uint2(r.z, r.w) : make_uint2(r.x, r.y));
-    } else {
-      return as_bf16x8(kk[st * 4 + c]);
-    }
-  };
-
-  int bi = blk0 + w;
-  if (bi < blk1) load_blk(bi, kr, vr);
+  if (bi < blk1 && !early) load_blk(bi, kr, vr);
   for (; bi < blk1; bi += 4) {
     uint4 kn[NK];
     Raw vn[8];
