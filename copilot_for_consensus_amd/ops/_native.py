@@ -34,6 +34,7 @@ _KERNEL_SIGS = {
     "cfc_rope_kv_write_part": [P, I, P, P, P, P, P, P, I, I, I, I, I, ctypes.c_float, ctypes.c_float, P],
     "cfc_rope_kv_write": [P, P, P, P, P, P, P, I, I, I, I, I, P],
     "cfc_set_kv_vstore_mode": [I],
+    "cfc_set_decode_rope_probe": [I],
     "cfc_v_cache_write_runs": [P, P, I, P, I, I, I, P],
     "cfc_decode_advance_cb": [P, P, I, P, P, P, P, P, P, P, I, P, P, I, I] + [P] * 6 + [I] * 4 + [P] * 4,
     "cfc_rope_kv_write_fp8": [P, P, P, P, P, P, P, I, I, I, I, I, F, F, P],

@@ -91,6 +91,24 @@ __device__ __forceinline__ bf16x8_t kv_operand(uint2 r) { return as_bf16x8(fp8x8
 // block writes the new key / value into the cache first -- the separate rope_kv launch, its q
 // round trip through HBM and its dependency edge disappear.  Same helpers (common.h) as
 // rope_kv_kernel, so the cache bytes and q values are identical to the two-kernel path.
+// Workgroup barrier that orders LDS only: global loads and stores issued before it stay in flight
+// (__syncthreads waits for every outstanding vector-memory operation first).
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Element e (0..7) of a bf16x8 fragment replaced by the bf16 bits h (register selects, no scratch).
+__device__ __forceinline__ uint4 set_bf16(uint4 v, int e, uint32_t h) {
+  const int wi = e >> 1;
+  const bool hi = e & 1;
+  auto put = [&](uint32_t x, int i) -> uint32_t {
+    return i != wi ? x : hi ? ((x & 0xffffu) | (h << 16)) : ((x & 0xffff0000u) | h);
+  };
+  return make_uint4(put(v.x, 0), put(v.y, 1), put(v.z, 2), put(v.w, 3));
+}
+
 struct DecRope {
   const uint16_t* qkv;     // [B, (Hq + 2 Hkv) D] bf16, or nullptr with part
   const float* part;       // [split, B, (Hq + 2 Hkv) D] fp32 split-K slabs
@@ -99,6 +117,7 @@ struct DecRope {
   const int32_t* slots;    // -1: no cache write
   const float* cos_sin;
   float inv_k, inv_v;
+  int probe;               // timing ablations only (cfc_set_decode_rope_probe); 0 in production
 };
 
 // One KV block's K fragments (bf16: 8 x 16 B per lane; fp8: 4 x 16 B) and V^T fragments (8) of
@@ -197,13 +216,21 @@ __global__ void __launch_bounds__(256, F8 ? 2 : 1) paged_decode_kernel(
     }
   };
 
-  // ROPE: every wave issues its first KV block before the prologue, so the block's HBM latency
-  // overlaps the slab reads / RoPE / cache write instead of following them -- except the wave whose
-  // first block is the one receiving the new key / value (it loads after the barrier below).
+  // ROPE, bf16 cache (PATCH): the new key / value make no round trip through memory inside the
+  // step.  The prologue ropes q and k into LDS and writes the new key's cache row (256 contiguous
+  // bytes, whole lines); the wave that streams the sequence's last block patches the new slot's K
+  // and V into the fragments it loaded and stores that block's whole V^T tile back -- 64 full lines
+  // instead of 128 two-byte stores into 128 different lines per (sequence, kv head), whose
+  // partial-line write-backs cost the step far more than their bytes
+  // (scripts/probe_decode_rope_fused.py).  Every wave issues its first block before the prologue, so
+  // that block's HBM latency overlaps the slab reads.  FP8 keeps the write-then-read order: the
+  // prologue writes K and V and the wave whose first block receives them loads it after the barrier.
+  constexpr bool PATCH = ROPE && !F8;
+  __shared__ __attribute__((aligned(16))) uint16_t sm_kv[PATCH ? 2 : 1][PATCH ? D : 1];
   const int slot = ROPE ? rp.slots[b] : -1;
   const bool owner = ROPE && slot >= 0 && blk0 <= nblk - 1 && nblk - 1 < blk1;   // holds the new key's block
   int bi = blk0 + w;
-  const bool early = ROPE && bi < blk1 && !(owner && bi == nblk - 1);
+  const bool early = ROPE && bi < blk1 && (PATCH || !(owner && bi == nblk - 1));
   if (early) load_blk(bi, kr, vr);
   if constexpr (ROPE) {
     constexpr int NV = D / 16;    // 8-vectors per half-head
@@ -221,18 +248,25 @@ __global__ void __launch_bounds__(256, F8 ? 2 : 1) paged_decode_kernel(
           *reinterpret_cast<uint4*>(&sm_q[hh][c * 8]) = pa;
           *reinterpret_cast<uint4*>(&sm_q[hh][D / 2 + c * 8]) = pb;
         } else {
-          kv_write_k<F8>(const_cast<void*>(kc), slot, h, Hkv, D, c, pa, pb, rp.inv_k);
+          if (!(rp.probe & 1)) kv_write_k<F8>(const_cast<void*>(kc), slot, h, Hkv, D, c, pa, pb, rp.inv_k);
+          if constexpr (PATCH) {
+            *reinterpret_cast<uint4*>(&sm_kv[0][c * 8]) = pa;
+            *reinterpret_cast<uint4*>(&sm_kv[0][D / 2 + c * 8]) = pb;
+          }
         }
       }
     } else if (owner && t < (G + 1) * NV + D / 8) {
       const int c = t - (G + 1) * NV;
       float vf[8];
       qkv_load8(rp.qkv, rp.part, rp.split, slab, row0 + (size_t)(Hq + Hkv + h) * D + c * 8, vf);
-      kv_write_v<F8>(const_cast<void*>(vc), slot, h, Hkv, D, c, pack8(vf), rp.inv_v);
+      if constexpr (PATCH) *reinterpret_cast<uint4*>(&sm_kv[1][c * 8]) = pack8(vf);
+      else kv_write_v<F8>(const_cast<void*>(vc), slot, h, Hkv, D, c, pack8(vf), rp.inv_v);
     }
-    // workgroup-scope release / acquire: the cache stores above are visible to this workgroup's
-    // KV loads below (same CU), and sm_q to every wave
-    __syncthreads();
+    // workgroup-scope release / acquire: sm_q / sm_kv to every wave and (FP8) the cache stores above
+    // to this workgroup's KV loads below (same CU).  PATCH reads nothing back from memory, so its
+    // barrier orders LDS only: the early KV loads and the key-row store stay in flight across it.
+    if constexpr (PATCH) lds_barrier();
+    else __syncthreads();
   }
   bf16x8_t qf[4];
   {
@@ -252,6 +286,39 @@ __global__ void __launch_bounds__(256, F8 ? 2 : 1) paged_decode_kernel(
     Raw vn[8];
     const bool more = bi + 4 < blk1;
     if (more) load_blk(bi + 4, kn, vn);
+    if constexpr (PATCH) {
+      if (owner && bi == nblk - 1) {
+        const int sn = slot % KV_BS;
+        // K row sn: lanes col == sn % 16 of fragment half st = sn / 16 hold its d-chunks 32c + 8g
+        if (col == (sn & 15)) {
+#pragma unroll
+          for (int st = 0; st < 2; ++st)
+            if (st == (sn >> 4))
+#pragma unroll
+              for (int c = 0; c < 4; ++c) kr[st * 4 + c] = *reinterpret_cast<const uint4*>(&sm_kv[0][32 * c + 8 * g]);
+        }
+        // V^T column of key sn: stored at slot position ps = kv_v_slot(sn), i.e. element ps % 8 of
+        // the lanes g == ps / 8 (rows d = 16 dt + col)
+        const int ps = kv_v_slot(sn);
+        if (g == (ps >> 3)) {
+#pragma unroll
+          for (int dt = 0; dt < 8; ++dt) vr[dt] = set_bf16(vr[dt], ps & 7, sm_kv[1][16 * dt + col]);
+        }
+        // the block's whole V^T tile back to the cache: every lane one 16-byte piece per dt
+        uint16_t* vt = reinterpret_cast<uint16_t*>(const_cast<void*>(vc)) + ((size_t)bt[bi] * Hkv + h) * head_stride;
+        if (rp.probe & 4) {
+#pragma unroll
+          for (int dt = 0; dt < 8; ++dt) {
+            const uint4 v = vr[dt];
+            __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w},
+                                        reinterpret_cast<u32x4_t*>(vt + (16 * dt + col) * KV_BS + 8 * g));
+          }
+        } else if (!(rp.probe & 2)) {
+#pragma unroll
+          for (int dt = 0; dt < 8; ++dt) *reinterpret_cast<uint4*>(vt + (16 * dt + col) * KV_BS + 8 * g) = vr[dt];
+        }
+      }
+    }
 
     f32x4_t s[2];
 #pragma unroll
@@ -306,7 +373,10 @@ __global__ void __launch_bounds__(256, F8 ? 2 : 1) paged_decode_kernel(
 #pragma unroll
     for (int i = 0; i < 4; ++i) sm_o[w][16 * dt + 4 * g + i][col] = o[dt][i];
   if (g == 0) { sm_m[w][col] = m; sm_l[w][col] = l; }
-  __syncthreads();
+  // PATCH: the V^T tile store of the last block stays in flight (a full barrier would wait for its
+  // write acknowledgement here, once per workgroup, behind the chip-wide KV read stream)
+  if constexpr (PATCH) lds_barrier();
+  else __syncthreads();
 
   for (int idx = threadIdx.x; idx < G * D; idx += 256) {
     const int qh = idx / D, d = idx % D;
@@ -1338,6 +1408,15 @@ CFC_API int cfc_paged_decode_attention(const void* q, const void* k_cache, const
                                     shared_blocks);
 }
 
+// Timing ablations of the fused decode RoPE (scripts/probe_decode_rope_fused.py): bit 1 skips the new
+// key's cache row, bit 2 the V^T tile store, bit 4 makes that store nontemporal.  Results are wrong
+// with bits 1 / 2 set; production never sets it.
+static int g_dec_rope_probe = 0;
+CFC_API int cfc_set_decode_rope_probe(int bits) {
+  g_dec_rope_probe = bits;
+  return 0;
+}
+
 // Decode attention with the step's RoPE + KV write in its prologue (DecRope).  qkv [B, (Hq+2Hkv)*128]
 // bf16 OR part [split, B, (Hq+2Hkv)*128] fp32 slabs (exactly one non-null); positions / slots [B];
 // fp8 != 0: e4m3 caches (K / k_scale, V / v_scale).  Writes out [B, Hq, 128]; q never leaves the chip.
@@ -1348,7 +1427,8 @@ CFC_API int cfc_paged_decode_rope_attention(const void* qkv, const float* part, 
                                             int window, int fp8, float k_scale, float v_scale, float* part_o,
                                             float* part_ml, void* out, const int32_t* shared_blocks,
                                             hipStream_t stream) {
-  const DecRope rp{(const uint16_t*)qkv, part, split, positions, slots, cos_sin, 1.f / k_scale, 1.f / v_scale};
+  const DecRope rp{(const uint16_t*)qkv, part, split, positions, slots, cos_sin, 1.f / k_scale, 1.f / v_scale,
+                   g_dec_rope_probe};
   if (fp8)
     return launch_paged_decode<true>(nullptr, k_cache, v_cache, block_tables, ctx_lens, B, Hq, Hkv, head_dim,
                                      max_blocks, part_blocks, P, scale * k_scale, window, v_scale, part_o, part_ml,

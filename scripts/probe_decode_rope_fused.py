@@ -105,6 +105,13 @@ def main():
         K.rope_kv_write(qkv_b, pos, slots, cs, kc, vc, Hq, Hkv, D, q_out=q_b, runs=no_runs)
         K.paged_decode_attention(q_b, kc, vc, bt_d, ctx_d, scale, out=out_u, part_blocks=-1)
 
+    def probe_arm(bits):
+        def run():
+            K.kernels().cfc_set_decode_rope_probe(bits)
+            fused()
+            K.kernels().cfc_set_decode_rope_probe(0)
+        return run
+
     def attn_only():
         K.paged_decode_attention(q_fixed, kc, vc, bt_d, ctx_d, scale, out=out_u, part_blocks=-1)
 
@@ -125,7 +132,9 @@ def main():
     base = graph_us(gemm)
     base_b = graph_us(gemm_b)
     arms = [("unfused", unfused), ("fused", fused), ("unfused_noKV", unfused_nokv), ("fused_noKV", fused_nokv),
-            ("attention_only", attn_only), ("unfused_bf16", unfused_bf16), ("unfused_bf16_noV", unfused_bf16_noV)]
+            ("attention_only", attn_only), ("unfused_bf16", unfused_bf16), ("unfused_bf16_noV", unfused_bf16_noV),
+            ("fused_noKrow", probe_arm(1)), ("fused_noVtile", probe_arm(2)), ("fused_noKrow_noVtile", probe_arm(3)),
+            ("fused_ntVtile", probe_arm(4))]
     only = sys.argv[1:]
     for rnd in range(2):
         for name, fn in arms:
