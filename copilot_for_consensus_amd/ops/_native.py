@@ -8,6 +8,7 @@ PyTorch fallback.  ``build()`` in ``__graft_entry__`` produces both libraries.
 from __future__ import annotations
 
 import ctypes
+from pathlib import Path
 import os
 import threading
 from ctypes import c_float, c_int, c_int64, c_uint32, c_void_p
@@ -141,11 +142,13 @@ def kernels():
     if _kernels is None:
         with _lock:
             if _kernels is None:
-                if not KERNELS_LIB.exists():
+                # CFC_KERNELS_LIB: another build of the library (A/B of two kernel versions on one box)
+                lib = Path(os.environ.get("CFC_KERNELS_LIB") or KERNELS_LIB)
+                if not lib.exists():
                     raise RuntimeError(
-                        f"native HIP kernels not built: {KERNELS_LIB} is missing. Run "
+                        f"native HIP kernels not built: {lib} is missing. Run "
                         "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950).")
-                _kernels = _bind(ctypes.CDLL(str(KERNELS_LIB), mode=os.RTLD_LOCAL), _KERNEL_SIGS)
+                _kernels = _bind(ctypes.CDLL(str(lib), mode=os.RTLD_LOCAL), _KERNEL_SIGS)
     return _kernels
 
 

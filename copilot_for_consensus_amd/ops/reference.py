@@ -25,6 +25,14 @@ def v_slot_perm(device=None) -> torch.Tensor:
     return 8 * g + j
 
 
+def v_groups(v_cache: torch.Tensor) -> torch.Tensor:
+    """View of a V cache [nblk, Hkv, D, 32] as its storage order [nblk, Hkv, 4, D, 8]: slot position
+    p of row d lives at [..., p // 8, d, p % 8] (common.h kv_v_off) -- the 8 positions of one P.V
+    fragment stay 16 contiguous bytes, and one token's column spans 16 cache lines instead of 64."""
+    nb, h, d, s = v_cache.shape
+    return v_cache.view(nb, h, s // 8, d, 8)
+
+
 def rmsnorm(x, w, eps, residual=None):
     """Returns (out, new_residual).  With residual: residual <- x + residual; out = norm(residual)."""
     if residual is not None:
@@ -102,7 +110,8 @@ def rope_kv_write(qkv, positions, slots, cos_sin, k_cache, v_cache, Hq, Hkv, D, 
             continue
         blk, off = divmod(s, KV_BLOCK)
         k_cache[blk, :, off, :] = _to_cache(k[t], k_cache, k_scale)
-        v_cache[blk, :, :, int(perm[off])] = _to_cache(v[t], v_cache, v_scale)
+        p = int(perm[off])
+        v_groups(v_cache)[blk, :, p >> 3, :, p & 7] = _to_cache(v[t], v_cache, v_scale)
     return q
 
 
@@ -113,7 +122,8 @@ def gather_kv(k_cache, v_cache, block_table, n, k_scale=1.0, v_scale=1.0):
     nb = (n + KV_BLOCK - 1) // KV_BLOCK
     blocks = block_table[:nb].long()
     k = k_cache[blocks].permute(0, 2, 1, 3).reshape(nb * KV_BLOCK, k_cache.shape[1], k_cache.shape[3])
-    v = v_cache[blocks][..., perm].permute(0, 3, 1, 2).reshape(nb * KV_BLOCK, v_cache.shape[1], v_cache.shape[2])
+    vt = v_groups(v_cache)[blocks].permute(0, 1, 3, 2, 4).reshape(nb, v_cache.shape[1], v_cache.shape[2], KV_BLOCK)
+    v = vt[..., perm].permute(0, 3, 1, 2).reshape(nb * KV_BLOCK, v_cache.shape[1], v_cache.shape[2])
     if k_cache.dtype == torch.float8_e4m3fn:
         k, v = k.float() * k_scale, v.float() * v_scale
     return k[:n], v[:n]

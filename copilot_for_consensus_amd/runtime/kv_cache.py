@@ -74,7 +74,8 @@ class BlockPool:
 
 
 class PagedKVCache:
-    """K [layers][blocks, kv_heads, 32, D] and V^T [layers][blocks, kv_heads, D, 32] (slot-permuted).
+    """K [layers][blocks, kv_heads, 32, D] and V^T [layers][blocks, kv_heads, D, 32] (slot-permuted,
+    stored as [4 slot groups][D][8] per block and head: ops.reference.v_groups).
 
     ``dtype`` bf16 (default) or ``torch.float8_e4m3fn``: the FP8 cache halves the bytes the decode
     attention streams; it holds K / ``k_scale`` and V / ``v_scale`` (clamped to +-448) and the

@@ -15,10 +15,12 @@
 //     online-softmax max/sum are lane-local plus two xor-shuffles, and the S^T accumulator is
 //     already the P^T B-operand of the next MFMA (guide §3 "accumulator as the next operand").
 //   * KV cache block = 32 tokens = one MFMA k-step.  K is stored [blk][kvh][32][D] (row = key),
-//     V is stored TRANSPOSED [blk][kvh][D][32] with the keys of each block permuted so that slot
-//     8g+j holds key perm(g,j) = (j<4 ? 4g+j : 16+4g+j-4).  That is exactly the key order a lane
-//     holds in its S^T registers, so the V^T A-operand is one contiguous 16-byte load per lane
-//     (no LDS transpose, no ds_read_tr needed) in both decode (straight from HBM) and prefill.
+//     V is stored TRANSPOSED in slot groups, [blk][kvh][4 groups g][D][8] (common.h kv_v_off), with
+//     the keys of each block permuted so that slot 8g+j holds key perm(g,j) = (j<4 ? 4g+j : 16+4g+j-4).
+//     That is exactly the key order a lane holds in its S^T registers, so the V^T A-operand is one
+//     contiguous 16-byte load per lane (no LDS transpose, no ds_read_tr needed) in both decode
+//     (straight from HBM) and prefill; and one decode token's V column dirties 16 cache lines
+//     ([D][32] rows: 64), which is what its write costs the step.
 //   * LDS tiles are XOR-swizzled for conflict-free ds_read_b128 (guide §5.5 T2); the swizzles
 //     were derived against the gfx950 ds_read_b128 lane groups {0-3,12-15,20-27}, ...
 #include "common.h"
@@ -135,7 +137,7 @@ __device__ __forceinline__ void dec_load_blk(const void* kc, const void* vc, siz
         kk[st * 2 + pp] = kv_load<NT>(reinterpret_cast<const uint16_t*>(kb + (16 * st + col) * D + 64 * pp + 16 * g));
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt)
-      vv[dt] = kv_load8<NT>(reinterpret_cast<const uint8_t*>(vc) + base + (16 * dt + col) * KV_BS + 8 * g);
+      vv[dt] = kv_load8<NT>(reinterpret_cast<const uint8_t*>(vc) + base + kv_v_off(16 * dt + col, 8 * g, D));
   } else {
 #pragma unroll
     for (int st = 0; st < 2; ++st)
@@ -144,7 +146,7 @@ __device__ __forceinline__ void dec_load_blk(const void* kc, const void* vc, siz
         kk[st * 4 + c] = kv_load<NT>(reinterpret_cast<const uint16_t*>(kc) + base + (16 * st + col) * D + 32 * c + 8 * g);
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt)
-      vv[dt] = kv_load<NT>(reinterpret_cast<const uint16_t*>(vc) + base + (16 * dt + col) * KV_BS + 8 * g);
+      vv[dt] = kv_load<NT>(reinterpret_cast<const uint16_t*>(vc) + base + kv_v_off(16 * dt + col, 8 * g, D));
   }
 }
 
@@ -219,12 +221,11 @@ __global__ void __launch_bounds__(256, F8 ? 2 : 1) paged_decode_kernel(
   // ROPE, bf16 cache (PATCH): the new key / value make no round trip through memory inside the
   // step.  The prologue ropes q and k into LDS and writes the new key's cache row (256 contiguous
   // bytes, whole lines); the wave that streams the sequence's last block patches the new slot's K
-  // and V into the fragments it loaded and stores that block's whole V^T tile back -- 64 full lines
-  // instead of 128 two-byte stores into 128 different lines per (sequence, kv head), whose
-  // partial-line write-backs cost the step far more than their bytes
-  // (scripts/probe_decode_rope_fused.py).  Every wave issues its first block before the prologue, so
-  // that block's HBM latency overlaps the slab reads.  FP8 keeps the write-then-read order: the
-  // prologue writes K and V and the wave whose first block receives them loads it after the barrier.
+  // and V into the fragments it loaded and stores the V^T slot group holding the new key back (16
+  // full lines; the write costs the step by lines dirtied, scripts/probe_decode_rope_fused.py).
+  // Every wave issues its first block before the prologue, so that block's HBM latency overlaps
+  // the slab reads.  FP8 keeps the write-then-read order: the prologue writes K and V and the wave
+  // whose first block receives them loads it after the barrier.
   constexpr bool PATCH = ROPE && !F8;
   __shared__ __attribute__((aligned(16))) uint16_t sm_kv[PATCH ? 2 : 1][PATCH ? D : 1];
   const int slot = ROPE ? rp.slots[b] : -1;
@@ -304,18 +305,20 @@ __global__ void __launch_bounds__(256, F8 ? 2 : 1) paged_decode_kernel(
 #pragma unroll
           for (int dt = 0; dt < 8; ++dt) vr[dt] = set_bf16(vr[dt], ps & 7, sm_kv[1][16 * dt + col]);
         }
-        // the block's whole V^T tile back to the cache: every lane one 16-byte piece per dt
+        // the new key's slot group of the V^T tile back to the cache: the lanes g == ps / 8 store
+        // their 8 x 16-byte pieces, the group's 16 full cache lines
         uint16_t* vt = reinterpret_cast<uint16_t*>(const_cast<void*>(vc)) + ((size_t)bt[bi] * Hkv + h) * head_stride;
-        if (rp.probe & 4) {
+        if (g != (ps >> 3)) {
+        } else if (rp.probe & 4) {
 #pragma unroll
           for (int dt = 0; dt < 8; ++dt) {
             const uint4 v = vr[dt];
             __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w},
-                                        reinterpret_cast<u32x4_t*>(vt + (16 * dt + col) * KV_BS + 8 * g));
+                                        reinterpret_cast<u32x4_t*>(vt + kv_v_off(16 * dt + col, 8 * g, D)));
           }
         } else if (!(rp.probe & 2)) {
 #pragma unroll
-          for (int dt = 0; dt < 8; ++dt) *reinterpret_cast<uint4*>(vt + (16 * dt + col) * KV_BS + 8 * g) = vr[dt];
+          for (int dt = 0; dt < 8; ++dt) *reinterpret_cast<uint4*>(vt + kv_v_off(16 * dt + col, 8 * g, D)) = vr[dt];
         }
       }
     }
@@ -547,7 +550,7 @@ __global__ void __launch_bounds__(512, MINW) prefill_paged_kernel(
         const int key0 = kt * PF_KT + bi * KV_BS;
         if (key0 < kend) {
           const int blk = bt[key0 / KV_BS];
-          vst[i] = *reinterpret_cast<const uint4*>(vc + (((size_t)blk * Hkv + hk) * D + d) * KV_BS + ch * 8);
+          vst[i] = *reinterpret_cast<const uint4*>(vc + ((size_t)blk * Hkv + hk) * D * KV_BS + kv_v_off(d, 8 * ch, D));
         } else {
           vst[i] = make_uint4(0, 0, 0, 0);
         }
@@ -725,7 +728,7 @@ __global__ void __launch_bounds__(256, MINW) prefill_paged_kernel_v4(
         const int bi = id >> 9, d = (id >> 2) & 127, g = id & 3;
         const int key0 = kt * PF_KT + bi * KV_BS;
         vst[i] = key0 < kend ? *reinterpret_cast<const uint4*>(
-                                   vc + (((size_t)bt[key0 / KV_BS] * Hkv + hk) * D + d) * KV_BS + g * 8)
+                                   vc + ((size_t)bt[key0 / KV_BS] * Hkv + hk) * D * KV_BS + kv_v_off(d, 8 * g, D))
                              : make_uint4(0, 0, 0, 0);
       }
     }
@@ -980,16 +983,18 @@ __global__ void __launch_bounds__(512, 2) prefill_gqa_kernel(
       const int key = (e >> 3) + 32 * b, ch = 2 * (e & 7);          // 16 d values = bf16 chunks ch, ch+1
       *reinterpret_cast<uint4*>(kb + k_lds_off(key, ch)) = fp8x8_to_bf16x8(make_uint2(ks0.x, ks0.y));
       *reinterpret_cast<uint4*>(kb + k_lds_off(key, ch + 1)) = fp8x8_to_bf16x8(make_uint2(ks0.z, ks0.w));
-      const int d = e >> 1, c = 4 * b + 2 * (e & 1);                  // 16 slots = cache chunks c, c+1
+      // 16 bytes of the [4][D][8] tile = slot chunk e >> 6 of rows d, d + 1
+      const int d = 2 * (e & 63), c = 4 * b + (e >> 6);
       const bool z = b ? z1 : z0;
       const uint4 zero = make_uint4(0, 0, 0, 0);
       *reinterpret_cast<uint4*>(vb + v5_off(d, c)) = z ? zero : fp8x8_to_bf16x8(make_uint2(vs0.x, vs0.y));
-      *reinterpret_cast<uint4*>(vb + v5_off(d, c + 1)) = z ? zero : fp8x8_to_bf16x8(make_uint2(vs0.z, vs0.w));
+      *reinterpret_cast<uint4*>(vb + v5_off(d + 1, c)) = z ? zero : fp8x8_to_bf16x8(make_uint2(vs0.z, vs0.w));
     } else {
       *reinterpret_cast<uint4*>(kb + k_lds_off(tid >> 4, tid & 15)) = ks0;
       *reinterpret_cast<uint4*>(kb + k_lds_off((tid >> 4) + 32, tid & 15)) = ks1;
-      *reinterpret_cast<uint4*>(vb + v5_off((tid >> 2) & 127, tid & 3)) = z0 ? make_uint4(0, 0, 0, 0) : vs0;
-      *reinterpret_cast<uint4*>(vb + v5_off((tid >> 2) & 127, 4 + (tid & 3))) = z1 ? make_uint4(0, 0, 0, 0) : vs1;
+      // element 8 tid of the [4][D][8] tile = slot chunk tid >> 7 of row tid & 127
+      *reinterpret_cast<uint4*>(vb + v5_off(tid & 127, tid >> 7)) = z0 ? make_uint4(0, 0, 0, 0) : vs0;
+      *reinterpret_cast<uint4*>(vb + v5_off(tid & 127, 4 + (tid >> 7))) = z1 ? make_uint4(0, 0, 0, 0) : vs1;
     }
   };
 
@@ -1409,7 +1414,7 @@ CFC_API int cfc_paged_decode_attention(const void* q, const void* k_cache, const
 }
 
 // Timing ablations of the fused decode RoPE (scripts/probe_decode_rope_fused.py): bit 1 skips the new
-// key's cache row, bit 2 the V^T tile store, bit 4 makes that store nontemporal.  Results are wrong
+// key's cache row, bit 2 the V^T slot-group store, bit 4 makes that store nontemporal.  Results are wrong
 // with bits 1 / 2 set; production never sets it.
 static int g_dec_rope_probe = 0;
 CFC_API int cfc_set_decode_rope_probe(int bits) {

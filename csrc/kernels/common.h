@@ -149,14 +149,22 @@ __device__ __forceinline__ uint4 fp8x8_to_bf16x8(uint2 v) {
 // ---------------------------------------------------------------------------------------------
 // Decode RoPE + paged KV write, shared by rope_kv_kernel (elementwise.hip) and the decode attention
 // kernel that does it in its prologue (attention.hip), so both write bit-identical caches.
-// Cache layouts (attention.hip header): K [blk][kvh][32][D]; V transposed [blk][kvh][D][32] with
-// key (16 hi + 4 g + j) of a block at slot 8 g + 4 hi + j.
+// Cache layouts (attention.hip header): K [blk][kvh][32][D]; V transposed [blk][kvh][4][D][8] (slot
+// position p = 8 g' + j' of row d at kv_v_off(d, p)) with key (16 hi + 4 g + j) of a block at slot
+// position 8 g + 4 hi + j.
 constexpr int CFC_KV_BS = 32;
 
 __device__ __forceinline__ int kv_v_slot(int key_in_block) {
   const int hi = key_in_block >> 4, g = (key_in_block >> 2) & 3, j = (key_in_block & 3) + 4 * hi;
   return 8 * g + j;
 }
+
+// Element offset of (d, slot position p) inside one (block, kv head) V tile, stored as
+// [4 slot groups][D][8 slots]: the 8 positions 8g..8g+7 of one d (one P.V MFMA fragment) are 16
+// contiguous bytes, and one token's column touches D * 2 B / 128 B = 16 cache lines (bf16, D = 128)
+// instead of 64 in a [D][32] tile -- the decode step's V write costs by lines dirtied
+// (profiles/ROOFLINE.md, round 6).
+__device__ __forceinline__ int kv_v_off(int d, int p, int D) { return (p >> 3) * (D * 8) + d * 8 + (p & 7); }
 
 // 8 consecutive qkv values of token row element offset `off`: from the bf16 qkv, or summed from
 // `split` fp32 split-K slabs of the decode GEMM (slab stride `slab` elements) and rounded to bf16
@@ -292,25 +300,25 @@ template <bool F8, int VM = 0>
 __device__ __forceinline__ void kv_write_v(void* v_cache, int slot, int kh, int Hkv, int D, int c, uint4 val,
                                            float inv_v) {
   const int blk = slot / CFC_KV_BS, off = slot % CFC_KV_BS;
-  const size_t e0 = (((size_t)blk * Hkv + kh) * D + c * 8) * CFC_KV_BS + kv_v_slot(off);
+  const size_t e0 = ((size_t)blk * Hkv + kh) * D * CFC_KV_BS + kv_v_off(c * 8, kv_v_slot(off), D);
   const uint16_t* e = reinterpret_cast<const uint16_t*>(&val);
   if constexpr (F8) {
     uint8_t* dst = reinterpret_cast<uint8_t*>(v_cache) + e0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const uint8_t b = f2fp8(bf2f(e[j]) * inv_v);
-      if constexpr (VM == 1) __hip_atomic_store(dst + j * CFC_KV_BS, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else if constexpr (VM == 2) __builtin_nontemporal_store(b, dst + j * CFC_KV_BS);
-      else dst[j * CFC_KV_BS] = b;
+      if constexpr (VM == 1) __hip_atomic_store(dst + j * 8, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else if constexpr (VM == 2) __builtin_nontemporal_store(b, dst + j * 8);
+      else dst[j * 8] = b;
     }
   } else {
     uint16_t* dst = reinterpret_cast<uint16_t*>(v_cache) + e0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const uint16_t h = e[j];
-      if constexpr (VM == 1) __hip_atomic_store(dst + j * CFC_KV_BS, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else if constexpr (VM == 2) __builtin_nontemporal_store(h, dst + j * CFC_KV_BS);
-      else dst[j * CFC_KV_BS] = h;
+      if constexpr (VM == 1) __hip_atomic_store(dst + j * 8, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else if constexpr (VM == 2) __builtin_nontemporal_store(h, dst + j * 8);
+      else dst[j * 8] = h;
     }
   }
 }

@@ -82,7 +82,7 @@ __global__ void __launch_bounds__(256) v_cache_runs_kernel(const uint16_t* __res
         *reinterpret_cast<const uint4*>(qkv + (size_t)(t0 + j) * stride + (size_t)(Hq + Hkv + kh) * D + c * 8);
   }
   __syncthreads();
-  const size_t e0 = ((size_t)blk * Hkv + kh) * D * KV_BS;   // [D][32 slots]
+  const size_t e0 = ((size_t)blk * Hkv + kh) * D * KV_BS;   // [4][D][8 slots] (common.h kv_v_off)
   if (n == KV_BS) {
     for (int i = tid; i < D * 4; i += 256) {
       const int d = i >> 2, g = i & 3;
@@ -93,21 +93,21 @@ __global__ void __launch_bounds__(256) v_cache_runs_kernel(const uint16_t* __res
         float f[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] = bf2f(e[j]) * inv_v;
-        *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(v_cache) + e0 + d * KV_BS + 8 * g) = pack8_fp8(f);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(v_cache) + e0 + kv_v_off(d, 8 * g, D)) = pack8_fp8(f);
       } else {
         uint4 v;
         v.x = e[0] | ((uint32_t)e[1] << 16); v.y = e[2] | ((uint32_t)e[3] << 16);
         v.z = e[4] | ((uint32_t)e[5] << 16); v.w = e[6] | ((uint32_t)e[7] << 16);
-        *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(v_cache) + e0 + d * KV_BS + 8 * g) = v;
+        *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(v_cache) + e0 + kv_v_off(d, 8 * g, D)) = v;
       }
     }
   } else {
     for (int i = tid; i < n * D; i += 256) {
       const int j = i / D, d = i - j * D, off = off0 + j;
       if constexpr (F8)
-        reinterpret_cast<uint8_t*>(v_cache)[e0 + d * KV_BS + v_slot(off)] = f2fp8(bf2f(sv[off][d]) * inv_v);
+        reinterpret_cast<uint8_t*>(v_cache)[e0 + kv_v_off(d, v_slot(off), D)] = f2fp8(bf2f(sv[off][d]) * inv_v);
       else
-        reinterpret_cast<uint16_t*>(v_cache)[e0 + d * KV_BS + v_slot(off)] = sv[off][d];
+        reinterpret_cast<uint16_t*>(v_cache)[e0 + kv_v_off(d, v_slot(off), D)] = sv[off][d];
     }
   }
 }

@@ -70,6 +70,32 @@ def test_encoder_cpu_pooling_normalized():
     assert torch.allclose(e.norm(dim=1), torch.ones(2), atol=1e-3)
 
 
+def test_v_cache_slot_groups_layout_and_round_trip():
+    """V tiles are stored [4 slot groups][D][8] (common.h kv_v_off): slot position p of row d at
+    element (p // 8) * 8 D + 8 d + p % 8 of the tile, so one token's column spans D / 8 lines of
+    128 B; the reference writes and gathers through that order."""
+    Hq, Hkv, D, nblk = 4, 2, 16, 3
+    torch.manual_seed(0)
+    kc = torch.zeros(nblk, Hkv, R.KV_BLOCK, D)
+    vc = torch.zeros(nblk, Hkv, D, R.KV_BLOCK)
+    T = 40
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D)
+    slots = torch.randperm(nblk * R.KV_BLOCK)[:T].int()
+    cs = R.rope_cos_sin(64, D, 1e4)
+    R.rope_kv_write(qkv, torch.arange(T, dtype=torch.int32), slots, cs, kc, vc, Hq, Hkv, D)
+    v = qkv.view(T, Hq + 2 * Hkv, D)[:, Hq + Hkv:]
+    perm = R.v_slot_perm()
+    flat = vc.view(nblk, Hkv, -1)
+    for t in range(T):
+        blk, off = divmod(int(slots[t]), R.KV_BLOCK)
+        p = int(perm[off])
+        for d in (0, 5, D - 1):
+            assert torch.equal(flat[blk, :, (p // 8) * 8 * D + 8 * d + p % 8], v[t, :, d])
+    k_all, v_all = R.gather_kv(kc, vc, torch.arange(nblk, dtype=torch.int32), nblk * R.KV_BLOCK)
+    for t in range(T):
+        assert torch.equal(v_all[int(slots[t])], v[t])
+
+
 def test_v_slot_perm_is_permutation():
     p = R.v_slot_perm()
     assert sorted(p.tolist()) == list(range(32))
